@@ -1,0 +1,179 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Qwen3-8B QLoRA fine-tune throughput (tokens/s, whole node).
+
+Config = the reference's ``Fine-Tuning/qwen3-8b-qlora-dist.py`` (BASELINE.json / BASELINE.md):
+NF4 + double-quant base (compute bf16), LoRA r=8 / alpha=16 / dropout=0.1 on q_proj+v_proj,
+per-device batch 2 × 512 tokens, gradient accumulation 2, paged-AdamW-8bit (lr 5e-5, linear
+schedule), max_grad_norm 1.0, DDP over RCCL for N>1.  Synthetic random token ids and
+random-init weights of the Qwen3-8B architecture (no checkpoint / dataset download).
+
+Every timed step is a full optimizer step: GA forward+backward micro-steps, the DDP gradient
+all-reduce, global-norm clipping and the 8-bit AdamW update.
+
+    python bench.py --gpus 1 --steps 10 --warmup 3
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
+
+Rank 0 prints ONE JSON line (value = aggregate tokens/s over all ranks, max time over ranks).
+"""
+import argparse
+import contextlib
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from llm_in_practise_amd.models.qwen3 import Qwen3ForCausalLM, qwen3_config  # noqa: E402
+from llm_in_practise_amd.optim.adamw import LRScheduler, build_optimizer  # noqa: E402
+from llm_in_practise_amd.parallel import dist as D  # noqa: E402
+from llm_in_practise_amd.parallel.ddp import DistributedDataParallel  # noqa: E402
+from llm_in_practise_amd.peft.lora import LoraConfig, get_peft_model, quantize_model_nf4  # noqa: E402
+
+BASELINE_TOKENS_PER_S = None   # the reference publishes no fine-tune throughput
+MODEL_NAMES = {"qwen3-8b": "Qwen3-8B", "qwen3-14b": "Qwen3-14B", "qwen3-4b": "Qwen3-4B",
+               "deepseek-r1-0528-qwen3-8b": "DeepSeek-R1-0528-Qwen3-8B", "qwen3-tiny": "qwen3-tiny",
+               "qwen3-small": "qwen3-small"}
+
+
+def log(*a):
+    if D.is_main():
+        print(*a, file=sys.stderr, flush=True)
+
+
+def build(args, device):
+    cfg = qwen3_config(args.model)
+    t0 = time.time()
+    dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
+    model = Qwen3ForCausalLM.from_config(cfg, dtype=dtype, device=device, seed=1234)
+    if args.mode == "qlora":
+        quantize_model_nf4(model, double_quant=True, compute_dtype=dtype)
+    lcfg = LoraConfig(r=args.lora_r, lora_alpha=args.lora_alpha, lora_dropout=args.lora_dropout,
+                      target_modules=args.targets.split(","))
+    pm = get_peft_model(model, lcfg)
+    model.fuse_projections()
+    if args.grad_ckpt:
+        model.gradient_checkpointing_enable()
+    pm.train()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    log(f"[bench] built {args.model} ({args.mode}) in {time.time() - t0:.1f}s; "
+        f"trainable={sum(p.numel() for p in pm.parameters() if p.requires_grad):,}")
+    return cfg, pm
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="qwen3-8b")
+    ap.add_argument("--mode", default="qlora", choices=["qlora", "lora"])
+    ap.add_argument("--micro-batch", type=int, default=2)
+    ap.add_argument("--grad-accum", type=int, default=2)
+    ap.add_argument("--seq-len", type=int, default=512)
+    ap.add_argument("--lora-r", type=int, default=8)
+    ap.add_argument("--lora-alpha", type=int, default=16)
+    ap.add_argument("--lora-dropout", type=float, default=0.1)
+    ap.add_argument("--targets", default="q_proj,v_proj")
+    ap.add_argument("--optim", default="paged_adamw_8bit")
+    ap.add_argument("--lr", type=float, default=5e-5)
+    ap.add_argument("--grad-ckpt", action="store_true",
+                    help="recompute each decoder layer in backward (the reference's 24 GB-GPU setting; "
+                         "off by default: 288 GB HBM holds every activation)")
+    args = ap.parse_args()
+
+    rank, local_rank, world = D.init_distributed()
+    device = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    cfg, model = build(args, device)
+    opt = build_optimizer(args.optim, [p for p in model.parameters() if p.requires_grad], args.lr,
+                          weight_decay=0.0, max_grad_norm=1.0)
+    total_steps = args.warmup + args.steps
+    sched = LRScheduler(opt, "linear", args.lr, total_steps)
+    ddp = DistributedDataParallel(model, grad_buffer=opt.grad_buffer)
+
+    gen = torch.Generator(device=device).manual_seed(1000 + rank)
+    n_batches = 8
+    data = torch.randint(0, cfg.vocab_size, (n_batches, args.micro_batch, args.seq_len), device=device,
+                         generator=gen)
+    it = [0]
+
+    def step():
+        for micro in range(args.grad_accum):
+            ids = data[it[0] % n_batches]
+            it[0] += 1
+            ctx = ddp.no_sync() if micro < args.grad_accum - 1 else contextlib.nullcontext()
+            with ctx:
+                out = model(ids, labels=ids)
+                (out.loss / args.grad_accum).backward()
+        ddp.allreduce_grads()
+        opt.clip_grad_norm_(1.0)
+        opt.step()
+        sched.step()
+        opt.zero_grad()
+        return out.loss
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+        D.barrier()
+
+    for i in range(args.warmup):
+        loss = step()
+        if i == 0:
+            sync()
+            log(f"[bench] first step done, loss={loss.item():.4f}")
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    sync()
+    elapsed = D.all_reduce_max(time.perf_counter() - t0)
+    ms = 1000 * elapsed / max(1, args.steps)
+    tokens = args.micro_batch * args.seq_len * args.grad_accum * world * args.steps
+    tps = tokens / elapsed
+    fl_per_tok = 6 * 0  # filled below
+    lin = cfg.num_params() - cfg.vocab_size * cfg.hidden_size * (1 if cfg.tie_word_embeddings else 2)
+    head = cfg.vocab_size * cfg.hidden_size
+    # fwd 2·(linear+head) + bwd dX 2·(linear+head); no weight grads for the frozen base
+    fl_per_tok = 4 * (lin + head) * (1.5 if args.grad_ckpt else 1.0)
+    mem = torch.cuda.max_memory_allocated(device) / 2 ** 30 if device.type == "cuda" else 0.0
+    log(f"[bench] loss={loss.item():.4f} {ms:.1f} ms/step  {tps:,.0f} tok/s  "
+        f"~{tps * fl_per_tok / world / 1e12:.0f} TFLOP/s/GPU (matmul)  peak HBM {mem:.1f} GiB")
+    if D.is_main():
+        rec = {
+            "metric": "tokens/sec (whole node) Qwen3-8B QLoRA fine-tune at 1/2/4/8 MI355X",
+            "value": round(tps, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(tps / BASELINE_TOKENS_PER_S, 3) if BASELINE_TOKENS_PER_S else None),
+            "dtype": "bf16",
+            "data": "synthetic",
+            "config": {
+                "model": MODEL_NAMES.get(args.model, args.model),
+                "global_batch": args.micro_batch * args.grad_accum * world,
+                "seq_len": args.seq_len,
+                "parallelism": f"dp{world}",
+                "micro_batch": args.micro_batch,
+                "grad_accum": args.grad_accum,
+                "quant": "nf4+double_quant" if args.mode == "qlora" else "none",
+                "lora": f"r{args.lora_r}/a{args.lora_alpha}/drop{args.lora_dropout}/{args.targets}",
+                "optimizer": args.optim,
+                "gradient_checkpointing": bool(args.grad_ckpt),
+                "weights": "random-init",
+                "peak_hbm_gib": round(mem, 1),
+            },
+        }
+        print(json.dumps(rec), flush=True)
+    D.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,438 @@
+// PyTorch bindings for the gfx950 kernels.  Launchers take raw pointers + the current HIP
+// stream (so every op is capturable in a hipGraph and ordered with PyTorch's own work).
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+// ---- launcher declarations (csrc/kernels/*.hip)
+void launch_rmsnorm_fwd(int, const void*, const void*, void*, float*, int, int, float, hipStream_t);
+void launch_rmsnorm_bwd(int, const void*, const void*, const void*, const float*, void*, float*, float*, int, int,
+                        hipStream_t);
+void launch_layernorm_fwd(int, const void*, const void*, const void*, void*, float*, float*, int, int, float,
+                          hipStream_t);
+void launch_layernorm_bwd(int, const void*, const void*, const void*, const float*, const float*, void*, float*,
+                          float*, float*, int, int, hipStream_t);
+int norm_partial_rows(int M);
+void launch_qk_norm_rope_fwd(const void*, const void*, const void*, const float*, const float*, void*, void*, float*,
+                             float*, int, int, int, int, float, hipStream_t);
+void launch_qk_norm_rope_bwd(const void*, const void*, const void*, const void*, const void*, const float*,
+                             const float*, const float*, const float*, void*, int, int, int, int, hipStream_t);
+void launch_rope(int, const void*, const float*, const float*, void*, int, int, int, int, int, hipStream_t);
+void launch_swiglu_fwd(const void*, void*, int, int, hipStream_t);
+void launch_swiglu_bwd(const void*, const void*, void*, int, int, hipStream_t);
+void launch_gelu_fwd(int, const void*, void*, size_t, hipStream_t);
+void launch_gelu_bwd(int, const void*, const void*, void*, size_t, hipStream_t);
+void launch_ce_fwd_bwd(int, void*, const int64_t*, float*, int, int, int, const float*, float, hipStream_t);
+void launch_grad_norm(int, const void*, size_t, float*, float*, float, int, hipStream_t);
+void launch_adamw(int, float*, const void*, float*, float*, void*, size_t, float, float, float, float, float, float,
+                  float, const float*, const float*, hipStream_t);
+void launch_adamw8bit(int, float*, const void*, uint8_t*, uint8_t*, float*, float*, const float*, const float*, void*,
+                      size_t, float, float, float, float, float, float, float, const float*, const float*,
+                      hipStream_t);
+void launch_unscale(int, void*, size_t, const float*, float*, hipStream_t);
+void launch_gemm_w4(int, const void*, int, const uint32_t*, const float*, const void*, const void*, int, const void*,
+                    void*, int, int, int, hipStream_t);
+void launch_gemm_bf16w(const void*, int, const void*, const void*, const void*, int, const void*, void*, int, int, int,
+                       hipStream_t);
+void launch_pack_nf4(const uint8_t*, uint32_t*, int, int, int, hipStream_t);
+void launch_absmax_t(const float*, const uint8_t*, const float*, const float*, const float*, float*, int, int,
+                     hipStream_t);
+void launch_nf4_quantize(const void*, uint8_t*, float*, size_t, hipStream_t);
+void launch_nf4_dequant(const uint8_t*, const float*, const uint8_t*, const float*, const float*, const float*, void*,
+                        size_t, hipStream_t);
+void launch_attn_fwd(const void*, const void*, const void*, int, int, int, const int*, void*, float*, int, int, int,
+                     int, int, int, float, hipStream_t);
+void launch_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const int*, int,
+                     int, int, void*, void*, void*, float*, float*, float*, float*, int, int, int, int, int, int,
+                     float, hipStream_t);
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+hipStream_t stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+#define CHECK_BF16(x) TORCH_CHECK((x).scalar_type() == at::kBFloat16, #x " must be bf16")
+
+int dtype_code(const Tensor& t) {
+  if (t.scalar_type() == at::kBFloat16) return 1;
+  TORCH_CHECK(t.scalar_type() == at::kFloat, "expected fp32 or bf16, got ", t.scalar_type());
+  return 0;
+}
+const void* optr(const optional<Tensor>& t) { return t.has_value() && t->defined() ? t->data_ptr() : nullptr; }
+template <typename T>
+const T* optr_t(const optional<Tensor>& t) {
+  return t.has_value() && t->defined() ? t->data_ptr<T>() : nullptr;
+}
+
+// ------------------------------------------------------------------ norms
+std::vector<Tensor> rmsnorm_fwd(Tensor x, optional<Tensor> w, double eps) {
+  CHECK_CUDA(x);
+  CHECK_CONTIG(x);
+  const int N = x.size(-1), M = x.numel() / N;
+  TORCH_CHECK(N % 8 == 0, "rmsnorm: hidden size must be a multiple of 8");
+  if (w) TORCH_CHECK(w->scalar_type() == x.scalar_type() && w->is_contiguous(), "rmsnorm weight dtype/layout");
+  auto y = at::empty_like(x);
+  auto rstd = at::empty({M}, x.options().dtype(at::kFloat));
+  launch_rmsnorm_fwd(dtype_code(x), x.data_ptr(), optr(w), y.data_ptr(), rstd.data_ptr<float>(), M, N, (float)eps,
+                     stream());
+  return {y, rstd};
+}
+
+std::vector<Tensor> rmsnorm_bwd(Tensor dy, Tensor x, optional<Tensor> w, Tensor rstd, bool need_dw) {
+  CHECK_CONTIG(dy);
+  CHECK_CONTIG(x);
+  const int N = x.size(-1), M = x.numel() / N;
+  auto dx = at::empty_like(x);
+  Tensor part, dw;
+  if (need_dw) {
+    part = at::empty({norm_partial_rows(M), N}, x.options().dtype(at::kFloat));
+    dw = at::empty({N}, x.options().dtype(at::kFloat));
+  }
+  launch_rmsnorm_bwd(dtype_code(x), dy.data_ptr(), x.data_ptr(), optr(w), rstd.data_ptr<float>(), dx.data_ptr(),
+                     need_dw ? part.data_ptr<float>() : nullptr, need_dw ? dw.data_ptr<float>() : nullptr, M, N,
+                     stream());
+  return {dx, dw};
+}
+
+std::vector<Tensor> layernorm_fwd(Tensor x, optional<Tensor> w, optional<Tensor> b, double eps) {
+  CHECK_CUDA(x);
+  CHECK_CONTIG(x);
+  const int N = x.size(-1), M = x.numel() / N;
+  TORCH_CHECK(N % 8 == 0, "layernorm: hidden size must be a multiple of 8");
+  auto y = at::empty_like(x);
+  auto mean = at::empty({M}, x.options().dtype(at::kFloat));
+  auto rstd = at::empty({M}, x.options().dtype(at::kFloat));
+  launch_layernorm_fwd(dtype_code(x), x.data_ptr(), optr(w), optr(b), y.data_ptr(), mean.data_ptr<float>(),
+                       rstd.data_ptr<float>(), M, N, (float)eps, stream());
+  return {y, mean, rstd};
+}
+
+std::vector<Tensor> layernorm_bwd(Tensor dy, Tensor x, optional<Tensor> w, Tensor mean, Tensor rstd, bool need_dw) {
+  const int N = x.size(-1), M = x.numel() / N;
+  auto dx = at::empty_like(x);
+  Tensor part, dw, db;
+  if (need_dw) {
+    part = at::empty({2 * norm_partial_rows(M), N}, x.options().dtype(at::kFloat));
+    dw = at::empty({N}, x.options().dtype(at::kFloat));
+    db = at::empty({N}, x.options().dtype(at::kFloat));
+  }
+  launch_layernorm_bwd(dtype_code(x), dy.data_ptr(), x.data_ptr(), optr(w), mean.data_ptr<float>(),
+                       rstd.data_ptr<float>(), dx.data_ptr(), need_dw ? part.data_ptr<float>() : nullptr,
+                       need_dw ? dw.data_ptr<float>() : nullptr, need_dw ? db.data_ptr<float>() : nullptr, M, N,
+                       stream());
+  return {dx, dw, db};
+}
+
+// ------------------------------------------------------------------ rope
+Tensor rope(Tensor x, Tensor cos, Tensor sin, bool interleaved, bool inverse) {
+  CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 3, "rope expects [T, H, D]");
+  auto y = at::empty_like(x);
+  launch_rope(dtype_code(x), x.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), y.data_ptr(), x.size(0),
+              x.size(1), x.size(2), interleaved, inverse, stream());
+  return y;
+}
+
+std::vector<Tensor> qk_norm_rope_fwd(Tensor qkv, optional<Tensor> qw, optional<Tensor> kw, Tensor cos, Tensor sin,
+                                     int64_t hq, int64_t hkv, int64_t d, double eps) {
+  CHECK_BF16(qkv);
+  CHECK_CONTIG(qkv);
+  const int T = qkv.size(0);
+  TORCH_CHECK(qkv.size(1) == (hq + 2 * hkv) * d, "qkv width mismatch");
+  TORCH_CHECK(cos.scalar_type() == at::kFloat && cos.size(0) == T && cos.size(1) == d / 2, "cos table [T, D/2] fp32");
+  auto q = at::empty({T, hq * d}, qkv.options());
+  auto k = at::empty({T, hkv * d}, qkv.options());
+  auto rq = at::empty({T * hq}, qkv.options().dtype(at::kFloat));
+  auto rk = at::empty({T * hkv}, qkv.options().dtype(at::kFloat));
+  launch_qk_norm_rope_fwd(qkv.data_ptr(), optr(qw), optr(kw), cos.data_ptr<float>(), sin.data_ptr<float>(),
+                          q.data_ptr(), k.data_ptr(), rq.data_ptr<float>(), rk.data_ptr<float>(), T, hq, hkv, d,
+                          (float)eps, stream());
+  return {q, k, rq, rk};
+}
+
+Tensor qk_norm_rope_bwd(Tensor dq, Tensor dk, optional<Tensor> dv, Tensor qkv, optional<Tensor> qw,
+                        optional<Tensor> kw, Tensor cos, Tensor sin, Tensor rq, Tensor rk, int64_t hq, int64_t hkv,
+                        int64_t d) {
+  const int T = qkv.size(0);
+  auto dqkv = at::empty_like(qkv);
+  launch_qk_norm_rope_bwd(dq.data_ptr(), dk.data_ptr(), qkv.data_ptr(), optr(qw), optr(kw), cos.data_ptr<float>(),
+                          sin.data_ptr<float>(), rq.data_ptr<float>(), rk.data_ptr<float>(), dqkv.data_ptr(), T, hq,
+                          hkv, d, stream());
+  auto vslice = dqkv.narrow(1, (hq + hkv) * d, hkv * d);
+  if (dv && dv->defined()) vslice.copy_(*dv);
+  else vslice.zero_();
+  return dqkv;
+}
+
+// ------------------------------------------------------------------ activations
+Tensor swiglu_fwd(Tensor gu) {
+  CHECK_BF16(gu);
+  CHECK_CONTIG(gu);
+  const int F = gu.size(-1) / 2, M = gu.numel() / gu.size(-1);
+  TORCH_CHECK(F % 8 == 0, "swiglu: intermediate size must be a multiple of 8");
+  auto sizes = gu.sizes().vec();
+  sizes.back() = F;
+  auto y = at::empty(sizes, gu.options());
+  launch_swiglu_fwd(gu.data_ptr(), y.data_ptr(), M, F, stream());
+  return y;
+}
+Tensor swiglu_bwd(Tensor dy, Tensor gu) {
+  const int F = gu.size(-1) / 2, M = gu.numel() / gu.size(-1);
+  auto dgu = at::empty_like(gu);
+  launch_swiglu_bwd(dy.data_ptr(), gu.data_ptr(), dgu.data_ptr(), M, F, stream());
+  return dgu;
+}
+Tensor gelu_fwd(Tensor x) {
+  CHECK_CONTIG(x);
+  auto y = at::empty_like(x);
+  launch_gelu_fwd(dtype_code(x), x.data_ptr(), y.data_ptr(), x.numel(), stream());
+  return y;
+}
+Tensor gelu_bwd(Tensor dy, Tensor x) {
+  auto dx = at::empty_like(x);
+  launch_gelu_bwd(dtype_code(x), dy.data_ptr(), x.data_ptr(), dx.data_ptr(), x.numel(), stream());
+  return dx;
+}
+
+// ------------------------------------------------------------------ cross entropy
+Tensor ce_fwd_bwd(Tensor logits, Tensor labels, int64_t ignore_index, Tensor scale) {
+  CHECK_CONTIG(logits);
+  TORCH_CHECK(labels.scalar_type() == at::kLong, "labels int64");
+  const int M = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(V % 8 == 0, "vocab must be a multiple of 8");
+  auto loss = at::empty({M}, logits.options().dtype(at::kFloat));
+  auto sc = scale.to(at::kFloat).contiguous();
+  launch_ce_fwd_bwd(dtype_code(logits), logits.data_ptr(), labels.contiguous().data_ptr<int64_t>(),
+                    loss.data_ptr<float>(), M, V, ignore_index, sc.data_ptr<float>(), 1.f, stream());
+  return loss;
+}
+
+// ------------------------------------------------------------------ optimizers
+Tensor grad_norm(Tensor g, double max_norm, optional<Tensor> out, bool accumulate) {
+  CHECK_CONTIG(g);
+  Tensor o = out && out->defined() ? *out : at::zeros({3}, g.options().dtype(at::kFloat));
+  auto part = at::empty({1024}, g.options().dtype(at::kFloat));
+  launch_grad_norm(dtype_code(g), g.data_ptr(), g.numel(), part.data_ptr<float>(), o.data_ptr<float>(),
+                   (float)max_norm, accumulate, stream());
+  return o;
+}
+
+void adamw(Tensor p, Tensor g, Tensor m, Tensor v, optional<Tensor> p16, double lr, double b1, double b2, double eps,
+           double wd, int64_t step, optional<Tensor> gscale, optional<Tensor> skip) {
+  TORCH_CHECK(p.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
+              "adamw: fp32 master/state");
+  TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous(), "adamw: contiguous");
+  const float bc1 = 1.f - std::pow((float)b1, (float)step), bc2 = 1.f - std::pow((float)b2, (float)step);
+  launch_adamw(dtype_code(g), p.data_ptr<float>(), g.data_ptr(), m.data_ptr<float>(), v.data_ptr<float>(),
+               (void*)optr(p16), p.numel(), lr, b1, b2, eps, wd, bc1, bc2, optr_t<float>(gscale), optr_t<float>(skip),
+               stream());
+}
+
+void adamw8bit(Tensor p, Tensor g, Tensor qm, Tensor qv, Tensor am, Tensor av, Tensor code_s, Tensor code_u,
+               optional<Tensor> p16, double lr, double b1, double b2, double eps, double wd, int64_t step,
+               optional<Tensor> gscale, optional<Tensor> skip) {
+  const float bc1 = 1.f - std::pow((float)b1, (float)step), bc2 = 1.f - std::pow((float)b2, (float)step);
+  launch_adamw8bit(dtype_code(g), p.data_ptr<float>(), g.data_ptr(), qm.data_ptr<uint8_t>(), qv.data_ptr<uint8_t>(),
+                   am.data_ptr<float>(), av.data_ptr<float>(), code_s.data_ptr<float>(), code_u.data_ptr<float>(),
+                   (void*)optr(p16), p.numel(), lr, b1, b2, eps, wd, bc1, bc2, optr_t<float>(gscale),
+                   optr_t<float>(skip), stream());
+}
+
+void unscale(Tensor g, Tensor inv_scale, Tensor found_inf) {
+  launch_unscale(dtype_code(g), g.data_ptr(), g.numel(), inv_scale.data_ptr<float>(), found_inf.data_ptr<float>(),
+                 stream());
+}
+
+// ------------------------------------------------------------------ NF4
+std::vector<Tensor> nf4_quantize(Tensor w, int64_t blocksize) {
+  CHECK_BF16(w);
+  CHECK_CONTIG(w);
+  TORCH_CHECK(blocksize == 64, "NF4 kernel quantises with blocksize 64");
+  TORCH_CHECK(w.size(-1) % 64 == 0, "in_features % 64");
+  auto codes = at::empty({w.size(0), w.size(1) / 2}, w.options().dtype(at::kByte));
+  auto absmax = at::empty({w.numel() / 64}, w.options().dtype(at::kFloat));
+  launch_nf4_quantize(w.data_ptr(), codes.data_ptr<uint8_t>(), absmax.data_ptr<float>(), w.numel(), stream());
+  return {codes, absmax};
+}
+
+Tensor nf4_dequant(Tensor codes, optional<Tensor> absmax, optional<Tensor> qabs, optional<Tensor> absmax2,
+                   optional<Tensor> offset, optional<Tensor> dcode, int64_t N, int64_t K) {
+  auto w = at::empty({N, K}, codes.options().dtype(at::kBFloat16));
+  launch_nf4_dequant(codes.data_ptr<uint8_t>(), optr_t<float>(absmax), optr_t<uint8_t>(qabs), optr_t<float>(absmax2),
+                     optr_t<float>(offset), optr_t<float>(dcode), w.data_ptr(), N * K, stream());
+  return w;
+}
+
+std::vector<Tensor> nf4_pack(Tensor codes, int64_t N, int64_t K) {
+  CHECK_CONTIG(codes);
+  TORCH_CHECK(N % 64 == 0 && K % 64 == 0, "nf4_pack: N, K multiples of 64");
+  auto f = at::empty({N * K / 8}, codes.options().dtype(at::kInt));
+  auto b = at::empty({N * K / 8}, codes.options().dtype(at::kInt));
+  launch_pack_nf4(codes.data_ptr<uint8_t>(), (uint32_t*)f.data_ptr(), N, K, 0, stream());
+  launch_pack_nf4(codes.data_ptr<uint8_t>(), (uint32_t*)b.data_ptr(), N, K, 1, stream());
+  return {f, b};
+}
+
+Tensor nf4_absmax_t(optional<Tensor> absmax, optional<Tensor> qabs, optional<Tensor> absmax2, optional<Tensor> offset,
+                    optional<Tensor> dcode, int64_t N, int64_t K) {
+  const auto& ref = absmax ? *absmax : *qabs;
+  auto out = at::empty({K / 64, N}, ref.options().dtype(at::kFloat));
+  launch_absmax_t(optr_t<float>(absmax), optr_t<uint8_t>(qabs), optr_t<float>(absmax2), optr_t<float>(offset),
+                  optr_t<float>(dcode), out.data_ptr<float>(), N, K, stream());
+  return out;
+}
+
+void check_ext(const optional<Tensor>& ea, const optional<Tensor>& eb, int M, int C, int& R_ext) {
+  R_ext = 0;
+  if (ea && ea->defined()) {
+    TORCH_CHECK(eb && eb->defined(), "ext_b required with ext_a");
+    CHECK_BF16(*ea);
+    CHECK_BF16(*eb);
+    CHECK_CONTIG(*ea);
+    CHECK_CONTIG(*eb);
+    R_ext = ea->size(1);
+    TORCH_CHECK(R_ext % 32 == 0 && ea->size(0) == M && eb->size(0) == C && eb->size(1) == R_ext,
+                "LoRA K-slice shapes: ext_a [M, R], ext_b [C, R], R % 32 == 0");
+  }
+}
+
+// Y[M, N] = X[M, K] · deq(W)ᵀ + ext_a·ext_bᵀ + residual
+Tensor gemm_nf4(Tensor x, Tensor codes_f, Tensor absmax_t, int64_t N, optional<Tensor> ext_a, optional<Tensor> ext_b,
+                optional<Tensor> residual) {
+  CHECK_BF16(x);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "gemm_nf4: x row-major, 16-B aligned rows");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(N % 32 == 0 && K % 64 == 0, "gemm_nf4: N % 32, K % 64");
+  TORCH_CHECK(codes_f.numel() == N * K / 8 && absmax_t.numel() == N * K / 64, "gemm_nf4: packed weight size");
+  int R_ext;
+  check_ext(ext_a, ext_b, M, N, R_ext);
+  if (residual) TORCH_CHECK(residual->is_contiguous() && residual->size(0) == M && residual->size(1) == N, "residual");
+  auto y = at::empty({M, N}, x.options());
+  launch_gemm_w4(0, x.data_ptr(), x.stride(0), (const uint32_t*)codes_f.data_ptr(), absmax_t.data_ptr<float>(),
+                 optr(ext_a), optr(ext_b), R_ext, optr(residual), y.data_ptr(), M, N, K, stream());
+  return y;
+}
+
+// dX[M, K] = dY[M, N] · deq(W) + ext_a·ext_bᵀ  (ext_b is [K, R])
+Tensor gemm_nf4_t(Tensor dy, Tensor codes_b, Tensor absmax_t, int64_t K, optional<Tensor> ext_a,
+                  optional<Tensor> ext_b) {
+  CHECK_BF16(dy);
+  TORCH_CHECK(dy.dim() == 2 && dy.stride(1) == 1 && dy.stride(0) % 8 == 0, "gemm_nf4_t: dy row-major");
+  const int M = dy.size(0), N = dy.size(1);
+  TORCH_CHECK(N % 64 == 0 && K % 32 == 0, "gemm_nf4_t: N % 64, K % 32");
+  TORCH_CHECK(codes_b.numel() == N * K / 8, "gemm_nf4_t: packed weight size");
+  int R_ext;
+  check_ext(ext_a, ext_b, M, K, R_ext);
+  auto dx = at::empty({M, K}, dy.options());
+  launch_gemm_w4(1, dy.data_ptr(), dy.stride(0), (const uint32_t*)codes_b.data_ptr(), absmax_t.data_ptr<float>(),
+                 optr(ext_a), optr(ext_b), R_ext, nullptr, dx.data_ptr(), M, K, N, stream());
+  return dx;
+}
+
+Tensor gemm_bf16(Tensor x, Tensor w, optional<Tensor> ext_a, optional<Tensor> ext_b, optional<Tensor> residual) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_CONTIG(w);
+  const int M = x.size(0), K = x.size(1), N = w.size(0);
+  if (N % 32 != 0 || K % 64 != 0 || x.stride(1) != 1 || x.stride(0) % 8 != 0) {
+    auto y = at::matmul(x, w.t());
+    if (ext_a && ext_a->defined()) y.addmm_(*ext_a, ext_b->t());
+    if (residual && residual->defined()) y.add_(*residual);
+    return y;
+  }
+  int R_ext;
+  check_ext(ext_a, ext_b, M, N, R_ext);
+  auto y = at::empty({M, N}, x.options());
+  launch_gemm_bf16w(x.data_ptr(), x.stride(0), w.data_ptr(), optr(ext_a), optr(ext_b), R_ext, optr(residual),
+                    y.data_ptr(), M, N, K, stream());
+  return y;
+}
+
+// bf16 base backward: plain library GEMM (hipBLASLt) + the low-rank K-slice as a rank-R update
+Tensor gemm_bf16_t(Tensor dy, Tensor w, optional<Tensor> ext_a, optional<Tensor> ext_b) {
+  auto dx = at::matmul(dy, w);
+  if (ext_a && ext_a->defined()) dx.addmm_(*ext_a, ext_b->t());
+  return dx;
+}
+
+// ------------------------------------------------------------------ attention
+std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, optional<Tensor> kv_lens, int64_t B, int64_t S, int64_t hq,
+                             int64_t hkv, int64_t d, bool causal, double scale) {
+  CHECK_BF16(q);
+  TORCH_CHECK(q.stride(-1) == 1 && k.stride(-1) == 1 && v.stride(-1) == 1, "attn: unit inner stride");
+  TORCH_CHECK(d == 64 || d == 128, "attn: head_dim 64 or 128");
+  TORCH_CHECK(hq % hkv == 0, "attn: GQA group");
+  auto o = at::empty({B * S, hq * d}, q.options());
+  auto lse = at::empty({B, hq, S}, q.options().dtype(at::kFloat));
+  const int* kl = nullptr;
+  Tensor klc;
+  if (kv_lens && kv_lens->defined()) {
+    klc = kv_lens->to(at::kInt).contiguous();
+    kl = klc.data_ptr<int>();
+  }
+  launch_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0), v.stride(0), kl, o.data_ptr(),
+                  lse.data_ptr<float>(), B, S, hq, hkv, d, causal, scale, stream());
+  return {o, lse};
+}
+
+std::vector<Tensor> attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse,
+                             optional<Tensor> kv_lens, int64_t B, int64_t S, int64_t hq, int64_t hkv, int64_t d,
+                             bool causal, double scale) {
+  auto dq = at::empty({B * S, hq * d}, q.options());
+  auto dk = at::empty({B * S, hkv * d}, q.options());
+  auto dv = at::empty({B * S, hkv * d}, q.options());
+  TORCH_CHECK(S % 64 == 0, "attn_bwd: seq_len must be a multiple of 64");
+  auto dqacc = at::zeros({B * S, hq * d}, q.options().dtype(at::kFloat));
+  auto dkf = at::empty({B * S, hq * d}, q.options().dtype(at::kFloat));
+  auto dvf = at::empty({B * S, hq * d}, q.options().dtype(at::kFloat));
+  auto delta = at::empty({B, hq, S}, q.options().dtype(at::kFloat));
+  const int* kl = nullptr;
+  Tensor klc;
+  if (kv_lens && kv_lens->defined()) {
+    klc = kv_lens->to(at::kInt).contiguous();
+    kl = klc.data_ptr<int>();
+  }
+  launch_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), kl,
+                  q.stride(0), k.stride(0), v.stride(0), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
+                  dqacc.data_ptr<float>(), delta.data_ptr<float>(), dkf.data_ptr<float>(), dvf.data_ptr<float>(), B, S,
+                  hq, hkv, d, causal, scale, stream());
+  return {dq, dk, dv};
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "llm_in_practise_amd gfx950 (MI355X / CDNA4) kernels";
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("rope", &rope);
+  m.def("qk_norm_rope_fwd", &qk_norm_rope_fwd);
+  m.def("qk_norm_rope_bwd", &qk_norm_rope_bwd);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("gelu_fwd", &gelu_fwd);
+  m.def("gelu_bwd", &gelu_bwd);
+  m.def("ce_fwd_bwd", &ce_fwd_bwd);
+  m.def("grad_norm", &grad_norm);
+  m.def("adamw", &adamw);
+  m.def("adamw8bit", &adamw8bit);
+  m.def("unscale", &unscale);
+  m.def("nf4_quantize", &nf4_quantize);
+  m.def("nf4_dequant", &nf4_dequant);
+  m.def("nf4_pack", &nf4_pack);
+  m.def("nf4_absmax_t", &nf4_absmax_t);
+  m.def("gemm_nf4", &gemm_nf4);
+  m.def("gemm_nf4_t", &gemm_nf4_t);
+  m.def("gemm_bf16", &gemm_bf16);
+  m.def("gemm_bf16_t", &gemm_bf16_t);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+}

@@ -1,0 +1,92 @@
+// Elementwise kernels (K5): SwiGLU over the fused [gate | up] projection, exact GELU.
+// 16-byte vector loads per lane (8 bf16), grid-stride, memory-bound by design.
+#include "common.h"
+
+using namespace lipa;
+
+namespace {
+
+__device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
+
+// gu [M, 2F] -> y [M, F];  F % 8 == 0
+__global__ __launch_bounds__(256) void swiglu_fwd_k(const bf16* __restrict__ gu, bf16* __restrict__ y, int M, int F) {
+  const size_t nvec = (size_t)M * F / 8;
+  for (size_t v = (size_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (size_t)gridDim.x * 256) {
+    const size_t e = v * 8;
+    const size_t m = e / F, f = e % F;
+    float g[8], u[8], o[8];
+    load8(gu + m * 2 * F + f, g);
+    load8(gu + m * 2 * F + F + f, u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = silu(g[i]) * u[i];
+    store8(y + e, o);
+  }
+}
+
+// dgu = [dy*u*silu'(g) | dy*silu(g)]
+__global__ __launch_bounds__(256) void swiglu_bwd_k(const bf16* __restrict__ dy, const bf16* __restrict__ gu,
+                                                    bf16* __restrict__ dgu, int M, int F) {
+  const size_t nvec = (size_t)M * F / 8;
+  for (size_t v = (size_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (size_t)gridDim.x * 256) {
+    const size_t e = v * 8;
+    const size_t m = e / F, f = e % F;
+    float g[8], u[8], d[8], dg[8], du[8];
+    load8(gu + m * 2 * F + f, g);
+    load8(gu + m * 2 * F + F + f, u);
+    load8(dy + e, d);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float sg = 1.f / (1.f + __expf(-g[i]));
+      const float s = g[i] * sg;
+      du[i] = d[i] * s;
+      dg[i] = d[i] * u[i] * (sg * (1.f + g[i] * (1.f - sg)));
+    }
+    store8(dgu + m * 2 * F + f, dg);
+    store8(dgu + m * 2 * F + F + f, du);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gelu_fwd_k(const T* __restrict__ x, T* __restrict__ y, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const float v = (float)x[i];
+    y[i] = (T)(0.5f * v * (1.f + erff(v * 0.70710678118654752f)));
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gelu_bwd_k(const T* __restrict__ dy, const T* __restrict__ x, T* __restrict__ dx,
+                                                  size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const float v = (float)x[i];
+    const float cdf = 0.5f * (1.f + erff(v * 0.70710678118654752f));
+    const float pdf = 0.3989422804014327f * __expf(-0.5f * v * v);
+    dx[i] = (T)((float)dy[i] * (cdf + v * pdf));
+  }
+}
+
+inline int grid_for(size_t work) {
+  size_t g = (work + 255) / 256;
+  return (int)(g < 2048 ? (g ? g : 1) : 2048);
+}
+
+}  // namespace
+
+void launch_swiglu_fwd(const void* gu, void* y, int M, int F, hipStream_t st) {
+  swiglu_fwd_k<<<grid_for((size_t)M * F / 8), 256, 0, st>>>((const bf16*)gu, (bf16*)y, M, F);
+  LIPA_CHECK_LAUNCH();
+}
+void launch_swiglu_bwd(const void* dy, const void* gu, void* dgu, int M, int F, hipStream_t st) {
+  swiglu_bwd_k<<<grid_for((size_t)M * F / 8), 256, 0, st>>>((const bf16*)dy, (const bf16*)gu, (bf16*)dgu, M, F);
+  LIPA_CHECK_LAUNCH();
+}
+void launch_gelu_fwd(int dtype, const void* x, void* y, size_t n, hipStream_t st) {
+  if (dtype == 1) gelu_fwd_k<bf16><<<grid_for(n), 256, 0, st>>>((const bf16*)x, (bf16*)y, n);
+  else gelu_fwd_k<float><<<grid_for(n), 256, 0, st>>>((const float*)x, (float*)y, n);
+  LIPA_CHECK_LAUNCH();
+}
+void launch_gelu_bwd(int dtype, const void* dy, const void* x, void* dx, size_t n, hipStream_t st) {
+  if (dtype == 1) gelu_bwd_k<bf16><<<grid_for(n), 256, 0, st>>>((const bf16*)dy, (const bf16*)x, (bf16*)dx, n);
+  else gelu_bwd_k<float><<<grid_for(n), 256, 0, st>>>((const float*)dy, (const float*)x, (float*)dx, n);
+  LIPA_CHECK_LAUNCH();
+}

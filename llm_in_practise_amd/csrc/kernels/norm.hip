@@ -1,0 +1,342 @@
+// RMSNorm / LayerNorm forward + backward for gfx950.
+//
+// One wave (64 lanes) per row; each lane owns CH chunks of 8 contiguous elements loaded as
+// 16-byte vectors (bf16) so a row of 4096 bf16 is 8 independent 16-B loads per lane in
+// flight.  The row stays in registers between the reduction and the normalisation (single
+// HBM pass).  4 rows per 256-thread workgroup.  Backward optionally accumulates dW/db with
+// per-workgroup fp32 partial rows + a second reduction kernel (no float atomics).
+#include "common.h"
+
+using namespace lipa;
+
+namespace {
+
+constexpr int ROWS = 4;  // waves (rows) per workgroup
+
+template <typename T, typename TW, int CH>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_k(const T* __restrict__ x, const TW* __restrict__ w,
+                                                     T* __restrict__ y, float* __restrict__ rstd_out, int M,
+                                                     int N, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * ROWS + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const T* xr = x + (size_t)row * N;
+  float v[CH][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < N) {
+      load8(xr + col, v[c]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss += v[c][i] * v[c][i];
+    }
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / N + eps);
+  if (lane == 0) rstd_out[row] = r;
+  T* yr = y + (size_t)row * N;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < N) {
+      float wv[8];
+      if (w) load8(w + col, wv);
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = v[c][i] * r * (w ? wv[i] : 1.f);
+      store8(yr + col, o);
+    }
+  }
+}
+
+// dx = r * (w*dy - xhat * mean(xhat * w * dy)) ; dw_part[blk] += dy * xhat
+template <typename T, typename TW, int CH>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
+                                                     const TW* __restrict__ w, const float* __restrict__ rstd,
+                                                     T* __restrict__ dx, float* __restrict__ dw_part, int M,
+                                                     int N) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int row = blockIdx.x * ROWS + wid;
+  const bool valid = row < M;
+  float xv[CH][8], gv[CH][8];
+  float dot = 0.f;
+  const float r = valid ? rstd[row] : 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (valid && col < N) {
+      load8(x + (size_t)row * N + col, xv[c]);
+      load8(dy + (size_t)row * N + col, gv[c]);
+      float wv[8];
+      if (w) load8(w + col, wv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        xv[c][i] *= r;                                  // xhat
+        const float wg = gv[c][i] * (w ? wv[i] : 1.f);
+        dot += xv[c][i] * wg;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) xv[c][i] = gv[c][i] = 0.f;
+    }
+  }
+  dot = wave_sum(dot) / N;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (valid && col < N) {
+      float wv[8];
+      if (w) load8(w + col, wv);
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = r * (gv[c][i] * (w ? wv[i] : 1.f) - xv[c][i] * dot);
+      store8(dx + (size_t)row * N + col, o);
+    }
+  }
+  if (dw_part) {
+    // reduce dy*xhat over the block's rows through LDS, one partial row per block
+    __shared__ float red[ROWS][8 * 64 + 4];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int col = (c * 64 + lane) * 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) red[wid][lane * 8 + i] = gv[c][i] * xv[c][i];
+      __syncthreads();
+      for (int t = threadIdx.x; t < 512; t += 256) {
+        const int cc = c * 512 + t;
+        if (cc < N) {
+          float s = 0.f;
+#pragma unroll
+          for (int q = 0; q < ROWS; ++q) s += red[q][t];
+          dw_part[(size_t)blockIdx.x * N + cc] = s;
+        }
+      }
+      __syncthreads();
+      (void)col;
+    }
+  }
+}
+
+template <typename T, typename TW, int CH>
+__global__ __launch_bounds__(256) void layernorm_fwd_k(const T* __restrict__ x, const TW* __restrict__ w,
+                                                       const TW* __restrict__ b, T* __restrict__ y,
+                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                       int M, int N, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * ROWS + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const T* xr = x + (size_t)row * N;
+  float v[CH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < N) {
+      load8(xr + col, v[c]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[c][i];
+    }
+  }
+  const float mu = wave_sum(s) / N;
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < N) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = v[c][i] - mu;
+        ss += d * d;
+      }
+    }
+  }
+  const float r = rsqrtf(wave_sum(ss) / N + eps);
+  if (lane == 0) {
+    mean_out[row] = mu;
+    rstd_out[row] = r;
+  }
+  T* yr = y + (size_t)row * N;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < N) {
+      float wv[8], bv[8], o[8];
+      if (w) load8(w + col, wv);
+      if (b) load8(b + col, bv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mu) * r * (w ? wv[i] : 1.f) + (b ? bv[i] : 0.f);
+      store8(yr + col, o);
+    }
+  }
+}
+
+template <typename T, typename TW, int CH>
+__global__ __launch_bounds__(256) void layernorm_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
+                                                       const TW* __restrict__ w, const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd, T* __restrict__ dx,
+                                                       float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                       int M, int N) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int row = blockIdx.x * ROWS + wid;
+  const bool valid = row < M;
+  float xv[CH][8], gv[CH][8];
+  float s1 = 0.f, s2 = 0.f;
+  const float mu = valid ? mean[row] : 0.f, r = valid ? rstd[row] : 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (valid && col < N) {
+      load8(x + (size_t)row * N + col, xv[c]);
+      load8(dy + (size_t)row * N + col, gv[c]);
+      float wv[8];
+      if (w) load8(w + col, wv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        xv[c][i] = (xv[c][i] - mu) * r;
+        const float wg = gv[c][i] * (w ? wv[i] : 1.f);
+        s1 += wg;
+        s2 += wg * xv[c][i];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) xv[c][i] = gv[c][i] = 0.f;
+    }
+  }
+  s1 = wave_sum(s1) / N;
+  s2 = wave_sum(s2) / N;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (valid && col < N) {
+      float wv[8], o[8];
+      if (w) load8(w + col, wv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = r * (gv[c][i] * (w ? wv[i] : 1.f) - s1 - xv[c][i] * s2);
+      store8(dx + (size_t)row * N + col, o);
+    }
+  }
+  if (dw_part) {
+    __shared__ float red[2][ROWS][8 * 64 + 4];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        red[0][wid][lane * 8 + i] = gv[c][i] * xv[c][i];
+        red[1][wid][lane * 8 + i] = gv[c][i];
+      }
+      __syncthreads();
+      for (int t = threadIdx.x; t < 512; t += 256) {
+        const int cc = c * 512 + t;
+        if (cc < N) {
+          float a = 0.f, bb = 0.f;
+#pragma unroll
+          for (int q = 0; q < ROWS; ++q) {
+            a += red[0][q][t];
+            bb += red[1][q][t];
+          }
+          dw_part[(size_t)blockIdx.x * N + cc] = a;
+          db_part[(size_t)blockIdx.x * N + cc] = bb;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// sum partial rows [P, N] -> out [N] (fp32)
+__global__ __launch_bounds__(256) void colsum_k(const float* __restrict__ part, float* __restrict__ out, int P, int N) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= N) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += part[(size_t)p * N + col];
+  out[col] = s;
+}
+
+template <int CH>
+struct ChTag {};
+
+#define LIPA_CH_DISPATCH(N, FN)                                    \
+  do {                                                             \
+    const int ch__ = ((N) + 511) / 512;                            \
+    if (ch__ <= 1) { FN(1); }                                      \
+    else if (ch__ <= 2) { FN(2); }                                 \
+    else if (ch__ <= 4) { FN(4); }                                 \
+    else if (ch__ <= 8) { FN(8); }                                 \
+    else if (ch__ <= 10) { FN(10); }                               \
+    else if (ch__ <= 12) { FN(12); }                               \
+    else if (ch__ <= 16) { FN(16); }                               \
+    else { fprintf(stderr, "norm: N=%d too large\n", (int)(N)); }  \
+  } while (0)
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ launchers
+// dtype: 0 = fp32, 1 = bf16 (activations and weight share the dtype)
+void launch_rmsnorm_fwd(int dtype, const void* x, const void* w, void* y, float* rstd, int M, int N, float eps,
+                        hipStream_t st) {
+  dim3 g((M + ROWS - 1) / ROWS), b(256);
+#define F(CH)                                                                                                  \
+  if (dtype == 1)                                                                                              \
+    rmsnorm_fwd_k<bf16, bf16, CH><<<g, b, 0, st>>>((const bf16*)x, (const bf16*)w, (bf16*)y, rstd, M, N, eps); \
+  else                                                                                                         \
+    rmsnorm_fwd_k<float, float, CH><<<g, b, 0, st>>>((const float*)x, (const float*)w, (float*)y, rstd, M, N, eps);
+  LIPA_CH_DISPATCH(N, F);
+#undef F
+  LIPA_CHECK_LAUNCH();
+}
+
+void launch_rmsnorm_bwd(int dtype, const void* dy, const void* x, const void* w, const float* rstd, void* dx,
+                        float* dw_part, float* dw, int M, int N, hipStream_t st) {
+  dim3 g((M + ROWS - 1) / ROWS), b(256);
+#define F(CH)                                                                                               \
+  if (dtype == 1)                                                                                           \
+    rmsnorm_bwd_k<bf16, bf16, CH><<<g, b, 0, st>>>((const bf16*)dy, (const bf16*)x, (const bf16*)w, rstd,   \
+                                                   (bf16*)dx, dw_part, M, N);                               \
+  else                                                                                                      \
+    rmsnorm_bwd_k<float, float, CH><<<g, b, 0, st>>>((const float*)dy, (const float*)x, (const float*)w,    \
+                                                     rstd, (float*)dx, dw_part, M, N);
+  LIPA_CH_DISPATCH(N, F);
+#undef F
+  if (dw_part) colsum_k<<<(N + 255) / 256, 256, 0, st>>>(dw_part, dw, g.x, N);
+  LIPA_CHECK_LAUNCH();
+}
+
+void launch_layernorm_fwd(int dtype, const void* x, const void* w, const void* bias, void* y, float* mean,
+                          float* rstd, int M, int N, float eps, hipStream_t st) {
+  dim3 g((M + ROWS - 1) / ROWS), b(256);
+#define F(CH)                                                                                            \
+  if (dtype == 1)                                                                                        \
+    layernorm_fwd_k<bf16, bf16, CH><<<g, b, 0, st>>>((const bf16*)x, (const bf16*)w, (const bf16*)bias, \
+                                                     (bf16*)y, mean, rstd, M, N, eps);                   \
+  else                                                                                                   \
+    layernorm_fwd_k<float, float, CH><<<g, b, 0, st>>>((const float*)x, (const float*)w,                \
+                                                       (const float*)bias, (float*)y, mean, rstd, M, N, eps);
+  LIPA_CH_DISPATCH(N, F);
+#undef F
+  LIPA_CHECK_LAUNCH();
+}
+
+void launch_layernorm_bwd(int dtype, const void* dy, const void* x, const void* w, const float* mean,
+                          const float* rstd, void* dx, float* part, float* dw, float* db, int M, int N,
+                          hipStream_t st) {
+  dim3 g((M + ROWS - 1) / ROWS), b(256);
+  float* dwp = part;
+  float* dbp = part ? part + (size_t)g.x * N : nullptr;
+#define F(CH)                                                                                              \
+  if (dtype == 1)                                                                                          \
+    layernorm_bwd_k<bf16, bf16, CH><<<g, b, 0, st>>>((const bf16*)dy, (const bf16*)x, (const bf16*)w, mean, \
+                                                     rstd, (bf16*)dx, dwp, dbp, M, N);                     \
+  else                                                                                                     \
+    layernorm_bwd_k<float, float, CH><<<g, b, 0, st>>>((const float*)dy, (const float*)x,                  \
+                                                       (const float*)w, mean, rstd, (float*)dx, dwp, dbp, M, N);
+  LIPA_CH_DISPATCH(N, F);
+#undef F
+  if (part) {
+    colsum_k<<<(N + 255) / 256, 256, 0, st>>>(dwp, dw, g.x, N);
+    colsum_k<<<(N + 255) / 256, 256, 0, st>>>(dbp, db, g.x, N);
+  }
+  LIPA_CHECK_LAUNCH();
+}
+
+int norm_partial_rows(int M) { return (M + ROWS - 1) / ROWS; }

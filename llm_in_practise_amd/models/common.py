@@ -1,0 +1,157 @@
+"""Shared model plumbing: fused projections, output container, KV cache."""
+from __future__ import annotations
+
+import dataclasses
+
+import torch
+import torch.nn as nn
+
+from ..ops.linear import LoraBranch, fused_linear
+from ..peft.lora import Linear4bit, LoraLayer, base_of
+from ..quant.nf4 import NF4Weight, concat_nf4
+
+
+@dataclasses.dataclass
+class CausalLMOutput:
+    loss: torch.Tensor | None = None
+    logits: torch.Tensor | None = None
+    past_key_values: object | None = None
+    hidden_states: torch.Tensor | None = None
+
+    def __getitem__(self, i):
+        return [v for v in (self.loss, self.logits) if v is not None][i]
+
+
+def _leaf_linear(m: nn.Module) -> nn.Module:
+    return m.base_layer if isinstance(m, LoraLayer) else m
+
+
+def _out_features(m: nn.Module) -> int:
+    return _leaf_linear(m).out_features
+
+
+def _trainable_base(m: nn.Module) -> bool:
+    leaf = _leaf_linear(m)
+    return isinstance(leaf, nn.Linear) and leaf.weight.requires_grad
+
+
+class FusedProjection:
+    """Row-concatenation of projections that share one input (q|k|v, gate|up).
+
+    The concatenated base replaces the parts' storage (each part's buffers / weight become
+    views into it), so fusion costs no extra HBM.  LoRA branches keep their own A/B and
+    address their column range of the fused output.  Not used when a base weight is
+    trainable (full fine-tune) — then each projection runs on its own.
+    """
+
+    def __init__(self, mods: list[nn.Module]):
+        self.mods = mods
+        leaves = [_leaf_linear(m) for m in mods]
+        self.splits = [_out_features(m) for m in mods]
+        if all(isinstance(l, Linear4bit) for l in leaves):
+            parts = [l.nf4 for l in leaves]
+            fused = concat_nf4(parts)
+            self.base: NF4Weight | torch.Tensor = fused
+            r0, b0 = 0, 0
+            for l in leaves:                      # re-point parts at views of the fused storage
+                n = l.out_features
+                nblk = n * l.in_features // l.blocksize
+                l.codes = fused.codes[r0:r0 + n]
+                if fused.double_quant:
+                    g0, ng = b0 // 256, nblk // 256
+                    l.qabsmax = fused.qabsmax[b0:b0 + nblk]
+                    l.absmax2 = fused.absmax2[g0:g0 + ng]
+                    l.offset = fused.offset[g0:g0 + ng]
+                else:
+                    l.absmax = fused.absmax[b0:b0 + nblk]
+                r0 += n
+                b0 += nblk
+            biases = [l.bias for l in leaves]
+        else:
+            w = torch.cat([l.weight.detach() for l in leaves], 0)
+            self.base = w
+            r0 = 0
+            for l in leaves:
+                n = l.out_features
+                l.weight = nn.Parameter(w[r0:r0 + n], requires_grad=False)
+                r0 += n
+            biases = [l.bias for l in leaves]
+        self.bias = None
+        if any(b is not None for b in biases):
+            self.bias = torch.cat([b.detach() if b is not None else torch.zeros(n, dtype=self.dtype, device=self.device)
+                                   for b, n in zip(biases, self.splits)])
+
+    @property
+    def dtype(self):
+        return self.base.dtype
+
+    @property
+    def device(self):
+        return self.base.device
+
+    def branches(self, training: bool) -> list[LoraBranch]:
+        out, c0 = [], 0
+        for m, n in zip(self.mods, self.splits):
+            if isinstance(m, LoraLayer) and not m.merged:
+                br = m.branch(c0)
+                if not training:
+                    br.dropout = 0.0
+                out.append(br)
+            c0 += n
+        return out
+
+    def __call__(self, x, residual=None, training: bool = True):
+        return fused_linear(x, self.base, self.bias, self.branches(training), residual, training)
+
+
+def project(mods: list[nn.Module], x: torch.Tensor, residual: torch.Tensor | None = None,
+            training: bool = True, fused: FusedProjection | None = None) -> torch.Tensor:
+    """Run projections that share input ``x`` and concatenate their outputs."""
+    if fused is not None:
+        return fused(x, residual, training)
+    if len(mods) == 1:
+        m = mods[0]
+        if _trainable_base(m) or not isinstance(_leaf_linear(m), (nn.Linear, Linear4bit)):
+            y = m(x)
+            return y if residual is None else y + residual
+        base, bias = base_of(m)
+        br = [m.branch()] if isinstance(m, LoraLayer) and not m.merged else []
+        if br and not training:
+            br[0].dropout = 0.0
+        cd = base.dtype if isinstance(base, torch.Tensor) else base.dtype
+        return fused_linear(x.to(cd), base, bias, br, residual, training)
+    ys = [project([m], x, None, training) for m in mods]
+    y = torch.cat(ys, -1)
+    return y if residual is None else y + residual
+
+
+def can_fuse(mods: list[nn.Module]) -> bool:
+    leaves = [_leaf_linear(m) for m in mods]
+    if any(_trainable_base(m) for m in mods):
+        return False
+    if all(isinstance(l, Linear4bit) for l in leaves):
+        k = leaves[0].in_features
+        return all(l.in_features == k and (l.out_features * l.in_features // l.blocksize) % 256 == 0 for l in leaves)
+    if all(isinstance(l, nn.Linear) for l in leaves):
+        return len({l.in_features for l in leaves}) == 1 and len({l.weight.dtype for l in leaves}) == 1
+    return False
+
+
+class KVCache:
+    """Contiguous pre-allocated KV cache ``[B, Smax, Hkv*D]`` per layer (K17)."""
+
+    def __init__(self, n_layers: int, batch: int, max_len: int, hkv: int, d: int, dtype, device):
+        self.k = [torch.zeros(batch, max_len, hkv * d, dtype=dtype, device=device) for _ in range(n_layers)]
+        self.v = [torch.zeros(batch, max_len, hkv * d, dtype=dtype, device=device) for _ in range(n_layers)]
+        self.len = 0
+        self.max_len = max_len
+
+    def update(self, layer: int, k: torch.Tensor, v: torch.Tensor, start: int):
+        """k/v [B, s, Hkv*D] written at ``start``; returns views up to start+s."""
+        s = k.shape[1]
+        self.k[layer][:, start:start + s] = k
+        self.v[layer][:, start:start + s] = v
+        return self.k[layer][:, :start + s], self.v[layer][:, :start + s]
+
+    def get_seq_length(self) -> int:
+        return self.len

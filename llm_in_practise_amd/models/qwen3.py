@@ -1,0 +1,372 @@
+"""Native Qwen3 causal LM (Qwen3-4B/8B/14B, DeepSeek-R1-0528-Qwen3-8B).
+
+Replaces the reference's ``AutoModelForCausalLM.from_pretrained(<Qwen3 dir>)``
+(``Fine-Tuning/qwen3-8b-qlora.py:86-101``, ``deepseek-r1-0528-qwen3-8b-qlora.dist.py:99-112``).
+Module names match HF's ``Qwen3ForCausalLM`` so safetensors checkpoints load as-is and
+PEFT adapter keys (``base_model.model.model.layers.{i}.self_attn.q_proj.lora_A.weight``)
+line up.  Architecture [ext: public HF config]: RMSNorm (eps 1e-6), GQA attention with
+per-head q/k RMSNorm, rotate-half RoPE (θ = 1e6, optional YaRN), SwiGLU MLP, untied head
+(4B ties it).
+
+MI355X execution path (one decoder layer):
+  rms_norm → fused q|k|v NF4/bf16 GEMM with LoRA K-slice → q/k-norm+RoPE kernel →
+  flash attention (GQA, causal) → o_proj GEMM with the residual add in its epilogue →
+  rms_norm → fused gate|up GEMM → SwiGLU kernel → down GEMM (+residual) ;
+  final norm → chunked LM-head + cross-entropy kernel (never materialises [T, V] fp32).
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import math
+import os
+
+import torch
+import torch.nn as nn
+import torch.utils.checkpoint as ckpt
+
+from ..ops import reference as ref
+from ..ops.activation import swiglu_fused
+from ..ops.attention import flash_attention
+from ..ops.loss import fused_linear_cross_entropy, shift_labels
+from ..ops.norm import RMSNorm, rms_norm
+from ..ops.rope import qk_norm_rope
+from .common import CausalLMOutput, FusedProjection, KVCache, can_fuse, project
+
+
+@dataclasses.dataclass
+class Qwen3Config:
+    vocab_size: int = 151936
+    hidden_size: int = 4096
+    intermediate_size: int = 12288
+    num_hidden_layers: int = 36
+    num_attention_heads: int = 32
+    num_key_value_heads: int = 8
+    head_dim: int = 128
+    rms_norm_eps: float = 1e-6
+    rope_theta: float = 1_000_000.0
+    rope_scaling: dict | None = None
+    max_position_embeddings: int = 40960
+    tie_word_embeddings: bool = False
+    attention_dropout: float = 0.0
+    bos_token_id: int = 151643
+    eos_token_id: int = 151645
+    pad_token_id: int | None = None
+    torch_dtype: str = "bfloat16"
+    model_type: str = "qwen3"
+    use_cache: bool = True
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "Qwen3Config":
+        fields = {f.name for f in dataclasses.fields(cls)}
+        kw = {k: v for k, v in d.items() if k in fields}
+        if "rope_parameters" in d and isinstance(d["rope_parameters"], dict):   # transformers>=5 layout
+            rp = d["rope_parameters"]
+            kw.setdefault("rope_theta", rp.get("rope_theta", cls.rope_theta))
+            if rp.get("rope_type", "default") not in ("default", None):
+                kw.setdefault("rope_scaling", rp)
+        return cls(**kw)
+
+    @classmethod
+    def from_pretrained(cls, path: str) -> "Qwen3Config":
+        with open(os.path.join(path, "config.json")) as f:
+            return cls.from_dict(json.load(f))
+
+    def to_dict(self) -> dict:
+        d = dataclasses.asdict(self)
+        d["architectures"] = ["Qwen3ForCausalLM"]
+        return d
+
+    def num_params(self) -> int:
+        h, f, L = self.hidden_size, self.intermediate_size, self.num_hidden_layers
+        d, hq, hkv = self.head_dim, self.num_attention_heads, self.num_key_value_heads
+        attn = h * hq * d * 2 + h * hkv * d * 2 + 2 * d
+        mlp = 3 * h * f
+        emb = self.vocab_size * h * (1 if self.tie_word_embeddings else 2)
+        return L * (attn + mlp + 2 * h) + emb + h
+
+
+# [ext] public HF configs
+PRESETS: dict[str, dict] = {
+    "qwen3-8b": dict(hidden_size=4096, intermediate_size=12288, num_hidden_layers=36,
+                     num_attention_heads=32, num_key_value_heads=8, max_position_embeddings=40960),
+    "qwen3-14b": dict(hidden_size=5120, intermediate_size=17408, num_hidden_layers=40,
+                      num_attention_heads=40, num_key_value_heads=8, max_position_embeddings=40960),
+    "qwen3-4b": dict(hidden_size=2560, intermediate_size=9728, num_hidden_layers=36,
+                     num_attention_heads=32, num_key_value_heads=8, tie_word_embeddings=True,
+                     max_position_embeddings=40960),
+    "deepseek-r1-0528-qwen3-8b": dict(hidden_size=4096, intermediate_size=12288, num_hidden_layers=36,
+                                      num_attention_heads=32, num_key_value_heads=8,
+                                      max_position_embeddings=131072,
+                                      rope_scaling={"rope_type": "yarn", "factor": 4.0,
+                                                    "original_max_position_embeddings": 32768}),
+    # small random-init configs for CPU tests / smoke
+    "qwen3-tiny": dict(vocab_size=512, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
+                       num_attention_heads=4, num_key_value_heads=2, head_dim=32,
+                       max_position_embeddings=512),
+    "qwen3-small": dict(vocab_size=4096, hidden_size=1024, intermediate_size=3072, num_hidden_layers=4,
+                        num_attention_heads=8, num_key_value_heads=4, head_dim=128,
+                        max_position_embeddings=4096),
+}
+
+
+def qwen3_config(name: str, **overrides) -> Qwen3Config:
+    kw = dict(PRESETS[name])
+    kw.update(overrides)
+    return Qwen3Config(**kw)
+
+
+class Qwen3Attention(nn.Module):
+    def __init__(self, cfg: Qwen3Config, layer_idx: int):
+        super().__init__()
+        self.cfg, self.layer_idx = cfg, layer_idx
+        h, d = cfg.hidden_size, cfg.head_dim
+        self.hq, self.hkv, self.d = cfg.num_attention_heads, cfg.num_key_value_heads, d
+        self.q_proj = nn.Linear(h, self.hq * d, bias=False)
+        self.k_proj = nn.Linear(h, self.hkv * d, bias=False)
+        self.v_proj = nn.Linear(h, self.hkv * d, bias=False)
+        self.o_proj = nn.Linear(self.hq * d, h, bias=False)
+        self.q_norm = RMSNorm(d, cfg.rms_norm_eps)
+        self.k_norm = RMSNorm(d, cfg.rms_norm_eps)
+        self._qkv: FusedProjection | None = None
+
+    def fuse(self):
+        mods = [self.q_proj, self.k_proj, self.v_proj]
+        self._qkv = FusedProjection(mods) if can_fuse(mods) else None
+
+    def forward(self, x, cos, sin, B, S, residual=None, cache: KVCache | None = None, start: int = 0,
+                kv_lens=None):
+        tr = self.training
+        qkv = project([self.q_proj, self.k_proj, self.v_proj], x, None, tr, self._qkv)
+        q, k, v = qk_norm_rope(qkv, self.q_norm.weight, self.k_norm.weight, cos, sin,
+                               self.hq, self.hkv, self.d, self.cfg.rms_norm_eps)
+        if cache is None:
+            o = flash_attention(q, k, v, B, S, self.hq, self.hkv, self.d, causal=True, kv_lens=kv_lens)
+        else:
+            kc, vc = cache.update(self.layer_idx, k.view(B, S, -1), v.reshape(B, S, -1), start)
+            Sk = kc.shape[1]
+            o = ref.attention(q.view(B, S, self.hq, self.d), kc.view(B, Sk, self.hkv, self.d),
+                              vc.view(B, Sk, self.hkv, self.d), causal=True,
+                              key_padding_mask=(torch.arange(Sk, device=x.device)[None] < kv_lens[:, None])
+                              if kv_lens is not None else None).reshape(B * S, -1)
+        return project([self.o_proj], o, residual, tr)
+
+
+class Qwen3MLP(nn.Module):
+    def __init__(self, cfg: Qwen3Config):
+        super().__init__()
+        h, f = cfg.hidden_size, cfg.intermediate_size
+        self.gate_proj = nn.Linear(h, f, bias=False)
+        self.up_proj = nn.Linear(h, f, bias=False)
+        self.down_proj = nn.Linear(f, h, bias=False)
+        self._gu: FusedProjection | None = None
+
+    def fuse(self):
+        mods = [self.gate_proj, self.up_proj]
+        self._gu = FusedProjection(mods) if can_fuse(mods) else None
+
+    def forward(self, x, residual=None):
+        tr = self.training
+        gu = project([self.gate_proj, self.up_proj], x, None, tr, self._gu)
+        return project([self.down_proj], swiglu_fused(gu), residual, tr)
+
+
+class Qwen3DecoderLayer(nn.Module):
+    def __init__(self, cfg: Qwen3Config, layer_idx: int):
+        super().__init__()
+        self.self_attn = Qwen3Attention(cfg, layer_idx)
+        self.mlp = Qwen3MLP(cfg)
+        self.input_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
+        self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
+
+    def forward(self, x, cos, sin, B, S, cache=None, start=0, kv_lens=None):
+        h = self.self_attn(rms_norm(x, self.input_layernorm.weight, self.input_layernorm.eps),
+                           cos, sin, B, S, residual=x, cache=cache, start=start, kv_lens=kv_lens)
+        return self.mlp(rms_norm(h, self.post_attention_layernorm.weight, self.post_attention_layernorm.eps),
+                        residual=h)
+
+
+class Qwen3Model(nn.Module):
+    def __init__(self, cfg: Qwen3Config):
+        super().__init__()
+        self.cfg = cfg
+        self.embed_tokens = nn.Embedding(cfg.vocab_size, cfg.hidden_size)
+        self.layers = nn.ModuleList([Qwen3DecoderLayer(cfg, i) for i in range(cfg.num_hidden_layers)])
+        self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
+        inv, attn_factor = ref.rope_inv_freq(cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
+        self.register_buffer("inv_freq", inv, persistent=False)
+        self.attn_factor = attn_factor
+        self.gradient_checkpointing = False
+
+    def rope(self, position_ids: torch.Tensor):
+        ang = position_ids.reshape(-1).float()[:, None] * self.inv_freq[None, :]
+        return (torch.cos(ang) * self.attn_factor).contiguous(), (torch.sin(ang) * self.attn_factor).contiguous()
+
+    def forward(self, input_ids, position_ids=None, cache: KVCache | None = None, kv_lens=None):
+        B, S = input_ids.shape
+        start = cache.len if cache is not None else 0
+        if position_ids is None:
+            position_ids = torch.arange(start, start + S, device=input_ids.device).expand(B, S)
+        cos, sin = self.rope(position_ids)
+        x = self.embed_tokens(input_ids).reshape(B * S, -1)
+        for layer in self.layers:
+            if self.gradient_checkpointing and self.training and cache is None:
+                x = ckpt.checkpoint(layer, x, cos, sin, B, S, None, 0, kv_lens, use_reentrant=False)
+            else:
+                x = layer(x, cos, sin, B, S, cache, start, kv_lens)
+        if cache is not None:
+            cache.len = start + S
+        return rms_norm(x, self.norm.weight, self.norm.eps)
+
+
+class Qwen3ForCausalLM(nn.Module):
+    def __init__(self, cfg: Qwen3Config):
+        super().__init__()
+        self.config = cfg
+        self.model = Qwen3Model(cfg)
+        self.lm_head = nn.Linear(cfg.hidden_size, cfg.vocab_size, bias=False)
+        if cfg.tie_word_embeddings:
+            self.lm_head.weight = self.model.embed_tokens.weight
+
+    # -------------------------------------------------------------- construction
+    @classmethod
+    def from_config(cls, cfg: Qwen3Config, dtype=torch.bfloat16, device=None, init_std: float = 0.02,
+                    seed: int | None = 0) -> "Qwen3ForCausalLM":
+        """Random-init (synthetic benchmark weights, no checkpoint download)."""
+        if seed is not None:
+            torch.manual_seed(seed)
+        with torch.device(device or "cpu"):
+            m = cls(cfg)
+        m.to(dtype)
+        with torch.no_grad():
+            for n, p in m.named_parameters():
+                if p.dim() == 2:
+                    p.normal_(0.0, init_std)
+        return m
+
+    def gradient_checkpointing_enable(self, gradient_checkpointing_kwargs=None):
+        self.model.gradient_checkpointing = True
+
+    def gradient_checkpointing_disable(self):
+        self.model.gradient_checkpointing = False
+
+    def enable_input_require_grads(self):
+        pass  # inputs of our fused ops never need requires_grad for checkpointing
+
+    def fuse_projections(self):
+        """Fuse q|k|v and gate|up into single GEMMs (call after quantisation / LoRA)."""
+        for layer in self.model.layers:
+            layer.self_attn.fuse()
+            layer.mlp.fuse()
+        return self
+
+    def invalidate_fusion(self):
+        for layer in self.model.layers:
+            layer.self_attn._qkv = None
+            layer.mlp._gu = None
+
+    # -------------------------------------------------------------- forward
+    def forward(self, input_ids, attention_mask=None, labels=None, position_ids=None,
+                past_key_values: KVCache | None = None, use_cache: bool = False,
+                return_logits: bool | None = None, **_) -> CausalLMOutput:
+        B, S = input_ids.shape
+        kv_lens = None
+        if attention_mask is not None and past_key_values is None:
+            am = attention_mask.to(torch.int32)
+            lens = am.sum(1).to(torch.int32)
+            if torch.equal(am, (torch.arange(S, device=am.device)[None] < lens[:, None]).int()):
+                kv_lens = lens                     # right padding: exact via per-row key length
+        h = self.model(input_ids, position_ids, past_key_values, kv_lens)
+        loss = logits = None
+        if labels is not None:
+            tgt = shift_labels(labels).reshape(-1)
+            loss = fused_linear_cross_entropy(h, self.lm_head.weight, tgt)
+            if return_logits:
+                logits = (h @ self.lm_head.weight.t()).view(B, S, -1)
+        else:
+            logits = (h @ self.lm_head.weight.t()).view(B, S, -1)
+        return CausalLMOutput(loss=loss, logits=logits, past_key_values=past_key_values)
+
+    # -------------------------------------------------------------- checkpoint IO
+    def load_hf_state_dict(self, sd: dict[str, torch.Tensor], strict: bool = False):
+        own = self.state_dict()
+        missing = [k for k in own if k not in sd and "inv_freq" not in k]
+        with torch.no_grad():
+            for k, v in sd.items():
+                if k in own:
+                    own[k].copy_(v.to(own[k].dtype))
+        if strict and missing:
+            raise KeyError(f"missing keys: {missing[:8]}")
+        return missing
+
+    @classmethod
+    def from_pretrained(cls, path: str, dtype=torch.bfloat16, device=None, quantization_config=None,
+                        rope_scaling="keep", **_) -> "Qwen3ForCausalLM":
+        """Load ``config.json`` + ``*.safetensors`` shards from a local HF-layout dir.
+        ``quantization_config`` (``BitsAndBytesConfig``-like, ``load_in_4bit``) quantises each
+        linear to NF4 as it is loaded (on the GPU kernel when ``device`` is cuda)."""
+        from safetensors import safe_open
+        cfg = Qwen3Config.from_pretrained(path)
+        if rope_scaling != "keep":
+            cfg.rope_scaling = rope_scaling          # E7 passes rope_scaling=None
+        with torch.device("meta"):
+            m = cls(cfg)
+        m.to_empty(device=device or "cpu")
+        m.to(dtype)
+        files = sorted(f for f in os.listdir(path) if f.endswith(".safetensors"))
+        sd = {}
+        for f in files:
+            with safe_open(os.path.join(path, f), framework="pt", device="cpu") as fh:
+                for k in fh.keys():
+                    sd[k] = fh.get_tensor(k)
+        m.load_hf_state_dict(sd)
+        inv, af = ref.rope_inv_freq(cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
+        m.model.inv_freq = inv.to(device or "cpu")
+        m.model.attn_factor = af
+        if cfg.tie_word_embeddings:
+            m.lm_head.weight = m.model.embed_tokens.weight
+        if quantization_config is not None and getattr(quantization_config, "load_in_4bit", False):
+            from ..peft.lora import quantize_model_nf4
+            quantize_model_nf4(m, double_quant=quantization_config.bnb_4bit_use_double_quant,
+                               compute_dtype=quantization_config.bnb_4bit_compute_dtype)
+        return m
+
+    def save_pretrained(self, path: str, max_shard_bytes: int = 4 << 30):
+        from safetensors.torch import save_file
+        os.makedirs(path, exist_ok=True)
+        sd = {k: v.detach().cpu().contiguous() for k, v in self.state_dict().items()
+              if "inv_freq" not in k}
+        if self.config.tie_word_embeddings:
+            sd.pop("lm_head.weight", None)
+        shards, cur, size = [], {}, 0
+        for k, v in sd.items():
+            nb = v.numel() * v.element_size()
+            if cur and size + nb > max_shard_bytes:
+                shards.append(cur)
+                cur, size = {}, 0
+            cur[k] = v
+            size += nb
+        shards.append(cur)
+        index = {}
+        for i, sh in enumerate(shards):
+            name = f"model-{i + 1:05d}-of-{len(shards):05d}.safetensors" if len(shards) > 1 else "model.safetensors"
+            save_file(sh, os.path.join(path, name), metadata={"format": "pt"})
+            index.update({k: name for k in sh})
+        if len(shards) > 1:
+            with open(os.path.join(path, "model.safetensors.index.json"), "w") as f:
+                json.dump({"metadata": {}, "weight_map": index}, f, indent=1)
+        with open(os.path.join(path, "config.json"), "w") as f:
+            json.dump(self.config.to_dict(), f, indent=2)
+
+
+class BitsAndBytesConfig:
+    """Argument-compatible stand-in for ``transformers.BitsAndBytesConfig`` (NF4 only)."""
+
+    def __init__(self, load_in_4bit=False, bnb_4bit_compute_dtype=torch.bfloat16, bnb_4bit_quant_type="nf4",
+                 bnb_4bit_use_double_quant=False, bnb_4bit_quant_storage=torch.uint8, **_):
+        assert bnb_4bit_quant_type == "nf4", "only NF4 is implemented (the reference uses nf4)"
+        self.load_in_4bit = load_in_4bit
+        self.bnb_4bit_compute_dtype = bnb_4bit_compute_dtype
+        self.bnb_4bit_quant_type = bnb_4bit_quant_type
+        self.bnb_4bit_use_double_quant = bnb_4bit_use_double_quant
+        self.bnb_4bit_quant_storage = bnb_4bit_quant_storage

@@ -1,0 +1,77 @@
+"""RMSNorm / LayerNorm (K2, K4).  One-pass row-reduce HIP kernels on gfx950."""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import reference as ref
+from ._native import native, use_native
+
+
+class _RMSNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, eps):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).contiguous()
+        y, rstd = native().rmsnorm_fwd(x2, weight, eps)
+        ctx.save_for_backward(x2, weight, rstd)
+        ctx.shape = shape
+        return y.view(shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight, rstd = ctx.saved_tensors
+        need_dw = weight is not None and ctx.needs_input_grad[1]
+        dx, dw = native().rmsnorm_bwd(dy.reshape(x2.shape).contiguous(), x2, weight, rstd, need_dw)
+        return dx.view(ctx.shape), (dw.to(weight.dtype) if need_dw else None), None
+
+
+def rms_norm(x: torch.Tensor, weight: torch.Tensor | None, eps: float = 1e-6) -> torch.Tensor:
+    if use_native(x):
+        return _RMSNormFn.apply(x, weight, eps)
+    return ref.rmsnorm(x, weight, eps)
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).contiguous()
+        y, mean, rstd = native().layernorm_fwd(x2, weight, bias, eps)
+        ctx.save_for_backward(x2, weight, mean, rstd)
+        ctx.shape = shape
+        ctx.has_bias = bias is not None
+        return y.view(shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight, mean, rstd = ctx.saved_tensors
+        need_dw = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        dx, dw, db = native().layernorm_bwd(dy.reshape(x2.shape).contiguous(), x2, weight, mean, rstd, need_dw)
+        return (dx.view(ctx.shape), dw.to(weight.dtype) if need_dw else None,
+                db.to(weight.dtype) if (need_dw and ctx.has_bias) else None, None)
+
+
+def layer_norm(x, weight, bias, eps: float = 1e-5):
+    if use_native(x):
+        return _LayerNormFn.apply(x, weight, bias, eps)
+    return torch.nn.functional.layer_norm(x, (x.shape[-1],), weight, bias, eps)
+
+
+class RMSNorm(nn.Module):
+    """Qwen3 ``RMSNorm`` (input/post-attention/final norms and per-head q/k norms)."""
+
+    def __init__(self, dim: int, eps: float = 1e-6):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(dim))
+        self.eps = eps
+
+    def forward(self, x):
+        return rms_norm(x, self.weight, self.eps)
+
+
+class LayerNorm(nn.LayerNorm):
+    """``nn.LayerNorm`` with the gfx950 kernel underneath (GPTLike / MiniGPT blocks)."""
+
+    def forward(self, x):
+        return layer_norm(x, self.weight, self.bias, self.eps)

@@ -1,0 +1,281 @@
+"""Numerics of every gfx950 HIP kernel against a plain PyTorch fp32 reference of the same op
+(SURVEY.md §7.4).  All tests need the GPU and the in-tree ``_C`` extension."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from llm_in_practise_amd.ops import reference as ref
+from llm_in_practise_amd.quant.nf4 import dequantize_nf4, quantize_nf4
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+@pytest.fixture(autouse=True)
+def _seed():
+    torch.manual_seed(0)
+
+
+# ----------------------------------------------------------------------------- norms
+@pytest.mark.parametrize("M,N", [(1024, 4096), (37, 5120), (8, 128), (300, 768)])
+def test_rmsnorm_fwd_bwd(native_ext, M, N):
+    x = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16)
+    y, rstd = native_ext.rmsnorm_fwd(x, w, 1e-6)
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * wr
+    assert rel_err(y, yr) < 1e-2
+    dy = torch.randn_like(x)
+    dx, dw = native_ext.rmsnorm_bwd(dy, x, w, rstd, True)
+    yr.backward(dy.float())
+    assert rel_err(dx, xr.grad) < 1e-2
+    assert rel_err(dw, wr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("M,N", [(512, 768), (33, 1024), (16, 64)])
+def test_layernorm_fwd_bwd(native_ext, M, N):
+    x = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, device=DEV).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV).to(torch.bfloat16)
+    y, mean, rstd = native_ext.layernorm_fwd(x, w, b, 1e-5)
+    xr, wr, br = [t.float().requires_grad_(True) for t in (x, w, b)]
+    yr = F.layer_norm(xr, (N,), wr, br, 1e-5)
+    assert rel_err(y, yr) < 1e-2
+    dy = torch.randn_like(x)
+    dx, dw, db = native_ext.layernorm_bwd(dy, x, w, mean, rstd, True)
+    yr.backward(dy.float())
+    assert rel_err(dx, xr.grad) < 2e-2
+    assert rel_err(dw, wr.grad) < 1e-2
+    assert rel_err(db, br.grad) < 1e-2
+
+
+# ----------------------------------------------------------------------------- rope
+@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (4, 2, 64), (8, 8, 32)])
+def test_qk_norm_rope(native_ext, hq, hkv, d):
+    T = 300
+    qkv = torch.randn(T, (hq + 2 * hkv) * d, device=DEV, dtype=torch.bfloat16)
+    qw = (1 + 0.1 * torch.randn(d, device=DEV)).to(torch.bfloat16)
+    kw = (1 + 0.1 * torch.randn(d, device=DEV)).to(torch.bfloat16)
+    pos = torch.arange(T, device=DEV)
+    cos, sin = ref.rope_cos_sin(pos, d, 1e6)
+    q, k, rq, rk = native_ext.qk_norm_rope_fwd(qkv, qw, kw, cos, sin, hq, hkv, d, 1e-6)
+    x = qkv.float().requires_grad_(True)
+    qr = x[:, :hq * d].view(T, hq, d)
+    kr = x[:, hq * d:(hq + hkv) * d].view(T, hkv, d)
+    qn = qr * torch.rsqrt(qr.pow(2).mean(-1, keepdim=True) + 1e-6) * qw.float()
+    kn = kr * torch.rsqrt(kr.pow(2).mean(-1, keepdim=True) + 1e-6) * kw.float()
+    qo = ref.apply_rope(qn, cos, sin)
+    ko = ref.apply_rope(kn, cos, sin)
+    assert rel_err(q.view(T, hq, d), qo) < 1e-2
+    assert rel_err(k.view(T, hkv, d), ko) < 1e-2
+    dq = torch.randn_like(q)
+    dk = torch.randn_like(k)
+    dv = torch.randn(T, hkv * d, device=DEV, dtype=torch.bfloat16)
+    dqkv = native_ext.qk_norm_rope_bwd(dq, dk, dv, qkv, qw, kw, cos, sin, rq, rk, hq, hkv, d)
+    (qo * dq.float().view(T, hq, d)).sum().add((ko * dk.float().view(T, hkv, d)).sum()).backward()
+    g = x.grad.clone()
+    g[:, (hq + hkv) * d:] = dv.float()
+    assert rel_err(dqkv, g) < 2e-2
+
+
+def test_rope_generic(native_ext):
+    T, H, D = 64, 4, 32
+    x = torch.randn(T, H, D, device=DEV, dtype=torch.bfloat16)
+    cos, sin = ref.rope_cos_sin(torch.arange(T, device=DEV), D, 1e4)
+    for inter in (False, True):
+        y = native_ext.rope(x, cos, sin, inter, False)
+        assert rel_err(y, ref.apply_rope(x.float(), cos, sin, inter)) < 1e-2
+        back = native_ext.rope(y, cos, sin, inter, True)
+        assert rel_err(back, x) < 2e-2
+
+
+# ----------------------------------------------------------------------------- activations / loss
+def test_swiglu(native_ext):
+    gu = torch.randn(100, 2 * 1024, device=DEV, dtype=torch.bfloat16)
+    y = native_ext.swiglu_fwd(gu)
+    x = gu.float().requires_grad_(True)
+    yr = F.silu(x[:, :1024]) * x[:, 1024:]
+    assert rel_err(y, yr) < 1e-2
+    dy = torch.randn_like(y)
+    yr.backward(dy.float())
+    assert rel_err(native_ext.swiglu_bwd(dy, gu), x.grad) < 1e-2
+
+
+def test_gelu(native_ext):
+    x = torch.randn(1000, 96, device=DEV, dtype=torch.bfloat16)
+    xr = x.float().requires_grad_(True)
+    yr = F.gelu(xr)
+    assert rel_err(native_ext.gelu_fwd(x), yr) < 1e-2
+    dy = torch.randn_like(x)
+    yr.backward(dy.float())
+    assert rel_err(native_ext.gelu_bwd(dy, x), xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("V", [151936, 512])
+def test_cross_entropy(native_ext, V):
+    M = 64
+    logits = (3 * torch.randn(M, V, device=DEV)).to(torch.bfloat16)
+    labels = torch.randint(0, V, (M,), device=DEV)
+    labels[::7] = -100
+    n_valid = (labels != -100).sum()
+    lf = logits.float().requires_grad_(True)
+    loss_ref = F.cross_entropy(lf, labels, ignore_index=-100)
+    loss_ref.backward()
+    lg = logits.clone()
+    rows = native_ext.ce_fwd_bwd(lg, labels, -100, (1.0 / n_valid.float()).reshape(1))
+    assert abs(rows.sum().item() / n_valid.item() - loss_ref.item()) < 1e-3 * max(1, loss_ref.item())
+    assert rel_err(lg, lf.grad) < 2e-2
+
+
+# ----------------------------------------------------------------------------- optimizer
+def test_adamw_matches_torch(native_ext):
+    n = 100_003
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    pt = p.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([pt], lr=1e-2, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1)
+    for step in range(1, 4):
+        native_ext.adamw(p, g, m, v, None, 1e-2, 0.9, 0.999, 1e-8, 0.1, step, None, None)
+        pt.grad = g.clone()
+        opt.step()
+    assert rel_err(p, pt.detach()) < 1e-5
+
+
+def test_grad_norm_and_clip(native_ext):
+    g = torch.randn(1_000_000, device=DEV)
+    out = native_ext.grad_norm(g, 1.0, None, False)
+    assert abs(out[0].item() - g.norm().item()) / g.norm().item() < 1e-4
+    assert abs(out[1].item() - min(1.0, 1.0 / (g.norm().item() + 1e-6))) < 1e-6
+
+
+def test_adamw8bit_tracks_fp32(native_ext):
+    from llm_in_practise_amd.quant.nf4 import create_dynamic_map
+    n = 4096
+    p = torch.randn(n, device=DEV)
+    p8 = p.clone()
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    qm = torch.full((n,), 127, dtype=torch.uint8, device=DEV)
+    qv = torch.zeros(n, dtype=torch.uint8, device=DEV)
+    am = torch.zeros(n // 256, device=DEV)
+    av = torch.zeros(n // 256, device=DEV)
+    cs = create_dynamic_map(True).to(DEV)
+    cu = create_dynamic_map(False).to(DEV)
+    qm.fill_(int(torch.argmin(cs.abs())))
+    qv.fill_(int(torch.argmin(cu.abs())))
+    for step in range(1, 6):
+        g = torch.randn(n, device=DEV)
+        native_ext.adamw(p, g, m, v, None, 1e-3, 0.9, 0.999, 1e-8, 0.0, step, None, None)
+        native_ext.adamw8bit(p8, g, qm, qv, am, av, cs, cu, None, 1e-3, 0.9, 0.999, 1e-8, 0.0, step, None, None)
+    assert rel_err(p8, p) < 1e-3
+
+
+# ----------------------------------------------------------------------------- NF4
+def test_nf4_quantize_matches_reference(native_ext):
+    w = torch.randn(256, 512, device=DEV).to(torch.bfloat16)
+    codes, absmax = native_ext.nf4_quantize(w, 64)
+    q = quantize_nf4(w, 64, double_quant=False)
+    assert torch.equal(codes, q.codes)
+    assert torch.allclose(absmax, q.absmax)
+    deq = native_ext.nf4_dequant(codes, absmax, None, None, None, None, 256, 512)
+    assert torch.equal(deq, dequantize_nf4(q, torch.bfloat16))
+
+
+def _lora_ref(x, w, ext_a=None, ext_b=None, res=None):
+    y = x.float() @ w.float().t()
+    if ext_a is not None:
+        y = y + ext_a.float() @ ext_b.float().t()
+    if res is not None:
+        y = y + res.float()
+    return y
+
+
+@pytest.mark.parametrize("M,N,K", [(1024, 6144, 4096), (1000, 512, 1024), (64, 128, 256), (2048, 24576, 512)])
+@pytest.mark.parametrize("dq", [True, False])
+def test_gemm_nf4_fwd_bwd(native_ext, M, N, K, dq):
+    w = torch.randn(N, K, device=DEV).to(torch.bfloat16)
+    q = quantize_nf4(w, 64, double_quant=dq)
+    wd = dequantize_nf4(q, torch.float32)
+    cf, cb, at = q.kernel_pack()
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    R = 32
+    ea = (0.1 * torch.randn(M, R, device=DEV)).to(torch.bfloat16)
+    eb = (0.1 * torch.randn(N, R, device=DEV)).to(torch.bfloat16)
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    y = native_ext.gemm_nf4(x, cf, at, N, ea, eb, res)
+    assert rel_err(y, _lora_ref(x, wd, ea, eb, res)) < 1e-2
+    y0 = native_ext.gemm_nf4(x, cf, at, N, None, None, None)
+    assert rel_err(y0, _lora_ref(x, wd)) < 1e-2
+    dy = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    eb2 = (0.1 * torch.randn(K, R, device=DEV)).to(torch.bfloat16)
+    dx = native_ext.gemm_nf4_t(dy, cb, at, K, ea, eb2)
+    assert rel_err(dx, dy.float() @ wd + ea.float() @ eb2.float().t()) < 1e-2
+
+
+def test_gemm_nf4_asymmetric_layout(native_ext):
+    """A = I style check with an asymmetric weight catches a transposed epilogue."""
+    N, K = 128, 128
+    w = torch.arange(N * K, device=DEV, dtype=torch.float32).view(N, K) % 13 - 6
+    q = quantize_nf4(w.to(torch.bfloat16), 64, double_quant=False)
+    wd = dequantize_nf4(q, torch.float32)
+    cf, cb, at = q.kernel_pack()
+    x = torch.eye(K, device=DEV, dtype=torch.bfloat16)
+    y = native_ext.gemm_nf4(x, cf, at, N, None, None, None)
+    assert torch.allclose(y.float(), wd.t().to(torch.bfloat16).float(), atol=1e-2)
+    dx = native_ext.gemm_nf4_t(torch.eye(N, device=DEV, dtype=torch.bfloat16), cb, at, K, None, None)
+    assert torch.allclose(dx.float(), wd.to(torch.bfloat16).float(), atol=1e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(1024, 4096, 4096), (77, 256, 128)])
+def test_gemm_bf16_lora(native_ext, M, N, K):
+    w = (0.05 * torch.randn(N, K, device=DEV)).to(torch.bfloat16)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    ea = torch.randn(M, 32, device=DEV).to(torch.bfloat16)
+    eb = (0.1 * torch.randn(N, 32, device=DEV)).to(torch.bfloat16)
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    y = native_ext.gemm_bf16(x, w, ea, eb, res)
+    assert rel_err(y, _lora_ref(x, w, ea, eb, res)) < 1e-2
+
+
+# ----------------------------------------------------------------------------- attention
+@pytest.mark.parametrize("B,S,hq,hkv,d,causal", [(2, 512, 32, 8, 128, True), (1, 256, 4, 4, 64, True),
+                                                  (2, 128, 8, 2, 128, False), (1, 192, 4, 2, 64, True)])
+def test_flash_attention_fwd_bwd(native_ext, B, S, hq, hkv, d, causal):
+    T = B * S
+    q = torch.randn(T, hq * d, device=DEV).to(torch.bfloat16)
+    kv = torch.randn(T, 2 * hkv * d, device=DEV).to(torch.bfloat16)
+    k, v = kv[:, :hkv * d], kv[:, hkv * d:]          # strided views (fused-projection layout)
+    scale = 1 / math.sqrt(d)
+    o, lse = native_ext.attn_fwd(q, k, v, None, B, S, hq, hkv, d, causal, scale)
+    qr, kr, vr = [t.float().reshape(B, S, -1, d).requires_grad_(True) for t in (q, k, v)]
+    orf = ref.attention(qr, kr, vr, causal=causal, scale=scale)
+    assert rel_err(o.view(B, S, hq, d), orf) < 1e-2
+    do = torch.randn_like(o)
+    dq, dk, dv = native_ext.attn_bwd(do, q, k, v, o, lse, None, B, S, hq, hkv, d, causal, scale)
+    orf.backward(do.float().view(B, S, hq, d))
+    assert rel_err(dq.view(B, S, hq, d), qr.grad) < 2e-2
+    assert rel_err(dk.view(B, S, hkv, d), kr.grad) < 2e-2
+    assert rel_err(dv.view(B, S, hkv, d), vr.grad) < 2e-2
+
+
+def test_flash_attention_padding(native_ext):
+    B, S, h, d = 2, 128, 4, 64
+    q = torch.randn(B * S, h * d, device=DEV).to(torch.bfloat16)
+    k = torch.randn(B * S, h * d, device=DEV).to(torch.bfloat16)
+    v = torch.randn(B * S, h * d, device=DEV).to(torch.bfloat16)
+    lens = torch.tensor([100, 128], device=DEV, dtype=torch.int32)
+    o, _ = native_ext.attn_fwd(q, k, v, lens, B, S, h, h, d, True, 0.125)
+    mask = torch.arange(S, device=DEV)[None] < lens[:, None]
+    orf = ref.attention(*(t.float().view(B, S, h, d) for t in (q, k, v)), causal=True, key_padding_mask=mask,
+                        scale=0.125)
+    assert rel_err(o.view(B, S, h, d)[mask], orf[mask]) < 1e-2
