@@ -83,6 +83,9 @@ def main():
     ap.add_argument("--grad-ckpt", action="store_true",
                     help="recompute each decoder layer in backward (the reference's 24 GB-GPU setting; "
                          "off by default: 288 GB HBM holds every activation)")
+    ap.add_argument("--ga-fusion", type=int, default=1,
+                    help="1: execute the grad-accum micro-batches in one pass (per-micro-batch loss "
+                         "normalisation, identical gradient); 0: sequential micro-steps")
     args = ap.parse_args()
 
     rank, local_rank, world = D.init_distributed()
@@ -101,13 +104,21 @@ def main():
     it = [0]
 
     def step():
-        for micro in range(args.grad_accum):
-            ids = data[it[0] % n_batches]
-            it[0] += 1
-            ctx = ddp.no_sync() if micro < args.grad_accum - 1 else contextlib.nullcontext()
-            with ctx:
-                out = model(ids, labels=ids)
-                (out.loss / args.grad_accum).backward()
+        if args.ga_fusion:
+            # the GA micro-batches are independent given the (frozen-during-the-step) weights:
+            # run them as one pass with per-micro-batch loss normalisation (same gradient)
+            ids = torch.cat([data[(it[0] + g) % n_batches] for g in range(args.grad_accum)])
+            it[0] += args.grad_accum
+            out = model(ids, labels=ids, num_micro_batches=args.grad_accum)
+            out.loss.backward()
+        else:
+            for micro in range(args.grad_accum):
+                ids = data[it[0] % n_batches]
+                it[0] += 1
+                ctx = ddp.no_sync() if micro < args.grad_accum - 1 else contextlib.nullcontext()
+                with ctx:
+                    out = model(ids, labels=ids)
+                    (out.loss / args.grad_accum).backward()
         ddp.allreduce_grads()
         opt.clip_grad_norm_(1.0)
         opt.step()
@@ -167,6 +178,7 @@ def main():
                 "lora": f"r{args.lora_r}/a{args.lora_alpha}/drop{args.lora_dropout}/{args.targets}",
                 "optimizer": args.optim,
                 "gradient_checkpointing": bool(args.grad_ckpt),
+                "ga_execution": "fused-pass" if args.ga_fusion else "sequential",
                 "weights": "random-init",
                 "peak_hbm_gib": round(mem, 1),
             },

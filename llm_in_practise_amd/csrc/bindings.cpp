@@ -48,6 +48,9 @@ void launch_attn_bwd(const void*, const void*, const void*, const void*, const v
                      int, int, void*, void*, void*, float*, float*, float*, float*, int, int, int, int, int, int,
                      float, hipStream_t);
 
+void launch_dropout_fwd(const void*, void*, size_t, uint64_t, float, hipStream_t);
+void launch_dropout_bwd_add(void*, const void*, size_t, uint64_t, float, hipStream_t);
+
 namespace {
 
 using at::Tensor;
@@ -198,6 +201,21 @@ Tensor gelu_bwd(Tensor dy, Tensor x) {
   auto dx = at::empty_like(x);
   launch_gelu_bwd(dtype_code(x), dy.data_ptr(), x.data_ptr(), dx.data_ptr(), x.numel(), stream());
   return dx;
+}
+
+// ------------------------------------------------------------------ dropout (counter RNG)
+Tensor dropout_fwd(Tensor x, double p, int64_t key) {
+  CHECK_BF16(x);
+  CHECK_CONTIG(x);
+  TORCH_CHECK(x.numel() % 8 == 0, "dropout: numel % 8");
+  auto y = at::empty_like(x);
+  launch_dropout_fwd(x.data_ptr(), y.data_ptr(), x.numel(), (uint64_t)key, (float)p, stream());
+  return y;
+}
+void dropout_bwd_add(Tensor dx, Tensor t, double p, int64_t key) {
+  CHECK_CONTIG(dx);
+  CHECK_CONTIG(t);
+  launch_dropout_bwd_add(dx.data_ptr(), t.data_ptr(), dx.numel(), (uint64_t)key, (float)p, stream());
 }
 
 // ------------------------------------------------------------------ cross entropy
@@ -421,6 +439,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("ce_fwd_bwd", &ce_fwd_bwd);
+  m.def("dropout_fwd", &dropout_fwd);
+  m.def("dropout_bwd_add", &dropout_bwd_add);
   m.def("grad_norm", &grad_norm);
   m.def("adamw", &adamw);
   m.def("adamw8bit", &adamw8bit);

@@ -69,19 +69,124 @@ __device__ __forceinline__ const char* a_frag_addr(const char* buf, int mt, int 
   return buf + r * 128 + ((c ^ ((r >> 1) & 7)) << 4);
 }
 
-// 8 nibbles (nibble j at bits 4j) → 8 bf16 = code[nib]*scale (fwd: one absmax per dword)
-__device__ __forceinline__ bf16x8 dequant8(uint32_t x, float sc, const float* lut) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (bf16)(lut[(x >> (4 * j)) & 15] * sc);
-  return r;
+// LUT lookup by byte offset (nibble*4) into the 16-entry fp32 code table in LDS
+__device__ __forceinline__ float lut_at(const float* lut, uint32_t byte_off) {
+  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(lut) + byte_off);
 }
-// backward: nibble j has its own absmax
-__device__ __forceinline__ bf16x8 dequant8v(uint32_t x, const float (&sc)[8], const float* lut) {
-  bf16x8 r;
+// 8 nibbles (nibble j at bits 4j) → 8 byte offsets: lo4 holds nibbles 0,2,4,6 ×4, hi4 nibbles 1,3,5,7 ×4
+__device__ __forceinline__ void nib_offsets(uint32_t x, uint32_t& lo4, uint32_t& hi4) {
+  lo4 = (x << 2) & 0x3C3C3C3Cu;
+  hi4 = (x >> 2) & 0x3C3C3C3Cu;
+}
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// one v_bfe_u32 (hipcc otherwise expands ubfe into shift+and: 2 VALU per nibble)
+template <int OFF>
+__device__ __forceinline__ uint32_t bfe8_c(uint32_t x) {
+  if constexpr (OFF == 0) return x & 0xFFu;
+  else if constexpr (OFF == 24) return x >> 24;
+  else {
+    uint32_t r;
+    asm("v_bfe_u32 %0, %1, %2, 8" : "=v"(r) : "v"(x), "i"(OFF));
+    return r;
+  }
+}
+__device__ __forceinline__ uint32_t bfe8(uint32_t x, int off) {
+  switch (off) {
+    case 0: return bfe8_c<0>(x);
+    case 8: return bfe8_c<8>(x);
+    case 16: return bfe8_c<16>(x);
+    default: return bfe8_c<24>(x);
+  }
+}
+// two fp32 → packed bf16x2 in one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t pk2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
+}
+// 8 LUT values for the 8 nibbles of x: one v_bfe_u32 per element on the pre-scaled (×4)
+// nibble images, then ds_read_b32 from the LDS code table
+__device__ __forceinline__ void lut8(uint32_t x, const float* lut, float (&v)[8]) {
+  uint32_t lo4, hi4;
+  nib_offsets(x, lo4, hi4);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (bf16)(lut[(x >> (4 * j)) & 15] * sc[j]);
-  return r;
+  for (int b = 0; b < 4; ++b) {
+    v[2 * b] = lut_at(lut, bfe8(lo4, 8 * b));
+    v[2 * b + 1] = lut_at(lut, bfe8(hi4, 8 * b));
+  }
+}
+// fwd: one absmax for all 8 elements
+__device__ __forceinline__ bf16x8 dequant8(uint32_t x, float sc, const float* lut) {
+  float v[8];
+  lut8(x, lut, v);
+  u32x4 r{pk2(v[0] * sc, v[1] * sc), pk2(v[2] * sc, v[3] * sc), pk2(v[4] * sc, v[5] * sc),
+          pk2(v[6] * sc, v[7] * sc)};
+  return __builtin_bit_cast(bf16x8, r);
+}
+// bwd: nibble j has its own absmax
+__device__ __forceinline__ bf16x8 dequant8v(uint32_t x, f32x4 s0, f32x4 s1, const float* lut) {
+  float v[8];
+  lut8(x, lut, v);
+  u32x4 r{pk2(v[0] * s0[0], v[1] * s0[1]), pk2(v[2] * s0[2], v[3] * s0[3]), pk2(v[4] * s1[0], v[5] * s1[1]),
+          pk2(v[6] * s1[2], v[7] * s1[3])};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+// One K-step worth of a wave's packed weights: 4 code dwords + absmax (fwd: 2 scalars for
+// the lane's two columns; bwd: 8 per 32-row half for the lane's 8 reduction rows).
+template <bool BWD>
+struct StepW;
+template <>
+struct StepW<false> {
+  u32x4 c;
+  float a0, a1;
+};
+template <>
+struct StepW<true> {
+  u32x4 c;
+  f32x4 a[4];
+};
+
+template <bool BWD>
+__device__ __forceinline__ void load_step(StepW<BWD>& q, const u32x4* cptr, const float* aptr, int t, int C) {
+  q.c = cptr[(size_t)t * 64];
+  if constexpr (!BWD) {
+    q.a0 = aptr[(size_t)t * C];
+    q.a1 = aptr[(size_t)t * C + 16];
+  } else {
+    const float* p = aptr + t * BK;
+    q.a[0] = *reinterpret_cast<const f32x4*>(p);
+    q.a[1] = *reinterpret_cast<const f32x4*>(p + 4);
+    q.a[2] = *reinterpret_cast<const f32x4*>(p + 32);
+    q.a[3] = *reinterpret_cast<const f32x4*>(p + 36);
+  }
+}
+
+// half h = column half st (fwd) — both reduction substeps of one 16-column fragment pair
+template <bool BWD>
+__device__ __forceinline__ void dequant_half(const StepW<BWD>& q, const float* lut, bf16x8 (&wf)[2][2], int h) {
+  if constexpr (!BWD) {
+    const float a = h ? q.a1 : q.a0;
+    wf[h][0] = dequant8(q.c[2 * h], a, lut);
+    wf[h][1] = dequant8(q.c[2 * h + 1], a, lut);
+  } else {
+    wf[h][0] = dequant8v(q.c[2 * h], q.a[0], q.a[1], lut);
+    wf[h][1] = dequant8v(q.c[2 * h + 1], q.a[2], q.a[3], lut);
+  }
+}
+
+template <bool BWD>
+__device__ __forceinline__ void dequant_step(const StepW<BWD>& q, const float* lut, bf16x8 (&wf)[2][2]) {
+  if constexpr (!BWD) {
+    wf[0][0] = dequant8(q.c[0], q.a0, lut);
+    wf[0][1] = dequant8(q.c[1], q.a0, lut);
+    wf[1][0] = dequant8(q.c[2], q.a1, lut);
+    wf[1][1] = dequant8(q.c[3], q.a1, lut);
+  } else {
+    // dword (st, s): rows 32s + 8(lane>>4) + j share the lane's absmax run for half s
+    wf[0][0] = dequant8v(q.c[0], q.a[0], q.a[1], lut);
+    wf[0][1] = dequant8v(q.c[1], q.a[2], q.a[3], lut);
+    wf[1][0] = dequant8v(q.c[2], q.a[0], q.a[1], lut);
+    wf[1][1] = dequant8v(q.c[3], q.a[2], q.a[3], lut);
+  }
 }
 
 // OUT[m][c] = Σ_r A[m][r] · Wop(c, r)  (+ Σ_e ext_a[m][e]·ext_b[c][e])  (+ residual[m][c])
@@ -118,56 +223,59 @@ __global__ __launch_bounds__(NTHR) void gemm_w4_k(const bf16* __restrict__ A, in
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[st][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Software pipeline (per wave, registers): codes + absmax are loaded TWO K-steps ahead and
+  // dequantised ONE step ahead, so the dequant VALU/LUT work of step t+1 overlaps the MFMAs
+  // of step t and no register load is ever consumed in the iteration that issued it (the
+  // end-of-iteration barrier drains the LDS-DMA and the register loads together).
   const u32x4* cptr = reinterpret_cast<const u32x4*>(codes) + ((size_t)(active ? T : 0) * nk) * 64 + lane;
-  u32x4 c_cur = active ? cptr[0] : u32x4{0, 0, 0, 0};
-  u32x4 c_nxt = (active && nk > 1) ? cptr[64] : u32x4{0, 0, 0, 0};
-
+  const float* aptr = BWD ? absmax_t + (size_t)((active ? cw : 0) >> 6) * R + 8 * (lane >> 4)
+                          : absmax_t + (active ? cw : 0) + (lane & 15);
+  StepW<BWD> q1, q2;
+  if (active) {
+    load_step<BWD>(q1, cptr, aptr, 0, C);
+    if (nk > 1) load_step<BWD>(q2, cptr, aptr, 1, C);
+  }
   stage_a<BM>(A, lda, m0, M, 0, smem);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  bf16x8 wf[2][2];
+  if (active) dequant_step<BWD>(q1, lut, wf);
+  q1 = q2;
 
   for (int t = 0; t < nk; ++t) {
-    char* cur = smem + (t & 1) * ABUF;
-    if (t + 1 < nk) stage_a<BM>(A, lda, m0, M, (t + 1) * BK, smem + ((t + 1) & 1) * ABUF);
-    u32x4 c_nn = (active && t + 2 < nk) ? cptr[(size_t)(t + 2) * 64] : u32x4{0, 0, 0, 0};
+    const char* cur = smem + (t & 1) * ABUF;
+    // branch-free prefetch: past the end, re-load the last step (into a buffer / registers
+    // nobody reads again) so the loop body is one basic block the scheduler can interleave
+    stage_a<BM>(A, lda, m0, M, min(t + 1, nk - 1) * BK, smem + ((t + 1) & 1) * ABUF);
+    if (active) load_step<BWD>(q2, cptr, aptr, min(t + 2, nk - 1), C);
     if (active) {
-      // ---- dequantise this wave's 4 weight fragments (32 columns × 64 reduction)
-      bf16x8 wf[2][2];
-      if constexpr (!BWD) {
-        float sc0 = absmax_t[(size_t)t * C + cw + (lane & 15)];
-        float sc1 = absmax_t[(size_t)t * C + cw + 16 + (lane & 15)];
-        wf[0][0] = dequant8(c_cur[0], sc0, lut);
-        wf[0][1] = dequant8(c_cur[1], sc0, lut);
-        wf[1][0] = dequant8(c_cur[2], sc1, lut);
-        wf[1][1] = dequant8(c_cur[3], sc1, lut);
-      } else {
-        const float* ab = absmax_t + (size_t)(cw >> 6) * R + t * BK + 8 * (lane >> 4);
-        float s0[8], s1[8];
-        f32x4 a0 = *reinterpret_cast<const f32x4*>(ab), a1 = *reinterpret_cast<const f32x4*>(ab + 4);
-        f32x4 b0 = *reinterpret_cast<const f32x4*>(ab + 32), b1 = *reinterpret_cast<const f32x4*>(ab + 36);
+      // MFMA over the staged activation tile (weights of step t in wf) with the dequant of
+      // step t+1 interleaved: substep s=0 overlaps the column-half-0 fragments, s=1 the
+      // column-half-1 fragments; activation fragments are read one substep ahead.
+      bf16x8 wn[2][2];
+      // activation fragments f = s*MT + mt stream through a register ring of depth RD
+      constexpr int RD = MT < 8 ? MT : 8;
+      bf16x8 xr[RD];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          s0[j] = a0[j]; s0[j + 4] = a1[j]; s1[j] = b0[j]; s1[j + 4] = b1[j];
-        }
-        wf[0][0] = dequant8v(c_cur[0], s0, lut);
-        wf[0][1] = dequant8v(c_cur[1], s1, lut);
-        wf[1][0] = dequant8v(c_cur[2], s0, lut);
-        wf[1][1] = dequant8v(c_cur[3], s1, lut);
+      for (int f = 0; f < RD; ++f) xr[f] = lds_read16(a_frag_addr(cur, f % MT, f / MT, lane));
+#pragma unroll
+      for (int f = 0; f < 2 * MT; ++f) {
+        const int s = f / MT, mt = f % MT;
+        if (f == 0) dequant_half<BWD>(q1, lut, wn, 0);
+        if (f == MT) dequant_half<BWD>(q1, lut, wn, 1);
+        const bf16x8 xf = xr[f % RD];
+        if (f + RD < 2 * MT) xr[f % RD] = lds_read16(a_frag_addr(cur, (f + RD) % MT, (f + RD) / MT, lane));
+        acc[0][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0][s], xf, acc[0][mt], 0, 0, 0);
+        acc[1][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[1][s], xf, acc[1][mt], 0, 0, 0);
       }
-      // ---- MFMA over the staged activation tile
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const bf16x8 xf = lds_read16(a_frag_addr(cur, mt, s, lane));
-          acc[0][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0][s], xf, acc[0][mt], 0, 0, 0);
-          acc[1][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[1][s], xf, acc[1][mt], 0, 0, 0);
-        }
+      for (int i = 0; i < 4 * MT; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read (LUT / next fragment)
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // 2 VALU (dequant)
       }
+      wf[0][0] = wn[0][0]; wf[0][1] = wn[0][1]; wf[1][0] = wn[1][0]; wf[1][1] = wn[1][1];
+      q1 = q2;
     }
-    c_cur = c_nxt;
-    c_nxt = c_nn;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
@@ -397,9 +505,16 @@ __global__ __launch_bounds__(256) void nf4_dequant_k(const uint8_t* __restrict__
 
 // ------------------------------------------------------------------ launchers
 static inline int pick_mt(int M, int C) {
-  // 256-row tiles halve the dequant work per MFMA; use them only when they still fill the chip
+  static const int forced = [] {
+    const char* e = getenv("LIPA_GEMM_MT");  // A/B experiments: 8 or 16
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 8 || forced == 16) return forced;
+  // Measured (scripts/bench_gemm.py, MI355X): the 128-row tile at 2 waves/SIMD beats the
+  // 256-row tile (1 wave/SIMD at 338 registers) at every Qwen3 shape for M = 1024-2048;
+  // 256-row tiles only win once there are >= 4 of them per CU.
   const long tiles256 = (long)((M + 255) / 256) * ((C + BN - 1) / BN);
-  return tiles256 >= 512 ? 16 : 8;
+  return tiles256 >= 1024 ? 16 : 8;
 }
 
 void launch_gemm_w4(int bwd, const void* A, int lda, const uint32_t* codes, const float* absmax_t, const void* ext_a,

@@ -268,7 +268,10 @@ class Qwen3ForCausalLM(nn.Module):
     # -------------------------------------------------------------- forward
     def forward(self, input_ids, attention_mask=None, labels=None, position_ids=None,
                 past_key_values: KVCache | None = None, use_cache: bool = False,
-                return_logits: bool | None = None, **_) -> CausalLMOutput:
+                return_logits: bool | None = None, num_micro_batches: int = 1, **_) -> CausalLMOutput:
+        """``num_micro_batches=G`` treats the batch as G gradient-accumulation micro-batches
+        run in ONE pass: the loss is the mean of the G per-micro-batch mean losses, exactly
+        what sequential accumulation of ``loss_i / G`` produces (same gradient)."""
         B, S = input_ids.shape
         kv_lens = None
         if attention_mask is not None and past_key_values is None:
@@ -280,7 +283,14 @@ class Qwen3ForCausalLM(nn.Module):
         loss = logits = None
         if labels is not None:
             tgt = shift_labels(labels).reshape(-1)
-            loss = fused_linear_cross_entropy(h, self.lm_head.weight, tgt)
+            G = num_micro_batches
+            if G > 1:
+                assert B % G == 0, "batch must split into equal micro-batches"
+                rows = (B // G) * S
+                loss = sum(fused_linear_cross_entropy(h[g * rows:(g + 1) * rows], self.lm_head.weight,
+                                                      tgt[g * rows:(g + 1) * rows]) for g in range(G)) / G
+            else:
+                loss = fused_linear_cross_entropy(h, self.lm_head.weight, tgt)
             if return_logits:
                 logits = (h @ self.lm_head.weight.t()).view(B, S, -1)
         else:

@@ -11,8 +11,9 @@ One op covers every projection of the stack:
   block-placed ``B`` ([N, Σr]) enter the MFMA kernel as an extra K-slice of the same tile
   loop (``gemm_nf4`` / ``gemm_bf16`` in ``csrc/kernels/gemm_*.hip``), and the residual add
   is the epilogue.  Backward ``dX = dY·deq(W)`` is the transposed-operand variant of the
-  same kernel (the NF4 tile is dequantised into LDS and read back transposed), with the
-  LoRA ``(s·dY·B)·A`` term again an extra K-slice when the branch has no dropout.
+  same kernel over a second fragment-native packing of the same NF4 codes, with the LoRA
+  ``(s·dY·B)·A`` term again an extra K-slice when the branch has no dropout (with dropout
+  the counter-RNG mask is regenerated in a fused ``dx += mask·t`` kernel — never stored).
 
 Reference parity: PEFT ``LoraConfig(r, lora_alpha, lora_dropout, target_modules)``
 (``Fine-Tuning/qwen3-8b-qlora.py:107-114``), scaling = alpha / r.
@@ -71,12 +72,35 @@ def _base_gemm_t(dy, base, ext_a=None, ext_b=None):
     return native().gemm_bf16_t(dy, base, ext_a, ext_b)
 
 
+_KEY = [0x5DEECE66D << 20]
+
+
+def next_dropout_key() -> int:
+    """Counter-based dropout stream: every call gets a fresh 63-bit key (deterministic given
+    the seed set by :func:`seed_dropout`)."""
+    _KEY[0] = (_KEY[0] + 0x9E3779B97F4A7C15) & 0x7FFFFFFFFFFFFFFF
+    return _KEY[0]
+
+
+def seed_dropout(seed: int):
+    _KEY[0] = (int(seed) * 0x2545F4914F6CDD1D) & 0x7FFFFFFFFFFFFFFF
+
+
+def bf16_view(p: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
+    """The optimizer-maintained low-precision shadow of a fp32 trainable parameter
+    (written by the fused AdamW kernel every step), else a cast."""
+    sh = getattr(p, "_lipa_shadow", None)
+    if sh is not None and sh.dtype == dtype:
+        return sh
+    return p.detach().to(dtype)
+
+
 class _FusedLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, meta, *ab):
         base, branches, training = meta
         dense = not isinstance(base, NF4Weight)
-        xa_list, xd_list, mask_list = [], [], []
+        xa_list, keys = [], []
         ext_a = ext_b = None
         if branches:
             N = base.shape[0]
@@ -86,26 +110,24 @@ class _FusedLinearFn(torch.autograd.Function):
             for br, (a, b) in zip(branches, zip(ab[0::2], ab[1::2])):
                 r = a.shape[0]
                 if training and br.dropout > 0:
-                    mask = torch.rand_like(x, dtype=torch.float32).ge_(br.dropout)
-                    xd = x * mask.to(x.dtype) * (1.0 / (1.0 - br.dropout))
+                    key = next_dropout_key()
+                    xd = native().dropout_fwd(x, br.dropout, key)
                 else:
-                    mask, xd = None, x
-                xa = xd @ a.to(x.dtype).t()                       # [T, r]
+                    key, xd = None, x
+                xa = xd @ bf16_view(a, x.dtype).t()                # [T, r]
                 cols.append(xa * br.scaling)
-                ext_b[br.c0:br.c1, r0:r0 + r] = b.to(x.dtype)
+                ext_b[br.c0:br.c1, r0:r0 + r] = bf16_view(b, x.dtype)
                 xa_list.append(xa)
-                xd_list.append(xd if mask is not None else None)
-                mask_list.append(mask)
+                keys.append(key)
                 r0 += r
             ext_a = _pad_cols(torch.cat(cols, 1))
         y = _base_gemm(x, base if not dense else weight, ext_a, ext_b, residual)
         if bias is not None:
             y = y + bias
         ctx.meta = meta
+        ctx.keys = keys
         ctx.has_residual = residual is not None
-        ctx.save_for_backward(x, weight, *ab, *[t for t in xa_list],
-                              *[t if t is not None else torch.empty(0) for t in xd_list],
-                              *[t if t is not None else torch.empty(0) for t in mask_list])
+        ctx.save_for_backward(x, weight, *ab, *xa_list)
         ctx.nb = len(branches)
         return y
 
@@ -117,8 +139,6 @@ class _FusedLinearFn(torch.autograd.Function):
         nb = ctx.nb
         ab = saved[2:2 + 2 * nb]
         xa_list = saved[2 + 2 * nb:2 + 3 * nb]
-        xd_list = saved[2 + 3 * nb:2 + 4 * nb]
-        mask_list = saved[2 + 4 * nb:2 + 5 * nb]
         dense = not isinstance(base, NF4Weight)
         dy = dy.contiguous()
         grads_ab = []
@@ -126,25 +146,25 @@ class _FusedLinearFn(torch.autograd.Function):
         for i, br in enumerate(branches):
             a, b = ab[2 * i], ab[2 * i + 1]
             dyi = dy[:, br.c0:br.c1]
-            g = (dyi @ b.to(dy.dtype)) * br.scaling            # [T, r]  = d(xa)
-            db = (dyi.t() @ xa_list[i]) * br.scaling           # [n, r]
-            xin = xd_list[i] if xd_list[i].numel() else x
-            da = g.t() @ xin                                   # [r, K]
+            g = (dyi @ bf16_view(b, dy.dtype)) * br.scaling      # [T, r]  = d(xa)
+            db = (dyi.t() @ xa_list[i]) * br.scaling             # [n, r]
+            key = ctx.keys[i]
+            xin = native().dropout_fwd(x, br.dropout, key) if key is not None else x   # regenerate drop(x)
+            da = g.t() @ xin                                     # [r, K]
             grads_ab += [da.to(a.dtype), db.to(b.dtype)]
             g_list.append(g)
         dx = None
         if ctx.needs_input_grad[0]:
-            fold = [i for i, br in enumerate(branches) if not mask_list[i].numel()]
+            fold = [i for i in range(nb) if ctx.keys[i] is None]
             ext_a = ext_b = None
             if fold:
                 ext_a = _pad_cols(torch.cat([g_list[i] for i in fold], 1))
-                ext_b = torch.cat([ab[2 * i].to(dy.dtype) for i in fold], 0)            # [R, K]
+                ext_b = torch.cat([bf16_view(ab[2 * i], dy.dtype) for i in fold], 0)            # [R, K]
                 ext_b = F.pad(ext_b, (0, 0, 0, ext_a.shape[1] - ext_b.shape[0])).t().contiguous()  # [K, Rp]
             dx = _base_gemm_t(dy, base if not dense else weight, ext_a, ext_b)
             for i, br in enumerate(branches):
-                if mask_list[i].numel():
-                    scale = 1.0 / (1.0 - br.dropout)
-                    dx.addcmul_(g_list[i] @ ab[2 * i].to(dy.dtype), mask_list[i].to(dy.dtype), value=scale)
+                if ctx.keys[i] is not None:   # LoRA input grad through the regenerated dropout mask
+                    native().dropout_bwd_add(dx, g_list[i] @ bf16_view(ab[2 * i], dy.dtype), br.dropout, ctx.keys[i])
         dres = dy if ctx.has_residual else None
         dw = None
         if dense and weight is not None and ctx.needs_input_grad[2]:

@@ -53,6 +53,13 @@ class FlatParams:
                 p.data = self.low[o:o + k].view_as(p)
             p.grad = self.grad[o:o + k].view_as(p) if p.dtype == torch.float32 else None
         self.mixed = self.low is not None
+        # bf16 shadows of fp32 params (LoRA adapters): refreshed by the update kernel itself,
+        # consumed by the fused GEMMs — no per-forward fp32→bf16 conversion kernels
+        self.shadow = None
+        if not self.mixed and dev.type == "cuda":
+            self.shadow = self.data.to(torch.bfloat16)
+            for p, o in zip(self.params, self.offsets):
+                p._lipa_shadow = self.shadow[o:o + p.numel()].view_as(p)
 
     def sync_grads(self):
         """Copy grads that autograd allocated separately (low-precision params) into the flat
@@ -122,12 +129,14 @@ class _FlatOptimizer:
             st[k].copy_(v)
         if self.flat.mixed:
             self.flat.low.copy_(self.flat.data)
+        elif self.flat.shadow is not None:
+            self.flat.shadow.copy_(self.flat.data)
 
     def _lr(self):
         return self.param_groups[0]["lr"]
 
     def _sync_low(self):
-        return self.flat.low if self.flat.mixed else None
+        return self.flat.low if self.flat.mixed else self.flat.shadow
 
 
 class AdamW(_FlatOptimizer):
@@ -216,6 +225,8 @@ class AdamW8bit(_FlatOptimizer):
         self.qv.copy_(_nearest((v / self.av[:, None].clamp_min(1e-30)).view(-1)[:n], self.code_u))
         if self.flat.mixed:
             self.flat.low.copy_(self.flat.data)
+        elif self.flat.shadow is not None:
+            self.flat.shadow.copy_(self.flat.data)
 
 
 def build_optimizer(name: str, params, lr: float, weight_decay: float = 0.0, betas=(0.9, 0.999), eps=1e-8,

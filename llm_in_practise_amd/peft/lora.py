@@ -310,6 +310,9 @@ class PeftModel(nn.Module):
             if name in params:
                 with torch.no_grad():
                     params[name].copy_(v.to(params[name].dtype))
+                    sh = getattr(params[name], "_lipa_shadow", None)
+                    if sh is not None:           # optimizer-maintained bf16 shadow
+                        sh.copy_(params[name])
             else:
                 missing.append(k)
         if strict and missing:
