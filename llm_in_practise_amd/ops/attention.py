@@ -55,8 +55,9 @@ def sdpa_bshd(q, k, v, causal=True, scale=None, dropout_p=0.0, window=None, key_
     notebook attention variants).  Routes to the fused kernel when shapes allow it."""
     B, S, Hq, D = q.shape
     Hkv = k.shape[2]
-    if (use_native(q) and dropout_p == 0.0 and window is None and key_padding_mask is None
-            and k.shape[1] == S and D in (32, 64, 128) and Hq % Hkv == 0):
+    if (use_native(q) and q.dtype == torch.bfloat16 and dropout_p == 0.0 and window is None
+            and key_padding_mask is None and k.shape[1] == S and D in (64, 128) and Hq % Hkv == 0
+            and (S % 64 == 0 or not torch.is_grad_enabled())):
         o = flash_attention(q.reshape(B * S, Hq * D), k.reshape(B * S, Hkv * D).contiguous(),
                             v.reshape(B * S, Hkv * D).contiguous(), B, S, Hq, Hkv, D, causal, scale)
         return o.view(B, S, Hq, D)

@@ -1,0 +1,560 @@
+"""ZeRO-1/2/3 (+ CPU offload) engine with DeepSpeed-config semantics.
+
+One process per GPU; collectives are ``torch.distributed`` (``"nccl"`` = RCCL over xGMI on
+MI355X, ``gloo`` on CPU):
+
+* stage 0: gradients all-reduced (DDP-equivalent); replicated optimizer.
+* stage 1: gradients all-reduced; optimizer state + fp32 master partitioned — each rank updates
+  its contiguous 1/W shard of the flat parameter buffer, then ``all_gather_into_tensor``.
+* stage 2: gradients ``reduce_scatter_tensor``-ed straight into the owner's shard (bucketed
+  by ``reduce_bucket_size``); grad-norm from shard partial sums + one scalar all-reduce.
+* stage 3: parameters partitioned per *unit* (each block of a ModuleList, plus the root).
+  A unit's full flat weight is all-gathered in a forward pre-hook and its storage freed
+  (``resize_(0)``) after the forward unless it is under ``stage3_param_persistence_threshold``;
+  a hook on the unit's output gradient re-gathers it before its backward; once the unit's
+  gradients are accumulated they are reduce-scattered into the fp32 shard gradient and the
+  full buffers are freed again.  Frozen parameters (NF4 bases) stay replicated — only
+  trainable parameters and their optimizer state are partitioned (QLoRA + ZeRO-3, SURVEY
+  §7.5 option 2).
+* ``offload_optimizer: cpu``: fp32 master shard and Adam moments live in (pinned) host memory;
+  the update is the native OpenMP/AVX host AdamW (``csrc/cpu/cpu_adam.cpp``); gradients
+  stream D2H and the updated compute-dtype shard H2D.
+* fp16 ``loss_scale: 0`` → dynamic loss scaling (initial 2^power, window, hysteresis, min);
+  bf16 → no scaling.  ``gradient_clipping`` → global-norm clip.
+
+Surface mirrors the DeepSpeed engine the reference drives
+(``DeepSpeed-GPTLike-ZeRO-1.py:287-330``): ``engine(x)``, ``engine.backward(loss)``,
+``engine.step()`` (steps the optimizer at gradient-accumulation boundaries),
+``save_checkpoint(dir, tag)`` / ``load_checkpoint(dir, tag)`` (``<dir>/<tag>/`` with
+``mp_rank_00_model_states.pt`` + ``zero_pp_rank_{r}_mp_rank_00_optim_states.pt`` and a
+``latest`` file), and :func:`initialize` ≈ ``deepspeed.initialize``.
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+import os
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..ops import reference as ref
+from ..ops._native import native, use_native
+from ..optim.adamw import LRScheduler
+from .dist import is_dist
+from .ds_config import DSConfig, load_ds_config
+
+
+def _world():
+    return dist.get_world_size() if is_dist() else 1
+
+
+def _rank():
+    return dist.get_rank() if is_dist() else 0
+
+
+def _pad_to(n, m):
+    return (n + m - 1) // m * m
+
+
+class LossScaler:
+    """DeepSpeed-style dynamic fp16 loss scaling (skip / halve with hysteresis / grow per window)."""
+
+    def __init__(self, cfg: DSConfig):
+        self.dynamic = cfg.fp16 and cfg.fp16_loss_scale == 0
+        self.scale = float(2 ** cfg.fp16_initial_scale_power) if self.dynamic else (cfg.fp16_loss_scale or 1.0)
+        self.window, self.hysteresis, self.min_scale = cfg.fp16_loss_scale_window, cfg.fp16_hysteresis, \
+            cfg.fp16_min_loss_scale
+        self.good_steps, self.cur_hyst = 0, cfg.fp16_hysteresis
+        self.enabled = cfg.fp16
+
+    def update(self, overflow: bool):
+        if not self.dynamic:
+            return
+        if overflow:
+            self.cur_hyst -= 1
+            if self.cur_hyst <= 0:
+                self.scale = max(self.min_scale, self.scale / 2)
+                self.cur_hyst = self.hysteresis
+            self.good_steps = 0
+        else:
+            self.good_steps += 1
+            if self.good_steps % self.window == 0:
+                self.scale *= 2
+                self.cur_hyst = self.hysteresis
+
+
+class _Unit:
+    """A stage-3 partition unit: trainable params of one module, flattened and sharded."""
+
+    def __init__(self, name, module, params, world, rank, dtype, device):
+        self.name, self.module, self.params = name, module, params
+        self.shapes = [p.shape for p in params]
+        self.numels = [p.numel() for p in params]
+        n = sum(self.numels)
+        self.n = n
+        self.npad = _pad_to(max(n, 1), world)
+        self.shard_n = self.npad // world
+        self.world, self.rank = world, rank
+        self.dtype, self.device = dtype, device
+        full = torch.zeros(self.npad, dtype=dtype, device=device)
+        o = 0
+        for p, k in zip(params, self.numels):
+            full[o:o + k].copy_(p.detach().reshape(-1))
+            o += k
+        self.shard = full[rank * self.shard_n:(rank + 1) * self.shard_n].clone()
+        self.full = full
+        self.gathered = True
+        self._point_params()
+        self.grads_ready = 0
+
+    def _point_params(self):
+        o = 0
+        for p, k, s in zip(self.params, self.numels, self.shapes):
+            p.data = self.full[o:o + k].view(s)
+            o += k
+
+    def gather(self):
+        if self.gathered:
+            return
+        st = self.full.untyped_storage()
+        st.resize_(self.npad * self.full.element_size())
+        if self.world > 1:
+            dist.all_gather_into_tensor(self.full, self.shard)
+        else:
+            self.full.copy_(self.shard)
+        self.gathered = True
+
+    def release(self):
+        if not self.gathered:
+            return
+        self.full.untyped_storage().resize_(0)
+        self.gathered = False
+
+
+class ZeroEngine:
+    def __init__(self, model: nn.Module, config, lr: float | None = None, weight_decay: float | None = None,
+                 betas=(0.9, 0.999), eps: float = 1e-8, hidden_size: int | None = None,
+                 micro_batch: int | None = None, grad_accum: int | None = None, units: list[nn.Module] | None = None,
+                 total_steps: int = 10 ** 9):
+        self.world, self.rank = _world(), _rank()
+        self.cfg: DSConfig = load_ds_config(config, self.world, micro_batch, grad_accum, hidden_size)
+        self.module = model
+        self.stage = self.cfg.zero.stage
+        opt = (self.cfg.optimizer or {}).get("params", {}) if self.cfg.optimizer else {}
+        self.lr = float(opt.get("lr", lr if lr is not None else 1e-3)) if opt.get("lr") != "auto" else float(lr)
+        self.wd = float(opt.get("weight_decay", weight_decay if weight_decay is not None else 0.0))
+        self.betas = tuple(opt.get("betas", betas))
+        self.eps = float(opt.get("eps", eps))
+        self.device = next(model.parameters()).device
+        self.compute_dtype = torch.bfloat16 if self.cfg.bf16 else torch.float16 if self.cfg.fp16 else None
+        if self.compute_dtype is not None:
+            for p in model.parameters():
+                if p.requires_grad and p.is_floating_point():
+                    p.data = p.data.to(self.compute_dtype)
+        self.offload = self.cfg.zero.offload_optimizer == "cpu"
+        self.scaler = LossScaler(self.cfg)
+        self.micro_steps = 0
+        self.global_steps = 0
+        self.ga = self.cfg.gradient_accumulation_steps
+        self.clip = self.cfg.gradient_clipping
+        self.last_grad_norm = torch.zeros((), device=self.device)
+        self._skipped = 0
+        self._sync = True
+        params = [p for p in model.parameters() if p.requires_grad]
+        # de-duplicate tied params
+        seen, uniq = set(), []
+        for p in params:
+            if id(p) not in seen:
+                seen.add(id(p))
+                uniq.append(p)
+        self.params = uniq
+        if self.stage == 3:
+            self._init_stage3(units)
+        else:
+            self._init_flat()
+        self._init_optimizer_state()
+        self.lr_scheduler = self._build_scheduler(total_steps)
+        if is_dist():
+            with torch.no_grad():
+                for b in model.buffers():
+                    dist.broadcast(b, src=0)
+
+    # ------------------------------------------------------------------ layout
+    def _init_flat(self):
+        W, r = self.world, self.rank
+        dtype = self.params[0].dtype
+        n = sum(p.numel() for p in self.params)
+        self.n = n
+        self.npad = _pad_to(n, W)
+        self.shard_n = self.npad // W
+        self.flat_model = torch.zeros(self.npad, dtype=dtype, device=self.device)
+        self.flat_grad = torch.zeros(self.npad, dtype=torch.float32, device=self.device)
+        o = 0
+        for p in self.params:
+            k = p.numel()
+            self.flat_model[o:o + k].copy_(p.detach().reshape(-1))
+            p.data = self.flat_model[o:o + k].view_as(p)
+            if dtype == torch.float32:
+                p.grad = self.flat_grad[o:o + k].view_as(p)
+            o += k
+        if is_dist():
+            dist.broadcast(self.flat_model, src=0)
+        if self.stage == 0:               # replicated optimizer (DDP semantics)
+            self.shard_n = self.npad
+            r = 0
+        self.shard_slice = slice(r * self.shard_n, (r + 1) * self.shard_n)
+        self.master = self.flat_model[self.shard_slice].float().clone()
+        if self.stage == 2:
+            self.grad_shard = torch.zeros(self.shard_n, dtype=torch.float32, device=self.device)
+
+    def _init_stage3(self, units):
+        W, r = self.world, self.rank
+        if units is None:
+            units = []
+            for m in self.module.modules():
+                if isinstance(m, nn.ModuleList):
+                    units.extend(list(m))
+        unit_of = {}
+        for u in units:
+            for p in u.parameters():
+                if p.requires_grad:
+                    unit_of.setdefault(id(p), u)
+        groups: dict[int, list] = {}
+        order: list = []
+        for p in self.params:
+            u = unit_of.get(id(p), self.module)
+            if id(u) not in groups:
+                groups[id(u)] = []
+                order.append(u)
+            groups[id(u)].append(p)
+        if is_dist():
+            with torch.no_grad():
+                for p in self.params:
+                    dist.broadcast(p.data, src=0)
+        self.units = [_Unit(f"u{i}", u, groups[id(u)], W, r, self.params[0].dtype, self.device)
+                      for i, u in enumerate(order)]
+        self.master = torch.cat([u.shard.float() for u in self.units])
+        self.grad_shard = torch.zeros_like(self.master)
+        self.unit_offsets, o = [], 0
+        for u in self.units:
+            self.unit_offsets.append(o)
+            o += u.shard_n
+        thr = self.cfg.zero.stage3_param_persistence_threshold
+        self.persistent = {id(u): (u.n < thr or u.module is self.module) for u in self.units}
+        for u in self.units:
+            if u.module is not self.module:
+                u.module.register_forward_pre_hook(self._pre_fwd(u))
+                u.module.register_forward_hook(self._post_fwd(u))
+            for p in u.params:
+                p.register_post_accumulate_grad_hook(self._grad_hook(u))
+        for u in self.units:
+            if not self.persistent[id(u)]:
+                u.release()
+
+    def _pre_fwd(self, u):
+        def hook(mod, args):
+            u.gather()
+        return hook
+
+    def _post_fwd(self, u):
+        def hook(mod, args, out):
+            if self.persistent[id(u)] or not torch.is_grad_enabled():
+                if not self.persistent[id(u)]:
+                    u.release()
+                return out
+            t = out[0] if isinstance(out, (tuple, list)) else out
+            if isinstance(t, torch.Tensor) and t.requires_grad:
+                t.register_hook(lambda g: (u.gather(), g)[1])
+            u.release()
+            return out
+        return hook
+
+    def _grad_hook(self, u):
+        def hook(p):
+            u.grads_ready += 1
+            if u.grads_ready == len(u.params):
+                u.grads_ready = 0
+                self._reduce_unit(u)
+        return hook
+
+    def _reduce_unit(self, u):
+        g = torch.zeros(u.npad, dtype=torch.float32, device=self.device)
+        o = 0
+        for p, k in zip(u.params, u.numels):
+            if p.grad is not None:
+                g[o:o + k].copy_(p.grad.reshape(-1))
+                p.grad = None
+            o += k
+        i = self.units.index(u)
+        dst = self.grad_shard[self.unit_offsets[i]:self.unit_offsets[i] + u.shard_n]
+        if self.world > 1:
+            part = torch.empty(u.shard_n, dtype=torch.float32, device=self.device)
+            dist.reduce_scatter_tensor(part, g, op=dist.ReduceOp.SUM)
+            dst.add_(part, alpha=1.0 / self.world)
+        else:
+            dst.add_(g[:u.shard_n])
+        if not self.persistent[id(u)]:
+            u.release()
+
+    # ------------------------------------------------------------------ optimizer state
+    def _init_optimizer_state(self):
+        dev = torch.device("cpu") if self.offload else self.device
+        if self.offload:
+            self.master = self.master.cpu().pin_memory() if (self.cfg.zero.pin_memory and torch.cuda.is_available()) \
+                else self.master.cpu()
+        self.exp_avg = torch.zeros(self.master.numel(), dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros_like(self.exp_avg)
+        self.opt_step = 0
+
+    def _build_scheduler(self, total_steps):
+        s = self.cfg.scheduler
+        if not s:
+            return None
+        p = s.get("params", {})
+        if s.get("type") == "WarmupLR":
+            return LRScheduler(self, "warmup_lr", float(p.get("warmup_max_lr", self.lr)), total_steps,
+                               int(p.get("warmup_num_steps", 1000)), float(p.get("warmup_min_lr", 0.0)))
+        if s.get("type") in ("WarmupDecayLR", "WarmupCosineLR"):
+            return LRScheduler(self, "linear" if s["type"] == "WarmupDecayLR" else "cosine",
+                               float(p.get("warmup_max_lr", self.lr)), int(p.get("total_num_steps", total_steps)),
+                               int(p.get("warmup_num_steps", 0)))
+        return None
+
+    @property
+    def param_groups(self):
+        if not hasattr(self, "_pg"):
+            self._pg = [{"lr": self.lr, "weight_decay": self.wd}]
+        return self._pg
+
+    # ------------------------------------------------------------------ train-loop surface
+    def __call__(self, *a, **kw):
+        return self.forward(*a, **kw)
+
+    def forward(self, *a, **kw):
+        if self.stage == 3:
+            for u in self.units:
+                if self.persistent[id(u)]:
+                    u.gather()
+        return self.module(*a, **kw)
+
+    def train(self, mode=True):
+        self.module.train(mode)
+        return self
+
+    def eval(self):
+        self.module.eval()
+        return self
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        prev = self._sync
+        self._sync = False
+        try:
+            yield
+        finally:
+            self._sync = prev
+
+    def is_gradient_accumulation_boundary(self) -> bool:
+        return (self.micro_steps + 1) % self.ga == 0
+
+    def backward(self, loss: torch.Tensor):
+        scale = self.scaler.scale if self.scaler.enabled else 1.0
+        (loss * (scale / self.ga)).backward()
+        if self.stage < 3 and self.params[0].dtype != torch.float32:
+            o = 0
+            for p in self.params:
+                k = p.numel()
+                if p.grad is not None:
+                    self.flat_grad[o:o + k].add_(p.grad.reshape(-1).float())
+                    p.grad = None
+                o += k
+
+    def step(self):
+        boundary = self.is_gradient_accumulation_boundary()
+        self.micro_steps += 1
+        if not boundary:
+            return
+        self._optimizer_step()
+        self.global_steps += 1
+        if self.lr_scheduler is not None:
+            self.lr_scheduler.step()
+
+    def zero_grad(self):
+        if self.stage == 3:
+            self.grad_shard.zero_()
+        else:
+            self.flat_grad.zero_()
+            if self.stage == 2:
+                self.grad_shard.zero_()
+
+    # ------------------------------------------------------------------ the update
+    def _reduce_grads(self) -> torch.Tensor:
+        """Return this rank's fp32 gradient shard (averaged over ranks)."""
+        if self.stage == 3:
+            for u in self.units:          # units whose params did not all receive grads
+                if u.grads_ready:
+                    u.grads_ready = 0
+                    self._reduce_unit(u)
+            return self.grad_shard
+        if self.stage == 2:
+            if self.world > 1:
+                dist.reduce_scatter_tensor(self.grad_shard, self.flat_grad, op=dist.ReduceOp.SUM)
+                self.grad_shard.div_(self.world)
+            else:
+                self.grad_shard.copy_(self.flat_grad[self.shard_slice])
+            return self.grad_shard
+        if self.world > 1:
+            dist.all_reduce(self.flat_grad)
+            self.flat_grad.div_(self.world)
+        return self.flat_grad[self.shard_slice]
+
+    def _global_sumsq(self, g: torch.Tensor) -> torch.Tensor:
+        s = g.double().pow(2).sum().float().reshape(1) if g.device.type == "cpu" else g.float().pow(2).sum().reshape(1)
+        if self.world > 1 and self.stage > 0:      # stage 0 holds the full replicated gradient
+            s = s.to(self.device)
+            dist.all_reduce(s)
+        return s
+
+    def _optimizer_step(self):
+        g = self._reduce_grads()
+        inv = 1.0 / self.scaler.scale if self.scaler.enabled else 1.0
+        overflow = False
+        if self.scaler.enabled:
+            bad = torch.tensor([0.0 if torch.isfinite(g).all() else 1.0], device=self.device)
+            if self.world > 1:
+                dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+            overflow = bad.item() > 0
+            self.scaler.update(overflow)
+            if overflow:
+                self._skipped += 1
+                self.zero_grad()
+                return
+        sumsq = self._global_sumsq(g) * inv * inv
+        norm = sumsq.sqrt()
+        self.last_grad_norm = norm.reshape(())
+        coef = inv
+        if self.clip > 0:
+            coef = inv * min(1.0, self.clip / (norm.item() + 1e-6))
+        lr = self.param_groups[0]["lr"]
+        self.opt_step += 1
+        b1, b2 = self.betas
+        if self.offload:
+            from ..ops._native import cpu_native
+            gc = g.float().cpu()
+            cpu_native().adamw_step(self.master, gc, self.exp_avg, self.exp_avg_sq, lr, b1, b2, self.eps, self.wd,
+                                    self.opt_step, coef)
+        elif use_native(self.master):
+            gg = g.float().contiguous() if g.dtype != torch.float32 or not g.is_contiguous() else g
+            if coef != 1.0:
+                gg = gg * coef
+            native().adamw(self.master, gg, self.exp_avg, self.exp_avg_sq, None, lr, b1, b2, self.eps, self.wd,
+                           self.opt_step, None, None)
+        else:
+            ref.adamw_step(self.master, g.float() * coef, self.exp_avg, self.exp_avg_sq, self.opt_step, lr, b1, b2,
+                           self.eps, self.wd)
+        self._publish_params()
+        self.zero_grad()
+
+    def _publish_params(self):
+        m = self.master.to(self.device, non_blocking=True)
+        if self.stage == 3:
+            for u, o in zip(self.units, self.unit_offsets):
+                u.shard.copy_(m[o:o + u.shard_n])
+                if u.gathered:            # persistent units keep a live full copy: refresh it
+                    u.gathered = False
+                    u.gather()
+            return
+        self.flat_model[self.shard_slice].copy_(m)
+        if self.world > 1 and self.stage > 0:
+            dist.all_gather_into_tensor(self.flat_model, self.flat_model[self.shard_slice].clone())
+
+    # ------------------------------------------------------------------ state / checkpoints
+    def consolidated_state_dict(self) -> dict:
+        """Full (16-bit where trained in 16-bit) model state dict; gathers stage-3 shards."""
+        if self.stage == 3:
+            for u in self.units:
+                u.gather()
+        sd = {k: v.detach().clone() for k, v in self.module.state_dict().items()}
+        if self.stage == 3:
+            for u in self.units:
+                if not self.persistent[id(u)]:
+                    u.release()
+        return sd
+
+    def save_checkpoint(self, save_dir: str, tag: str | None = None, client_state: dict | None = None):
+        tag = tag or f"global_step{self.global_steps}"
+        d = os.path.join(save_dir, tag)
+        os.makedirs(d, exist_ok=True)
+        module = None
+        if self.stage < 3 or self.cfg.zero.stage3_gather_16bit_weights_on_model_save:
+            module = self.consolidated_state_dict()     # collective under stage 3
+        if self.rank == 0:
+            torch.save({"module": module, "global_steps": self.global_steps, "micro_steps": self.micro_steps,
+                        "loss_scale": self.scaler.scale, "client_state": client_state or {},
+                        "ds_config": self.cfg.raw, "zero_stage": self.stage, "world_size": self.world},
+                       os.path.join(d, "mp_rank_00_model_states.pt"))
+        torch.save({"master": self.master.cpu(), "exp_avg": self.exp_avg.cpu(), "exp_avg_sq": self.exp_avg_sq.cpu(),
+                    "opt_step": self.opt_step, "zero_stage": self.stage, "rank": self.rank, "world": self.world,
+                    "lr_scheduler": self.lr_scheduler.state_dict() if self.lr_scheduler else None},
+                   os.path.join(d, f"zero_pp_rank_{self.rank}_mp_rank_00_optim_states.pt"))
+        if is_dist():
+            dist.barrier()
+        if self.rank == 0:
+            with open(os.path.join(save_dir, "latest"), "w") as f:
+                f.write(tag)
+        return d
+
+    def load_checkpoint(self, load_dir: str, tag: str | None = None):
+        if tag is None:
+            with open(os.path.join(load_dir, "latest")) as f:
+                tag = f.read().strip()
+        d = os.path.join(load_dir, tag)
+        ms = torch.load(os.path.join(d, "mp_rank_00_model_states.pt"), map_location="cpu", weights_only=True)
+        os_ = torch.load(os.path.join(d, f"zero_pp_rank_{self.rank}_mp_rank_00_optim_states.pt"),
+                         map_location="cpu", weights_only=True)
+        assert os_["world"] == self.world, "re-partitioning across world sizes is not supported"
+        self.master.copy_(os_["master"])
+        self.exp_avg.copy_(os_["exp_avg"])
+        self.exp_avg_sq.copy_(os_["exp_avg_sq"])
+        self.opt_step = os_["opt_step"]
+        if self.lr_scheduler is not None and os_.get("lr_scheduler"):
+            self.lr_scheduler.load_state_dict(os_["lr_scheduler"])
+        self.global_steps, self.micro_steps = ms["global_steps"], ms["micro_steps"]
+        self.scaler.scale = ms["loss_scale"]
+        self._publish_params()
+        return d, ms.get("client_state", {})
+
+    # DeepSpeed accessors used by the reference scripts
+    def train_micro_batch_size_per_gpu(self):
+        return self.cfg.train_micro_batch_size_per_gpu
+
+    def gradient_accumulation_steps(self):
+        return self.ga
+
+    def get_lr(self):
+        return [self.param_groups[0]["lr"]]
+
+    def get_global_grad_norm(self):
+        return float(self.last_grad_norm)
+
+    @property
+    def skipped_steps(self):
+        return self._skipped
+
+
+def initialize(model: nn.Module, config, model_parameters=None, optimizer=None, lr_scheduler=None, **kw):
+    """``deepspeed.initialize`` analogue → (engine, optimizer, dataloader=None, lr_scheduler).
+
+    A client ``optimizer`` is accepted for API compatibility; when the config also declares an
+    ``optimizer`` block the config wins (documented precedence), otherwise the client's
+    ``lr`` / ``weight_decay`` / ``betas`` / ``eps`` are adopted."""
+    lr = wd = None
+    betas, eps = (0.9, 0.999), 1e-8
+    if optimizer is not None and hasattr(optimizer, "param_groups"):
+        g = optimizer.param_groups[0]
+        lr, wd = g.get("lr"), g.get("weight_decay")
+        betas, eps = g.get("betas", betas), g.get("eps", eps)
+    engine = ZeroEngine(model, config, lr=lr, weight_decay=wd, betas=betas, eps=eps, **kw)
+    return engine, engine, None, engine.lr_scheduler

@@ -1,0 +1,195 @@
+"""ZeRO-0/1/2/3 (+offload, fp16 scaler) equivalence on CPU with gloo, world_size 2.
+
+Oracle: the same model trained in ONE process on the concatenation of both ranks' batches
+(mean loss) — data parallelism with averaged gradients must reproduce it for every stage.
+"""
+import json
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+import torch.nn as nn
+
+from llm_in_practise_amd.parallel.zero import LossScaler, ZeroEngine, initialize
+from llm_in_practise_amd.parallel.ds_config import load_ds_config
+
+
+class Net(nn.Module):
+    def __init__(self, d=16, n=3):
+        super().__init__()
+        self.inp = nn.Linear(8, d)
+        self.blocks = nn.ModuleList([nn.Sequential(nn.Linear(d, d), nn.Tanh()) for _ in range(n)])
+        self.out = nn.Linear(d, 1)
+
+    def forward(self, x):
+        h = self.inp(x)
+        for b in self.blocks:
+            h = h + b(h)
+        return self.out(h)
+
+
+def _data(step, rank, n=4):
+    g = torch.Generator().manual_seed(1000 * step + rank)
+    return torch.randn(n, 8, generator=g), torch.randn(n, 1, generator=g)
+
+
+def _cfg(stage, offload=False, clip=0.05, ga=1):
+    z = {"stage": stage}
+    if offload:
+        z["offload_optimizer"] = {"device": "cpu"}
+    return {"train_micro_batch_size_per_gpu": 4, "gradient_accumulation_steps": ga, "gradient_clipping": clip,
+            "optimizer": {"type": "AdamW", "params": {"lr": 1e-2, "weight_decay": 0.01}},
+            "zero_optimization": z}
+
+
+def _train(engine, world, rank, steps=3, ga=1):
+    for s in range(steps):
+        for mstep in range(ga):
+            x, y = _data(s * ga + mstep, rank)
+            loss = ((engine(x) - y) ** 2).mean()
+            engine.backward(loss)
+            engine.step()
+
+
+def _worker(rank, world, port, stage, offload, ga, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    net = Net()
+    eng = ZeroEngine(net, _cfg(stage, offload, ga=ga))
+    _train(eng, world, rank, ga=ga)
+    sd = eng.consolidated_state_dict()
+    if rank == 0:
+        torch.save(sd, out)
+    torch.distributed.destroy_process_group()
+
+
+def _oracle(steps=3, ga=1):
+    torch.manual_seed(0)
+    net = Net()
+    eng = ZeroEngine(net, _cfg(0, ga=ga))
+    for s in range(steps):
+        for mstep in range(ga):
+            xs, ys = zip(*[_data(s * ga + mstep, r) for r in range(2)])
+            loss = ((eng(torch.cat(xs)) - torch.cat(ys)) ** 2).mean()
+            eng.backward(loss)
+            eng.step()
+    return net.state_dict()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("stage,offload,ga", [(0, False, 1), (1, False, 1), (2, False, 2), (3, False, 1),
+                                               (3, False, 2), (2, True, 1)])
+def test_zero_stage_matches_single_process(tmp_path, stage, offload, ga):
+    if offload:
+        from llm_in_practise_amd.ops._native import cpu_native
+        cpu_native()
+    out = str(tmp_path / "sd.pt")
+    mp.spawn(_worker, args=(2, _free_port(), stage, offload, ga, out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    want = _oracle(ga=ga)
+    for k in want:
+        assert torch.allclose(got[k], want[k], atol=2e-5), (stage, k, (got[k] - want[k]).abs().max())
+
+
+def _ckpt_worker(rank, world, port, d, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    eng = ZeroEngine(Net(), _cfg(2))
+    _train(eng, world, rank, steps=2)
+    eng.save_checkpoint(d, client_state={"epoch": 1})
+    torch.manual_seed(123)                       # different init: load must restore everything
+    eng2 = ZeroEngine(Net(), _cfg(2))
+    _, client = eng2.load_checkpoint(d)
+    for e in (eng, eng2):
+        x, y = _data(99, rank)
+        e.backward(((e(x) - y) ** 2).mean())
+        e.step()
+    a, b = eng.consolidated_state_dict(), eng2.consolidated_state_dict()
+    if rank == 0:
+        torch.save({"ok": all(torch.equal(a[k], b[k]) for k in a), "client": client["epoch"],
+                    "files": sorted(os.listdir(os.path.join(d, "global_step2")))}, out)
+    torch.distributed.destroy_process_group()
+
+
+def test_zero_checkpoint_roundtrip(tmp_path):
+    out = str(tmp_path / "r.pt")
+    mp.spawn(_ckpt_worker, args=(2, _free_port(), str(tmp_path / "ck"), out), nprocs=2, join=True)
+    r = torch.load(out, weights_only=True)
+    assert r["ok"] and r["client"] == 1
+    assert r["files"] == ["mp_rank_00_model_states.pt", "zero_pp_rank_0_mp_rank_00_optim_states.pt",
+                          "zero_pp_rank_1_mp_rank_00_optim_states.pt"]
+    assert open(tmp_path / "ck" / "latest").read() == "global_step2"
+
+
+def test_stage3_single_process_frees_and_regathers():
+    torch.manual_seed(0)
+    net = Net(d=64)
+    eng = ZeroEngine(net, {"zero_optimization": {"stage": 3, "stage3_param_persistence_threshold": 10},
+                           "optimizer": {"type": "AdamW", "params": {"lr": 1e-3}}})
+    blocks = [u for u in eng.units if u.module is not net]
+    assert blocks and all(not u.gathered for u in blocks)
+    x, y = _data(0, 0)
+    eng.backward(((eng(x) - y) ** 2).mean())
+    assert all(not u.gathered for u in blocks)
+    eng.step()
+    assert float(eng.grad_shard.abs().sum()) == 0.0
+
+
+def test_loss_scaler_dynamics():
+    cfg = load_ds_config({"fp16": {"enabled": True, "loss_scale": 0, "initial_scale_power": 4,
+                                   "loss_scale_window": 2, "hysteresis": 1, "min_loss_scale": 1}})
+    s = LossScaler(cfg)
+    assert s.scale == 16
+    s.update(True)
+    assert s.scale == 8
+    s.update(False)
+    s.update(False)
+    assert s.scale == 16
+
+
+def test_fp16_overflow_skips_step():
+    torch.manual_seed(0)
+    net = Net()
+    eng = ZeroEngine(net, {"fp16": {"enabled": True, "initial_scale_power": 4, "hysteresis": 1},
+                           "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}}, "zero_optimization": {"stage": 1}})
+    before = {k: v.clone() for k, v in net.state_dict().items()}
+    x, y = _data(0, 0)
+    loss = ((eng(x.half()) - y.half()) ** 2).mean() * float("inf")
+    eng.backward(loss)
+    eng.step()
+    assert eng.skipped_steps == 1 and eng.scaler.scale == 8
+    assert all(torch.equal(before[k], v) for k, v in net.state_dict().items())
+
+
+def test_ds_config_auto_resolution_and_validation():
+    c = load_ds_config({"train_batch_size": "auto", "train_micro_batch_size_per_gpu": "auto",
+                        "gradient_accumulation_steps": "auto",
+                        "zero_optimization": {"stage": 3, "reduce_bucket_size": "auto",
+                                              "stage3_prefetch_bucket_size": "auto",
+                                              "stage3_param_persistence_threshold": "auto"}},
+                       world_size=4, micro_batch=2, grad_accum=8, hidden_size=4096)
+    assert c.train_batch_size == 64 and c.zero.reduce_bucket_size == 4096 ** 2
+    assert c.zero.stage3_param_persistence_threshold == 40960
+    with pytest.raises(ValueError):
+        load_ds_config({"train_batch_size": 10, "train_micro_batch_size_per_gpu": 2,
+                        "gradient_accumulation_steps": 1}, world_size=4)
+
+
+def test_initialize_api():
+    net = Net()
+    opt = torch.optim.AdamW(net.parameters(), lr=3e-4, weight_decay=0.1)
+    eng, o, _, sched = initialize(net, {"train_micro_batch_size_per_gpu": 4,
+                                        "scheduler": {"type": "WarmupLR", "params": {"warmup_min_lr": 0,
+                                                                                     "warmup_max_lr": 3e-4,
+                                                                                     "warmup_num_steps": 10}}},
+                                  optimizer=opt)
+    assert eng.lr == 3e-4 and eng.wd == 0.1 and sched is not None and eng.get_lr()[0] == 0.0
