@@ -32,6 +32,7 @@ void launch_adamw8bit(int, float*, const void*, uint8_t*, uint8_t*, float*, floa
                       size_t, float, float, float, float, float, float, float, const float*, const float*,
                       hipStream_t);
 void launch_unscale(int, void*, size_t, const float*, float*, hipStream_t);
+void set_gemm_impl(int impl);
 void launch_gemm_w4(int, const void*, int, const uint32_t*, const float*, const void*, const void*, int, const void*,
                     void*, int, int, int, hipStream_t);
 void launch_gemm_bf16w(const void*, int, const void*, const void*, const void*, int, const void*, void*, int, int, int,
@@ -442,6 +443,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dropout_fwd", &dropout_fwd);
   m.def("dropout_bwd_add", &dropout_bwd_add);
   m.def("grad_norm", &grad_norm);
+  m.def("set_gemm_impl", &set_gemm_impl);
   m.def("adamw", &adamw);
   m.def("adamw8bit", &adamw8bit);
   m.def("unscale", &unscale);

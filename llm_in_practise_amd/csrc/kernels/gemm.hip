@@ -517,9 +517,28 @@ static inline int pick_mt(int M, int C) {
   return tiles256 >= 1024 ? 16 : 8;
 }
 
+bool gemm_w4v2_supported(int M, int C, int R, int lda);
+void launch_gemm_w4v2(int bwd, const void* A, int lda, const uint32_t* codes, const float* absmax_t,
+                      const void* ext_a, const void* ext_b, int R_ext, const void* residual, void* out, int M, int C,
+                      int R, hipStream_t st);
+
+static int g_gemm_impl_override = 0;
+void set_gemm_impl(int impl) { g_gemm_impl_override = impl; }  // A/B benches in one process
+static inline int gemm_impl() {
+  static const int impl = [] {
+    const char* e = getenv("LIPA_GEMM_IMPL");  // 1 = generation-1 kernel, 2 = buffer-SRD kernel
+    return e ? atoi(e) : 2;
+  }();
+  return g_gemm_impl_override ? g_gemm_impl_override : impl;
+}
+
 void launch_gemm_w4(int bwd, const void* A, int lda, const uint32_t* codes, const float* absmax_t, const void* ext_a,
                     const void* ext_b, int R_ext, const void* residual, void* out, int M, int C, int R,
                     hipStream_t st) {
+  if (gemm_impl() == 2 && gemm_w4v2_supported(M, C, R, lda)) {
+    launch_gemm_w4v2(bwd, A, lda, codes, absmax_t, ext_a, ext_b, R_ext, residual, out, M, C, R, st);
+    return;
+  }
   const int mt = pick_mt(M, C);
   const int BM = mt * 16;
   const int nwg = ((M + BM - 1) / BM) * ((C + BN - 1) / BN);

@@ -1,0 +1,327 @@
+// NF4 weight GEMM, generation 2: same math and packed layouts as gemm.hip's
+// gemm_w4_k, restructured after rocprofv3 PMC counters of generation 1 (profiles/gemm_pmc_*.txt):
+// the main loop spent 217 VALU per 64-deep K-step of which ~45 were 64-bit address math for the
+// LDS-DMA staging (global_load_lds + v_readfirstlane per instruction) and the code loads, and
+// hipcc SLP-packed the absmax scaling into v_pk_mul_f32 (packed f32 beside MFMA is an
+// anti-lever on CDNA4).  Generation 2:
+//  * every global access is a buffer instruction on a wave-uniform SRD (T8/T20): per-lane
+//    32-bit voffsets are computed ONCE, the K-step advance is a scalar soffset, the LDS-DMA
+//    (buffer_load_dwordx4 ... lds) destination is set through M0 by s_mov — the staging costs
+//    no VALU inside the loop;
+//  * per-wave tile = ALL 256 tile rows × 32 weight columns (BM = 256): 0.5 dequantised values
+//    per MFMA, so the dequant VALU (bfe + LUT ds_read + v_mul + v_cvt_pk) fits the MFMA gaps;
+//  * scaling stays scalar v_mul_f32 (inline asm pins it; no SLP packing);
+//  * 2 workgroups per CU (64 KB LDS, <=256 VGPR): the other workgroup's MFMAs hide this one's
+//    end-of-step barrier.
+// Weight codes / absmax are loaded two K-steps ahead into registers and dequantised one step
+// ahead (same software pipeline as generation 1).
+#include "common.h"
+
+using namespace lipa;
+
+namespace {
+
+constexpr int BN = 128;
+constexpr int BK = 64;
+constexpr int NTHR = 256;
+
+__constant__ float kNF4v2[16] = {
+    -1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f,
+    -0.28444138169288635f, -0.18477343022823334f, -0.09105003625154495f, 0.0f,
+    0.07958029955625534f, 0.16093020141124725f, 0.24611230194568634f, 0.33791524171829224f,
+    0.44070982933044434f, 0.5626170039176941f, 0.7229568362236023f, 1.0f};
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint64_t bytes) {
+  const uint64_t p = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(p));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(p >> 32));
+  const uint32_t n = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(bytes > 0xFFFFFFFFull ? 0xFFFFFFFFull : bytes));
+  void* b = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(b, 0, n, 0x00020000);
+}
+
+__device__ __forceinline__ float fmul(float a, float b) {
+  float r;
+  asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ uint32_t pk2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
+}
+template <int OFF>
+__device__ __forceinline__ uint32_t bfe8_c(uint32_t x) {
+  if constexpr (OFF == 0) return x & 0xFFu;
+  else if constexpr (OFF == 24) return x >> 24;
+  else {
+    uint32_t r;
+    asm("v_bfe_u32 %0, %1, %2, 8" : "=v"(r) : "v"(x), "i"(OFF));
+    return r;
+  }
+}
+__device__ __forceinline__ float lut_at(const float* lut, uint32_t byte_off) {
+  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(lut) + byte_off);
+}
+// 8 nibbles (nibble j at bits 4j) → LUT values, element order j = 0..7
+__device__ __forceinline__ void lut8(uint32_t x, const float* lut, float (&v)[8]) {
+  const uint32_t lo4 = (x << 2) & 0x3C3C3C3Cu, hi4 = (x >> 2) & 0x3C3C3C3Cu;
+  v[0] = lut_at(lut, bfe8_c<0>(lo4));
+  v[1] = lut_at(lut, bfe8_c<0>(hi4));
+  v[2] = lut_at(lut, bfe8_c<8>(lo4));
+  v[3] = lut_at(lut, bfe8_c<8>(hi4));
+  v[4] = lut_at(lut, bfe8_c<16>(lo4));
+  v[5] = lut_at(lut, bfe8_c<16>(hi4));
+  v[6] = lut_at(lut, bfe8_c<24>(lo4));
+  v[7] = lut_at(lut, bfe8_c<24>(hi4));
+}
+__device__ __forceinline__ bf16x8 dequant8(uint32_t x, float sc, const float* lut) {
+  float v[8];
+  lut8(x, lut, v);
+  u32x4 r{pk2(fmul(v[0], sc), fmul(v[1], sc)), pk2(fmul(v[2], sc), fmul(v[3], sc)),
+          pk2(fmul(v[4], sc), fmul(v[5], sc)), pk2(fmul(v[6], sc), fmul(v[7], sc))};
+  return __builtin_bit_cast(bf16x8, r);
+}
+__device__ __forceinline__ bf16x8 dequant8v(uint32_t x, f32x4 s0, f32x4 s1, const float* lut) {
+  float v[8];
+  lut8(x, lut, v);
+  u32x4 r{pk2(fmul(v[0], s0[0]), fmul(v[1], s0[1])), pk2(fmul(v[2], s0[2]), fmul(v[3], s0[3])),
+          pk2(fmul(v[4], s1[0]), fmul(v[5], s1[1])), pk2(fmul(v[6], s1[2]), fmul(v[7], s1[3]))};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+template <bool BWD>
+struct StepW;
+template <>
+struct StepW<false> {
+  u32x4 c;
+  float a0, a1;
+};
+template <>
+struct StepW<true> {
+  u32x4 c;
+  f32x4 a[4];
+};
+
+// codes: wave's [nk][64 lanes][16 B] run; absmax: fwd [K/64][C] fp32, bwd [C/64][R] fp32
+template <bool BWD>
+__device__ __forceinline__ void load_step(StepW<BWD>& q, rsrc_t cr, uint32_t coff, rsrc_t ar, uint32_t aoff, int t,
+                                          int C) {
+  q.c = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(cr, coff, t * 1024, 0));
+  if constexpr (!BWD) {
+    const uint32_t so = (uint32_t)t * (uint32_t)C * 4u;
+    q.a0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ar, aoff, so, 0));
+    q.a1 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ar, aoff + 64, so, 0));
+  } else {
+    const uint32_t so = (uint32_t)t * BK * 4u;
+    q.a[0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ar, aoff, so, 0));
+    q.a[1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ar, aoff + 16, so, 0));
+    q.a[2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ar, aoff + 128, so, 0));
+    q.a[3] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ar, aoff + 144, so, 0));
+  }
+}
+
+template <bool BWD>
+__device__ __forceinline__ void dequant_half(const StepW<BWD>& q, const float* lut, bf16x8 (&wf)[2][2], int h) {
+  if constexpr (!BWD) {
+    const float a = h ? q.a1 : q.a0;
+    wf[h][0] = dequant8(q.c[2 * h], a, lut);
+    wf[h][1] = dequant8(q.c[2 * h + 1], a, lut);
+  } else {
+    wf[h][0] = dequant8v(q.c[2 * h], q.a[0], q.a[1], lut);
+    wf[h][1] = dequant8v(q.c[2 * h + 1], q.a[2], q.a[3], lut);
+  }
+}
+
+__device__ __forceinline__ const char* a_frag_addr(const char* buf, int mt, int s, int lane) {
+  const int r = 16 * mt + (lane & 15);
+  const int c = 4 * s + (lane >> 4);
+  return buf + r * 128 + ((c ^ ((r >> 1) & 7)) << 4);
+}
+
+// Stage the 256×64 activation tile: 32 LDS-DMA instructions (1 KB each) per workgroup, 8 per
+// wave.  voff[i] is the lane's precomputed source byte offset (row clamp + chunk swizzle), the
+// K-step advance is the scalar soffset.
+// (not a template: hipcc rejects __amdgpu_buffer_rsrc_t in a deduced template signature; pw is
+// a literal at every call site, so the loop still unrolls after inlining)
+__device__ __forceinline__ void stage_a(rsrc_t ar, const uint32_t* voff, int pw, uint32_t soff, char* wave_dst) {
+#pragma unroll
+  for (int i = 0; i < pw; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ar, (lds_ptr_t)(wave_dst + i * 1024), 16, voff[i], soff, 0, 0);
+}
+
+template <int MT, bool BWD>
+__global__ __launch_bounds__(NTHR, 2) void gemm_w4v2_k(const bf16* __restrict__ A, int lda,
+                                                      const uint32_t* __restrict__ codes,
+                                                      const float* __restrict__ absmax_t,
+                                                      const bf16* __restrict__ ext_a, const bf16* __restrict__ ext_b,
+                                                      int R_ext, const bf16* __restrict__ residual,
+                                                      bf16* __restrict__ out, int M, int C, int R) {
+  // one LDS array (a second __shared__ object can make hipcc drain vmcnt before ds_reads):
+  // [0, 64) NF4 code table — at offset 0 so every LUT ds_read is "base-free" (immediate
+  // offsets are 16-bit), then the two 32 KB activation buffers
+  constexpr int BM = MT * 16;
+  constexpr int ABUF = BM * BK * 2;  // 32 KB (MT 16) / 16 KB (MT 8)
+  constexpr int PW = BM / 32;        // 1-KB LDS-DMA instructions per wave per K-step
+  __shared__ __attribute__((aligned(16))) char lds[64 + 2 * ABUF];
+  float* lut = reinterpret_cast<float*>(lds);
+  char* smem = lds + 64;
+  if (threadIdx.x < 16) lut[threadIdx.x] = kNF4v2[threadIdx.x];
+
+  const int tiles_m = (M + BM - 1) / BM, tiles_c = (C + BN - 1) / BN;
+  const int nwg = tiles_m * tiles_c;
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int tm = id % tiles_m, tc = id / tiles_m;
+  const int m0 = tm * BM;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int cw = tc * BN + 32 * wu;
+  const bool active = cw < C;
+  const int T = cw >> 5;
+  const int nk = R / BK;
+
+  // ---- descriptors (wave-uniform) and per-lane offsets (computed once)
+  const rsrc_t a_rs = make_rsrc(A, (uint64_t)M * lda * 2);
+  const rsrc_t c_rs = make_rsrc(codes, (uint64_t)C * R / 2);
+  const rsrc_t s_rs = make_rsrc(absmax_t, (uint64_t)C * R / 64 * 4);
+  uint32_t voff[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int slot = (wu * PW + i) * 64 + lane;
+    const int row = slot >> 3, q = slot & 7;
+    const int c = q ^ ((row >> 1) & 7);
+    int gr = m0 + row;
+    gr = gr < M ? gr : M - 1;
+    voff[i] = (uint32_t)gr * (uint32_t)lda * 2u + (uint32_t)c * 16u;
+  }
+  char* wave_dst0 = smem + wu * PW * 1024;
+  const int Ts = active ? T : 0;
+  const uint32_t coff = ((uint32_t)Ts * (uint32_t)nk * 64u + lane) * 16u;
+  const int cws = active ? cw : 0;
+  const uint32_t aoff = BWD ? ((uint32_t)(cws >> 6) * (uint32_t)R + 8u * (lane >> 4)) * 4u
+                            : (uint32_t)(cws + (lane & 15)) * 4u;
+
+  f32x4 acc[2][MT];
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[st][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  StepW<BWD> q1, q2;
+  load_step<BWD>(q1, c_rs, coff, s_rs, aoff, 0, C);
+  load_step<BWD>(q2, c_rs, coff, s_rs, aoff, nk > 1 ? 1 : 0, C);
+  stage_a(a_rs, voff, PW, 0, wave_dst0);
+  __syncthreads();
+  bf16x8 wf[2][2];
+  dequant_half<BWD>(q1, lut, wf, 0);
+  dequant_half<BWD>(q1, lut, wf, 1);
+  q1 = q2;
+
+  constexpr int RD = BWD ? 4 : (MT < 8 ? MT : 8);  // bwd holds 16 absmax per K-step: shorter fragment ring keeps it spill-free
+  for (int t = 0; t < nk; ++t) {
+    const char* cur = smem + (t & 1) * ABUF;
+    const int tn = t + 1 < nk ? t + 1 : nk - 1;
+    stage_a(a_rs, voff, PW, (uint32_t)tn * BK * 2u, wave_dst0 + ((t + 1) & 1) * ABUF);
+    load_step<BWD>(q2, c_rs, coff, s_rs, aoff, t + 2 < nk ? t + 2 : nk - 1, C);
+    bf16x8 wn[2][2];
+    bf16x8 xr[RD];
+#pragma unroll
+    for (int f = 0; f < RD; ++f) xr[f] = *reinterpret_cast<const bf16x8*>(a_frag_addr(cur, f % MT, f / MT, lane));
+#pragma unroll
+    for (int f = 0; f < 2 * MT; ++f) {
+      const int s = f / MT, mt = f % MT;
+      if (f == 0) dequant_half<BWD>(q1, lut, wn, 0);
+      if (f == MT) dequant_half<BWD>(q1, lut, wn, 1);
+      const bf16x8 xf = xr[f % RD];
+      if (f + RD < 2 * MT)
+        xr[f % RD] = *reinterpret_cast<const bf16x8*>(a_frag_addr(cur, (f + RD) % MT, (f + RD) / MT, lane));
+      acc[0][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0][s], xf, acc[0][mt], 0, 0, 0);
+      acc[1][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[1][s], xf, acc[1][mt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4 * MT; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // 2 VALU
+    }
+    wf[0][0] = wn[0][0]; wf[0][1] = wn[0][1]; wf[1][0] = wn[1][0]; wf[1][1] = wn[1][1];
+    q1 = q2;
+    __syncthreads();
+  }
+
+  if (!active) return;
+  for (int e0 = 0; ext_a && e0 < R_ext; e0 += 32) {
+    bf16x8 eb[2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int c = cw + 16 * st + (lane & 15);
+      eb[st] = *reinterpret_cast<const bf16x8*>(ext_b + (size_t)c * R_ext + e0 + 8 * (lane >> 4));
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      int m = m0 + 16 * mt + (lane & 15);
+      m = m < M ? m : M - 1;
+      const bf16x8 ea = *reinterpret_cast<const bf16x8*>(ext_a + (size_t)m * R_ext + e0 + 8 * (lane >> 4));
+      acc[0][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(eb[0], ea, acc[0][mt], 0, 0, 0);
+      acc[1][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(eb[1], ea, acc[1][mt], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = m0 + 16 * mt + (lane & 15);
+    if (m >= M) continue;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int c = cw + 16 * st + 4 * (lane >> 4);
+      f32x4 v = acc[st][mt];
+      if (residual) {
+        const bf16x4 rr = *reinterpret_cast<const bf16x4*>(residual + (size_t)m * C + c);
+        v[0] += (float)rr[0]; v[1] += (float)rr[1]; v[2] += (float)rr[2]; v[3] += (float)rr[3];
+      }
+      bf16x4 o;
+      o[0] = (bf16)v[0]; o[1] = (bf16)v[1]; o[2] = (bf16)v[2]; o[3] = (bf16)v[3];
+      *reinterpret_cast<bf16x4*>(out + (size_t)m * C + c) = o;
+    }
+  }
+}
+
+}  // namespace
+
+bool gemm_w4v2_supported(int M, int C, int R, int lda) {
+  // 32-bit buffer offsets; every K-step a whole NF4 block
+  return (uint64_t)M * lda * 2 < 0xFFFFFFFFull && (uint64_t)C * R / 2 < 0xFFFFFFFFull && R % BK == 0 && C % 32 == 0;
+}
+
+// 256-row tiles need >= 2 workgroups per CU (their occupancy) to pay; otherwise 128-row tiles
+// (twice the workgroups, 1 dequantised value per MFMA).  LIPA_GEMM_MT=8|16 forces one.
+static int pick_mt_v2(int M, int C) {
+  static const int forced = [] {
+    const char* e = getenv("LIPA_GEMM_MT");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 8 || forced == 16) return forced;
+  const long tiles256 = (long)((M + 255) / 256) * ((C + BN - 1) / BN);
+  return tiles256 >= 512 ? 16 : 8;
+}
+
+void launch_gemm_w4v2(int bwd, const void* A, int lda, const uint32_t* codes, const float* absmax_t,
+                      const void* ext_a, const void* ext_b, int R_ext, const void* residual, void* out, int M, int C,
+                      int R, hipStream_t st) {
+  const int mt = pick_mt_v2(M, C);
+  const int BM = mt * 16;
+  const int nwg = ((M + BM - 1) / BM) * ((C + BN - 1) / BN);
+#define L(MT_, B)                                                                                                 \
+  gemm_w4v2_k<MT_, B><<<nwg, NTHR, 0, st>>>((const bf16*)A, lda, codes, absmax_t, (const bf16*)ext_a,            \
+                                            (const bf16*)ext_b, R_ext, (const bf16*)residual, (bf16*)out, M, C, R)
+  if (bwd) {
+    if (mt == 16) L(16, true);
+    else L(8, true);
+  } else {
+    if (mt == 16) L(16, false);
+    else L(8, false);
+  }
+#undef L
+  LIPA_CHECK_LAUNCH();
+}

@@ -136,10 +136,14 @@ def set_seed(seed: int):
     torch.manual_seed(seed)
     if torch.cuda.is_available():
         torch.cuda.manual_seed_all(seed)
+    from ..ops.linear import seed_dropout
+    seed_dropout(seed)
 
 
 def _rng_state():
-    st = {"python": random.getstate(), "numpy": np.random.get_state(), "cpu": torch.get_rng_state()}
+    from ..ops.linear import _KEY
+    st = {"python": random.getstate(), "numpy": np.random.get_state(), "cpu": torch.get_rng_state(),
+          "dropout_key": int(_KEY[0])}
     if torch.cuda.is_available():
         st["cuda"] = torch.cuda.get_rng_state_all()
     return st
@@ -149,6 +153,9 @@ def _set_rng_state(st):
     random.setstate(st["python"])
     np.random.set_state(st["numpy"])
     torch.set_rng_state(st["cpu"])
+    if "dropout_key" in st:
+        from ..ops.linear import _KEY
+        _KEY[0] = int(st["dropout_key"])
     if "cuda" in st and torch.cuda.is_available():
         torch.cuda.set_rng_state_all(st["cuda"])
 
@@ -160,7 +167,7 @@ def _rng_to_safe(st):
     out = {"python": [py[0], list(py[1]), py[2]],
            "numpy": [npst[0], torch.from_numpy(np.asarray(npst[1]).astype(np.int64)), int(npst[2]), int(npst[3]),
                      float(npst[4])],
-           "cpu": st["cpu"]}
+           "cpu": st["cpu"], "dropout_key": st.get("dropout_key", 0)}
     if "cuda" in st:
         out["cuda"] = list(st["cuda"])
     return out
@@ -171,7 +178,7 @@ def _rng_from_safe(d):
     npst = d["numpy"]
     st = {"python": (py[0], tuple(py[1]), py[2]),
           "numpy": (npst[0], npst[1].numpy().astype(np.uint32), npst[2], npst[3], npst[4]),
-          "cpu": d["cpu"]}
+          "cpu": d["cpu"], "dropout_key": d.get("dropout_key", 0)}
     if "cuda" in d:
         st["cuda"] = d["cuda"]
     return st

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--m", type=int, nargs="+", default=[1024, 2048])
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--model", default="8b")
+    ap.add_argument("--impls", type=int, nargs="+", default=[1, 2])
+    ap.add_argument("--quick", action="store_true", help="NF4 impls + hipBLASLt only")
     a = ap.parse_args()
     C = native()
     h, f = (4096, 12288) if a.model == "8b" else (5120, 17408)
@@ -49,8 +51,19 @@ def main():
             dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
             fl = 2 * M * N * K
             r = {}
-            r["nf4_fwd"] = timeit(lambda: C.gemm_nf4(x, cf, at, N, None, None, None), a.iters)
-            r["nf4_bwd"] = timeit(lambda: C.gemm_nf4_t(dy, cb, at, K, None, None), a.iters)
+            for impl in a.impls:
+                C.set_gemm_impl(impl)
+                r[f"nf4_fwd_v{impl}"] = timeit(lambda: C.gemm_nf4(x, cf, at, N, None, None, None), a.iters)
+                r[f"nf4_bwd_v{impl}"] = timeit(lambda: C.gemm_nf4_t(dy, cb, at, K, None, None), a.iters)
+            C.set_gemm_impl(0)
+            if a.quick:
+                r["bf16_fwd_hipblaslt"] = timeit(lambda: x @ w.t(), a.iters)
+                r["bf16_bwd_hipblaslt"] = timeit(lambda: dy @ w, a.iters)
+                for k, us in r.items():
+                    tot[(M, k)] = tot.get((M, k), 0) + us
+                    print(f"M={M:5d} {name:8s} N={N:6d} K={K:6d} {k:20s} {us:9.1f} us {fl / us / 1e6:8.1f} TF/s",
+                          flush=True)
+                continue
             r["bf16_fwd_hipblaslt"] = timeit(lambda: x @ w.t(), a.iters)
             r["bf16_bwd_hipblaslt"] = timeit(lambda: dy @ w, a.iters)
             r["bf16_fwd_lipa"] = timeit(lambda: C.gemm_bf16(x, w, None, None, None), a.iters)
