@@ -38,7 +38,7 @@ def flash_attention(q, k, v, batch: int, seqlen: int, hq: int, hkv: int, d: int,
                     causal: bool = True, scale: float | None = None,
                     kv_lens: torch.Tensor | None = None) -> torch.Tensor:
     scale = scale if scale is not None else 1.0 / math.sqrt(d)
-    if use_native(q):
+    if use_native(q) and d in (64, 128) and q.dtype == torch.bfloat16:
         return _FlashAttnFn.apply(q, k, v, batch, seqlen, hq, hkv, d, causal, scale, kv_lens)
     qb = q.reshape(batch, seqlen, hq, d)
     kb = k.reshape(batch, seqlen, hkv, d)

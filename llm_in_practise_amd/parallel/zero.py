@@ -471,6 +471,21 @@ class ZeroEngine:
             dist.all_gather_into_tensor(self.flat_model, self.flat_model[self.shard_slice].clone())
 
     # ------------------------------------------------------------------ state / checkpoints
+    @contextlib.contextmanager
+    def gathered_params(self):
+        """All stage-3 partitions gathered for the duration (collective: call on every rank);
+        e.g. around an adapter ``save_pretrained`` (``stage3_gather_16bit_weights_on_model_save``)."""
+        if self.stage == 3:
+            for u in self.units:
+                u.gather()
+        try:
+            yield
+        finally:
+            if self.stage == 3:
+                for u in self.units:
+                    if not self.persistent[id(u)]:
+                        u.release()
+
     def consolidated_state_dict(self) -> dict:
         """Full (16-bit where trained in 16-bit) model state dict; gathers stage-3 shards."""
         if self.stage == 3:

@@ -330,28 +330,25 @@ class Trainer:
     # ------------------------------------------------------------------ checkpoint
     def _save_weights(self, out):
         m = _unwrap(self.model)
-        if self.engine is not None and self.engine.stage == 3:
-            sd = self.engine.consolidated_state_dict()       # collective
-        else:
-            sd = None
-        if self.rank != 0:
-            return
-        os.makedirs(out, exist_ok=True)
-        if hasattr(m, "save_pretrained") and hasattr(m, "adapter_state_dict"):
-            m.save_pretrained(out)
-        else:
-            from safetensors.torch import save_file
-            sd = sd or m.state_dict()
-            seen, clean = {}, {}
-            for k, v in sd.items():                 # safetensors rejects shared storage (tied heads)
-                key = (v.data_ptr(), v.shape)
-                if key in seen:
-                    continue
-                seen[key] = k
-                clean[k] = v.detach().contiguous().cpu()
-            save_file(clean, os.path.join(out, "model.safetensors"), metadata={"format": "pt"})
-        if self.tokenizer is not None and hasattr(self.tokenizer, "save_pretrained"):
-            self.tokenizer.save_pretrained(out)
+        gather = self.engine.gathered_params() if self.engine is not None else _null()
+        with gather:                                  # collective under ZeRO-3: every rank enters
+            if self.rank != 0:
+                return
+            os.makedirs(out, exist_ok=True)
+            if hasattr(m, "save_pretrained") and hasattr(m, "adapter_state_dict"):
+                m.save_pretrained(out)
+            else:
+                from safetensors.torch import save_file
+                seen, clean = set(), {}
+                for k, v in m.state_dict().items():   # safetensors rejects shared storage (tied heads)
+                    key = (v.data_ptr(), tuple(v.shape))
+                    if key in seen:
+                        continue
+                    seen.add(key)
+                    clean[k] = v.detach().contiguous().cpu()
+                save_file(clean, os.path.join(out, "model.safetensors"), metadata={"format": "pt"})
+            if self.tokenizer is not None and hasattr(self.tokenizer, "save_pretrained"):
+                self.tokenizer.save_pretrained(out)
 
     def save_model(self, output_dir: str | None = None):
         self._save_weights(output_dir or self.args.output_dir)

@@ -130,3 +130,16 @@ def test_trainer_ddp_and_zero_world2_match_single(tmp_path, ds_cfg):
     want = _adapter(m)
     for k in want:
         assert torch.allclose(got[k], want[k], atol=2e-5), (k, (got[k] - want[k]).abs().max())
+
+
+def test_trainer_zero3_saves_gathered_adapter(tmp_path):
+    ds = SyntheticLMDataset(512, 32, 8, seed=5)
+    m = _model()
+    cfg = {"zero_optimization": {"stage": 3, "stage3_param_persistence_threshold": 0}}
+    tr = Trainer(m, _args(tmp_path, max_steps=2, save_steps=2, deepspeed=cfg), train_dataset=ds,
+                 data_collator=_PadCollator())
+    tr.train()
+    from safetensors.torch import load_file
+    sd = load_file(str(tmp_path / "checkpoint-2" / "adapter_model.safetensors"))
+    assert sd and all(v.numel() > 0 for v in sd.values())
+    assert os.path.isdir(tmp_path / "checkpoint-2" / "global_step2")
