@@ -49,6 +49,11 @@ void launch_attn_bwd(const void*, const void*, const void*, const void*, const v
                      int, int, void*, void*, void*, float*, float*, float*, float*, int, int, int, int, int, int,
                      float, hipStream_t);
 
+void launch_decode_attention(const void*, const void*, const void*, const int*, float*, float*, float*, void*, int, int,
+                             int, int, int, int, float, hipStream_t);
+int decode_chunk();
+void launch_sample(int, const void*, const int*, int, float*, int64_t*, int, int, float, int, float, float, uint64_t,
+                   hipStream_t);
 void launch_dropout_fwd(const void*, void*, size_t, uint64_t, float, hipStream_t);
 void launch_dropout_bwd_add(void*, const void*, size_t, uint64_t, float, hipStream_t);
 
@@ -424,6 +429,55 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o
   return {dq, dk, dv};
 }
 
+// ------------------------------------------------------------------ generation (K16, K17)
+// q [B, hq*d] bf16; kc/vc [B, Smax, hkv*d] bf16 contiguous; lens [B] int32 (valid keys per row);
+// max_len >= max(lens) bounds the split count without a host sync.
+Tensor decode_attention(Tensor q, Tensor kc, Tensor vc, Tensor lens, int64_t hq, int64_t hkv, int64_t d,
+                        int64_t max_len, double scale) {
+  CHECK_CUDA(q);
+  CHECK_BF16(q);
+  CHECK_BF16(kc);
+  CHECK_BF16(vc);
+  CHECK_CONTIG(q);
+  CHECK_CONTIG(kc);
+  CHECK_CONTIG(vc);
+  TORCH_CHECK(lens.scalar_type() == at::kInt && lens.is_contiguous(), "lens: int32");
+  TORCH_CHECK(d == 64 || d == 128, "decode_attention: head_dim 64 or 128");
+  const int64_t G = hq / hkv;
+  TORCH_CHECK(hq % hkv == 0 && (G == 1 || G == 2 || G == 4 || G == 5 || G == 8), "decode_attention: group size");
+  const int64_t B = q.size(0), Smax = kc.size(1);
+  TORCH_CHECK(kc.size(0) == B && kc.size(2) == hkv * d && vc.sizes() == kc.sizes(), "decode_attention: cache shape");
+  TORCH_CHECK(max_len <= Smax, "decode_attention: max_len > cache");
+  const int nsplit = std::max<int64_t>(1, (max_len + decode_chunk() - 1) / decode_chunk());
+  auto f32 = q.options().dtype(at::kFloat);
+  Tensor opart = at::empty({B * hq * nsplit, d}, f32);
+  Tensor mpart = at::empty({B * hq * nsplit}, f32), lpart = at::empty({B * hq * nsplit}, f32);
+  Tensor out = at::empty({B, hq * d}, q.options());
+  launch_decode_attention(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), lens.data_ptr<int>(), opart.data_ptr<float>(),
+                          mpart.data_ptr<float>(), lpart.data_ptr<float>(), out.data_ptr(), B, Smax, hq, hkv, d,
+                          nsplit, (float)scale, stream());
+  return out;
+}
+
+// logits [B, V] fp32|bf16; hist [B, L] int32 (-1 = pad) or None; temperature <= 0 → greedy
+Tensor sample(Tensor logits, optional<Tensor> hist, double temperature, int64_t top_k, double top_p, double penalty,
+              int64_t key) {
+  CHECK_CUDA(logits);
+  CHECK_CONTIG(logits);
+  const int64_t B = logits.size(0), V = logits.size(1);
+  Tensor work = at::empty({B, V}, logits.options().dtype(at::kFloat));
+  Tensor out = at::empty({B}, logits.options().dtype(at::kLong));
+  int L = 0;
+  if (hist.has_value() && hist->defined()) {
+    TORCH_CHECK(hist->scalar_type() == at::kInt && hist->is_contiguous() && hist->size(0) == B, "hist: [B,L] int32");
+    L = hist->size(1);
+  }
+  launch_sample(dtype_code(logits), logits.data_ptr(), L ? hist->data_ptr<int>() : nullptr, L,
+                work.data_ptr<float>(), out.data_ptr<int64_t>(), B, V, (float)temperature, (int)top_k, (float)top_p,
+                (float)penalty, (uint64_t)key, stream());
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -444,6 +498,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dropout_bwd_add", &dropout_bwd_add);
   m.def("grad_norm", &grad_norm);
   m.def("set_gemm_impl", &set_gemm_impl);
+  m.def("decode_attention", &decode_attention);
+  m.def("sample", &sample);
   m.def("adamw", &adamw);
   m.def("adamw8bit", &adamw8bit);
   m.def("unscale", &unscale);

@@ -1,0 +1,302 @@
+// Generation-time kernels: KV-cache decode attention and the fused
+// logits → token sampler.
+//
+// decode attention ("flash-decoding" on CDNA4): one query token per sequence against its
+// contiguous KV cache [B, Smax, Hkv*D].  Decode is HBM-bound on the cache read, so the design
+// goal is to stream K/V once with 16-B loads and to spread one sequence over many CUs:
+//  * grid (splits, Hkv, B); each workgroup owns a 128-key chunk of ONE kv head and all of its
+//    G = Hq/Hkv query heads (GQA: K/V are read once for the whole group);
+//  * D/8 lanes hold one key row (8 bf16 = 16 B per lane); a wave covers 64/(D/8) keys per
+//    step, the dot products finish with log2(D/8) xor-shuffles; online softmax per lane slot;
+//  * slots are merged through LDS, splits by a second tiny kernel (log-sum-exp merge).
+// Per-row valid lengths (right-padded batches / different prompt lengths) come from lens[B].
+//
+// sampler: one 1024-thread workgroup per row; repetition penalty (HF semantics: applied once
+// per distinct history token), temperature, top-k and top-p by value-threshold bisection over
+// the row (no sort of the 151,936-entry vocabulary), then an inverse-CDF draw from a
+// counter-based RNG (splitmix64 of (key, row)) with a block prefix scan.  Greedy = argmax.
+#include "common.h"
+
+using namespace lipa;
+
+namespace {
+
+constexpr int DEC_CHUNK = 128;  // keys per workgroup
+constexpr int DEC_THR = 256;
+
+template <int D, int G>
+__global__ __launch_bounds__(DEC_THR) void decode_attn_partial_k(const bf16* __restrict__ q,
+                                                                 const bf16* __restrict__ kc,
+                                                                 const bf16* __restrict__ vc,
+                                                                 const int* __restrict__ lens, float* __restrict__ opart,
+                                                                 float* __restrict__ mpart, float* __restrict__ lpart,
+                                                                 int Smax, int hq, int hkv, int nsplit, float scale) {
+  constexpr int LPK = D / 8;          // lanes per key row
+  constexpr int KPW = 64 / LPK;       // keys per wave step
+  constexpr int NSLOT = 4 * KPW;      // key slots per workgroup
+  const int split = blockIdx.x, kh = blockIdx.y, b = blockIdx.z;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int slot = w * KPW + lane / LPK, e = lane % LPK;  // e: which 8-element piece of the row
+  const int len = lens[b];
+  const int k0 = split * DEC_CHUNK, k1 = min(k0 + DEC_CHUNK, len);
+
+  float qf[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(q + ((size_t)b * hq + kh * G + g) * D + e * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[g][j] = (float)v[j] * scale;
+  }
+  float m[G], l[G], acc[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    m[g] = -INFINITY;
+    l[g] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
+  }
+  const size_t row_stride = (size_t)hkv * D;
+  const bf16* kb = kc + (size_t)b * Smax * row_stride + kh * D + e * 8;
+  const bf16* vb = vc + (size_t)b * Smax * row_stride + kh * D + e * 8;
+  for (int t = k0 + slot; t < k1; t += NSLOT) {
+    const bf16x8 kv = *reinterpret_cast<const bf16x8*>(kb + (size_t)t * row_stride);
+    const bf16x8 vv = *reinterpret_cast<const bf16x8*>(vb + (size_t)t * row_stride);
+    float s[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float d = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d += qf[g][j] * (float)kv[j];
+#pragma unroll
+      for (int o = LPK / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+      s[g] = d;
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float mn = fmaxf(m[g], s[g]);
+      const float c = __expf(m[g] - mn), p = __expf(s[g] - mn);
+      l[g] = l[g] * c + p;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[g][j] = acc[g][j] * c + p * (float)vv[j];
+      m[g] = mn;
+    }
+  }
+  // merge the NSLOT slots through LDS: [slot][g] stats, [slot][g][D] accumulators
+  __shared__ float sm[NSLOT][G], sl[NSLOT][G];
+  __shared__ float sacc[NSLOT][G][D];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    if (e == 0) {
+      sm[slot][g] = m[g];
+      sl[slot][g] = l[g];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sacc[slot][g][e * 8 + j] = acc[g][j];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < G * D; i += DEC_THR) {
+    const int g = i / D, d = i % D;
+    float M = -INFINITY;
+    for (int s2 = 0; s2 < NSLOT; ++s2) M = fmaxf(M, sm[s2][g]);
+    float L = 0.f, A = 0.f;
+    if (M != -INFINITY) {
+      for (int s2 = 0; s2 < NSLOT; ++s2) {
+        const float c = __expf(sm[s2][g] - M);
+        L += sl[s2][g] * c;
+        A += sacc[s2][g][d] * c;
+      }
+    }
+    const size_t hrow = ((size_t)b * hq + kh * G + g) * nsplit + split;
+    opart[hrow * D + d] = A;
+    if (d == 0) {
+      mpart[hrow] = M;
+      lpart[hrow] = L;
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(D) void decode_attn_merge_k(const float* __restrict__ opart,
+                                                         const float* __restrict__ mpart,
+                                                         const float* __restrict__ lpart, bf16* __restrict__ out,
+                                                         int nsplit) {
+  const size_t h = blockIdx.x;  // b*hq + head
+  const int d = threadIdx.x;
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, mpart[h * nsplit + s]);
+  float L = 0.f, A = 0.f;
+  if (M != -INFINITY) {
+    for (int s = 0; s < nsplit; ++s) {
+      const float c = __expf(mpart[h * nsplit + s] - M);
+      L += lpart[h * nsplit + s] * c;
+      A += opart[(h * nsplit + s) * D + d] * c;
+    }
+  }
+  out[h * D + d] = (bf16)(L > 0.f ? A / L : 0.f);
+}
+
+// ------------------------------------------------------------------------------ sampler
+constexpr int SMP_THR = 1024;
+constexpr int SMP_NW = SMP_THR / 64;
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ float bsum(float v, float* red) { return block_sum<SMP_NW>(v, red); }
+
+template <typename T>
+__global__ __launch_bounds__(SMP_THR) void sample_k(const T* __restrict__ logits, const int* __restrict__ hist,
+                                                    int hist_len, float* __restrict__ work, int64_t* __restrict__ out,
+                                                    int V, float temperature, int top_k, float top_p, float penalty,
+                                                    uint64_t key) {
+  __shared__ float red[SMP_NW];
+  __shared__ float sc[SMP_THR];
+  __shared__ int si[SMP_NW];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const T* x = logits + (size_t)row * V;
+  float* wv = work + (size_t)row * V;
+  for (int i = tid; i < V; i += SMP_THR) wv[i] = (float)x[i];
+  __syncthreads();
+  if (hist && penalty != 1.f) {
+    for (int i = tid; i < hist_len; i += SMP_THR) {
+      const int id = hist[(size_t)row * hist_len + i];
+      if (id >= 0 && id < V) {
+        const float s = (float)x[id];  // from the ORIGINAL row: duplicates write the same value
+        wv[id] = s < 0.f ? s * penalty : s / penalty;
+      }
+    }
+  }
+  __syncthreads();
+  // max + argmax (lowest index wins ties)
+  float best = -INFINITY;
+  int bidx = 0x7FFFFFFF;
+  for (int i = tid; i < V; i += SMP_THR) {
+    const float v = wv[i];
+    if (v > best || (v == best && i < bidx)) { best = v; bidx = i; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bidx, o, 64);
+    if (ov > best || (ov == best && oi < bidx)) { best = ov; bidx = oi; }
+  }
+  if ((tid & 63) == 0) { red[tid >> 6] = best; si[tid >> 6] = bidx; }
+  __syncthreads();
+  best = red[0];
+  bidx = si[0];
+  for (int i = 1; i < SMP_NW; ++i)
+    if (red[i] > best || (red[i] == best && si[i] < bidx)) { best = red[i]; bidx = si[i]; }
+  __syncthreads();
+  if (!(temperature > 0.f)) {  // greedy
+    if (tid == 0) out[row] = bidx;
+    return;
+  }
+  const float invT = 1.f / temperature;
+  const float mx = best * invT;
+  // unnormalised probabilities p_i = exp(x_i/T - max)
+  auto prob = [&](int i) { return __expf(wv[i] * invT - mx); };
+  float lo = 0.f, hi = 1.f;  // threshold on p (max p == 1)
+  // ---- top-k: largest threshold t with count(p >= t) >= k (bisection)
+  float thr = 0.f;
+  if (top_k > 0 && top_k < V) {
+    lo = 0.f; hi = 1.f;
+    for (int it = 0; it < 40; ++it) {
+      const float mid = 0.5f * (lo + hi);
+      float c = 0.f;
+      for (int i = tid; i < V; i += SMP_THR) c += prob(i) >= mid ? 1.f : 0.f;
+      c = bsum(c, red);
+      if (c >= (float)top_k) lo = mid; else hi = mid;
+    }
+    thr = lo;
+  }
+  // ---- top-p over the kept set: largest t >= thr with mass(p >= t) >= top_p * mass(kept)
+  if (top_p < 1.f) {
+    float tot = 0.f;
+    for (int i = tid; i < V; i += SMP_THR) { const float p = prob(i); tot += p >= thr ? p : 0.f; }
+    tot = bsum(tot, red);
+    lo = thr; hi = 1.f;
+    for (int it = 0; it < 40; ++it) {
+      const float mid = 0.5f * (lo + hi);
+      float c = 0.f;
+      for (int i = tid; i < V; i += SMP_THR) { const float p = prob(i); c += p >= mid ? p : 0.f; }
+      c = bsum(c, red);
+      if (c >= top_p * tot) lo = mid; else hi = mid;
+    }
+    thr = lo;
+  }
+  // ---- inverse-CDF draw over kept tokens in index order: contiguous chunk per thread
+  const int per = (V + SMP_THR - 1) / SMP_THR;
+  const int i0 = tid * per, i1 = min(i0 + per, V);
+  float mine = 0.f;
+  for (int i = i0; i < i1; ++i) { const float p = prob(i); mine += p >= thr ? p : 0.f; }
+  sc[tid] = mine;
+  __syncthreads();
+  for (int off = 1; off < SMP_THR; off <<= 1) {  // inclusive Hillis-Steele scan
+    const float add = tid >= off ? sc[tid - off] : 0.f;
+    __syncthreads();
+    sc[tid] += add;
+    __syncthreads();
+  }
+  const float total = sc[SMP_THR - 1];
+  const uint64_t r = mix64(key ^ mix64((uint64_t)row + 0x1234567ull));
+  const float u = (float)((r >> 40) * (1.0 / 16777216.0)) * total;
+  const float before = tid ? sc[tid - 1] : 0.f;
+  if (u >= before && u < sc[tid] && mine > 0.f) {
+    float run = before;
+    int pick = i1 - 1;
+    for (int i = i0; i < i1; ++i) {
+      const float p = prob(i);
+      if (p < thr) continue;
+      run += p;
+      if (u < run) { pick = i; break; }
+    }
+    out[row] = pick;
+  }
+  if (tid == 0 && !(total > 0.f)) out[row] = bidx;
+}
+
+}  // namespace
+
+void launch_decode_attention(const void* q, const void* kc, const void* vc, const int* lens, float* opart, float* mpart,
+                             float* lpart, void* out, int B, int Smax, int hq, int hkv, int d, int nsplit, float scale,
+                             hipStream_t st) {
+  const int G = hq / hkv;
+  dim3 grid(nsplit, hkv, B);
+#define P(D_, G_)                                                                                           \
+  decode_attn_partial_k<D_, G_><<<grid, DEC_THR, 0, st>>>((const bf16*)q, (const bf16*)kc, (const bf16*)vc, \
+                                                          lens, opart, mpart, lpart, Smax, hq, hkv, nsplit, scale)
+#define GS(D_)                          \
+  switch (G) {                          \
+    case 1: P(D_, 1); break;            \
+    case 2: P(D_, 2); break;            \
+    case 4: P(D_, 4); break;            \
+    case 5: P(D_, 5); break;            \
+    case 8: P(D_, 8); break;            \
+    default: break;                     \
+  }
+  if (d == 128) { GS(128) } else if (d == 64) { GS(64) }
+#undef GS
+#undef P
+  if (d == 128)
+    decode_attn_merge_k<128><<<B * hq, 128, 0, st>>>(opart, mpart, lpart, (bf16*)out, nsplit);
+  else
+    decode_attn_merge_k<64><<<B * hq, 64, 0, st>>>(opart, mpart, lpart, (bf16*)out, nsplit);
+  LIPA_CHECK_LAUNCH();
+}
+
+int decode_chunk() { return DEC_CHUNK; }
+
+void launch_sample(int dtype, const void* logits, const int* hist, int hist_len, float* work, int64_t* out, int B, int V,
+                   float temperature, int top_k, float top_p, float penalty, uint64_t key, hipStream_t st) {
+  if (dtype == 0)
+    sample_k<float><<<B, SMP_THR, 0, st>>>((const float*)logits, hist, hist_len, work, out, V, temperature, top_k,
+                                           top_p, penalty, key);
+  else
+    sample_k<bf16><<<B, SMP_THR, 0, st>>>((const bf16*)logits, hist, hist_len, work, out, V, temperature, top_k,
+                                          top_p, penalty, key);
+  LIPA_CHECK_LAUNCH();
+}

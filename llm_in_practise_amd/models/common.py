@@ -138,13 +138,21 @@ def can_fuse(mods: list[nn.Module]) -> bool:
 
 
 class KVCache:
-    """Contiguous pre-allocated KV cache ``[B, Smax, Hkv*D]`` per layer (K17)."""
+    """Contiguous pre-allocated KV cache ``[B, Smax, Hkv*D]`` per layer (K17).
+
+    Prefill writes a uniform prefix (``update``; rows may be right-padded, their valid lengths
+    live in ``lens``); decode appends one token per row at its own position ``pos[b]``
+    (``write_rows``), so a batch of prompts of different lengths decodes without re-padding.
+    ``pos`` is a device tensor, so a decode step has no host sync (hipGraph-capturable)."""
 
     def __init__(self, n_layers: int, batch: int, max_len: int, hkv: int, d: int, dtype, device):
         self.k = [torch.zeros(batch, max_len, hkv * d, dtype=dtype, device=device) for _ in range(n_layers)]
         self.v = [torch.zeros(batch, max_len, hkv * d, dtype=dtype, device=device) for _ in range(n_layers)]
         self.len = 0
         self.max_len = max_len
+        self.batch = batch
+        self.pos: torch.Tensor | None = None      # [B] int64 next write position (decode mode)
+        self._rows = torch.arange(batch, device=device)
 
     def update(self, layer: int, k: torch.Tensor, v: torch.Tensor, start: int):
         """k/v [B, s, Hkv*D] written at ``start``; returns views up to start+s."""
@@ -152,6 +160,14 @@ class KVCache:
         self.k[layer][:, start:start + s] = k
         self.v[layer][:, start:start + s] = v
         return self.k[layer][:, :start + s], self.v[layer][:, :start + s]
+
+    def write_rows(self, layer: int, k: torch.Tensor, v: torch.Tensor):
+        """k/v [B, Hkv*D] written at row-specific positions ``pos``."""
+        self.k[layer][self._rows, self.pos] = k
+        self.v[layer][self._rows, self.pos] = v
+
+    def start_decode(self, lens: torch.Tensor):
+        self.pos = lens.to(torch.long).clone()
 
     def get_seq_length(self) -> int:
         return self.len

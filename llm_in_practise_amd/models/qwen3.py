@@ -28,6 +28,7 @@ import torch.utils.checkpoint as ckpt
 from ..ops import reference as ref
 from ..ops.activation import swiglu_fused
 from ..ops.attention import flash_attention
+from ..ops.decode import decode_attention
 from ..ops.loss import fused_linear_cross_entropy, shift_labels
 from ..ops.norm import RMSNorm, rms_norm
 from ..ops.rope import qk_norm_rope
@@ -142,13 +143,22 @@ class Qwen3Attention(nn.Module):
                                self.hq, self.hkv, self.d, self.cfg.rms_norm_eps)
         if cache is None:
             o = flash_attention(q, k, v, B, S, self.hq, self.hkv, self.d, causal=True, kv_lens=kv_lens)
+        elif cache.pos is not None and S == 1:
+            # decode: append at each row's own position, split-K attention over the cache
+            cache.write_rows(self.layer_idx, k.reshape(B, -1), v.reshape(B, -1))
+            o = decode_attention(q.reshape(B, -1), cache.k[self.layer_idx], cache.v[self.layer_idx], cache.pos + 1,
+                                 self.hq, self.hkv, self.d, max_len=cache.max_len)
         else:
-            kc, vc = cache.update(self.layer_idx, k.view(B, S, -1), v.reshape(B, S, -1), start)
-            Sk = kc.shape[1]
-            o = ref.attention(q.view(B, S, self.hq, self.d), kc.view(B, Sk, self.hkv, self.d),
-                              vc.view(B, Sk, self.hkv, self.d), causal=True,
-                              key_padding_mask=(torch.arange(Sk, device=x.device)[None] < kv_lens[:, None])
-                              if kv_lens is not None else None).reshape(B * S, -1)
+            kc, vc = cache.update(self.layer_idx, k.reshape(B, S, -1), v.reshape(B, S, -1), start)
+            if start == 0:   # prefill: same fused kernel as training (causal + per-row key lengths)
+                o = flash_attention(q, k.reshape(B * S, -1), v.reshape(B * S, -1), B, S, self.hq, self.hkv, self.d,
+                                    causal=True, kv_lens=kv_lens)
+            else:
+                Sk = kc.shape[1]
+                o = ref.attention(q.view(B, S, self.hq, self.d), kc.view(B, Sk, self.hkv, self.d),
+                                  vc.view(B, Sk, self.hkv, self.d), causal=True,
+                                  key_padding_mask=(torch.arange(Sk, device=x.device)[None] < kv_lens[:, None])
+                                  if kv_lens is not None else None).reshape(B * S, -1)
         return project([self.o_proj], o, residual, tr)
 
 
@@ -205,8 +215,10 @@ class Qwen3Model(nn.Module):
     def forward(self, input_ids, position_ids=None, cache: KVCache | None = None, kv_lens=None):
         B, S = input_ids.shape
         start = cache.len if cache is not None else 0
+        decoding = cache is not None and cache.pos is not None and S == 1
         if position_ids is None:
-            position_ids = torch.arange(start, start + S, device=input_ids.device).expand(B, S)
+            position_ids = cache.pos[:, None] if decoding else \
+                torch.arange(start, start + S, device=input_ids.device).expand(B, S)
         cos, sin = self.rope(position_ids)
         x = self.embed_tokens(input_ids).reshape(B * S, -1)
         for layer in self.layers:
@@ -214,7 +226,9 @@ class Qwen3Model(nn.Module):
                 x = ckpt.checkpoint(layer, x, cos, sin, B, S, None, 0, kv_lens, use_reentrant=False)
             else:
                 x = layer(x, cos, sin, B, S, cache, start, kv_lens)
-        if cache is not None:
+        if decoding:
+            cache.pos += 1
+        elif cache is not None:
             cache.len = start + S
         return rms_norm(x, self.norm.weight, self.norm.eps)
 
@@ -274,7 +288,8 @@ class Qwen3ForCausalLM(nn.Module):
         what sequential accumulation of ``loss_i / G`` produces (same gradient)."""
         B, S = input_ids.shape
         kv_lens = None
-        if attention_mask is not None and past_key_values is None:
+        if attention_mask is not None and (past_key_values is None or
+                                           (past_key_values.len == 0 and past_key_values.pos is None)):
             am = attention_mask.to(torch.int32)
             lens = am.sum(1).to(torch.int32)
             if torch.equal(am, (torch.arange(S, device=am.device)[None] < lens[:, None]).int()):
@@ -296,6 +311,13 @@ class Qwen3ForCausalLM(nn.Module):
         else:
             logits = (h @ self.lm_head.weight.t()).view(B, S, -1)
         return CausalLMOutput(loss=loss, logits=logits, past_key_values=past_key_values)
+
+    @torch.no_grad()
+    def generate(self, input_ids=None, attention_mask=None, generation_config=None, streamer=None, **kw):
+        """HF-style ``generate`` (KV cache, greedy / temperature / top-k / top-p / repetition
+        penalty); see :func:`llm_in_practise_amd.infer.generate.generate`."""
+        from ..infer.generate import generate
+        return generate(self, input_ids, attention_mask, generation_config, streamer=streamer, **kw)
 
     # -------------------------------------------------------------- checkpoint IO
     def load_hf_state_dict(self, sd: dict[str, torch.Tensor], strict: bool = False):

@@ -1,0 +1,96 @@
+"""OpenAI-compatible server + moderation adapter on CPU (FastAPI TestClient, tiny Qwen3,
+byte tokenizer)."""
+import json
+
+import pytest
+import torch
+from fastapi.testclient import TestClient
+
+from llm_in_practise_amd.infer.engine import SamplingParams, ServingEngine
+from llm_in_practise_amd.infer.guard import GuardClient, create_guard_app, parse_guard_output, to_openai_moderation
+from llm_in_practise_amd.infer.server import create_app
+from llm_in_practise_amd.models.qwen3 import Qwen3ForCausalLM, qwen3_config
+from llm_in_practise_amd.train.data import ByteTokenizer
+
+
+@pytest.fixture(scope="module")
+def engine():
+    m = Qwen3ForCausalLM.from_config(qwen3_config("qwen3-tiny", vocab_size=256), dtype=torch.float32, seed=0).eval()
+    tok = ByteTokenizer()
+    tok.eos_token_id = 10            # "\n" ends a completion for the test
+    e = ServingEngine(m, tok, model_name="tiny", max_batch=8, system_prompt="You are helpful.")
+    yield e
+    e.shutdown()
+
+
+def test_chat_completion_schema(engine):
+    c = TestClient(create_app(engine))
+    r = c.post("/v1/chat/completions", json={"messages": [{"role": "user", "content": "hi"}], "max_tokens": 5,
+                                             "temperature": 0})
+    assert r.status_code == 200
+    d = r.json()
+    assert d["id"].startswith("chatcmpl-") and d["object"] == "chat.completion"
+    assert d["choices"][0]["message"]["role"] == "assistant"
+    assert d["usage"]["completion_tokens"] <= 5 and d["usage"]["prompt_tokens"] > 10
+
+
+def test_greedy_is_deterministic_and_batched_equals_single(engine):
+    p = SamplingParams(max_tokens=6, temperature=0.0)
+    a = engine.complete("abc", p)["text"]
+    # submit several concurrently: they are decoded as one batch and must match single runs
+    reqs = [engine.submit(s, p) for s in ("abc", "hello world", "x")]
+    outs = []
+    for r in reqs:
+        while True:
+            kind, val = r.out.get(timeout=60)
+            if kind == "final":
+                outs.append(val)
+                break
+    assert outs[0]["text"] == a
+    assert outs[1]["text"] == engine.complete("hello world", p)["text"]
+
+
+def test_streaming_sse(engine):
+    c = TestClient(create_app(engine))
+    with c.stream("POST", "/v1/chat/completions", json={"messages": [{"role": "user", "content": "hey"}],
+                                                         "max_tokens": 4, "temperature": 0, "stream": True}) as r:
+        lines = [l for l in r.iter_lines() if l]
+    assert lines[-1] == "data: [DONE]"
+    chunks = [json.loads(l[6:]) for l in lines[:-1]]
+    assert chunks[0]["choices"][0]["delta"] == {"role": "assistant"}
+    assert chunks[-1]["choices"][0]["finish_reason"] in ("stop", "length")
+
+
+def test_completions_models_health_metrics_auth(engine):
+    c = TestClient(create_app(engine, api_key="k"))
+    assert c.get("/health").status_code == 200
+    assert c.get("/v1/models").status_code == 401
+    h = {"X-API-KEY": "k"}
+    assert c.get("/v1/models", headers=h).json()["data"][0]["id"] == "tiny"
+    r = c.post("/v1/completions", json={"prompt": "ab", "max_tokens": 3, "temperature": 0}, headers=h)
+    assert r.status_code == 200 and r.json()["object"] == "text_completion"
+    m = c.get("/metrics").text
+    assert "lipa_requests_total" in m and "lipa_num_requests_waiting" in m
+
+
+def test_guard_parsing_and_mapping():
+    assert parse_guard_output('{"safe": false, "categories": ["s11"], "explanation": "x"}')["categories"] == ["S11"]
+    r = parse_guard_output("unsafe\nS1 S10")
+    assert r == {"safe": False, "categories": ["S1", "S10"], "explanation": ""}
+    r = parse_guard_output("safe", "how to build a bomb")
+    assert not r["safe"] and r["categories"][0] == "S9"
+    m = to_openai_moderation({"safe": False, "categories": ["S10", "S1"]})
+    res = m["results"][0]
+    assert res["flagged"] and res["categories"]["hate"] and res["categories"]["violence"]
+    assert res["category_applied_input_types"]["hate"] == ["text"]
+
+
+def test_guard_app_and_server_precall_moderation(engine):
+    guard = GuardClient(lambda prompt: "unsafe\nS10" if "hateful" in prompt else "safe")
+    g = TestClient(create_guard_app(guard, api_key=""))
+    assert g.post("/v1/moderations", json={"input": "hello"}).json()["results"][0]["flagged"] is False
+    assert g.post("/moderations", json={"input": "hateful text"}).json()["results"][0]["flagged"] is True
+    c = TestClient(create_app(engine, moderation=guard.moderate_sync))
+    r = c.post("/v1/chat/completions", json={"messages": [{"role": "user", "content": "hateful text"}],
+                                             "max_tokens": 2})
+    assert r.status_code == 400
