@@ -49,6 +49,10 @@ void launch_attn_bwd(const void*, const void*, const void*, const void*, const v
                      int, int, void*, void*, void*, float*, float*, float*, float*, int, int, int, int, int, int,
                      float, hipStream_t);
 
+void launch_gemm_int4(const void*, int, const uint32_t*, const float*, const float*, const void*, const void*, int,
+                      const void*, void*, int, int, int, hipStream_t);
+void launch_gemv_w4(int, const void*, int, const uint8_t*, const float*, const float*, int, const void*, void*, int, int,
+                    int, hipStream_t);
 void launch_decode_attention(const void*, const void*, const void*, const int*, float*, float*, float*, void*, int, int,
                              int, int, int, int, float, hipStream_t);
 int decode_chunk();
@@ -343,6 +347,43 @@ Tensor gemm_nf4(Tensor x, Tensor codes_f, Tensor absmax_t, int64_t N, optional<T
   return y;
 }
 
+// W4A16 affine int4 (K15): Y = X·(q·s + b)ᵀ (+ ext_a·ext_bᵀ) (+ residual); scale_t/bias_t [K/64, N]
+Tensor gemm_int4(Tensor x, Tensor codes_f, Tensor scale_t, Tensor bias_t, int64_t N, optional<Tensor> ext_a,
+                 optional<Tensor> ext_b, optional<Tensor> residual) {
+  CHECK_BF16(x);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "gemm_int4: x row-major, 16-B aligned rows");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(N % 32 == 0 && K % 64 == 0, "gemm_int4: N % 32, K % 64");
+  TORCH_CHECK(codes_f.numel() == N * K / 8 && scale_t.numel() == N * K / 64 && bias_t.numel() == N * K / 64,
+              "gemm_int4: packed weight size");
+  int R_ext;
+  check_ext(ext_a, ext_b, M, N, R_ext);
+  if (residual) TORCH_CHECK(residual->is_contiguous() && residual->size(0) == M && residual->size(1) == N, "residual");
+  auto y = at::empty({M, N}, x.options());
+  launch_gemm_int4(x.data_ptr(), x.stride(0), (const uint32_t*)codes_f.data_ptr(), scale_t.data_ptr<float>(),
+                   bias_t.data_ptr<float>(), optr(ext_a), optr(ext_b), R_ext, optr(residual), y.data_ptr(), M, N, K,
+                   stream());
+  return y;
+}
+
+// decode GEMV (M <= 8): codes [N, K/2] bytes (high nibble = even k), scales [N, K/blk] fp32,
+// bias [N, K/blk] fp32 (affine int4) or None (NF4)
+Tensor gemv_w4(Tensor x, Tensor codes, Tensor scales, optional<Tensor> bias, int64_t N, int64_t blk,
+               optional<Tensor> residual) {
+  CHECK_BF16(x);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "gemv_w4: x row-major");
+  const int M = x.size(0), K = x.size(1);
+  TORCH_CHECK(M <= 8, "gemv_w4: M <= 8");
+  TORCH_CHECK(K % 32 == 0 && blk % 32 == 0 && K % blk == 0, "gemv_w4: K % 32, blk % 32");
+  TORCH_CHECK(codes.numel() == N * K / 2 && scales.numel() == N * K / blk, "gemv_w4: weight size");
+  if (residual) TORCH_CHECK(residual->is_contiguous() && residual->size(0) == M && residual->size(1) == N, "residual");
+  auto y = at::empty({M, N}, x.options());
+  const bool aff = bias.has_value() && bias->defined();
+  launch_gemv_w4(aff ? 2 : 0, x.data_ptr(), x.stride(0), codes.data_ptr<uint8_t>(), scales.data_ptr<float>(),
+                 aff ? bias->data_ptr<float>() : nullptr, blk, optr(residual), y.data_ptr(), M, N, K, stream());
+  return y;
+}
+
 // dX[M, K] = dY[M, N] · deq(W) + ext_a·ext_bᵀ  (ext_b is [K, R])
 Tensor gemm_nf4_t(Tensor dy, Tensor codes_b, Tensor absmax_t, int64_t K, optional<Tensor> ext_a,
                   optional<Tensor> ext_b) {
@@ -499,6 +540,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_norm", &grad_norm);
   m.def("set_gemm_impl", &set_gemm_impl);
   m.def("decode_attention", &decode_attention);
+  m.def("gemm_int4", &gemm_int4);
+  m.def("gemv_w4", &gemv_w4);
   m.def("sample", &sample);
   m.def("adamw", &adamw);
   m.def("adamw8bit", &adamw8bit);

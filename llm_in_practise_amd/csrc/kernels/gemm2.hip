@@ -92,28 +92,51 @@ __device__ __forceinline__ bf16x8 dequant8v(uint32_t x, f32x4 s0, f32x4 s1, cons
   return __builtin_bit_cast(bf16x8, r);
 }
 
-template <bool BWD>
-struct StepW;
-template <>
-struct StepW<false> {
+// MODE 0: NF4 forward  (Y = X·deq(W)ᵀ, one absmax per lane column per K-step)
+// MODE 1: NF4 backward (dX = dY·deq(W), one absmax per reduction row)
+// MODE 2: affine int4 forward (W4A16 GPTQ/AWQ, K15): w = q·s + b with b = −z·s per (group, column)
+template <int MODE>
+struct StepW {
   u32x4 c;
   float a0, a1;
 };
 template <>
-struct StepW<true> {
+struct StepW<1> {
   u32x4 c;
   f32x4 a[4];
 };
+template <>
+struct StepW<2> {
+  u32x4 c;
+  float a0, a1, b0, b1;
+};
 
-// codes: wave's [nk][64 lanes][16 B] run; absmax: fwd [K/64][C] fp32, bwd [C/64][R] fp32
-template <bool BWD>
-__device__ __forceinline__ void load_step(StepW<BWD>& q, rsrc_t cr, uint32_t coff, rsrc_t ar, uint32_t aoff, int t,
-                                          int C) {
+__device__ __forceinline__ float ffma(float a, float b, float c) {
+  float r;
+  asm("v_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ bf16x8 dequant8a(uint32_t x, float sc, float bi, const float* lut) {
+  float v[8];
+  lut8(x, lut, v);
+  u32x4 r{pk2(ffma(v[0], sc, bi), ffma(v[1], sc, bi)), pk2(ffma(v[2], sc, bi), ffma(v[3], sc, bi)),
+          pk2(ffma(v[4], sc, bi), ffma(v[5], sc, bi)), pk2(ffma(v[6], sc, bi), ffma(v[7], sc, bi))};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+// codes: wave's [nk][64 lanes][16 B] run; absmax/scale: fwd [K/64][C] fp32, bwd [C/64][R] fp32
+template <int MODE>
+__device__ __forceinline__ void load_step(StepW<MODE>& q, rsrc_t cr, uint32_t coff, rsrc_t ar, rsrc_t br,
+                                          uint32_t aoff, int t, int C) {
   q.c = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(cr, coff, t * 1024, 0));
-  if constexpr (!BWD) {
+  if constexpr (MODE != 1) {
     const uint32_t so = (uint32_t)t * (uint32_t)C * 4u;
     q.a0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ar, aoff, so, 0));
     q.a1 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ar, aoff + 64, so, 0));
+    if constexpr (MODE == 2) {
+      q.b0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(br, aoff, so, 0));
+      q.b1 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(br, aoff + 64, so, 0));
+    }
   } else {
     const uint32_t so = (uint32_t)t * BK * 4u;
     q.a[0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ar, aoff, so, 0));
@@ -123,12 +146,16 @@ __device__ __forceinline__ void load_step(StepW<BWD>& q, rsrc_t cr, uint32_t cof
   }
 }
 
-template <bool BWD>
-__device__ __forceinline__ void dequant_half(const StepW<BWD>& q, const float* lut, bf16x8 (&wf)[2][2], int h) {
-  if constexpr (!BWD) {
+template <int MODE>
+__device__ __forceinline__ void dequant_half(const StepW<MODE>& q, const float* lut, bf16x8 (&wf)[2][2], int h) {
+  if constexpr (MODE == 0) {
     const float a = h ? q.a1 : q.a0;
     wf[h][0] = dequant8(q.c[2 * h], a, lut);
     wf[h][1] = dequant8(q.c[2 * h + 1], a, lut);
+  } else if constexpr (MODE == 2) {
+    const float a = h ? q.a1 : q.a0, b = h ? q.b1 : q.b0;
+    wf[h][0] = dequant8a(q.c[2 * h], a, b, lut);
+    wf[h][1] = dequant8a(q.c[2 * h + 1], a, b, lut);
   } else {
     wf[h][0] = dequant8v(q.c[2 * h], q.a[0], q.a[1], lut);
     wf[h][1] = dequant8v(q.c[2 * h + 1], q.a[2], q.a[3], lut);
@@ -152,10 +179,11 @@ __device__ __forceinline__ void stage_a(rsrc_t ar, const uint32_t* voff, int pw,
     __builtin_amdgcn_raw_ptr_buffer_load_lds(ar, (lds_ptr_t)(wave_dst + i * 1024), 16, voff[i], soff, 0, 0);
 }
 
-template <int MT, bool BWD>
+template <int MT, int MODE>
 __global__ __launch_bounds__(NTHR, 2) void gemm_w4v2_k(const bf16* __restrict__ A, int lda,
                                                       const uint32_t* __restrict__ codes,
                                                       const float* __restrict__ absmax_t,
+                                                      const float* __restrict__ bias_t,
                                                       const bf16* __restrict__ ext_a, const bf16* __restrict__ ext_b,
                                                       int R_ext, const bf16* __restrict__ residual,
                                                       bf16* __restrict__ out, int M, int C, int R) {
@@ -168,7 +196,8 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_w4v2_k(const bf16* __restrict__ 
   __shared__ __attribute__((aligned(16))) char lds[64 + 2 * ABUF];
   float* lut = reinterpret_cast<float*>(lds);
   char* smem = lds + 64;
-  if (threadIdx.x < 16) lut[threadIdx.x] = kNF4v2[threadIdx.x];
+  constexpr bool BWD = MODE == 1;
+  if (threadIdx.x < 16) lut[threadIdx.x] = MODE == 2 ? (float)threadIdx.x : kNF4v2[threadIdx.x];
 
   const int tiles_m = (M + BM - 1) / BM, tiles_c = (C + BN - 1) / BN;
   const int nwg = tiles_m * tiles_c;
@@ -186,6 +215,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_w4v2_k(const bf16* __restrict__ 
   const rsrc_t a_rs = make_rsrc(A, (uint64_t)M * lda * 2);
   const rsrc_t c_rs = make_rsrc(codes, (uint64_t)C * R / 2);
   const rsrc_t s_rs = make_rsrc(absmax_t, (uint64_t)C * R / 64 * 4);
+  const rsrc_t b_rs = make_rsrc(MODE == 2 ? bias_t : absmax_t, (uint64_t)C * R / 64 * 4);
   uint32_t voff[PW];
 #pragma unroll
   for (int i = 0; i < PW; ++i) {
@@ -209,14 +239,14 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_w4v2_k(const bf16* __restrict__ 
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[st][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  StepW<BWD> q1, q2;
-  load_step<BWD>(q1, c_rs, coff, s_rs, aoff, 0, C);
-  load_step<BWD>(q2, c_rs, coff, s_rs, aoff, nk > 1 ? 1 : 0, C);
+  StepW<MODE> q1, q2;
+  load_step<MODE>(q1, c_rs, coff, s_rs, b_rs, aoff, 0, C);
+  load_step<MODE>(q2, c_rs, coff, s_rs, b_rs, aoff, nk > 1 ? 1 : 0, C);
   stage_a(a_rs, voff, PW, 0, wave_dst0);
   __syncthreads();
   bf16x8 wf[2][2];
-  dequant_half<BWD>(q1, lut, wf, 0);
-  dequant_half<BWD>(q1, lut, wf, 1);
+  dequant_half<MODE>(q1, lut, wf, 0);
+  dequant_half<MODE>(q1, lut, wf, 1);
   q1 = q2;
 
   constexpr int RD = BWD ? 4 : (MT < 8 ? MT : 8);  // bwd holds 16 absmax per K-step: shorter fragment ring keeps it spill-free
@@ -224,7 +254,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_w4v2_k(const bf16* __restrict__ 
     const char* cur = smem + (t & 1) * ABUF;
     const int tn = t + 1 < nk ? t + 1 : nk - 1;
     stage_a(a_rs, voff, PW, (uint32_t)tn * BK * 2u, wave_dst0 + ((t + 1) & 1) * ABUF);
-    load_step<BWD>(q2, c_rs, coff, s_rs, aoff, t + 2 < nk ? t + 2 : nk - 1, C);
+    load_step<MODE>(q2, c_rs, coff, s_rs, b_rs, aoff, t + 2 < nk ? t + 2 : nk - 1, C);
     bf16x8 wn[2][2];
     bf16x8 xr[RD];
 #pragma unroll
@@ -232,8 +262,8 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_w4v2_k(const bf16* __restrict__ 
 #pragma unroll
     for (int f = 0; f < 2 * MT; ++f) {
       const int s = f / MT, mt = f % MT;
-      if (f == 0) dequant_half<BWD>(q1, lut, wn, 0);
-      if (f == MT) dequant_half<BWD>(q1, lut, wn, 1);
+      if (f == 0) dequant_half<MODE>(q1, lut, wn, 0);
+      if (f == MT) dequant_half<MODE>(q1, lut, wn, 1);
       const bf16x8 xf = xr[f % RD];
       if (f + RD < 2 * MT)
         xr[f % RD] = *reinterpret_cast<const bf16x8*>(a_frag_addr(cur, (f + RD) % MT, (f + RD) / MT, lane));
@@ -312,16 +342,35 @@ void launch_gemm_w4v2(int bwd, const void* A, int lda, const uint32_t* codes, co
   const int mt = pick_mt_v2(M, C);
   const int BM = mt * 16;
   const int nwg = ((M + BM - 1) / BM) * ((C + BN - 1) / BN);
-#define L(MT_, B)                                                                                                 \
-  gemm_w4v2_k<MT_, B><<<nwg, NTHR, 0, st>>>((const bf16*)A, lda, codes, absmax_t, (const bf16*)ext_a,            \
-                                            (const bf16*)ext_b, R_ext, (const bf16*)residual, (bf16*)out, M, C, R)
+#define L(MT_, MODE_)                                                                                         \
+  gemm_w4v2_k<MT_, MODE_><<<nwg, NTHR, 0, st>>>((const bf16*)A, lda, codes, absmax_t, nullptr,               \
+                                                (const bf16*)ext_a, (const bf16*)ext_b, R_ext,                \
+                                                (const bf16*)residual, (bf16*)out, M, C, R)
   if (bwd) {
-    if (mt == 16) L(16, true);
-    else L(8, true);
+    if (mt == 16) L(16, 1);
+    else L(8, 1);
   } else {
-    if (mt == 16) L(16, false);
-    else L(8, false);
+    if (mt == 16) L(16, 0);
+    else L(8, 0);
   }
 #undef L
+  LIPA_CHECK_LAUNCH();
+}
+
+// W4A16 affine int4 forward (GPTQ / AWQ / compressed-tensors weights repacked at load time):
+// codes in the NF4 fragment-native forward packing, scale_t/bias_t fp32 [K/64][N] (group 128 →
+// each value repeated for the group's two 64-deep K-steps), w = q·scale + bias.
+void launch_gemm_int4(const void* A, int lda, const uint32_t* codes, const float* scale_t, const float* bias_t,
+                      const void* ext_a, const void* ext_b, int R_ext, const void* residual, void* out, int M, int N,
+                      int K, hipStream_t st) {
+  const int mt = pick_mt_v2(M, N);
+  const int BM = mt * 16;
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (mt == 16)
+    gemm_w4v2_k<16, 2><<<nwg, NTHR, 0, st>>>((const bf16*)A, lda, codes, scale_t, bias_t, (const bf16*)ext_a,
+                                             (const bf16*)ext_b, R_ext, (const bf16*)residual, (bf16*)out, M, N, K);
+  else
+    gemm_w4v2_k<8, 2><<<nwg, NTHR, 0, st>>>((const bf16*)A, lda, codes, scale_t, bias_t, (const bf16*)ext_a,
+                                            (const bf16*)ext_b, R_ext, (const bf16*)residual, (bf16*)out, M, N, K);
   LIPA_CHECK_LAUNCH();
 }

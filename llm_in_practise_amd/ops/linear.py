@@ -56,6 +56,15 @@ def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
             if ext_a is not None:
                 y = y + ext_a @ ext_b.t()
             return y if residual is None else y + residual
+        if x.shape[0] <= 8:           # decode: weight-streaming GEMV, no MFMA tile
+            n, k = base.shape
+            y = native().gemv_w4(x, base.codes, base.gemv_scales(), None, n, base.blocksize,
+                                 residual if ext_a is None else None)
+            if ext_a is not None:
+                y = y + ext_a @ ext_b.t()
+                if residual is not None:
+                    y = y + residual
+            return y
         cf, _, at = base.kernel_pack()
         return native().gemm_nf4(x, cf, at, base.shape[0], ext_a, ext_b, residual)
     return native().gemm_bf16(x, base, ext_a, ext_b, residual)

@@ -139,6 +139,14 @@ class NF4Weight:
         n, k = self.shape
         return self.blocksize == 64 and n % 64 == 0 and k % 64 == 0
 
+    def gemv_scales(self) -> torch.Tensor:
+        """Decoded fp32 block absmax [N, K/64] for the decode GEMV (cached)."""
+        c = self.__dict__.get("_gemv_sc")
+        if c is None:
+            c = self.block_absmax().float().contiguous()
+            self.__dict__["_gemv_sc"] = c
+        return c
+
     def block_absmax(self) -> torch.Tensor:
         """fp32 absmax per block, decoding the double quant."""
         if self.absmax is not None:
