@@ -1,0 +1,587 @@
+"""``lipa`` — one entry point for every executable of the reference.
+
+    lipa minigpt-train | minigpt-generate | minigpt2-train | minigpt2-test      (A1-A5)
+    lipa lm-train --model {simple,gptlike,deepseek,deepseek-dense} ...           (B1-B6, single device)
+    lipa pretrain --strategy {ddp,fsdp,fsdp2,zero1,zero2,zero3,zero-offload}     (C1-C6, D0-D6; torchrun)
+    lipa finetune --preset qwen3-8b-qlora-dist ...                              (E1-E7, E11)
+    lipa chat --base DIR [--adapter DIR]                                        (E8, G1, G2)
+    lipa merge --base DIR --adapter DIR --out DIR                               (E10 export, E11 02/04, K19)
+    lipa quantize --method {gptq,awq,rtn} --model DIR --out DIR [--format ...]  (F1-F4)
+    lipa eval-quant --model DIR                                                  (F2b)
+    lipa infer --model DIR --prompt TEXT                                        (F1b, F2c, G1)
+    lipa serve --model DIR [--adapter DIR] [--port 8000]                        (G4, H1)
+    lipa guard --backend URL [--port 8099]                                      (H3)
+    lipa convert-alpaca --input self_cognition.jsonl --out alpaca.json           (E10 converter)
+    lipa bench ...                                                               (bench.py)
+
+Datasets / checkpoints are LOCAL paths (no hub access); ``--random-init`` builds the named
+architecture with random weights for smoke runs.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+
+def _device(arg: str | None = None):
+    if arg:
+        return torch.device(arg)
+    return torch.device("cuda", int(os.environ.get("LOCAL_RANK", 0))) if torch.cuda.is_available() else \
+        torch.device("cpu")
+
+
+# ============================================================================ track A
+DEMO_TEXT = "马哥教育创立于2009年，是一家专注于云计算、SRE、DevOps、网络安全、Go开发和云原生课程培训的高端IT教育机构。"
+
+
+def cmd_minigpt_train(a):
+    from ..models.minigpt import MiniGPT
+    from ..train.data import CharTokenizer, CharWindowDataset
+    from ..train.loops import LoopConfig, train_lm
+    text = open(a.text).read() if a.text else DEMO_TEXT
+    tok = CharTokenizer(text)
+    ds = CharWindowDataset(text, tok.stoi, a.seq_len, a.repeat)
+    m = MiniGPT(tok.vocab_size, a.embed_dim, a.n_heads, a.n_layers, 0.1, a.seq_len,
+                reference_layout=not a.causal, causal=a.causal).to(_device(a.device))
+    hist = train_lm(m, ds, LoopConfig(epochs=a.epochs, batch_size=a.batch_size, lr=a.lr, weight_decay=0.01,
+                                      clip_grad_norm=1.0, log_every=0, seed=a.seed))
+    torch.save({"model_state": m.state_dict(), "char2idx": tok.stoi,
+                "config": {"embed_dim": a.embed_dim, "seq_len": a.seq_len, "n_heads": a.n_heads,
+                           "n_layers": a.n_layers, "causal": a.causal}}, a.out)
+    print(json.dumps({"final_loss": hist["train_loss"][-1], "checkpoint": a.out}))
+
+
+def cmd_minigpt_generate(a):
+    from ..infer.generate import generate_simple
+    from ..models.minigpt import MiniGPT
+    ck = torch.load(a.checkpoint, map_location="cpu", weights_only=True)
+    stoi = ck["char2idx"]
+    itos = {i: c for c, i in stoi.items()}
+    c = ck["config"]
+    m = MiniGPT(len(stoi), c["embed_dim"], c.get("n_heads", 2), c.get("n_layers", 2), 0.1, c["seq_len"],
+                reference_layout=not c.get("causal", False), causal=c.get("causal", False))
+    m.load_state_dict(ck["model_state"])
+    idx = torch.tensor([[stoi[ch] for ch in a.prompt if ch in stoi]])
+    out = generate_simple(m, idx, a.max_new, c["seq_len"], temperature=a.temperature)
+    print("".join(itos[int(i)] for i in out[0]))
+
+
+def cmd_minigpt2_train(a):
+    from ..models.minigpt import MiniGPT2, MiniGPT2Config
+    from ..train.data import CharTokenizer, CharWindowDataset
+    from ..train.loops import LoopConfig, train_lm
+    text = open(a.text).read() if a.text else DEMO_TEXT
+    tok = CharTokenizer(text)
+    cfg = MiniGPT2Config(vocab_size=tok.vocab_size, seq_len=min(a.seq_len, max(2, len(text) - 1)))
+    # the reference's dataset is empty when text < seq_len (minigpt2/model.py:111, ZeroDivisionError);
+    # here the window shrinks to the text length instead
+    ds = CharWindowDataset(text, tok.stoi, cfg.seq_len, 1)
+    m = MiniGPT2(cfg).to(_device(a.device))
+    hist = train_lm(m, ds, LoopConfig(epochs=a.epochs, batch_size=min(cfg.batch_size, len(ds)), lr=cfg.lr,
+                                      weight_decay=cfg.weight_decay, log_every=0))
+    torch.save({"model_state": m.state_dict(), "stoi": tok.stoi, "itos": {i: c for c, i in tok.stoi.items()},
+                "config": cfg.__dict__}, a.out)
+    print(json.dumps({"final_loss": hist["train_loss"][-1], "checkpoint": a.out}))
+
+
+def cmd_minigpt2_test(a):
+    from ..infer.generate import generate_simple
+    from ..models.minigpt import MiniGPT2, MiniGPT2Config
+    ck = torch.load(a.checkpoint, map_location="cpu", weights_only=True)
+    cfg = MiniGPT2Config(**{k: v for k, v in ck["config"].items() if k in MiniGPT2Config.__dataclass_fields__})
+    m = MiniGPT2(cfg)
+    m.load_state_dict(ck["model_state"])
+    stoi, itos = ck["stoi"], {int(k): v for k, v in ck["itos"].items()}
+    x = torch.tensor([[stoi.get(ch, 0) for ch in a.prompt]])
+    logits = m(torch.nn.functional.pad(x, (cfg.seq_len - x.shape[1], 0))[:, -cfg.seq_len:])
+    assert logits.shape == (1, cfg.seq_len, cfg.vocab_size), "output shape test"
+    out = generate_simple(m, x, a.max_new, cfg.seq_len, temperature=0.8, pad_left_to=cfg.seq_len)
+    print("".join(itos.get(int(i), "?") for i in out[0]))
+
+
+# ============================================================================ tracks B-D
+def _lm_corpus(a):
+    from ..train.data import (ByteBlocksDataset, ByteTokenizer, TokenBlockDataset, load_text_corpus,
+                              train_bpe_tokenizer)
+    texts = load_text_corpus(a.data) if a.data else [DEMO_TEXT * 40]
+    if a.tokenizer == "byte":
+        tok = ByteTokenizer()
+        return ByteBlocksDataset(texts, a.block_size), tok
+    if a.tokenizer.startswith("hf:"):
+        from ..train.data import load_tokenizer
+        tok = load_tokenizer(a.tokenizer[3:])
+    else:
+        tok = train_bpe_tokenizer(texts, a.vocab_size, "bytelevel" if a.tokenizer == "bpe-bytelevel" else "whitespace",
+                                  save_path=os.path.join(a.save_dir or ".", "tokenizer.json"))
+    ids = []
+    for t in texts:
+        ids.extend(tok.encode(t))
+    return TokenBlockDataset(ids, a.block_size), tok
+
+
+def _build_lm(a, vocab):
+    from ..models.deepseeklike import DeepSeekLike
+    from ..models.gptlike import GPTLike, SimpleTransformer
+    if a.model == "simple":
+        return SimpleTransformer(vocab, a.d_model, a.n_head, a.n_layer, a.block_size, a.dropout)
+    if a.model.startswith("deepseek"):
+        return DeepSeekLike(vocab, a.block_size, a.n_layer, a.n_head, a.d_model, a.dropout, a.latent_dim,
+                            a.num_experts, a.top_k, a.num_shared, a.rope_theta,
+                            moe_dispatch="dense" if a.model == "deepseek-dense" else "sparse")
+    return GPTLike(vocab, a.block_size, a.n_layer, a.n_head, a.d_model, a.dropout,
+                   pos="learned" if a.pe == "learned" else "sinusoidal")
+
+
+def cmd_lm_train(a, strategy="single"):
+    from ..parallel import dist as D
+    from ..train.loops import LoopConfig, train_lm
+    if strategy != "single":
+        D.init_distributed(timeout_s=a.timeout)
+    ds, tok = _lm_corpus(a)
+    vocab = getattr(tok, "vocab_size", 256)
+    torch.manual_seed(a.seed)
+    m = _build_lm(a, vocab).to(_device())
+    cfg = LoopConfig(epochs=a.epochs, batch_size=a.batch_size, lr=a.lr, weight_decay=a.weight_decay,
+                     clip_grad_norm=a.clip_grad_norm, strategy=strategy, ds_config=a.ds_config,
+                     precision=a.precision, scheduler=a.scheduler, step_per_batch=a.step_per_batch,
+                     save_dir=a.save_dir, keep_last=a.keep_last, final_model=a.final_model, seed=a.seed,
+                     max_steps=a.max_steps, grad_accum=a.grad_accum)
+    hist = train_lm(m, ds, cfg, meta={"vocab_size": vocab, "block_size": a.block_size})
+    if D.is_main():
+        print(json.dumps({"train_loss": hist["train_loss"], "strategy": strategy}))
+    if strategy != "single":
+        D.destroy()
+
+
+# ============================================================================ track E
+def _load_base(a, preset, device):
+    from ..models.qwen3 import BitsAndBytesConfig, Qwen3ForCausalLM, qwen3_config
+    qc = BitsAndBytesConfig(load_in_4bit=True, bnb_4bit_quant_type="nf4", bnb_4bit_use_double_quant=True,
+                            bnb_4bit_compute_dtype=torch.bfloat16) if preset.quant == "nf4" else None
+    if a.random_init or not a.model_path:
+        m = Qwen3ForCausalLM.from_config(qwen3_config(a.random_init or preset.model), dtype=torch.bfloat16,
+                                         device=device)
+        if qc is not None:
+            from ..peft.lora import quantize_model_nf4
+            quantize_model_nf4(m)
+        return m
+    return Qwen3ForCausalLM.from_pretrained(a.model_path, dtype=torch.bfloat16, device=device, quantization_config=qc,
+                                            rope_scaling=None if preset.rope_scaling == "none" else "keep")
+
+
+def cmd_finetune(a):
+    from ..cli.recipes import PRESETS
+    from ..parallel import dist as D
+    from ..peft.lora import LoraConfig, get_peft_model, prepare_model_for_kbit_training
+    from ..train.data import (ByteTokenizer, DataCollatorForLanguageModeling, SFTDataset, SyntheticLMDataset,
+                              load_records, load_tokenizer, synthetic_self_cognition)
+    from ..train.trainer import Trainer, TrainingArguments
+    p = PRESETS[a.preset]
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        D.init_distributed(timeout_s=1800)
+    dev = _device()
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    model = _load_base(a, p, dev)
+    if p.quant:
+        model = prepare_model_for_kbit_training(model, use_gradient_checkpointing=p.grad_ckpt and not a.no_grad_ckpt)
+    elif p.grad_ckpt and not a.no_grad_ckpt:
+        model.gradient_checkpointing_enable()
+    model = get_peft_model(model, LoraConfig(r=p.lora_r, lora_alpha=p.lora_alpha, lora_dropout=p.lora_dropout,
+                                             target_modules=list(p.targets), task_type="CAUSAL_LM"))
+    if D.is_main():
+        model.print_trainable_parameters()
+    if not (p.grad_ckpt and not a.no_grad_ckpt):
+        model.fuse_projections()
+    tok = load_tokenizer(a.tokenizer or a.model_path, pad_to_eos=p.pad_to_eos) if (a.tokenizer or a.model_path) \
+        else None
+    if tok is not None:
+        recs = load_records(a.data) if a.data else synthetic_self_cognition()
+        train_ds = SFTDataset(recs, tok, p.max_length, p.padding, label_mode=a.label_mode, system=p.system,
+                              space_before_end=p.space_before_end)
+        collator = DataCollatorForLanguageModeling(tok, mlm=False) if a.label_mode == "reference" else None
+    else:                                        # no tokenizer available offline: synthetic ids at the preset shape
+        vocab = model.config.vocab_size
+        train_ds = SyntheticLMDataset(vocab, p.max_length, a.synthetic_samples)
+        collator = None
+    ds = p.deepspeed if not a.no_deepspeed else None
+    if ds and not os.path.exists(ds):            # bundled configs/ next to the package
+        ds = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), ds)
+    args = TrainingArguments(
+        output_dir=a.output_dir or p.output_dir, per_device_train_batch_size=p.per_device_batch,
+        gradient_accumulation_steps=p.grad_accum, num_train_epochs=a.epochs or p.epochs, max_steps=a.max_steps,
+        learning_rate=p.lr, weight_decay=p.weight_decay, logging_steps=p.logging_steps, save_steps=p.save_steps,
+        save_total_limit=p.save_total_limit, bf16=True, optim=p.optim, report_to=[], remove_unused_columns=False,
+        deepspeed=ds, ddp_timeout=1800,
+        gradient_checkpointing=p.grad_ckpt and not a.no_grad_ckpt, metrics_jsonl=a.metrics_jsonl)
+    tr = Trainer(model, args, train_dataset=train_ds, data_collator=collator, tokenizer=tok)
+    try:
+        out = tr.train(resume_from_checkpoint=a.resume)
+    except Exception:
+        d = tr.save_interrupted()                # reference: qwen3-8b-lora.py:190-204
+        print(f"training interrupted; adapter saved to {d}", file=sys.stderr)
+        raise
+    tr.save_model(args.output_dir)
+    tr.log_metrics("train", out.metrics)
+    tr.save_metrics("train", out.metrics)
+    tr.save_state()
+
+
+# ============================================================================ inference / quant
+def _load_for_inference(path, adapter=None, device=None, quant=None):
+    from ..models.qwen3 import BitsAndBytesConfig, Qwen3ForCausalLM, qwen3_config
+    dev = device or _device()
+    if path.startswith("random:"):
+        m = Qwen3ForCausalLM.from_config(qwen3_config(path[7:]), dtype=torch.bfloat16, device=dev)
+    else:
+        with open(os.path.join(path, "config.json")) as f:
+            qc = json.load(f).get("quantization_config")
+        if qc and qc.get("quant_method") in ("compressed-tensors", "gptq", "awq"):
+            from ..quant.io import load_quantized
+            m = load_quantized(path, dev)
+        else:
+            bnb = BitsAndBytesConfig(load_in_4bit=True) if quant == "nf4" else None
+            m = Qwen3ForCausalLM.from_pretrained(path, dtype=torch.bfloat16, device=dev, quantization_config=bnb)
+    if adapter:
+        from ..peft.lora import PeftModel
+        m = PeftModel.from_pretrained(m, adapter)
+    return m.eval()
+
+
+def cmd_chat(a):
+    from ..infer.engine import SamplingParams, ServingEngine
+    from ..train.data import load_tokenizer
+    m = _load_for_inference(a.base, a.adapter, quant=a.quant)
+    tok = load_tokenizer(a.tokenizer or a.base)
+    eng = ServingEngine(m, tok, system_prompt=a.system, space_before_end=True)
+    history = []                                  # multi-turn (inferences.py:77-83, 04-*-multisession*.py)
+    params = SamplingParams(max_tokens=a.max_new, temperature=a.temperature, top_p=a.top_p)
+    while True:
+        try:
+            q = input("user> ").strip()
+        except EOFError:
+            break
+        if q in ("exit", "quit"):
+            break
+        if q == "clear":
+            history = []
+            continue
+        history.append({"role": "user", "content": q})
+        prompt = eng.build_chat_prompt(history)
+        print("assistant> ", end="", flush=True)
+        text = ""
+        for delta, final in eng.stream(prompt, params):
+            print(delta, end="", flush=True)
+            text += delta
+        print()
+        history.append({"role": "assistant", "content": text})
+
+
+def cmd_infer(a):
+    from ..infer.generate import generate
+    from ..train.data import load_tokenizer, render_chatml
+    m = _load_for_inference(a.model, a.adapter, quant=a.quant)
+    tok = load_tokenizer(a.tokenizer or a.model)
+    text = render_chatml([{"role": "user", "content": a.prompt}], add_generation_prompt=True) if a.chat else a.prompt
+    ids = torch.tensor([tok.encode(text, add_special_tokens=False)], device=_device())
+    out = generate(m, ids, max_new_tokens=a.max_new, do_sample=a.temperature > 0, temperature=a.temperature,
+                   top_p=a.top_p, repetition_penalty=a.repetition_penalty, eos_token_id=tok.eos_token_id)
+    print(tok.decode(out[0, ids.shape[1]:].tolist(), skip_special_tokens=True))
+
+
+def cmd_merge(a):
+    from ..peft.lora import PeftModel
+    from ..models.qwen3 import Qwen3ForCausalLM
+    base = Qwen3ForCausalLM.from_pretrained(a.base, dtype=torch.bfloat16, device=_device(a.device))
+    merged = PeftModel.from_pretrained(base, a.adapter).merge_and_unload()
+    merged.save_pretrained(a.out)
+    if a.tokenizer or os.path.exists(os.path.join(a.base, "tokenizer.json")):
+        from ..train.data import load_tokenizer
+        load_tokenizer(a.tokenizer or a.base).save_pretrained(a.out)
+    print(json.dumps({"merged": a.out}))
+
+
+def _calib_ids(a, tok, vocab, device):
+    if a.calib and tok is not None:
+        from ..train.data import load_text_corpus
+        texts = load_text_corpus(a.calib)[:a.n_calib]
+        return [torch.tensor([tok.encode(t)[:a.calib_len]], device=device) for t in texts if t.strip()]
+    g = torch.Generator().manual_seed(0)
+    return [torch.randint(0, vocab, (1, a.calib_len), generator=g).to(device) for _ in range(a.n_calib)]
+
+
+def cmd_quantize(a):
+    from ..quant.awq import awq_quantize_model
+    from ..quant.gptq import gptq_quantize_model, replace_with_int4
+    from ..quant.int4 import quantize_rtn
+    from ..quant.io import save_quantized
+    dev = _device(a.device)
+    m = _load_for_inference(a.model, device=dev)
+    tok = None
+    if not a.model.startswith("random:"):
+        try:
+            from ..train.data import load_tokenizer
+            tok = load_tokenizer(a.tokenizer or a.model)
+        except Exception:
+            tok = None
+    calib = _calib_ids(a, tok, m.config.vocab_size, dev)
+    if a.method == "gptq":
+        gptq_quantize_model(m, calib, a.group_size, a.sym)
+    elif a.method == "awq":
+        awq_quantize_model(m, calib, a.group_size)
+    else:
+        ws = {}
+        for n, mod in m.named_modules():
+            if isinstance(mod, torch.nn.Linear) and n.startswith("model.layers"):
+                ws[n] = quantize_rtn(mod.weight.detach(), a.group_size, a.sym)
+        replace_with_int4(m, ws)
+    save_quantized(m, a.out, a.format, tok)
+    print(json.dumps({"quantized": a.out, "method": a.method, "format": a.format}))
+
+
+def cmd_eval_quant(a):
+    from ..quant.eval import PASS_THRESHOLD, self_ppl
+    from ..train.data import load_text_corpus, load_tokenizer
+    dev = _device()
+    m = _load_for_inference(a.model, device=dev)
+    tok = load_tokenizer(a.tokenizer or a.model) if not a.model.startswith("random:") else None
+    if a.prompts and tok is not None:
+        prompts = [torch.tensor(tok.encode(t)[:256], device=dev) for t in load_text_corpus(a.prompts)[a.start:a.end]]
+    else:
+        prompts = [torch.randint(0, m.config.vocab_size, (32,), device=dev) for _ in range(a.end - a.start)]
+    ppl = self_ppl(m, prompts, a.max_new, getattr(tok, "eos_token_id", None))
+    print(json.dumps({"self_ppl": ppl, "pass": ppl < PASS_THRESHOLD, "threshold": PASS_THRESHOLD}))
+
+
+def cmd_serve(a):
+    from ..infer.engine import ServingEngine
+    from ..infer.server import serve
+    from ..train.data import load_tokenizer
+    m = _load_for_inference(a.model, a.adapter, quant=a.quant)
+    tok = load_tokenizer(a.tokenizer or a.model)
+    moderation = None
+    if a.guard_url:
+        from ..infer.guard import GuardClient
+        moderation = GuardClient(a.guard_url).moderate_sync
+    eng = ServingEngine(m, tok, model_name=a.served_model_name or os.path.basename(a.model.rstrip("/")),
+                        max_batch=a.max_batch, system_prompt=a.system)
+    serve(eng, a.host, a.port, api_key=a.api_key, moderation=moderation)
+
+
+def cmd_guard(a):
+    import uvicorn
+    from ..infer.guard import GuardClient, create_guard_app
+    uvicorn.run(create_guard_app(GuardClient(a.backend, a.model), a.api_key), host=a.host, port=a.port)
+
+
+def cmd_convert_alpaca(a):
+    from ..train.data import load_records, replace_placeholders
+    recs = [replace_placeholders(r, a.name, a.author) for r in load_records(a.input)]
+    out = [{"instruction": r["query"], "input": "", "output": r["response"]} for r in recs]
+    with open(a.out, "w") as f:
+        json.dump(out, f, ensure_ascii=False, indent=2)
+    print(json.dumps({"records": len(out), "out": a.out}))
+
+
+def cmd_bench(a):
+    import subprocess
+    here = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.exit(subprocess.call([sys.executable, os.path.join(here, "bench.py")] + a.rest))
+
+
+# ============================================================================ parser
+def _lm_args(p):
+    p.add_argument("--model", default="gptlike", choices=["simple", "gptlike", "deepseek", "deepseek-dense"])
+    p.add_argument("--pe", default="fixed", choices=["fixed", "learned"])
+    p.add_argument("--data", help="local text corpus (.txt/.jsonl/.parquet); default: built-in demo text")
+    p.add_argument("--tokenizer", default="bpe-whitespace",
+                   help="bpe-whitespace | bpe-bytelevel | byte | hf:<local dir> (e.g. a bert-base-uncased dir)")
+    p.add_argument("--vocab_size", type=int, default=3000)
+    p.add_argument("--epochs", type=int, default=3)
+    p.add_argument("--batch_size", type=int, default=16)
+    p.add_argument("--block_size", type=int, default=256)
+    p.add_argument("--lr", type=float, default=3e-4)
+    p.add_argument("--weight_decay", type=float, default=0.01)
+    p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--n_layer", type=int, default=6)
+    p.add_argument("--n_head", type=int, default=8)
+    p.add_argument("--d_model", type=int, default=768)
+    p.add_argument("--dropout", type=float, default=0.1)
+    p.add_argument("--clip_grad_norm", type=float, default=1.0)
+    p.add_argument("--save_dir", default=None)
+    p.add_argument("--keep_last", type=int, default=5)
+    p.add_argument("--final_model", default=None)
+    p.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "fp16"])
+    p.add_argument("--scheduler", default="none", choices=["none", "step", "cosine"])
+    p.add_argument("--step_per_batch", action="store_true", help="reproduce the per-batch StepLR of B2/B4/B6")
+    p.add_argument("--max_steps", type=int, default=-1)
+    p.add_argument("--grad_accum", type=int, default=1)
+    p.add_argument("--latent_dim", type=int, default=None)
+    p.add_argument("--num_experts", type=int, default=8)
+    p.add_argument("--top_k", type=int, default=2)
+    p.add_argument("--num_shared", type=int, default=2)
+    p.add_argument("--rope_theta", type=float, default=10000.0)
+    p.add_argument("--ds_config", default=None)
+    p.add_argument("--timeout", type=int, default=1800)
+    p.add_argument("--local_rank", type=int, default=None)
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="lipa", description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    sub = ap.add_subparsers(dest="cmd", required=True)
+
+    p = sub.add_parser("minigpt-train")
+    p.add_argument("--text")
+    p.add_argument("--epochs", type=int, default=200)
+    p.add_argument("--batch_size", type=int, default=4)
+    p.add_argument("--lr", type=float, default=1e-3)
+    p.add_argument("--seq_len", type=int, default=16)
+    p.add_argument("--repeat", type=int, default=10)
+    p.add_argument("--embed_dim", type=int, default=64)
+    p.add_argument("--n_heads", type=int, default=2)
+    p.add_argument("--n_layers", type=int, default=2)
+    p.add_argument("--causal", action="store_true", help="fix the reference's missing causal mask")
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--device", default="cpu")
+    p.add_argument("--out", default="mg_edu_gpt.pth")
+    p.set_defaults(fn=cmd_minigpt_train)
+    p = sub.add_parser("minigpt-generate")
+    p.add_argument("--checkpoint", default="mg_edu_gpt.pth")
+    p.add_argument("--prompt", default="马哥")
+    p.add_argument("--max_new", type=int, default=50)
+    p.add_argument("--temperature", type=float, default=0.0)
+    p.set_defaults(fn=cmd_minigpt_generate)
+    p = sub.add_parser("minigpt2-train")
+    p.add_argument("--text")
+    p.add_argument("--epochs", type=int, default=200)
+    p.add_argument("--seq_len", type=int, default=256)
+    p.add_argument("--device", default="cpu")
+    p.add_argument("--out", default="minigpt_model.pth")
+    p.set_defaults(fn=cmd_minigpt2_train)
+    p = sub.add_parser("minigpt2-test")
+    p.add_argument("--checkpoint", default="minigpt_model.pth")
+    p.add_argument("--prompt", default="马哥")
+    p.add_argument("--max_new", type=int, default=50)
+    p.set_defaults(fn=cmd_minigpt2_test)
+
+    p = sub.add_parser("lm-train")
+    _lm_args(p)
+    p.set_defaults(fn=lambda a: cmd_lm_train(a, "single"))
+    p = sub.add_parser("pretrain")
+    _lm_args(p)
+    p.add_argument("--strategy", default="ddp",
+                   choices=["ddp", "fsdp", "fsdp2", "zero1", "zero2", "zero3", "zero-offload"])
+    p.set_defaults(fn=lambda a: cmd_lm_train(a, a.strategy))
+
+    from .recipes import PRESETS
+    p = sub.add_parser("finetune")
+    p.add_argument("--preset", required=True, choices=sorted(PRESETS))
+    p.add_argument("--model-path", dest="model_path")
+    p.add_argument("--tokenizer")
+    p.add_argument("--data", help="self-cognition JSONL (query/response with {{NAME}}/{{AUTHOR}})")
+    p.add_argument("--random-init", dest="random_init", help="Qwen3 preset name: random weights, no checkpoint")
+    p.add_argument("--output-dir", dest="output_dir")
+    p.add_argument("--epochs", type=float, default=None)
+    p.add_argument("--max-steps", dest="max_steps", type=int, default=-1)
+    p.add_argument("--label-mode", dest="label_mode", default="reference", choices=["reference", "assistant", "none"])
+    p.add_argument("--no-grad-ckpt", dest="no_grad_ckpt", action="store_true")
+    p.add_argument("--no-deepspeed", dest="no_deepspeed", action="store_true")
+    p.add_argument("--resume", default=None)
+    p.add_argument("--metrics-jsonl", dest="metrics_jsonl")
+    p.add_argument("--synthetic-samples", dest="synthetic_samples", type=int, default=108)
+    p.set_defaults(fn=cmd_finetune)
+
+    for name, fn in (("chat", cmd_chat), ("infer", cmd_infer)):
+        p = sub.add_parser(name)
+        p.add_argument("--base" if name == "chat" else "--model", required=True)
+        p.add_argument("--adapter")
+        p.add_argument("--tokenizer")
+        p.add_argument("--quant", choices=["nf4"])
+        p.add_argument("--max_new", type=int, default=256)
+        p.add_argument("--temperature", type=float, default=0.7)
+        p.add_argument("--top_p", type=float, default=0.9)
+        if name == "chat":
+            p.add_argument("--system", default=None)
+        else:
+            p.add_argument("--prompt", required=True)
+            p.add_argument("--chat", action="store_true")
+            p.add_argument("--repetition_penalty", type=float, default=1.0)
+        p.set_defaults(fn=fn)
+
+    p = sub.add_parser("merge")
+    p.add_argument("--base", required=True)
+    p.add_argument("--adapter", required=True)
+    p.add_argument("--out", required=True)
+    p.add_argument("--tokenizer")
+    p.add_argument("--device", default=None)
+    p.set_defaults(fn=cmd_merge)
+
+    p = sub.add_parser("quantize")
+    p.add_argument("--method", default="awq", choices=["awq", "gptq", "rtn"])
+    p.add_argument("--model", required=True, help="HF dir or random:<qwen3 preset>")
+    p.add_argument("--out", required=True)
+    p.add_argument("--format", default="compressed-tensors", choices=["compressed-tensors", "gptq", "awq"])
+    p.add_argument("--group_size", type=int, default=128)
+    p.add_argument("--sym", action="store_true")
+    p.add_argument("--calib", help="local calibration corpus (Alpaca-style texts)")
+    p.add_argument("--n_calib", type=int, default=128)
+    p.add_argument("--calib_len", type=int, default=2048)
+    p.add_argument("--tokenizer")
+    p.add_argument("--device", default=None)
+    p.set_defaults(fn=cmd_quantize)
+
+    p = sub.add_parser("eval-quant")
+    p.add_argument("--model", required=True)
+    p.add_argument("--tokenizer")
+    p.add_argument("--prompts")
+    p.add_argument("--start", type=int, default=128)
+    p.add_argument("--end", type=int, default=256)
+    p.add_argument("--max_new", type=int, default=256)
+    p.set_defaults(fn=cmd_eval_quant)
+
+    p = sub.add_parser("serve")
+    p.add_argument("--model", required=True)
+    p.add_argument("--adapter")
+    p.add_argument("--tokenizer")
+    p.add_argument("--quant", choices=["nf4"])
+    p.add_argument("--host", default="0.0.0.0")
+    p.add_argument("--port", type=int, default=8000)
+    p.add_argument("--max-batch", dest="max_batch", type=int, default=32)
+    p.add_argument("--served-model-name", dest="served_model_name")
+    p.add_argument("--api-key", dest="api_key")
+    p.add_argument("--guard-url", dest="guard_url")
+    p.add_argument("--system", default=None)
+    p.set_defaults(fn=cmd_serve)
+
+    p = sub.add_parser("guard")
+    p.add_argument("--backend", required=True, help="guard model completions URL")
+    p.add_argument("--model", default="llama-guard-3")
+    p.add_argument("--host", default="0.0.0.0")
+    p.add_argument("--port", type=int, default=8099)
+    p.add_argument("--api-key", dest="api_key", default=None)
+    p.set_defaults(fn=cmd_guard)
+
+    p = sub.add_parser("convert-alpaca")
+    p.add_argument("--input", required=True)
+    p.add_argument("--out", required=True)
+    p.add_argument("--name", default="马哥教育AI小助手")
+    p.add_argument("--author", default="马哥教育AI团队")
+    p.set_defaults(fn=cmd_convert_alpaca)
+
+    p = sub.add_parser("bench")
+    p.add_argument("rest", nargs=argparse.REMAINDER)
+    p.set_defaults(fn=cmd_bench)
+    return ap
+
+
+def main(argv=None):
+    a = build_parser().parse_args(argv)
+    a.fn(a)
+
+
+if __name__ == "__main__":
+    main()

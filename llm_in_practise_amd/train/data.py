@@ -228,7 +228,7 @@ class ByteBlocksDataset(TokenBlockDataset):
         data = bytearray()
         for t in texts:
             data.extend(t.encode("utf-8"))
-        super().__init__(torch.frombuffer(bytes(data), dtype=torch.uint8).long(), block_size)
+        super().__init__(torch.tensor(list(data), dtype=torch.long), block_size)
 
 
 class SyntheticLMDataset(Dataset):

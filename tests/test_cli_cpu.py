@@ -1,0 +1,92 @@
+"""CLI smoke tests (CPU): every track's entry point runs end to end on tiny configs."""
+import json
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from llm_in_practise_amd.cli.main import main
+
+
+def test_minigpt_train_and_generate(tmp_path, capsys):
+    ck = str(tmp_path / "mg.pth")
+    main(["minigpt-train", "--epochs", "30", "--out", ck])
+    first = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert first["final_loss"] < 1.0
+    ckd = torch.load(ck, weights_only=True)
+    assert set(ckd) == {"model_state", "char2idx", "config"}
+    main(["minigpt-generate", "--checkpoint", ck, "--max_new", "10"])
+    assert capsys.readouterr().out.startswith("马哥")
+
+
+def test_minigpt2_train_and_test(tmp_path, capsys):
+    ck = str(tmp_path / "m2.pth")
+    main(["minigpt2-train", "--epochs", "2", "--out", ck])
+    capsys.readouterr()
+    main(["minigpt2-test", "--checkpoint", ck, "--max_new", "5"])
+    assert len(capsys.readouterr().out.strip()) >= 2
+
+
+@pytest.mark.parametrize("model", ["gptlike", "deepseek", "simple"])
+def test_lm_train(tmp_path, capsys, model):
+    main(["lm-train", "--model", model, "--tokenizer", "byte", "--block_size", "32", "--n_layer", "1",
+          "--d_model", "64", "--n_head", "4", "--batch_size", "4", "--epochs", "1", "--max_steps", "3",
+          "--save_dir", str(tmp_path / "ck"), "--scheduler", "step", "--step_per_batch"])
+    out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert out["train_loss"][0] > 0
+    ck = torch.load(tmp_path / "ck" / "model_epoch_1.pth", weights_only=True)
+    assert {"epoch", "model_state_dict", "optimizer_state_dict", "vocab_size", "block_size"} <= set(ck)
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _pretrain_worker(rank, world, port, strategy, d):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    main(["pretrain", "--strategy", strategy, "--tokenizer", "byte", "--block_size", "32", "--n_layer", "2",
+          "--d_model", "64", "--n_head", "4", "--batch_size", "2", "--epochs", "1", "--max_steps", "2",
+          "--save_dir", d, "--final_model", os.path.join(d, "final_model.pth")])
+
+
+@pytest.mark.parametrize("strategy", ["ddp", "zero2", "fsdp"])
+def test_pretrain_strategies_world2(tmp_path, strategy):
+    d = str(tmp_path / strategy)
+    mp.spawn(_pretrain_worker, args=(2, _port(), strategy, d), nprocs=2, join=True)
+    assert os.path.exists(os.path.join(d, "final_model.pth"))
+    if strategy != "ddp":
+        assert os.path.exists(os.path.join(d, "latest"))
+
+
+def test_finetune_random_init_qlora(tmp_path):
+    out = str(tmp_path / "ft")
+    main(["finetune", "--preset", "qwen3-8b-qlora-dist", "--random-init", "qwen3-tiny", "--max-steps", "2",
+          "--output-dir", out, "--synthetic-samples", "8", "--no-grad-ckpt"])
+    assert os.path.exists(os.path.join(out, "adapter_model.safetensors"))
+    assert os.path.exists(os.path.join(out, "train_results.json"))
+
+
+def test_quantize_and_eval_cli(tmp_path, capsys):
+    out = str(tmp_path / "q")
+    main(["quantize", "--method", "awq", "--model", "random:qwen3-tiny", "--out", out, "--n_calib", "2",
+          "--calib_len", "32"])
+    assert json.load(open(os.path.join(out, "config.json")))["quantization_config"]["quant_method"] == \
+        "compressed-tensors"
+    capsys.readouterr()
+    main(["eval-quant", "--model", out, "--start", "0", "--end", "2", "--max_new", "6"])
+    r = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert r["self_ppl"] > 1
+
+
+def test_convert_alpaca(tmp_path):
+    src = tmp_path / "sc.jsonl"
+    src.write_text(json.dumps({"query": "你是谁?", "response": "我是{{NAME}}，由{{AUTHOR}}开发。"}, ensure_ascii=False))
+    out = tmp_path / "a.json"
+    main(["convert-alpaca", "--input", str(src), "--out", str(out)])
+    d = json.load(open(out))
+    assert d[0]["instruction"] == "你是谁?" and "马哥教育AI小助手" in d[0]["output"]
