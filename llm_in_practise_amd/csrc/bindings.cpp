@@ -53,6 +53,11 @@ void launch_gemm_int4(const void*, int, const uint32_t*, const float*, const flo
                       const void*, void*, int, int, int, hipStream_t);
 void launch_gemv_w4(int, const void*, int, const uint8_t*, const float*, const float*, int, const void*, void*, int, int,
                     int, hipStream_t);
+void launch_lora_proj(const void*, int, const void*, int, int, float*, int, void*, int, int, uint64_t, float, float,
+                      size_t, hipStream_t);
+int lora_acc_chunks(int M);
+void launch_lora_acc(const float*, int, int, const void*, int, void*, int, const void*, int, float*, int64_t, int64_t,
+                     float*, int, uint64_t, float, size_t, hipStream_t);
 void launch_decode_attention(const void*, const void*, const void*, const int*, float*, float*, float*, void*, int, int,
                              int, int, int, int, float, hipStream_t);
 int decode_chunk();
@@ -470,6 +475,73 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o
   return {dq, dk, dv};
 }
 
+// ------------------------------------------------------------------ fused LoRA branch kernels
+// out = scale·D(x)·Wᵀ over x[:, c0:c0+K] (row stride = x.stride(0)); writes bf16 into outb (a column
+// slice view, any row stride) and/or returns fp32 [M, r].
+Tensor lora_proj(Tensor x, int64_t c0, int64_t K, Tensor w, optional<Tensor> outb, bool want_f32, double p,
+                 int64_t key, double scale) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && c0 % 8 == 0, "lora_proj: x layout");
+  TORCH_CHECK(w.is_contiguous() && w.size(1) == K && w.size(0) <= 16 && K % 32 == 0, "lora_proj: w [r<=16, K%32]");
+  const int M = x.size(0), r = w.size(0);
+  Tensor of;
+  if (want_f32) of = at::empty({M, r}, x.options().dtype(at::kFloat));
+  void* ob = nullptr;
+  int ldob = 0;
+  if (outb) {
+    TORCH_CHECK(outb->scalar_type() == at::kBFloat16 && outb->stride(1) == 1 && outb->size(0) == M &&
+                    outb->size(1) == r, "lora_proj: outb");
+    ob = outb->data_ptr();
+    ldob = outb->stride(0);
+  }
+  TORCH_CHECK(ob || want_f32, "lora_proj: no output");
+  launch_lora_proj((const char*)x.data_ptr() + c0 * 2, x.stride(0), w.data_ptr(), r, K,
+                   want_f32 ? of.data_ptr<float>() : nullptr, r, ob, ldob, M, (uint64_t)key, (float)p, (float)scale,
+                   (size_t)x.stride(0), stream());
+  return want_f32 ? of : Tensor();
+}
+
+// out (fp32, 2-D, [r, K] or its transpose view [K, r]) += gᵀ·D(x[:, c0:c0+K]); with dx: dx += D(g·w)
+void lora_acc(Tensor g, Tensor x, int64_t c0, int64_t K, Tensor out, bool out_transposed, optional<Tensor> dx,
+              optional<Tensor> w, double p, int64_t key, bool deterministic) {
+  TORCH_CHECK(g.scalar_type() == at::kFloat && g.dim() == 2 && g.stride(1) == 1 && g.size(1) <= 16, "lora_acc: g");
+  CHECK_BF16(x);
+  TORCH_CHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && c0 % 8 == 0 && K % 8 == 0, "lora_acc: x layout");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.dim() == 2, "lora_acc: out fp32 2-D");
+  const int M = x.size(0), r = g.size(1);
+  int64_t sj, sk;
+  if (out_transposed) {
+    TORCH_CHECK(out.size(0) == K && out.size(1) == r, "lora_acc: out [K, r]");
+    sj = out.stride(1);
+    sk = out.stride(0);
+  } else {
+    TORCH_CHECK(out.size(0) == r && out.size(1) == K, "lora_acc: out [r, K]");
+    sj = out.stride(0);
+    sk = out.stride(1);
+  }
+  void* dxp = nullptr;
+  int lddx = 0;
+  if (dx) {
+    TORCH_CHECK(w.has_value() && w->is_contiguous() && w->size(0) == r && w->size(1) == K, "lora_acc: w");
+    TORCH_CHECK(dx->scalar_type() == at::kBFloat16 && dx->stride(1) == 1 && dx->size(0) == M && dx->size(1) == K,
+                "lora_acc: dx");
+    dxp = dx->data_ptr();
+    lddx = dx->stride(0);
+  }
+  Tensor part;
+  if (deterministic) part = at::empty({lora_acc_chunks(M), r, K}, g.options());
+  launch_lora_acc(g.data_ptr<float>(), g.stride(0), r, (const char*)x.data_ptr() + c0 * 2, x.stride(0), dxp, lddx,
+                  dx ? w->data_ptr() : nullptr, K, out.data_ptr<float>(), sj, sk,
+                  deterministic ? part.data_ptr<float>() : nullptr, M, (uint64_t)key, (float)p,
+                  (size_t)x.stride(0), stream());
+  if (deterministic) {
+    Tensor s = part.sum(0);
+    if (out_transposed) out.add_(s.t());
+    else out.add_(s);
+  }
+}
+
 // ------------------------------------------------------------------ generation (K16, K17)
 // q [B, hq*d] bf16; kc/vc [B, Smax, hkv*d] bf16 contiguous; lens [B] int32 (valid keys per row);
 // max_len >= max(lens) bounds the split count without a host sync.
@@ -540,6 +612,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_norm", &grad_norm);
   m.def("set_gemm_impl", &set_gemm_impl);
   m.def("decode_attention", &decode_attention);
+  m.def("lora_proj", &lora_proj);
+  m.def("lora_acc", &lora_acc);
   m.def("gemm_int4", &gemm_int4);
   m.def("gemv_w4", &gemv_w4);
   m.def("sample", &sample);

@@ -90,6 +90,25 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
 
+// Counter-based dropout mask shared by every kernel that applies or regenerates the LoRA input
+// dropout (dropout.hip, lora.hip): 8 keep flags for elements [8v, 8v+8) of the row-major tensor,
+// a pure function of (key, v) — masks are never stored.
+__device__ __forceinline__ uint64_t splitmix_fin(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint32_t dropout_keep8(uint64_t key, size_t v, uint32_t thr16) {
+  const uint64_t h0 = splitmix_fin(key + 2 * v), h1 = splitmix_fin(key + 2 * v + 1);
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    m |= (uint32_t)(((h0 >> (16 * i)) & 0xFFFF) >= thr16) << i;
+    m |= (uint32_t)(((h1 >> (16 * i)) & 0xFFFF) >= thr16) << (i + 4);
+  }
+  return m;
+}
+
 }  // namespace lipa
 
 #define LIPA_CHECK_LAUNCH()                                                              \

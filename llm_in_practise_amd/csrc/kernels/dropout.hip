@@ -11,22 +11,8 @@ using namespace lipa;
 
 namespace {
 
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
-// 8 keep flags for elements [8v, 8v+8)
 __device__ __forceinline__ uint32_t keep8(uint64_t key, size_t v, uint32_t thr16) {
-  const uint64_t h0 = mix64(key + 2 * v), h1 = mix64(key + 2 * v + 1);
-  uint32_t m = 0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    m |= (uint32_t)(((h0 >> (16 * i)) & 0xFFFF) >= thr16) << i;
-    m |= (uint32_t)(((h1 >> (16 * i)) & 0xFFFF) >= thr16) << (i + 4);
-  }
-  return m;
+  return dropout_keep8(key, v, thr16);
 }
 
 __global__ __launch_bounds__(256) void dropout_fwd_k(const bf16* __restrict__ x, bf16* __restrict__ y, size_t n,

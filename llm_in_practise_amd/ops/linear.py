@@ -104,6 +104,20 @@ def bf16_view(p: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
     return p.detach().to(dtype)
 
 
+def deterministic() -> bool:
+    """Bit-reproducible LoRA gradients (``LIPA_DETERMINISTIC=1`` or
+    ``torch.use_deterministic_algorithms(True)``): fixed-order partial sums instead of fp32
+    atomics in the fused LoRA backward (≈0.5 % slower)."""
+    import os
+    return os.environ.get("LIPA_DETERMINISTIC", "0") == "1" or torch.are_deterministic_algorithms_enabled()
+
+
+def _fast_lora_ok(x, branches) -> bool:
+    """Shapes the fused LoRA branch kernels (csrc/kernels/lora.hip) take."""
+    K = x.shape[1]
+    return (K % 128 == 0 and all(br.a.shape[0] <= 16 and (br.c1 - br.c0) % 128 == 0 for br in branches))
+
+
 class _FusedLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, meta, *ab):
@@ -111,32 +125,42 @@ class _FusedLinearFn(torch.autograd.Function):
         dense = not isinstance(base, NF4Weight)
         xa_list, keys = [], []
         ext_a = ext_b = None
+        fast = bool(branches) and _fast_lora_ok(x, branches)
+        need_xa = any(ctx.needs_input_grad[5:])     # (grad mode is off inside forward: ask autograd)
         if branches:
             N = base.shape[0]
             rtot = sum(br.a.shape[0] for br in branches)
-            ext_b = x.new_zeros(N, (rtot + EXT_ALIGN - 1) // EXT_ALIGN * EXT_ALIGN)
+            rp = (rtot + EXT_ALIGN - 1) // EXT_ALIGN * EXT_ALIGN
+            ext_b = x.new_zeros(N, rp)
+            if fast:
+                ext_a = x.new_zeros(x.shape[0], rp)
             cols, r0 = [], 0
             for br, (a, b) in zip(branches, zip(ab[0::2], ab[1::2])):
                 r = a.shape[0]
-                if training and br.dropout > 0:
-                    key = next_dropout_key()
-                    xd = native().dropout_fwd(x, br.dropout, key)
+                p = br.dropout if training else 0.0
+                key = next_dropout_key() if p > 0 else None
+                if fast:   # one MFMA pass: s·D(x)·Aᵀ into the ext slice (bf16) + fp32 copy for dB
+                    xa = native().lora_proj(x, 0, x.shape[1], bf16_view(a, x.dtype), ext_a[:, r0:r0 + r],
+                                            need_xa, p, key or 0, br.scaling)
                 else:
-                    key, xd = None, x
-                xa = xd @ bf16_view(a, x.dtype).t()                # [T, r]
-                cols.append(xa * br.scaling)
+                    xd = native().dropout_fwd(x, p, key) if key is not None else x
+                    xa = xd @ bf16_view(a, x.dtype).t()                # [T, r]
+                    cols.append(xa * br.scaling)
                 ext_b[br.c0:br.c1, r0:r0 + r] = bf16_view(b, x.dtype)
                 xa_list.append(xa)
                 keys.append(key)
                 r0 += r
-            ext_a = _pad_cols(torch.cat(cols, 1))
+            if not fast:
+                ext_a = _pad_cols(torch.cat(cols, 1))
         y = _base_gemm(x, base if not dense else weight, ext_a, ext_b, residual)
         if bias is not None:
             y = y + bias
         ctx.meta = meta
         ctx.keys = keys
+        ctx.fast = fast
+        ctx.ab_refs = ab          # the parameters themselves: fused kernels accumulate into their .grad
         ctx.has_residual = residual is not None
-        ctx.save_for_backward(x, weight, *ab, *xa_list)
+        ctx.save_for_backward(x, weight, *ab, *[t for t in xa_list if t is not None])
         ctx.nb = len(branches)
         return y
 
@@ -150,30 +174,57 @@ class _FusedLinearFn(torch.autograd.Function):
         xa_list = saved[2 + 2 * nb:2 + 3 * nb]
         dense = not isinstance(base, NF4Weight)
         dy = dy.contiguous()
-        grads_ab = []
+        fast = ctx.fast
+        grads_ab = [None] * (2 * nb)
         g_list = []
+
+        def dest(i):   # the optimizer-owned fp32 grad view (accumulate in place) or a fresh buffer
+            prm = ctx.ab_refs[i]
+            gr = prm.grad
+            if gr is not None and getattr(prm, "_lipa_flat_grad", False) and gr.dtype == torch.float32:
+                return gr, False
+            return torch.zeros(prm.shape, dtype=torch.float32, device=dy.device), True
+
         for i, br in enumerate(branches):
             a, b = ab[2 * i], ab[2 * i + 1]
-            dyi = dy[:, br.c0:br.c1]
-            g = (dyi @ bf16_view(b, dy.dtype)) * br.scaling      # [T, r]  = d(xa)
-            db = (dyi.t() @ xa_list[i]) * br.scaling             # [n, r]
-            key = ctx.keys[i]
-            xin = native().dropout_fwd(x, br.dropout, key) if key is not None else x   # regenerate drop(x)
-            da = g.t() @ xin                                     # [r, K]
-            grads_ab += [da.to(a.dtype), db.to(b.dtype)]
+            n_i = br.c1 - br.c0
+            if fast:
+                bt = bf16_view(b, dy.dtype).t().contiguous()                      # [r, n_i]
+                g = native().lora_proj(dy, br.c0, n_i, bt, None, True, 0.0, 0, br.scaling)   # s·dy_i·B, fp32
+                if ctx.needs_input_grad[5 + 2 * i + 1]:
+                    out, ret = dest(2 * i + 1)                                     # dB [n_i, r] += dy_iᵀ·xa_s
+                    native().lora_acc(xa_list[i], dy, br.c0, n_i, out, True, None, None, 0.0, 0, deterministic())
+                    grads_ab[2 * i + 1] = out.to(b.dtype) if ret else None
+            else:
+                dyi = dy[:, br.c0:br.c1]
+                g = (dyi @ bf16_view(b, dy.dtype)) * br.scaling      # [T, r]  = d(xa)
+                db = (dyi.t() @ xa_list[i]) * br.scaling             # [n, r]
+                key = ctx.keys[i]
+                xin = native().dropout_fwd(x, br.dropout, key) if key is not None else x   # regenerate drop(x)
+                grads_ab[2 * i] = (g.t() @ xin).to(a.dtype)
+                grads_ab[2 * i + 1] = db.to(b.dtype)
             g_list.append(g)
         dx = None
         if ctx.needs_input_grad[0]:
             fold = [i for i in range(nb) if ctx.keys[i] is None]
             ext_a = ext_b = None
             if fold:
-                ext_a = _pad_cols(torch.cat([g_list[i] for i in fold], 1))
+                ext_a = _pad_cols(torch.cat([g_list[i].to(dy.dtype) for i in fold], 1))
                 ext_b = torch.cat([bf16_view(ab[2 * i], dy.dtype) for i in fold], 0)            # [R, K]
                 ext_b = F.pad(ext_b, (0, 0, 0, ext_a.shape[1] - ext_b.shape[0])).t().contiguous()  # [K, Rp]
             dx = _base_gemm_t(dy, base if not dense else weight, ext_a, ext_b)
-            for i, br in enumerate(branches):
-                if ctx.keys[i] is not None:   # LoRA input grad through the regenerated dropout mask
-                    native().dropout_bwd_add(dx, g_list[i] @ bf16_view(ab[2 * i], dy.dtype), br.dropout, ctx.keys[i])
+        for i, br in enumerate(branches):
+            key = ctx.keys[i]
+            if fast:   # dA += gᵀ·D(x) and (dropout branches) dx += D(g·A), one pass over x / dx
+                upd = dx if (dx is not None and key is not None) else None
+                if ctx.needs_input_grad[5 + 2 * i] or upd is not None:
+                    out, ret = dest(2 * i)
+                    native().lora_acc(g_list[i], x, 0, x.shape[1], out, False, upd,
+                                      bf16_view(ab[2 * i], dy.dtype) if upd is not None else None,
+                                      br.dropout if key is not None else 0.0, key or 0, deterministic())
+                    grads_ab[2 * i] = out.to(ab[2 * i].dtype) if (ret and ctx.needs_input_grad[5 + 2 * i]) else None
+            elif dx is not None and key is not None:   # LoRA input grad through the regenerated dropout mask
+                native().dropout_bwd_add(dx, g_list[i] @ bf16_view(ab[2 * i], dy.dtype), br.dropout, key)
         dres = dy if ctx.has_residual else None
         dw = None
         if dense and weight is not None and ctx.needs_input_grad[2]:

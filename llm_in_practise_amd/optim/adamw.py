@@ -52,6 +52,7 @@ class FlatParams:
                 self.low[o:o + k].copy_(p.detach().reshape(-1))
                 p.data = self.low[o:o + k].view_as(p)
             p.grad = self.grad[o:o + k].view_as(p) if p.dtype == torch.float32 else None
+            p._lipa_flat_grad = p.dtype == torch.float32   # kernels may accumulate into p.grad in place
         self.mixed = self.low is not None
         # bf16 shadows of fp32 params (LoRA adapters): refreshed by the update kernel itself,
         # consumed by the fused GEMMs — no per-forward fp32→bf16 conversion kernels

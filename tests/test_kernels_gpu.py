@@ -339,3 +339,36 @@ def test_qwen3_native_matches_reference(mode, monkeypatch):
     assert abs(l0 - l1) < 2e-2 * abs(l1)
     for n in g1:
         assert rel_err(g0[n], g1[n]) < 5e-2, n
+
+
+@pytest.mark.parametrize("M,K,r,p", [(2048, 4096, 8, 0.1), (1000, 1024, 16, 0.0), (77, 512, 4, 0.05)])
+def test_lora_fused_kernels(native_ext, M, K, r, p):
+    """lora_proj / lora_acc vs PyTorch fp32 with the same (regenerated) dropout mask."""
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    a = (0.05 * torch.randn(r, K, device=DEV)).to(torch.bfloat16)
+    key = 12345
+    xd = native_ext.dropout_fwd(x, p, key) if p > 0 else x            # reference mask from the dropout kernel
+    outb = torch.zeros(M, 32, device=DEV, dtype=torch.bfloat16)
+    xs = native_ext.lora_proj(x, 0, K, a, outb[:, 3:3 + r], True, p, key, 2.0)
+    ref = 2.0 * xd.float() @ a.float().t()
+    assert rel_err(xs, ref) < 1e-2 and rel_err(outb[:, 3:3 + r], ref) < 1e-2
+    assert outb[:, :3].abs().sum() == 0 and outb[:, 3 + r:].abs().sum() == 0
+    # column-offset input (a dy slice) without dropout
+    big = torch.randn(M, K + 256, device=DEV).to(torch.bfloat16)
+    g = native_ext.lora_proj(big, 128, K, a, None, True, 0.0, 0, 0.5)
+    assert rel_err(g, 0.5 * big[:, 128:128 + K].float() @ a.float().t()) < 1e-2
+    # accumulation (in place into an fp32 grad): dA += gᵀ·D(x); dx += D(g·A)
+    gg = torch.randn(M, r, device=DEV)
+    dx = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    dx0 = dx.float().clone()
+    da = torch.ones(r, K, device=DEV)
+    native_ext.lora_acc(gg, x, 0, K, da, False, dx, a, p, key, False)
+    assert rel_err(da - 1, gg.t() @ xd.float()) < 1e-2
+    mask = (xd != 0) | (x == 0) if p > 0 else torch.ones_like(x, dtype=torch.bool)
+    scale = 1.0 / (1.0 - p) if p > 0 else 1.0
+    want = dx0 + mask.float() * scale * (gg @ a.float())
+    assert rel_err(dx, want) < 1e-2
+    dbt = torch.zeros(K, r, device=DEV)                       # transposed destination ([n, r] grad of B)
+    native_ext.lora_acc(gg, big, 128, K, dbt, True, None, None, 0.0, 0, True)
+    assert rel_err(dbt, (gg.t() @ big[:, 128:128 + K].float()).t()) < 1e-2

@@ -35,7 +35,8 @@ def _args(out, **kw):
     return TrainingArguments(**a)
 
 
-def test_qlora_trainer_gpu_resume_exact(tmp_path, native_ext):
+def test_qlora_trainer_gpu_resume_exact(tmp_path, native_ext, monkeypatch):
+    monkeypatch.setenv("LIPA_DETERMINISTIC", "1")     # fixed-order LoRA grad sums (no fp32 atomics)
     torch.manual_seed(0)
     ds = SyntheticLMDataset(4096, 128, 16, seed=1)
     full = _qlora()
