@@ -12,6 +12,8 @@
     lipa serve --model DIR [--adapter DIR] [--port 8000]                        (G4, H1)
     lipa guard --backend URL [--port 8099]                                      (H3)
     lipa convert-alpaca --input self_cognition.jsonl --out alpaca.json           (E10 converter)
+    lipa hf-classify [--model-path bert-dir] [--data imdb.jsonl]                 (G5 Trainer demo)
+    lipa env                                                                     (G5 env_test)
     lipa bench ...                                                               (bench.py)
 
 Datasets / checkpoints are LOCAL paths (no hub access); ``--random-init`` builds the named
@@ -387,6 +389,50 @@ def cmd_convert_alpaca(a):
     print(json.dumps({"records": len(out), "out": a.out}))
 
 
+def cmd_hf_classify(a):
+    """G5 ``HF_Basics/trainer_demo.py``: BERT sequence classification with the Trainer (eval and
+    save per epoch, best model by accuracy)."""
+    from ..models.bert import BertConfig, BertForSequenceClassification, accuracy_metric
+    from ..train.data import DataCollatorWithPadding, load_records, load_tokenizer
+    from ..train.trainer import Trainer, TrainingArguments
+    dev = _device()
+    if a.model_path:
+        m = BertForSequenceClassification.from_pretrained(a.model_path, a.num_labels, dev)
+        tok = load_tokenizer(a.model_path, pad_to_eos=False)
+        enc = lambda t: tok(t, truncation=True, max_length=a.max_length)["input_ids"]  # noqa: E731
+    else:                                  # offline smoke: byte tokens on a tiny encoder
+        m = BertForSequenceClassification(BertConfig(vocab_size=260, hidden_size=128, num_hidden_layers=2,
+                                                     num_attention_heads=4, intermediate_size=256,
+                                                     num_labels=a.num_labels)).to(dev)
+        enc = lambda t: [257] + list(t.encode("utf-8"))[:a.max_length - 1]  # noqa: E731
+    recs = load_records(a.data) if a.data else \
+        [{"text": ("great film " if i % 2 else "awful film ") * (1 + i % 3), "label": i % 2} for i in range(200)]
+    rows = [{"input_ids": enc(r[a.text_field]), "label": int(r[a.label_field])} for r in recs]
+    n_eval = max(1, int(len(rows) * a.eval_fraction))
+    args = TrainingArguments(output_dir=a.output_dir, per_device_train_batch_size=a.batch_size,
+                             per_device_eval_batch_size=a.batch_size, num_train_epochs=a.epochs,
+                             learning_rate=a.lr, weight_decay=0.01, eval_strategy="epoch", save_strategy="epoch",
+                             load_best_model_at_end=True, metric_for_best_model="accuracy", save_total_limit=2,
+                             logging_steps=50)
+    tr = Trainer(m, args, train_dataset=rows[n_eval:], eval_dataset=rows[:n_eval],
+                 data_collator=DataCollatorWithPadding(pad_token_id=0), compute_metrics=accuracy_metric)
+    tr.train()
+    res = tr.evaluate()
+    tr.log_metrics("eval", res)
+    tr.save_metrics("eval", res)
+
+
+def cmd_env(a):
+    """G5 ``env_test.py``: device / runtime versions."""
+    info = {"torch": torch.__version__, "hip": getattr(torch.version, "hip", None),
+            "gpu_available": torch.cuda.is_available(), "device_count": torch.cuda.device_count()}
+    if torch.cuda.is_available():
+        p = torch.cuda.get_device_properties(0)
+        info.update(name=p.name, arch=getattr(p, "gcnArchName", ""), hbm_gib=round(p.total_memory / 2 ** 30, 1),
+                    cus=p.multi_processor_count)
+    print(json.dumps(info, indent=2))
+
+
 def cmd_bench(a):
     import subprocess
     here = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -571,6 +617,22 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--name", default="马哥教育AI小助手")
     p.add_argument("--author", default="马哥教育AI团队")
     p.set_defaults(fn=cmd_convert_alpaca)
+
+    p = sub.add_parser("hf-classify")
+    p.add_argument("--model-path", dest="model_path", help="local bert-base-uncased style dir")
+    p.add_argument("--data", help="local jsonl/json/csv with text + label")
+    p.add_argument("--text-field", dest="text_field", default="text")
+    p.add_argument("--label-field", dest="label_field", default="label")
+    p.add_argument("--num-labels", dest="num_labels", type=int, default=2)
+    p.add_argument("--max-length", dest="max_length", type=int, default=256)
+    p.add_argument("--eval-fraction", dest="eval_fraction", type=float, default=0.1)
+    p.add_argument("--epochs", type=float, default=3)
+    p.add_argument("--batch-size", dest="batch_size", type=int, default=16)
+    p.add_argument("--lr", type=float, default=2e-5)
+    p.add_argument("--output-dir", dest="output_dir", default="./results")
+    p.set_defaults(fn=cmd_hf_classify)
+    p = sub.add_parser("env")
+    p.set_defaults(fn=cmd_env)
 
     p = sub.add_parser("bench")
     p.add_argument("rest", nargs=argparse.REMAINDER)

@@ -164,6 +164,29 @@ class DataCollatorForLanguageModeling:
         return out
 
 
+class DataCollatorWithPadding:
+    """Pad ``input_ids`` / ``attention_mask`` / ``token_type_ids`` to the longest row of the batch
+    (``HF_Basics/trainer_demo.py``: dynamic padding for classification); ``label(s)`` stacked."""
+
+    def __init__(self, tokenizer=None, pad_to_multiple_of: int | None = None, pad_token_id: int | None = None):
+        self.pad = pad_token_id if pad_token_id is not None else (_pad_id(tokenizer) if tokenizer is not None else 0)
+        self.mult = pad_to_multiple_of
+
+    def __call__(self, batch):
+        out = {"input_ids": _pad([b["input_ids"] for b in batch], self.pad, self.mult)}
+        n = out["input_ids"].shape[1]
+        if "attention_mask" in batch[0]:
+            out["attention_mask"] = _pad([b["attention_mask"] for b in batch], 0, self.mult)[:, :n]
+        else:
+            out["attention_mask"] = _pad([[1] * len(b["input_ids"]) for b in batch], 0, self.mult)[:, :n]
+        if "token_type_ids" in batch[0]:
+            out["token_type_ids"] = _pad([b["token_type_ids"] for b in batch], 0, self.mult)[:, :n]
+        for key in ("labels", "label"):
+            if key in batch[0]:
+                out["labels"] = torch.tensor([int(b[key]) for b in batch])
+        return out
+
+
 class DataCollatorForSeq2Seq:
     """Pads and keeps the provided labels (pad → -100): the corrected-objective collator."""
 

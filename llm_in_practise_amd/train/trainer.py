@@ -87,6 +87,9 @@ class TrainingArguments:
     dataloader_drop_last: bool = False
     eval_strategy: str = "no"
     eval_steps: int | None = None
+    load_best_model_at_end: bool = False
+    metric_for_best_model: str | None = None
+    greater_is_better: bool | None = None
     resume_from_checkpoint: str | None = None
     local_rank: int = -1
     # MI355X-native additions
@@ -121,6 +124,21 @@ class TrainerState:
         with open(path) as f:
             d = json.load(f)
         return cls(**{k: v for k, v in d.items() if k in {f.name for f in dataclasses.fields(cls)}})
+
+
+class EvalPrediction(tuple):
+    """``(predictions, label_ids)`` as handed to ``compute_metrics``."""
+
+    def __new__(cls, predictions, label_ids):
+        return super().__new__(cls, (predictions, label_ids))
+
+    @property
+    def predictions(self):
+        return self[0]
+
+    @property
+    def label_ids(self):
+        return self[1]
 
 
 @dataclasses.dataclass
@@ -224,7 +242,7 @@ def _unwrap(m):
 class Trainer:
     def __init__(self, model: nn.Module, args: TrainingArguments, train_dataset=None, eval_dataset=None,
                  data_collator=None, tokenizer=None, processing_class=None, optimizers=(None, None),
-                 compute_loss_fn=None, callbacks=None):
+                 compute_loss_fn=None, callbacks=None, compute_metrics=None):
         self.args = args
         self.model = model
         self.train_dataset, self.eval_dataset = train_dataset, eval_dataset
@@ -232,6 +250,7 @@ class Trainer:
         self.tokenizer = processing_class or tokenizer
         self.optimizer, self.lr_scheduler = optimizers
         self.compute_loss_fn = compute_loss_fn
+        self.compute_metrics = compute_metrics
         self.callbacks = callbacks or []
         self.state = TrainerState(logging_steps=args.logging_steps, save_steps=args.save_steps)
         if os.environ.get("WORLD_SIZE") and int(os.environ["WORLD_SIZE"]) > 1 and not D.is_dist():
@@ -384,6 +403,10 @@ class Trainer:
         if not lim or lim <= 0:
             return
         cks = self._sorted_checkpoints()
+        best = self.state.best_model_checkpoint
+        if best in cks and len(cks) > lim:         # HF keeps the best checkpoint out of the rotation
+            cks.remove(best)
+            lim -= 1
         for c in cks[:max(0, len(cks) - lim)]:
             shutil.rmtree(c, ignore_errors=True)
 
@@ -544,16 +567,21 @@ class Trainer:
                         self._save_checkpoint()
                     for cb in self.callbacks:
                         cb(self)
-                if self.state.global_step >= total:
-                    break
+                if a.eval_strategy == "epoch" and self.eval_dataset is not None:
+                    self._eval_and_track()
                 if a.save_strategy == "epoch":
                     self._save_checkpoint()
+                    self._track_best()
+                if self.state.global_step >= total:
+                    break
         except BaseException:
             self._interrupt_dir = a.output_dir.rstrip("/") + "_interrupted"
             raise
         if log_n:
             tr_loss_sum += float(log_loss)
             tr_loss_n += log_n
+        if a.load_best_model_at_end and self.state.best_model_checkpoint:
+            self._load_weights_only(self.state.best_model_checkpoint)
         runtime = time.perf_counter() - step_t0
         train_loss = tr_loss_sum / max(1, tr_loss_n)
         metrics = {"train_runtime": round(runtime, 4),
@@ -620,15 +648,24 @@ class Trainer:
 
     @torch.no_grad()
     def evaluate(self, eval_dataset=None):
+        """Mean loss (+ ``compute_metrics(EvalPrediction(predictions, label_ids))`` when given,
+        e.g. accuracy for ``HF_Basics/trainer_demo.py``); distributed: sums all-reduced."""
         ds = eval_dataset or self.eval_dataset
         self.model.eval()
         bs = self.args.per_device_eval_batch_size
         samp = _EpochSampler(len(ds), self.world, self.rank, 0, shuffle=False)
         idx = samp.indices(0)
         tot = torch.zeros(2, device=self.device, dtype=torch.float64)
+        preds, labels = [], []
         for s in range(0, len(idx), bs):
             b = self._to_device(self.data_collator([ds[j] for j in idx[s:s + bs]]))
-            loss = self.compute_loss(self.model, b)
+            if self.compute_metrics is not None and isinstance(b, dict):
+                out = self.model(**b)
+                loss = out.loss
+                preds.append(out.logits.float().cpu())
+                labels.append(b["labels"].cpu())
+            else:
+                loss = self.compute_loss(self.model, b)
             tot[0] += float(loss) * len(idx[s:s + bs])
             tot[1] += len(idx[s:s + bs])
         if self.world > 1:
@@ -636,7 +673,55 @@ class Trainer:
             dist.all_reduce(tot)
         self.model.train()
         el = float(tot[0] / tot[1])
-        return {"eval_loss": el, "perplexity": math.exp(min(el, 50))}
+        res = {"eval_loss": el}
+        if self.compute_metrics is not None and preds:
+            p, l = torch.cat(preds), torch.cat(labels)
+            if self.world > 1:
+                import torch.distributed as dist
+                gp = [None] * self.world
+                dist.all_gather_object(gp, (p, l))
+                p, l = torch.cat([x[0] for x in gp]), torch.cat([x[1] for x in gp])
+            res.update({f"eval_{k}": v for k, v in self.compute_metrics(EvalPrediction(p, l)).items()})
+        else:
+            res["perplexity"] = math.exp(min(el, 50))
+        return res
+
+    def _eval_and_track(self):
+        m = self.evaluate()
+        m["epoch"] = round(self.state.epoch, 4)
+        self.state.log_history.append(dict(m, step=self.state.global_step))
+        self._last_eval = m
+        if self.rank == 0:
+            print(m, flush=True)
+
+    def _track_best(self):
+        a = self.args
+        m = getattr(self, "_last_eval", None)
+        if not m:
+            return
+        key = a.metric_for_best_model or "loss"
+        key = key if key.startswith("eval_") else "eval_" + key
+        if key not in m:
+            return
+        gib = a.greater_is_better if a.greater_is_better is not None else not key.endswith("loss")
+        v = m[key]
+        if self.state.best_metric is None or (v > self.state.best_metric if gib else v < self.state.best_metric):
+            self.state.best_metric = v
+            self.state.best_model_checkpoint = os.path.join(a.output_dir,
+                                                            f"{PREFIX_CHECKPOINT_DIR}-{self.state.global_step}")
+
+    def _load_weights_only(self, ck):
+        m = _unwrap(self.model)
+        if os.path.exists(os.path.join(ck, "adapter_model.safetensors")) and hasattr(m, "load_adapter"):
+            m.load_adapter(ck)
+        elif os.path.exists(os.path.join(ck, "model.safetensors")):
+            from safetensors.torch import load_file
+            sd = load_file(os.path.join(ck, "model.safetensors"))
+            with torch.no_grad():
+                own = m.state_dict()
+                for k, v in sd.items():
+                    if k in own:
+                        own[k].copy_(v.to(own[k].device, own[k].dtype))
 
 
 class _null:

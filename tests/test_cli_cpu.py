@@ -90,3 +90,10 @@ def test_convert_alpaca(tmp_path):
     main(["convert-alpaca", "--input", str(src), "--out", str(out)])
     d = json.load(open(out))
     assert d[0]["instruction"] == "你是谁?" and "马哥教育AI小助手" in d[0]["output"]
+
+
+def test_hf_classify_and_env(tmp_path, capsys):
+    main(["hf-classify", "--epochs", "2", "--lr", "1e-3", "--output-dir", str(tmp_path / "r"), "--batch-size", "32"])
+    assert os.path.exists(tmp_path / "r" / "eval_results.json")
+    main(["env"])
+    assert "torch" in capsys.readouterr().out

@@ -193,3 +193,31 @@ def test_initialize_api():
                                                                                      "warmup_num_steps": 10}}},
                                   optimizer=opt)
     assert eng.lr == 3e-4 and eng.wd == 0.1 and sched is not None and eng.get_lr()[0] == 0.0
+
+
+def _fsdp_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    from llm_in_practise_amd.parallel.fsdp import FSDP, ShardingStrategy, get_state_dict, \
+        transformer_auto_wrap_policy
+    torch.manual_seed(0)
+    net = Net()
+    m = FSDP(net, auto_wrap_policy=transformer_auto_wrap_policy({nn.Sequential}),
+             sharding_strategy=ShardingStrategy.FULL_SHARD, lr=1e-2, weight_decay=0.01, grad_clip=0.05)
+    for s in range(3):
+        x, y = _data(s, rank)
+        m.backward(((m(x) - y) ** 2).mean())
+        m.step()
+    sd, _ = get_state_dict(m)
+    if rank == 0:
+        torch.save(sd, out)
+    torch.distributed.destroy_process_group()
+
+
+def test_fsdp_api_full_shard_matches_single_process(tmp_path):
+    out = str(tmp_path / "f.pt")
+    mp.spawn(_fsdp_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    want = _oracle()
+    for k in want:
+        assert torch.allclose(got[k], want[k], atol=2e-5), k
