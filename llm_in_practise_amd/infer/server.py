@@ -113,6 +113,13 @@ def create_app(engine: ServingEngine, api_key: str | None = None, moderation=Non
         if res["results"][0]["flagged"]:
             raise HTTPException(status_code=400, detail={"error": "content_policy_violation", "moderation": res})
 
+    @app.get("/ui")
+    async def ui():
+        """Browser chat page (the Gradio web UI of ``Scripts/inference/06-*webui*.py`` as plain
+        HTML + SSE: streamed deltas, temperature / top-p sliders, multi-turn history)."""
+        from fastapi.responses import HTMLResponse
+        return HTMLResponse(_UI_HTML.replace("__MODEL__", engine.model_name))
+
     @app.get("/health")
     async def health():
         return {"status": "ok", "model": engine.model_name}
@@ -191,6 +198,30 @@ async def _sse_completion(engine, prompt, params, cid, created, name):
         yield "data: " + json.dumps({**head, "choices": [{"index": 0, "text": delta, "finish_reason": fr}]},
                                     ensure_ascii=False) + "\n\n"
     yield "data: [DONE]\n\n"
+
+
+_UI_HTML = """<!doctype html><html><head><meta charset="utf-8"><title>__MODEL__</title>
+<style>body{font-family:sans-serif;max-width:860px;margin:2em auto}#log div{margin:.4em 0;white-space:pre-wrap}
+.u{color:#036}.a{color:#222}textarea{width:100%;height:4em}</style></head><body>
+<h3>__MODEL__</h3><div id="log"></div><textarea id="q"></textarea><br>
+temperature <input id="t" type="range" min="0" max="1.5" step="0.05" value="0.7"><span id="tv">0.7</span>
+top-p <input id="p" type="range" min="0.05" max="1" step="0.05" value="0.9"><span id="pv">0.9</span>
+<button onclick="send()">send</button> <button onclick="hist=[];log.innerHTML=''">clear</button>
+<script>
+let hist=[];const log=document.getElementById('log');
+for(const [s,v] of [['t','tv'],['p','pv']]){const e=document.getElementById(s);e.oninput=()=>document.getElementById(v).textContent=e.value;}
+async function send(){const q=document.getElementById('q').value;if(!q)return;document.getElementById('q').value='';
+hist.push({role:'user',content:q});const u=document.createElement('div');u.className='u';u.textContent='user: '+q;log.appendChild(u);
+const a=document.createElement('div');a.className='a';a.textContent='assistant: ';log.appendChild(a);
+const r=await fetch('/v1/chat/completions',{method:'POST',headers:{'Content-Type':'application/json'},
+body:JSON.stringify({messages:hist,stream:true,max_tokens:512,temperature:+document.getElementById('t').value,top_p:+document.getElementById('p').value})});
+const rd=r.body.getReader();const dec=new TextDecoder();let buf='',text='';
+while(true){const {done,value}=await rd.read();if(done)break;buf+=dec.decode(value,{stream:true});
+let i;while((i=buf.indexOf('\\n\\n'))>=0){const line=buf.slice(0,i);buf=buf.slice(i+2);
+if(!line.startsWith('data: ')||line==='data: [DONE]')continue;const d=JSON.parse(line.slice(6)).choices[0].delta||{};
+if(d.content){text+=d.content;a.textContent='assistant: '+text;}}}
+hist.push({role:'assistant',content:text});}
+</script></body></html>"""
 
 
 def serve(engine: ServingEngine, host: str = "0.0.0.0", port: int = 8000, **kw):

@@ -1,0 +1,141 @@
+#!/usr/bin/env python3
+"""Serving benchmark against any OpenAI-compatible endpoint (the reference's
+``vllm bench serve --dataset-name sharegpt --request-rate inf --max-concurrency C --ignore-eos
+--sharegpt-output-len 256`` plus ``generate_mixed_dataset.py`` / ``extract_metrics.py``,
+``LLM_on_Kubernetes/Inference_Platfrom/README.md:1177-1493``).
+
+    python scripts/bench_serve.py --url http://127.0.0.1:8000 --concurrency 8 16 32 --num-prompts 128
+    python scripts/bench_serve.py --inprocess random:qwen3-small --concurrency 4     # no server needed
+
+Dataset: ``--dataset mixed`` = 70 % short chat / 30 % long RAG-style prompts (synthetic text,
+no network), or a ShareGPT-format JSON file.  Metrics per concurrency (streamed requests):
+mean / p99 TTFT, mean / p99 ITL, request throughput, output tokens/s — the columns of the
+reference's results table (``README.md:1504-1511``).  Token counts use streamed deltas (one
+delta ≈ one token for the OpenAI stream), or the server's ``usage`` when not streaming.
+"""
+import argparse
+import asyncio
+import json
+import random
+import statistics
+import time
+
+
+def mixed_dataset(n: int, seed: int = 0):
+    rnd = random.Random(seed)
+    words = ("cluster gpu kernel memory latency throughput scheduler token model serving cache network storage "
+             "pod node replica request batch prompt context quantization adapter").split()
+    out = []
+    for i in range(n):
+        if rnd.random() < 0.7:
+            q = " ".join(rnd.choice(words) for _ in range(rnd.randint(8, 40)))
+            out.append([{"role": "user", "content": f"Explain briefly: {q}?"}])
+        else:
+            doc = " ".join(rnd.choice(words) for _ in range(rnd.randint(600, 1500)))
+            out.append([{"role": "system", "content": "Answer using the document."},
+                        {"role": "user", "content": f"Document:\n{doc}\n\nQuestion: summarise the document."}])
+    return out
+
+
+def sharegpt(path: str, n: int):
+    data = json.load(open(path))
+    out = []
+    for conv in data:
+        turns = conv.get("conversations", [])
+        if turns:
+            out.append([{"role": "user", "content": turns[0]["value"]}])
+        if len(out) >= n:
+            break
+    return out
+
+
+def pct(xs, p):
+    if not xs:
+        return float("nan")
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(round(p / 100 * (len(xs) - 1))))]
+
+
+async def one_request(client, url, model, msgs, max_tokens):
+    t0 = time.perf_counter()
+    ttft, last, itl, n = None, None, [], 0
+    body = {"model": model, "messages": msgs, "max_tokens": max_tokens, "stream": True, "temperature": 0.0}
+    async with client.stream("POST", url + "/v1/chat/completions", json=body, timeout=600) as r:
+        async for line in r.aiter_lines():
+            if not line.startswith("data: ") or line == "data: [DONE]":
+                continue
+            d = json.loads(line[6:])["choices"][0].get("delta", {})
+            if d.get("content"):
+                now = time.perf_counter()
+                if ttft is None:
+                    ttft = now - t0
+                else:
+                    itl.append(now - last)
+                last = now
+                n += 1
+    return {"ttft": ttft or (time.perf_counter() - t0), "itl": itl, "out_tokens": n, "e2e": time.perf_counter() - t0}
+
+
+async def run_level(url, model, prompts, conc, max_tokens):
+    import httpx
+    sem = asyncio.Semaphore(conc)
+    async with httpx.AsyncClient() as client:
+        async def task(m):
+            async with sem:
+                return await one_request(client, url, model, m, max_tokens)
+        t0 = time.perf_counter()
+        res = await asyncio.gather(*[task(m) for m in prompts])
+        dur = time.perf_counter() - t0
+    ttft = [r["ttft"] * 1e3 for r in res]
+    itl = [x * 1e3 for r in res for x in r["itl"]]
+    toks = sum(r["out_tokens"] for r in res)
+    return {"concurrency": conc, "requests": len(res), "duration_s": round(dur, 3),
+            "mean_ttft_ms": round(statistics.mean(ttft), 2), "p99_ttft_ms": round(pct(ttft, 99), 2),
+            "mean_itl_ms": round(statistics.mean(itl), 2) if itl else None,
+            "p99_itl_ms": round(pct(itl, 99), 2) if itl else None,
+            "req_per_s": round(len(res) / dur, 3), "output_tok_per_s": round(toks / dur, 1)}
+
+
+def start_inprocess(spec: str, port: int):
+    """Launch our server in a background thread with a random-init model and byte tokenizer."""
+    import threading
+
+    import uvicorn
+
+    from llm_in_practise_amd.cli.main import _load_for_inference
+    from llm_in_practise_amd.infer.engine import ServingEngine
+    from llm_in_practise_amd.infer.server import create_app
+    from llm_in_practise_amd.train.data import ByteTokenizer
+    m = _load_for_inference(spec)
+    tok = ByteTokenizer()
+    eng = ServingEngine(m, tok, model_name=spec, max_batch=64)
+    cfg = uvicorn.Config(create_app(eng), host="127.0.0.1", port=port, log_level="warning")
+    th = threading.Thread(target=uvicorn.Server(cfg).run, daemon=True)
+    th.start()
+    time.sleep(2.0)
+    return f"http://127.0.0.1:{port}"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--url", default=None)
+    ap.add_argument("--inprocess", default=None, help="e.g. random:qwen3-small (starts our server in-process)")
+    ap.add_argument("--port", type=int, default=8765)
+    ap.add_argument("--model", default="default")
+    ap.add_argument("--dataset", default="mixed")
+    ap.add_argument("--num-prompts", type=int, default=64)
+    ap.add_argument("--max-tokens", type=int, default=256)
+    ap.add_argument("--concurrency", type=int, nargs="+", default=[8])
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    url = a.url or start_inprocess(a.inprocess, a.port)
+    prompts = mixed_dataset(a.num_prompts) if a.dataset == "mixed" else sharegpt(a.dataset, a.num_prompts)
+    rows = [asyncio.run(run_level(url, a.model, prompts, c, a.max_tokens)) for c in a.concurrency]
+    for r in rows:
+        print(json.dumps(r))
+    if a.out:
+        json.dump(rows, open(a.out, "w"), indent=2)
+
+
+if __name__ == "__main__":
+    main()
