@@ -1,13 +1,24 @@
-"""Serving engine: model + tokenizer + a dynamic-batching worker.
+"""Serving engine with iteration-level (continuous) batching.
 
-The reference serves through vLLM; its own FastAPI app (``Scripts/inference/07-…-api-infr.py``)
-runs one ``model.generate`` per request.  Here one worker thread owns the GPU and drains a
-request queue: requests that arrive while a batch is running are grouped (up to
-``max_batch``) by identical sampling parameters and decoded TOGETHER — right-padded prompts of
-different lengths, per-row KV positions (``infer/generate.py``) — so concurrent clients share
-every decode step (the weights are read once per step for the whole batch, which is what makes
-decode on a 288 GB HBM part efficient).  Streaming requests get per-row text deltas through a
-fan-out streamer.  Metrics for ``/metrics`` (Prometheus text) are kept here.
+The reference serves through vLLM (continuous batching, paged KV); its own FastAPI app
+(``Scripts/inference/07-…-api-infr.py``) runs one ``model.generate`` per request.  Here one worker
+thread owns the GPU and keeps a fixed pool of ``max_batch`` sequence slots over ONE pre-allocated
+KV cache ``[max_batch, max_model_len, Hkv·D]`` per layer (288 GB of HBM makes a contiguous cache
+per slot affordable: Qwen3-8B, 64 slots × 4096 tokens = 36 GB):
+
+* every iteration, waiting requests are admitted into free slots: their prompts are prefilled
+  together (right-padded, fused flash-attention with per-row key lengths) into a scratch cache and
+  copied into their slots; their first token is sampled from the prefill logits;
+* then ONE decode step runs for all slots at once — each row appends at its own position
+  (``KVCache.write_rows``) and the split-K decode-attention kernel reads per-row lengths, so
+  sequences of any length and age share every step (weights are read once per step for the
+  whole batch);
+* finished rows (EOS / max_tokens / cache full) are released immediately and refilled on the next
+  iteration — no request waits for another's completion;
+* per-request sampling parameters: rows are sampled in groups of identical parameters with the
+  fused sampler kernel.
+
+Streaming requests receive text deltas per token; ``/metrics`` data (Prometheus text) is kept here.
 """
 from __future__ import annotations
 
@@ -20,8 +31,9 @@ from typing import Any
 
 import torch
 
+from ..models.common import KVCache
+from ..ops.decode import sample
 from ..train.data import render_chatml
-from .generate import generate
 
 
 @dataclasses.dataclass
@@ -32,6 +44,7 @@ class SamplingParams:
     top_k: int = 0
     repetition_penalty: float = 1.0
     stop: list[str] | None = None
+    ignore_eos: bool = False            # vLLM extra param (``vllm bench serve --ignore-eos``)
 
     def key(self):
         return (self.temperature, self.top_p, self.top_k, self.repetition_penalty)
@@ -45,6 +58,16 @@ class _Request:
     out: "queue.Queue[Any]"
     t_arrive: float
     rid: str = dataclasses.field(default_factory=lambda: uuid.uuid4().hex)
+
+
+@dataclasses.dataclass
+class _Slot:
+    req: _Request
+    gen: list = dataclasses.field(default_factory=list)
+    sent: int = 0
+    t_first: float | None = None
+    done: bool = False
+    finish: str = "length"
 
 
 class _Histogram:
@@ -70,46 +93,32 @@ class _Histogram:
         return lines
 
 
-class _FanoutStreamer:
-    """Per-row incremental detokenisation for a batched decode."""
-
-    def __init__(self, tokenizer, reqs: list[_Request], eos: set[int]):
-        self.tok, self.reqs, self.eos = tokenizer, reqs, eos
-        self.ids = [[] for _ in reqs]
-        self.sent = [0] * len(reqs)
-        self.done = [False] * len(reqs)
-        self.first = [None] * len(reqs)
-
-    def put(self, tok: torch.Tensor):
-        now = time.time()
-        for i, t in enumerate(tok.tolist()):
-            if self.done[i]:
-                continue
-            if self.first[i] is None:
-                self.first[i] = now
-            if t in self.eos or len(self.ids[i]) >= self.reqs[i].params.max_tokens:
-                self.done[i] = True
-                continue
-            self.ids[i].append(t)
-            if self.reqs[i].stream:
-                text = self.tok.decode(self.ids[i], skip_special_tokens=True)
-                if len(text) > self.sent[i] and not text.endswith("�"):
-                    self.reqs[i].out.put(("delta", text[self.sent[i]:]))
-                    self.sent[i] = len(text)
-
-    def end(self):
-        pass
+def _unwrap_lm(model):
+    m = model
+    for _ in range(4):
+        if hasattr(m, "lm_head") and hasattr(m, "model"):
+            return m
+        m = getattr(m, "model", None) or getattr(m, "module", None)
+        if m is None:
+            break
+    raise TypeError("ServingEngine needs a causal LM with .model and .lm_head")
 
 
 class ServingEngine:
     def __init__(self, model, tokenizer, model_name: str = "lipa-model", max_batch: int = 16,
-                 system_prompt: str | None = None, chat_template: str = "auto", space_before_end: bool = False):
+                 system_prompt: str | None = None, chat_template: str = "auto", space_before_end: bool = False,
+                 max_model_len: int | None = None, max_prefill_batch: int = 8):
         self.model, self.tok, self.model_name = model, tokenizer, model_name
+        self.lm = _unwrap_lm(model)
+        self.lm.eval()
         self.max_batch = max_batch
+        self.max_prefill_batch = max_prefill_batch
         self.system_prompt = system_prompt
         self.chat_template = chat_template
         self.space_before_end = space_before_end
         self.device = next(model.parameters()).device
+        cfg = self.lm.config
+        self.max_len = int(max_model_len or min(getattr(cfg, "max_position_embeddings", 4096), 4096))
         eos = getattr(tokenizer, "eos_token_id", None)
         self.eos = {eos} if isinstance(eos, int) else set(eos or [])
         im_end = None
@@ -126,9 +135,14 @@ class ServingEngine:
         self.q: "queue.Queue[_Request]" = queue.Queue()
         self.lock = threading.Lock()
         self.stats = {"requests_total": 0, "prompt_tokens_total": 0, "generation_tokens_total": 0,
-                      "batches_total": 0, "running": 0}
+                      "batches_total": 0, "running": 0, "decode_steps_total": 0}
         self.h_latency = _Histogram([0.05, 0.1, 0.25, 0.5, 1, 2, 5, 10, 30, 60])
         self.h_ttft = _Histogram([0.01, 0.025, 0.05, 0.1, 0.2, 0.5, 1, 2, 5])
+        self.cache = KVCache(cfg.num_hidden_layers, max_batch, self.max_len, cfg.num_key_value_heads, cfg.head_dim,
+                             self.lm.lm_head.weight.dtype, self.device)
+        self.cache.pos = torch.zeros(max_batch, dtype=torch.long, device=self.device)
+        self.slots: list[_Slot | None] = [None] * max_batch
+        self.next_tok = torch.full((max_batch,), self.pad, dtype=torch.long, device=self.device)
         self._stop = False
         self._worker = threading.Thread(target=self._loop, daemon=True)
         self._worker.start()
@@ -148,7 +162,8 @@ class ServingEngine:
 
     # ------------------------------------------------------------------ request API (thread-safe)
     def submit(self, prompt: str, params: SamplingParams, stream: bool = False) -> _Request:
-        ids = self.encode(prompt)
+        room = self.max_len - 1 - min(params.max_tokens, self.max_len // 2)   # keep space to generate
+        ids = self.encode(prompt)[-room:]
         r = _Request(ids, params, stream, queue.Queue(), time.time())
         self.q.put(r)
         return r
@@ -176,69 +191,155 @@ class ServingEngine:
 
     def shutdown(self):
         self._stop = True
+        self.q.put(None)
 
     # ------------------------------------------------------------------ worker
-    def _collect(self) -> list[_Request]:
-        first = self.q.get()
-        batch = [first]
-        pending = []
-        while len(batch) < self.max_batch:
-            try:
-                r = self.q.get_nowait()
-            except queue.Empty:
-                break
-            (batch if r.params.key() == first.params.key() else pending).append(r)
-        for r in pending:
-            self.q.put(r)
-        return batch
-
     def _loop(self):
         while not self._stop:
-            batch = self._collect()
             try:
-                self._run(batch)
-            except Exception as e:  # report to every waiting client, keep serving
-                for r in batch:
-                    r.out.put(("error", repr(e)))
+                self._iteration()
+            except Exception as e:  # fail the in-flight requests, keep serving
+                for i, s in enumerate(self.slots):
+                    if s is not None:
+                        s.req.out.put(("error", repr(e)))
+                        self.slots[i] = None
+                self.cache.pos.zero_()
 
-    def _run(self, batch: list[_Request]):
-        B = len(batch)
-        S = max(len(r.prompt_ids) for r in batch)
+    def _iteration(self):
+        active = [i for i, s in enumerate(self.slots) if s is not None]
+        free = [i for i, s in enumerate(self.slots) if s is None]
+        new = []
+        block = not active
+        while free and len(new) < self.max_prefill_batch:
+            try:
+                r = self.q.get(block=block, timeout=None if block else 0)
+            except queue.Empty:
+                break
+            block = False
+            if r is None:
+                return
+            new.append((free.pop(0), r))
+        with self.lock, torch.no_grad():
+            if new:
+                self._admit(new)
+            if any(s is not None for s in self.slots):
+                self._decode_step()
+
+    def _admit(self, new):
+        """Prefill the new prompts together into a scratch cache, copy into their slots, sample
+        each one's first token."""
+        lm = self.lm
+        B = len(new)
+        S = max(len(r.prompt_ids) for _, r in new)
         ids = torch.full((B, S), self.pad, dtype=torch.long)
-        am = torch.zeros(B, S, dtype=torch.long)
-        for i, r in enumerate(batch):
-            ids[i, :len(r.prompt_ids)] = torch.tensor(r.prompt_ids, dtype=torch.long)
-            am[i, :len(r.prompt_ids)] = 1
-        p = batch[0].params
-        max_new = max(r.params.max_tokens for r in batch)
-        fan = _FanoutStreamer(self.tok, batch, self.eos)
-        self.stats["running"] = B
-        t0 = time.time()
-        with self.lock:
-            out = generate(self.model, ids.to(self.device), am.to(self.device), max_new_tokens=max_new,
-                           do_sample=p.temperature > 0, temperature=p.temperature, top_p=p.top_p, top_k=p.top_k,
-                           repetition_penalty=p.repetition_penalty, eos_token_id=sorted(self.eos) or None,
-                           pad_token_id=self.pad, streamer=fan)
-        self.stats["running"] = 0
-        self.stats["batches_total"] += 1
-        t1 = time.time()
-        for i, r in enumerate(batch):
-            gen = fan.ids[i][:r.params.max_tokens]
-            text = self.tok.decode(gen, skip_special_tokens=True)
-            finish = "stop" if fan.done[i] and len(gen) < r.params.max_tokens else "length"
-            if r.params.stop:
-                cut = min((text.find(s) for s in r.params.stop if s and s in text), default=-1)
-                if cut >= 0:
-                    text, finish = text[:cut], "stop"
-            self.stats["requests_total"] += 1
+        lens = torch.zeros(B, dtype=torch.long)
+        for b, (_, r) in enumerate(new):
+            ids[b, :len(r.prompt_ids)] = torch.tensor(r.prompt_ids, dtype=torch.long)
+            lens[b] = len(r.prompt_ids)
+        ids, lens = ids.to(self.device), lens.to(self.device)
+        cfg = lm.config
+        tmp = KVCache(cfg.num_hidden_layers, B, S, cfg.num_key_value_heads, cfg.head_dim, self.cache.k[0].dtype,
+                      self.device)
+        h = lm.model(ids, None, tmp, lens.to(torch.int32))
+        last = h.view(B, S, -1)[torch.arange(B, device=self.device), lens - 1]
+        logits = last @ lm.lm_head.weight.t()
+        rows = torch.tensor([s for s, _ in new], device=self.device)
+        for l in range(cfg.num_hidden_layers):
+            self.cache.k[l][rows, :S] = tmp.k[l]
+            self.cache.v[l][rows, :S] = tmp.v[l]
+        self.cache.pos[rows] = lens
+        now = time.time()
+        for b, (slot, r) in enumerate(new):
+            self.slots[slot] = _Slot(r)
             self.stats["prompt_tokens_total"] += len(r.prompt_ids)
-            self.stats["generation_tokens_total"] += len(gen)
-            self.h_latency.observe(t1 - r.t_arrive)
-            if fan.first[i] is not None:
-                self.h_ttft.observe(fan.first[i] - r.t_arrive)
-            r.out.put(("final", {"text": text, "finish_reason": finish, "prompt_tokens": len(r.prompt_ids),
-                                 "completion_tokens": len(gen), "latency_s": t1 - r.t_arrive,
-                                 "batch_size": B, "decode_s": t1 - t0}))
+        toks = self._sample(logits, [s for s, _ in new])
+        for b, (slot, r) in enumerate(new):
+            self._accept(slot, int(toks[b]), now)
+        self.stats["batches_total"] += 1
+
+    def _sample(self, logits, slot_ids):
+        """Sample one token per row, grouping rows with identical sampling parameters."""
+        out = torch.empty(len(slot_ids), dtype=torch.long, device=self.device)
+        groups: dict = {}
+        for j, s in enumerate(slot_ids):
+            groups.setdefault(self.slots[s].req.params.key(), []).append(j)
+        for (temp, top_p, top_k, pen), js in groups.items():
+            idx = torch.tensor(js, device=self.device)
+            hist = None
+            if pen != 1.0:
+                L = max(len(self.slots[slot_ids[j]].req.prompt_ids) + len(self.slots[slot_ids[j]].gen) for j in js)
+                hist = torch.full((len(js), max(1, L)), -1, dtype=torch.int32)
+                for q, j in enumerate(js):
+                    s = self.slots[slot_ids[j]]
+                    seq = s.req.prompt_ids + s.gen
+                    hist[q, :len(seq)] = torch.tensor(seq, dtype=torch.int32)
+                hist = hist.to(self.device)
+            out[idx] = sample(logits[idx].float(), hist, temp, top_k, top_p, pen)
+        return out.tolist()
+
+    def _accept(self, slot: int, tok: int, now: float):
+        s = self.slots[slot]
+        if s.t_first is None:
+            s.t_first = now
+        p = s.req.params
+        if tok in self.eos and not p.ignore_eos:
+            s.done, s.finish = True, "stop"
+        else:
+            s.gen.append(tok)
+            if len(s.gen) >= p.max_tokens or len(s.req.prompt_ids) + len(s.gen) >= self.max_len - 1:
+                s.done, s.finish = True, "length"
+            if s.req.stream:
+                text = self.tok.decode(s.gen, skip_special_tokens=True)
+                if len(text) > s.sent and not text.endswith("�"):
+                    s.req.out.put(("delta", text[s.sent:]))
+                    s.sent = len(text)
+            if p.stop:
+                text = self.tok.decode(s.gen, skip_special_tokens=True)
+                if any(st and st in text for st in p.stop):
+                    s.done, s.finish = True, "stop"
+        if s.done:
+            self._finish(slot)
+        else:
+            self.next_tok[slot] = tok
+
+    def _finish(self, slot: int):
+        s = self.slots[slot]
+        r = s.req
+        text = self.tok.decode(s.gen, skip_special_tokens=True)
+        if r.params.stop:
+            cut = min((text.find(st) for st in r.params.stop if st and st in text), default=-1)
+            if cut >= 0:
+                text = text[:cut]
+        t1 = time.time()
+        self.stats["requests_total"] += 1
+        self.stats["generation_tokens_total"] += len(s.gen)
+        self.h_latency.observe(t1 - r.t_arrive)
+        if s.t_first is not None:
+            self.h_ttft.observe(s.t_first - r.t_arrive)
+        r.out.put(("final", {"text": text, "finish_reason": s.finish, "prompt_tokens": len(r.prompt_ids),
+                             "completion_tokens": len(s.gen), "latency_s": t1 - r.t_arrive,
+                             "ttft_s": (s.t_first or t1) - r.t_arrive}))
+        self.slots[slot] = None
+        self.cache.pos[slot] = 0
+        self.next_tok[slot] = self.pad
+
+    def _decode_step(self):
+        lm = self.lm
+        active = [i for i, s in enumerate(self.slots) if s is not None]
+        self.stats["running"] = len(active)
+        n = active[-1] + 1                       # slots fill lowest-first: decode rows [0, n) only
+        h = lm.model(self.next_tok[:n, None], None, self.cache.head_rows(n), None)   # per-row positions
+        free = [i for i in range(n) if self.slots[i] is None]
+        if free:                                                              # idle rows stay at position 0
+            self.cache.pos[torch.tensor(free, device=self.device)] = 0
+        rows = torch.tensor(active, device=self.device)
+        logits = h[rows] @ lm.lm_head.weight.t()
+        toks = self._sample(logits, active)
+        now = time.time()
+        for j, slot in enumerate(active):
+            self._accept(slot, int(toks[j]), now)
+        self.stats["decode_steps_total"] += 1
+        self.stats["running"] = sum(s is not None for s in self.slots)
 
     # ------------------------------------------------------------------ metrics
     def prometheus(self) -> str:
@@ -248,6 +349,7 @@ class ServingEngine:
             "# TYPE lipa_prompt_tokens_total counter", f"lipa_prompt_tokens_total {s['prompt_tokens_total']}",
             "# TYPE lipa_generation_tokens_total counter",
             f"lipa_generation_tokens_total {s['generation_tokens_total']}",
+            "# TYPE lipa_decode_steps_total counter", f"lipa_decode_steps_total {s['decode_steps_total']}",
             "# TYPE lipa_batches_total counter", f"lipa_batches_total {s['batches_total']}",
             "# TYPE lipa_num_requests_waiting gauge", f"lipa_num_requests_waiting {self.q.qsize()}",
             "# TYPE lipa_num_requests_running gauge", f"lipa_num_requests_running {s['running']}",

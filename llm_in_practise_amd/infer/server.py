@@ -13,8 +13,8 @@ with Pydantic request/response models, ``chatcmpl-<uuid>`` ids, a system message
   result;
 * optional ``X-API-KEY`` / ``Authorization: Bearer`` auth.
 
-Generation runs on the :class:`~llm_in_practise_amd.infer.engine.ServingEngine` worker, which
-batches concurrent requests into one decode.
+Generation runs on the :class:`~llm_in_practise_amd.infer.engine.ServingEngine` worker
+(continuous batching: requests join and leave the running decode batch every iteration).
 """
 from __future__ import annotations
 
@@ -46,6 +46,7 @@ class ChatCompletionRequest(BaseModel):
     max_tokens: int = Field(256, ge=1, le=32768)
     stream: bool = False
     stop: Optional[Union[str, list[str]]] = None
+    ignore_eos: bool = False
 
 
 class CompletionRequest(BaseModel):
@@ -58,6 +59,7 @@ class CompletionRequest(BaseModel):
     max_tokens: int = Field(256, ge=1, le=32768)
     stream: bool = False
     stop: Optional[Union[str, list[str]]] = None
+    ignore_eos: bool = False
 
 
 class ChoiceMessage(BaseModel):
@@ -89,7 +91,8 @@ class ChatCompletionResponse(BaseModel):
 def _params(req) -> SamplingParams:
     stop = [req.stop] if isinstance(req.stop, str) else req.stop
     return SamplingParams(max_tokens=req.max_tokens, temperature=req.temperature, top_p=req.top_p, top_k=req.top_k,
-                          repetition_penalty=req.repetition_penalty, stop=stop)
+                          repetition_penalty=req.repetition_penalty, stop=stop,
+                          ignore_eos=req.ignore_eos)
 
 
 def create_app(engine: ServingEngine, api_key: str | None = None, moderation=None) -> FastAPI:

@@ -166,6 +166,19 @@ class KVCache:
         self.k[layer][self._rows, self.pos] = k
         self.v[layer][self._rows, self.pos] = v
 
+    def head_rows(self, n: int) -> "KVCache":
+        """View of the first ``n`` rows sharing storage (and ``pos``) with this cache — the serving
+        engine decodes only up to its highest occupied slot."""
+        if n == self.batch:
+            return self
+        v = KVCache.__new__(KVCache)
+        v.k = [t[:n] for t in self.k]
+        v.v = [t[:n] for t in self.v]
+        v.len, v.max_len, v.batch = self.len, self.max_len, n
+        v.pos = self.pos[:n] if self.pos is not None else None
+        v._rows = self._rows[:n]
+        return v
+
     def start_decode(self, lens: torch.Tensor):
         self.pos = lens.to(torch.long).clone()
 

@@ -294,7 +294,7 @@ class ByteTokenizer:
         return list(s.encode("utf-8"))
 
     def decode(self, ids, skip_special_tokens=True):
-        return bytes(int(i) for i in ids).decode("utf-8", errors="replace")
+        return bytes(int(i) for i in ids if 0 <= int(i) < 256).decode("utf-8", errors="replace")
 
 
 def train_bpe_tokenizer(texts: Iterable[str], vocab_size: int = 3000, kind: str = "whitespace",

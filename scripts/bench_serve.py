@@ -16,9 +16,13 @@ delta ≈ one token for the OpenAI stream), or the server's ``usage`` when not s
 import argparse
 import asyncio
 import json
+import os
 import random
 import statistics
+import sys
 import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def mixed_dataset(n: int, seed: int = 0):
@@ -59,7 +63,8 @@ def pct(xs, p):
 async def one_request(client, url, model, msgs, max_tokens):
     t0 = time.perf_counter()
     ttft, last, itl, n = None, None, [], 0
-    body = {"model": model, "messages": msgs, "max_tokens": max_tokens, "stream": True, "temperature": 0.0}
+    body = {"model": model, "messages": msgs, "max_tokens": max_tokens, "stream": True, "temperature": 0.0,
+            "ignore_eos": True}
     async with client.stream("POST", url + "/v1/chat/completions", json=body, timeout=600) as r:
         async for line in r.aiter_lines():
             if not line.startswith("data: ") or line == "data: [DONE]":
@@ -96,8 +101,21 @@ async def run_level(url, model, prompts, conc, max_tokens):
             "req_per_s": round(len(res) / dur, 3), "output_tok_per_s": round(toks / dur, 1)}
 
 
-def start_inprocess(spec: str, port: int):
-    """Launch our server in a background thread with a random-init model and byte tokenizer."""
+class _SyntheticTokenizer:
+    """Random-init models emit ids over the whole vocabulary: encode prompts as bytes, decode each
+    id to exactly one printable character so one streamed delta = one token."""
+    eos_token_id = None
+    pad_token_id = 0
+
+    def encode(self, text, add_special_tokens=False):
+        return list(text.encode("utf-8"))
+
+    def decode(self, ids, skip_special_tokens=True):
+        return "".join(chr(0x4E00 + int(i) % 20000) for i in ids)
+
+
+def start_inprocess(spec: str, port: int, max_batch: int = 64):
+    """Launch our server in a background thread with a random-init model (synthetic tokenizer)."""
     import threading
 
     import uvicorn
@@ -105,10 +123,8 @@ def start_inprocess(spec: str, port: int):
     from llm_in_practise_amd.cli.main import _load_for_inference
     from llm_in_practise_amd.infer.engine import ServingEngine
     from llm_in_practise_amd.infer.server import create_app
-    from llm_in_practise_amd.train.data import ByteTokenizer
     m = _load_for_inference(spec)
-    tok = ByteTokenizer()
-    eng = ServingEngine(m, tok, model_name=spec, max_batch=64)
+    eng = ServingEngine(m, _SyntheticTokenizer(), model_name=spec, max_batch=max_batch, chat_template="chatml")
     cfg = uvicorn.Config(create_app(eng), host="127.0.0.1", port=port, log_level="warning")
     th = threading.Thread(target=uvicorn.Server(cfg).run, daemon=True)
     th.start()
@@ -127,8 +143,9 @@ def main():
     ap.add_argument("--max-tokens", type=int, default=256)
     ap.add_argument("--concurrency", type=int, nargs="+", default=[8])
     ap.add_argument("--out", default=None)
+    ap.add_argument("--max-batch", type=int, default=64)
     a = ap.parse_args()
-    url = a.url or start_inprocess(a.inprocess, a.port)
+    url = a.url or start_inprocess(a.inprocess, a.port, a.max_batch)
     prompts = mixed_dataset(a.num_prompts) if a.dataset == "mixed" else sharegpt(a.dataset, a.num_prompts)
     rows = [asyncio.run(run_level(url, a.model, prompts, c, a.max_tokens)) for c in a.concurrency]
     for r in rows:

@@ -94,3 +94,27 @@ def test_guard_app_and_server_precall_moderation(engine):
     r = c.post("/v1/chat/completions", json={"messages": [{"role": "user", "content": "hateful text"}],
                                              "max_tokens": 2})
     assert r.status_code == 400
+
+
+def test_continuous_batching_admits_midflight(engine):
+    """A request arriving while another is decoding joins the running batch (iteration-level
+    scheduling) and its greedy output equals a solo run; slots are recycled."""
+    p_long = SamplingParams(max_tokens=24, temperature=0.0)
+    p_short = SamplingParams(max_tokens=3, temperature=0.0)
+    solo_long = engine.complete("the quick brown fox", p_long)["text"]
+    solo_short = engine.complete("zz", p_short)["text"]
+    steps0 = engine.stats["decode_steps_total"]
+    r_long = engine.submit("the quick brown fox", p_long)
+    r_short = [engine.submit("zz", p_short) for _ in range(10)]   # more than max_batch in total
+    outs = []
+    for r in r_short + [r_long]:
+        while True:
+            kind, val = r.out.get(timeout=120)
+            if kind == "final":
+                outs.append(val)
+                break
+    assert all(o["text"] == solo_short for o in outs[:-1])
+    assert outs[-1]["text"] == solo_long
+    # all 11 requests shared decode steps: far fewer steps than running them one after another
+    assert engine.stats["decode_steps_total"] - steps0 < 24 + 10 * 3
+    assert all(s is None for s in engine.slots)
