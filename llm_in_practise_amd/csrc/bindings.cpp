@@ -77,6 +77,14 @@ hipStream_t stream() { return at::hip::getCurrentHIPStream().stream(); }
 #define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
 #define CHECK_BF16(x) TORCH_CHECK((x).scalar_type() == at::kBFloat16, #x " must be bf16")
 
+void launch_moe_route(int, const void*, int*, float*, float*, int, int, int, int, hipStream_t);
+void launch_moe_route_bwd(int, const float*, const float*, const int*, const float*, void*, int, int, int, int,
+                          hipStream_t);
+void launch_moe_permute(const int*, int, int, int*, int*, int*, hipStream_t);
+void launch_moe_gather(int, const void*, const int*, const float*, void*, int, int, int, hipStream_t);
+void launch_moe_combine(int, const void*, const int*, const float*, const void*, void*, int, int, int, hipStream_t);
+void launch_moe_wgrad(int, const void*, const void*, const int*, float*, int, int, int, hipStream_t);
+
 int dtype_code(const Tensor& t) {
   if (t.scalar_type() == at::kBFloat16) return 1;
   TORCH_CHECK(t.scalar_type() == at::kFloat, "expected fp32 or bf16, got ", t.scalar_type());
@@ -593,9 +601,90 @@ Tensor sample(Tensor logits, optional<Tensor> hist, double temperature, int64_t 
 
 }  // namespace
 
+
+// ---- MoE routing / dispatch (moe.hip)
+std::vector<Tensor> moe_route(Tensor logits, int64_t k, int64_t mode, bool want_probs) {
+  CHECK_CONTIG(logits);
+  TORCH_CHECK(logits.dim() == 2 && logits.size(1) <= 64 && k >= 1 && k <= 8 && k <= logits.size(1),
+              "moe_route: logits [T, E<=64], 1<=k<=min(8,E)");
+  const int T = logits.size(0), E = logits.size(1);
+  auto oi = logits.options();
+  Tensor idx = torch::empty({T, k}, oi.dtype(at::kInt));
+  Tensor w = torch::empty({T, k}, oi.dtype(at::kFloat));
+  Tensor probs = want_probs ? torch::empty({T, E}, oi.dtype(at::kFloat)) : Tensor();
+  if (T) launch_moe_route(dtype_code(logits), logits.data_ptr(), idx.data_ptr<int>(), w.data_ptr<float>(),
+                          want_probs ? probs.data_ptr<float>() : nullptr, T, E, k, mode, stream());
+  return {idx, w, probs};
+}
+
+Tensor moe_route_bwd(Tensor dw, Tensor w, Tensor idx, optional<Tensor> probs, int64_t E, int64_t mode,
+                     at::ScalarType dt) {
+  CHECK_CONTIG(dw); CHECK_CONTIG(w); CHECK_CONTIG(idx);
+  TORCH_CHECK(dw.scalar_type() == at::kFloat && w.scalar_type() == at::kFloat && idx.scalar_type() == at::kInt,
+              "moe_route_bwd: dtypes");
+  TORCH_CHECK(mode == 0 || (probs.has_value() && probs->is_contiguous()), "moe_route_bwd: mode 1 needs probs");
+  const int T = idx.size(0), k = idx.size(1);
+  Tensor dl = torch::empty({T, E}, dw.options().dtype(dt));
+  if (T) launch_moe_route_bwd(dtype_code(dl), dw.data_ptr<float>(), w.data_ptr<float>(), idx.data_ptr<int>(),
+                              mode == 1 ? probs->data_ptr<float>() : nullptr, dl.data_ptr(), T, E, k, mode, stream());
+  return dl;
+}
+
+std::vector<Tensor> moe_permute(Tensor ids, int64_t E) {
+  CHECK_CONTIG(ids);
+  TORCH_CHECK(ids.scalar_type() == at::kInt && ids.numel() < (1 << 24), "moe_permute: int32 ids, < 2^24 pairs");
+  const int P = ids.numel();
+  auto o = ids.options();
+  Tensor pos_of = torch::empty({P}, o), perm = torch::empty({P}, o), offsets = torch::empty({E + 1}, o);
+  launch_moe_permute(ids.data_ptr<int>(), P, E, pos_of.data_ptr<int>(), perm.data_ptr<int>(),
+                     offsets.data_ptr<int>(), stream());
+  return {pos_of, perm, offsets};
+}
+
+Tensor moe_gather(Tensor x, Tensor perm, int64_t k, optional<Tensor> w) {
+  CHECK_CONTIG(x); CHECK_CONTIG(perm);
+  TORCH_CHECK(x.dim() == 2 && x.size(1) % 8 == 0 && perm.scalar_type() == at::kInt, "moe_gather: x [T, H%8==0]");
+  if (w.has_value()) TORCH_CHECK(w->is_contiguous() && w->scalar_type() == at::kFloat, "moe_gather: w fp32");
+  const int R = perm.numel(), H = x.size(1);
+  Tensor out = torch::empty({R, H}, x.options());
+  if (R) launch_moe_gather(dtype_code(x), x.data_ptr(), perm.data_ptr<int>(), w.has_value() ? w->data_ptr<float>() : nullptr,
+                           out.data_ptr(), R, H, k, stream());
+  return out;
+}
+
+Tensor moe_combine(Tensor ys, Tensor pos_of, int64_t k, optional<Tensor> w, optional<Tensor> base) {
+  CHECK_CONTIG(ys); CHECK_CONTIG(pos_of);
+  TORCH_CHECK(ys.dim() == 2 && ys.size(1) % 8 == 0 && pos_of.scalar_type() == at::kInt && pos_of.numel() % k == 0,
+              "moe_combine: ys [R, H%8==0], pos_of int32 [T*k]");
+  if (w.has_value()) TORCH_CHECK(w->is_contiguous() && w->scalar_type() == at::kFloat, "moe_combine: w fp32");
+  if (base.has_value()) TORCH_CHECK(base->is_contiguous() && base->scalar_type() == ys.scalar_type(), "moe_combine: base");
+  const int T = pos_of.numel() / k, H = ys.size(1);
+  Tensor out = torch::empty({T, H}, ys.options());
+  if (T) launch_moe_combine(dtype_code(ys), ys.data_ptr(), pos_of.data_ptr<int>(),
+                            w.has_value() ? w->data_ptr<float>() : nullptr, optr(base), out.data_ptr(), T, H, k, stream());
+  return out;
+}
+
+Tensor moe_wgrad(Tensor dout, Tensor ys, Tensor pos_of, int64_t k) {
+  CHECK_CONTIG(dout); CHECK_CONTIG(ys); CHECK_CONTIG(pos_of);
+  TORCH_CHECK(dout.scalar_type() == ys.scalar_type() && dout.size(1) == ys.size(1) && ys.size(1) % 8 == 0,
+              "moe_wgrad: shapes");
+  const int T = dout.size(0), H = dout.size(1);
+  Tensor dw = torch::empty({T, k}, dout.options().dtype(at::kFloat));
+  if (T) launch_moe_wgrad(dtype_code(ys), dout.data_ptr(), ys.data_ptr(), pos_of.data_ptr<int>(), dw.data_ptr<float>(),
+                          T, H, k, stream());
+  return dw;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "llm_in_practise_amd gfx950 (MI355X / CDNA4) kernels";
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("moe_route", &moe_route);
+  m.def("moe_route_bwd", &moe_route_bwd);
+  m.def("moe_permute", &moe_permute);
+  m.def("moe_gather", &moe_gather);
+  m.def("moe_combine", &moe_combine);
+  m.def("moe_wgrad", &moe_wgrad);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);

@@ -21,6 +21,7 @@ import torch.nn.functional as F
 from ..ops import reference as ref
 from ..ops.activation import gelu
 from ..ops.attention import sdpa_bshd
+from ..ops.moe import moe_combine, moe_dispatch, moe_gather, moe_route
 from ..ops.norm import LayerNorm
 
 
@@ -409,23 +410,19 @@ class MoEFeedForward(nn.Module):
     def route(self, x_flat):
         logits = self.router(x_flat)
         k = min(self.top_k, self.num_experts)
-        if self.routing == "softmax_topk":
-            probs = F.softmax(logits, -1)
-            w, idx = probs.topk(k, -1)
-        else:
-            top, idx = logits.topk(k, -1)
-            w = F.softmax(top, -1)
+        w, idx = moe_route(logits, k, self.routing)
         self.last_router_probs = F.softmax(logits.float(), -1)
         return w, idx
 
     def forward(self, x):
         shape = x.shape
         xf = x.reshape(-1, shape[-1])
-        out = torch.zeros_like(xf)
+        shared = None
         if self.num_shared:
-            out = out + sum(e(xf) for e in self.shared_experts) / self.num_shared
+            shared = sum(e(xf) for e in self.shared_experts) / self.num_shared
         w, idx = self.route(xf)
         if self.dispatch == "dense":
+            out = torch.zeros_like(xf) if shared is None else shared
             for j in range(idx.shape[1]):
                 eo = torch.zeros_like(xf)
                 for e, expert in enumerate(self.experts):
@@ -433,20 +430,17 @@ class MoEFeedForward(nn.Module):
                     eo = eo + m * expert(xf)
                 out = out + eo * w[:, j:j + 1].to(xf.dtype)
         else:
-            T, k = idx.shape
-            flat_e = idx.reshape(-1)
-            order = torch.argsort(flat_e, stable=True)               # sort (token, slot) pairs by expert
-            tok = order // k
-            counts = torch.bincount(flat_e, minlength=self.num_experts).tolist()
-            xs = xf.index_select(0, tok)
-            ws = w.reshape(-1).index_select(0, order).to(xf.dtype)
+            # expert-sorted dispatch (ops/moe.py: HIP routing/permute/gather/combine kernels);
+            # one host read of the segment offsets drives the per-expert GEMMs
+            d = moe_dispatch(idx, self.num_experts)
+            xs = moe_gather(xf, d)
             ys, s = [], 0
-            for e, c in enumerate(counts):
+            for e, c in enumerate(d.counts()):
                 if c:
                     ys.append(self.experts[e](xs[s:s + c]))
                 s += c
-            y = torch.cat(ys, 0) * ws[:, None]
-            out = out.index_add(0, tok, y)
+            y = torch.cat(ys, 0) if ys else xs
+            out = moe_combine(y, d, w, shared)
         return self.dropout(out.view(shape))
 
 
