@@ -234,7 +234,7 @@ def cmd_finetune(a):
 
 
 # ============================================================================ inference / quant
-def _load_for_inference(path, adapter=None, device=None, quant=None):
+def _load_for_inference(path, adapter=None, device=None, quant=None, fuse=True):
     from ..models.qwen3 import BitsAndBytesConfig, Qwen3ForCausalLM, qwen3_config
     dev = device or _device()
     if path.startswith("random:"):
@@ -251,6 +251,12 @@ def _load_for_inference(path, adapter=None, device=None, quant=None):
     if adapter:
         from ..peft.lora import PeftModel
         m = PeftModel.from_pretrained(m, adapter)
+    m.requires_grad_(False)
+    lm = m
+    while not hasattr(lm, "fuse_projections") and hasattr(lm, "model"):
+        lm = lm.model
+    if fuse and hasattr(lm, "fuse_projections"):
+        lm.fuse_projections()          # q|k|v and gate|up as single GEMMs (frozen weights)
     return m.eval()
 
 
@@ -316,13 +322,13 @@ def _calib_ids(a, tok, vocab, device):
     return [torch.randint(0, vocab, (1, a.calib_len), generator=g).to(device) for _ in range(a.n_calib)]
 
 
-def cmd_quantize(a):
+def cmd_quantize(a):  # calibration hooks need the unfused Linear modules
     from ..quant.awq import awq_quantize_model
     from ..quant.gptq import gptq_quantize_model, replace_with_int4
     from ..quant.int4 import quantize_rtn
     from ..quant.io import save_quantized
     dev = _device(a.device)
-    m = _load_for_inference(a.model, device=dev)
+    m = _load_for_inference(a.model, device=dev, fuse=False)
     tok = None
     if not a.model.startswith("random:"):
         try:
@@ -349,7 +355,7 @@ def cmd_eval_quant(a):
     from ..quant.eval import PASS_THRESHOLD, self_ppl
     from ..train.data import load_text_corpus, load_tokenizer
     dev = _device()
-    m = _load_for_inference(a.model, device=dev)
+    m = _load_for_inference(a.model, device=dev, fuse=False)
     tok = load_tokenizer(a.tokenizer or a.model) if not a.model.startswith("random:") else None
     if a.prompts and tok is not None:
         prompts = [torch.tensor(tok.encode(t)[:256], device=dev) for t in load_text_corpus(a.prompts)[a.start:a.end]]

@@ -55,6 +55,13 @@ void launch_gemv_w4(int, const void*, int, const uint8_t*, const float*, const f
                     int, hipStream_t);
 void launch_lora_proj(const void*, int, const void*, int, int, float*, int, void*, int, int, uint64_t, float, float,
                       size_t, hipStream_t);
+void launch_moe_route(int, const void*, int*, float*, float*, int, int, int, int, hipStream_t);
+void launch_moe_route_bwd(int, const float*, const float*, const int*, const float*, void*, int, int, int, int,
+                          hipStream_t);
+void launch_moe_permute(const int*, int, int, int*, int*, int*, hipStream_t);
+void launch_moe_gather(int, const void*, const int*, const float*, void*, int, int, int, hipStream_t);
+void launch_moe_combine(int, const void*, const int*, const float*, const void*, void*, int, int, int, hipStream_t);
+void launch_moe_wgrad(int, const void*, const void*, const int*, float*, int, int, int, hipStream_t);
 int lora_acc_chunks(int M);
 void launch_lora_acc(const float*, int, int, const void*, int, void*, int, const void*, int, float*, int64_t, int64_t,
                      float*, int, uint64_t, float, size_t, hipStream_t);
@@ -77,13 +84,6 @@ hipStream_t stream() { return at::hip::getCurrentHIPStream().stream(); }
 #define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
 #define CHECK_BF16(x) TORCH_CHECK((x).scalar_type() == at::kBFloat16, #x " must be bf16")
 
-void launch_moe_route(int, const void*, int*, float*, float*, int, int, int, int, hipStream_t);
-void launch_moe_route_bwd(int, const float*, const float*, const int*, const float*, void*, int, int, int, int,
-                          hipStream_t);
-void launch_moe_permute(const int*, int, int, int*, int*, int*, hipStream_t);
-void launch_moe_gather(int, const void*, const int*, const float*, void*, int, int, int, hipStream_t);
-void launch_moe_combine(int, const void*, const int*, const float*, const void*, void*, int, int, int, hipStream_t);
-void launch_moe_wgrad(int, const void*, const void*, const int*, float*, int, int, int, hipStream_t);
 
 int dtype_code(const Tensor& t) {
   if (t.scalar_type() == at::kBFloat16) return 1;

@@ -107,12 +107,14 @@ def _unwrap_lm(model):
 class ServingEngine:
     def __init__(self, model, tokenizer, model_name: str = "lipa-model", max_batch: int = 16,
                  system_prompt: str | None = None, chat_template: str = "auto", space_before_end: bool = False,
-                 max_model_len: int | None = None, max_prefill_batch: int = 8):
+                 max_model_len: int | None = None, max_prefill_batch: int = 16, prefill_token_budget: int = 8192,
+                 use_graphs: bool | None = None):
         self.model, self.tok, self.model_name = model, tokenizer, model_name
         self.lm = _unwrap_lm(model)
         self.lm.eval()
         self.max_batch = max_batch
         self.max_prefill_batch = max_prefill_batch
+        self.prefill_token_budget = prefill_token_budget
         self.system_prompt = system_prompt
         self.chat_template = chat_template
         self.space_before_end = space_before_end
@@ -143,6 +145,14 @@ class ServingEngine:
         self.cache.pos = torch.zeros(max_batch, dtype=torch.long, device=self.device)
         self.slots: list[_Slot | None] = [None] * max_batch
         self.next_tok = torch.full((max_batch,), self.pad, dtype=torch.long, device=self.device)
+        self.graphs = None
+        if use_graphs is None:
+            use_graphs = self.device.type == "cuda"
+        if use_graphs:                     # one hipGraph per batch bucket (infer/graphs.py)
+            from .graphs import DecodeGraphs
+            with torch.no_grad():
+                self.graphs = DecodeGraphs(self.lm, self.cache, max_batch, tokens=self.next_tok)
+        self._held: _Request | None = None
         self._stop = False
         self._worker = threading.Thread(target=self._loop, daemon=True)
         self._worker.start()
@@ -210,14 +220,22 @@ class ServingEngine:
         free = [i for i, s in enumerate(self.slots) if s is None]
         new = []
         block = not active
+        budget = self.prefill_token_budget
         while free and len(new) < self.max_prefill_batch:
-            try:
-                r = self.q.get(block=block, timeout=None if block else 0)
-            except queue.Empty:
-                break
+            if self._held is not None:
+                r, self._held = self._held, None
+            else:
+                try:
+                    r = self.q.get(block=block, timeout=None if block else 0)
+                except queue.Empty:
+                    break
             block = False
             if r is None:
                 return
+            if new and len(r.prompt_ids) > budget:      # over the prefill token budget: next iteration
+                self._held = r
+                break
+            budget -= len(r.prompt_ids)
             new.append((free.pop(0), r))
         with self.lock, torch.no_grad():
             if new:
@@ -252,19 +270,21 @@ class ServingEngine:
         for b, (slot, r) in enumerate(new):
             self.slots[slot] = _Slot(r)
             self.stats["prompt_tokens_total"] += len(r.prompt_ids)
-        toks = self._sample(logits, [s for s, _ in new])
+        dev_toks, toks = self._sample(logits, [s for s, _ in new])
+        self.next_tok[rows] = dev_toks
         for b, (slot, r) in enumerate(new):
-            self._accept(slot, int(toks[b]), now)
+            self._accept(slot, toks[b], now)
         self.stats["batches_total"] += 1
 
     def _sample(self, logits, slot_ids):
-        """Sample one token per row, grouping rows with identical sampling parameters."""
+        """Sample one token per row, grouping rows with identical sampling parameters.
+        Returns (device tensor, host list)."""
         out = torch.empty(len(slot_ids), dtype=torch.long, device=self.device)
         groups: dict = {}
         for j, s in enumerate(slot_ids):
             groups.setdefault(self.slots[s].req.params.key(), []).append(j)
         for (temp, top_p, top_k, pen), js in groups.items():
-            idx = torch.tensor(js, device=self.device)
+            idx = None if len(groups) == 1 else torch.tensor(js, device=self.device)
             hist = None
             if pen != 1.0:
                 L = max(len(self.slots[slot_ids[j]].req.prompt_ids) + len(self.slots[slot_ids[j]].gen) for j in js)
@@ -274,8 +294,11 @@ class ServingEngine:
                     seq = s.req.prompt_ids + s.gen
                     hist[q, :len(seq)] = torch.tensor(seq, dtype=torch.int32)
                 hist = hist.to(self.device)
-            out[idx] = sample(logits[idx].float(), hist, temp, top_k, top_p, pen)
-        return out.tolist()
+            if idx is None:
+                out = sample(logits.float(), hist, temp, top_k, top_p, pen)
+            else:
+                out[idx] = sample(logits[idx].float(), hist, temp, top_k, top_p, pen)
+        return out, out.tolist()
 
     def _accept(self, slot: int, tok: int, now: float):
         s = self.slots[slot]
@@ -299,8 +322,6 @@ class ServingEngine:
                     s.done, s.finish = True, "stop"
         if s.done:
             self._finish(slot)
-        else:
-            self.next_tok[slot] = tok
 
     def _finish(self, slot: int):
         s = self.slots[slot]
@@ -321,23 +342,29 @@ class ServingEngine:
                              "ttft_s": (s.t_first or t1) - r.t_arrive}))
         self.slots[slot] = None
         self.cache.pos[slot] = 0
-        self.next_tok[slot] = self.pad
 
     def _decode_step(self):
         lm = self.lm
         active = [i for i, s in enumerate(self.slots) if s is not None]
         self.stats["running"] = len(active)
         n = active[-1] + 1                       # slots fill lowest-first: decode rows [0, n) only
-        h = lm.model(self.next_tok[:n, None], None, self.cache.head_rows(n), None)   # per-row positions
+        if self.graphs is not None:              # hipGraph replay of the whole step (bucket >= n rows)
+            n = self.graphs.bucket(n)
+            logits = self.graphs.step(None, n)
+        else:
+            h = lm.model(self.next_tok[:n, None], None, self.cache.head_rows(n), None)   # per-row positions
+            logits = h @ lm.lm_head.weight.t()
         free = [i for i in range(n) if self.slots[i] is None]
         if free:                                                              # idle rows stay at position 0
             self.cache.pos[torch.tensor(free, device=self.device)] = 0
         rows = torch.tensor(active, device=self.device)
-        logits = h[rows] @ lm.lm_head.weight.t()
-        toks = self._sample(logits, active)
+        if len(active) != n:
+            logits = logits[rows]
+        dev_toks, toks = self._sample(logits, active)
+        self.next_tok[rows] = dev_toks
         now = time.time()
         for j, slot in enumerate(active):
-            self._accept(slot, int(toks[j]), now)
+            self._accept(slot, toks[j], now)
         self.stats["decode_steps_total"] += 1
         self.stats["running"] = sum(s is not None for s in self.slots)
 

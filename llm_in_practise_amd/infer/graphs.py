@@ -35,12 +35,13 @@ class DecodeGraphs:
     ``step(tokens, n)`` runs rows ``[0, bucket(n))`` and returns logits ``[bucket, V]`` (a static
     buffer, valid until the next call)."""
 
-    def __init__(self, lm, cache: KVCache, max_batch: int | None = None, buckets: list[int] | None = None):
+    def __init__(self, lm, cache: KVCache, max_batch: int | None = None, buckets: list[int] | None = None,
+                 tokens: torch.Tensor | None = None):
         self.lm, self.cache = lm, cache
         self.max_batch = max_batch or cache.batch
         self.buckets = buckets or _buckets(self.max_batch)
         dev = cache.k[0].device
-        self.tokens = torch.zeros(self.max_batch, dtype=torch.long, device=dev)
+        self.tokens = tokens if tokens is not None else torch.zeros(self.max_batch, dtype=torch.long, device=dev)
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.logits: dict[int, torch.Tensor] = {}
         self.pool = None
@@ -75,8 +76,10 @@ class DecodeGraphs:
                 return b
         raise ValueError(f"batch {n} > max_batch {self.max_batch}")
 
-    def step(self, tokens: torch.Tensor, n: int) -> torch.Tensor:
+    def step(self, tokens: torch.Tensor | None, n: int) -> torch.Tensor:
+        """``tokens=None``: the caller already wrote the static ``self.tokens`` buffer."""
         b = self.bucket(n)
-        self.tokens[:tokens.shape[0]].copy_(tokens)
+        if tokens is not None:
+            self.tokens[:tokens.shape[0]].copy_(tokens)
         self.graphs[b].replay()
         return self.logits[b]

@@ -15,7 +15,8 @@ import torch  # noqa: E402
 
 from llm_in_practise_amd.infer.graphs import DecodeGraphs  # noqa: E402
 from llm_in_practise_amd.models.common import KVCache  # noqa: E402
-from llm_in_practise_amd.models.qwen3 import BitsAndBytesConfig, Qwen3ForCausalLM, qwen3_config  # noqa: E402
+from llm_in_practise_amd.models.qwen3 import Qwen3ForCausalLM, qwen3_config  # noqa: E402
+from llm_in_practise_amd.peft.lora import quantize_model_nf4  # noqa: E402
 
 
 def main():
@@ -29,9 +30,11 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     a = ap.parse_args()
     dev = "cuda"
-    q = BitsAndBytesConfig(load_in_4bit=True) if a.nf4 else None
-    lm = Qwen3ForCausalLM.from_config(qwen3_config(a.model), dtype=torch.bfloat16, device=dev,
-                                      quantization_config=q).eval()
+    lm = Qwen3ForCausalLM.from_config(qwen3_config(a.model), dtype=torch.bfloat16, device=dev).eval()
+    lm.requires_grad_(False)
+    if a.nf4:
+        quantize_model_nf4(lm)
+    lm.fuse_projections()
     cfg = lm.config
     B = max(a.batches)
     cache = KVCache(cfg.num_hidden_layers, B, a.max_len, cfg.num_key_value_heads, cfg.head_dim, torch.bfloat16, dev)
