@@ -17,12 +17,14 @@
 // counter-based RNG (splitmix64 of (key, row)) with a block prefix scan.  Greedy = argmax.
 #include "common.h"
 
+#include <algorithm>
+
 using namespace lipa;
 
 namespace {
 
-constexpr int DEC_CHUNK = 128;  // keys per workgroup
 constexpr int DEC_THR = 256;
+constexpr int DEC_TARGET_WG = 2048;   // ≈ 8 workgroups per CU in flight
 
 template <int D, int G>
 __global__ __launch_bounds__(DEC_THR) void decode_attn_partial_k(const bf16* __restrict__ q,
@@ -30,15 +32,17 @@ __global__ __launch_bounds__(DEC_THR) void decode_attn_partial_k(const bf16* __r
                                                                  const bf16* __restrict__ vc,
                                                                  const int* __restrict__ lens, float* __restrict__ opart,
                                                                  float* __restrict__ mpart, float* __restrict__ lpart,
-                                                                 int Smax, int hq, int hkv, int nsplit, float scale) {
-  constexpr int LPK = D / 8;          // lanes per key row
+                                                                 int Smax, int hq, int hkv, int nsplit, int chunk,
+                                                                 float scale) {
+  constexpr int LPK = D / 8;          // lanes per key row (16 B each)
   constexpr int KPW = 64 / LPK;       // keys per wave step
-  constexpr int NSLOT = 4 * KPW;      // key slots per workgroup
+  constexpr int NSLOT = 4 * KPW;      // keys per workgroup step
   const int split = blockIdx.x, kh = blockIdx.y, b = blockIdx.z;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int slot = w * KPW + lane / LPK, e = lane % LPK;  // e: which 8-element piece of the row
+  const int sw = lane / LPK, e = lane % LPK;   // key slot within the wave, 8-element piece of the row
   const int len = lens[b];
-  const int k0 = split * DEC_CHUNK, k1 = min(k0 + DEC_CHUNK, len);
+  const int k0 = split * chunk, k1 = min(k0 + chunk, len);
+  if (k0 >= len) return;              // empty split: the merge kernel never reads it
 
   float qf[G][8];
 #pragma unroll
@@ -58,9 +62,8 @@ __global__ __launch_bounds__(DEC_THR) void decode_attn_partial_k(const bf16* __r
   const size_t row_stride = (size_t)hkv * D;
   const bf16* kb = kc + (size_t)b * Smax * row_stride + kh * D + e * 8;
   const bf16* vb = vc + (size_t)b * Smax * row_stride + kh * D + e * 8;
-  for (int t = k0 + slot; t < k1; t += NSLOT) {
-    const bf16x8 kv = *reinterpret_cast<const bf16x8*>(kb + (size_t)t * row_stride);
-    const bf16x8 vv = *reinterpret_cast<const bf16x8*>(vb + (size_t)t * row_stride);
+
+  auto consume = [&](const bf16x8& kv, const bf16x8& vv) {
     float s[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -80,27 +83,59 @@ __global__ __launch_bounds__(DEC_THR) void decode_attn_partial_k(const bf16* __r
       for (int j = 0; j < 8; ++j) acc[g][j] = acc[g][j] * c + p * (float)vv[j];
       m[g] = mn;
     }
+  };
+  // two keys per lane-slot in flight: both K/V pairs are loaded before either is consumed
+  const int my0 = k0 + w * KPW + sw;
+  int t = my0;
+  for (; t + NSLOT < k1; t += 2 * NSLOT) {
+    const bf16x8 ka = *reinterpret_cast<const bf16x8*>(kb + (size_t)t * row_stride);
+    const bf16x8 va = *reinterpret_cast<const bf16x8*>(vb + (size_t)t * row_stride);
+    const bf16x8 kb2 = *reinterpret_cast<const bf16x8*>(kb + (size_t)(t + NSLOT) * row_stride);
+    const bf16x8 vb2 = *reinterpret_cast<const bf16x8*>(vb + (size_t)(t + NSLOT) * row_stride);
+    consume(ka, va);
+    consume(kb2, vb2);
   }
-  // merge the NSLOT slots through LDS: [slot][g] stats, [slot][g][D] accumulators
-  __shared__ float sm[NSLOT][G], sl[NSLOT][G];
-  __shared__ float sacc[NSLOT][G][D];
+  if (t < k1) {
+    const bf16x8 ka = *reinterpret_cast<const bf16x8*>(kb + (size_t)t * row_stride);
+    const bf16x8 va = *reinterpret_cast<const bf16x8*>(vb + (size_t)t * row_stride);
+    consume(ka, va);
+  }
+  // merge the KPW slots of this wave with xor shuffles (lanes LPK apart hold the same piece e)
 #pragma unroll
-  for (int g = 0; g < G; ++g) {
-    if (e == 0) {
-      sm[slot][g] = m[g];
-      sl[slot][g] = l[g];
+  for (int o = LPK; o < 64; o <<= 1) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float mo = __shfl_xor(m[g], o, 64), lo = __shfl_xor(l[g], o, 64);
+      const float mn = fmaxf(m[g], mo);
+      const float c0 = mn == -INFINITY ? 0.f : __expf(m[g] - mn), c1 = mn == -INFINITY ? 0.f : __expf(mo - mn);
+      l[g] = l[g] * c0 + lo * c1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[g][j] = acc[g][j] * c0 + __shfl_xor(acc[g][j], o, 64) * c1;
+      m[g] = mn;
     }
+  }
+  // then the 4 waves through LDS
+  __shared__ float sm[4][G], sl[4][G];
+  __shared__ float sacc[4][G][D];
+  if (sw == 0) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) sacc[slot][g][e * 8 + j] = acc[g][j];
+    for (int g = 0; g < G; ++g) {
+      if (e == 0) {
+        sm[w][g] = m[g];
+        sl[w][g] = l[g];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sacc[w][g][e * 8 + j] = acc[g][j];
+    }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < G * D; i += DEC_THR) {
     const int g = i / D, d = i % D;
-    float M = -INFINITY;
-    for (int s2 = 0; s2 < NSLOT; ++s2) M = fmaxf(M, sm[s2][g]);
+    const float M = fmaxf(fmaxf(sm[0][g], sm[1][g]), fmaxf(sm[2][g], sm[3][g]));
     float L = 0.f, A = 0.f;
     if (M != -INFINITY) {
-      for (int s2 = 0; s2 < NSLOT; ++s2) {
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
         const float c = __expf(sm[s2][g] - M);
         L += sl[s2][g] * c;
         A += sacc[s2][g][d] * c;
@@ -118,15 +153,17 @@ __global__ __launch_bounds__(DEC_THR) void decode_attn_partial_k(const bf16* __r
 template <int D>
 __global__ __launch_bounds__(D) void decode_attn_merge_k(const float* __restrict__ opart,
                                                          const float* __restrict__ mpart,
-                                                         const float* __restrict__ lpart, bf16* __restrict__ out,
-                                                         int nsplit) {
+                                                         const float* __restrict__ lpart, const int* __restrict__ lens,
+                                                         bf16* __restrict__ out, int hq, int nsplit, int chunk) {
   const size_t h = blockIdx.x;  // b*hq + head
   const int d = threadIdx.x;
+  const int len = lens[h / hq];
+  const int nv = min(nsplit, (len + chunk - 1) / chunk);   // splits that wrote partials
   float M = -INFINITY;
-  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, mpart[h * nsplit + s]);
+  for (int s = 0; s < nv; ++s) M = fmaxf(M, mpart[h * nsplit + s]);
   float L = 0.f, A = 0.f;
   if (M != -INFINITY) {
-    for (int s = 0; s < nsplit; ++s) {
+    for (int s = 0; s < nv; ++s) {
       const float c = __expf(mpart[h * nsplit + s] - M);
       L += lpart[h * nsplit + s] * c;
       A += opart[(h * nsplit + s) * D + d] * c;
@@ -261,14 +298,27 @@ __global__ __launch_bounds__(SMP_THR) void sample_k(const T* __restrict__ logits
 
 }  // namespace
 
+// Split-K plan: enough (split, kv-head, sequence) workgroups to fill the chip, each split a
+// multiple of 64 keys; depends only on (B, hkv, max_len) so a captured hipGraph stays valid
+// as the live lengths grow.
+void decode_split_plan(int B, int hkv, int max_len, int* nsplit, int* chunk) {
+  const int pairs = std::max(1, B * hkv);
+  int ns = std::max(1, (DEC_TARGET_WG + pairs - 1) / pairs);
+  ns = std::min(ns, std::max(1, (max_len + 63) / 64));
+  int ch = (max_len + ns - 1) / ns;
+  ch = (ch + 63) / 64 * 64;
+  *chunk = ch;
+  *nsplit = (max_len + ch - 1) / ch;
+}
+
 void launch_decode_attention(const void* q, const void* kc, const void* vc, const int* lens, float* opart, float* mpart,
-                             float* lpart, void* out, int B, int Smax, int hq, int hkv, int d, int nsplit, float scale,
-                             hipStream_t st) {
+                             float* lpart, void* out, int B, int Smax, int hq, int hkv, int d, int nsplit, int chunk,
+                             float scale, hipStream_t st) {
   const int G = hq / hkv;
   dim3 grid(nsplit, hkv, B);
 #define P(D_, G_)                                                                                           \
   decode_attn_partial_k<D_, G_><<<grid, DEC_THR, 0, st>>>((const bf16*)q, (const bf16*)kc, (const bf16*)vc, \
-                                                          lens, opart, mpart, lpart, Smax, hq, hkv, nsplit, scale)
+                                                          lens, opart, mpart, lpart, Smax, hq, hkv, nsplit, chunk, scale)
 #define GS(D_)                          \
   switch (G) {                          \
     case 1: P(D_, 1); break;            \
@@ -282,13 +332,11 @@ void launch_decode_attention(const void* q, const void* kc, const void* vc, cons
 #undef GS
 #undef P
   if (d == 128)
-    decode_attn_merge_k<128><<<B * hq, 128, 0, st>>>(opart, mpart, lpart, (bf16*)out, nsplit);
+    decode_attn_merge_k<128><<<B * hq, 128, 0, st>>>(opart, mpart, lpart, lens, (bf16*)out, hq, nsplit, chunk);
   else
-    decode_attn_merge_k<64><<<B * hq, 64, 0, st>>>(opart, mpart, lpart, (bf16*)out, nsplit);
+    decode_attn_merge_k<64><<<B * hq, 64, 0, st>>>(opart, mpart, lpart, lens, (bf16*)out, hq, nsplit, chunk);
   LIPA_CHECK_LAUNCH();
 }
-
-int decode_chunk() { return DEC_CHUNK; }
 
 void launch_sample(int dtype, const void* logits, const int* hist, int hist_len, float* work, int64_t* out, int B, int V,
                    float temperature, int top_k, float top_p, float penalty, uint64_t key, hipStream_t st) {

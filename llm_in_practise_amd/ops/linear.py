@@ -67,6 +67,14 @@ def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
             return y
         cf, _, at = base.kernel_pack()
         return native().gemm_nf4(x, cf, at, base.shape[0], ext_a, ext_b, residual)
+    if x.shape[0] <= 256:
+        # decode / small batch: the 128-column tiles give too few workgroups to stream the
+        # weights (N/128 WGs), hipBLASLt's split-K skinny kernels reach 2.6-6 TB/s here
+        # (profiles/decode_skinny_gemm.txt); residual folded in as addmm's beta term
+        y = torch.addmm(residual, x, base.t()) if residual is not None else x @ base.t()
+        if ext_a is not None:
+            y.addmm_(ext_a, ext_b.t())
+        return y
     return native().gemm_bf16(x, base, ext_a, ext_b, residual)
 
 

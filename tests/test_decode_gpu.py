@@ -70,3 +70,18 @@ def test_generate_qwen3_gpu_kv_cache_matches_recompute(native_ext):
             ids = torch.cat([ids, m(ids).logits[:, -1].float().argmax(-1, keepdim=True)], 1)
     # bf16 rounding can flip near-ties late in the sequence; the first tokens must agree
     assert torch.equal(out[0, :37], ids[0, :37])
+
+
+@pytest.mark.parametrize("B,max_len", [(64, 4096), (1, 1024), (7, 3000)])
+def test_decode_attention_split_plans(native_ext, B, max_len):
+    """Batch sizes that select different split plans (1 split per head up to 64-key chunks)."""
+    torch.manual_seed(B)
+    hq, hkv, d, Smax = 32, 8, 128, 4096
+    kc = torch.randn(B, Smax, hkv * d, device=DEV).to(torch.bfloat16)
+    vc = torch.randn(B, Smax, hkv * d, device=DEV).to(torch.bfloat16)
+    q = torch.randn(B, hq * d, device=DEV).to(torch.bfloat16)
+    L = torch.randint(1, max_len + 1, (B,), device=DEV, dtype=torch.int32)
+    L[0] = max_len
+    o = native_ext.decode_attention(q, kc, vc, L, hq, hkv, d, max_len, 1 / math.sqrt(d))
+    r = decode_attention_reference(q.float(), kc.float(), vc.float(), L, hq, hkv, d)
+    assert (o.float() - r).abs().max().item() < 2e-2
