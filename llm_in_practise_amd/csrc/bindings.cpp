@@ -66,8 +66,8 @@ int lora_acc_chunks(int M);
 void launch_lora_acc(const float*, int, int, const void*, int, void*, int, const void*, int, float*, int64_t, int64_t,
                      float*, int, uint64_t, float, size_t, hipStream_t);
 void launch_decode_attention(const void*, const void*, const void*, const int*, float*, float*, float*, void*, int, int,
-                             int, int, int, int, int, float, hipStream_t);
-void decode_split_plan(int, int, int, int*, int*);
+                             int, int, int, int, float, hipStream_t);
+int decode_split_plan(int, int, int);
 void launch_sample(int, const void*, const int*, int, float*, int64_t*, int, int, float, int, float, float, uint64_t,
                    hipStream_t);
 void launch_dropout_fwd(const void*, void*, size_t, uint64_t, float, hipStream_t);
@@ -569,15 +569,14 @@ Tensor decode_attention(Tensor q, Tensor kc, Tensor vc, Tensor lens, int64_t hq,
   const int64_t B = q.size(0), Smax = kc.size(1);
   TORCH_CHECK(kc.size(0) == B && kc.size(2) == hkv * d && vc.sizes() == kc.sizes(), "decode_attention: cache shape");
   TORCH_CHECK(max_len <= Smax, "decode_attention: max_len > cache");
-  int nsplit, chunk;
-  decode_split_plan(B, hkv, max_len, &nsplit, &chunk);
+  const int nsplit = decode_split_plan(B, hkv, max_len);
   auto f32 = q.options().dtype(at::kFloat);
   Tensor opart = at::empty({B * hq * nsplit, d}, f32);
   Tensor mpart = at::empty({B * hq * nsplit}, f32), lpart = at::empty({B * hq * nsplit}, f32);
   Tensor out = at::empty({B, hq * d}, q.options());
   launch_decode_attention(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), lens.data_ptr<int>(), opart.data_ptr<float>(),
                           mpart.data_ptr<float>(), lpart.data_ptr<float>(), out.data_ptr(), B, Smax, hq, hkv, d,
-                          nsplit, chunk, (float)scale, stream());
+                          nsplit, (float)scale, stream());
   return out;
 }
 

@@ -4,11 +4,14 @@
 // decode attention ("flash-decoding" on CDNA4): one query token per sequence against its
 // contiguous KV cache [B, Smax, Hkv*D].  Decode is HBM-bound on the cache read, so the design
 // goal is to stream K/V once with 16-B loads and to spread one sequence over many CUs:
-//  * grid (splits, Hkv, B); each workgroup owns a 128-key chunk of ONE kv head and all of its
-//    G = Hq/Hkv query heads (GQA: K/V are read once for the whole group);
+//  * grid (splits, Hkv, B); the split count is chosen on the host for occupancy (~2048
+//    workgroups) and each workgroup takes 1/splits of its sequence's LIVE length (read on the
+//    device), for ONE kv head and all of its G = Hq/Hkv query heads (K/V read once per group);
 //  * D/8 lanes hold one key row (8 bf16 = 16 B per lane); a wave covers 64/(D/8) keys per
 //    step, the dot products finish with log2(D/8) xor-shuffles; online softmax per lane slot;
-//  * slots are merged through LDS, splits by a second tiny kernel (log-sum-exp merge).
+//  * two keys per lane slot are loaded before either is consumed (memory-level parallelism);
+//  * slots merge by xor shuffles inside the wave, waves through LDS, splits by a second tiny
+//    kernel (log-sum-exp merge over the splits that had keys).
 // Per-row valid lengths (right-padded batches / different prompt lengths) come from lens[B].
 //
 // sampler: one 1024-thread workgroup per row; repetition penalty (HF semantics: applied once
@@ -26,14 +29,16 @@ namespace {
 constexpr int DEC_THR = 256;
 constexpr int DEC_TARGET_WG = 2048;   // ≈ 8 workgroups per CU in flight
 
+// keys per split for a sequence of `len` keys: multiple of 16 (one workgroup step)
+__device__ __forceinline__ int split_chunk(int len, int nsplit) { return ((len + nsplit - 1) / nsplit + 15) & ~15; }
+
 template <int D, int G>
 __global__ __launch_bounds__(DEC_THR) void decode_attn_partial_k(const bf16* __restrict__ q,
                                                                  const bf16* __restrict__ kc,
                                                                  const bf16* __restrict__ vc,
                                                                  const int* __restrict__ lens, float* __restrict__ opart,
                                                                  float* __restrict__ mpart, float* __restrict__ lpart,
-                                                                 int Smax, int hq, int hkv, int nsplit, int chunk,
-                                                                 float scale) {
+                                                                 int Smax, int hq, int hkv, int nsplit, float scale) {
   constexpr int LPK = D / 8;          // lanes per key row (16 B each)
   constexpr int KPW = 64 / LPK;       // keys per wave step
   constexpr int NSLOT = 4 * KPW;      // keys per workgroup step
@@ -41,6 +46,7 @@ __global__ __launch_bounds__(DEC_THR) void decode_attn_partial_k(const bf16* __r
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int sw = lane / LPK, e = lane % LPK;   // key slot within the wave, 8-element piece of the row
   const int len = lens[b];
+  const int chunk = split_chunk(len, nsplit);   // splits divide the LIVE length evenly
   const int k0 = split * chunk, k1 = min(k0 + chunk, len);
   if (k0 >= len) return;              // empty split: the merge kernel never reads it
 
@@ -154,11 +160,12 @@ template <int D>
 __global__ __launch_bounds__(D) void decode_attn_merge_k(const float* __restrict__ opart,
                                                          const float* __restrict__ mpart,
                                                          const float* __restrict__ lpart, const int* __restrict__ lens,
-                                                         bf16* __restrict__ out, int hq, int nsplit, int chunk) {
+                                                         bf16* __restrict__ out, int hq, int nsplit) {
   const size_t h = blockIdx.x;  // b*hq + head
   const int d = threadIdx.x;
   const int len = lens[h / hq];
-  const int nv = min(nsplit, (len + chunk - 1) / chunk);   // splits that wrote partials
+  const int chunk = split_chunk(len, nsplit);
+  const int nv = len > 0 ? min(nsplit, (len + chunk - 1) / chunk) : 0;   // splits that wrote partials
   float M = -INFINITY;
   for (int s = 0; s < nv; ++s) M = fmaxf(M, mpart[h * nsplit + s]);
   float L = 0.f, A = 0.f;
@@ -298,27 +305,24 @@ __global__ __launch_bounds__(SMP_THR) void sample_k(const T* __restrict__ logits
 
 }  // namespace
 
-// Split-K plan: enough (split, kv-head, sequence) workgroups to fill the chip, each split a
-// multiple of 64 keys; depends only on (B, hkv, max_len) so a captured hipGraph stays valid
-// as the live lengths grow.
-void decode_split_plan(int B, int hkv, int max_len, int* nsplit, int* chunk) {
+// Split-K plan: enough (split, kv-head, sequence) workgroups to fill the chip.  The number of
+// splits depends only on (B, hkv, max_len), so a captured hipGraph stays valid as sequences
+// grow; each workgroup derives its key range from the live length on the device (all splits
+// busy whatever the context length, no host sync).
+int decode_split_plan(int B, int hkv, int max_len) {
   const int pairs = std::max(1, B * hkv);
   int ns = std::max(1, (DEC_TARGET_WG + pairs - 1) / pairs);
-  ns = std::min(ns, std::max(1, (max_len + 63) / 64));
-  int ch = (max_len + ns - 1) / ns;
-  ch = (ch + 63) / 64 * 64;
-  *chunk = ch;
-  *nsplit = (max_len + ch - 1) / ch;
+  return std::min(ns, std::max(1, (max_len + 31) / 32));
 }
 
 void launch_decode_attention(const void* q, const void* kc, const void* vc, const int* lens, float* opart, float* mpart,
-                             float* lpart, void* out, int B, int Smax, int hq, int hkv, int d, int nsplit, int chunk,
+                             float* lpart, void* out, int B, int Smax, int hq, int hkv, int d, int nsplit,
                              float scale, hipStream_t st) {
   const int G = hq / hkv;
   dim3 grid(nsplit, hkv, B);
 #define P(D_, G_)                                                                                           \
   decode_attn_partial_k<D_, G_><<<grid, DEC_THR, 0, st>>>((const bf16*)q, (const bf16*)kc, (const bf16*)vc, \
-                                                          lens, opart, mpart, lpart, Smax, hq, hkv, nsplit, chunk, scale)
+                                                          lens, opart, mpart, lpart, Smax, hq, hkv, nsplit, scale)
 #define GS(D_)                          \
   switch (G) {                          \
     case 1: P(D_, 1); break;            \
@@ -332,9 +336,9 @@ void launch_decode_attention(const void* q, const void* kc, const void* vc, cons
 #undef GS
 #undef P
   if (d == 128)
-    decode_attn_merge_k<128><<<B * hq, 128, 0, st>>>(opart, mpart, lpart, lens, (bf16*)out, hq, nsplit, chunk);
+    decode_attn_merge_k<128><<<B * hq, 128, 0, st>>>(opart, mpart, lpart, lens, (bf16*)out, hq, nsplit);
   else
-    decode_attn_merge_k<64><<<B * hq, 64, 0, st>>>(opart, mpart, lpart, lens, (bf16*)out, hq, nsplit, chunk);
+    decode_attn_merge_k<64><<<B * hq, 64, 0, st>>>(opart, mpart, lpart, lens, (bf16*)out, hq, nsplit);
   LIPA_CHECK_LAUNCH();
 }
 
