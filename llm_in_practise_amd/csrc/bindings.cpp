@@ -46,8 +46,7 @@ void launch_nf4_dequant(const uint8_t*, const float*, const uint8_t*, const floa
 void launch_attn_fwd(const void*, const void*, const void*, int, int, int, const int*, void*, float*, int, int, int,
                      int, int, int, float, hipStream_t);
 void launch_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const int*, int,
-                     int, int, void*, void*, void*, float*, float*, float*, float*, int, int, int, int, int, int,
-                     float, hipStream_t);
+                     int, int, void*, void*, void*, float*, int, int, int, int, int, int, float, hipStream_t);
 
 void launch_gemm_int4(const void*, int, const uint32_t*, const float*, const float*, const void*, const void*, int,
                       const void*, void*, int, int, int, hipStream_t);
@@ -466,9 +465,6 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o
   auto dk = at::empty({B * S, hkv * d}, q.options());
   auto dv = at::empty({B * S, hkv * d}, q.options());
   TORCH_CHECK(S % 64 == 0, "attn_bwd: seq_len must be a multiple of 64");
-  auto dqacc = at::zeros({B * S, hq * d}, q.options().dtype(at::kFloat));
-  auto dkf = at::empty({B * S, hq * d}, q.options().dtype(at::kFloat));
-  auto dvf = at::empty({B * S, hq * d}, q.options().dtype(at::kFloat));
   auto delta = at::empty({B, hq, S}, q.options().dtype(at::kFloat));
   const int* kl = nullptr;
   Tensor klc;
@@ -478,8 +474,7 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o
   }
   launch_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), kl,
                   q.stride(0), k.stride(0), v.stride(0), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
-                  dqacc.data_ptr<float>(), delta.data_ptr<float>(), dkf.data_ptr<float>(), dvf.data_ptr<float>(), B, S,
-                  hq, hkv, d, causal, scale, stream());
+                  delta.data_ptr<float>(), B, S, hq, hkv, d, causal, scale, stream());
   return {dq, dk, dv};
 }
 

@@ -36,6 +36,21 @@ __device__ __forceinline__ bf16x8 f2b8(f32x4 a, f32x4 b) {
 
 constexpr float LOG2E = 1.4426950408889634f;
 
+// raw v_exp_f32 (no denormal range reduction: the arguments here are <= 0 and a flushed tiny
+// probability is harmless)
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Grid (n0, n1, n2) → logical block (i0, i1, i2) with consecutive logical blocks (i0 fastest)
+// on the same XCD, so the blocks that re-read one (batch, kv-head)'s K/V (or Q/dO) share its L2.
+__device__ __forceinline__ void xcd_grid3(int& i0, int& i1, int& i2) {
+  const int n0 = gridDim.x, n1 = gridDim.y;
+  const int nwg = n0 * n1 * gridDim.z;
+  const int id = xcd_remap(blockIdx.x + n0 * (blockIdx.y + n1 * blockIdx.z), nwg);
+  i0 = id % n0;
+  i1 = (id / n0) % n1;
+  i2 = id / (n0 * n1);
+}
+
 // ============================================================================ forward
 template <int D>
 __global__ __launch_bounds__(256) void attn_fwd_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
@@ -52,8 +67,9 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16* __restrict__ Q, co
   __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // K0 V0 K1 V1
 
   const int nqb = (S + 127) / 128;
-  const int qb = nqb - 1 - blockIdx.x;  // heavy (late, causal) blocks first
-  const int h = blockIdx.y, b = blockIdx.z;
+  int i0, h, b;
+  xcd_grid3(i0, h, b);
+  const int qb = nqb - 1 - i0;  // heavy (late, causal) blocks first
   const int hk = h / (hq / hkv);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   const int q0 = qb * 128 + 32 * w;
@@ -130,29 +146,33 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16* __restrict__ Q, co
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       const int qa = q0 + 16 * qt + li;
+      const int klim = min(causal ? qa : S, kvlen - 1);  // last key this query may see
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc[kt][qt][r] *= scale_log2;
+      if (need_mask) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            sc[kt][qt][r] = (k0 + 16 * kt + 4 * g + r <= klim) ? sc[kt][qt][r] : -INFINITY;
+      }
       float mx = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = sc[kt][qt][r] * scale_log2;
-          if (need_mask) {
-            const int ka = k0 + 16 * kt + 4 * g + r;
-            if ((causal && ka > qa) || ka >= kvlen) v = -INFINITY;
-          }
-          sc[kt][qt][r] = v;
-          mx = fmaxf(mx, v);
-        }
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sc[kt][qt][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mn = fmaxf(m_run[qt], mx);
-      const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m_run[qt] - mn);
+      const float alpha = (mn == -INFINITY) ? 1.f : fexp2(m_run[qt] - mn);
       float rs = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = (mn == -INFINITY) ? 0.f : exp2f(sc[kt][qt][r] - mn);
+          const float p = (mn == -INFINITY) ? 0.f : fexp2(sc[kt][qt][r] - mn);
           sc[kt][qt][r] = p;
           rs += p;
         }
@@ -199,59 +219,167 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16* __restrict__ Q, co
 }
 
 // ============================================================================ backward
-// delta[b][h][q] = Σ_d dO·O
+// Two atomic-free kernels (FA2 split).  Both recompute P from the saved log-sum-exp.
+//  * attn_bwd_dq_k : workgroup = 64 queries of one q-head (4 waves × 16, one query per lane, so
+//    lse/delta are lane-uniform); computes delta = Σ dO·O for its queries first (written for the
+//    dK/dV kernel), then sweeps key tiles: Sᵀ = K·Qᵀ, dPᵀ = V·dOᵀ, dS, dQᵀ += Kᵀ·dSᵀ with dS kept
+//    in registers (permuted key order, Kᵀ via ds_read_b64_tr_b16).  dQ is written once, in bf16.
+//  * attn_bwd_dkv_k: workgroup = 64 keys of one KV head (4 waves × 16 keys, K/V fragments in
+//    registers) that sweeps every q-head of its GQA group × 64-query tiles, so the group's
+//    dK/dV sum stays in registers: no fp32 partials, no finalize pass.  Q/dO tiles (plus
+//    their lse/delta) are register-prefetched one tile ahead into double-buffered LDS.
 template <int D>
-__global__ __launch_bounds__(256) void attn_bwd_pre_k(const bf16* __restrict__ dO, const bf16* __restrict__ O,
-                                                      float* __restrict__ delta, int B, int S, int hq) {
-  const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per (token, head)
-  const int lane = threadIdx.x & 63;
-  if (idx >= B * S * hq) return;
-  const int t = idx / hq, h = idx % hq;
-  float s = 0.f;
-  for (int d = lane * 2; d < D; d += 128) {
-    const size_t off = (size_t)t * hq * D + h * D + d;
-    s += (float)dO[off] * (float)O[off] + (float)dO[off + 1] * (float)O[off + 1];
+__global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16* __restrict__ dO, const bf16* __restrict__ O,
+                                                     const bf16* __restrict__ Q, const bf16* __restrict__ K,
+                                                     const bf16* __restrict__ V, const float* __restrict__ lse,
+                                                     float* __restrict__ delta, const int* __restrict__ kv_lens,
+                                                     int ldq, int ldk, int ldv, bf16* __restrict__ dQ, int S, int hq,
+                                                     int hkv, int causal, float scale, float scale_log2) {
+  constexpr int LDR = D + 8, CH = D / 8, TILE = 64 * LDR, NS = D / 32, ND = D / 16;
+  constexpr int LOADS = 64 * CH / 256;
+  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // K0 V0 K1 V1
+
+  const int nqb = S / 64;
+  int i0, h, b;
+  xcd_grid3(i0, h, b);
+  const int qb = nqb - 1 - i0;  // heavy (late, causal) blocks first
+  const int hk = h / (hq / hkv);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  const int q0 = qb * 64;
+  const int qa = q0 + 16 * w + li;  // this lane's query
+  const int kvlen = kv_lens ? kv_lens[b] : S;
+  const size_t tok0 = (size_t)b * S;
+  const size_t ldo = (size_t)hq * D;
+
+  bf16x8 qf[NS], dof[NS];
+  float dsum = 0.f;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const size_t off = (tok0 + qa) * ldo + h * D + 32 * s + 8 * g;
+    qf[s] = *reinterpret_cast<const bf16x8*>(Q + (tok0 + qa) * ldq + h * D + 32 * s + 8 * g);
+    dof[s] = *reinterpret_cast<const bf16x8*>(dO + off);
+    const bf16x8 of = *reinterpret_cast<const bf16x8*>(O + off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dsum += (float)dof[s][j] * (float)of[j];
   }
-  s = wave_sum(s);
-  if (lane == 0) {
-    const int b = t / S, q = t % S;
-    delta[((size_t)b * hq + h) * S + q] = s;
+  dsum += __shfl_xor(dsum, 16, 64);
+  dsum += __shfl_xor(dsum, 32, 64);
+  const size_t bh = ((size_t)b * hq + h) * S;
+  if (g == 0) delta[bh + qa] = dsum;
+  const float lse2 = lse[bh + qa] * LOG2E;
+  const int klim = min(causal ? qa : S, kvlen - 1);  // last key this query may see
+
+  int kend = causal ? min(S, q0 + 64) : S;
+  kend = min(kend, kvlen);
+  const int nt = (kend + 63) / 64;
+
+  f32x4 acc[ND];
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 kr[LOADS], vr[LOADS];
+  auto load_tile = [&](int t) {
+#pragma unroll
+    for (int p = 0; p < LOADS; ++p) {
+      const int ci = p * 256 + threadIdx.x;
+      const int row = ci / CH, ch = ci % CH;
+      const size_t key = tok0 + t * 64 + row;
+      kr[p] = *reinterpret_cast<const bf16x8*>(K + key * ldk + hk * D + ch * 8);
+      vr[p] = *reinterpret_cast<const bf16x8*>(V + key * ldv + hk * D + ch * 8);
+    }
+  };
+  auto store_tile = [&](int buf) {
+    bf16* Kl = smem + buf * 2 * TILE;
+    bf16* Vl = Kl + TILE;
+#pragma unroll
+    for (int p = 0; p < LOADS; ++p) {
+      const int ci = p * 256 + threadIdx.x;
+      const int row = ci / CH, ch = ci % CH;
+      *reinterpret_cast<bf16x8*>(Kl + row * LDR + ch * 8) = kr[p];
+      *reinterpret_cast<bf16x8*>(Vl + row * LDR + ch * 8) = vr[p];
+    }
+  };
+
+  if (nt > 0) load_tile(0);
+  for (int t = 0; t < nt; ++t) {
+    store_tile(t & 1);
+    __syncthreads();
+    if (t + 1 < nt) load_tile(t + 1);
+    const bf16* Kl = smem + (t & 1) * 2 * TILE;
+    const bf16* Vl = Kl + TILE;
+    const int k0 = t * 64;
+    // ---- Sᵀ[key][q], dPᵀ[key][q] for 4 key-subtiles (lane: query li, keys 16kt + 4g + r)
+    f32x4 sc[4], dp[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      sc[kt] = dp[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kl + (16 * kt + li) * LDR + 32 * s + 8 * g);
+        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(Vl + (16 * kt + li) * LDR + 32 * s + 8 * g);
+        sc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], sc[kt], 0, 0, 0);
+        dp[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, dof[s], dp[kt], 0, 0, 0);
+      }
+    }
+    const bool need_mask = (causal && k0 + 63 > q0) || (k0 + 64 > kvlen);
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sc[kt][r] = fexp2(sc[kt][r] * scale_log2 - lse2);
+    if (need_mask) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc[kt][r] = (k0 + 16 * kt + 4 * g + r <= klim) ? sc[kt][r] : 0.f;
+    }
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sc[kt][r] *= dp[kt][r] - dsum;
+    // ---- dQᵀ[d][q] += Kᵀ[d][key] · dSᵀ[key][q]  (permuted key order, as the forward's PV)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const bf16x8 dsf = f2b8(sc[2 * kb], sc[2 * kb + 1]);
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) {
+        const bf16* p0 = Kl + (32 * kb + 4 * g + (li >> 2)) * LDR + 16 * dt + 4 * (li & 3);
+        const bf16x8 ktf = cat8(tr_read(p0), tr_read(p0 + 16 * LDR));
+        acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ktf, dsf, acc[dt], 0, 0, 0);
+      }
+    }
+  }
+  // ---- dQ[q][16dt + 4g + r] = scale · acc
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt) {
+    bf16x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[dt][r] * scale);
+    *reinterpret_cast<bf16x4*>(dQ + (tok0 + qa) * ldo + h * D + 16 * dt + 4 * g) = o;
   }
 }
 
 template <int D>
-__global__ __launch_bounds__(256) void attn_bwd_k(const bf16* __restrict__ dO, const bf16* __restrict__ Q,
-                                                  const bf16* __restrict__ K, const bf16* __restrict__ V,
-                                                  const float* __restrict__ lse, const float* __restrict__ delta,
-                                                  const int* __restrict__ kv_lens, int ldq, int ldk, int ldv,
-                                                  float* __restrict__ dqacc, float* __restrict__ dkf,
-                                                  float* __restrict__ dvf, int S, int hq, int hkv, int causal,
-                                                  float scale, float scale_log2) {
-  constexpr int LDR = D + 8;
-  constexpr int NS = D / 32, ND = D / 16;
-  constexpr int LDS_S = 64 + 8;
-  __shared__ __attribute__((aligned(16))) bf16 Kl[64 * LDR];
-  __shared__ __attribute__((aligned(16))) bf16 Ql[32 * LDR];
-  __shared__ __attribute__((aligned(16))) bf16 dOl[32 * LDR];
-  __shared__ __attribute__((aligned(16))) bf16 dSl[32 * LDS_S];
+__global__ __launch_bounds__(256) void attn_bwd_dkv_k(const bf16* __restrict__ dO, const bf16* __restrict__ Q,
+                                                      const bf16* __restrict__ K, const bf16* __restrict__ V,
+                                                      const float* __restrict__ lse, const float* __restrict__ delta,
+                                                      const int* __restrict__ kv_lens, int ldq, int ldk, int ldv,
+                                                      bf16* __restrict__ dK, bf16* __restrict__ dV, int S, int hq,
+                                                      int hkv, int causal, float scale, float scale_log2) {
+  constexpr int LDR = D + 8, CH = D / 8, TILE = 64 * LDR, NS = D / 32, ND = D / 16;
+  constexpr int LOADS = 64 * CH / 256;
+  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // Q0 dO0 Q1 dO1
+  __shared__ __attribute__((aligned(16))) float stat[2][2][64];  // [buf][lse|delta][q]
 
-  const int nkb = S / 64;
-  const int kbi = blockIdx.x;
-  const int h = blockIdx.y, b = blockIdx.z;
-  const int hk = h / (hq / hkv);
+  int kbi, hk, b;  // causal: block 0 (most query tiles) first
+  xcd_grid3(kbi, hk, b);
+  const int rep = hq / hkv;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   const int kb0 = kbi * 64;
-  const int kw = kb0 + 16 * w + li;  // this lane's key (column of S / dP tiles)
+  const int kw = kb0 + 16 * w + li;  // this lane's key (column of the S / dP tiles)
   const int kvlen = kv_lens ? kv_lens[b] : S;
   const size_t tok0 = (size_t)b * S;
-  (void)nkb;
+  const size_t ldo = (size_t)hq * D, ldkv = (size_t)hkv * D;
 
-  // K block → LDS (for dQ) ; K/V fragments (B operands) → registers
-  for (int ci = threadIdx.x; ci < 64 * (D / 8); ci += 256) {
-    const int row = ci / (D / 8), ch = ci % (D / 8);
-    *reinterpret_cast<bf16x8*>(Kl + row * LDR + ch * 8) =
-        *reinterpret_cast<const bf16x8*>(K + (tok0 + kb0 + row) * ldk + hk * D + ch * 8);
-  }
   bf16x8 kf[NS], vf[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
@@ -262,124 +390,106 @@ __global__ __launch_bounds__(256) void attn_bwd_k(const bf16* __restrict__ dO, c
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt) dv[dt] = dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int qt_start = causal ? kb0 / 32 : 0;
-  const int nqt = S / 32;
-  const float* lse_bh = lse + ((size_t)b * hq + h) * S;
-  const float* del_bh = delta + ((size_t)b * hq + h) * S;
+  const int qt0 = causal ? kbi : 0;
+  const int qmin = kw < kvlen ? (causal ? kw : 0) : 1 << 30;  // first query that sees this key
+  const int nqt = S / 64 - qt0;
+  const int n_it = kb0 < kvlen ? rep * nqt : 0;  // keys past kv_len get zero gradient
 
-  for (int qtile = qt_start; qtile < nqt; ++qtile) {
-    const int qa0 = qtile * 32;
-    __syncthreads();  // previous iteration's LDS reads done
-    for (int ci = threadIdx.x; ci < 32 * (D / 8); ci += 256) {
-      const int row = ci / (D / 8), ch = ci % (D / 8);
-      const size_t tq = tok0 + qa0 + row;
-      *reinterpret_cast<bf16x8*>(Ql + row * LDR + ch * 8) =
-          *reinterpret_cast<const bf16x8*>(Q + tq * ldq + h * D + ch * 8);
-      *reinterpret_cast<bf16x8*>(dOl + row * LDR + ch * 8) =
-          *reinterpret_cast<const bf16x8*>(dO + tq * (size_t)(hq * D) + h * D + ch * 8);
-    }
-    __syncthreads();
-    // ---- S[q][key], dP[q][key]: rows q = 16qt + 4g + r, col key = kw
-    f32x4 sp[2], dp[2];
+  bf16x8 qr[LOADS], dr[LOADS];
+  float st = 0.f;
+  auto load_it = [&](int it) {
+    const int h = hk * rep + it / nqt;
+    const int qa0 = (qt0 + it % nqt) * 64;
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
+    for (int p = 0; p < LOADS; ++p) {
+      const int ci = p * 256 + threadIdx.x;
+      const int row = ci / CH, ch = ci % CH;
+      const size_t tq = tok0 + qa0 + row;
+      qr[p] = *reinterpret_cast<const bf16x8*>(Q + tq * ldq + h * D + ch * 8);
+      dr[p] = *reinterpret_cast<const bf16x8*>(dO + tq * ldo + h * D + ch * 8);
+    }
+    if (threadIdx.x < 128) {
+      const size_t bh = ((size_t)b * hq + h) * S + qa0 + (threadIdx.x & 63);
+      st = threadIdx.x < 64 ? lse[bh] * LOG2E : delta[bh];
+    }
+  };
+  auto store_it = [&](int buf) {
+    bf16* Ql = smem + buf * 2 * TILE;
+    bf16* dOl = Ql + TILE;
+#pragma unroll
+    for (int p = 0; p < LOADS; ++p) {
+      const int ci = p * 256 + threadIdx.x;
+      const int row = ci / CH, ch = ci % CH;
+      *reinterpret_cast<bf16x8*>(Ql + row * LDR + ch * 8) = qr[p];
+      *reinterpret_cast<bf16x8*>(dOl + row * LDR + ch * 8) = dr[p];
+    }
+    if (threadIdx.x < 128) stat[buf][threadIdx.x >> 6][threadIdx.x & 63] = st;
+  };
+
+  if (n_it > 0) load_it(0);
+  for (int it = 0; it < n_it; ++it) {
+    store_it(it & 1);
+    __syncthreads();
+    if (it + 1 < n_it) load_it(it + 1);
+    const bf16* Ql = smem + (it & 1) * 2 * TILE;
+    const bf16* dOl = Ql + TILE;
+    const float* Ls = stat[it & 1][0];
+    const float* Dls = stat[it & 1][1];
+    const int qa0 = (qt0 + it % nqt) * 64;
+    // ---- S[q][key], dP[q][key]: rows q = 16qt + 4g + r, col key = kw
+    f32x4 sp[4], dp[4];
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
       sp[qt] = dp[qt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        const bf16x8 qf = *reinterpret_cast<const bf16x8*>(Ql + (16 * qt + li) * LDR + 32 * s + 8 * g);
-        const bf16x8 of = *reinterpret_cast<const bf16x8*>(dOl + (16 * qt + li) * LDR + 32 * s + 8 * g);
-        sp[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf, kf[s], sp[qt], 0, 0, 0);
-        dp[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(of, vf[s], dp[qt], 0, 0, 0);
+        const bf16x8 qfr = *reinterpret_cast<const bf16x8*>(Ql + (16 * qt + li) * LDR + 32 * s + 8 * g);
+        const bf16x8 ofr = *reinterpret_cast<const bf16x8*>(dOl + (16 * qt + li) * LDR + 32 * s + 8 * g);
+        sp[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qfr, kf[s], sp[qt], 0, 0, 0);
+        dp[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ofr, vf[s], dp[qt], 0, 0, 0);
       }
     }
-    f32x4 pp[2], ds[2];
+    const bool need_mask = (causal && qa0 < kb0 + 63) || (kb0 + 64 > kvlen);
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const int qb4 = qa0 + 16 * qt + 4 * g;
-      const f32x4 L = *reinterpret_cast<const f32x4*>(lse_bh + qb4);
-      const f32x4 Dl = *reinterpret_cast<const f32x4*>(del_bh + qb4);
+    for (int qt = 0; qt < 4; ++qt) {
+      const f32x4 L = *reinterpret_cast<const f32x4*>(Ls + 16 * qt + 4 * g);
+      const f32x4 Dl = *reinterpret_cast<const f32x4*>(Dls + 16 * qt + 4 * g);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qa = qb4 + r;
-        float p = exp2f(sp[qt][r] * scale_log2 - L[r] * LOG2E);
-        if ((causal && kw > qa) || kw >= kvlen) p = 0.f;
-        pp[qt][r] = p;
-        ds[qt][r] = p * (dp[qt][r] - Dl[r]);
+      for (int r = 0; r < 4; ++r) sp[qt][r] = fexp2(sp[qt][r] * scale_log2 - L[r]);
+      if (need_mask) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sp[qt][r] = (qa0 + 16 * qt + 4 * g + r >= qmin) ? sp[qt][r] : 0.f;
       }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dp[qt][r] = sp[qt][r] * (dp[qt][r] - Dl[r]);
     }
-    // permuted-q operand order j ↔ 16(j>>2) + 4g + (j&3)
-    const bf16x8 pfr = f2b8(pp[0], pp[1]);
-    const bf16x8 dsf = f2b8(ds[0], ds[1]);
-    // ---- dVᵀ[d][key] += dOᵀ[d][q]·P[q][key] ; dKᵀ += Qᵀ·dS
+    // ---- dVᵀ[d][key] += dOᵀ[d][q]·P[q][key] ; dKᵀ += Qᵀ·dS   (permuted-q operand order)
 #pragma unroll
-    for (int dt = 0; dt < ND; ++dt) {
-      const int rr = 4 * g + (li >> 2), cc = 16 * dt + 4 * (li & 3);
-      const bf16x8 of = cat8(tr_read(dOl + rr * LDR + cc), tr_read(dOl + (rr + 16) * LDR + cc));
-      const bf16x8 qf = cat8(tr_read(Ql + rr * LDR + cc), tr_read(Ql + (rr + 16) * LDR + cc));
-      dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(of, pfr, dv[dt], 0, 0, 0);
-      dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf, dsf, dk[dt], 0, 0, 0);
-    }
-    // ---- dS → LDS [q][key] for the dQ product
+    for (int qk = 0; qk < 2; ++qk) {
+      const bf16x8 pfr = f2b8(sp[2 * qk], sp[2 * qk + 1]);
+      const bf16x8 dsf = f2b8(dp[2 * qk], dp[2 * qk + 1]);
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) dSl[(16 * qt + 4 * g + r) * LDS_S + 16 * w + li] = (bf16)ds[qt][r];
-    __syncthreads();
-    // ---- dQ[q][d] += dS[q][key]·K[key][d] over the 64-key block; wave w: qt = w>>1, 4 d-subtiles
-    {
-      const int qt = w >> 1;
-#pragma unroll
-      for (int i = 0; i < ND / 2; ++i) {
-        const int dt = (w & 1) * (ND / 2) + i;
-        f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-          const bf16x8 sf = *reinterpret_cast<const bf16x8*>(dSl + (16 * qt + li) * LDS_S + 32 * kb + 8 * g);
-          const int rr = 32 * kb + 8 * g + (li >> 2), cc = 16 * dt + 4 * (li & 3);
-          const bf16x8 kt = cat8(tr_read(Kl + rr * LDR + cc), tr_read(Kl + (rr + 4) * LDR + cc));
-          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sf, kt, a, 0, 0, 0);
-        }
-        // C layout: col d = 16dt + li, rows q = 16qt + 4g + r
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const size_t tq = tok0 + qa0 + 16 * qt + 4 * g + r;
-          atomicAdd(dqacc + tq * (size_t)(hq * D) + h * D + 16 * dt + li, a[r] * scale);
-        }
+      for (int dt = 0; dt < ND; ++dt) {
+        const int rr = 32 * qk + 4 * g + (li >> 2), cc = 16 * dt + 4 * (li & 3);
+        const bf16x8 of = cat8(tr_read(dOl + rr * LDR + cc), tr_read(dOl + (rr + 16) * LDR + cc));
+        const bf16x8 qfr = cat8(tr_read(Ql + rr * LDR + cc), tr_read(Ql + (rr + 16) * LDR + cc));
+        dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(of, pfr, dv[dt], 0, 0, 0);
+        dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qfr, dsf, dk[dt], 0, 0, 0);
       }
     }
   }
-  // ---- write per-q-head dK (scaled) / dV (fp32): lane col key = kw, rows d = 16dt + 4g + r
+  // ---- dK (scaled) / dV, summed over the GQA group: lane col key = kw, rows d = 16dt + 4g + r
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt) {
-    const size_t off = (tok0 + kw) * (size_t)(hq * D) + h * D + 16 * dt + 4 * g;
-    *reinterpret_cast<f32x4*>(dkf + off) = dk[dt] * scale;
-    *reinterpret_cast<f32x4*>(dvf + off) = dv[dt];
-  }
-}
-
-// dq = bf16(dqacc); dk/dv = bf16(Σ over the GQA group of per-q-head partials)
-template <int D>
-__global__ __launch_bounds__(256) void attn_bwd_fin_k(const float* __restrict__ dqacc, const float* __restrict__ dkf,
-                                                      const float* __restrict__ dvf, bf16* __restrict__ dq,
-                                                      bf16* __restrict__ dk, bf16* __restrict__ dv, int T, int hq,
-                                                      int hkv) {
-  const size_t n1 = (size_t)T * hq * D;
-  const size_t n2 = (size_t)T * hkv * D;
-  const int rep = hq / hkv;
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n1; i += (size_t)gridDim.x * 256) {
-    dq[i] = (bf16)dqacc[i];
-    if (i < n2) {
-      const size_t t = i / (hkv * D), rem = i % (hkv * D);
-      const int hk = rem / D, d = rem % D;
-      float a = 0.f, c = 0.f;
-      for (int r = 0; r < rep; ++r) {
-        const size_t o = t * (size_t)(hq * D) + (size_t)(hk * rep + r) * D + d;
-        a += dkf[o];
-        c += dvf[o];
-      }
-      dk[i] = (bf16)a;
-      dv[i] = (bf16)c;
+    const size_t off = (tok0 + kw) * ldkv + hk * D + 16 * dt + 4 * g;
+    bf16x4 ok, ov;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      ok[r] = (bf16)(dk[dt][r] * scale);
+      ov[r] = (bf16)dv[dt][r];
     }
+    *reinterpret_cast<bf16x4*>(dK + off) = ok;
+    *reinterpret_cast<bf16x4*>(dV + off) = ov;
   }
 }
 
@@ -400,21 +510,17 @@ void launch_attn_fwd(const void* q, const void* k, const void* v, int ldq, int l
 }
 
 void launch_attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
-                     const int* kv_lens, int ldq, int ldk, int ldv, void* dq, void* dk, void* dv, float* dqacc,
-                     float* delta, float* dkf, float* dvf, int B, int S, int hq, int hkv, int D, int causal,
-                     float scale, hipStream_t st) {
-  const int rows = B * S * hq;
+                     const int* kv_lens, int ldq, int ldk, int ldv, void* dq, void* dk, void* dv, float* delta, int B,
+                     int S, int hq, int hkv, int D, int causal, float scale, hipStream_t st) {
   const float sl2 = scale * LOG2E;
-  dim3 grid(S / 64, hq, B), blk(256);
-  const int T = B * S;
-  size_t nfin = (size_t)T * hq * D;
-  int gfin = (int)((nfin + 255) / 256 < 4096 ? (nfin + 255) / 256 : 4096);
+  dim3 gq(S / 64, hq, B), gkv(S / 64, hkv, B), blk(256);
 #define RUN(DD)                                                                                                    \
-  attn_bwd_pre_k<DD><<<(rows + 3) / 4, 256, 0, st>>>((const bf16*)dout, (const bf16*)o, delta, B, S, hq);          \
-  attn_bwd_k<DD><<<grid, blk, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k, (const bf16*)v, lse,     \
-                                       delta, kv_lens, ldq, ldk, ldv, dqacc, dkf, dvf, S, hq, hkv, causal, scale,  \
-                                       sl2);                                                                       \
-  attn_bwd_fin_k<DD><<<gfin, 256, 0, st>>>(dqacc, dkf, dvf, (bf16*)dq, (bf16*)dk, (bf16*)dv, T, hq, hkv)
+  attn_bwd_dq_k<DD><<<gq, blk, 0, st>>>((const bf16*)dout, (const bf16*)o, (const bf16*)q, (const bf16*)k,         \
+                                        (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dq, S, hq, hkv,  \
+                                        causal, scale, sl2);                                                        \
+  attn_bwd_dkv_k<DD><<<gkv, blk, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k, (const bf16*)v, lse,  \
+                                          delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, (bf16*)dv, S, hq, hkv, causal, \
+                                          scale, sl2)
   if (D == 128) {
     RUN(128);
   } else {
