@@ -48,7 +48,7 @@ void launch_attn_fwd(const void*, const void*, const void*, int, int, int, const
 void launch_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const int*, int,
                      int, int, void*, void*, void*, float*, int, int, int, int, int, int, float, hipStream_t);
 
-void launch_gemm_int4(const void*, int, const uint32_t*, const float*, const float*, const void*, const void*, int,
+void launch_gemm_int4_any(const void*, int, const uint32_t*, const float*, const float*, const void*, const void*, int,
                       const void*, void*, int, int, int, hipStream_t);
 void launch_gemv_w4(int, const void*, int, const uint8_t*, const float*, const float*, int, const void*, void*, int, int,
                     int, hipStream_t);
@@ -372,7 +372,7 @@ Tensor gemm_int4(Tensor x, Tensor codes_f, Tensor scale_t, Tensor bias_t, int64_
   check_ext(ext_a, ext_b, M, N, R_ext);
   if (residual) TORCH_CHECK(residual->is_contiguous() && residual->size(0) == M && residual->size(1) == N, "residual");
   auto y = at::empty({M, N}, x.options());
-  launch_gemm_int4(x.data_ptr(), x.stride(0), (const uint32_t*)codes_f.data_ptr(), scale_t.data_ptr<float>(),
+  launch_gemm_int4_any(x.data_ptr(), x.stride(0), (const uint32_t*)codes_f.data_ptr(), scale_t.data_ptr<float>(),
                    bias_t.data_ptr<float>(), optr(ext_a), optr(ext_b), R_ext, optr(residual), y.data_ptr(), M, N, K,
                    stream());
   return y;

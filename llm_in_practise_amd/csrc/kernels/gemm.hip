@@ -522,12 +522,18 @@ void launch_gemm_w4v2(int bwd, const void* A, int lda, const uint32_t* codes, co
                       const void* ext_a, const void* ext_b, int R_ext, const void* residual, void* out, int M, int C,
                       int R, hipStream_t st);
 
+bool gemm_w4v3_supported(int M, int C, int R, int lda);
+void launch_gemm_w4v3(int bwd, const void* A, int lda, const uint32_t* codes, const float* absmax_t,
+                      const void* ext_a, const void* ext_b, int R_ext, const void* residual, void* out, int M, int C,
+                      int R, hipStream_t st);
+
 static int g_gemm_impl_override = 0;
 void set_gemm_impl(int impl) { g_gemm_impl_override = impl; }  // A/B benches in one process
 static inline int gemm_impl() {
   static const int impl = [] {
-    const char* e = getenv("LIPA_GEMM_IMPL");  // 1 = generation-1 kernel, 2 = buffer-SRD kernel
-    return e ? atoi(e) : 2;
+    // 1 = generation 1, 2 = buffer-SRD staging, 3 = pair-table dequant (gemm3.hip)
+    const char* e = getenv("LIPA_GEMM_IMPL");
+    return e ? atoi(e) : 3;
   }();
   return g_gemm_impl_override ? g_gemm_impl_override : impl;
 }
@@ -535,7 +541,11 @@ static inline int gemm_impl() {
 void launch_gemm_w4(int bwd, const void* A, int lda, const uint32_t* codes, const float* absmax_t, const void* ext_a,
                     const void* ext_b, int R_ext, const void* residual, void* out, int M, int C, int R,
                     hipStream_t st) {
-  if (gemm_impl() == 2 && gemm_w4v2_supported(M, C, R, lda)) {
+  if (gemm_impl() == 3 && gemm_w4v3_supported(M, C, R, lda)) {
+    launch_gemm_w4v3(bwd, A, lda, codes, absmax_t, ext_a, ext_b, R_ext, residual, out, M, C, R, st);
+    return;
+  }
+  if (gemm_impl() >= 2 && gemm_w4v2_supported(M, C, R, lda)) {
     launch_gemm_w4v2(bwd, A, lda, codes, absmax_t, ext_a, ext_b, R_ext, residual, out, M, C, R, st);
     return;
   }
@@ -554,6 +564,21 @@ void launch_gemm_w4(int bwd, const void* A, int lda, const uint32_t* codes, cons
   }
 #undef L
   LIPA_CHECK_LAUNCH();
+}
+
+void launch_gemm_int4(const void* A, int lda, const uint32_t* codes, const float* scale_t, const float* bias_t,
+                      const void* ext_a, const void* ext_b, int R_ext, const void* residual, void* out, int M, int N,
+                      int K, hipStream_t st);
+void launch_gemm_int4_v3(const void* A, int lda, const uint32_t* codes, const float* scale_t, const float* bias_t,
+                         const void* ext_a, const void* ext_b, int R_ext, const void* residual, void* out, int M, int N,
+                         int K, hipStream_t st);
+void launch_gemm_int4_any(const void* A, int lda, const uint32_t* codes, const float* scale_t, const float* bias_t,
+                          const void* ext_a, const void* ext_b, int R_ext, const void* residual, void* out, int M, int N,
+                          int K, hipStream_t st) {
+  if (gemm_impl() == 3)
+    launch_gemm_int4_v3(A, lda, codes, scale_t, bias_t, ext_a, ext_b, R_ext, residual, out, M, N, K, st);
+  else
+    launch_gemm_int4(A, lda, codes, scale_t, bias_t, ext_a, ext_b, R_ext, residual, out, M, N, K, st);
 }
 
 void launch_gemm_bf16w(const void* A, int lda, const void* W, const void* ext_a, const void* ext_b, int R_ext,
