@@ -527,15 +527,20 @@ void launch_gemm_w4v3(int bwd, const void* A, int lda, const uint32_t* codes, co
                       const void* ext_a, const void* ext_b, int R_ext, const void* residual, void* out, int M, int C,
                       int R, hipStream_t st);
 
+extern int g_gemm3_tab;
 static int g_gemm_impl_override = 0;
+// 1 = generation 1, 2 = buffer-SRD staging (default), 3 = gen 3 pair table, 4 = gen 3 with the 16-entry
+// table.  Gen 3 is 7 % faster in the isolated-GEMM microbenchmark but 2-4 % SLOWER in the full
+// training step on the same box (profiles/gemm_gen3_ab.txt), so generation 2 stays the default.
 void set_gemm_impl(int impl) { g_gemm_impl_override = impl; }  // A/B benches in one process
 static inline int gemm_impl() {
   static const int impl = [] {
-    // 1 = generation 1, 2 = buffer-SRD staging, 3 = pair-table dequant (gemm3.hip)
     const char* e = getenv("LIPA_GEMM_IMPL");
-    return e ? atoi(e) : 3;
+    return e ? atoi(e) : 2;
   }();
-  return g_gemm_impl_override ? g_gemm_impl_override : impl;
+  const int r = g_gemm_impl_override ? g_gemm_impl_override : impl;
+  g_gemm3_tab = r == 4 ? 0 : 1;
+  return r == 4 ? 3 : r;
 }
 
 void launch_gemm_w4(int bwd, const void* A, int lda, const uint32_t* codes, const float* absmax_t, const void* ext_a,

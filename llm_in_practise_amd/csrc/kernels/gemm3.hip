@@ -67,6 +67,27 @@ __device__ __forceinline__ void lut_issue(uint32_t x, const char* lut2, f32x2 (&
   p[2] = *reinterpret_cast<const f32x2*>(lut2 + boff<2>(x));
   p[3] = *reinterpret_cast<const f32x2*>(lut2 + boff<3>(x));
 }
+// 16-entry f32 table variant (generation-2 extraction: nibble×4 via lo4/hi4 masks + bfe)
+template <int OFF>
+__device__ __forceinline__ uint32_t bfe8_c(uint32_t x) {
+  if constexpr (OFF == 0) return x & 0xFFu;
+  else if constexpr (OFF == 24) return x >> 24;
+  else {
+    uint32_t r;
+    asm("v_bfe_u32 %0, %1, %2, 8" : "=v"(r) : "v"(x), "i"(OFF));
+    return r;
+  }
+}
+__device__ __forceinline__ float lut_at(const char* lut, uint32_t byte_off) {
+  return *reinterpret_cast<const float*>(lut + byte_off);
+}
+__device__ __forceinline__ void lut_issue16(uint32_t x, const char* lut, f32x2 (&p)[4]) {
+  const uint32_t lo4 = (x << 2) & 0x3C3C3C3Cu, hi4 = (x >> 2) & 0x3C3C3C3Cu;
+  p[0] = f32x2{lut_at(lut, bfe8_c<0>(lo4)), lut_at(lut, bfe8_c<0>(hi4))};
+  p[1] = f32x2{lut_at(lut, bfe8_c<8>(lo4)), lut_at(lut, bfe8_c<8>(hi4))};
+  p[2] = f32x2{lut_at(lut, bfe8_c<16>(lo4)), lut_at(lut, bfe8_c<16>(hi4))};
+  p[3] = f32x2{lut_at(lut, bfe8_c<24>(lo4)), lut_at(lut, bfe8_c<24>(hi4))};
+}
 __device__ __forceinline__ bf16x8 cvt8(const f32x2 (&v)[4], float sc) {
   u32x4 r{pk2(fmul(v[0][0], sc), fmul(v[0][1], sc)), pk2(fmul(v[1][0], sc), fmul(v[1][1], sc)),
           pk2(fmul(v[2][0], sc), fmul(v[2][1], sc)), pk2(fmul(v[3][0], sc), fmul(v[3][1], sc))};
@@ -147,12 +168,15 @@ __device__ __forceinline__ void convert_half(const StepW<MODE>& q, const f32x2 (
     wf[h][1] = cvt8v(lv[h][1], q.a[2], q.a[3]);
   }
 }
-template <int MODE>
+template <int MODE, int TAB>
 __device__ __forceinline__ void lut_step(const StepW<MODE>& q, const char* lut2, f32x2 (&lv)[2][2][4]) {
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int s = 0; s < 2; ++s) lut_issue(q.c[2 * h + s], lut2, lv[h][s]);
+    for (int s = 0; s < 2; ++s) {
+      if constexpr (TAB) lut_issue(q.c[2 * h + s], lut2, lv[h][s]);
+      else lut_issue16(q.c[2 * h + s], lut2, lv[h][s]);
+    }
 }
 
 __device__ __forceinline__ const char* a_frag_addr(const char* buf, int mt, int s, int lane) {
@@ -172,7 +196,7 @@ __device__ __forceinline__ void stage_a(rsrc_t ar, const uint32_t* voff, int pw,
     __builtin_amdgcn_raw_ptr_buffer_load_lds(ar, (lds_ptr_t)(wave_dst + i * 1024), 16, voff[i], soff, 0, 0);
 }
 
-template <int MT, int MODE>
+template <int MT, int MODE, int TAB>
 __global__ __launch_bounds__(NTHR, 2) void gemm_w4v3_k(const bf16* __restrict__ A, int lda,
                                                       const uint32_t* __restrict__ codes,
                                                       const float* __restrict__ absmax_t,
@@ -190,11 +214,13 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_w4v3_k(const bf16* __restrict__ 
   const char* lut2 = lds;  // 256 × float2 pair table at LDS offset 0
   char* smem = lds + 2048;
   constexpr bool BWD = MODE == 1;
-  {
+  if constexpr (TAB) {
     const uint32_t v = threadIdx.x;  // NTHR == 256: one entry per thread
     const float lo = MODE == 2 ? (float)(v & 15) : kNF4v3[v & 15];
     const float hi = MODE == 2 ? (float)(v >> 4) : kNF4v3[v >> 4];
     reinterpret_cast<f32x2*>(lds)[v] = f32x2{lo, hi};
+  } else if (threadIdx.x < 16) {
+    reinterpret_cast<float*>(lds)[threadIdx.x] = MODE == 2 ? (float)threadIdx.x : kNF4v3[threadIdx.x];
   }
 
   const int tiles_m = (M + BM - 1) / BM, tiles_c = (C + BN - 1) / BN;
@@ -244,7 +270,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_w4v3_k(const bf16* __restrict__ 
   __syncthreads();
   bf16x8 wf[2][2];
   f32x2 lv[2][2][4];
-  lut_step<MODE>(q1, lut2, lv);
+  lut_step<MODE, TAB>(q1, lut2, lv);
   convert_half<MODE>(q1, lv, wf, 0);
   convert_half<MODE>(q1, lv, wf, 1);
   q1 = q2;
@@ -254,7 +280,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_w4v3_k(const bf16* __restrict__ 
     const char* cur = smem + (t & 1) * ABUF;
     const int tn = t + 1 < nk ? t + 1 : nk - 1;
     stage_a(a_rs, voff, PW, (uint32_t)tn * BK * 2u, wave_dst0 + ((t + 1) & 1) * ABUF);
-    lut_step<MODE>(q1, lut2, lv);  // table reads for step t+1, consumed in the second half
+    lut_step<MODE, TAB>(q1, lut2, lv);  // table reads for step t+1, consumed in the second half
     load_step<MODE>(q2, c_rs, coff, s_rs, b_rs, aoff, t + 2 < nk ? t + 2 : nk - 1, C);
     bf16x8 wn[2][2];
     bf16x8 xr[RD];
@@ -345,23 +371,31 @@ static int pick_mt_v3(int M, int C) {
   return tiles256 >= 512 ? 16 : 8;
 }
 
+int g_gemm3_tab = 1;  // 1: 256-entry pair table, 0: 16-entry table (A/B knob)
+
 void launch_gemm_w4v3(int bwd, const void* A, int lda, const uint32_t* codes, const float* absmax_t,
                       const void* ext_a, const void* ext_b, int R_ext, const void* residual, void* out, int M, int C,
                       int R, hipStream_t st) {
   const int mt = pick_mt_v3(M, C);
   const int BM = mt * 16;
   const int nwg = ((M + BM - 1) / BM) * ((C + BN - 1) / BN);
-#define L(MT_, MODE_)                                                                                         \
-  gemm_w4v3_k<MT_, MODE_><<<nwg, NTHR, 0, st>>>((const bf16*)A, lda, codes, absmax_t, nullptr,               \
-                                                (const bf16*)ext_a, (const bf16*)ext_b, R_ext,                \
-                                                (const bf16*)residual, (bf16*)out, M, C, R)
+#define L(MT_, MODE_, TAB_)                                                                                    \
+  gemm_w4v3_k<MT_, MODE_, TAB_><<<nwg, NTHR, 0, st>>>((const bf16*)A, lda, codes, absmax_t, nullptr,          \
+                                                      (const bf16*)ext_a, (const bf16*)ext_b, R_ext,          \
+                                                      (const bf16*)residual, (bf16*)out, M, C, R)
+#define L2(MT_, MODE_)      \
+  if (g_gemm3_tab)          \
+    L(MT_, MODE_, 1);       \
+  else                      \
+    L(MT_, MODE_, 0)
   if (bwd) {
-    if (mt == 16) L(16, 1);
-    else L(8, 1);
+    if (mt == 16) { L2(16, 1); }
+    else { L2(8, 1); }
   } else {
-    if (mt == 16) L(16, 0);
-    else L(8, 0);
+    if (mt == 16) { L2(16, 0); }
+    else { L2(8, 0); }
   }
+#undef L2
 #undef L
   LIPA_CHECK_LAUNCH();
 }
@@ -376,10 +410,10 @@ void launch_gemm_int4_v3(const void* A, int lda, const uint32_t* codes, const fl
   const int BM = mt * 16;
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (mt == 16)
-    gemm_w4v3_k<16, 2><<<nwg, NTHR, 0, st>>>((const bf16*)A, lda, codes, scale_t, bias_t, (const bf16*)ext_a,
+    gemm_w4v3_k<16, 2, 1><<<nwg, NTHR, 0, st>>>((const bf16*)A, lda, codes, scale_t, bias_t, (const bf16*)ext_a,
                                              (const bf16*)ext_b, R_ext, (const bf16*)residual, (bf16*)out, M, N, K);
   else
-    gemm_w4v3_k<8, 2><<<nwg, NTHR, 0, st>>>((const bf16*)A, lda, codes, scale_t, bias_t, (const bf16*)ext_a,
+    gemm_w4v3_k<8, 2, 1><<<nwg, NTHR, 0, st>>>((const bf16*)A, lda, codes, scale_t, bias_t, (const bf16*)ext_a,
                                             (const bf16*)ext_b, R_ext, (const bf16*)residual, (bf16*)out, M, N, K);
   LIPA_CHECK_LAUNCH();
 }
