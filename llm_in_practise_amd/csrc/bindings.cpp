@@ -8,7 +8,7 @@
 
 // ---- launcher declarations (csrc/kernels/*.hip)
 void launch_rmsnorm_fwd(int, const void*, const void*, void*, float*, int, int, float, hipStream_t);
-void launch_rmsnorm_bwd(int, const void*, const void*, const void*, const float*, void*, float*, float*, int, int,
+void launch_rmsnorm_bwd(int, const void*, const void*, const void*, const float*, void*, float*, float*, int, int, const void*,
                         hipStream_t);
 void launch_layernorm_fwd(int, const void*, const void*, const void*, void*, float*, float*, int, int, float,
                           hipStream_t);
@@ -61,7 +61,7 @@ void launch_moe_permute(const int*, int, int, int*, int*, int*, hipStream_t);
 void launch_moe_gather(int, const void*, const int*, const float*, void*, int, int, int, hipStream_t);
 void launch_moe_combine(int, const void*, const int*, const float*, const void*, void*, int, int, int, hipStream_t);
 void launch_moe_wgrad(int, const void*, const void*, const int*, float*, int, int, int, hipStream_t);
-int lora_acc_chunks(int M);
+int lora_acc_chunks(int M, int K);
 void launch_lora_acc(const float*, int, int, const void*, int, void*, int, const void*, int, float*, int64_t, int64_t,
                      float*, int, uint64_t, float, size_t, hipStream_t);
 void launch_decode_attention(const void*, const void*, const void*, const int*, float*, float*, float*, void*, int, int,
@@ -109,9 +109,14 @@ std::vector<Tensor> rmsnorm_fwd(Tensor x, optional<Tensor> w, double eps) {
   return {y, rstd};
 }
 
-std::vector<Tensor> rmsnorm_bwd(Tensor dy, Tensor x, optional<Tensor> w, Tensor rstd, bool need_dw) {
+std::vector<Tensor> rmsnorm_bwd(Tensor dy, Tensor x, optional<Tensor> w, Tensor rstd, bool need_dw,
+                                optional<Tensor> dres) {
   CHECK_CONTIG(dy);
   CHECK_CONTIG(x);
+  if (dres && dres->defined()) {
+    TORCH_CHECK(dres->is_contiguous() && dres->sizes() == x.sizes() && dres->scalar_type() == x.scalar_type(),
+                "rmsnorm_bwd: dres must match x");
+  }
   const int N = x.size(-1), M = x.numel() / N;
   auto dx = at::empty_like(x);
   Tensor part, dw;
@@ -121,7 +126,7 @@ std::vector<Tensor> rmsnorm_bwd(Tensor dy, Tensor x, optional<Tensor> w, Tensor 
   }
   launch_rmsnorm_bwd(dtype_code(x), dy.data_ptr(), x.data_ptr(), optr(w), rstd.data_ptr<float>(), dx.data_ptr(),
                      need_dw ? part.data_ptr<float>() : nullptr, need_dw ? dw.data_ptr<float>() : nullptr, M, N,
-                     stream());
+                     optr(dres), stream());
   return {dx, dw};
 }
 
@@ -533,7 +538,7 @@ void lora_acc(Tensor g, Tensor x, int64_t c0, int64_t K, Tensor out, bool out_tr
     lddx = dx->stride(0);
   }
   Tensor part;
-  if (deterministic) part = at::empty({lora_acc_chunks(M), r, K}, g.options());
+  if (deterministic) part = at::empty({lora_acc_chunks(M, K), r, K}, g.options());
   launch_lora_acc(g.data_ptr<float>(), g.stride(0), r, (const char*)x.data_ptr() + c0 * 2, x.stride(0), dxp, lddx,
                   dx ? w->data_ptr() : nullptr, K, out.data_ptr<float>(), sj, sk,
                   deterministic ? part.data_ptr<float>() : nullptr, M, (uint64_t)key, (float)p,

@@ -86,88 +86,96 @@ __global__ __launch_bounds__(NW * 64) void lora_proj_k(const bf16* __restrict__ 
   }
 }
 
-template <int R, bool DXU>
-__global__ __launch_bounds__(256) void lora_acc_k(const float* __restrict__ G, int ldg, int r,
-                                                 const bf16* __restrict__ X, int ldx, bf16* __restrict__ DX, int lddx,
-                                                 const bf16* __restrict__ W, int K, float* __restrict__ out,
-                                                 int64_t sj, int64_t sk, float* __restrict__ part, int M,
-                                                 int rows_per_chunk, uint64_t key, uint32_t thr16, float dscale,
-                                                 size_t mask_ld) {
+// NRL row-lanes × 64 k-threads (8 consecutive k each); a chunk of ROWS rows is split RB = ROWS/NRL
+// rows per thread, and ALL of a thread's x / dx rows are loaded before any is used (one exposed
+// HBM round trip per workgroup instead of one per 4 rows); the chunk's G rows are staged in LDS.
+template <int R, bool DXU, int NRL, int ROWS>
+__global__ __launch_bounds__(NRL * 64) void lora_acc_k(const float* __restrict__ G, int ldg, int r,
+                                                      const bf16* __restrict__ X, int ldx, bf16* __restrict__ DX,
+                                                      int lddx, const bf16* __restrict__ W, int K,
+                                                      float* __restrict__ out, int64_t sj, int64_t sk,
+                                                      float* __restrict__ part, int M, uint64_t key, uint32_t thr16,
+                                                      float dscale, size_t mask_ld) {
+  constexpr int RB = ROWS / NRL;
+  constexpr int NT = NRL * 64;
   __shared__ float red[64][R * 8 + 1];
+  __shared__ float gs[ROWS][R];
   const int tid = threadIdx.x;
   const int kv = blockIdx.x * 64 + (tid & 63), rl = tid >> 6;
   const int k0 = kv * 8;
   const bool kin = k0 < K;
-  const int c = blockIdx.y;
-  const int mb = c * rows_per_chunk, me = min(mb + rows_per_chunk, M);
-  float acc[R][8];
-#pragma unroll
-  for (int j = 0; j < R; ++j)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[j][i] = 0.f;
+  const int mb = blockIdx.y * ROWS, me = min(mb + ROWS, M);
+  for (int i = tid; i < ROWS * R; i += NT) {
+    const int m = mb + i / R, j = i % R;
+    gs[i / R][j] = (m < me && j < r) ? G[(size_t)m * ldg + j] : 0.f;
+  }
   bf16x8 wv[DXU ? R : 1];
   if constexpr (DXU) {
 #pragma unroll
     for (int j = 0; j < R; ++j) wv[j] = (kin && j < r) ? *reinterpret_cast<const bf16x8*>(W + (size_t)j * K + k0) : bf16x8{};
   }
-  // rows m = mb + rl + 4i; RB rows are loaded together (x, dx, g) so RB × 16-32 B per thread are in
-  // flight — one dependent HBM round trip per RB rows instead of per row
-  constexpr int RB = 4;
-  const float ds = thr16 ? dscale : 1.f;
-  for (int m0 = mb + rl; kin && m0 < me; m0 += 4 * RB) {
-    float xv[RB][8], dv[DXU ? RB : 1][8], g[RB][R];
-    uint32_t keep[RB];
+  bf16x8 xb[RB], db[DXU ? RB : 1];
 #pragma unroll
-    for (int q = 0; q < RB; ++q) {
-      const int m = min(m0 + 4 * q, M - 1);
-      load8(X + (size_t)m * ldx + k0, xv[q]);
-      if constexpr (DXU) load8(DX + (size_t)m * lddx + k0, dv[q]);
-#pragma unroll
-      for (int j = 0; j < R; ++j) g[q][j] = (j < r && m0 + 4 * q < me) ? G[(size_t)m * ldg + j] : 0.f;
-      keep[q] = thr16 ? dropout_keep8(key, ((size_t)m * mask_ld + k0) >> 3, thr16) : 0xFFu;
+  for (int q = 0; q < RB; ++q) {
+    const int m = min(mb + rl + NRL * q, M - 1);
+    if (kin) {
+      xb[q] = *reinterpret_cast<const bf16x8*>(X + (size_t)m * ldx + k0);
+      if constexpr (DXU) db[q] = *reinterpret_cast<const bf16x8*>(DX + (size_t)m * lddx + k0);
     }
+  }
+  __syncthreads();  // gs ready
+  float acc[R][8];
 #pragma unroll
-    for (int q = 0; q < RB; ++q) {
+  for (int j = 0; j < R; ++j)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) xv[q][i] = ((keep[q] >> i) & 1) ? xv[q][i] * ds : 0.f;
+    for (int i = 0; i < 8; ++i) acc[j][i] = 0.f;
+  const float ds = thr16 ? dscale : 1.f;
+#pragma unroll
+  for (int q = 0; q < RB; ++q) {
+    const int ml = rl + NRL * q, m = mb + ml;
+    if (!kin || m >= me) continue;
+    const uint32_t keep = thr16 ? dropout_keep8(key, ((size_t)m * mask_ld + k0) >> 3, thr16) : 0xFFu;
+    float xv[8], g[R];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xv[i] = ((keep >> i) & 1) ? (float)xb[q][i] * ds : 0.f;
+#pragma unroll
+    for (int j = 0; j < R; ++j) g[j] = gs[ml][j];
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[j][i] += g[j] * xv[i];
+    if constexpr (DXU) {
+      float t[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t[i] = 0.f;
 #pragma unroll
       for (int j = 0; j < R; ++j)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[j][i] += g[q][j] * xv[q][i];
-      if constexpr (DXU) {
-        if (m0 + 4 * q < me) {
-          float t[8];
+        for (int i = 0; i < 8; ++i) t[i] += g[j] * (float)wv[j][i];
+      bf16x8 o;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) t[i] = 0.f;
-#pragma unroll
-          for (int j = 0; j < R; ++j)
-#pragma unroll
-            for (int i = 0; i < 8; ++i) t[i] += g[q][j] * (float)wv[j][i];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) dv[q][i] += ((keep[q] >> i) & 1) ? t[i] * ds : 0.f;
-          store8(DX + (size_t)(m0 + 4 * q) * lddx + k0, dv[q]);
-        }
-      }
+      for (int i = 0; i < 8; ++i) o[i] = (bf16)((float)db[q][i] + (((keep >> i) & 1) ? t[i] * ds : 0.f));
+      *reinterpret_cast<bf16x8*>(DX + (size_t)m * lddx + k0) = o;
     }
   }
-  // reduce the 4 row-lanes through LDS (one wave at a time), then write this chunk's partial
-  for (int s = 0; s < 4; ++s) {
-    if (rl == s) {
+  // reduce the NRL row-lanes through LDS (one wave at a time), then write this chunk's partial
+  for (int s2 = 0; s2 < NRL; ++s2) {
+    if (rl == s2) {
 #pragma unroll
       for (int j = 0; j < R; ++j)
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           float& dst = red[tid & 63][j * 8 + i];
-          dst = (s == 0 ? 0.f : dst) + acc[j][i];
+          dst = (s2 == 0 ? 0.f : dst) + acc[j][i];
         }
     }
     __syncthreads();
   }
-  // this workgroup's 512-wide k block: 256 threads add j-rows with consecutive k per lane (full-rate
+  // this workgroup's 512-wide k block: threads add j-rows with consecutive k per lane (full-rate
   // 256-B atomic wave instructions when sk == 1), straight into the fp32 destination (the grad)
   const int kb = blockIdx.x * 512;
   const bool jfast = sj == 1;        // order lanes along the destination's unit stride (full-rate atomics)
-  for (int idx = tid; idx < r * 512; idx += 256) {
+  for (int idx = tid; idx < r * 512; idx += NT) {
     const int j = jfast ? idx % r : idx / 512, kk = jfast ? idx / r : idx % 512;
     if (kb + kk >= K) continue;
     const float v = red[kk / 8][j * 8 + (kk & 7)];
@@ -196,25 +204,34 @@ void launch_lora_proj(const void* X, int ldx, const void* W, int r, int K, float
 }
 
 // out[j*sj + k*sk] += Σ_m G[m,j]·D(X)[m,k] (fp32 atomics: accumulate straight into a gradient), or
-// with part != null the per-64-row-chunk partials [chunks, r, K] (deterministic mode);
+// with part != null the per-chunk partials [chunks, r, K] (deterministic mode);
 // with DX: DX[m,k] += D(Σ_j G[m,j]·W[j,k]).
-int lora_acc_chunks(int M) { return (M + 63) / 64; }
+// Chunk height: 64 rows, or 32 when that leaves fewer than 256 workgroups (narrow K).
+static int lora_acc_rows(int M, int K) { return ((K / 8 + 63) / 64) * ((M + 63) / 64) >= 256 ? 64 : 32; }
+int lora_acc_chunks(int M, int K) { const int rows = lora_acc_rows(M, K); return (M + rows - 1) / rows; }
 
 void launch_lora_acc(const float* G, int ldg, int r, const void* X, int ldx, void* DX, int lddx, const void* W, int K,
                      float* out, int64_t sj, int64_t sk, float* part, int M, uint64_t key, float p, size_t mask_ld,
                      hipStream_t st) {
   const uint32_t thr = p > 0.f ? (uint32_t)(p * 65536.0f + 0.5f) : 0u;
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  const int rows = 64;
+  const int rows = lora_acc_rows(M, K);
   dim3 grid((K / 8 + 63) / 64, (M + rows - 1) / rows);
-#define A(R_, D_)                                                                                             \
-  lora_acc_k<R_, D_><<<grid, 256, 0, st>>>(G, ldg, r, (const bf16*)X, ldx, (bf16*)DX, lddx, (const bf16*)W, K, \
-                                           out, sj, sk, part, M, rows, key, thr, ds, mask_ld)
+// r <= 8: 8 row-lanes (512 threads, 2 waves/SIMD); r <= 16: 4 row-lanes (the accumulators double)
+#define A(R_, D_, ROWS_)                                                                                          \
+  lora_acc_k<R_, D_, (R_ > 8 ? 4 : 8), ROWS_><<<grid, (R_ > 8 ? 256 : 512), 0, st>>>(                            \
+      G, ldg, r, (const bf16*)X, ldx, (bf16*)DX, lddx, (const bf16*)W, K, out, sj, sk, part, M, key, thr, ds, mask_ld)
+#define B(R_, D_)       \
+  if (rows == 64)       \
+    A(R_, D_, 64);      \
+  else                  \
+    A(R_, D_, 32)
   if (r <= 8) {
-    if (DX) A(8, true); else A(8, false);
+    if (DX) { B(8, true); } else { B(8, false); }
   } else {
-    if (DX) A(16, true); else A(16, false);
+    if (DX) { B(16, true); } else { B(16, false); }
   }
+#undef B
 #undef A
   LIPA_CHECK_LAUNCH();
 }

@@ -55,7 +55,7 @@ template <typename T, typename TW, int CH>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
                                                      const TW* __restrict__ w, const float* __restrict__ rstd,
                                                      T* __restrict__ dx, float* __restrict__ dw_part, int M,
-                                                     int N) {
+                                                     int N, const T* __restrict__ dres) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int row = blockIdx.x * ROWS + wid;
   const bool valid = row < M;
@@ -91,6 +91,12 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_k(const T* __restrict__ dy, c
       float o[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = r * (gv[c][i] * (w ? wv[i] : 1.f) - xv[c][i] * dot);
+      if (dres) {  // the residual branch's gradient (x feeds both the norm and the skip connection)
+        float rv[8];
+        load8(dres + (size_t)row * N + col, rv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] += rv[i];
+      }
       store8(dx + (size_t)row * N + col, o);
     }
   }
@@ -287,15 +293,15 @@ void launch_rmsnorm_fwd(int dtype, const void* x, const void* w, void* y, float*
 }
 
 void launch_rmsnorm_bwd(int dtype, const void* dy, const void* x, const void* w, const float* rstd, void* dx,
-                        float* dw_part, float* dw, int M, int N, hipStream_t st) {
+                        float* dw_part, float* dw, int M, int N, const void* dres, hipStream_t st) {
   dim3 g((M + ROWS - 1) / ROWS), b(256);
 #define F(CH)                                                                                               \
   if (dtype == 1)                                                                                           \
     rmsnorm_bwd_k<bf16, bf16, CH><<<g, b, 0, st>>>((const bf16*)dy, (const bf16*)x, (const bf16*)w, rstd,   \
-                                                   (bf16*)dx, dw_part, M, N);                               \
+                                                   (bf16*)dx, dw_part, M, N, (const bf16*)dres);          \
   else                                                                                                      \
     rmsnorm_bwd_k<float, float, CH><<<g, b, 0, st>>>((const float*)dy, (const float*)x, (const float*)w,    \
-                                                     rstd, (float*)dx, dw_part, M, N);
+                                                     rstd, (float*)dx, dw_part, M, N, (const float*)dres);
   LIPA_CH_DISPATCH(N, F);
 #undef F
   if (dw_part) colsum_k<<<(N + 255) / 256, 256, 0, st>>>(dw_part, dw, g.x, N);

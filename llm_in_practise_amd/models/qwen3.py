@@ -30,7 +30,7 @@ from ..ops.activation import swiglu_fused
 from ..ops.attention import flash_attention
 from ..ops.decode import decode_attention
 from ..ops.loss import fused_linear_cross_entropy, shift_labels
-from ..ops.norm import RMSNorm, rms_norm
+from ..ops.norm import RMSNorm, rms_norm, rms_norm_residual
 from ..ops.rope import qk_norm_rope
 from .common import CausalLMOutput, FusedProjection, KVCache, can_fuse, project
 
@@ -190,10 +190,10 @@ class Qwen3DecoderLayer(nn.Module):
         self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
 
     def forward(self, x, cos, sin, B, S, cache=None, start=0, kv_lens=None):
-        h = self.self_attn(rms_norm(x, self.input_layernorm.weight, self.input_layernorm.eps),
-                           cos, sin, B, S, residual=x, cache=cache, start=start, kv_lens=kv_lens)
-        return self.mlp(rms_norm(h, self.post_attention_layernorm.weight, self.post_attention_layernorm.eps),
-                        residual=h)
+        xn, skip = rms_norm_residual(x, self.input_layernorm.weight, self.input_layernorm.eps)
+        h = self.self_attn(xn, cos, sin, B, S, residual=skip, cache=cache, start=start, kv_lens=kv_lens)
+        hn, skip = rms_norm_residual(h, self.post_attention_layernorm.weight, self.post_attention_layernorm.eps)
+        return self.mlp(hn, residual=skip)
 
 
 class Qwen3Model(nn.Module):

@@ -120,6 +120,23 @@ def deterministic() -> bool:
     return os.environ.get("LIPA_DETERMINISTIC", "0") == "1" or torch.are_deterministic_algorithms_enabled()
 
 
+_ZBUF: dict = {}
+
+
+def _zero_buffer(tag: str, rows: int, cols: int, like: torch.Tensor) -> torch.Tensor:
+    """A persistent zero-initialised scratch tensor.  The LoRA extra K-slice buffers only ever
+    get the same block regions rewritten (B blocks / the x·Aᵀ columns); everything else must
+    stay zero, so one allocation + fill serves every step instead of a fill kernel per call.
+    Consumers are stream-ordered (each buffer is read by the GEMM launched right after it is
+    written), so sharing a buffer between projections of the same shape is safe."""
+    key = (tag, rows, cols, like.dtype, like.device)
+    t = _ZBUF.get(key)
+    if t is None:
+        t = torch.zeros(rows, cols, dtype=like.dtype, device=like.device)
+        _ZBUF[key] = t
+    return t
+
+
 def _fast_lora_ok(x, branches) -> bool:
     """Shapes the fused LoRA branch kernels (csrc/kernels/lora.hip) take."""
     K = x.shape[1]
@@ -139,9 +156,13 @@ class _FusedLinearFn(torch.autograd.Function):
             N = base.shape[0]
             rtot = sum(br.a.shape[0] for br in branches)
             rp = (rtot + EXT_ALIGN - 1) // EXT_ALIGN * EXT_ALIGN
-            ext_b = x.new_zeros(N, rp)
-            if fast:
-                ext_a = x.new_zeros(x.shape[0], rp)
+            layout = tuple((br.c0, br.c1, br.a.shape[0]) for br in branches)
+            if x.is_cuda and not torch.cuda.is_current_stream_capturing():
+                ext_b = _zero_buffer(f"lora_b{layout}", N, rp, x)
+                ext_a = _zero_buffer(f"lora_xa{rtot}", x.shape[0], rp, x) if fast else None
+            else:
+                ext_b = x.new_zeros(N, rp)
+                ext_a = x.new_zeros(x.shape[0], rp) if fast else None
             cols, r0 = [], 0
             for br, (a, b) in zip(branches, zip(ab[0::2], ab[1::2])):
                 r = a.shape[0]

@@ -22,7 +22,33 @@ class _RMSNormFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, weight, rstd = ctx.saved_tensors
         need_dw = weight is not None and ctx.needs_input_grad[1]
-        dx, dw = native().rmsnorm_bwd(dy.reshape(x2.shape).contiguous(), x2, weight, rstd, need_dw)
+        dx, dw = native().rmsnorm_bwd(dy.reshape(x2.shape).contiguous(), x2, weight, rstd, need_dw, None)
+        return dx.view(ctx.shape), (dw.to(weight.dtype) if need_dw else None), None
+
+
+class _RMSNormResidualFn(torch.autograd.Function):
+    """(norm(x), x): x feeds both the pre-norm branch and the skip connection.  Returning the
+    skip path from the same node lets backward fold the skip gradient into the norm backward
+    kernel (one pass: dx = norm_bwd(dy_norm) + dy_skip) instead of autograd cloning one
+    gradient and adding the other (two extra [T, hidden] passes per norm)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, eps):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).contiguous()
+        y, rstd = native().rmsnorm_fwd(x2, weight, eps)
+        ctx.save_for_backward(x2, weight, rstd)
+        ctx.shape = shape
+        return y.view(shape), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dskip):
+        x2, weight, rstd = ctx.saved_tensors
+        need_dw = weight is not None and ctx.needs_input_grad[1]
+        if dy is None:
+            return dskip, None, None
+        dres = None if dskip is None else dskip.reshape(x2.shape).contiguous()
+        dx, dw = native().rmsnorm_bwd(dy.reshape(x2.shape).contiguous(), x2, weight, rstd, need_dw, dres)
         return dx.view(ctx.shape), (dw.to(weight.dtype) if need_dw else None), None
 
 
@@ -30,6 +56,14 @@ def rms_norm(x: torch.Tensor, weight: torch.Tensor | None, eps: float = 1e-6) ->
     if use_native(x):
         return _RMSNormFn.apply(x, weight, eps)
     return ref.rmsnorm(x, weight, eps)
+
+
+def rms_norm_residual(x: torch.Tensor, weight: torch.Tensor | None, eps: float = 1e-6):
+    """Pre-norm block entry: returns ``(rmsnorm(x), skip)`` where ``skip`` is ``x`` for the
+    residual add; on the GPU the two gradients meet inside the norm backward kernel."""
+    if use_native(x):
+        return _RMSNormResidualFn.apply(x, weight, eps)
+    return ref.rmsnorm(x, weight, eps), x
 
 
 class _LayerNormFn(torch.autograd.Function):

@@ -1,0 +1,11 @@
+#!/bin/bash
+# kernel tests (subset by -k expr) then N bench runs.  usage: scripts/gpu_quick.sh "<-k expr>" <nbench>
+set -u
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+mkdir -p gpurun_out
+timeout -k 10 400 python -m pytest tests -m gpu -q -x -k "$1" --timeout 120 --timeout-method thread > gpurun_out/q_tests.log 2>&1 || { tail -30 gpurun_out/q_tests.log; exit 1; }
+tail -1 gpurun_out/q_tests.log
+for i in $(seq 1 $2); do
+timeout -k 10 300 python bench.py --steps 8 --warmup 2 > gpurun_out/q_bench.log 2>&1 || { tail -20 gpurun_out/q_bench.log; exit 1; }
+echo "$(grep -o '[0-9.]* ms/step  [0-9,]* tok/s' gpurun_out/q_bench.log)"
+done

@@ -34,10 +34,27 @@ def test_rmsnorm_fwd_bwd(native_ext, M, N):
     yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * wr
     assert rel_err(y, yr) < 1e-2
     dy = torch.randn_like(x)
-    dx, dw = native_ext.rmsnorm_bwd(dy, x, w, rstd, True)
+    dx, dw = native_ext.rmsnorm_bwd(dy, x, w, rstd, True, None)
     yr.backward(dy.float())
     assert rel_err(dx, xr.grad) < 1e-2
     assert rel_err(dw, wr.grad) < 1e-2
+
+
+def test_rmsnorm_residual_fn(native_ext):
+    """(norm(x), skip) node: the skip gradient is folded into the norm backward kernel."""
+    from llm_in_practise_amd.ops.norm import rms_norm_residual
+    M, N = 256, 1024
+    x = torch.randn(M, N, device=DEV, dtype=torch.bfloat16).requires_grad_(True)
+    w = (1 + 0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    y, skip = rms_norm_residual(x, w, 1e-6)
+    g1, g2 = torch.randn_like(y), torch.randn_like(y)
+    ((y * g1).sum() + (skip * g2).sum()).backward()
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * wr
+    ((yr * g1.float()).sum() + (xr * g2.float()).sum()).backward()
+    assert rel_err(x.grad, xr.grad) < 1e-2
+    assert rel_err(w.grad, wr.grad) < 1e-2
 
 
 @pytest.mark.parametrize("M,N", [(512, 768), (33, 1024), (16, 64)])
