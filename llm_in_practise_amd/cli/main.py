@@ -234,9 +234,33 @@ def cmd_finetune(a):
 
 
 # ============================================================================ inference / quant
-def _load_for_inference(path, adapter=None, device=None, quant=None, fuse=True):
+def _tp_group():
+    """torchrun with WORLD_SIZE > 1 on an inference command = tensor parallel over all ranks
+    (the vLLM ``--tensor-parallel-size`` role)."""
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        return None
+    from ..parallel import dist as D
+    D.init_distributed()
+    import torch.distributed as dist
+    return dist.group.WORLD
+
+
+def _load_for_inference(path, adapter=None, device=None, quant=None, fuse=True, tp_group=None):
     from ..models.qwen3 import BitsAndBytesConfig, Qwen3ForCausalLM, qwen3_config
     dev = device or _device()
+    if tp_group is not None:      # shard the bf16 weights (+ adapter), THEN quantise the shards
+        from ..parallel.tensor_parallel import apply_tensor_parallel
+        from ..peft.lora import quantize_model_nf4
+        m = _load_for_inference(path, adapter, dev, None, fuse=False)
+        apply_tensor_parallel(m, tp_group)
+        if quant == "nf4":
+            quantize_model_nf4(m)
+        lm = m
+        while not hasattr(lm, "fuse_projections") and hasattr(lm, "model"):
+            lm = lm.model
+        if fuse and hasattr(lm, "fuse_projections"):
+            lm.fuse_projections()
+        return m.eval()
     if path.startswith("random:"):
         m = Qwen3ForCausalLM.from_config(qwen3_config(path[7:]), dtype=torch.bfloat16, device=dev)
     else:
@@ -292,13 +316,16 @@ def cmd_chat(a):
 def cmd_infer(a):
     from ..infer.generate import generate
     from ..train.data import load_tokenizer, render_chatml
-    m = _load_for_inference(a.model, a.adapter, quant=a.quant)
+    tp = _tp_group()                 # torchrun → tensor parallel; every rank decodes in lockstep
+    m = _load_for_inference(a.model, a.adapter, quant=a.quant, tp_group=tp)
     tok = load_tokenizer(a.tokenizer or a.model)
     text = render_chatml([{"role": "user", "content": a.prompt}], add_generation_prompt=True) if a.chat else a.prompt
     ids = torch.tensor([tok.encode(text, add_special_tokens=False)], device=_device())
     out = generate(m, ids, max_new_tokens=a.max_new, do_sample=a.temperature > 0, temperature=a.temperature,
-                   top_p=a.top_p, repetition_penalty=a.repetition_penalty, eos_token_id=tok.eos_token_id)
-    print(tok.decode(out[0, ids.shape[1]:].tolist(), skip_special_tokens=True))
+                   top_p=a.top_p, repetition_penalty=a.repetition_penalty, eos_token_id=tok.eos_token_id,
+                   seed=1234 if tp is not None else None)
+    if tp is None or torch.distributed.get_rank() == 0:
+        print(tok.decode(out[0, ids.shape[1]:].tolist(), skip_special_tokens=True))
 
 
 def cmd_merge(a):
@@ -369,14 +396,18 @@ def cmd_serve(a):
     from ..infer.engine import ServingEngine
     from ..infer.server import serve
     from ..train.data import load_tokenizer
-    m = _load_for_inference(a.model, a.adapter, quant=a.quant)
+    tp = _tp_group()
+    m = _load_for_inference(a.model, a.adapter, quant=a.quant, tp_group=tp)
     tok = load_tokenizer(a.tokenizer or a.model)
     moderation = None
     if a.guard_url:
         from ..infer.guard import GuardClient
         moderation = GuardClient(a.guard_url).moderate_sync
     eng = ServingEngine(m, tok, model_name=a.served_model_name or os.path.basename(a.model.rstrip("/")),
-                        max_batch=a.max_batch, system_prompt=a.system)
+                        max_batch=a.max_batch, system_prompt=a.system, tp_group=tp)
+    if tp is not None and eng.tp_rank != 0:
+        eng.follower_loop()              # TP followers replay rank 0's iterations
+        return
     serve(eng, a.host, a.port, api_key=a.api_key, moderation=moderation)
 
 

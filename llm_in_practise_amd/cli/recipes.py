@@ -68,7 +68,7 @@ PRESETS = {
         space_before_end=False, system=DEEPSEEK_R1_SYSTEM, rope_scaling="none",
         output_dir="./finetuned/deepseek-r1-0528-qwen3-8b-qlora-dist"),
     "deepseek-r1-distill-1.5b-lora": FinetunePreset(
-        "deepseek-r1-distill-1.5b-lora", "Scripts/fine-tuning/01-*.py:7-105", "qwen3-small", None, 8, 16, 0.05,
+        "deepseek-r1-distill-1.5b-lora", "Scripts/fine-tuning/01-*.py:7-105", "deepseek-r1-distill-qwen-1.5b", None, 8, 16, 0.05,
         ("q_proj", "v_proj"), 4, 8, 2e-5, 3, "adamw_torch", save_steps=500, grad_ckpt=False,
         output_dir="./finetuned/deepseek-r1-distill-1.5b-lora"),
 }

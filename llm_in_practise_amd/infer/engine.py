@@ -108,8 +108,23 @@ class ServingEngine:
     def __init__(self, model, tokenizer, model_name: str = "lipa-model", max_batch: int = 16,
                  system_prompt: str | None = None, chat_template: str = "auto", space_before_end: bool = False,
                  max_model_len: int | None = None, max_prefill_batch: int = 16, prefill_token_budget: int = 8192,
-                 use_graphs: bool | None = None):
+                 use_graphs: bool | None = None, tp_group=None):
+        """``tp_group``: the model was sharded by ``parallel.tensor_parallel`` over this group.
+        The engine then runs SPMD — group rank 0 owns the request queue and broadcasts each
+        iteration's admissions; the other ranks call :meth:`follower_loop` and replay exactly the
+        same prefill / decode / sampling (logits are bit-identical across ranks, the samplers
+        are seeded identically), so no tokens need to be exchanged."""
         self.model, self.tok, self.model_name = model, tokenizer, model_name
+        self.tp_group = tp_group
+        self.tp_rank = 0
+        if tp_group is not None:
+            import torch.distributed as dist
+            self.tp_rank = dist.get_rank(tp_group)
+            self.tp_src = dist.get_global_rank(tp_group, 0) if hasattr(dist, "get_global_rank") else 0
+            use_graphs = False                 # collectives stay eager (no capture of RCCL calls)
+            from ..ops.decode import seed_sampler
+            seed_sampler(1234)
+            torch.manual_seed(1234)
         self.lm = _unwrap_lm(model)
         self.lm.eval()
         self.max_batch = max_batch
@@ -154,8 +169,14 @@ class ServingEngine:
                 self.graphs = DecodeGraphs(self.lm, self.cache, max_batch, tokens=self.next_tok)
         self._held: _Request | None = None
         self._stop = False
-        self._worker = threading.Thread(target=self._loop, daemon=True)
-        self._worker.start()
+        self._worker = None
+        if self.tp_rank == 0:
+            self._worker = threading.Thread(target=self._loop, daemon=True)
+            self._worker.start()
+
+    def follower_loop(self):
+        """TP ranks > 0: replay rank 0's iterations until it shuts down."""
+        self._loop()
 
     # ------------------------------------------------------------------ prompt formatting
     def build_chat_prompt(self, messages: list[dict]) -> str:
@@ -216,6 +237,33 @@ class ServingEngine:
                 self.cache.pos.zero_()
 
     def _iteration(self):
+        new = self._collect() if self.tp_rank == 0 else []
+        if self.tp_group is not None:
+            new = self._tp_sync(new)
+        if new is None:
+            self._stop = True
+            return
+        with self.lock, torch.no_grad():
+            if new:
+                self._admit(new)
+            if any(s is not None for s in self.slots):
+                self._decode_step()
+
+    def _tp_sync(self, new):
+        """Broadcast this iteration's admissions (slot, prompt ids, sampling params) from TP rank 0."""
+        import torch.distributed as dist
+        payload = None if new is None else [(slot, r.prompt_ids, dataclasses.asdict(r.params), r.t_arrive)
+                                            for slot, r in new]
+        box = [payload]
+        dist.broadcast_object_list(box, src=self.tp_src, group=self.tp_group)
+        if self.tp_rank == 0:
+            return new
+        if box[0] is None:
+            return None
+        return [(slot, _Request(ids, SamplingParams(**pd), False, queue.Queue(), t)) for slot, ids, pd, t in box[0]]
+
+    def _collect(self):
+        """Pull the requests to admit this iteration (None = shut down)."""
         active = [i for i, s in enumerate(self.slots) if s is not None]
         free = [i for i, s in enumerate(self.slots) if s is None]
         new = []
@@ -226,22 +274,20 @@ class ServingEngine:
                 r, self._held = self._held, None
             else:
                 try:
-                    r = self.q.get(block=block, timeout=None if block else 0)
+                    # idle TP ranks wait inside a collective: heartbeat once a second
+                    tmo = (1.0 if self.tp_group is not None else None) if block else 0
+                    r = self.q.get(block=block, timeout=tmo)
                 except queue.Empty:
                     break
             block = False
             if r is None:
-                return
+                return None
             if new and len(r.prompt_ids) > budget:      # over the prefill token budget: next iteration
                 self._held = r
                 break
             budget -= len(r.prompt_ids)
             new.append((free.pop(0), r))
-        with self.lock, torch.no_grad():
-            if new:
-                self._admit(new)
-            if any(s is not None for s in self.slots):
-                self._decode_step()
+        return new
 
     def _admit(self, new):
         """Prefill the new prompts together into a scratch cache, copy into their slots, sample

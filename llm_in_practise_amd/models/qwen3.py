@@ -31,7 +31,8 @@ from ..ops.attention import flash_attention
 from ..ops.decode import decode_attention
 from ..ops.loss import fused_linear_cross_entropy, shift_labels
 from ..ops.norm import RMSNorm, rms_norm, rms_norm_residual
-from ..ops.rope import qk_norm_rope
+from ..ops.rope import apply_rope, qk_norm_rope
+from ..parallel.tensor_parallel import tp_all_reduce
 from .common import CausalLMOutput, FusedProjection, KVCache, can_fuse, project
 
 
@@ -56,11 +57,18 @@ class Qwen3Config:
     torch_dtype: str = "bfloat16"
     model_type: str = "qwen3"
     use_cache: bool = True
+    attention_bias: bool = False      # Qwen2 (DeepSeek-R1-Distill-Qwen) has q/k/v biases
+    qk_norm: bool = True              # Qwen3 per-head q/k RMSNorm; Qwen2 has none
 
     @classmethod
     def from_dict(cls, d: dict) -> "Qwen3Config":
         fields = {f.name for f in dataclasses.fields(cls)}
         kw = {k: v for k, v in d.items() if k in fields}
+        if d.get("model_type") == "qwen2":         # DeepSeek-R1-Distill-Qwen-*: biased qkv, no qk-norm
+            kw.setdefault("attention_bias", True)
+            kw["qk_norm"] = False
+        if "head_dim" not in d and "hidden_size" in d and "num_attention_heads" in d:
+            kw["head_dim"] = d["hidden_size"] // d["num_attention_heads"]
         if "rope_parameters" in d and isinstance(d["rope_parameters"], dict):   # transformers>=5 layout
             rp = d["rope_parameters"]
             kw.setdefault("rope_theta", rp.get("rope_theta", cls.rope_theta))
@@ -75,13 +83,14 @@ class Qwen3Config:
 
     def to_dict(self) -> dict:
         d = dataclasses.asdict(self)
-        d["architectures"] = ["Qwen3ForCausalLM"]
+        d["architectures"] = ["Qwen2ForCausalLM" if self.model_type == "qwen2" else "Qwen3ForCausalLM"]
         return d
 
     def num_params(self) -> int:
         h, f, L = self.hidden_size, self.intermediate_size, self.num_hidden_layers
         d, hq, hkv = self.head_dim, self.num_attention_heads, self.num_key_value_heads
-        attn = h * hq * d * 2 + h * hkv * d * 2 + 2 * d
+        attn = h * hq * d * 2 + h * hkv * d * 2 + (2 * d if self.qk_norm else 0)
+        attn += (hq + 2 * hkv) * d if self.attention_bias else 0
         mlp = 3 * h * f
         emb = self.vocab_size * h * (1 if self.tie_word_embeddings else 2)
         return L * (attn + mlp + 2 * h) + emb + h
@@ -101,6 +110,12 @@ PRESETS: dict[str, dict] = {
                                       max_position_embeddings=131072,
                                       rope_scaling={"rope_type": "yarn", "factor": 4.0,
                                                     "original_max_position_embeddings": 32768}),
+    # Qwen2 architecture (biased q/k/v, no qk-norm): Scripts/inference/*, Scripts/fine-tuning/01-04
+    "deepseek-r1-distill-qwen-1.5b": dict(vocab_size=151936, hidden_size=1536, intermediate_size=8960,
+                                          num_hidden_layers=28, num_attention_heads=12, num_key_value_heads=2,
+                                          head_dim=128, rope_theta=10000.0, max_position_embeddings=131072,
+                                          bos_token_id=151646, eos_token_id=151643, model_type="qwen2",
+                                          attention_bias=True, qk_norm=False),
     # small random-init configs for CPU tests / smoke
     "qwen3-tiny": dict(vocab_size=512, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
                        num_attention_heads=4, num_key_value_heads=2, head_dim=32,
@@ -108,6 +123,9 @@ PRESETS: dict[str, dict] = {
     "qwen3-small": dict(vocab_size=4096, hidden_size=1024, intermediate_size=3072, num_hidden_layers=4,
                         num_attention_heads=8, num_key_value_heads=4, head_dim=128,
                         max_position_embeddings=4096),
+    "qwen2-tiny": dict(vocab_size=512, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
+                       num_attention_heads=4, num_key_value_heads=2, head_dim=32, max_position_embeddings=512,
+                       rope_theta=10000.0, model_type="qwen2", attention_bias=True, qk_norm=False),
 }
 
 
@@ -123,12 +141,17 @@ class Qwen3Attention(nn.Module):
         self.cfg, self.layer_idx = cfg, layer_idx
         h, d = cfg.hidden_size, cfg.head_dim
         self.hq, self.hkv, self.d = cfg.num_attention_heads, cfg.num_key_value_heads, d
-        self.q_proj = nn.Linear(h, self.hq * d, bias=False)
-        self.k_proj = nn.Linear(h, self.hkv * d, bias=False)
-        self.v_proj = nn.Linear(h, self.hkv * d, bias=False)
+        ab = cfg.attention_bias
+        self.q_proj = nn.Linear(h, self.hq * d, bias=ab)
+        self.k_proj = nn.Linear(h, self.hkv * d, bias=ab)
+        self.v_proj = nn.Linear(h, self.hkv * d, bias=ab)
         self.o_proj = nn.Linear(self.hq * d, h, bias=False)
-        self.q_norm = RMSNorm(d, cfg.rms_norm_eps)
-        self.k_norm = RMSNorm(d, cfg.rms_norm_eps)
+        self.tp_group, self.tp_rank = None, 0        # set by parallel.tensor_parallel
+        if cfg.qk_norm:
+            self.q_norm = RMSNorm(d, cfg.rms_norm_eps)
+            self.k_norm = RMSNorm(d, cfg.rms_norm_eps)
+        else:
+            self.q_norm = self.k_norm = None
         self._qkv: FusedProjection | None = None
 
     def fuse(self):
@@ -139,8 +162,15 @@ class Qwen3Attention(nn.Module):
                 kv_lens=None):
         tr = self.training
         qkv = project([self.q_proj, self.k_proj, self.v_proj], x, None, tr, self._qkv)
-        q, k, v = qk_norm_rope(qkv, self.q_norm.weight, self.k_norm.weight, cos, sin,
-                               self.hq, self.hkv, self.d, self.cfg.rms_norm_eps)
+        if self.q_norm is not None:
+            q, k, v = qk_norm_rope(qkv, self.q_norm.weight, self.k_norm.weight, cos, sin,
+                                   self.hq, self.hkv, self.d, self.cfg.rms_norm_eps)
+        else:   # Qwen2: RoPE only
+            T = qkv.shape[0]
+            nq, nk = self.hq * self.d, self.hkv * self.d
+            q = apply_rope(qkv[:, :nq].reshape(T, self.hq, self.d), cos, sin).reshape(T, nq)
+            k = apply_rope(qkv[:, nq:nq + nk].reshape(T, self.hkv, self.d), cos, sin).reshape(T, nk)
+            v = qkv[:, nq + nk:]
         if cache is None:
             o = flash_attention(q, k, v, B, S, self.hq, self.hkv, self.d, causal=True, kv_lens=kv_lens)
         elif cache.pos is not None and S == 1:
@@ -159,7 +189,10 @@ class Qwen3Attention(nn.Module):
                                   vc.view(B, Sk, self.hkv, self.d), causal=True,
                                   key_padding_mask=(torch.arange(Sk, device=x.device)[None] < kv_lens[:, None])
                                   if kv_lens is not None else None).reshape(B * S, -1)
-        return project([self.o_proj], o, residual, tr)
+        if self.tp_group is None:
+            return project([self.o_proj], o, residual, tr)
+        # row-parallel o_proj: partial sums + the residual on rank 0 only, then one all-reduce
+        return tp_all_reduce(project([self.o_proj], o, residual if self.tp_rank == 0 else None, tr), self.tp_group)
 
 
 class Qwen3MLP(nn.Module):
@@ -170,6 +203,7 @@ class Qwen3MLP(nn.Module):
         self.up_proj = nn.Linear(h, f, bias=False)
         self.down_proj = nn.Linear(f, h, bias=False)
         self._gu: FusedProjection | None = None
+        self.tp_group, self.tp_rank = None, 0        # set by parallel.tensor_parallel
 
     def fuse(self):
         mods = [self.gate_proj, self.up_proj]
@@ -178,7 +212,10 @@ class Qwen3MLP(nn.Module):
     def forward(self, x, residual=None):
         tr = self.training
         gu = project([self.gate_proj, self.up_proj], x, None, tr, self._gu)
-        return project([self.down_proj], swiglu_fused(gu), residual, tr)
+        if self.tp_group is None:
+            return project([self.down_proj], swiglu_fused(gu), residual, tr)
+        y = project([self.down_proj], swiglu_fused(gu), residual if self.tp_rank == 0 else None, tr)
+        return tp_all_reduce(y, self.tp_group)
 
 
 class Qwen3DecoderLayer(nn.Module):

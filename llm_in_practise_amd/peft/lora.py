@@ -372,7 +372,7 @@ def prepare_model_for_kbit_training(model: nn.Module, use_gradient_checkpointing
     return model
 
 
-def quantize_model_nf4(model: nn.Module, skip: Iterable[str] = ("lm_head",), double_quant: bool = True,
+def quantize_model_nf4(model: nn.Module, skip: Iterable[str] = ("lm_head", "lora_A", "lora_B"), double_quant: bool = True,
                        compute_dtype=torch.bfloat16) -> nn.Module:
     """Replace every ``nn.Linear`` (except ``skip``) by :class:`Linear4bit` — the
     ``from_pretrained(quantization_config=BitsAndBytesConfig(nf4))`` role."""

@@ -340,7 +340,10 @@ class HFTokenizerWrapper:
 
 
 def load_tokenizer(path: str, pad_to_eos: bool = True):
-    """HF tokenizer from a LOCAL directory (no hub access); pad defaults to eos like the reference."""
+    """HF tokenizer from a LOCAL directory (no hub access); pad defaults to eos like the reference.
+    ``"bytes"`` gives the UTF-8 byte tokenizer (random-init demos and tests, vocab 256)."""
+    if path == "bytes":
+        return ByteTokenizer()
     from transformers import AutoTokenizer
     tok = AutoTokenizer.from_pretrained(path, local_files_only=True, trust_remote_code=False)
     if pad_to_eos and tok.pad_token is None:

@@ -320,18 +320,23 @@ def test_dropout_counter_rng(native_ext):
     assert torch.equal(dx != 0, kept & (t != 0))
 
 
-@pytest.mark.parametrize("mode", ["qlora", "lora"])
-def test_qwen3_native_matches_reference(mode, monkeypatch):
+@pytest.mark.parametrize("mode,arch", [("qlora", "qwen3"), ("lora", "qwen3"), ("qlora", "qwen2")])
+def test_qwen3_native_matches_reference(mode, arch, monkeypatch):
     """Whole-model check: the HIP path (fused q|k|v / gate|up GEMMs, LoRA K-slice, flash attention,
-    qk-norm+RoPE, fused CE) against the pure-PyTorch path on the same weights (dropout off)."""
+    qk-norm+RoPE (Qwen3) or biased qkv + RoPE (Qwen2), fused CE) against the pure-PyTorch path on
+    the same weights (dropout off)."""
     from llm_in_practise_amd.models.qwen3 import Qwen3ForCausalLM, qwen3_config
     from llm_in_practise_amd.peft.lora import LoraConfig, get_peft_model, quantize_model_nf4
-    cfg = qwen3_config("qwen3-tiny", vocab_size=512, hidden_size=256, intermediate_size=512,
-                       num_attention_heads=4, num_key_value_heads=2, head_dim=64)
+    cfg = qwen3_config("qwen3-tiny" if arch == "qwen3" else "qwen2-tiny", vocab_size=512, hidden_size=256,
+                       intermediate_size=512, num_attention_heads=4, num_key_value_heads=2, head_dim=64)
 
     def build():
         torch.manual_seed(0)
         m = Qwen3ForCausalLM.from_config(cfg, dtype=torch.bfloat16, device=DEV)
+        with torch.no_grad():
+            for n, p in m.named_parameters():
+                if n.endswith(".bias"):
+                    p.normal_(0, 0.05)
         if mode == "qlora":
             quantize_model_nf4(m)
         pm = get_peft_model(m, LoraConfig(r=8, lora_alpha=16, lora_dropout=0.0, target_modules=["q_proj", "v_proj"]))
