@@ -404,7 +404,9 @@ def cmd_serve(a):
         from ..infer.guard import GuardClient
         moderation = GuardClient(a.guard_url).moderate_sync
     eng = ServingEngine(m, tok, model_name=a.served_model_name or os.path.basename(a.model.rstrip("/")),
-                        max_batch=a.max_batch, system_prompt=a.system, tp_group=tp)
+                        max_batch=a.max_batch, system_prompt=a.system, tp_group=tp,
+                        max_model_len=a.max_model_len,
+                        prefix_cache_blocks=a.prefix_blocks if a.prefix_caching else 0)
     if tp is not None and eng.tp_rank != 0:
         eng.follower_loop()              # TP followers replay rank 0's iterations
         return
@@ -415,6 +417,13 @@ def cmd_guard(a):
     import uvicorn
     from ..infer.guard import GuardClient, create_guard_app
     uvicorn.run(create_guard_app(GuardClient(a.backend, a.model), a.api_key), host=a.host, port=a.port)
+
+
+def cmd_cache_gateway(a):
+    import uvicorn
+    from ..infer.cache_gateway import create_cache_gateway, http_backend, make_store
+    app = create_cache_gateway(http_backend(a.backend, a.api_key), make_store(a.redis), a.exact_ttl, a.semantic_ttl)
+    uvicorn.run(app, host=a.host, port=a.port)
 
 
 def cmd_convert_alpaca(a):
@@ -638,6 +647,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--api-key", dest="api_key")
     p.add_argument("--guard-url", dest="guard_url")
     p.add_argument("--system", default=None)
+    p.add_argument("--enable-prefix-caching", dest="prefix_caching", action="store_true",
+                   help="reuse the KV of cached prompt chunks (vLLM --enable-prefix-caching)")
+    p.add_argument("--prefix-cache-blocks", dest="prefix_blocks", type=int, default=1024,
+                   help="HBM pool size in 64-token chunks")
+    p.add_argument("--max-model-len", dest="max_model_len", type=int, default=None)
     p.set_defaults(fn=cmd_serve)
 
     p = sub.add_parser("guard")
@@ -647,6 +661,16 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--port", type=int, default=8099)
     p.add_argument("--api-key", dest="api_key", default=None)
     p.set_defaults(fn=cmd_guard)
+
+    p = sub.add_parser("cache-gateway", help="exact + semantic response cache in front of a server (H6)")
+    p.add_argument("--backend", required=True, help="upstream OpenAI-compatible base URL")
+    p.add_argument("--api-key", dest="api_key", default=None)
+    p.add_argument("--redis", default=None, help="redis://host:port/db (default: in-process store)")
+    p.add_argument("--exact-ttl", dest="exact_ttl", type=int, default=300)
+    p.add_argument("--semantic-ttl", dest="semantic_ttl", type=int, default=600)
+    p.add_argument("--host", default="0.0.0.0")
+    p.add_argument("--port", type=int, default=8088)
+    p.set_defaults(fn=cmd_cache_gateway)
 
     p = sub.add_parser("convert-alpaca")
     p.add_argument("--input", required=True)

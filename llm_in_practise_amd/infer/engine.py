@@ -60,6 +60,84 @@ class _Request:
     rid: str = dataclasses.field(default_factory=lambda: uuid.uuid4().hex)
 
 
+class PrefixCache:
+    """Automatic prefix caching — the vLLM ``--enable-prefix-caching`` / LMCache chunk-reuse role
+    (``LLM_on_Kubernetes/Inference_Platfrom/07-L1-Cache``, README "APC": system-prompt /
+    RAG-document / multi-turn TTFT reductions).
+
+    Prompts are cut into ``block``-token chunks identified by a chained content hash (blake2b of
+    the previous chunk's digest + this chunk's token ids — stable across processes, so TP ranks
+    and restarts agree without PYTHONHASHSEED).  Each cached chunk keeps its K/V rows for every
+    layer in an HBM pool ``[layers][capacity, block, Hkv·D]``; a hit copies the longest cached
+    chunk run into the request's KV slot (one gather per layer) and only the suffix is
+    prefilled.  LRU eviction; at least one prompt token is always recomputed (its logits seed
+    the first sampled token)."""
+
+    def __init__(self, n_layers: int, width: int, dtype, device, block: int = 64, capacity_blocks: int = 512):
+        import collections
+        self.block, self.capacity = block, capacity_blocks
+        self.k = [torch.zeros(capacity_blocks, block, width, dtype=dtype, device=device) for _ in range(n_layers)]
+        self.v = [torch.zeros(capacity_blocks, block, width, dtype=dtype, device=device) for _ in range(n_layers)]
+        self.map: "collections.OrderedDict[bytes, int]" = collections.OrderedDict()
+        self.free = list(range(capacity_blocks))
+        self.hit_tokens = 0
+        self.query_tokens = 0
+
+    def _digests(self, ids: list[int], n_blocks: int) -> list[bytes]:
+        import hashlib
+        out, prev = [], b""
+        for i in range(n_blocks):
+            h = hashlib.blake2b(prev, digest_size=16)
+            h.update(torch.tensor(ids[i * self.block:(i + 1) * self.block], dtype=torch.int32).numpy().tobytes())
+            prev = h.digest()
+            out.append(prev)
+        return out
+
+    def match(self, ids: list[int]) -> list[int]:
+        """Pool indices of the longest cached chunk run (leaving >= 1 token to prefill)."""
+        n = (len(ids) - 1) // self.block
+        idx = []
+        for d in self._digests(ids, n):
+            j = self.map.get(d)
+            if j is None:
+                break
+            self.map.move_to_end(d)
+            idx.append(j)
+        self.query_tokens += len(ids)
+        self.hit_tokens += len(idx) * self.block
+        return idx
+
+    def load(self, idx: list[int], cache: KVCache, slot: int):
+        n = len(idx) * self.block
+        t = torch.tensor(idx, device=self.k[0].device)
+        for l in range(len(self.k)):
+            cache.k[l][slot, :n] = self.k[l][t].reshape(n, -1)
+            cache.v[l][slot, :n] = self.v[l][t].reshape(n, -1)
+
+    def store(self, ids: list[int], cache: KVCache, slot: int):
+        """Insert every full prompt chunk of a freshly prefilled slot that is not cached yet."""
+        n = len(ids) // self.block
+        new = []
+        for i, d in enumerate(self._digests(ids, n)):
+            if d in self.map:
+                self.map.move_to_end(d)
+                continue
+            if not self.free:
+                _, j = self.map.popitem(last=False)          # evict LRU
+                self.free.append(j)
+            j = self.free.pop()
+            self.map[d] = j
+            new.append((i, j))
+        if not new:
+            return
+        src = torch.tensor([i for i, _ in new], device=self.k[0].device)
+        dst = torch.tensor([j for _, j in new], device=self.k[0].device)
+        B = self.block
+        for l in range(len(self.k)):
+            self.k[l][dst] = cache.k[l][slot, :n * B].view(n, B, -1)[src]
+            self.v[l][dst] = cache.v[l][slot, :n * B].view(n, B, -1)[src]
+
+
 @dataclasses.dataclass
 class _Slot:
     req: _Request
@@ -108,7 +186,8 @@ class ServingEngine:
     def __init__(self, model, tokenizer, model_name: str = "lipa-model", max_batch: int = 16,
                  system_prompt: str | None = None, chat_template: str = "auto", space_before_end: bool = False,
                  max_model_len: int | None = None, max_prefill_batch: int = 16, prefill_token_budget: int = 8192,
-                 use_graphs: bool | None = None, tp_group=None):
+                 use_graphs: bool | None = None, tp_group=None, prefix_cache_blocks: int = 0,
+                 prefix_block: int = 64):
         """``tp_group``: the model was sharded by ``parallel.tensor_parallel`` over this group.
         The engine then runs SPMD — group rank 0 owns the request queue and broadcasts each
         iteration's admissions; the other ranks call :meth:`follower_loop` and replay exactly the
@@ -158,6 +237,10 @@ class ServingEngine:
         self.cache = KVCache(cfg.num_hidden_layers, max_batch, self.max_len, cfg.num_key_value_heads, cfg.head_dim,
                              self.lm.lm_head.weight.dtype, self.device)
         self.cache.pos = torch.zeros(max_batch, dtype=torch.long, device=self.device)
+        self.prefix = None
+        if prefix_cache_blocks > 0:
+            self.prefix = PrefixCache(cfg.num_hidden_layers, cfg.num_key_value_heads * cfg.head_dim,
+                                      self.lm.lm_head.weight.dtype, self.device, prefix_block, prefix_cache_blocks)
         self.slots: list[_Slot | None] = [None] * max_batch
         self.next_tok = torch.full((max_batch,), self.pad, dtype=torch.long, device=self.device)
         self.graphs = None
@@ -291,7 +374,45 @@ class ServingEngine:
 
     def _admit(self, new):
         """Prefill the new prompts together into a scratch cache, copy into their slots, sample
-        each one's first token."""
+        each one's first token.  With prefix caching, prompts whose leading chunks are cached
+        load them and prefill only their suffix (one request at a time)."""
+        if self.prefix is not None:
+            rest = []
+            for slot, r in new:
+                idx = self.prefix.match(r.prompt_ids)
+                if idx:
+                    self._admit_suffix(slot, r, idx)
+                else:
+                    rest.append((slot, r))
+            if rest:
+                self._admit_batch(rest)
+            for slot, r in new:      # (a slot that already finished keeps its rows until reused)
+                self.prefix.store(r.prompt_ids, self.cache, slot)
+            return
+        self._admit_batch(new)
+
+    def _admit_suffix(self, slot, r, idx):
+        lm = self.lm
+        P = len(idx) * self.prefix.block
+        self.prefix.load(idx, self.cache, slot)
+        view = KVCache.__new__(KVCache)
+        view.k = [t[slot:slot + 1] for t in self.cache.k]
+        view.v = [t[slot:slot + 1] for t in self.cache.v]
+        view.len, view.max_len, view.batch, view.pos = P, self.cache.max_len, 1, None
+        view._rows = self.cache._rows[:1]
+        ids = torch.tensor([r.prompt_ids[P:]], dtype=torch.long, device=self.device)
+        h = lm.model(ids, None, view, None)
+        logits = h[-1:] @ lm.lm_head.weight.t()
+        L = len(r.prompt_ids)
+        self.cache.pos[slot] = L
+        self.slots[slot] = _Slot(r)
+        self.stats["prompt_tokens_total"] += L
+        dev_toks, toks = self._sample(logits, [slot])
+        self.next_tok[slot] = dev_toks[0]
+        self._accept(slot, toks[0], time.time())
+        self.stats["batches_total"] += 1
+
+    def _admit_batch(self, new):
         lm = self.lm
         B = len(new)
         S = max(len(r.prompt_ids) for _, r in new)
@@ -427,6 +548,11 @@ class ServingEngine:
             "# TYPE lipa_num_requests_waiting gauge", f"lipa_num_requests_waiting {self.q.qsize()}",
             "# TYPE lipa_num_requests_running gauge", f"lipa_num_requests_running {s['running']}",
         ]
+        if self.prefix is not None:
+            lines += ["# TYPE lipa_prefix_cache_queries_total counter",
+                      f"lipa_prefix_cache_queries_total {self.prefix.query_tokens}",
+                      "# TYPE lipa_prefix_cache_hits_total counter",
+                      f"lipa_prefix_cache_hits_total {self.prefix.hit_tokens}"]
         lines += self.h_latency.render("lipa_e2e_request_latency_seconds")
         lines += self.h_ttft.render("lipa_time_to_first_token_seconds")
         if torch.cuda.is_available():

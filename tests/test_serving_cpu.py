@@ -118,3 +118,47 @@ def test_continuous_batching_admits_midflight(engine):
     # all 11 requests shared decode steps: far fewer steps than running them one after another
     assert engine.stats["decode_steps_total"] - steps0 < 24 + 10 * 3
     assert all(s is None for s in engine.slots)
+
+
+def test_prefix_caching_same_outputs_and_hits():
+    """APC: a shared long system prompt is prefilled once; greedy outputs are unchanged."""
+    cfg = qwen3_config("qwen3-tiny", vocab_size=256)
+    tok = ByteTokenizer()
+    tok.eos_token_id = 10
+    sysmsg = "You are a careful assistant for the MI355X course. " * 6      # > 4 chunks of 64 tokens
+    outs = {}
+    for blocks in (0, 64):
+        m = Qwen3ForCausalLM.from_config(cfg, dtype=torch.float32, seed=0).eval()
+        e = ServingEngine(m, tok, max_batch=4, system_prompt=sysmsg, prefix_cache_blocks=blocks)
+        p = SamplingParams(max_tokens=6, temperature=0.0)
+        outs[blocks] = [e.complete(e.build_chat_prompt([{"role": "user", "content": q}]), p)["text"]
+                        for q in ("first question", "second one", "first question")]
+        if blocks:
+            assert e.prefix.hit_tokens >= 2 * 4 * 64, e.prefix.hit_tokens
+            assert "lipa_prefix_cache_hits_total" in e.prometheus()
+        e.shutdown()
+    assert outs[0] == outs[64]
+
+
+def test_cache_gateway_exact_and_semantic_levels():
+    """H6 L2/L3 cache gateway: exact SHA-256 key, then the 8-dim/2-decimal semantic key."""
+    from llm_in_practise_amd.infer.cache_gateway import create_cache_gateway
+    calls = []
+
+    def backend(path, body):
+        calls.append(body)
+        return {"id": f"chatcmpl-{len(calls)}", "choices": [{"message": {"content": "answer"}}]}
+
+    c = TestClient(create_cache_gateway(backend))
+    q = {"model": "m", "temperature": 0, "messages": [{"role": "user", "content": "What is xGMI bandwidth?"}]}
+    r1 = c.post("/v1/chat/completions", json=q).json()
+    r2 = c.post("/v1/chat/completions", json=q).json()
+    assert len(calls) == 1 and r2["lipa_cache"] == "exact" and r2["id"] == r1["id"]
+    q2 = dict(q, max_tokens=99)          # different request bytes, same text → semantic hit
+    assert c.post("/v1/chat/completions", json=q2).json()["lipa_cache"] == "semantic" and len(calls) == 1
+    q3 = dict(q, temperature=0.8)        # sampled requests bypass the cache
+    c.post("/v1/chat/completions", json=q3)
+    c.post("/v1/chat/completions", json=q3)
+    assert len(calls) == 3
+    m = c.get("/metrics").text
+    assert "lipa_cache_hits_exact_total 1" in m and "lipa_cache_hits_semantic_total 1" in m
