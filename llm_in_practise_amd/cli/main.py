@@ -426,6 +426,30 @@ def cmd_cache_gateway(a):
     uvicorn.run(app, host=a.host, port=a.port)
 
 
+def cmd_lf(a):
+    """``llamafactory-cli train|export|webchat <yaml>``."""
+    from .llamafactory import lf_export, lf_train, load_lf_yaml
+    cfg = load_lf_yaml(a.config)
+    cfg.update({k: v for k, v in (kv.split("=", 1) for kv in a.overrides)})   # key=value CLI overrides
+    for k in ("learning_rate", "num_train_epochs", "warmup_ratio", "lora_dropout"):
+        if isinstance(cfg.get(k), str):
+            cfg[k] = float(cfg[k])
+    for k in ("max_steps", "save_steps", "logging_steps", "lora_rank", "cutoff_len", "max_samples"):
+        if isinstance(cfg.get(k), str):
+            cfg[k] = int(cfg[k])
+    if a.action == "train":
+        lf_train(cfg, a.tokenizer)
+    elif a.action == "export":
+        print(json.dumps({"exported": lf_export(cfg, a.tokenizer)}))
+    else:  # webchat / api: the OpenAI server + browser UI at /ui
+        ns = argparse.Namespace(model=str(cfg["model_name_or_path"]), adapter=cfg.get("adapter_name_or_path"),
+                                tokenizer=a.tokenizer, quant="nf4" if int(cfg.get("quantization_bit") or 0) == 4
+                                else None, host="0.0.0.0", port=int(cfg.get("port", 7860)), max_batch=16,
+                                served_model_name=None, api_key=None, guard_url=None, system=None,
+                                prefix_caching=True, prefix_blocks=512, max_model_len=None)
+        cmd_serve(ns)
+
+
 def cmd_convert_alpaca(a):
     from ..train.data import load_records, replace_placeholders
     recs = [replace_placeholders(r, a.name, a.author) for r in load_records(a.input)]
@@ -671,6 +695,13 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--host", default="0.0.0.0")
     p.add_argument("--port", type=int, default=8088)
     p.set_defaults(fn=cmd_cache_gateway)
+
+    p = sub.add_parser("lf", help="llamafactory-cli train|export|webchat <yaml> equivalents (E10)")
+    p.add_argument("action", choices=["train", "export", "webchat", "api"])
+    p.add_argument("config")
+    p.add_argument("overrides", nargs="*", help="key=value overrides of the YAML")
+    p.add_argument("--tokenizer", default=None)
+    p.set_defaults(fn=cmd_lf)
 
     p = sub.add_parser("convert-alpaca")
     p.add_argument("--input", required=True)
