@@ -57,3 +57,22 @@ def test_continuous_batching_under_load(lm):
         assert eng.stats["requests_total"] == 20
     finally:
         eng.shutdown()
+
+
+def test_prefix_cache_hit_matches_full_prefill(lm):
+    """APC on the GPU: a prompt whose leading 64-token chunks are cached (loaded into the slot,
+    suffix prefilled against them) decodes the same greedy tokens as a cold full prefill."""
+    p = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True)
+    shared = "system: you answer questions about MI355X kernels. " * 8
+    cold = ServingEngine(lm, _tok(), max_batch=4, use_graphs=True)
+    warm = ServingEngine(lm, _tok(), max_batch=4, use_graphs=True, prefix_cache_blocks=64)
+    try:
+        for q in ("what is LDS?", "what is MFMA?"):
+            a = cold.complete(shared + q, p, timeout=120)["text"]
+            warm.complete(shared + "warm-up", p, timeout=120)
+            b = warm.complete(shared + q, p, timeout=120)["text"]
+            assert a == b
+        assert warm.prefix.hit_tokens >= 2 * 64
+    finally:
+        cold.shutdown()
+        warm.shutdown()
