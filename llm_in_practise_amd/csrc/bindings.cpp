@@ -24,7 +24,7 @@ void launch_swiglu_fwd(const void*, void*, int, int, hipStream_t);
 void launch_swiglu_bwd(const void*, const void*, void*, int, int, hipStream_t);
 void launch_gelu_fwd(int, const void*, void*, size_t, hipStream_t);
 void launch_gelu_bwd(int, const void*, const void*, void*, size_t, hipStream_t);
-void launch_ce_fwd_bwd(int, void*, const int64_t*, float*, int, int, int, const float*, float, hipStream_t);
+void launch_ce_fwd_bwd(int, void*, const int64_t*, float*, int, int, int, const float*, float, int, hipStream_t);
 void launch_grad_norm(int, const void*, size_t, float*, float*, float, int, hipStream_t);
 void launch_adamw(int, float*, const void*, float*, float*, void*, size_t, float, float, float, float, float, float,
                   float, const float*, const float*, hipStream_t);
@@ -253,8 +253,11 @@ Tensor ce_fwd_bwd(Tensor logits, Tensor labels, int64_t ignore_index, Tensor sca
   TORCH_CHECK(V % 8 == 0, "vocab must be a multiple of 8");
   auto loss = at::empty({M}, logits.options().dtype(at::kFloat));
   auto sc = scale.to(at::kFloat).contiguous();
+  // scale: one value, or one per equal group of rows (fused gradient-accumulation micro-batches)
+  TORCH_CHECK(sc.numel() >= 1 && M % sc.numel() == 0, "ce_fwd_bwd: scale groups must split the rows evenly");
+  const int rows_per_scale = sc.numel() > 1 ? M / (int)sc.numel() : 0;
   launch_ce_fwd_bwd(dtype_code(logits), logits.data_ptr(), labels.contiguous().data_ptr<int64_t>(),
-                    loss.data_ptr<float>(), M, V, ignore_index, sc.data_ptr<float>(), 1.f, stream());
+                    loss.data_ptr<float>(), M, V, ignore_index, sc.data_ptr<float>(), 1.f, rows_per_scale, stream());
   return loss;
 }
 

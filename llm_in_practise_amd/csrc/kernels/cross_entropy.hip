@@ -16,12 +16,14 @@ constexpr int NT = 512, NW = NT / 64;
 template <typename T>
 __global__ __launch_bounds__(NT) void ce_fwd_bwd_k(T* __restrict__ logits, const int64_t* __restrict__ labels,
                                                    float* __restrict__ row_loss, int V, int ignore_index,
-                                                   const float* __restrict__ scale_ptr, float scale_val) {
+                                                   const float* __restrict__ scale_ptr, float scale_val,
+                                                   int rows_per_scale) {
   __shared__ float red[NW];
   const int row = blockIdx.x;
   T* lr = logits + (size_t)row * V;
   const int64_t lab = labels[row];
-  const float scale = scale_ptr ? *scale_ptr : scale_val;
+  // per-group scale (gradient-accumulation micro-batches fused into one pass: 1/(G·n_valid_g))
+  const float scale = scale_ptr ? scale_ptr[rows_per_scale > 0 ? row / rows_per_scale : 0] : scale_val;
   if (lab == ignore_index) {
     for (int v = threadIdx.x * 8; v < V; v += NT * 8) {
       if (v + 8 <= V) {
@@ -79,10 +81,13 @@ __global__ __launch_bounds__(NT) void ce_fwd_bwd_k(T* __restrict__ logits, const
 }  // namespace
 
 void launch_ce_fwd_bwd(int dtype, void* logits, const int64_t* labels, float* row_loss, int M, int V,
-                       int ignore_index, const float* scale_ptr, float scale_val, hipStream_t st) {
+                       int ignore_index, const float* scale_ptr, float scale_val, int rows_per_scale,
+                       hipStream_t st) {
   if (dtype == 1)
-    ce_fwd_bwd_k<bf16><<<M, NT, 0, st>>>((bf16*)logits, labels, row_loss, V, ignore_index, scale_ptr, scale_val);
+    ce_fwd_bwd_k<bf16><<<M, NT, 0, st>>>((bf16*)logits, labels, row_loss, V, ignore_index, scale_ptr, scale_val,
+                                         rows_per_scale);
   else
-    ce_fwd_bwd_k<float><<<M, NT, 0, st>>>((float*)logits, labels, row_loss, V, ignore_index, scale_ptr, scale_val);
+    ce_fwd_bwd_k<float><<<M, NT, 0, st>>>((float*)logits, labels, row_loss, V, ignore_index, scale_ptr, scale_val,
+                                          rows_per_scale);
   LIPA_CHECK_LAUNCH();
 }

@@ -338,11 +338,7 @@ class Qwen3ForCausalLM(nn.Module):
             G = num_micro_batches
             if G > 1:
                 assert B % G == 0, "batch must split into equal micro-batches"
-                rows = (B // G) * S
-                loss = sum(fused_linear_cross_entropy(h[g * rows:(g + 1) * rows], self.lm_head.weight,
-                                                      tgt[g * rows:(g + 1) * rows]) for g in range(G)) / G
-            else:
-                loss = fused_linear_cross_entropy(h, self.lm_head.weight, tgt)
+            loss = fused_linear_cross_entropy(h, self.lm_head.weight, tgt, groups=G)
             if return_logits:
                 logits = (h @ self.lm_head.weight.t()).view(B, S, -1)
         else:

@@ -23,38 +23,52 @@ def cross_entropy(logits, labels, ignore_index: int = -100):
 
 class _FusedLinearCEFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, weight, labels, ignore_index, chunk, need_wgrad):
+    def forward(ctx, h, weight, labels, ignore_index, chunk, need_wgrad, groups):
+        """``groups`` > 1: the rows are ``groups`` equal gradient-accumulation micro-batches and the
+        loss is the mean of their per-micro-batch mean losses (row scale 1/(G·n_valid_g)), so
+        the LM head runs as ONE larger GEMM instead of G smaller ones."""
         T = h.shape[0]
-        n_valid = (labels != ignore_index).sum().clamp_min(1)
-        inv = 1.0 / n_valid.float()
+        valid = (labels != ignore_index).view(groups, -1).sum(1).clamp_min(1).float()
+        inv = 1.0 / (valid * groups)                                # [G] per-row-group loss scale
+        rows_g = T // groups
+        if chunk % rows_g and groups > 1:
+            chunk = rows_g * max(1, chunk // rows_g)               # chunks hold whole micro-batches
         dh = torch.empty_like(h)
         dw = torch.zeros(weight.shape, dtype=torch.float32, device=h.device) if need_wgrad else None
-        loss_sum = torch.zeros((), dtype=torch.float32, device=h.device)
+        loss = torch.zeros((), dtype=torch.float32, device=h.device)
         for s in range(0, T, chunk):
             hc = h[s:s + chunk]
             logits = hc @ weight.t()                               # [c, V] bf16 (hipBLASLt)
-            row_loss = native().ce_fwd_bwd(logits, labels[s:s + chunk], ignore_index, inv)
-            loss_sum += row_loss.sum()
+            g0, g1 = s // rows_g, (s + hc.shape[0]) // rows_g
+            row_loss = native().ce_fwd_bwd(logits, labels[s:s + chunk], ignore_index, inv[g0:g1])
+            loss += (row_loss.view(g1 - g0, -1).sum(1) * inv[g0:g1]).sum()
             torch.matmul(logits, weight, out=dh[s:s + chunk])      # dlogits @ W
             if need_wgrad:
                 dw.add_(logits.t().float() @ hc.float())
         ctx.save_for_backward(dh, dw)
-        return loss_sum * inv
+        return loss
 
     @staticmethod
     def backward(ctx, gloss):
         dh, dw = ctx.saved_tensors
-        return (dh * gloss.to(dh.dtype)), (None if dw is None else (dw * gloss).to(torch.bfloat16)), None, None, None, None
+        return ((dh * gloss.to(dh.dtype)), (None if dw is None else (dw * gloss).to(torch.bfloat16)),
+                None, None, None, None, None)
 
 
 def fused_linear_cross_entropy(h: torch.Tensor, weight: torch.Tensor, labels: torch.Tensor,
-                               ignore_index: int = -100, chunk: int = 2048) -> torch.Tensor:
-    """mean CE of ``h @ weightᵀ`` against ``labels`` (already shifted), h [T, d]."""
+                               ignore_index: int = -100, chunk: int = 4096, groups: int = 1) -> torch.Tensor:
+    """mean CE of ``h @ weightᵀ`` against ``labels`` (already shifted), h [T, d].  With
+    ``groups`` = G the rows are G equal micro-batches and the result is the mean over micro-batches
+    of each one's mean loss (gradient-accumulation semantics)."""
     if use_native(h):
         need_w = weight.requires_grad
-        return _FusedLinearCEFn.apply(h.contiguous(), weight, labels.contiguous(), ignore_index, chunk, need_w)
+        return _FusedLinearCEFn.apply(h.contiguous(), weight, labels.contiguous(), ignore_index, chunk, need_w,
+                                      groups)
     logits = h.float() @ weight.float().t()
-    return F.cross_entropy(logits, labels, ignore_index=ignore_index)
+    if groups == 1:
+        return F.cross_entropy(logits, labels, ignore_index=ignore_index)
+    lg, lb = logits.view(groups, -1, logits.shape[-1]), labels.view(groups, -1)
+    return sum(F.cross_entropy(lg[g], lb[g], ignore_index=ignore_index) for g in range(groups)) / groups
 
 
 def shift_labels(labels: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:

@@ -152,6 +152,26 @@ def test_cross_entropy(native_ext, V):
     assert rel_err(lg, lf.grad) < 2e-2
 
 
+@pytest.mark.parametrize("groups", [1, 2])
+def test_fused_linear_ce_groups(native_ext, groups):
+    """LM head + CE in one pass over G fused micro-batches = mean of the per-micro-batch mean
+    losses (gradient-accumulation semantics), loss and dh/dW vs fp32 PyTorch."""
+    from llm_in_practise_amd.ops.loss import fused_linear_cross_entropy
+    T, d, V = 256, 128, 1000
+    h = torch.randn(T, d, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    w = (0.05 * torch.randn(V, d, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    lab = torch.randint(0, V, (T,), device=DEV)
+    lab[: T // groups // 3] = -100          # uneven valid counts across the groups
+    loss = fused_linear_cross_entropy(h, w, lab, groups=groups)
+    loss.backward()
+    hr, wr = h.detach().float().requires_grad_(True), w.detach().float().requires_grad_(True)
+    lg = (hr @ wr.t()).view(groups, -1, V)
+    ref = sum(F.cross_entropy(lg[g], lab.view(groups, -1)[g], ignore_index=-100) for g in range(groups)) / groups
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 2e-3 * ref.item()
+    assert rel_err(h.grad, hr.grad) < 2e-2 and rel_err(w.grad, wr.grad) < 2e-2
+
+
 # ----------------------------------------------------------------------------- optimizer
 def test_adamw_matches_torch(native_ext):
     n = 100_003

@@ -217,3 +217,15 @@ def test_mha_module_matches_torch_nn():
     a = ours(x, x, x, attn_mask=mask, key_padding_mask=kpm)[0]
     b = ref(x, x, x, attn_mask=mask, key_padding_mask=kpm)[0]
     assert torch.allclose(a, b, atol=1e-5)
+
+
+def test_fused_micro_batches_equal_mean_of_losses():
+    """num_micro_batches=G (one pass) == mean of G separate micro-batch losses (CPU path)."""
+    from llm_in_practise_amd.models.qwen3 import Qwen3ForCausalLM, qwen3_config
+    m = Qwen3ForCausalLM.from_config(qwen3_config("qwen3-tiny"), dtype=torch.float32, seed=0)
+    ids = torch.randint(0, 512, (4, 16))
+    lab = ids.clone()
+    lab[0, :10] = -100
+    fused = m(ids, labels=lab, num_micro_batches=2).loss
+    sep = (m(ids[:2], labels=lab[:2]).loss + m(ids[2:], labels=lab[2:]).loss) / 2
+    assert torch.allclose(fused, sep, rtol=1e-5)
