@@ -450,6 +450,20 @@ def cmd_lf(a):
         cmd_serve(ns)
 
 
+def cmd_cluster_check(a):
+    """torchrun-launched collective health probe (H4 ray_cluster_healthcheck.py role)."""
+    from ..parallel import dist as D
+    from ..parallel.healthcheck import cluster_check
+    D.init_distributed(timeout_s=a.timeout)
+    if not D.is_dist():
+        print(json.dumps({"error": "run under torchrun with WORLD_SIZE >= 2"}))
+        return
+    rep = cluster_check(a.allreduce_mib, a.iters)
+    if rep is not None:
+        print(json.dumps(rep, indent=1))
+    D.destroy()
+
+
 def cmd_convert_alpaca(a):
     from ..train.data import load_records, replace_placeholders
     recs = [replace_placeholders(r, a.name, a.author) for r in load_records(a.input)]
@@ -702,6 +716,12 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("overrides", nargs="*", help="key=value overrides of the YAML")
     p.add_argument("--tokenizer", default=None)
     p.set_defaults(fn=cmd_lf)
+
+    p = sub.add_parser("cluster-check", help="per-rank inventory + broadcast / all-reduce probe (torchrun)")
+    p.add_argument("--allreduce-mib", dest="allreduce_mib", type=int, default=64)
+    p.add_argument("--iters", type=int, default=5)
+    p.add_argument("--timeout", type=int, default=300)
+    p.set_defaults(fn=cmd_cluster_check)
 
     p = sub.add_parser("convert-alpaca")
     p.add_argument("--input", required=True)

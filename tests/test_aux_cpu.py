@@ -83,3 +83,34 @@ def test_metrics_and_timer(tmp_path):
         sum(range(1000))
     s = t.summary()
     assert "a" in s and s["a"] >= 0
+
+
+def _hc_worker(rank, world, port, q):
+    import os as _os
+    import torch as _t
+    _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    _t.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    from llm_in_practise_amd.parallel.healthcheck import cluster_check
+    q.put((rank, cluster_check(allreduce_mib=1, iters=1)))
+    _t.distributed.destroy_process_group()
+
+
+def test_cluster_check_gloo():
+    """H4 health probe: inventory of every rank, broadcast + all-reduce values verified."""
+    import socket as _s
+    import torch.multiprocessing as _mp
+    s = _s.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = _mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_hc_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+    assert res[1] is None
+    rep = res[0]
+    assert rep["all_ok"] and rep["world_size"] == 2 and len(rep["ranks"]) == 2
