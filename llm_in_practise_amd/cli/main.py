@@ -151,10 +151,17 @@ def cmd_lm_train(a, strategy="single"):
                      clip_grad_norm=a.clip_grad_norm, strategy=strategy, ds_config=a.ds_config,
                      precision=a.precision, scheduler=a.scheduler, step_per_batch=a.step_per_batch,
                      save_dir=a.save_dir, keep_last=a.keep_last, final_model=a.final_model, seed=a.seed,
-                     max_steps=a.max_steps, grad_accum=a.grad_accum)
-    hist = train_lm(m, ds, cfg, meta={"vocab_size": vocab, "block_size": a.block_size})
+                     max_steps=a.max_steps, grad_accum=a.grad_accum, patience=a.patience, best_model=a.best_model,
+                     resume=a.resume, eval_every_epoch=a.val_fraction > 0)
+    eval_ds = None
+    if a.val_fraction > 0:       # temp/ddp_gpt_bpe_tokenizer_02.py:262-300: seeded random_split
+        n_val = max(1, int(len(ds) * a.val_fraction))
+        ds, eval_ds = torch.utils.data.random_split(ds, [len(ds) - n_val, n_val],
+                                                    generator=torch.Generator().manual_seed(a.seed))
+    hist = train_lm(m, ds, cfg, eval_ds=eval_ds, meta={"vocab_size": vocab, "block_size": a.block_size})
     if D.is_main():
-        print(json.dumps({"train_loss": hist["train_loss"], "strategy": strategy}))
+        print(json.dumps({"train_loss": hist["train_loss"], "eval_loss": hist["eval_loss"],
+                          "global_step": hist.get("global_step"), "strategy": strategy}))
     if strategy != "single":
         D.destroy()
 
@@ -550,6 +557,10 @@ def _lm_args(p):
     p.add_argument("--step_per_batch", action="store_true", help="reproduce the per-batch StepLR of B2/B4/B6")
     p.add_argument("--max_steps", type=int, default=-1)
     p.add_argument("--grad_accum", type=int, default=1)
+    p.add_argument("--val_fraction", type=float, default=0.0, help="seeded random_split validation set (C6)")
+    p.add_argument("--patience", type=int, default=0, help="early stopping on validation loss (C6)")
+    p.add_argument("--best_model", default=None, help="path for the best-validation checkpoint (C6)")
+    p.add_argument("--resume", action="store_true", help="continue from <save_dir>/latest_checkpoint.pt (C6)")
     p.add_argument("--latent_dim", type=int, default=None)
     p.add_argument("--num_experts", type=int, default=8)
     p.add_argument("--top_k", type=int, default=2)

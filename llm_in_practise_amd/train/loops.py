@@ -56,6 +56,10 @@ class LoopConfig:
     seed: int = 42
     max_steps: int = -1
     eval_every_epoch: bool = False
+    # temp/ddp_gpt_bpe_tokenizer_02.py parity (C6): validation split, best model, early stop, resume
+    patience: int = 0                  # epochs without val improvement before stopping (0 = off)
+    best_model: str | None = None      # path for the best-validation weights (rank 0)
+    resume: bool = False               # continue from <save_dir>/latest_checkpoint.pt if present
 
 
 def lm_loss(model: nn.Module, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
@@ -140,7 +144,17 @@ def train_lm(model: nn.Module, train_ds, cfg: LoopConfig, eval_ds=None, meta: di
         sched = None                         # engine steps its own (ds_config WarmupLR)
     hist = {"train_loss": [], "eval_loss": [], "step_time": []}
     step = 0
-    for epoch in range(cfg.epochs):
+    start_epoch, best, bad = 0, float("inf"), 0
+    latest = os.path.join(cfg.save_dir, "latest_checkpoint.pt") if cfg.save_dir else None
+    if cfg.resume and engine is None and latest and os.path.exists(latest):
+        st = _load_latest(latest, model, opt, sched, dev)
+        start_epoch, step, best, bad = st["epoch"], st["global_step"], st["best_val_loss"], st["bad_epochs"]
+        hist = st.get("history", hist)
+        if rank == 0:
+            log.info(f"resumed from {latest}: epoch {start_epoch}, step {step}")
+    from ..utils.faults import FaultInjector
+    faults = FaultInjector()                   # FAULT_INJECT=rank:step:kind (resume / failure tests)
+    for epoch in range(start_epoch, cfg.epochs):
         model.train()
         idx = _sampler_indices(n, world, rank, epoch, cfg.seed)
         tot, cnt, t0 = 0.0, 0, time.time()
@@ -169,6 +183,8 @@ def train_lm(model: nn.Module, train_ds, cfg: LoopConfig, eval_ds=None, meta: di
                 step += 1
                 if sched is not None:
                     sched.step()
+                if faults:
+                    faults.check(step)
             tot += float(loss.detach())
             cnt += 1
             if rank == 0 and cfg.log_every and (bi + 1) % cfg.log_every == 0:
@@ -182,14 +198,35 @@ def train_lm(model: nn.Module, train_ds, cfg: LoopConfig, eval_ds=None, meta: di
             avg = float(t)
         hist["train_loss"].append(avg)
         hist["step_time"].append((time.time() - t0) / max(1, cnt))
+        stop = False
         if eval_ds is not None and cfg.eval_every_epoch:
-            hist["eval_loss"].append(evaluate_lm(engine.module if engine else model, eval_ds, bs))
+            val = evaluate_lm(engine.module if engine else model, eval_ds, bs)   # identical on every rank
+            hist["eval_loss"].append(val)
+            if val < best:
+                best, bad = val, 0
+                if cfg.best_model:
+                    sd = engine.consolidated_state_dict() if engine is not None else model.state_dict()
+                    if rank == 0:
+                        os.makedirs(os.path.dirname(cfg.best_model) or ".", exist_ok=True)
+                        torch.save({"epoch": epoch + 1, "val_loss": val, "model_state_dict": sd, **(meta or {})},
+                                   cfg.best_model)
+            else:
+                bad += 1
+                stop = cfg.patience > 0 and bad >= cfg.patience
         if rank == 0:
-            log.info(f"epoch {epoch + 1}/{cfg.epochs} train loss {avg:.4f}")
+            log.info(f"epoch {epoch + 1}/{cfg.epochs} train loss {avg:.4f}"
+                     + (f" val loss {hist['eval_loss'][-1]:.4f}" if hist["eval_loss"] else ""))
         if cfg.save_dir and (epoch + 1) % cfg.save_interval == 0:
             save_epoch_checkpoint(model, opt, sched, engine, cfg, epoch + 1, meta or {})
+        if latest and engine is None:
+            _save_latest(latest, model, opt, sched, epoch + 1, step, best, bad, hist)
+        if stop:
+            if rank == 0:
+                log.info(f"early stop: no val improvement for {cfg.patience} epochs")
+            break
         if 0 < cfg.max_steps <= step:
             break
+    hist["global_step"] = step
     if cfg.final_model:
         sd = engine.consolidated_state_dict() if engine is not None else model.state_dict()
         if rank == 0:
@@ -233,6 +270,54 @@ def save_epoch_checkpoint(model, opt, sched, engine, cfg: LoopConfig, epoch: int
         old = os.path.join(cfg.save_dir, f"model_epoch_{epoch - cfg.keep_last}.pth")
         if os.path.exists(old):
             os.remove(old)
+
+
+def _rng_state() -> dict:
+    import random
+    import numpy as np
+    st = {"python": random.getstate(), "numpy": np.random.get_state(), "torch": torch.get_rng_state()}
+    if torch.cuda.is_available():
+        st["cuda"] = torch.cuda.get_rng_state_all()
+    return st
+
+
+def _set_rng_state(st: dict):
+    import random
+    import numpy as np
+    random.setstate(st["python"])
+    np.random.set_state(st["numpy"])
+    torch.set_rng_state(st["torch"])
+    if torch.cuda.is_available() and "cuda" in st:
+        torch.cuda.set_rng_state_all(st["cuda"])
+
+
+def _save_latest(path, model, opt, sched, epoch, step, best, bad, hist):
+    """``latest_checkpoint.pt`` with everything a bit-exact continuation needs (rank 0 writes;
+    every rank has identical replicated state under DDP)."""
+    if D.rank() != 0:
+        return
+    tmp = path + ".tmp"
+    torch.save({"epoch": epoch, "global_step": step, "model_state_dict": model.state_dict(),
+                "optimizer_state_dict": opt.state_dict(),
+                "scheduler_state_dict": sched.state_dict() if sched is not None else None,
+                "best_val_loss": best, "bad_epochs": bad, "history": hist, "rng": _rng_state()}, tmp)
+    os.replace(tmp, path)
+
+
+def _load_latest(path, model, opt, sched, dev) -> dict:
+    # our own file (written by _save_latest): RNG states are Python objects, so full unpickling
+    st = torch.load(path, map_location=dev, weights_only=False)
+    model.load_state_dict(st["model_state_dict"])
+    opt.load_state_dict(st["optimizer_state_dict"])
+    if sched is not None and st["scheduler_state_dict"] is not None:
+        sched.load_state_dict(st["scheduler_state_dict"])
+    rng = st["rng"]
+    if isinstance(rng.get("torch"), torch.Tensor):
+        rng["torch"] = rng["torch"].cpu()
+    if "cuda" in rng:
+        rng["cuda"] = [t.cpu() for t in rng["cuda"]]
+    _set_rng_state(rng)
+    return st
 
 
 class _Null:

@@ -40,6 +40,33 @@ def test_lm_train(tmp_path, capsys, model):
     assert {"epoch", "model_state_dict", "optimizer_state_dict", "vocab_size", "block_size"} <= set(ck)
 
 
+def test_lm_train_val_best_earlystop_resume(tmp_path, capsys, monkeypatch):
+    """C6 (temp/ddp_gpt_bpe_tokenizer_02.py): seeded validation split, best_model.pt, early stopping
+    on validation loss, and resume from latest_checkpoint.pt reproducing the uninterrupted run."""
+    base = ["lm-train", "--model", "gptlike", "--tokenizer", "byte", "--block_size", "32", "--n_layer", "1",
+            "--d_model", "64", "--n_head", "4", "--batch_size", "4", "--val_fraction", "0.2",
+            "--scheduler", "cosine", "--dropout", "0.0"]
+    full = tmp_path / "full"
+    main(base + ["--epochs", "3", "--save_dir", str(full), "--best_model", str(full / "best_model.pt")])
+    ref = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert len(ref["eval_loss"]) == 3 and (full / "best_model.pt").exists()
+    part = tmp_path / "part"
+    per_epoch = ref["global_step"] // 3
+    monkeypatch.setenv("FAULT_INJECT", f"*:{2 * per_epoch + 1}:raise")   # crash in epoch 3
+    from llm_in_practise_amd.utils.faults import InjectedFault
+    with pytest.raises(InjectedFault):
+        main(base + ["--epochs", "3", "--save_dir", str(part)])
+    monkeypatch.delenv("FAULT_INJECT")
+    capsys.readouterr()
+    main(base + ["--epochs", "3", "--save_dir", str(part), "--resume"])
+    res = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert res["train_loss"] == pytest.approx(ref["train_loss"], rel=1e-5)
+    assert res["eval_loss"] == pytest.approx(ref["eval_loss"], rel=1e-5)
+    main(base + ["--epochs", "6", "--lr", "0", "--patience", "1", "--save_dir", str(tmp_path / "es")])
+    es = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert len(es["train_loss"]) == 2      # lr 0: no val improvement after epoch 1 → stop after epoch 2
+
+
 def _port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
