@@ -165,7 +165,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(tps / BASELINE_TOKENS_PER_S, 3) if BASELINE_TOKENS_PER_S else None),
-            "dtype": "bf16",
+            "dtype": "bf16" if device.type == "cuda" else "fp32",
             "data": "synthetic",
             "config": {
                 "model": MODEL_NAMES.get(args.model, args.model),
