@@ -358,8 +358,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16* __restrict__ dO
   }
 }
 
-template <int D>
-__global__ __launch_bounds__(256) void attn_bwd_dkv_k(const bf16* __restrict__ dO, const bf16* __restrict__ Q,
+// HALVES = 2: a 512-thread workgroup, the two 4-wave halves sweep different q-heads of the GQA
+// group over the SAME 64 keys (2 waves per SIMD instead of 1) and meet in LDS at the end.
+template <int D, int HALVES>
+__global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __restrict__ dO, const bf16* __restrict__ Q,
                                                       const bf16* __restrict__ K, const bf16* __restrict__ V,
                                                       const float* __restrict__ lse, const float* __restrict__ delta,
                                                       const int* __restrict__ kv_lens, int ldq, int ldk, int ldv,
@@ -367,13 +369,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_k(const bf16* __restrict__ d
                                                       int hkv, int causal, float scale, float scale_log2) {
   constexpr int LDR = D + 8, CH = D / 8, TILE = 64 * LDR, NS = D / 32, ND = D / 16;
   constexpr int LOADS = 64 * CH / 256;
-  __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // Q0 dO0 Q1 dO1
-  __shared__ __attribute__((aligned(16))) float stat[2][2][64];  // [buf][lse|delta][q]
+  __shared__ __attribute__((aligned(16))) bf16 smem_all[HALVES * 4 * TILE];  // per half: Q0 dO0 Q1 dO1
+  __shared__ __attribute__((aligned(16))) float stat_all[HALVES][2][2][64];  // [half][buf][lse|delta][q]
 
   int kbi, hk, b;  // causal: block 0 (most query tiles) first
   xcd_grid3(kbi, hk, b);
   const int rep = hq / hkv;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  const int tid = threadIdx.x & 255, hw = threadIdx.x >> 8;       // thread within half, half index
+  const int hp = rep / HALVES;                                    // q-heads per half
+  bf16* smem = smem_all + hw * 4 * TILE;
+  float (*stat)[2][64] = stat_all[hw];
+  const int w = tid >> 6, lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   const int kb0 = kbi * 64;
   const int kw = kb0 + 16 * w + li;  // this lane's key (column of the S / dP tiles)
   const int kvlen = kv_lens ? kv_lens[b] : S;
@@ -393,24 +399,24 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_k(const bf16* __restrict__ d
   const int qt0 = causal ? kbi : 0;
   const int qmin = kw < kvlen ? (causal ? kw : 0) : 1 << 30;  // first query that sees this key
   const int nqt = S / 64 - qt0;
-  const int n_it = kb0 < kvlen ? rep * nqt : 0;  // keys past kv_len get zero gradient
+  const int n_it = kb0 < kvlen ? hp * nqt : 0;  // keys past kv_len get zero gradient
 
   bf16x8 qr[LOADS], dr[LOADS];
   float st = 0.f;
   auto load_it = [&](int it) {
-    const int h = hk * rep + it / nqt;
+    const int h = hk * rep + hw * hp + it / nqt;
     const int qa0 = (qt0 + it % nqt) * 64;
 #pragma unroll
     for (int p = 0; p < LOADS; ++p) {
-      const int ci = p * 256 + threadIdx.x;
+      const int ci = p * 256 + tid;
       const int row = ci / CH, ch = ci % CH;
       const size_t tq = tok0 + qa0 + row;
       qr[p] = *reinterpret_cast<const bf16x8*>(Q + tq * ldq + h * D + ch * 8);
       dr[p] = *reinterpret_cast<const bf16x8*>(dO + tq * ldo + h * D + ch * 8);
     }
-    if (threadIdx.x < 128) {
-      const size_t bh = ((size_t)b * hq + h) * S + qa0 + (threadIdx.x & 63);
-      st = threadIdx.x < 64 ? lse[bh] * LOG2E : delta[bh];
+    if (tid < 128) {
+      const size_t bh = ((size_t)b * hq + h) * S + qa0 + (tid & 63);
+      st = tid < 64 ? lse[bh] * LOG2E : delta[bh];
     }
   };
   auto store_it = [&](int buf) {
@@ -418,12 +424,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_k(const bf16* __restrict__ d
     bf16* dOl = Ql + TILE;
 #pragma unroll
     for (int p = 0; p < LOADS; ++p) {
-      const int ci = p * 256 + threadIdx.x;
+      const int ci = p * 256 + tid;
       const int row = ci / CH, ch = ci % CH;
       *reinterpret_cast<bf16x8*>(Ql + row * LDR + ch * 8) = qr[p];
       *reinterpret_cast<bf16x8*>(dOl + row * LDR + ch * 8) = dr[p];
     }
-    if (threadIdx.x < 128) stat[buf][threadIdx.x >> 6][threadIdx.x & 63] = st;
+    if (tid < 128) stat[buf][tid >> 6][tid & 63] = st;
   };
 
   if (n_it > 0) load_it(0);
@@ -478,6 +484,24 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_k(const bf16* __restrict__ d
       }
     }
   }
+  if constexpr (HALVES == 2) {  // half 1 hands its partial sums to half 0 through LDS
+    __syncthreads();
+    f32x4* red = reinterpret_cast<f32x4*>(smem_all);
+    if (hw == 1) {
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) {
+        red[(2 * dt) * 256 + tid] = dk[dt];
+        red[(2 * dt + 1) * 256 + tid] = dv[dt];
+      }
+    }
+    __syncthreads();
+    if (hw == 1) return;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {
+      dk[dt] += red[(2 * dt) * 256 + tid];
+      dv[dt] += red[(2 * dt + 1) * 256 + tid];
+    }
+  }
   // ---- dK (scaled) / dV, summed over the GQA group: lane col key = kw, rows d = 16dt + 4g + r
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt) {
@@ -518,9 +542,14 @@ void launch_attn_bwd(const void* dout, const void* q, const void* k, const void*
   attn_bwd_dq_k<DD><<<gq, blk, 0, st>>>((const bf16*)dout, (const bf16*)o, (const bf16*)q, (const bf16*)k,         \
                                         (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dq, S, hq, hkv,  \
                                         causal, scale, sl2);                                                        \
-  attn_bwd_dkv_k<DD><<<gkv, blk, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k, (const bf16*)v, lse,  \
-                                          delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, (bf16*)dv, S, hq, hkv, causal, \
-                                          scale, sl2)
+  if ((hq / hkv) % 2 == 0)                                                                                       \
+    attn_bwd_dkv_k<DD, 2><<<gkv, 512, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k, (const bf16*)v,   \
+                                               lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, (bf16*)dv, S, hq, hkv, \
+                                               causal, scale, sl2);                                                  \
+  else                                                                                                             \
+    attn_bwd_dkv_k<DD, 1><<<gkv, 256, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k, (const bf16*)v,   \
+                                               lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, (bf16*)dv, S, hq, hkv, \
+                                               causal, scale, sl2)
   if (D == 128) {
     RUN(128);
   } else {

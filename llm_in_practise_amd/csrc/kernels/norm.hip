@@ -22,12 +22,16 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_k(const T* __restrict__ x, co
   if (row >= M) return;
   const T* xr = x + (size_t)row * N;
   float v[CH][8];
+  bf16x8 wb[CH];  // the weight row is loaded with x, before the reduction (no second round trip)
   float ss = 0.f;
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
     const int col = (c * 64 + lane) * 8;
     if (col < N) {
       load8(xr + col, v[c]);
+      if constexpr (sizeof(TW) == 2) {
+        if (w) wb[c] = *reinterpret_cast<const bf16x8*>(w + col);
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i) ss += v[c][i] * v[c][i];
     }
@@ -41,7 +45,14 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_k(const T* __restrict__ x, co
     const int col = (c * 64 + lane) * 8;
     if (col < N) {
       float wv[8];
-      if (w) load8(w + col, wv);
+      if (w) {
+        if constexpr (sizeof(TW) == 2) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) wv[i] = (float)wb[c][i];
+        } else {
+          load8(w + col, wv);
+        }
+      }
       float o[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = v[c][i] * r * (w ? wv[i] : 1.f);
@@ -60,6 +71,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_k(const T* __restrict__ dy, c
   const int row = blockIdx.x * ROWS + wid;
   const bool valid = row < M;
   float xv[CH][8], gv[CH][8];
+  T rb[CH][8];  // residual-branch gradient, fetched with x / dy (one round trip per row)
   float dot = 0.f;
   const float r = valid ? rstd[row] : 0.f;
 #pragma unroll
@@ -68,6 +80,13 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_k(const T* __restrict__ dy, c
     if (valid && col < N) {
       load8(x + (size_t)row * N + col, xv[c]);
       load8(dy + (size_t)row * N + col, gv[c]);
+      if (dres) {
+        if constexpr (sizeof(T) == 2)
+          *reinterpret_cast<bf16x8*>(rb[c]) = *reinterpret_cast<const bf16x8*>(dres + (size_t)row * N + col);
+        else
+#pragma unroll
+          for (int i = 0; i < 8; ++i) rb[c][i] = dres[(size_t)row * N + col + i];
+      }
       float wv[8];
       if (w) load8(w + col, wv);
 #pragma unroll
@@ -92,10 +111,8 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_k(const T* __restrict__ dy, c
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = r * (gv[c][i] * (w ? wv[i] : 1.f) - xv[c][i] * dot);
       if (dres) {  // the residual branch's gradient (x feeds both the norm and the skip connection)
-        float rv[8];
-        load8(dres + (size_t)row * N + col, rv);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] += rv[i];
+        for (int i = 0; i < 8; ++i) o[i] += (float)rb[c][i];
       }
       store8(dx + (size_t)row * N + col, o);
     }
