@@ -83,6 +83,10 @@ def main():
     ap.add_argument("--grad-ckpt", action="store_true",
                     help="recompute each decoder layer in backward (the reference's 24 GB-GPU setting; "
                          "off by default: 288 GB HBM holds every activation)")
+    ap.add_argument("--strategy", default="ddp", choices=["ddp", "zero3"],
+                    help="ddp: flat-buffer DDP over RCCL (qwen3-8b-qlora-dist.py); zero3: the ZeRO-3 engine with "
+                         "ds_zero3_config.json semantics (qwen3-14b-qlora-dist-deepspeed.py, BASELINE config #4)")
+    ap.add_argument("--ds-config", dest="ds_config", default=None)
     ap.add_argument("--ga-fusion", type=int, default=1,
                     help="1: execute the grad-accum micro-batches in one pass (per-micro-batch loss "
                          "normalisation, identical gradient); 0: sequential micro-steps")
@@ -91,11 +95,26 @@ def main():
     rank, local_rank, world = D.init_distributed()
     device = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
     cfg, model = build(args, device)
-    opt = build_optimizer(args.optim, [p for p in model.parameters() if p.requires_grad], args.lr,
-                          weight_decay=0.0, max_grad_norm=1.0)
     total_steps = args.warmup + args.steps
-    sched = LRScheduler(opt, "linear", args.lr, total_steps)
-    ddp = DistributedDataParallel(model, grad_buffer=opt.grad_buffer)
+    engine = None
+    if args.strategy == "zero3":
+        from llm_in_practise_amd.parallel.zero import ZeroEngine
+        path = args.ds_config or os.path.join(os.path.dirname(os.path.abspath(__file__)), "configs",
+                                              "ds_zero3_config.json")
+        with open(path) as f:
+            ds = json.load(f)
+        if args.ga_fusion:   # the GA micro-batches run as ONE pass: the engine sees one micro-step
+            ds["gradient_accumulation_steps"] = 1
+            ds["train_micro_batch_size_per_gpu"] = args.micro_batch * args.grad_accum
+            ds["train_batch_size"] = args.micro_batch * args.grad_accum * world
+        engine = ZeroEngine(model, ds, lr=args.lr, weight_decay=0.0, hidden_size=cfg.hidden_size,
+                            total_steps=total_steps)
+        opt = sched = ddp = None
+    else:
+        opt = build_optimizer(args.optim, [p for p in model.parameters() if p.requires_grad], args.lr,
+                              weight_decay=0.0, max_grad_norm=1.0)
+        sched = LRScheduler(opt, "linear", args.lr, total_steps)
+        ddp = DistributedDataParallel(model, grad_buffer=opt.grad_buffer)
 
     gen = torch.Generator(device=device).manual_seed(1000 + rank)
     n_batches = 8
@@ -104,6 +123,13 @@ def main():
     it = [0]
 
     def step():
+        if engine is not None:      # ZeRO-3: reduce-scatter / optimizer partition / clip inside step()
+            ids = torch.cat([data[(it[0] + g) % n_batches] for g in range(args.grad_accum)])
+            it[0] += args.grad_accum
+            out = engine.module(ids, labels=ids, num_micro_batches=args.grad_accum if args.ga_fusion else 1)
+            engine.backward(out.loss)
+            engine.step()
+            return out.loss
         if args.ga_fusion:
             # the GA micro-batches are independent given the (frozen-during-the-step) weights:
             # run them as one pass with per-micro-batch loss normalisation (same gradient)
@@ -155,7 +181,8 @@ def main():
         f"~{tps * fl_per_tok / world / 1e12:.0f} TFLOP/s/GPU (matmul)  peak HBM {mem:.1f} GiB")
     if D.is_main():
         rec = {
-            "metric": "tokens/sec (whole node) Qwen3-8B QLoRA fine-tune at 1/2/4/8 MI355X",
+            "metric": f"tokens/sec (whole node) {MODEL_NAMES.get(args.model, args.model)} "
+                      f"{'QLoRA' if args.mode == 'qlora' else 'LoRA'} fine-tune at 1/2/4/8 MI355X",
             "value": round(tps, 1),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -171,12 +198,12 @@ def main():
                 "model": MODEL_NAMES.get(args.model, args.model),
                 "global_batch": args.micro_batch * args.grad_accum * world,
                 "seq_len": args.seq_len,
-                "parallelism": f"dp{world}",
+                "parallelism": f"dp{world}" if engine is None else f"zero3-dp{world}",
                 "micro_batch": args.micro_batch,
                 "grad_accum": args.grad_accum,
                 "quant": "nf4+double_quant" if args.mode == "qlora" else "none",
                 "lora": f"r{args.lora_r}/a{args.lora_alpha}/drop{args.lora_dropout}/{args.targets}",
-                "optimizer": args.optim,
+                "optimizer": args.optim if engine is None else "zero3-adamw",
                 "gradient_checkpointing": bool(args.grad_ckpt),
                 "ga_execution": "fused-pass" if args.ga_fusion else "sequential",
                 "weights": "random-init",
