@@ -143,6 +143,9 @@ class _Slot:
     req: _Request
     gen: list = dataclasses.field(default_factory=list)
     sent: int = 0
+    text: str = ""                       # streamed/stop-checked text so far (incremental detokenisation)
+    poff: int = 0                        # gen[poff:roff] = context tokens of the last emitted piece
+    roff: int = 0
     t_first: float | None = None
     done: bool = False
     finish: str = "length"
@@ -185,7 +188,7 @@ def _unwrap_lm(model):
 class ServingEngine:
     def __init__(self, model, tokenizer, model_name: str = "lipa-model", max_batch: int = 16,
                  system_prompt: str | None = None, chat_template: str = "auto", space_before_end: bool = False,
-                 max_model_len: int | None = None, max_prefill_batch: int = 16, prefill_token_budget: int = 8192,
+                 max_model_len: int | None = None, max_prefill_batch: int = 32, prefill_token_budget: int = 16384,
                  use_graphs: bool | None = None, tp_group=None, prefix_cache_blocks: int = 0,
                  prefix_block: int = 64):
         """``tp_group``: the model was sharded by ``parallel.tensor_parallel`` over this group.
@@ -251,6 +254,8 @@ class ServingEngine:
             with torch.no_grad():
                 self.graphs = DecodeGraphs(self.lm, self.cache, max_batch, tokens=self.next_tok)
         self._held: _Request | None = None
+        self._pending = None                     # (pinned host tokens, event, owners) of the in-flight step
+        self.pipeline = self.device.type == "cuda"
         self._stop = False
         self._worker = None
         if self.tp_rank == 0:
@@ -313,6 +318,7 @@ class ServingEngine:
             try:
                 self._iteration()
             except Exception as e:  # fail the in-flight requests, keep serving
+                self._pending = None
                 for i, s in enumerate(self.slots):
                     if s is not None:
                         s.req.out.put(("error", repr(e)))
@@ -331,6 +337,8 @@ class ServingEngine:
                 self._admit(new)
             if any(s is not None for s in self.slots):
                 self._decode_step()
+            else:
+                self._pending = None             # only finished requests' extra tokens were in flight
 
     def _tp_sync(self, new):
         """Broadcast this iteration's admissions (slot, prompt ids, sampling params) from TP rank 0."""
@@ -446,6 +454,10 @@ class ServingEngine:
     def _sample(self, logits, slot_ids):
         """Sample one token per row, grouping rows with identical sampling parameters.
         Returns (device tensor, host list)."""
+        out = self._sample_dev(logits, slot_ids)
+        return out, out.tolist()
+
+    def _sample_dev(self, logits, slot_ids):
         out = torch.empty(len(slot_ids), dtype=torch.long, device=self.device)
         groups: dict = {}
         for j, s in enumerate(slot_ids):
@@ -465,7 +477,7 @@ class ServingEngine:
                 out = sample(logits.float(), hist, temp, top_k, top_p, pen)
             else:
                 out[idx] = sample(logits[idx].float(), hist, temp, top_k, top_p, pen)
-        return out, out.tolist()
+        return out
 
     def _accept(self, slot: int, tok: int, now: float):
         s = self.slots[slot]
@@ -478,15 +490,22 @@ class ServingEngine:
             s.gen.append(tok)
             if len(s.gen) >= p.max_tokens or len(s.req.prompt_ids) + len(s.gen) >= self.max_len - 1:
                 s.done, s.finish = True, "length"
-            if s.req.stream:
-                text = self.tok.decode(s.gen, skip_special_tokens=True)
-                if len(text) > s.sent and not text.endswith("�"):
-                    s.req.out.put(("delta", text[s.sent:]))
-                    s.sent = len(text)
-            if p.stop:
-                text = self.tok.decode(s.gen, skip_special_tokens=True)
-                if any(st and st in text for st in p.stop):
-                    s.done, s.finish = True, "stop"
+            if s.req.stream or p.stop:
+                # incremental detokenisation: decode only the few tokens since the last emitted
+                # piece (plus their left context), not the whole generation every step
+                prev = self.tok.decode(s.gen[s.poff:s.roff], skip_special_tokens=True)
+                cur = self.tok.decode(s.gen[s.poff:], skip_special_tokens=True)
+                if len(cur) > len(prev) and not cur.endswith("\ufffd"):
+                    new = cur[len(prev):]
+                    s.poff, s.roff = s.roff, len(s.gen)
+                    s.text += new
+                    if s.req.stream:
+                        s.req.out.put(("delta", new))
+                        s.sent = len(s.text)
+                    if p.stop:
+                        tail = s.text[-(len(new) + max(len(st) for st in p.stop)):]
+                        if any(st and st in tail for st in p.stop):
+                            s.done, s.finish = True, "stop"
         if s.done:
             self._finish(slot)
 
@@ -527,13 +546,43 @@ class ServingEngine:
         rows = torch.tensor(active, device=self.device)
         if len(active) != n:
             logits = logits[rows]
-        dev_toks, toks = self._sample(logits, active)
-        self.next_tok[rows] = dev_toks
-        now = time.time()
-        for j, slot in enumerate(active):
-            self._accept(slot, toks[j], now)
+        if self.pipeline and all(self.slots[s].req.params.repetition_penalty == 1.0 for s in active):
+            # asynchronous: the sampled tokens stay on the device (next step's input), a pinned
+            # copy + event hand them to the host, and the host accepts the PREVIOUS step's
+            # tokens while this step runs on the GPU (a finished request decodes one extra,
+            # discarded token)
+            dev_toks = self._sample_dev(logits, active)
+            self.next_tok[rows] = dev_toks
+            host = torch.empty(len(active), dtype=torch.long, pin_memory=True)
+            host.copy_(dev_toks, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            prev, self._pending = self._pending, (host, ev, [(sl, self.slots[sl].req) for sl in active])
+            if prev is not None:
+                self._process_pending(prev)
+        else:
+            self._flush_pending()
+            dev_toks, toks = self._sample(logits, active)
+            self.next_tok[rows] = dev_toks
+            now = time.time()
+            for j, slot in enumerate(active):
+                self._accept(slot, toks[j], now)
         self.stats["decode_steps_total"] += 1
         self.stats["running"] = sum(s is not None for s in self.slots)
+
+    def _process_pending(self, pend):
+        host, ev, owners = pend
+        ev.synchronize()
+        now = time.time()
+        for (slot, req), tok in zip(owners, host.tolist()):
+            s = self.slots[slot]
+            if s is not None and s.req is req and not s.done:
+                self._accept(slot, tok, now)
+
+    def _flush_pending(self):
+        if self._pending is not None:
+            p, self._pending = self._pending, None
+            self._process_pending(p)
 
     # ------------------------------------------------------------------ metrics
     def prometheus(self) -> str:

@@ -84,7 +84,10 @@ async def one_request(client, url, model, msgs, max_tokens):
 async def run_level(url, model, prompts, conc, max_tokens):
     import httpx
     sem = asyncio.Semaphore(conc)
-    async with httpx.AsyncClient() as client:
+    # no client-side cap: httpx defaults to 100 pooled connections, which would silently limit
+    # concurrency 128 / 256 and show up as TTFT
+    limits = httpx.Limits(max_connections=None, max_keepalive_connections=None)
+    async with httpx.AsyncClient(limits=limits) as client:
         async def task(m):
             async with sem:
                 return await one_request(client, url, model, m, max_tokens)
@@ -114,7 +117,7 @@ class _SyntheticTokenizer:
         return "".join(chr(0x4E00 + int(i) % 20000) for i in ids)
 
 
-def start_inprocess(spec: str, port: int, max_batch: int = 64):
+def start_inprocess(spec: str, port: int, max_batch: int = 64, max_model_len: int | None = None):
     """Launch our server in a background thread with a random-init model (synthetic tokenizer)."""
     import threading
 
@@ -124,7 +127,8 @@ def start_inprocess(spec: str, port: int, max_batch: int = 64):
     from llm_in_practise_amd.infer.engine import ServingEngine
     from llm_in_practise_amd.infer.server import create_app
     m = _load_for_inference(spec)
-    eng = ServingEngine(m, _SyntheticTokenizer(), model_name=spec, max_batch=max_batch, chat_template="chatml")
+    eng = ServingEngine(m, _SyntheticTokenizer(), model_name=spec, max_batch=max_batch, chat_template="chatml",
+                        max_model_len=max_model_len)
     cfg = uvicorn.Config(create_app(eng), host="127.0.0.1", port=port, log_level="warning")
     th = threading.Thread(target=uvicorn.Server(cfg).run, daemon=True)
     th.start()
@@ -144,14 +148,49 @@ def main():
     ap.add_argument("--concurrency", type=int, nargs="+", default=[8])
     ap.add_argument("--out", default=None)
     ap.add_argument("--max-batch", type=int, default=64)
+    ap.add_argument("--max-model-len", type=int, default=None)
+    ap.add_argument("--spawn", action="store_true",
+                    help="with --inprocess: run the server in a child process (client and server do not share a GIL)")
+    ap.add_argument("--serve-only", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args()
-    url = a.url or start_inprocess(a.inprocess, a.port, a.max_batch)
-    prompts = mixed_dataset(a.num_prompts) if a.dataset == "mixed" else sharegpt(a.dataset, a.num_prompts)
+    if a.serve_only:                      # child of --spawn
+        start_inprocess(a.inprocess, a.port, a.max_batch, a.max_model_len)
+        while True:
+            time.sleep(3600)
+    child = None
+    if a.inprocess and a.spawn:
+        import subprocess
+        import urllib.request
+        cmd = [sys.executable, os.path.abspath(__file__), "--serve-only", "--inprocess", a.inprocess, "--port",
+               str(a.port), "--max-batch", str(a.max_batch)]
+        if a.max_model_len:
+            cmd += ["--max-model-len", str(a.max_model_len)]
+        child = subprocess.Popen(cmd)
+        url = f"http://127.0.0.1:{a.port}"
+        for _ in range(600):
+            try:
+                urllib.request.urlopen(url + "/health", timeout=2)
+                break
+            except Exception:
+                if child.poll() is not None:
+                    raise RuntimeError("server process exited")
+                time.sleep(1)
+    else:
+        url = a.url or start_inprocess(a.inprocess, a.port, a.max_batch, a.max_model_len)
+    if a.dataset == "mixed":
+        prompts = mixed_dataset(a.num_prompts)
+    elif a.dataset == "short":       # ShareGPT-like chat turns only (the reference table's workload shape)
+        prompts = [p for p in mixed_dataset(4 * a.num_prompts) if len(p) == 1][:a.num_prompts]
+    else:
+        prompts = sharegpt(a.dataset, a.num_prompts)
     rows = [asyncio.run(run_level(url, a.model, prompts, c, a.max_tokens)) for c in a.concurrency]
     for r in rows:
         print(json.dumps(r))
     if a.out:
         json.dump(rows, open(a.out, "w"), indent=2)
+    if child is not None:
+        child.terminate()
+        child.wait(timeout=60)
 
 
 if __name__ == "__main__":

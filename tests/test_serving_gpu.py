@@ -76,3 +76,44 @@ def test_prefix_cache_hit_matches_full_prefill(lm):
     finally:
         cold.shutdown()
         warm.shutdown()
+
+
+def _drain(reqs):
+    outs = []
+    for r in reqs:
+        deltas = []
+        while True:
+            kind, val = r.out.get(timeout=120)
+            assert kind != "error", val
+            if kind == "delta":
+                deltas.append(val)
+            else:
+                outs.append((val["text"], "".join(deltas), val["completion_tokens"], val["finish_reason"]))
+                break
+    return outs
+
+
+def test_pipelined_decode_matches_synchronous(lm):
+    """Asynchronous decode (host accepts step t-1 while step t runs) must produce exactly the
+    synchronous engine's tokens, finish reasons and stream deltas — including requests that stop
+    on EOS / a stop string mid-batch (their in-flight extra token is discarded)."""
+    tok = ByteTokenizer()
+    tok.eos_token_id = ord("e")
+    prompts = ["hello there %d " % i * (1 + i % 3) for i in range(12)]
+    params = [SamplingParams(max_tokens=6 + 5 * (i % 4), temperature=0.0, ignore_eos=(i % 2 == 0),
+                             stop=["th"] if i % 5 == 0 else None) for i in range(12)]
+    pa = ServingEngine(lm, tok, max_batch=8, use_graphs=True)
+    sy = ServingEngine(lm, tok, max_batch=8, use_graphs=True)
+    sy.pipeline = False
+    try:
+        assert pa.pipeline
+        a = _drain([pa.submit(p, q, stream=True) for p, q in zip(prompts, params)])
+        b = _drain([sy.submit(p, q, stream=True) for p, q in zip(prompts, params)])
+        assert [x[0] for x in a] == [x[0] for x in b]
+        assert [x[2:] for x in a] == [x[2:] for x in b]
+        for text, streamed, _, fin in a:
+            assert streamed.startswith(text) or fin == "stop"
+        assert all(s is None for s in pa.slots)
+    finally:
+        pa.shutdown()
+        sy.shutdown()
