@@ -517,6 +517,8 @@ class ServingEngine:
             cut = min((text.find(st) for st in r.params.stop if st and st in text), default=-1)
             if cut >= 0:
                 text = text[:cut]
+        if r.stream and len(text) > len(s.text) and text.startswith(s.text):
+            r.out.put(("delta", text[len(s.text):]))       # flush a held-back partial character
         t1 = time.time()
         self.stats["requests_total"] += 1
         self.stats["generation_tokens_total"] += len(s.gen)
