@@ -241,25 +241,36 @@ def cmd_finetune(a):
 
 
 # ============================================================================ inference / quant
-def _tp_group():
-    """torchrun with WORLD_SIZE > 1 on an inference command = tensor parallel over all ranks
-    (the vLLM ``--tensor-parallel-size`` role)."""
+def _parallel(a=None):
+    """torchrun with WORLD_SIZE > 1 on an inference command: ``world = tp × pp`` ranks
+    (vLLM ``--tensor-parallel-size`` / ``--pipeline-parallel-size``; default
+    all tensor parallel).  Returns ``(spmd_group, tp_group, pp_group)`` — every rank of the
+    world replays the same engine iterations."""
     if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
-        return None
+        return None, None, None
     from ..parallel import dist as D
     D.init_distributed()
     import torch.distributed as dist
-    return dist.group.WORLD
+    from ..parallel.pipeline_parallel import make_tp_pp_groups
+    world = dist.get_world_size()
+    pp = int(getattr(a, "pp", None) or 1)
+    tp = int(getattr(a, "tp", None) or world // pp)
+    tp_group, pp_group = make_tp_pp_groups(tp, pp)
+    return dist.group.WORLD, tp_group, pp_group
 
 
-def _load_for_inference(path, adapter=None, device=None, quant=None, fuse=True, tp_group=None):
+def _load_for_inference(path, adapter=None, device=None, quant=None, fuse=True, tp_group=None, pp_group=None):
     from ..models.qwen3 import BitsAndBytesConfig, Qwen3ForCausalLM, qwen3_config
     dev = device or _device()
-    if tp_group is not None:      # shard the bf16 weights (+ adapter), THEN quantise the shards
+    if tp_group is not None or pp_group is not None:   # shard the bf16 weights (+ adapter), THEN quantise
+        from ..parallel.pipeline_parallel import apply_pipeline_parallel
         from ..parallel.tensor_parallel import apply_tensor_parallel
         from ..peft.lora import quantize_model_nf4
         m = _load_for_inference(path, adapter, dev, None, fuse=False)
-        apply_tensor_parallel(m, tp_group)
+        if pp_group is not None:
+            apply_pipeline_parallel(m, pp_group)
+        if tp_group is not None:
+            apply_tensor_parallel(m, tp_group)
         if quant == "nf4":
             quantize_model_nf4(m)
         lm = m
@@ -289,6 +300,13 @@ def _load_for_inference(path, adapter=None, device=None, quant=None, fuse=True, 
     if fuse and hasattr(lm, "fuse_projections"):
         lm.fuse_projections()          # q|k|v and gate|up as single GEMMs (frozen weights)
     return m.eval()
+
+
+def _add_parallel_args(p):
+    p.add_argument("--tensor-parallel-size", "-tp", dest="tp", type=int, default=None,
+                   help="under torchrun: TP degree (default WORLD_SIZE / pp)")
+    p.add_argument("--pipeline-parallel-size", "-pp", dest="pp", type=int, default=1,
+                   help="under torchrun: pipeline stages (layers split across ranks)")
 
 
 def cmd_chat(a):
@@ -323,8 +341,8 @@ def cmd_chat(a):
 def cmd_infer(a):
     from ..infer.generate import generate
     from ..train.data import load_tokenizer, render_chatml
-    tp = _tp_group()                 # torchrun → tensor parallel; every rank decodes in lockstep
-    m = _load_for_inference(a.model, a.adapter, quant=a.quant, tp_group=tp)
+    tp, tpg, ppg = _parallel(a)      # torchrun → TP / PP; every rank decodes in lockstep
+    m = _load_for_inference(a.model, a.adapter, quant=a.quant, tp_group=tpg, pp_group=ppg)
     tok = load_tokenizer(a.tokenizer or a.model)
     text = render_chatml([{"role": "user", "content": a.prompt}], add_generation_prompt=True) if a.chat else a.prompt
     ids = torch.tensor([tok.encode(text, add_special_tokens=False)], device=_device())
@@ -403,8 +421,8 @@ def cmd_serve(a):
     from ..infer.engine import ServingEngine
     from ..infer.server import serve
     from ..train.data import load_tokenizer
-    tp = _tp_group()
-    m = _load_for_inference(a.model, a.adapter, quant=a.quant, tp_group=tp)
+    tp, tpg, ppg = _parallel(a)
+    m = _load_for_inference(a.model, a.adapter, quant=a.quant, tp_group=tpg, pp_group=ppg)
     tok = load_tokenizer(a.tokenizer or a.model)
     moderation = None
     if a.guard_url:
@@ -415,7 +433,7 @@ def cmd_serve(a):
                         max_model_len=a.max_model_len,
                         prefix_cache_blocks=a.prefix_blocks if a.prefix_caching else 0)
     if tp is not None and eng.tp_rank != 0:
-        eng.follower_loop()              # TP followers replay rank 0's iterations
+        eng.follower_loop()              # TP / PP followers replay rank 0's iterations
         return
     serve(eng, a.host, a.port, api_key=a.api_key, moderation=moderation)
 
@@ -651,6 +669,7 @@ def build_parser() -> argparse.ArgumentParser:
             p.add_argument("--prompt", required=True)
             p.add_argument("--chat", action="store_true")
             p.add_argument("--repetition_penalty", type=float, default=1.0)
+            _add_parallel_args(p)
         p.set_defaults(fn=fn)
 
     p = sub.add_parser("merge")
@@ -701,6 +720,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--prefix-cache-blocks", dest="prefix_blocks", type=int, default=1024,
                    help="HBM pool size in 64-token chunks")
     p.add_argument("--max-model-len", dest="max_model_len", type=int, default=None)
+    _add_parallel_args(p)
     p.set_defaults(fn=cmd_serve)
 
     p = sub.add_parser("guard")

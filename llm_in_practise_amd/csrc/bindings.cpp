@@ -67,6 +67,9 @@ void launch_lora_acc(const float*, int, int, const void*, int, void*, int, const
 void launch_decode_attention(const void*, const void*, const void*, const int*, float*, float*, float*, void*, int, int,
                              int, int, int, int, float, hipStream_t);
 int decode_split_plan(int, int, int);
+int decode_split_plan2(int, int, int);
+void launch_decode_attention2(const void*, int, const void*, int, const void*, int, void*, void*, const int64_t*, float*,
+                              float*, float*, void*, int, int, int, int, int, int, float, hipStream_t);
 void launch_sample(int, const void*, const int*, int, float*, int64_t*, int, int, float, int, float, float, uint64_t,
                    hipStream_t);
 void launch_dropout_fwd(const void*, void*, size_t, uint64_t, float, hipStream_t);
@@ -583,6 +586,37 @@ Tensor decode_attention(Tensor q, Tensor kc, Tensor vc, Tensor lens, int64_t hq,
   return out;
 }
 
+// q [B, hq*d], knew/vnew [B, hkv*d] (row-strided views allowed), caches [B, Smax, hkv*d], pos [B] int64:
+// appends knew/vnew at pos and attends over pos + 1 keys (MFMA split-K kernel)
+Tensor decode_attention_append(Tensor q, Tensor knew, Tensor vnew, Tensor kc, Tensor vc, Tensor pos, int64_t hq,
+                               int64_t hkv, int64_t d, int64_t max_len, double scale) {
+  CHECK_CUDA(q);
+  for (const Tensor* t : {&q, &knew, &vnew, &kc, &vc}) CHECK_BF16((*t));
+  CHECK_CONTIG(kc);
+  CHECK_CONTIG(vc);
+  TORCH_CHECK(pos.scalar_type() == at::kLong && pos.is_contiguous(), "pos: int64");
+  TORCH_CHECK(d == 64 || d == 128, "decode_attention_append: head_dim 64 or 128");
+  TORCH_CHECK(hq % hkv == 0 && hq / hkv <= 16, "decode_attention_append: group size <= 16");
+  const int64_t B = q.size(0), Smax = kc.size(1);
+  for (const Tensor* t : {&q, &knew, &vnew})
+    TORCH_CHECK(t->dim() == 2 && t->size(0) == B && t->stride(1) == 1 && t->stride(0) % 8 == 0,
+                "decode_attention_append: 2-D row-strided q/k/v with 16-B aligned rows");
+  TORCH_CHECK(q.size(1) == hq * d && knew.size(1) == hkv * d && vnew.size(1) == hkv * d, "decode_attention_append: q/k/v width");
+  TORCH_CHECK(kc.size(0) == B && kc.size(2) == hkv * d && vc.sizes() == kc.sizes() && pos.numel() == B,
+              "decode_attention_append: cache shape");
+  TORCH_CHECK(max_len <= Smax, "decode_attention_append: max_len > cache");
+  const int nsplit = decode_split_plan2(B, hkv, max_len);
+  auto f32 = q.options().dtype(at::kFloat);
+  Tensor opart = at::empty({B * hq * nsplit, d}, f32);
+  Tensor mpart = at::empty({B * hq * nsplit}, f32), lpart = at::empty({B * hq * nsplit}, f32);
+  Tensor out = at::empty({B, hq * d}, q.options());
+  launch_decode_attention2(q.data_ptr(), q.stride(0), knew.data_ptr(), knew.stride(0), vnew.data_ptr(), vnew.stride(0),
+                           kc.data_ptr(), vc.data_ptr(), pos.data_ptr<int64_t>(), opart.data_ptr<float>(),
+                           mpart.data_ptr<float>(), lpart.data_ptr<float>(), out.data_ptr(), B, Smax, hq, hkv, d, nsplit,
+                           (float)scale, stream());
+  return out;
+}
+
 // logits [B, V] fp32|bf16; hist [B, L] int32 (-1 = pad) or None; temperature <= 0 → greedy
 Tensor sample(Tensor logits, optional<Tensor> hist, double temperature, int64_t top_k, double top_p, double penalty,
               int64_t key) {
@@ -704,6 +738,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_norm", &grad_norm);
   m.def("set_gemm_impl", &set_gemm_impl);
   m.def("decode_attention", &decode_attention);
+  m.def("decode_attention_append", &decode_attention_append);
   m.def("lora_proj", &lora_proj);
   m.def("lora_acc", &lora_acc);
   m.def("gemm_int4", &gemm_int4);

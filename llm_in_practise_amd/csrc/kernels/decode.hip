@@ -179,6 +179,199 @@ __global__ __launch_bounds__(D) void decode_attn_merge_k(const float* __restrict
   out[h * D + d] = (bf16)(L > 0.f ? A / L : 0.f);
 }
 
+
+// ------------------------------------------------------------- decode attention v2 (MFMA)
+// Same split-K scheme, but the math runs on the matrix cores and the KV append is fused:
+//  * a wave owns 32-key tiles of its split (tiles w, w+4, ... of the workgroup's range); the
+//    G = Hq/Hkv query heads of the kv head are the 16 MFMA columns (lane li = head), scores
+//    are computed swapped, Sᵀ = K·Qᵀ (K fragments straight from HBM, 16 B per lane), so the
+//    online softmax is lane-local plus two shuffles and P is already Oᵀ = Vᵀ·Pᵀ's B operand;
+//    V goes through a wave-private LDS tile and the gfx950 transposed read ds_read_b64_tr_b16;
+//  * the new token's K/V rows are read from the projection output (not the cache), and the
+//    split holding the last key writes them into the cache at pos — no separate scatter
+//    kernel, no read-after-write hazard (no workgroup reads cache[pos] in this launch);
+//  * lengths come from pos (int64, len = pos + 1) — no host-side lens tensor.
+__device__ __forceinline__ bf16x4 dec_tr_read(const bf16* p) {
+  typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(p));
+}
+__device__ __forceinline__ int split_chunk32(int len, int nsplit) { return ((len + nsplit - 1) / nsplit + 31) & ~31; }
+
+template <int D>
+__global__ __launch_bounds__(256) void decode_attn_mfma_k(const bf16* __restrict__ q, int ldq,
+                                                          const bf16* __restrict__ knew, int ldkn,
+                                                          const bf16* __restrict__ vnew, int ldvn,
+                                                          bf16* __restrict__ kc, bf16* __restrict__ vc,
+                                                          const int64_t* __restrict__ pos, float* __restrict__ opart,
+                                                          float* __restrict__ mpart, float* __restrict__ lpart,
+                                                          int Smax, int hq, int hkv, int nsplit, float scale_log2) {
+  constexpr int LDR = D + 8;          // padded LDS row (elements)
+  constexpr int CH = D / 8;           // 16-B chunks per row
+  constexpr int NS = D / 32;          // k-steps over the head dim
+  constexpr int ND = D / 16;          // d-subtiles of O
+  constexpr int VL = 32 * CH / 64;    // V chunks per lane per 32-key tile
+  constexpr int VT = 32 * LDR;        // elements of one wave's V tile
+  __shared__ __attribute__((aligned(16))) char smem[4 * VT * 2];
+  __shared__ float sm[4][16], sl[4][16];
+  static_assert(4 * 16 * D * 4 <= 4 * VT * 2, "merge buffer aliases the V tiles");
+
+  const int split = blockIdx.x, kh = blockIdx.y, b = blockIdx.z;
+  const int G = hq / hkv;
+  const int len = (int)pos[b] + 1;
+  const int chunk = split_chunk32(len, nsplit);
+  const int k0 = split * chunk, k1 = min(k0 + chunk, len);
+  if (k0 >= len) return;              // whole workgroup: empty split, never merged
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+
+  const size_t rs = (size_t)hkv * D;
+  bf16* kcb = kc + (size_t)b * Smax * rs + kh * D;
+  bf16* vcb = vc + (size_t)b * Smax * rs + kh * D;
+  const bf16* knb = knew + (size_t)b * ldkn + kh * D;
+  const bf16* vnb = vnew + (size_t)b * ldvn + kh * D;
+  if (k1 == len && w == 0 && lane < 2 * CH) {      // append the new token's K/V rows
+    const int c = lane % CH;
+    if (lane < CH)
+      *reinterpret_cast<bf16x8*>(kcb + (size_t)(len - 1) * rs + 8 * c) = *reinterpret_cast<const bf16x8*>(knb + 8 * c);
+    else
+      *reinterpret_cast<bf16x8*>(vcb + (size_t)(len - 1) * rs + 8 * c) = *reinterpret_cast<const bf16x8*>(vnb + 8 * c);
+  }
+
+  bf16x8 qf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (li < G) qf[s] = *reinterpret_cast<const bf16x8*>(q + (size_t)b * ldq + (kh * G + li) * D + 32 * s + 8 * g);
+    else qf[s] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  f32x4 acc[ND];
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  bf16* vl = reinterpret_cast<bf16*>(smem) + w * VT;
+
+  for (int t = k0 + 32 * w; t < k1; t += 128) {
+    bf16x8 kr[2][NS], vr[VL];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const int key = min(t + 16 * kt + li, k1 - 1);
+      const bf16* kp = key == len - 1 ? knb : kcb + (size_t)key * rs;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) kr[kt][s] = *reinterpret_cast<const bf16x8*>(kp + 32 * s + 8 * g);
+    }
+#pragma unroll
+    for (int p = 0; p < VL; ++p) {
+      const int ci = p * 64 + lane, row = ci / CH, ch = ci % CH;
+      const int key = min(t + row, k1 - 1);
+      const bf16* vp = key == len - 1 ? vnb : vcb + (size_t)key * rs;
+      vr[p] = *reinterpret_cast<const bf16x8*>(vp + 8 * ch);
+    }
+    f32x4 sc[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      sc[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NS; ++s) sc[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr[kt][s], qf[s], sc[kt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int p = 0; p < VL; ++p) {
+      const int ci = p * 64 + lane, row = ci / CH, ch = ci % CH;
+      *reinterpret_cast<bf16x8*>(vl + row * LDR + 8 * ch) = vr[p];
+    }
+    // lane owns head li; keys t + 16kt + 4g + r
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = (t + 16 * kt + 4 * g + r < k1) ? sc[kt][r] * scale_log2 : -INFINITY;
+        sc[kt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m_run, mx);            // finite: every tile has >= 1 valid key
+    const float alpha = __builtin_amdgcn_exp2f(m_run - mn);
+    float rsum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pr = __builtin_amdgcn_exp2f(sc[kt][r] - mn);
+        sc[kt][r] = pr;
+        rsum += pr;
+      }
+    rsum += __shfl_xor(rsum, 16, 64);
+    rsum += __shfl_xor(rsum, 32, 64);
+    l_run = l_run * alpha + rsum;
+    m_run = mn;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) acc[dt] *= alpha;
+    const bf16x8 pf = bf16x8{(bf16)sc[0][0], (bf16)sc[0][1], (bf16)sc[0][2], (bf16)sc[0][3],
+                             (bf16)sc[1][0], (bf16)sc[1][1], (bf16)sc[1][2], (bf16)sc[1][3]};
+    __builtin_amdgcn_s_waitcnt(0xc07f);          // lgkmcnt(0): this wave's V tile is in LDS
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {
+      const bf16* p0 = vl + (4 * g + (li >> 2)) * LDR + 16 * dt + 4 * (li & 3);
+      const bf16x4 a = dec_tr_read(p0), c = dec_tr_read(p0 + 16 * LDR);
+      const bf16x8 vf = bf16x8{a[0], a[1], a[2], a[3], c[0], c[1], c[2], c[3]};
+      acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, acc[dt], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);          // transposed reads done before the tile is rewritten
+    __builtin_amdgcn_wave_barrier();
+  }
+  // ---- merge the 4 waves (Oᵀ[16dt + 4g + r][li]) through LDS, natural-log m for the merge kernel
+  __syncthreads();
+  float* sacc = reinterpret_cast<float*>(smem);   // [4][16][D], aliases the V tiles
+  if (g == 0) {
+    sm[w][li] = m_run;
+    sl[w][li] = l_run;
+  }
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sacc[(w * 16 + li) * D + 16 * dt + 4 * g + r] = acc[dt][r];
+  __syncthreads();
+  for (int i = threadIdx.x; i < G * D; i += 256) {
+    const int hh = i / D, d = i % D;
+    const float M = fmaxf(fmaxf(sm[0][hh], sm[1][hh]), fmaxf(sm[2][hh], sm[3][hh]));
+    float L = 0.f, A = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const float c = __builtin_amdgcn_exp2f(sm[s2][hh] - M);   // -inf (idle wave) → 0
+      L += sl[s2][hh] * c;
+      A += sacc[(s2 * 16 + hh) * D + d] * c;
+    }
+    const size_t hrow = ((size_t)b * hq + kh * G + hh) * nsplit + split;
+    opart[hrow * D + d] = A;
+    if (d == 0) {
+      mpart[hrow] = M * 0.6931471805599453f;
+      lpart[hrow] = L;
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(D) void decode_attn_merge2_k(const float* __restrict__ opart,
+                                                          const float* __restrict__ mpart,
+                                                          const float* __restrict__ lpart,
+                                                          const int64_t* __restrict__ pos, bf16* __restrict__ out,
+                                                          int hq, int nsplit) {
+  const size_t h = blockIdx.x;  // b*hq + head
+  const int d = threadIdx.x;
+  const int len = (int)pos[h / hq] + 1;
+  const int chunk = split_chunk32(len, nsplit);
+  const int nv = min(nsplit, (len + chunk - 1) / chunk);
+  float M = -INFINITY;
+  for (int s = 0; s < nv; ++s) M = fmaxf(M, mpart[h * nsplit + s]);
+  float L = 0.f, A = 0.f;
+  for (int s = 0; s < nv; ++s) {
+    const float c = __expf(mpart[h * nsplit + s] - M);
+    L += lpart[h * nsplit + s] * c;
+    A += opart[(h * nsplit + s) * D + d] * c;
+  }
+  out[h * D + d] = (bf16)(L > 0.f ? A / L : 0.f);
+}
+
 // ------------------------------------------------------------------------------ sampler
 constexpr int SMP_THR = 1024;
 constexpr int SMP_NW = SMP_THR / 64;
@@ -339,6 +532,29 @@ void launch_decode_attention(const void* q, const void* kc, const void* vc, cons
     decode_attn_merge_k<128><<<B * hq, 128, 0, st>>>(opart, mpart, lpart, lens, (bf16*)out, hq, nsplit);
   else
     decode_attn_merge_k<64><<<B * hq, 64, 0, st>>>(opart, mpart, lpart, lens, (bf16*)out, hq, nsplit);
+  LIPA_CHECK_LAUNCH();
+}
+
+
+// v2: MFMA split-K decode attention with the KV append fused (see decode_attn_mfma_k)
+int decode_split_plan2(int B, int hkv, int max_len) {
+  const int pairs = std::max(1, B * hkv);
+  int ns = std::max(1, (DEC_TARGET_WG + pairs - 1) / pairs);
+  return std::min(ns, std::max(1, (max_len + 127) / 128));
+}
+
+void launch_decode_attention2(const void* q, int ldq, const void* knew, int ldkn, const void* vnew, int ldvn, void* kc,
+                              void* vc, const int64_t* pos, float* opart, float* mpart, float* lpart, void* out, int B,
+                              int Smax, int hq, int hkv, int d, int nsplit, float scale, hipStream_t st) {
+  dim3 grid(nsplit, hkv, B);
+  const float sl2 = scale * 1.4426950408889634f;
+#define P(D_)                                                                                                          \
+  decode_attn_mfma_k<D_><<<grid, 256, 0, st>>>((const bf16*)q, ldq, (const bf16*)knew, ldkn, (const bf16*)vnew, ldvn, \
+                                               (bf16*)kc, (bf16*)vc, pos, opart, mpart, lpart, Smax, hq, hkv, nsplit, \
+                                               sl2);                                                                   \
+  decode_attn_merge2_k<D_><<<B * hq, D_, 0, st>>>(opart, mpart, lpart, pos, (bf16*)out, hq, nsplit)
+  if (d == 128) { P(128); } else { P(64); }
+#undef P
   LIPA_CHECK_LAUNCH();
 }
 

@@ -28,7 +28,7 @@ import torch.utils.checkpoint as ckpt
 from ..ops import reference as ref
 from ..ops.activation import swiglu_fused
 from ..ops.attention import flash_attention
-from ..ops.decode import decode_attention
+from ..ops.decode import decode_attention_append
 from ..ops.loss import fused_linear_cross_entropy, shift_labels
 from ..ops.norm import RMSNorm, rms_norm, rms_norm_residual
 from ..ops.rope import apply_rope, qk_norm_rope
@@ -175,9 +175,9 @@ class Qwen3Attention(nn.Module):
             o = flash_attention(q, k, v, B, S, self.hq, self.hkv, self.d, causal=True, kv_lens=kv_lens)
         elif cache.pos is not None and S == 1:
             # decode: append at each row's own position, split-K attention over the cache
-            cache.write_rows(self.layer_idx, k.reshape(B, -1), v.reshape(B, -1))
-            o = decode_attention(q.reshape(B, -1), cache.k[self.layer_idx], cache.v[self.layer_idx], cache.pos + 1,
-                                 self.hq, self.hkv, self.d, max_len=cache.max_len)
+            o = decode_attention_append(q.reshape(B, -1), k.reshape(B, -1), v.reshape(B, -1), cache.k[self.layer_idx],
+                                        cache.v[self.layer_idx], cache.pos, self.hq, self.hkv, self.d,
+                                        max_len=cache.max_len)
         else:
             kc, vc = cache.update(self.layer_idx, k.reshape(B, S, -1), v.reshape(B, S, -1), start)
             if start == 0:   # prefill: same fused kernel as training (causal + per-row key lengths)
@@ -244,6 +244,7 @@ class Qwen3Model(nn.Module):
         self.register_buffer("inv_freq", inv, persistent=False)
         self.attn_factor = attn_factor
         self.gradient_checkpointing = False
+        self.pp = None          # parallel.pipeline_parallel stage link (inference PP), else None
 
     def rope(self, position_ids: torch.Tensor):
         ang = position_ids.reshape(-1).float()[:, None] * self.inv_freq[None, :]
@@ -258,11 +259,15 @@ class Qwen3Model(nn.Module):
                 torch.arange(start, start + S, device=input_ids.device).expand(B, S)
         cos, sin = self.rope(position_ids)
         x = self.embed_tokens(input_ids).reshape(B * S, -1)
+        if self.pp is not None:
+            x = self.pp.enter(x)        # stages > 0: the previous stage's hidden states
         for layer in self.layers:
             if self.gradient_checkpointing and self.training and cache is None:
                 x = ckpt.checkpoint(layer, x, cos, sin, B, S, None, 0, kv_lens, use_reentrant=False)
             else:
                 x = layer(x, cos, sin, B, S, cache, start, kv_lens)
+        if self.pp is not None:
+            x = self.pp.exit(x)         # hand to the next stage; every stage gets the last one's output
         if decoding:
             cache.pos += 1
         elif cache is not None:

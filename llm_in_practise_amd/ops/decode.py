@@ -44,6 +44,24 @@ def decode_attention(q, kc, vc, lens, hq, hkv, d, max_len=None, scale=None):
     return decode_attention_reference(q, kc, vc, lens, hq, hkv, d, scale)
 
 
+def decode_attention_append(q, k, v, kc, vc, pos, hq, hkv, d, max_len=None, scale=None):
+    """One decode step of every row: write ``k``/``v`` [B, hkv*d] into the caches at ``pos``
+    [B] (int64) and attend ``q`` [B, hq*d] over the ``pos + 1`` keys.  On gfx950 one MFMA
+    split-K kernel does both (``decode_attn_mfma_k``): the new rows are consumed from ``k``/``v``
+    directly and stored by the split that holds the last key."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(d)
+    G = hq // hkv if hkv else 0
+    if (use_native(q) and q.dtype == torch.bfloat16 and d in (64, 128) and hq % hkv == 0 and 1 <= G <= 16
+            and kc.is_contiguous() and vc.is_contiguous() and pos.dtype == torch.long
+            and all(t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0 for t in (q, k, v))):
+        return native().decode_attention_append(q, k, v, kc, vc, pos.contiguous(), hq, hkv, d,
+                                                int(max_len or kc.shape[1]), float(scale))
+    rows = torch.arange(q.shape[0], device=q.device)
+    kc[rows, pos] = k
+    vc[rows, pos] = v
+    return decode_attention(q, kc, vc, pos + 1, hq, hkv, d, max_len, scale)
+
+
 def apply_repetition_penalty(logits: torch.Tensor, history: torch.Tensor | None, penalty: float) -> torch.Tensor:
     if history is None or penalty == 1.0:
         return logits

@@ -29,6 +29,8 @@ from ..quant.nf4 import NF4Weight, dequantize_nf4
 from ._native import native, use_native
 
 EXT_ALIGN = 32   # the kernels consume the LoRA K-slice in MFMA K-steps of 32
+# LIPA_DENSE_GEMM=native: frozen bf16 bases through gemm_bf16w / gemm_bf16_t instead of hipBLASLt
+_NATIVE_DENSE = __import__("os").environ.get("LIPA_DENSE_GEMM", "") == "native"
 
 
 @dataclasses.dataclass
@@ -67,10 +69,12 @@ def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
             return y
         cf, _, at = base.kernel_pack()
         return native().gemm_nf4(x, cf, at, base.shape[0], ext_a, ext_b, residual)
-    if x.shape[0] <= 256:
-        # decode / small batch: the 128-column tiles give too few workgroups to stream the
-        # weights (N/128 WGs), hipBLASLt's split-K skinny kernels reach 2.6-6 TB/s here
-        # (profiles/decode_skinny_gemm.txt); residual folded in as addmm's beta term
+    if not _NATIVE_DENSE:
+        # a bf16 base is a plain library GEMM: hipBLASLt's tuned kernels run it at 1.1-1.5
+        # PFLOP/s at the Qwen3 shapes (profiles/gemm_nf4_v1_v2_hipblaslt_ab.txt) and its split-K
+        # skinny kernels stream decode weights at 2.6-6 TB/s (profiles/decode_skinny_gemm.txt),
+        # ahead of the register-fed gemm_bf16w kernel; residual = addmm's beta term, the LoRA
+        # K-slice one rank-Σr update
         y = torch.addmm(residual, x, base.t()) if residual is not None else x @ base.t()
         if ext_a is not None:
             y.addmm_(ext_a, ext_b.t())
@@ -86,6 +90,9 @@ def _base_gemm_t(dy, base, ext_a=None, ext_b=None):
             return dx if ext_a is None else dx + ext_a @ ext_b.t()
         _, cb, at = base.kernel_pack()
         return native().gemm_nf4_t(dy, cb, at, base.shape[1], ext_a, ext_b)
+    if not _NATIVE_DENSE:
+        dx = dy @ base
+        return dx if ext_a is None else dx.addmm_(ext_a, ext_b.t())
     return native().gemm_bf16_t(dy, base, ext_a, ext_b)
 
 

@@ -124,3 +124,21 @@ def test_hf_classify_and_env(tmp_path, capsys):
     assert os.path.exists(tmp_path / "r" / "eval_results.json")
     main(["env"])
     assert "torch" in capsys.readouterr().out
+
+
+@pytest.mark.parametrize("par", [["-pp", "2"], ["-tp", "2"]])
+def test_infer_tp_pp_under_torchrun(par, capsys):
+    """`torchrun --nproc-per-node 2 lipa infer -pp 2 | -tp 2` prints the single-process greedy text."""
+    import subprocess
+    import sys
+    args = ["infer", "--model", "random:qwen3-tiny", "--tokenizer", "bytes", "--prompt", "pipeline",
+            "--temperature", "0", "--max_new", "8"]
+    main(args)
+    single = capsys.readouterr().out
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_port()), "-m",
+                        "llm_in_practise_amd.cli.main", *args, *par],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.rstrip("\n").splitlines()[-1] == single.rstrip("\n")   # (gloo logs its connects first)

@@ -85,3 +85,42 @@ def test_decode_attention_split_plans(native_ext, B, max_len):
     o = native_ext.decode_attention(q, kc, vc, L, hq, hkv, d, max_len, 1 / math.sqrt(d))
     r = decode_attention_reference(q.float(), kc.float(), vc.float(), L, hq, hkv, d)
     assert (o.float() - r).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("hq,hkv,d", [(32, 8, 128), (8, 8, 64), (40, 8, 128), (16, 1, 64), (64, 4, 128)])
+@pytest.mark.parametrize("pos", [[0, 299, 4095, 128], [76], [31, 32, 33, 1000, 1023, 1024, 5, 64]])
+def test_decode_attention_append_kernel(native_ext, hq, hkv, d, pos):
+    """MFMA decode kernel with the fused KV append: q/k/v are row-strided views of one fused
+    qkv projection output; the new rows must land in the caches at pos and take part in the
+    attention; no other cache row may change."""
+    torch.manual_seed(len(pos) + hq)
+    B, Smax = len(pos), 4096
+    kc = torch.randn(B, Smax, hkv * d, device=DEV).to(torch.bfloat16)
+    vc = torch.randn(B, Smax, hkv * d, device=DEV).to(torch.bfloat16)
+    qkv = torch.randn(B, (hq + 2 * hkv) * d, device=DEV).to(torch.bfloat16)
+    q, k, v = qkv[:, :hq * d], qkv[:, hq * d:(hq + hkv) * d], qkv[:, (hq + hkv) * d:]
+    P = torch.tensor(pos, device=DEV, dtype=torch.long)
+    kc0, vc0 = kc.clone(), vc.clone()
+    o = native_ext.decode_attention_append(q, k, v, kc, vc, P, hq, hkv, d, max(pos) + 1, 1 / math.sqrt(d))
+    rows = torch.arange(B, device=DEV)
+    kc0[rows, P] = k
+    vc0[rows, P] = v
+    assert torch.equal(kc, kc0) and torch.equal(vc, vc0)
+    r = decode_attention_reference(q.float(), kc0.float(), vc0.float(), (P + 1).int(), hq, hkv, d)
+    assert (o.float() - r).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("B,max_len", [(256, 1024), (64, 4096), (1, 1024), (7, 3000)])
+def test_decode_attention_append_split_plans(native_ext, B, max_len):
+    torch.manual_seed(B)
+    hq, hkv, d = 32, 8, 128
+    kc = torch.randn(B, max_len, hkv * d, device=DEV).to(torch.bfloat16)
+    vc = torch.randn(B, max_len, hkv * d, device=DEV).to(torch.bfloat16)
+    q = torch.randn(B, hq * d, device=DEV).to(torch.bfloat16)
+    k = torch.randn(B, hkv * d, device=DEV).to(torch.bfloat16)
+    v = torch.randn(B, hkv * d, device=DEV).to(torch.bfloat16)
+    P = torch.randint(0, max_len, (B,), device=DEV)
+    P[0] = max_len - 1
+    o = native_ext.decode_attention_append(q, k, v, kc, vc, P, hq, hkv, d, max_len, 1 / math.sqrt(d))
+    r = decode_attention_reference(q.float(), kc.float(), vc.float(), (P + 1).int(), hq, hkv, d)
+    assert (o.float() - r).abs().max().item() < 2e-2

@@ -22,8 +22,9 @@ def _port():
     return p
 
 
-def _model(arch, lora):
-    cfg = qwen3_config(arch, num_attention_heads=4, num_key_value_heads=4 if arch == "qwen2-tiny" else 2)
+def _model(arch, lora, layers=2):
+    cfg = qwen3_config(arch, num_attention_heads=4, num_key_value_heads=4 if arch == "qwen2-tiny" else 2,
+                       num_hidden_layers=layers)
     m = Qwen3ForCausalLM.from_config(cfg, dtype=torch.float32, device="cpu", seed=3)
     with torch.no_grad():
         for n, p in m.named_parameters():
@@ -41,18 +42,26 @@ def _model(arch, lora):
     return m
 
 
-def _worker(rank, world, port, arch, lora, q):
+def _worker(rank, world, port, arch, lora, q, pp=1, layers=2):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        from llm_in_practise_amd.parallel.pipeline_parallel import apply_pipeline_parallel, make_tp_pp_groups
         from llm_in_practise_amd.parallel.tensor_parallel import apply_tensor_parallel
         torch.manual_seed(0)
         ids = torch.randint(0, 512, (2, 12))
-        ref_model = _model(arch, lora)
+        ref_model = _model(arch, lora, layers)
         with torch.no_grad():
             ref = ref_model(ids).logits
             ref_gen = ref_model.generate(ids, max_new_tokens=6, do_sample=False) if not lora else None
-        tp_model = apply_tensor_parallel(_model(arch, lora))
+        tpg, ppg = make_tp_pp_groups(world // pp, pp)
+        tp_model = _model(arch, lora, layers)
+        if ppg is not None:
+            apply_pipeline_parallel(tp_model, ppg)
+            n_local = len(next(m for m in tp_model.modules() if hasattr(m, "embed_tokens")).layers)
+            assert n_local < layers
+        if tpg is not None:
+            apply_tensor_parallel(tp_model, tpg)
         with torch.no_grad():
             out = tp_model(ids).logits
             gen = tp_model.generate(ids, max_new_tokens=6, do_sample=False) if not lora else None
@@ -63,11 +72,11 @@ def _worker(rank, world, port, arch, lora, q):
         torch.distributed.destroy_process_group()
 
 
-def _run(world, arch, lora):
+def _run(world, arch, lora, pp=1, layers=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, arch, lora, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, arch, lora, q, pp, layers)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=240) for _ in range(world)]
@@ -85,7 +94,17 @@ def test_tp_matches_single_process(world, arch, lora):
         assert same_gen, rank
 
 
-def _engine_worker(rank, world, port, q):
+@pytest.mark.parametrize("world,pp,arch,lora,layers", [(2, 2, "qwen3-tiny", False, 3), (2, 2, "qwen2-tiny", True, 2),
+                                                       (4, 2, "qwen3-tiny", False, 3)])
+def test_pp_matches_single_process(world, pp, arch, lora, layers):
+    """Pipeline parallel: stages of 2+1 layers (uneven split), with a LoRA adapter,
+    and TP=2 x PP=2 over 4 ranks, all equal to the unsharded model."""
+    for rank, err, same_gen in _run(world, arch, lora, pp, layers):
+        assert err < 1e-5, (rank, err)
+        assert same_gen, rank
+
+
+def _engine_worker(rank, world, port, q, pp=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -102,7 +121,12 @@ def _engine_worker(rank, world, port, q):
             p = SamplingParams(max_tokens=8, temperature=0.0)
             single = [e1.complete(s, p)["text"] for s in ("abc", "hello", "tensor parallel")]
             e1.shutdown()
-        m = apply_tensor_parallel(Qwen3ForCausalLM.from_config(cfg, dtype=torch.float32, seed=0).eval())
+        m = Qwen3ForCausalLM.from_config(cfg, dtype=torch.float32, seed=0).eval()
+        if pp > 1:
+            from llm_in_practise_amd.parallel.pipeline_parallel import apply_pipeline_parallel
+            m = apply_pipeline_parallel(m)
+        else:
+            m = apply_tensor_parallel(m)
         eng = ServingEngine(m, tok, max_batch=4, tp_group=torch.distributed.group.WORLD)
         if rank == 0:
             p = SamplingParams(max_tokens=8, temperature=0.0)
@@ -124,12 +148,13 @@ def _engine_worker(rank, world, port, q):
         torch.distributed.destroy_process_group()
 
 
-def test_tp_serving_engine_spmd():
-    """vLLM-style TP serving: rank 0 owns the queue, followers replay its iterations."""
+@pytest.mark.parametrize("pp", [1, 2])
+def test_tp_serving_engine_spmd(pp):
+    """vLLM-style TP / PP serving: rank 0 owns the queue, followers replay its iterations."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_engine_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_engine_worker, args=(r, 2, port, q, pp)) for r in range(2)]
     for p in ps:
         p.start()
     res = [q.get(timeout=300) for _ in range(2)]
