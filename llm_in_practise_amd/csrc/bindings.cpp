@@ -41,6 +41,7 @@ void launch_pack_nf4(const uint8_t*, uint32_t*, int, int, int, hipStream_t);
 void launch_absmax_t(const float*, const uint8_t*, const float*, const float*, const float*, float*, int, int,
                      hipStream_t);
 void launch_nf4_quantize(const void*, uint8_t*, float*, size_t, hipStream_t);
+void launch_nf4_dequant2(const uint8_t*, const float*, void*, size_t, hipStream_t);
 void launch_nf4_dequant(const uint8_t*, const float*, const uint8_t*, const float*, const float*, const float*, void*,
                         size_t, hipStream_t);
 void launch_attn_fwd(const void*, const void*, const void*, int, int, int, const int*, void*, float*, int, int, int,
@@ -310,6 +311,19 @@ std::vector<Tensor> nf4_quantize(Tensor w, int64_t blocksize) {
   auto absmax = at::empty({w.numel() / 64}, w.options().dtype(at::kFloat));
   launch_nf4_quantize(w.data_ptr(), codes.data_ptr<uint8_t>(), absmax.data_ptr<float>(), w.numel(), stream());
   return {codes, absmax};
+}
+
+// codes [N, K/2] u8 (bnb layout), absmax fp32 [N*K/64] (decoded) → bf16 [N, K]
+Tensor nf4_dequant_fast(Tensor codes, Tensor absmax, int64_t N, int64_t K) {
+  CHECK_CUDA(codes);
+  CHECK_CONTIG(codes);
+  CHECK_CONTIG(absmax);
+  TORCH_CHECK(codes.numel() * 2 == N * K && K % 64 == 0, "nf4_dequant_fast: codes shape");
+  TORCH_CHECK(absmax.scalar_type() == at::kFloat && absmax.numel() * 64 == N * K, "nf4_dequant_fast: absmax");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(codes.data_ptr()) % 16 == 0, "nf4_dequant_fast: 16-B aligned codes");
+  auto w = at::empty({N, K}, codes.options().dtype(at::kBFloat16));
+  launch_nf4_dequant2(codes.data_ptr<uint8_t>(), absmax.data_ptr<float>(), w.data_ptr(), N * K, stream());
+  return w;
 }
 
 Tensor nf4_dequant(Tensor codes, optional<Tensor> absmax, optional<Tensor> qabs, optional<Tensor> absmax2,
@@ -749,6 +763,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("unscale", &unscale);
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequant", &nf4_dequant);
+  m.def("nf4_dequant_fast", &nf4_dequant_fast);
   m.def("nf4_pack", &nf4_pack);
   m.def("nf4_absmax_t", &nf4_absmax_t);
   m.def("gemm_nf4", &gemm_nf4);

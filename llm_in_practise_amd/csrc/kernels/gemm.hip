@@ -481,6 +481,35 @@ __global__ __launch_bounds__(256) void nf4_quantize_k(const bf16* __restrict__ w
   *reinterpret_cast<uint32_t*>(codes + v * 4) = packed;
 }
 
+
+// bnb-layout codes + decoded fp32 block absmax → bf16 [N][K] at HBM speed (the per-step
+// dequant of the "dequant" NF4 mode, ops/linear.py): one lane per 32 elements — one 16-B code
+// load, one absmax, a 256-entry LDS table of (hi, lo) nibble-value pairs, four 16-B stores
+// (a wave writes 4 KB contiguous).
+__global__ __launch_bounds__(256) void nf4_dequant2_k(const uint4* __restrict__ codes, const float* __restrict__ absmax,
+                                                      bf16* __restrict__ w, size_t n32) {
+  __shared__ float2 tab[256];
+  tab[threadIdx.x] = make_float2(kNF4[threadIdx.x >> 4], kNF4[threadIdx.x & 15]);
+  __syncthreads();
+  const size_t g = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= n32) return;
+  const uint4 c = codes[g];
+  const float a = absmax[g >> 1];
+  const uint32_t words[4] = {c.x, c.y, c.z, c.w};
+  bf16x8* dst = reinterpret_cast<bf16x8*>(w + g * 32);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    bf16x8 o;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const float2 t = tab[(words[j] >> (8 * b)) & 0xff];
+      o[2 * b] = (bf16)(t.x * a);
+      o[2 * b + 1] = (bf16)(t.y * a);
+    }
+    dst[j] = o;
+  }
+}
+
 // bnb-layout codes → bf16 (reference / merge path)
 __global__ __launch_bounds__(256) void nf4_dequant_k(const uint8_t* __restrict__ codes, const float* __restrict__ absmax,
                                                      const uint8_t* __restrict__ qabs, const float* __restrict__ absmax2,
@@ -616,6 +645,12 @@ void launch_absmax_t(const float* absmax, const uint8_t* qabs, const float* absm
 void launch_nf4_quantize(const void* w, uint8_t* codes, float* absmax, size_t nelem, hipStream_t st) {
   const size_t vecs = nelem / 8;
   nf4_quantize_k<<<(vecs + 255) / 256, 256, 0, st>>>((const bf16*)w, codes, absmax, nelem);
+  LIPA_CHECK_LAUNCH();
+}
+
+void launch_nf4_dequant2(const uint8_t* codes, const float* absmax, void* w, size_t nelem, hipStream_t st) {
+  const size_t n32 = nelem / 32;
+  nf4_dequant2_k<<<(n32 + 255) / 256, 256, 0, st>>>((const uint4*)codes, absmax, (bf16*)w, n32);
   LIPA_CHECK_LAUNCH();
 }
 

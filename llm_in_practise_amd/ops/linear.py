@@ -31,6 +31,19 @@ from ._native import native, use_native
 EXT_ALIGN = 32   # the kernels consume the LoRA K-slice in MFMA K-steps of 32
 # LIPA_DENSE_GEMM=native: frozen bf16 bases through gemm_bf16w / gemm_bf16_t instead of hipBLASLt
 _NATIVE_DENSE = __import__("os").environ.get("LIPA_DENSE_GEMM", "") == "native"
+# NF4 bases at training / prefill sizes (M > 8; decode uses the NF4 GEMV):
+#  "dequant" (default) — nf4_dequant2_k expands the layer's 4-bit weight to bf16 once per step
+#    at HBM speed, the copy is kept for the backward dX GEMM and freed with the autograd graph
+#    (≈14 GB for Qwen3-8B: memory the 288 GB part has), and hipBLASLt runs fwd + dX at
+#    1.1-1.5 PFLOP/s: 76.7 vs 82.9 ms per Qwen3-8B QLoRA step (profiles/nf4_dequant_vs_fused_ab.txt);
+#  "fused" — the register-dequant MFMA GEMMs (gemm_w4v2, LoRA K-slice + residual epilogue):
+#    no bf16 copy at all, for memory-bound deployments.
+_NF4_MODE = __import__("os").environ.get("LIPA_NF4_GEMM", "dequant")
+
+
+def _nf4_dequant_bf16(q: NF4Weight) -> torch.Tensor:
+    n, k = q.shape
+    return native().nf4_dequant_fast(q.codes, q.gemv_scales(), n, k)
 
 
 @dataclasses.dataclass
@@ -82,6 +95,19 @@ def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
     return native().gemm_bf16(x, base, ext_a, ext_b, residual)
 
 
+def _dense_dx(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dX = dY·W for a bf16 [N, K] weight.  A long reduction into a small output (gate|up:
+    N = 24576 → K = 4096 at M = 2048 is 128 output tiles for 256 CUs) leaves half the chip idle
+    in hipBLASLt's non-split-K kernel; four K-slices as one batched GEMM + an fp32-accumulated
+    sum fill it (491 → 328 µs, profiles/nf4_dequant_vs_fused_ab.txt)."""
+    M, N = dy.shape
+    K = w.shape[1]
+    if N % 4 == 0 and N >= 4 * K and M >= 256 and (M // 256) * max(1, K // 256) < 256:
+        s = 4
+        return torch.bmm(dy.view(M, s, N // s).transpose(0, 1), w.view(s, N // s, K)).sum(0)
+    return dy @ w
+
+
 def _base_gemm_t(dy, base, ext_a=None, ext_b=None):
     """dX = dY·W (+ ext_a · ext_bᵀ, ext_b given as [K, R])."""
     if isinstance(base, NF4Weight):
@@ -91,7 +117,7 @@ def _base_gemm_t(dy, base, ext_a=None, ext_b=None):
         _, cb, at = base.kernel_pack()
         return native().gemm_nf4_t(dy, cb, at, base.shape[1], ext_a, ext_b)
     if not _NATIVE_DENSE:
-        dx = dy @ base
+        dx = _dense_dx(dy, base)
         return dx if ext_a is None else dx.addmm_(ext_a, ext_b.t())
     return native().gemm_bf16_t(dy, base, ext_a, ext_b)
 
@@ -188,7 +214,11 @@ class _FusedLinearFn(torch.autograd.Function):
                 r0 += r
             if not fast:
                 ext_a = _pad_cols(torch.cat(cols, 1))
-        y = _base_gemm(x, base if not dense else weight, ext_a, ext_b, residual)
+        wdq = None
+        if not dense and _NF4_MODE == "dequant" and x.shape[0] > 8 and base.kernel_ok():
+            wdq = _nf4_dequant_bf16(base)
+        y = _base_gemm(x, wdq if wdq is not None else (base if not dense else weight), ext_a, ext_b, residual)
+        ctx.wdq = wdq if ctx.needs_input_grad[0] else None
         if bias is not None:
             y = y + bias
         ctx.meta = meta
@@ -248,7 +278,9 @@ class _FusedLinearFn(torch.autograd.Function):
                 ext_a = _pad_cols(torch.cat([g_list[i].to(dy.dtype) for i in fold], 1))
                 ext_b = torch.cat([bf16_view(ab[2 * i], dy.dtype) for i in fold], 0)            # [R, K]
                 ext_b = F.pad(ext_b, (0, 0, 0, ext_a.shape[1] - ext_b.shape[0])).t().contiguous()  # [K, Rp]
-            dx = _base_gemm_t(dy, base if not dense else weight, ext_a, ext_b)
+            wb = ctx.wdq if ctx.wdq is not None else (base if not dense else weight)
+            dx = _base_gemm_t(dy, wb, ext_a, ext_b)
+        ctx.wdq = None
         for i, br in enumerate(branches):
             key = ctx.keys[i]
             if fast:   # dA += gᵀ·D(x) and (dropout branches) dx += D(g·A), one pass over x / dx

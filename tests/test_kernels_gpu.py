@@ -228,6 +228,14 @@ def test_nf4_quantize_matches_reference(native_ext):
     assert torch.equal(deq, dequantize_nf4(q, torch.bfloat16))
 
 
+@pytest.mark.parametrize("N,K", [(6144, 4096), (128, 192)])
+def test_nf4_dequant_fast_matches_reference(native_ext, N, K):
+    """Per-step dequant kernel (LIPA_NF4_GEMM=dequant) with double-quantised absmax."""
+    w = (0.02 * torch.randn(N, K, device=DEV)).to(torch.bfloat16)
+    q = quantize_nf4(w, 64, True)
+    assert torch.equal(native_ext.nf4_dequant_fast(q.codes, q.gemv_scales(), N, K), dequantize_nf4(q, torch.bfloat16))
+
+
 def _lora_ref(x, w, ext_a=None, ext_b=None, res=None):
     y = x.float() @ w.float().t()
     if ext_a is not None:
@@ -340,7 +348,8 @@ def test_dropout_counter_rng(native_ext):
     assert torch.equal(dx != 0, kept & (t != 0))
 
 
-@pytest.mark.parametrize("mode,arch", [("qlora", "qwen3"), ("lora", "qwen3"), ("qlora", "qwen2")])
+@pytest.mark.parametrize("mode,arch", [("qlora", "qwen3"), ("lora", "qwen3"), ("qlora", "qwen2"),
+                                       ("qlora-dequant", "qwen3")])
 def test_qwen3_native_matches_reference(mode, arch, monkeypatch):
     """Whole-model check: the HIP path (fused q|k|v / gate|up GEMMs, LoRA K-slice, flash attention,
     qk-norm+RoPE (Qwen3) or biased qkv + RoPE (Qwen2), fused CE) against the pure-PyTorch path on
@@ -357,7 +366,7 @@ def test_qwen3_native_matches_reference(mode, arch, monkeypatch):
             for n, p in m.named_parameters():
                 if n.endswith(".bias"):
                     p.normal_(0, 0.05)
-        if mode == "qlora":
+        if mode.startswith("qlora"):
             quantize_model_nf4(m)
         pm = get_peft_model(m, LoraConfig(r=8, lora_alpha=16, lora_dropout=0.0, target_modules=["q_proj", "v_proj"]))
         with torch.no_grad():
@@ -368,6 +377,9 @@ def test_qwen3_native_matches_reference(mode, arch, monkeypatch):
         pm.train()
         return pm
 
+    if mode == "qlora-dequant":      # NF4 bases: HIP dequant once per step + hipBLASLt fwd / dX
+        from llm_in_practise_amd.ops import linear
+        monkeypatch.setattr(linear, "_NF4_MODE", "dequant")
     ids = torch.randint(0, cfg.vocab_size, (2, 128), device=DEV)
     res = {}
     for ref_mode in ("0", "1"):
