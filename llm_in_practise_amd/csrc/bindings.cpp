@@ -42,6 +42,7 @@ void launch_absmax_t(const float*, const uint8_t*, const float*, const float*, c
                      hipStream_t);
 void launch_nf4_quantize(const void*, uint8_t*, float*, size_t, hipStream_t);
 void launch_nf4_dequant2(const uint8_t*, const float*, void*, size_t, hipStream_t);
+void set_dequant_variant(int);
 void launch_nf4_dequant(const uint8_t*, const float*, const uint8_t*, const float*, const float*, const float*, void*,
                         size_t, hipStream_t);
 void launch_attn_fwd(const void*, const void*, const void*, int, int, int, const int*, void*, float*, int, int, int,
@@ -764,6 +765,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequant", &nf4_dequant);
   m.def("nf4_dequant_fast", &nf4_dequant_fast);
+  m.def("set_dequant_variant", &set_dequant_variant);
   m.def("nf4_pack", &nf4_pack);
   m.def("nf4_absmax_t", &nf4_absmax_t);
   m.def("gemm_nf4", &gemm_nf4);

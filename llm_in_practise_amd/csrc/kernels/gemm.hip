@@ -510,6 +510,39 @@ __global__ __launch_bounds__(256) void nf4_dequant2_k(const uint4* __restrict__ 
   }
 }
 
+
+// variant 3: one lane per 8 elements, 4 items per lane strided by the block (every load / store
+// instruction of a wave covers one contiguous range: 256 B of codes, 1 KB of bf16)
+__global__ __launch_bounds__(256) void nf4_dequant3_k(const uint32_t* __restrict__ codes,
+                                                      const float* __restrict__ absmax, bf16* __restrict__ w,
+                                                      size_t n8) {
+  __shared__ float2 tab[256];
+  tab[threadIdx.x] = make_float2(kNF4[threadIdx.x >> 4], kNF4[threadIdx.x & 15]);
+  __syncthreads();
+  const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x;
+  uint32_t c[4];
+  float a[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const size_t i = base + 256 * j;
+    c[j] = i < n8 ? codes[i] : 0u;
+    a[j] = i < n8 ? absmax[i >> 3] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const size_t i = base + 256 * j;
+    if (i >= n8) break;
+    bf16x8 o;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const float2 t = tab[(c[j] >> (8 * b)) & 0xff];
+      o[2 * b] = (bf16)(t.x * a[j]);
+      o[2 * b + 1] = (bf16)(t.y * a[j]);
+    }
+    *reinterpret_cast<bf16x8*>(w + i * 8) = o;
+  }
+}
+
 // bnb-layout codes → bf16 (reference / merge path)
 __global__ __launch_bounds__(256) void nf4_dequant_k(const uint8_t* __restrict__ codes, const float* __restrict__ absmax,
                                                      const uint8_t* __restrict__ qabs, const float* __restrict__ absmax2,
@@ -648,9 +681,16 @@ void launch_nf4_quantize(const void* w, uint8_t* codes, float* absmax, size_t ne
   LIPA_CHECK_LAUNCH();
 }
 
+static int g_dequant_variant = 3;
+void set_dequant_variant(int v) { g_dequant_variant = v; }
 void launch_nf4_dequant2(const uint8_t* codes, const float* absmax, void* w, size_t nelem, hipStream_t st) {
-  const size_t n32 = nelem / 32;
-  nf4_dequant2_k<<<(n32 + 255) / 256, 256, 0, st>>>((const uint4*)codes, absmax, (bf16*)w, n32);
+  if (g_dequant_variant == 2) {
+    const size_t n32 = nelem / 32;
+    nf4_dequant2_k<<<(n32 + 255) / 256, 256, 0, st>>>((const uint4*)codes, absmax, (bf16*)w, n32);
+  } else {
+    const size_t n8 = nelem / 8;
+    nf4_dequant3_k<<<(n8 + 1023) / 1024, 256, 0, st>>>((const uint32_t*)codes, absmax, (bf16*)w, n8);
+  }
   LIPA_CHECK_LAUNCH();
 }
 
