@@ -431,7 +431,8 @@ def cmd_serve(a):
     eng = ServingEngine(m, tok, model_name=a.served_model_name or os.path.basename(a.model.rstrip("/")),
                         max_batch=a.max_batch, system_prompt=a.system, tp_group=tp,
                         max_model_len=a.max_model_len,
-                        prefix_cache_blocks=a.prefix_blocks if a.prefix_caching else 0)
+                        prefix_cache_blocks=a.prefix_blocks if a.prefix_caching else 0,
+                        chunked_prefill=a.max_batched_tokens if a.chunked_prefill else 0)
     if tp is not None and eng.tp_rank != 0:
         eng.follower_loop()              # TP / PP followers replay rank 0's iterations
         return
@@ -720,6 +721,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--prefix-cache-blocks", dest="prefix_blocks", type=int, default=1024,
                    help="HBM pool size in 64-token chunks")
     p.add_argument("--max-model-len", dest="max_model_len", type=int, default=None)
+    p.add_argument("--enable-chunked-prefill", dest="chunked_prefill", action="store_true",
+                   help="prefill long prompts in chunks interleaved with decode (vLLM flag)")
+    p.add_argument("--max-num-batched-tokens", dest="max_batched_tokens", type=int, default=2048,
+                   help="chunk size for --enable-chunked-prefill")
     _add_parallel_args(p)
     p.set_defaults(fn=cmd_serve)
 

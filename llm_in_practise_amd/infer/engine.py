@@ -147,6 +147,7 @@ class _Slot:
     poff: int = 0                        # gen[poff:roff] = context tokens of the last emitted piece
     roff: int = 0
     t_first: float | None = None
+    prefilled: int = -1                  # chunked prefill: prompt tokens in the cache so far (-1 = decoding)
     done: bool = False
     finish: str = "length"
 
@@ -190,13 +191,16 @@ class ServingEngine:
                  system_prompt: str | None = None, chat_template: str = "auto", space_before_end: bool = False,
                  max_model_len: int | None = None, max_prefill_batch: int = 32, prefill_token_budget: int = 16384,
                  use_graphs: bool | None = None, tp_group=None, prefix_cache_blocks: int = 0,
-                 prefix_block: int = 64):
+                 prefix_block: int = 64, chunked_prefill: int = 0):
         """``tp_group``: the model was sharded by ``parallel.tensor_parallel`` over this group.
         The engine then runs SPMD — group rank 0 owns the request queue and broadcasts each
         iteration's admissions; the other ranks call :meth:`follower_loop` and replay exactly the
         same prefill / decode / sampling (logits are bit-identical across ranks, the samplers
         are seeded identically), so no tokens need to be exchanged."""
         self.model, self.tok, self.model_name = model, tokenizer, model_name
+        # vLLM --enable-chunked-prefill: prompts longer than this many tokens are prefilled one
+        # chunk per engine iteration, interleaved with the running batch's decode steps
+        self.chunked_prefill = int(chunked_prefill or 0)
         self.tp_group = tp_group
         self.tp_rank = 0
         if tp_group is not None:
@@ -335,10 +339,12 @@ class ServingEngine:
         with self.lock, torch.no_grad():
             if new:
                 self._admit(new)
-            if any(s is not None for s in self.slots):
+            if self.chunked_prefill:
+                self._prefill_chunks()
+            if any(s is not None and s.prefilled < 0 for s in self.slots):
                 self._decode_step()
             else:
-                self._pending = None             # only finished requests' extra tokens were in flight
+                self._flush_pending()            # only finished requests' extra tokens can be in flight
 
     def _tp_sync(self, new):
         """Broadcast this iteration's admissions (slot, prompt ids, sampling params) from TP rank 0."""
@@ -383,7 +389,25 @@ class ServingEngine:
     def _admit(self, new):
         """Prefill the new prompts together into a scratch cache, copy into their slots, sample
         each one's first token.  With prefix caching, prompts whose leading chunks are cached
-        load them and prefill only their suffix (one request at a time)."""
+        load them and prefill only their suffix (one request at a time).  With chunked prefill,
+        prompts longer than the chunk are only registered here (see :meth:`_prefill_chunks`)."""
+        if self.chunked_prefill:
+            short = []
+            for slot, r in new:
+                if len(r.prompt_ids) > self.chunked_prefill:
+                    P = 0
+                    if self.prefix is not None:
+                        idx = self.prefix.match(r.prompt_ids)
+                        if idx:
+                            self.prefix.load(idx, self.cache, slot)
+                            P = len(idx) * self.prefix.block
+                    self.slots[slot] = _Slot(r, prefilled=P)
+                    self.cache.pos[slot] = P
+                else:
+                    short.append((slot, r))
+            new = short
+            if not new:
+                return
         if self.prefix is not None:
             rest = []
             for slot, r in new:
@@ -399,15 +423,48 @@ class ServingEngine:
             return
         self._admit_batch(new)
 
+    def _slot_view(self, slot: int, length: int) -> KVCache:
+        view = KVCache.__new__(KVCache)
+        view.k = [t[slot:slot + 1] for t in self.cache.k]
+        view.v = [t[slot:slot + 1] for t in self.cache.v]
+        view.len, view.max_len, view.batch, view.pos = length, self.cache.max_len, 1, None
+        view._rows = self.cache._rows[:1]
+        return view
+
+    def _prefill_chunks(self):
+        """One chunk of at most ``chunked_prefill`` prompt tokens (oldest prefilling slot first)
+        per iteration; the chunk attends to the slot's cached prefix.  The last chunk samples the
+        request's first token and the slot joins the decode batch."""
+        pre = sorted((i for i, s in enumerate(self.slots) if s is not None and s.prefilled >= 0),
+                     key=lambda i: self.slots[i].req.t_arrive)
+        if not pre:
+            return
+        slot = pre[0]
+        s = self.slots[slot]
+        r, P = s.req, s.prefilled
+        L = len(r.prompt_ids)
+        C = min(self.chunked_prefill, L - P)
+        ids = torch.tensor([r.prompt_ids[P:P + C]], dtype=torch.long, device=self.device)
+        h = self.lm.model(ids, None, self._slot_view(slot, P), None)
+        s.prefilled = P + C
+        self.cache.pos[slot] = P + C
+        self.stats["batches_total"] += 1
+        if P + C < L:
+            return
+        s.prefilled = -1
+        self.stats["prompt_tokens_total"] += L
+        logits = h[-1:] @ self.lm.lm_head.weight.t()
+        dev_toks, toks = self._sample(logits, [slot])
+        self.next_tok[slot] = dev_toks[0]
+        if self.prefix is not None:
+            self.prefix.store(r.prompt_ids, self.cache, slot)
+        self._accept(slot, toks[0], time.time())
+
     def _admit_suffix(self, slot, r, idx):
         lm = self.lm
         P = len(idx) * self.prefix.block
         self.prefix.load(idx, self.cache, slot)
-        view = KVCache.__new__(KVCache)
-        view.k = [t[slot:slot + 1] for t in self.cache.k]
-        view.v = [t[slot:slot + 1] for t in self.cache.v]
-        view.len, view.max_len, view.batch, view.pos = P, self.cache.max_len, 1, None
-        view._rows = self.cache._rows[:1]
+        view = self._slot_view(slot, P)
         ids = torch.tensor([r.prompt_ids[P:]], dtype=torch.long, device=self.device)
         h = lm.model(ids, None, view, None)
         logits = h[-1:] @ lm.lm_head.weight.t()
@@ -533,7 +590,7 @@ class ServingEngine:
 
     def _decode_step(self):
         lm = self.lm
-        active = [i for i, s in enumerate(self.slots) if s is not None]
+        active = [i for i, s in enumerate(self.slots) if s is not None and s.prefilled < 0]
         self.stats["running"] = len(active)
         n = active[-1] + 1                       # slots fill lowest-first: decode rows [0, n) only
         if self.graphs is not None:              # hipGraph replay of the whole step (bucket >= n rows)
@@ -545,6 +602,10 @@ class ServingEngine:
         free = [i for i in range(n) if self.slots[i] is None]
         if free:                                                              # idle rows stay at position 0
             self.cache.pos[torch.tensor(free, device=self.device)] = 0
+        for i in range(n):       # a slot mid chunked-prefill decoded a junk row at its next prompt position
+            s = self.slots[i]     # (the next chunk overwrites it): put its position back
+            if s is not None and s.prefilled >= 0:
+                self.cache.pos[i] = s.prefilled
         rows = torch.tensor(active, device=self.device)
         if len(active) != n:
             logits = logits[rows]

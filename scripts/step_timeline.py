@@ -41,6 +41,17 @@ def main():
         print(f"step {i}: wall {wall / 1e6:8.2f} ms  gpu-busy {busy / 1e6:8.2f} ms  idle {100 * (1 - busy / wall):5.1f}%  "
               f"kernels {len(st)}")
     n = max(1, len(steps))
+    if steps:                                   # where the GPU waits for the host: largest gaps
+        st = steps[-1]
+        gaps = []
+        for j in range(1, len(st)):
+            g = st[j][0] - max(e for _, e, _ in st[:j]) if j < 400 else st[j][0] - st[j - 1][1]
+            if g > 0:
+                gaps.append((g, j))
+        short = lambda nm: re.sub(r"\(.*", "", nm.replace("(anonymous namespace)", "anon"))[:60]   # noqa: E731
+        print(f"\nlargest idle gaps of the last step (total {sum(g for g, _ in gaps) / 1e6:.2f} ms):")
+        for g, j in sorted(gaps, reverse=True)[:12]:
+            print(f"  {g / 1e3:8.1f} us  at kernel #{j:5d}  after {short(st[j - 1][2])}  before {short(st[j][2])}")
     print(f"\ntop kernels (ms/step over {n} steps):")
     for k, v in agg.most_common(a.top):
         print(f"  {v / 1e6 / n:8.3f} ms  x{cnt[k] / n:6.1f}  {k}")

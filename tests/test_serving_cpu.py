@@ -140,6 +140,39 @@ def test_prefix_caching_same_outputs_and_hits():
     assert outs[0] == outs[64]
 
 
+@pytest.mark.parametrize("prefix_blocks", [0, 64])
+def test_chunked_prefill_matches_whole_prefill(prefix_blocks):
+    """vLLM --enable-chunked-prefill: long prompts are prefilled 24 tokens per iteration while
+    the short ones decode; greedy outputs equal the whole-prompt engine's (also on a prefix-cache
+    hit, where chunking starts after the cached chunks)."""
+    cfg = qwen3_config("qwen3-tiny", vocab_size=256)
+    tok = ByteTokenizer()
+    tok.eos_token_id = None
+    prompts = ["long prompt about MI355X memory %d " % i * (3 + i) for i in range(4)] + ["hi", "short one"]
+    p = SamplingParams(max_tokens=7, temperature=0.0, ignore_eos=True)
+    outs = {}
+    for chunk in (0, 24):
+        m = Qwen3ForCausalLM.from_config(cfg, dtype=torch.float32, seed=0).eval()
+        e = ServingEngine(m, tok, max_batch=4, chunked_prefill=chunk, prefix_cache_blocks=prefix_blocks)
+        if prefix_blocks:
+            e.complete(prompts[3][:130] + " warm", p)
+        reqs = [e.submit(q, p) for q in prompts]
+        res = []
+        for r in reqs:
+            while True:
+                kind, val = r.out.get(timeout=120)
+                assert kind != "error", val
+                if kind == "final":
+                    res.append((val["text"], val["completion_tokens"]))
+                    break
+        outs[chunk] = res
+        if chunk:
+            assert e.stats["batches_total"] >= sum(-(-len(e.encode(q)) // chunk) for q in prompts[:4])
+        assert all(s is None for s in e.slots)
+        e.shutdown()
+    assert outs[0] == outs[24]
+
+
 def test_cache_gateway_exact_and_semantic_levels():
     """H6 L2/L3 cache gateway: exact SHA-256 key, then the 8-dim/2-decimal semantic key."""
     from llm_in_practise_amd.infer.cache_gateway import create_cache_gateway
