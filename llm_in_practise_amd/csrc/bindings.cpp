@@ -42,6 +42,8 @@ void launch_absmax_t(const float*, const uint8_t*, const float*, const float*, c
                      hipStream_t);
 void launch_nf4_quantize(const void*, uint8_t*, float*, size_t, hipStream_t);
 void launch_nf4_dequant2(const uint8_t*, const float*, void*, size_t, hipStream_t);
+int skinny_splits(int, int);
+void launch_gemm_skinny(const void*, int, const void*, const void*, void*, float*, int, int, int, int, hipStream_t);
 void set_dequant_variant(int);
 void launch_nf4_dequant(const uint8_t*, const float*, const uint8_t*, const float*, const float*, const float*, void*,
                         size_t, hipStream_t);
@@ -312,6 +314,33 @@ std::vector<Tensor> nf4_quantize(Tensor w, int64_t blocksize) {
   auto absmax = at::empty({w.numel() / 64}, w.options().dtype(at::kFloat));
   launch_nf4_quantize(w.data_ptr(), codes.data_ptr<uint8_t>(), absmax.data_ptr<float>(), w.numel(), stream());
   return {codes, absmax};
+}
+
+// decode-shaped y = x·Wᵀ (+ residual): x [M <= 64, K] row-strided, W [N, K] contiguous bf16
+Tensor gemm_skinny(Tensor x, Tensor w, optional<Tensor> residual) {
+  CHECK_CUDA(x);
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_CONTIG(w);
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && M >= 1 && M <= 64,
+              "gemm_skinny: x [M<=64, K] row-major, 16-B aligned rows");
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K && K % 64 == 0 && N % 16 == 0, "gemm_skinny: W [N%16, K%64]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              "gemm_skinny: 16-B aligned operands");
+  const void* rp = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    CHECK_BF16((*residual));
+    CHECK_CONTIG((*residual));
+    TORCH_CHECK(residual->size(0) == M && residual->size(1) == N, "gemm_skinny: residual shape");
+    rp = residual->data_ptr();
+  }
+  const int S = skinny_splits(N, K);
+  Tensor part = at::empty({S, M, N}, x.options().dtype(at::kFloat));
+  Tensor out = at::empty({M, N}, x.options());
+  launch_gemm_skinny(x.data_ptr(), x.stride(0), w.data_ptr(), rp, out.data_ptr(), part.data_ptr<float>(), M, N, K, S,
+                     stream());
+  return out;
 }
 
 // codes [N, K/2] u8 (bnb layout), absmax fp32 [N*K/64] (decoded) → bf16 [N, K]
@@ -765,6 +794,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequant", &nf4_dequant);
   m.def("nf4_dequant_fast", &nf4_dequant_fast);
+  m.def("gemm_skinny", &gemm_skinny);
   m.def("set_dequant_variant", &set_dequant_variant);
   m.def("nf4_pack", &nf4_pack);
   m.def("nf4_absmax_t", &nf4_absmax_t);

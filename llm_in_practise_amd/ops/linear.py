@@ -82,6 +82,15 @@ def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
             return y
         cf, _, at = base.kernel_pack()
         return native().gemm_nf4(x, cf, at, base.shape[0], ext_a, ext_b, residual)
+    M, K = x.shape
+    N = base.shape[0]
+    if (M <= 16 and N <= 8192 and K <= 8192 and N % 16 == 0 and K % 64 == 0 and x.stride(0) % 8 == 0
+            and x.stride(1) == 1 and base.is_contiguous() and not _NATIVE_DENSE):
+        # decode-sized q|k|v / o projections: the split-K weight-streaming MFMA kernel
+        # (csrc/kernels/skinny.hip) beats hipBLASLt's latency-bound 23 µs by 25-45 % and fuses
+        # the residual; the wide gate|up / long-K down stay on hipBLASLt (≥ 5 TB/s there)
+        y = native().gemm_skinny(x, base, residual)
+        return y if ext_a is None else y.addmm_(ext_a, ext_b.t())
     if not _NATIVE_DENSE:
         # a bf16 base is a plain library GEMM: hipBLASLt's tuned kernels run it at 1.1-1.5
         # PFLOP/s at the Qwen3 shapes (profiles/gemm_nf4_v1_v2_hipblaslt_ab.txt) and its split-K

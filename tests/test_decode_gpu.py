@@ -124,3 +124,20 @@ def test_decode_attention_append_split_plans(native_ext, B, max_len):
     o = native_ext.decode_attention_append(q, k, v, kc, vc, P, hq, hkv, d, max_len, 1 / math.sqrt(d))
     r = decode_attention_reference(q.float(), kc.float(), vc.float(), (P + 1).int(), hq, hkv, d)
     assert (o.float() - r).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 33, 64])
+@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 12288), (272, 192)])
+def test_gemm_skinny_matches_fp32(native_ext, M, N, K):
+    """Decode-shaped split-K GEMM (+ residual) vs fp32, incl. N not a multiple of the 128-row block."""
+    torch.manual_seed(M)
+    w = (torch.randn(N, K, device=DEV) * 0.02).to(torch.bfloat16)
+    xb = torch.randn(M, K + 64, device=DEV).to(torch.bfloat16)
+    x = xb[:, :K]                                   # row-strided input
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    y = native_ext.gemm_skinny(x, w, None)
+    assert ((y.float() - ref).abs().max() / ref.abs().max()).item() < 1e-2
+    y = native_ext.gemm_skinny(x, w, res)
+    want = ref + res.float()
+    assert ((y.float() - want).abs().max() / want.abs().max()).item() < 1e-2
