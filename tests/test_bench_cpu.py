@@ -1,0 +1,41 @@
+"""bench.py contract on CPU (gloo, 2 ranks): one JSON line from rank 0 with the driver's fields,
+whole-job tokens/s, weak scaling, for the DDP and ZeRO-3 strategies and both GA executions."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("extra", [[], ["--ga-fusion", "0"], ["--strategy", "zero3"]])
+def test_bench_json_contract_two_ranks(extra):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--model", "qwen3-tiny", "--seq-len", "64", *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout            # rank 0 only
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "weak"
+    assert d["higher_is_better"] is True and d["value"] > 0 and d["ms_per_step"] > 0
+    tokens = 2 * 64 * 2 * 2 * 2                  # micro 2 x seq 64 x GA 2 x world 2 x steps 2
+    assert abs(d["value"] - tokens / (d["ms_per_step"] * 2 / 1000)) / d["value"] < 0.02
+    assert d["config"]["global_batch"] == 8
+    assert d["config"]["parallelism"] == ("zero3-dp2" if "zero3" in extra else "dp2")
