@@ -31,7 +31,7 @@ from typing import Any
 
 import torch
 
-from ..models.common import KVCache
+from ..models.common import KVCache, PackedPrefill
 from ..ops.decode import sample
 from ..train.data import render_chatml
 
@@ -261,6 +261,7 @@ class ServingEngine:
         self._pending = None                     # (pinned host tokens, event, owners) of the in-flight step
         self.pipeline = self.device.type == "cuda"
         self._stop = False
+        self._closing = False
         self._worker = None
         if self.tp_rank == 0:
             self._worker = threading.Thread(target=self._loop, daemon=True)
@@ -313,7 +314,10 @@ class ServingEngine:
                 raise RuntimeError(val)
 
     def shutdown(self):
-        self._stop = True
+        if self.tp_group is None:
+            self._stop = True
+        else:   # SPMD: rank 0 must hand the stop to its followers inside the iteration protocol
+            self._closing = True
         self.q.put(None)
 
     # ------------------------------------------------------------------ worker
@@ -331,6 +335,8 @@ class ServingEngine:
 
     def _iteration(self):
         new = self._collect() if self.tp_rank == 0 else []
+        if self._closing and self.tp_rank == 0:
+            new = None
         if self.tp_group is not None:
             new = self._tp_sync(new)
         if new is None:
@@ -478,26 +484,16 @@ class ServingEngine:
         self.stats["batches_total"] += 1
 
     def _admit_batch(self, new):
+        """Prefill the admitted prompts packed back to back (no padding) directly into their
+        cache slots (models/common.py ``PackedPrefill``), sample each one's first token."""
         lm = self.lm
-        B = len(new)
-        S = max(len(r.prompt_ids) for _, r in new)
-        ids = torch.full((B, S), self.pad, dtype=torch.long)
-        lens = torch.zeros(B, dtype=torch.long)
-        for b, (_, r) in enumerate(new):
-            ids[b, :len(r.prompt_ids)] = torch.tensor(r.prompt_ids, dtype=torch.long)
-            lens[b] = len(r.prompt_ids)
-        ids, lens = ids.to(self.device), lens.to(self.device)
-        cfg = lm.config
-        tmp = KVCache(cfg.num_hidden_layers, B, S, cfg.num_key_value_heads, cfg.head_dim, self.cache.k[0].dtype,
-                      self.device)
-        h = lm.model(ids, None, tmp, lens.to(torch.int32))
-        last = h.view(B, S, -1)[torch.arange(B, device=self.device), lens - 1]
-        logits = last @ lm.lm_head.weight.t()
+        lens = [len(r.prompt_ids) for _, r in new]
+        ids = torch.tensor([[t for _, r in new for t in r.prompt_ids]], dtype=torch.long).to(self.device)
+        pp = PackedPrefill(self.cache, [s for s, _ in new], lens, self.device)
+        h = lm.model(ids, pp.positions, pp, None)
+        logits = h[pp.last] @ lm.lm_head.weight.t()
         rows = torch.tensor([s for s, _ in new], device=self.device)
-        for l in range(cfg.num_hidden_layers):
-            self.cache.k[l][rows, :S] = tmp.k[l]
-            self.cache.v[l][rows, :S] = tmp.v[l]
-        self.cache.pos[rows] = lens
+        self.cache.pos[rows] = torch.tensor(lens, dtype=torch.long, device=self.device)
         now = time.time()
         for b, (slot, r) in enumerate(new):
             self.slots[slot] = _Slot(r)

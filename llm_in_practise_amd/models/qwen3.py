@@ -33,7 +33,7 @@ from ..ops.loss import fused_linear_cross_entropy, shift_labels
 from ..ops.norm import RMSNorm, rms_norm, rms_norm_residual
 from ..ops.rope import apply_rope, qk_norm_rope
 from ..parallel.tensor_parallel import tp_all_reduce
-from .common import CausalLMOutput, FusedProjection, KVCache, can_fuse, project
+from .common import CausalLMOutput, FusedProjection, KVCache, PackedPrefill, can_fuse, project
 
 
 @dataclasses.dataclass
@@ -173,6 +173,8 @@ class Qwen3Attention(nn.Module):
             v = qkv[:, nq + nk:]
         if cache is None:
             o = flash_attention(q, k, v, B, S, self.hq, self.hkv, self.d, causal=True, kv_lens=kv_lens)
+        elif isinstance(cache, PackedPrefill):
+            o = cache.attend(self.layer_idx, q, k, v, self.hq, self.hkv, self.d, flash_attention)
         elif cache.pos is not None and S == 1:
             # decode: append at each row's own position, split-K attention over the cache
             o = decode_attention_append(q.reshape(B, -1), k.reshape(B, -1), v.reshape(B, -1), cache.k[self.layer_idx],

@@ -14,5 +14,5 @@ timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpu
   > $R/gpurun_out/prof_serve/bench.log 2>&1 || { tail -20 $R/gpurun_out/prof_serve/bench.log; exit 1; }
 grep output_tok $R/gpurun_out/prof_serve/bench.log
 S=$(find $R/gpurun_out/prof_serve -name "*kernel_stats.csv" | head -1)
-python3 $R/scripts/prof_summary.py $S 1 > $R/gpurun_out/prof_serve/summary.txt
-head -40 $R/gpurun_out/prof_serve/summary.txt
+python3 $R/scripts/prof_summary.py $S 1 30 > $R/gpurun_out/prof_serve/summary.txt
+find $R/gpurun_out/prof_serve -name "*.csv" ! -name "*kernel_stats.csv" -delete; head -32 $R/gpurun_out/prof_serve/summary.txt
