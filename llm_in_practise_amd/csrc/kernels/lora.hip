@@ -19,6 +19,8 @@
 // lora_acc_k   (VALU): part[c][j][k] = Σ_{m∈chunk c} G[m,j]·D(X)[m,k]  and optionally
 //              DX[m,k] += D(Σ_j G[m,j]·W[j,k]) — each thread owns 8 consecutive k of one row stream,
 //              reads X and DX once; the per-chunk (64-row) partials are summed by the caller.
+#include <cstdlib>
+
 #include "common.h"
 
 using namespace lipa;
@@ -86,9 +88,10 @@ __global__ __launch_bounds__(NW * 64) void lora_proj_k(const bf16* __restrict__ 
   }
 }
 
-// NRL row-lanes × 64 k-threads (8 consecutive k each); a chunk of ROWS rows is split RB = ROWS/NRL
-// rows per thread, and ALL of a thread's x / dx rows are loaded before any is used (one exposed
-// HBM round trip per workgroup instead of one per 4 rows); the chunk's G rows are staged in LDS.
+// NRL row-lanes × 64 k-threads (8 consecutive k each); a chunk of ROWS rows is walked in passes of
+// NRL·RB rows (RB rows per thread), the next pass's x / dx rows loaded before the current pass is
+// used (one exposed HBM round trip per workgroup, not one per pass); the chunk's G rows are staged
+// in LDS.  Taller chunks mean fewer workgroups and fewer fp32 atomics per output element.
 template <int R, bool DXU, int NRL, int ROWS>
 __global__ __launch_bounds__(NRL * 64) void lora_acc_k(const float* __restrict__ G, int ldg, int r,
                                                       const bf16* __restrict__ X, int ldx, bf16* __restrict__ DX,
@@ -96,7 +99,8 @@ __global__ __launch_bounds__(NRL * 64) void lora_acc_k(const float* __restrict__
                                                       float* __restrict__ out, int64_t sj, int64_t sk,
                                                       float* __restrict__ part, int M, uint64_t key, uint32_t thr16,
                                                       float dscale, size_t mask_ld) {
-  constexpr int RB = ROWS / NRL;
+  constexpr int RB = (ROWS / NRL) < 8 ? (ROWS / NRL) : 8;
+  constexpr int NP = ROWS / (NRL * RB);
   constexpr int NT = NRL * 64;
   __shared__ float red[64][R * 8 + 1];
   __shared__ float gs[ROWS][R];
@@ -114,15 +118,18 @@ __global__ __launch_bounds__(NRL * 64) void lora_acc_k(const float* __restrict__
 #pragma unroll
     for (int j = 0; j < R; ++j) wv[j] = (kin && j < r) ? *reinterpret_cast<const bf16x8*>(W + (size_t)j * K + k0) : bf16x8{};
   }
-  bf16x8 xb[RB], db[DXU ? RB : 1];
+  bf16x8 xb[2][RB], db[2][DXU ? RB : 1];
+  auto load = [&](int buf, int pass) {
 #pragma unroll
-  for (int q = 0; q < RB; ++q) {
-    const int m = min(mb + rl + NRL * q, M - 1);
-    if (kin) {
-      xb[q] = *reinterpret_cast<const bf16x8*>(X + (size_t)m * ldx + k0);
-      if constexpr (DXU) db[q] = *reinterpret_cast<const bf16x8*>(DX + (size_t)m * lddx + k0);
+    for (int q = 0; q < RB; ++q) {
+      const int m = min(mb + pass * NRL * RB + rl + NRL * q, M - 1);
+      if (kin) {
+        xb[buf][q] = *reinterpret_cast<const bf16x8*>(X + (size_t)m * ldx + k0);
+        if constexpr (DXU) db[buf][q] = *reinterpret_cast<const bf16x8*>(DX + (size_t)m * lddx + k0);
+      }
     }
-  }
+  };
+  load(0, 0);
   __syncthreads();  // gs ready
   float acc[R][8];
 #pragma unroll
@@ -131,31 +138,36 @@ __global__ __launch_bounds__(NRL * 64) void lora_acc_k(const float* __restrict__
     for (int i = 0; i < 8; ++i) acc[j][i] = 0.f;
   const float ds = thr16 ? dscale : 1.f;
 #pragma unroll
-  for (int q = 0; q < RB; ++q) {
-    const int ml = rl + NRL * q, m = mb + ml;
-    if (!kin || m >= me) continue;
-    const uint32_t keep = thr16 ? dropout_keep8(key, ((size_t)m * mask_ld + k0) >> 3, thr16) : 0xFFu;
-    float xv[8], g[R];
+  for (int pass = 0; pass < NP; ++pass) {
+    const int cur = pass & 1;
+    if (pass + 1 < NP) load(cur ^ 1, pass + 1);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) xv[i] = ((keep >> i) & 1) ? (float)xb[q][i] * ds : 0.f;
+    for (int q = 0; q < RB; ++q) {
+      const int ml = pass * NRL * RB + rl + NRL * q, m = mb + ml;
+      if (!kin || m >= me) continue;
+      const uint32_t keep = thr16 ? dropout_keep8(key, ((size_t)m * mask_ld + k0) >> 3, thr16) : 0xFFu;
+      float xv[8], g[R];
 #pragma unroll
-    for (int j = 0; j < R; ++j) g[j] = gs[ml][j];
+      for (int i = 0; i < 8; ++i) xv[i] = ((keep >> i) & 1) ? (float)xb[cur][q][i] * ds : 0.f;
 #pragma unroll
-    for (int j = 0; j < R; ++j)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[j][i] += g[j] * xv[i];
-    if constexpr (DXU) {
-      float t[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) t[i] = 0.f;
+      for (int j = 0; j < R; ++j) g[j] = gs[ml][j];
 #pragma unroll
       for (int j = 0; j < R; ++j)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) t[i] += g[j] * (float)wv[j][i];
-      bf16x8 o;
+        for (int i = 0; i < 8; ++i) acc[j][i] += g[j] * xv[i];
+      if constexpr (DXU) {
+        float t[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = (bf16)((float)db[q][i] + (((keep >> i) & 1) ? t[i] * ds : 0.f));
-      *reinterpret_cast<bf16x8*>(DX + (size_t)m * lddx + k0) = o;
+        for (int i = 0; i < 8; ++i) t[i] = 0.f;
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) t[i] += g[j] * (float)wv[j][i];
+        bf16x8 o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = (bf16)((float)db[cur][q][i] + (((keep >> i) & 1) ? t[i] * ds : 0.f));
+        *reinterpret_cast<bf16x8*>(DX + (size_t)m * lddx + k0) = o;
+      }
     }
   }
   // reduce the NRL row-lanes through LDS (one wave at a time), then write this chunk's partial
@@ -186,6 +198,111 @@ __global__ __launch_bounds__(NRL * 64) void lora_acc_k(const float* __restrict__
   }
 }
 
+
+// lora_acc on the matrix cores: part[j][k] = Σ_m G[m,j]·D(X)[m,k] as v_mfma_f32_16x16x32_bf16 with
+// the rank index j as the 16 MFMA rows (r <= 16), k as the columns and m as the reduction.  The
+// reduction runs down the columns of the row-major X, so no LDS transpose: lane (q = l/16, n = l%16)
+// loads 8 rows m0+8q+e of one 8-k chunk k8 = kb+8n (16 B each, 16 lanes = one 256-B row segment)
+// and that 8x8 register block supplies the B operand of 8 MFMAs, MFMA c taking column k8+c of all
+// 8 rows (so MFMA c's 16 columns are k = kb+8n+c, n = 0..15).  The VALU kernel above spent 2·R
+// FMAs per element and ran VALU-bound at 1-2 TB/s; here the dA / dB product is ≈ 1 % of MFMA time.
+// A workgroup = 4 waves stacked in m (SUB 32-row steps each) over one 128-wide k block; the waves'
+// partials meet in LDS and leave as one fp32 atomic per output per workgroup.  With DXU, each lane
+// also applies dx[m, k8..k8+7] += D(Σ_j G[m,j]·W[j,k]) to the rows it holds (VALU, R FMAs/element).
+template <int R, bool DXU, int SUB>
+__global__ __launch_bounds__(256) void lora_acc_mfma_k(const float* __restrict__ G, int ldg, int r,
+                                                      const bf16* __restrict__ X, int ldx, bf16* __restrict__ DX,
+                                                      int lddx, const bf16* __restrict__ W, int K,
+                                                      float* __restrict__ out, int64_t sj, int64_t sk, int M,
+                                                      uint64_t key, uint32_t thr16, float dscale, size_t mask_ld) {
+  __shared__ float red[4][64][33];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int q = lane >> 4, n = lane & 15;
+  const int kb = blockIdx.x * 128;
+  const int k8 = kb + 8 * n;
+  const int mw = blockIdx.y * (128 * SUB) + w * (32 * SUB);
+  bf16x8 wv[DXU ? R : 1];
+  if constexpr (DXU) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) wv[j] = j < r ? *reinterpret_cast<const bf16x8*>(W + (size_t)j * K + k8) : bf16x8{};
+  }
+  f32x4 acc[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float ds = thr16 ? dscale : 1.f;
+#pragma unroll
+  for (int s = 0; s < SUB; ++s) {
+    const int m0 = mw + 32 * s + 8 * q;
+    bf16x8 xb[8], db[DXU ? 8 : 1];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int m = min(m0 + e, M - 1);
+      xb[e] = *reinterpret_cast<const bf16x8*>(X + (size_t)m * ldx + k8);
+      if constexpr (DXU) db[e] = *reinterpret_cast<const bf16x8*>(DX + (size_t)m * lddx + k8);
+    }
+    bf16x8 a;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int m = m0 + e;
+      a[e] = (bf16)((m < M && n < r) ? G[(size_t)m * ldg + n] : 0.f);
+    }
+    uint32_t keep[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int m = m0 + e;
+      keep[e] = m >= M ? 0u : (thr16 ? dropout_keep8(key, ((size_t)m * mask_ld + k8) >> 3, thr16) : 0xFFu);
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      bf16x8 b;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) b[e] = ((keep[e] >> c) & 1) ? xb[e][c] : (bf16)0.f;
+      acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[c], 0, 0, 0);
+    }
+    if constexpr (DXU) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int m = m0 + e;
+        if (m >= M) continue;
+        float gr[R];
+#pragma unroll
+        for (int j = 0; j < R; j += 4) {
+          if (j < r) {
+            const f32x4 t4 = *reinterpret_cast<const f32x4*>(G + (size_t)m * ldg + j);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) gr[j + u] = j + u < r ? t4[u] : 0.f;   // never touch padding columns
+          } else {
+            gr[j] = gr[j + 1] = gr[j + 2] = gr[j + 3] = 0.f;
+          }
+        }
+        float t[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t[i] = 0.f;
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) t[i] += gr[j] * (float)wv[j][i];
+        bf16x8 o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = (bf16)((float)db[e][i] + (((keep[e] >> i) & 1) ? t[i] * ds : 0.f));
+        *reinterpret_cast<bf16x8*>(DX + (size_t)m * lddx + k8) = o;
+      }
+    }
+  }
+  // acc[c][t] = part[j = 4q + t][k = kb + 8n + c]
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) red[w][lane][c * 4 + t] = acc[c][t];
+  __syncthreads();
+  const bool jfast = sj == 1;   // consecutive threads along the destination's unit stride
+  for (int idx = threadIdx.x; idx < r * 128; idx += 256) {
+    const int j = jfast ? idx % r : idx / 128, kk = jfast ? idx / r : idx % 128;
+    const int ln = 16 * (j >> 2) + (kk >> 3), slot = (kk & 7) * 4 + (j & 3);
+    const float v = (red[0][ln][slot] + red[1][ln][slot] + red[2][ln][slot] + red[3][ln][slot]) * ds;
+    atomicAdd(out + j * sj + (int64_t)(kb + kk) * sk, v);
+  }
+}
 }  // namespace
 
 // X row stride ldx (elements), W [r, K] bf16 contiguous; K % 32 == 0; outf/outb may each be null.
@@ -207,7 +324,11 @@ void launch_lora_proj(const void* X, int ldx, const void* W, int r, int K, float
 // with part != null the per-chunk partials [chunks, r, K] (deterministic mode);
 // with DX: DX[m,k] += D(Σ_j G[m,j]·W[j,k]).
 // Chunk height: 64 rows, or 32 when that leaves fewer than 256 workgroups (narrow K).
-static int lora_acc_rows(int M, int K) { return ((K / 8 + 63) / 64) * ((M + 63) / 64) >= 256 ? 64 : 32; }
+static int lora_acc_rows(int M, int K) {
+  static const int forced = [] { const char* e = getenv("LIPA_LORA_ROWS"); return e ? atoi(e) : 0; }();
+  if (forced == 32 || forced == 64 || forced == 128 || forced == 256) return forced;
+  return ((K / 8 + 63) / 64) * ((M + 63) / 64) >= 256 ? 64 : 32;
+}
 int lora_acc_chunks(int M, int K) { const int rows = lora_acc_rows(M, K); return (M + rows - 1) / rows; }
 
 void launch_lora_acc(const float* G, int ldg, int r, const void* X, int ldx, void* DX, int lddx, const void* W, int K,
@@ -215,6 +336,30 @@ void launch_lora_acc(const float* G, int ldg, int r, const void* X, int ldx, voi
                      hipStream_t st) {
   const uint32_t thr = p > 0.f ? (uint32_t)(p * 65536.0f + 0.5f) : 0u;
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  static const bool valu_only = getenv("LIPA_LORA_ACC_VALU") != nullptr;
+  if (!part && r <= 16 && K % 128 == 0 && ldx % 8 == 0 && ldg % 4 == 0 && ((uintptr_t)G & 15) == 0 && !valu_only) {
+    // matrix-core path (deterministic mode keeps the VALU kernel's fixed-order partials)
+    static const int sub_env = [] { const char* e = getenv("LIPA_LORA_SUB"); return e ? atoi(e) : 0; }();
+    const int sub = sub_env == 2 ? 2 : 1;   // 32 rows per wave: 2 waves/SIMD beat longer waves (-10-25 %)
+    dim3 g2(K / 128, (M + 128 * sub - 1) / (128 * sub));
+#define C(R_, D_, S_)                                                                                        \
+  lora_acc_mfma_k<R_, D_, S_><<<g2, 256, 0, st>>>(G, ldg, r, (const bf16*)X, ldx, (bf16*)DX, lddx,            \
+                                                  (const bf16*)W, K, out, sj, sk, M, key, thr, ds, mask_ld)
+#define D2(R_, D_) \
+  if (sub == 2)    \
+    C(R_, D_, 2);  \
+  else             \
+    C(R_, D_, 1)
+    if (r <= 8) {
+      if (DX) { D2(8, true); } else { D2(8, false); }
+    } else {
+      if (DX) { D2(16, true); } else { D2(16, false); }
+    }
+#undef D2
+#undef C
+    LIPA_CHECK_LAUNCH();
+    return;
+  }
   const int rows = lora_acc_rows(M, K);
   dim3 grid((K / 8 + 63) / 64, (M + rows - 1) / rows);
 // r <= 8: 8 row-lanes (512 threads, 2 waves/SIMD); r <= 16: 4 row-lanes (the accumulators double)
@@ -222,7 +367,11 @@ void launch_lora_acc(const float* G, int ldg, int r, const void* X, int ldx, voi
   lora_acc_k<R_, D_, (R_ > 8 ? 4 : 8), ROWS_><<<grid, (R_ > 8 ? 256 : 512), 0, st>>>(                            \
       G, ldg, r, (const bf16*)X, ldx, (bf16*)DX, lddx, (const bf16*)W, K, out, sj, sk, part, M, key, thr, ds, mask_ld)
 #define B(R_, D_)       \
-  if (rows == 64)       \
+  if (rows == 256)      \
+    A(R_, D_, 256);     \
+  else if (rows == 128) \
+    A(R_, D_, 128);     \
+  else if (rows == 64)  \
     A(R_, D_, 64);      \
   else                  \
     A(R_, D_, 32)

@@ -426,3 +426,10 @@ def test_lora_fused_kernels(native_ext, M, K, r, p):
     dbt = torch.zeros(K, r, device=DEV)                       # transposed destination ([n, r] grad of B)
     native_ext.lora_acc(gg, big, 128, K, dbt, True, None, None, 0.0, 0, True)
     assert rel_err(dbt, (gg.t() @ big[:, 128:128 + K].float()).t()) < 1e-2
+    dbt2 = torch.full((K, r), 0.5, device=DEV)                 # same, atomic (matrix-core) path
+    native_ext.lora_acc(gg, big, 128, K, dbt2, True, None, None, 0.0, 0, False)
+    assert rel_err(dbt2 - 0.5, (gg.t() @ big[:, 128:128 + K].float()).t()) < 1e-2
+    # no-dropout dA without a dx update, and the VALU fallback agrees with the matrix-core path
+    da2 = torch.zeros(r, K, device=DEV)
+    native_ext.lora_acc(gg, x, 0, K, da2, False, None, None, 0.0, 0, False)
+    assert rel_err(da2, gg.t() @ x.float()) < 1e-2
