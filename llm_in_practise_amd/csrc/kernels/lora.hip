@@ -30,14 +30,15 @@ namespace {
 // One workgroup = 16 rows × ALL of K: its NW waves each own K/NW (all fragment loads of a wave in
 // flight at once), partials meet in LDS and the result is written once (fp32 and/or bf16) — no
 // atomics, no zero-initialised output, no follow-up cast kernel.
-template <int NW>
+template <int NW, int RW>
 __global__ __launch_bounds__(NW * 64) void lora_proj_k(const bf16* __restrict__ X, int ldx, const bf16* __restrict__ W,
                                                       int r, int K, float* __restrict__ outf, int ldof,
                                                       bf16* __restrict__ outb, int ldob, int M, uint64_t key,
                                                       uint32_t thr16, float dscale, float scale, size_t mask_ld) {
   __shared__ f32x4 red[NW][64];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int m0 = blockIdx.x * 16;
+  const int m0 = blockIdx.x * RW;
+  const bool rv = (lane & 15) < RW;   // RW = 8: MFMA rows 8..15 are zero padding (twice the workgroups)
   const int row = min(m0 + (lane & 15), M - 1);
   const int kw = K / NW;
   const int kbeg = w * kw;
@@ -52,14 +53,14 @@ __global__ __launch_bounds__(NW * 64) void lora_proj_k(const bf16* __restrict__ 
     for (int s = 0; s < 8; ++s)
       if (s < ns) {
         const int k = k0 + s * 32 + 8 * (lane >> 4);
-        av[s] = *reinterpret_cast<const bf16x8*>(xr + k);
+        av[s] = rv ? *reinterpret_cast<const bf16x8*>(xr + k) : bf16x8{};
         bv[s] = *reinterpret_cast<const bf16x8*>(wr + k);
       }
 #pragma unroll
     for (int s = 0; s < 8; ++s)
       if (s < ns) {
         bf16x8 a = av[s];
-        if (thr16) {
+        if (thr16 && rv) {
           const int k = k0 + s * 32 + 8 * (lane >> 4);
           const uint32_t keep = dropout_keep8(key, ((size_t)row * mask_ld + k) >> 3, thr16);
 #pragma unroll
@@ -80,8 +81,8 @@ __global__ __launch_bounds__(NW * 64) void lora_proj_k(const bf16* __restrict__ 
   if (j >= r) return;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int m = m0 + 4 * (lane >> 4) + i;
-    if (m >= M) continue;
+    const int ml = 4 * (lane >> 4) + i, m = m0 + ml;
+    if (ml >= RW || m >= M) continue;
     const float v = t[i] * scale;
     if (outf) outf[(size_t)m * ldof + j] = v;
     if (outb) outb[(size_t)m * ldob + j] = (bf16)v;
@@ -310,12 +311,18 @@ void launch_lora_proj(const void* X, int ldx, const void* W, int r, int K, float
                       int M, uint64_t key, float p, float scale, size_t mask_ld, hipStream_t st) {
   const uint32_t thr = p > 0.f ? (uint32_t)(p * 65536.0f + 0.5f) : 0u;
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  const int grid = (M + 15) / 16;
-  if (K % (16 * 32) == 0)
-    lora_proj_k<16><<<grid, 1024, 0, st>>>((const bf16*)X, ldx, (const bf16*)W, r, K, outf, ldof, (bf16*)outb, ldob,
+  // 16-row workgroups leave half of the 256 CUs idle below M = 4096: use 8 (zero-padded MFMA rows)
+  static const int rw_env = [] { const char* e = getenv("LIPA_LORA_PROJ_RW"); return e ? atoi(e) : 0; }();
+  const int rw = rw_env ? rw_env : (M < 4096 ? 8 : 16);
+  const int grid = (M + rw - 1) / rw;
+  if (K % (16 * 32) == 0 && rw == 8)
+    lora_proj_k<16, 8><<<grid, 1024, 0, st>>>((const bf16*)X, ldx, (const bf16*)W, r, K, outf, ldof, (bf16*)outb, ldob,
+                                              M, key, thr, ds, scale, mask_ld);
+  else if (K % (16 * 32) == 0)
+    lora_proj_k<16, 16><<<grid, 1024, 0, st>>>((const bf16*)X, ldx, (const bf16*)W, r, K, outf, ldof, (bf16*)outb, ldob,
                                            M, key, thr, ds, scale, mask_ld);
   else
-    lora_proj_k<1><<<grid, 64, 0, st>>>((const bf16*)X, ldx, (const bf16*)W, r, K, outf, ldof, (bf16*)outb, ldob, M,
+    lora_proj_k<1, 16><<<(M + 15) / 16, 64, 0, st>>>((const bf16*)X, ldx, (const bf16*)W, r, K, outf, ldof, (bf16*)outb, ldob, M,
                                         key, thr, ds, scale, mask_ld);
   LIPA_CHECK_LAUNCH();
 }
