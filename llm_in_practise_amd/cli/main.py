@@ -13,6 +13,7 @@
     lipa guard --backend URL [--port 8099]                                      (H3)
     lipa convert-alpaca --input self_cognition.jsonl --out alpaca.json           (E10 converter)
     lipa hf-classify [--model-path bert-dir] [--data imdb.jsonl]                 (G5 Trainer demo)
+    lipa dl-basics {mlp,optimizers,rnn,cnn,seq2seq}                            (B9 DL_Basics notebooks)
     lipa env                                                                     (G5 env_test)
     lipa bench ...                                                               (bench.py)
 
@@ -532,6 +533,50 @@ def cmd_hf_classify(a):
     tr.save_metrics("eval", res)
 
 
+def cmd_dl_basics(a):
+    """B9 ``DL_Basics/*.ipynb`` demos as runnable commands; prints one JSON line per result."""
+    import numpy as np
+
+    from ..dl_basics import numpy_cnn, numpy_nn, numpy_rnn, seq2seq
+    rng = np.random.default_rng(a.seed)
+    if a.demo == "mlp":                    # two-hidden-layer net on a noisy sine, mini-batches + L2
+        x = rng.uniform(-3, 3, (512, 1))
+        y = np.sin(x) + rng.normal(0, 0.05, x.shape)
+        m = numpy_nn.MLP([1, 32, 32, 1], act="tanh", l2=1e-4, seed=a.seed)
+        h = numpy_nn.train_mlp(m, x, y, optimizer="adam", lr=1e-2, epochs=a.epochs, batch_size=64, seed=a.seed)
+        print(json.dumps({"demo": "mlp", "first_loss": h["train"][0], "final_loss": h["train"][-1]}))
+    elif a.demo == "optimizers":           # the notebook's optimiser comparison on the same problem
+        x = rng.normal(size=(256, 4))
+        y = x @ rng.normal(size=(4, 1)) + 0.1 * rng.normal(size=(256, 1))
+        for name in numpy_nn.OPTIMIZERS:
+            m = numpy_nn.MLP([4, 16, 1], seed=a.seed)
+            h = numpy_nn.train_mlp(m, x, y, optimizer=name, lr=1e-2, epochs=a.epochs, batch_size=32, seed=a.seed)
+            print(json.dumps({"demo": "optimizers", "optimizer": name, "final_loss": h["train"][-1]}))
+    elif a.demo == "rnn":
+        for kind in ("rnn", "lstm", "gru"):
+            ls = numpy_rnn.train_sequence_regressor(kind, steps=10 * a.epochs, seed=a.seed)
+            print(json.dumps({"demo": "bptt", "cell": kind, "first_loss": ls[0], "final_loss": float(np.mean(ls[-20:]))}))
+    elif a.demo == "cnn":                  # LeNet-5 on synthetic 28x28 "digits" (class = bright quadrant)
+        net = numpy_cnn.LeNet5(num_classes=4)
+        opt = torch.optim.Adam(net.parameters(), lr=1e-3)
+        for step in range(a.epochs):
+            lab = torch.randint(0, 4, (64,))
+            img = torch.randn(64, 1, 28, 28) * 0.3
+            for i, c in enumerate(lab.tolist()):
+                img[i, 0, (c // 2) * 14:(c // 2) * 14 + 14, (c % 2) * 14:(c % 2) * 14 + 14] += 1.0
+            loss = torch.nn.functional.cross_entropy(net(img), lab)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+        print(json.dumps({"demo": "lenet5", "final_loss": loss.item()}))
+    else:                                  # seq2seq: string reversal with Bahdanau attention
+        words = ["".join(rng.choice(list("abcdefgh"), rng.integers(3, 8))) for _ in range(600)]
+        model, sv, tv, ls = seq2seq.train_seq2seq([(w, w[::-1]) for w in words], epochs=a.epochs, seed=a.seed)
+        test = words[:5]
+        print(json.dumps({"demo": "seq2seq", "final_loss": ls[-1],
+                          "samples": dict(zip(test, seq2seq.translate(model, sv, tv, test)))}, ensure_ascii=False))
+
+
 def cmd_env(a):
     """G5 ``env_test.py``: device / runtime versions."""
     info = {"torch": torch.__version__, "hip": getattr(torch.version, "hip", None),
@@ -779,6 +824,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--lr", type=float, default=2e-5)
     p.add_argument("--output-dir", dest="output_dir", default="./results")
     p.set_defaults(fn=cmd_hf_classify)
+    p = sub.add_parser("dl-basics", help="DL_Basics notebook demos (numpy backprop, BPTT, LeNet-5, seq2seq)")
+    p.add_argument("demo", choices=["mlp", "optimizers", "rnn", "cnn", "seq2seq"])
+    p.add_argument("--epochs", type=int, default=30)
+    p.add_argument("--seed", type=int, default=0)
+    p.set_defaults(fn=cmd_dl_basics)
     p = sub.add_parser("env")
     p.set_defaults(fn=cmd_env)
 
