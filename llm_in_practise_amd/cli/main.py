@@ -11,6 +11,7 @@
     lipa infer --model DIR --prompt TEXT                                        (F1b, F2c, G1)
     lipa serve --model DIR [--adapter DIR] [--port 8000]                        (G4, H1)
     lipa guard --backend URL [--port 8099]                                      (H3)
+    lipa router --config deploy/litellm/config.yaml [--port 4000]               (H2 LiteLLM router)
     lipa convert-alpaca --input self_cognition.jsonl --out alpaca.json           (E10 converter)
     lipa hf-classify [--model-path bert-dir] [--data imdb.jsonl]                 (G5 Trainer demo)
     lipa dl-basics {mlp,optimizers,rnn,cnn,seq2seq}                            (B9 DL_Basics notebooks)
@@ -453,6 +454,13 @@ def cmd_cache_gateway(a):
     uvicorn.run(app, host=a.host, port=a.port)
 
 
+def cmd_router(a):
+    """H2 LiteLLM proxy equivalent: model groups, routing strategy, retries, cooldown, fallbacks, guard."""
+    import uvicorn
+    from ..infer.router import Router, create_router_app
+    uvicorn.run(create_router_app(Router(a.config)), host=a.host, port=a.port)
+
+
 def cmd_lf(a):
     """``llamafactory-cli train|export|webchat <yaml>``."""
     from .llamafactory import lf_export, lf_train, load_lf_yaml
@@ -781,6 +789,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--api-key", dest="api_key", default=None)
     p.set_defaults(fn=cmd_guard)
 
+    p = sub.add_parser("router", help="LiteLLM-config model router: strategies, retries, cooldown, fallbacks (H2)")
+    p.add_argument("--config", required=True, help="LiteLLM proxy YAML (model_list / router_settings / guardrails)")
+    p.add_argument("--host", default="0.0.0.0")
+    p.add_argument("--port", type=int, default=4000)
+    p.set_defaults(fn=cmd_router)
     p = sub.add_parser("cache-gateway", help="exact + semantic response cache in front of a server (H6)")
     p.add_argument("--backend", required=True, help="upstream OpenAI-compatible base URL")
     p.add_argument("--api-key", dest="api_key", default=None)

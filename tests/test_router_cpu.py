@@ -1,0 +1,137 @@
+"""LiteLLM-semantics router gateway: strategies, retries, cooldown, fallbacks, guardrail."""
+import collections
+
+import pytest
+from fastapi.testclient import TestClient
+
+from llm_in_practise_amd.infer.router import Router, UpstreamError, create_router_app, load_config
+
+
+class Clock:
+    def __init__(self):
+        self.t = 1000.0
+
+    def __call__(self):
+        return self.t
+
+
+def cfg(strategy="simple-shuffle", **rs):
+    return {
+        "model_list": [
+            {"model_name": "qwen3-8b", "litellm_params": {"model": "openai/qwen3-8b", "api_base": "http://a/v1",
+                                                          "weight": 3, "input_cost_per_token": 2e-6}},
+            {"model_name": "qwen3-8b", "litellm_params": {"model": "openai/qwen3-8b", "api_base": "http://b/v1",
+                                                          "weight": 1, "input_cost_per_token": 1e-6}},
+            {"model_name": "r1-awq", "litellm_params": {"model": "openai/r1", "api_base": "http://c/v1"}},
+            {"model_name": "long-ctx", "litellm_params": {"model": "openai/long", "api_base": "http://d/v1"}},
+        ],
+        "router_settings": {"routing_strategy": strategy, "num_retries": 2,
+                            "retry_policy": {"RateLimitErrorRetries": 5, "InternalServerErrorRetries": 3,
+                                             "TimeoutErrorRetries": 4},
+                            "allowed_fails": 2, "cooldown_time": 120,
+                            "fallbacks": [{"r1-awq": ["qwen3-8b"]}],
+                            "context_window_fallbacks": [{"qwen3-8b": ["long-ctx"]}], **rs},
+    }
+
+
+def ok_sender(calls, fail=None):
+    def send(dep, path, body):
+        calls.append((dep.api_base, path, body["model"]))
+        if fail and dep.api_base in fail:
+            st = fail[dep.api_base]
+            raise UpstreamError(st, {"message": "maximum context length exceeded"} if st == 400 else "boom")
+        return {"choices": [{"message": {"content": f"hi from {dep.api_base}"}}], "model": body["model"]}
+    return send
+
+
+def test_weighted_shuffle_respects_weights():
+    calls = []
+    r = Router(cfg(), ok_sender(calls), seed=0)
+    for _ in range(400):
+        r.route("/chat/completions", {"model": "qwen3-8b", "messages": []})
+    c = collections.Counter(a for a, _, _ in calls)
+    assert 0.65 < c["http://a/v1"] / 400 < 0.85
+    assert calls[0][2] == "qwen3-8b"          # openai/ prefix stripped for the upstream call
+
+
+def test_cost_and_least_busy_strategies():
+    calls = []
+    r = Router(cfg("cost-based-routing"), ok_sender(calls))
+    r.route("/chat/completions", {"model": "qwen3-8b"})
+    assert calls[-1][0] == "http://b/v1"
+    r = Router(cfg("least-busy"), ok_sender(calls), seed=0)
+    a = r.pick("qwen3-8b")
+    b = r.pick("qwen3-8b")
+    assert a is not b                          # second pick avoids the busy deployment
+
+
+def test_retry_then_cooldown_then_recover():
+    calls, clock = [], Clock()
+    r = Router(cfg("cost-based-routing"), ok_sender(calls, {"http://b/v1": 503}), clock=clock)
+    out = r.route("/chat/completions", {"model": "qwen3-8b"})
+    assert "http://a/v1" in out["choices"][0]["message"]["content"]       # retried on the other deployment
+    r.route("/chat/completions", {"model": "qwen3-8b"})                 # second failure on b → cooldown
+    b = [d for d in r.groups["qwen3-8b"] if d.api_base == "http://b/v1"][0]
+    assert b.cooldowns == 1 and b.cooldown_until == clock.t + 120
+    n = len(calls)
+    r.route("/chat/completions", {"model": "qwen3-8b"})
+    assert len(calls) == n + 1 and calls[-1][0] == "http://a/v1"          # b skipped while cooling down
+    clock.t += 121
+    r.send = ok_sender(calls)
+    r.route("/chat/completions", {"model": "qwen3-8b"})
+    assert calls[-1][0] == "http://b/v1"                                  # back after cooldown_time
+
+
+def test_rate_limit_budget_and_fallback_chain():
+    calls = []
+    r = Router(cfg(allowed_fails=100), ok_sender(calls, {"http://c/v1": 429}), seed=0)
+    out = r.route("/chat/completions", {"model": "r1-awq"})
+    assert out["model"] == "qwen3-8b"
+    assert sum(1 for a, _, _ in calls if a == "http://c/v1") == 6          # 1 try + 5 RateLimitErrorRetries
+    assert r.counters["fallbacks_total"] == 1
+    calls.clear()
+    r = Router(cfg(), ok_sender(calls, {"http://c/v1": 429}), seed=0)
+    assert r.route("/chat/completions", {"model": "r1-awq"})["model"] == "qwen3-8b"
+    assert sum(1 for a, _, _ in calls if a == "http://c/v1") == 2          # cooled down after allowed_fails
+
+
+def test_context_window_fallback_and_plain_400():
+    calls = []
+    r = Router(cfg(), ok_sender(calls, {"http://a/v1": 400, "http://b/v1": 400}), seed=0)
+    out = r.route("/chat/completions", {"model": "qwen3-8b"})
+    assert out["model"] == "long-ctx"
+    r2 = Router(cfg(), ok_sender([], {"http://c/v1": 400}), seed=0)
+    with pytest.raises(UpstreamError) as ei:                            # non-context 400 on r1 → context
+        r2.route("/chat/completions", {"model": "r1-awq"})                #   fallback map has no r1 entry
+    assert ei.value.status == 400
+
+
+def test_app_guardrail_models_metrics():
+    calls = []
+    c = cfg()
+    c["guardrails"] = [{"guardrail_name": "g", "litellm_params": {"guardrail": "openai_moderation",
+                                                                   "mode": "pre_call", "api_base": "http://guard/v1"}}]
+
+    def send(dep, path, body):
+        if path == "/moderations":
+            return {"results": [{"flagged": "bomb" in body["input"]}]}
+        return ok_sender(calls)(dep, path, body)
+    app = create_router_app(Router(c, send, seed=0))
+    cl = TestClient(app)
+    assert [m["id"] for m in cl.get("/v1/models").json()["data"]] == ["qwen3-8b", "r1-awq", "long-ctx"]
+    r = cl.post("/v1/chat/completions", json={"model": "qwen3-8b", "messages": [{"role": "user", "content": "hello"}]})
+    assert r.status_code == 200 and r.json()["model"] == "qwen3-8b"
+    r = cl.post("/v1/chat/completions", json={"model": "qwen3-8b", "messages": [{"role": "user", "content": "a bomb"}]})
+    assert r.status_code == 400 and r.json()["error"]["type"] == "guardrail_violation"
+    assert cl.post("/v1/completions", json={"model": "nope", "prompt": "x"}).status_code == 404
+    m = cl.get("/metrics").text
+    assert "lipa_router_guard_blocked_total 1" in m and 'lipa_router_deployment_requests_total{group="qwen3-8b"' in m
+    assert cl.get("/health").json()["status"] == "ok"
+
+
+def test_repo_litellm_config_loads():
+    import os
+    path = os.path.join(os.path.dirname(__file__), "..", "deploy", "litellm", "config.yaml")
+    r = Router(load_config(path), ok_sender([]))
+    assert r.strategy == "least-busy" and len(r.groups["qwen3-8b"]) == 2
+    assert r.fallbacks == {"deepseek-r1-qwen3-8b-awq": ["qwen3-8b"]} and r.guards
