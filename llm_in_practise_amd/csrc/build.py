@@ -115,14 +115,45 @@ def build_cpu_extension(verbose: bool = True):
     return importlib.import_module("llm_in_practise_amd._cpu")
 
 
+def build_sanitizer_harness(kind: str = "address") -> str:
+    """Build ``tests/native/sanitize_host.cpp`` (the host runtime sources without bindings) as an
+    executable under ``-fsanitize=address,undefined`` (``kind="address"``) or ``-fsanitize=thread``.
+    Host code only: GPU sanitizers / XNACK are not available on the MI355X pool.  Returns the path;
+    rebuilt only when a source is newer than the binary."""
+    inc, libs, abi = _torch_flags()
+    src = os.path.join(ROOT, "tests", "native", "sanitize_host.cpp")
+    deps = [src] + sorted(glob.glob(os.path.join(HERE, "cpu", "*.cpp")))
+    san = {"address": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer"],
+           "thread": ["-fsanitize=thread"]}[kind]
+    os.makedirs(BUILD, exist_ok=True)
+    out = os.path.join(BUILD, f"sanitize_host_{kind}")
+    if os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
+        return out
+    lib_dirs = [p for p in libs if "rocm" not in p]
+    # no OpenMP here: libgomp is not TSan-instrumented, so the OMP pragmas compile to serial loops
+    cmd = ["g++", "-O1", "-g", "-std=c++17", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_API_INCLUDE_EXTENSION_H",
+           "-DTORCH_EXTENSION_NAME=_sanitize", f"-I{sysconfig.get_paths()['include']}", "-Wno-unknown-pragmas"]
+    cmd += san + [f"-I{p}" for p in inc] + [src, "-o", out + ".tmp"]
+    cmd += [f"-L{p}" for p in lib_dirs] + [f"-Wl,-rpath,{p}" for p in lib_dirs]
+    cmd += ["-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", f"-L{sysconfig.get_config_var('LIBDIR')}",
+            f"-lpython{sysconfig.get_python_version()}", "-lpthread"]
+    _run(cmd)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--hip", action="store_true")
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--clean", action="store_true")
+    ap.add_argument("--sanitize", choices=["address", "thread"], help="build + run the host sanitizer harness")
     a = ap.parse_args(argv)
     if a.clean:
         shutil.rmtree(BUILD, ignore_errors=True)
+    if a.sanitize:
+        exe = build_sanitizer_harness(a.sanitize)
+        return subprocess.call([exe])
     both = not (a.hip or a.cpu)
     if a.hip or both:
         build_hip_extension()

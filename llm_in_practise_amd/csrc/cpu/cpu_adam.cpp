@@ -59,6 +59,7 @@ double sum_squares(torch::Tensor g) {
 
 }  // namespace
 
+#ifndef LIPA_SANITIZER_HARNESS  // tests/native/sanitize_host.cpp includes this file without the bindings
 void register_loader(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -70,3 +71,4 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sum_squares", &sum_squares);
   register_loader(m);
 }
+#endif  // LIPA_SANITIZER_HARNESS

@@ -153,6 +153,7 @@ class TokenBlockLoader {
 
 }  // namespace
 
+#ifndef LIPA_SANITIZER_HARNESS
 void register_loader(pybind11::module& m) {
   pybind11::class_<TokenBlockLoader>(m, "TokenBlockLoader")
       .def(pybind11::init<torch::Tensor, int64_t, int64_t, int64_t, int64_t, uint64_t, bool, int64_t, bool>(),
@@ -165,3 +166,4 @@ void register_loader(pybind11::module& m) {
       .def_property_readonly("steps_per_epoch", &TokenBlockLoader::steps_per_epoch)
       .def_property_readonly("num_blocks", &TokenBlockLoader::num_blocks);
 }
+#endif  // LIPA_SANITIZER_HARNESS
