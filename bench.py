@@ -121,6 +121,7 @@ def main():
     data = torch.randint(0, cfg.vocab_size, (n_batches, args.micro_batch, args.seq_len), device=device,
                          generator=gen)
     it = [0]
+    spent = [None]
 
     def step():
         if engine is not None:      # ZeRO-3: reduce-scatter / optimizer partition / clip inside step()
@@ -128,15 +129,23 @@ def main():
             it[0] += args.grad_accum
             out = engine.module(ids, labels=ids, num_micro_batches=args.grad_accum if args.ga_fusion else 1)
             engine.backward(out.loss)
+            loss = out.loss.detach()
+            del out                 # tear the autograd graph down while the GPU still runs the backward
             engine.step()
-            return out.loss
+            return loss
         if args.ga_fusion:
             # the GA micro-batches are independent given the (frozen-during-the-step) weights:
             # run them as one pass with per-micro-batch loss normalisation (same gradient)
             ids = torch.cat([data[(it[0] + g) % n_batches] for g in range(args.grad_accum)])
             it[0] += args.grad_accum
             out = model(ids, labels=ids, num_micro_batches=args.grad_accum)
+            # the previous step's spent autograd graph (~2k nodes) is torn down here, while this
+            # forward is queued on the GPU; released at `loss = step()` the teardown left the GPU
+            # idle ~0.9 ms per step (profiles/bench_qwen3_8b_qlora_step_timeline_v12.txt)
+            spent[0] = None
             out.loss.backward()
+            loss = out.loss.detach()
+            spent[0] = out
         else:
             for micro in range(args.grad_accum):
                 ids = data[it[0] % n_batches]
@@ -145,12 +154,14 @@ def main():
                 with ctx:
                     out = model(ids, labels=ids)
                     (out.loss / args.grad_accum).backward()
+                loss = out.loss.detach()
+                del out
         ddp.allreduce_grads()
         opt.clip_grad_norm_(1.0)
         opt.step()
         sched.step()
         opt.zero_grad()
-        return out.loss
+        return loss
 
     def sync():
         if device.type == "cuda":
