@@ -449,6 +449,9 @@ class Trainer:
             if fused:
                 cat = {k: torch.cat([b[k] for b in batches]) for k in batches[0]}
                 loss = self.compute_loss(self.model, cat, num_micro_batches=len(batches))
+                # drop the previous step's spent autograd graph while this forward is queued on the
+                # GPU (freed at return, its teardown stalled the launch queue before the optimizer)
+                self._spent_graph = None
                 poison = self.faults.check(self.state.global_step + 1) if self.faults else None
                 if poison == "nan":
                     loss = loss * float("nan")
@@ -457,6 +460,7 @@ class Trainer:
                     self.engine.backward(loss)
                 else:
                     loss.backward()
+                self._spent_graph = loss
                 return loss.detach()
             total = 0.0
             for i, b in enumerate(batches):
@@ -580,6 +584,7 @@ class Trainer:
         if log_n:
             tr_loss_sum += float(log_loss)
             tr_loss_n += log_n
+        self._spent_graph = None
         if a.load_best_model_at_end and self.state.best_model_checkpoint:
             self._load_weights_only(self.state.best_model_checkpoint)
         runtime = time.perf_counter() - step_t0
