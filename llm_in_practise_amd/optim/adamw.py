@@ -54,6 +54,7 @@ class FlatParams:
             p.grad = self.grad[o:o + k].view_as(p) if p.dtype == torch.float32 else None
             p._lipa_flat_grad = p.dtype == torch.float32   # kernels may accumulate into p.grad in place
         self.mixed = self.low is not None
+        self.grad_ptrs = [self.grad[o:o + p.numel()].data_ptr() for p, o in zip(self.params, self.offsets)]
         # bf16 shadows of fp32 params (LoRA adapters): refreshed by the update kernel itself,
         # consumed by the fused GEMMs — no per-forward fp32→bf16 conversion kernels
         self.shadow = None
@@ -65,14 +66,14 @@ class FlatParams:
     def sync_grads(self):
         """Copy grads that autograd allocated separately (low-precision params) into the flat
         buffer.  fp32 params accumulate straight into their views."""
-        for p, o in zip(self.params, self.offsets):
-            k = p.numel()
-            if p.grad is None:
+        # pointer compare only: slicing a view of the flat buffer per parameter cost ~3 us each
+        # (0.2-0.4 ms of host time per step with 144 LoRA tensors, visible as GPU idle)
+        for p, o, ptr in zip(self.params, self.offsets, self.grad_ptrs):
+            g = p.grad
+            if g is None or g.data_ptr() == ptr:
                 continue
-            flat = self.grad[o:o + k]
-            if p.grad.data_ptr() != flat.data_ptr():
-                flat.add_(p.grad.reshape(-1).float())
-                p.grad = None
+            self.grad[o:o + p.numel()].add_(g.reshape(-1).float())
+            p.grad = None
 
     def zero_grad(self):
         self.grad.zero_()
