@@ -10,7 +10,8 @@
 Dataset: ``--dataset mixed`` = 70 % short chat / 30 % long RAG-style prompts (synthetic text,
 no network), or a ShareGPT-format JSON file.  Metrics per concurrency (streamed requests):
 mean / p99 TTFT, mean / p99 ITL, request throughput, output tokens/s — the columns of the
-reference's results table (``README.md:1504-1511``).  Token counts use streamed deltas (one
+reference's results table (``README.md:1504-1511``) — plus per-request tokens/s (mean / p50), the
+custom event of the reference's ``Deployment/Ray/scripts/locustfile-TPS.py:21-41``.  Token counts use streamed deltas (one
 delta ≈ one token for the OpenAI stream), or the server's ``usage`` when not streaming.
 """
 import argparse
@@ -97,11 +98,15 @@ async def run_level(url, model, prompts, conc, max_tokens):
     ttft = [r["ttft"] * 1e3 for r in res]
     itl = [x * 1e3 for r in res for x in r["itl"]]
     toks = sum(r["out_tokens"] for r in res)
+    # the reference's locustfile-TPS.py custom event: per-request output tokens / end-to-end latency
+    per_req = [r["out_tokens"] / r["e2e"] for r in res if r["e2e"] > 0]
     return {"concurrency": conc, "requests": len(res), "duration_s": round(dur, 3),
             "mean_ttft_ms": round(statistics.mean(ttft), 2), "p99_ttft_ms": round(pct(ttft, 99), 2),
             "mean_itl_ms": round(statistics.mean(itl), 2) if itl else None,
             "p99_itl_ms": round(pct(itl, 99), 2) if itl else None,
-            "req_per_s": round(len(res) / dur, 3), "output_tok_per_s": round(toks / dur, 1)}
+            "req_per_s": round(len(res) / dur, 3), "output_tok_per_s": round(toks / dur, 1),
+            "mean_request_tok_per_s": round(statistics.mean(per_req), 2) if per_req else None,
+            "p50_request_tok_per_s": round(statistics.median(per_req), 2) if per_req else None}
 
 
 class _SyntheticTokenizer:
