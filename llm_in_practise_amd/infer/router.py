@@ -19,6 +19,8 @@ and implements the routing behaviour in front of per-GPU ``lipa serve`` processe
   cooled down for ``cooldown_time`` seconds and skipped;
 * when a group is exhausted the ``fallbacks`` list for it is tried in order; a 400 whose message
   mentions the context length switches to ``context_window_fallbacks``;
+* ``max_parallel_requests`` per deployment caps its in-flight requests (the role of Ray Serve's
+  ``max_ongoing_requests: 64``); a group whose deployments are all at the cap answers 429;
 * ``pre_call`` moderation guardrails POST the prompt to ``<api_base>/moderations`` and reject
   flagged requests with 400 before any model is called;
 * ``/v1/models``, ``/health``, ``/metrics`` (Prometheus text: per-deployment requests / failures /
@@ -53,6 +55,7 @@ class Deployment:
     api_key: str | None = None
     weight: float = 1.0
     rpm: int | None = None
+    max_parallel: int | None = None  # ``max_parallel_requests`` (Ray Serve's ``max_ongoing_requests`` role)
     cost: float = 0.0
     in_flight: int = 0
     latency_ewma: float = 0.0
@@ -125,6 +128,7 @@ class Router:
                 group=m["model_name"], model=model.split("/", 1)[1] if model.startswith("openai/") else model,
                 api_base=lp.get("api_base", ""), api_key=lp.get("api_key"),
                 weight=float(lp.get("weight", lp.get("rpm", 1) or 1)), rpm=lp.get("rpm"),
+                max_parallel=lp.get("max_parallel_requests", m.get("max_parallel_requests")),
                 cost=float(lp.get("input_cost_per_token", 0) or 0) + float(lp.get("output_cost_per_token", 0) or 0)))
         self.send = send or http_sender()
         self.clock = clock
@@ -147,8 +151,11 @@ class Router:
 
     def pick(self, group: str, exclude: set[str] = frozenset()) -> Deployment | None:
         with self.lock:
-            cands = [d for d in self._healthy(group) if d.name not in exclude] or self._healthy(group)
+            healthy = [d for d in self._healthy(group) if d.max_parallel is None or d.in_flight < d.max_parallel]
+            cands = [d for d in healthy if d.name not in exclude] or healthy
             if not cands:
+                if self._healthy(group):            # every deployment is at max_parallel_requests
+                    raise UpstreamError(429, f"all deployments of {group!r} are at max_parallel_requests")
                 return None
             minute = int(self.clock() // 60)
             if self.strategy == "least-busy":

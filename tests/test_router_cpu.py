@@ -135,3 +135,17 @@ def test_repo_litellm_config_loads():
     r = Router(load_config(path), ok_sender([]))
     assert r.strategy == "least-busy" and len(r.groups["qwen3-8b"]) == 2
     assert r.fallbacks == {"deepseek-r1-qwen3-8b-awq": ["qwen3-8b"]} and r.guards
+
+
+def test_max_parallel_requests_caps_in_flight():
+    c = cfg("least-busy")
+    for m in c["model_list"][:2]:
+        m["litellm_params"]["max_parallel_requests"] = 1
+    r = Router(c, ok_sender([]), seed=0)
+    a, b = r.pick("qwen3-8b"), r.pick("qwen3-8b")
+    assert {a.api_base, b.api_base} == {"http://a/v1", "http://b/v1"}
+    with pytest.raises(UpstreamError) as ei:
+        r.pick("qwen3-8b")
+    assert ei.value.status == 429
+    r._done(a, True, 0.01)
+    assert r.pick("qwen3-8b") is a
