@@ -7,6 +7,7 @@ The reference teaches these in notebooks; here they are importable, tested modul
 * :mod:`.numpy_rnn`  — manual RNN / LSTM / GRU forward passes and BPTT in PyTorch's gate layout
   (checked against ``torch.nn.RNN/LSTM/GRU`` and autograd);
 * :mod:`.numpy_cnn`  — conv2d / max-pool forward + backward (sliding-window einsum), LeNet-5;
+* :mod:`.embeddings` — random / GloVe-initialised ``nn.Embedding`` (frozen or trainable);
 * :mod:`.seq2seq`    — GRU encoder / Bahdanau-attention decoder with teacher forcing and greedy
   decoding, plus the variable-length ``pad_collate`` used with ``DataLoader``.
 """

@@ -164,3 +164,14 @@ def test_cli_dl_basics(demo, capsys):
     from llm_in_practise_amd.cli.main import main
     main(["dl-basics", demo, "--epochs", "3"])
     assert '"demo"' in capsys.readouterr().out
+
+
+def test_glove_embedding(tmp_path):
+    from llm_in_practise_amd.dl_basics.embeddings import build_embedding
+    p = tmp_path / "glove.txt"
+    p.write_text("the 0.1 0.2 0.3\ncat -1 0.5 2\nbad 1 2\nzebra 9 9 9\n")
+    vocab = {"<pad>": 0, "the": 1, "cat": 2, "dog": 3}
+    emb, n = build_embedding(vocab, 3, str(p), freeze=True)
+    assert n == 2 and emb.weight.shape == (4, 3) and not emb.weight.requires_grad
+    assert torch.allclose(emb.weight[2], torch.tensor([-1.0, 0.5, 2.0]))
+    assert torch.all(emb.weight[0] == 0) and emb.weight[3].abs().sum() > 0
