@@ -43,6 +43,24 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _self_launch(n: int) -> int:
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
+
+
 def build(args, device):
     cfg = qwen3_config(args.model)
     t0 = time.time()
@@ -92,7 +110,13 @@ def main():
                          "normalisation, identical gradient); 0: sequential micro-steps")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` without a launcher: start N ranks under torch.distributed.run
+        # as a CHILD process (nothing here has touched the GPU yet; never exec) and exit with its code
+        sys.exit(_self_launch(args.gpus))
     rank, local_rank, world = D.init_distributed()
+    if world != args.gpus:
+        raise SystemExit(f"[bench] --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     device = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
     cfg, model = build(args, device)
     total_steps = args.warmup + args.steps
@@ -182,7 +206,7 @@ def main():
     ms = 1000 * elapsed / max(1, args.steps)
     tokens = args.micro_batch * args.seq_len * args.grad_accum * world * args.steps
     tps = tokens / elapsed
-    fl_per_tok = 6 * 0  # filled below
+    nonpad_frac = 1.0                # random ids: no pad token, every label position counts
     lin = cfg.num_params() - cfg.vocab_size * cfg.hidden_size * (1 if cfg.tie_word_embeddings else 2)
     head = cfg.vocab_size * cfg.hidden_size
     # fwd 2·(linear+head) + bwd dX 2·(linear+head); no weight grads for the frozen base
@@ -219,6 +243,12 @@ def main():
                 "ga_execution": "fused-pass" if args.ga_fusion else "sequential",
                 "weights": "random-init",
                 "peak_hbm_gib": round(mem, 1),
+                "dist_backend": (torch.distributed.get_backend() if D.is_dist() else "none"),
+                "dist_world_size": D.world_size(),
+                # padded = micro x 512 x GA x world / step; non-pad counts only label != -100 positions
+                # (synthetic ids carry no padding, so the two agree here)
+                "tokens_per_s_padded": round(tps, 1),
+                "tokens_per_s_nonpad": round(tps * nonpad_frac, 1),
             },
         }
         print(json.dumps(rec), flush=True)

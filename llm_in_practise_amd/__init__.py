@@ -12,6 +12,13 @@ Layers:
   infer/     KV-cache generation, sampling, OpenAI-compatible server, moderation (L8)
 """
 
-__version__ = "0.1.0"
+__version__ = "0.2.0"
+
+import os as _os
+
+# RCCL / CUDA-tensor IPC on this ROCm image only works through dmabuf: the legacy IPC path must be
+# off BEFORE the first HIP call of the process (HIP reads it at runtime init), so it is set at
+# package import rather than next to init_process_group.
+_os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 from .runtime.device import get_device, is_gfx950  # noqa: F401

@@ -154,7 +154,8 @@ def cmd_lm_train(a, strategy="single"):
                      precision=a.precision, scheduler=a.scheduler, step_per_batch=a.step_per_batch,
                      save_dir=a.save_dir, keep_last=a.keep_last, final_model=a.final_model, seed=a.seed,
                      max_steps=a.max_steps, grad_accum=a.grad_accum, patience=a.patience, best_model=a.best_model,
-                     resume=a.resume, eval_every_epoch=a.val_fraction > 0)
+                     resume=a.resume, eval_every_epoch=a.val_fraction > 0,
+                     no_decay_groups=getattr(a, "no_decay_groups", False))
     eval_ds = None
     if a.val_fraction > 0:       # temp/ddp_gpt_bpe_tokenizer_02.py:262-300: seeded random_split
         n_val = max(1, int(len(ds) * a.val_fraction))
@@ -615,6 +616,8 @@ def _lm_args(p):
     p.add_argument("--block_size", type=int, default=256)
     p.add_argument("--lr", type=float, default=3e-4)
     p.add_argument("--weight_decay", type=float, default=0.01)
+    p.add_argument("--no_decay_groups", action="store_true",
+                   help="AdamW decay / no-decay param groups (biases, LayerNorm) as temp/ddp_gpt_wikitext2.py:337-344")
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--n_layer", type=int, default=6)
     p.add_argument("--n_head", type=int, default=8)

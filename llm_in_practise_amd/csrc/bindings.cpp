@@ -47,10 +47,11 @@ void launch_gemm_skinny(const void*, int, const void*, const void*, void*, float
 void set_dequant_variant(int);
 void launch_nf4_dequant(const uint8_t*, const float*, const uint8_t*, const float*, const float*, const float*, void*,
                         size_t, hipStream_t);
-void launch_attn_fwd(const void*, const void*, const void*, int, int, int, const int*, void*, float*, int, int, int,
-                     int, int, int, float, hipStream_t);
+void launch_attn_fwd(const void*, const void*, const void*, int, int, int, const int*, const int*, void*, float*, int,
+                     int, int, int, int, int, int, int, float, float, uint64_t, hipStream_t);
 void launch_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const int*, int,
-                     int, int, void*, void*, void*, float*, int, int, int, int, int, int, float, hipStream_t);
+                     int, int, void*, void*, void*, float*, int, int, int, int, int, int, float, float, uint64_t,
+                     hipStream_t);
 
 void launch_gemm_int4_any(const void*, int, const uint32_t*, const float*, const float*, const void*, const void*, int,
                       const void*, void*, int, int, int, hipStream_t);
@@ -494,32 +495,62 @@ Tensor gemm_bf16_t(Tensor dy, Tensor w, optional<Tensor> ext_a, optional<Tensor>
 }
 
 // ------------------------------------------------------------------ attention
+static const int* int_ptr(const optional<Tensor>& t, Tensor& keep) {
+  if (!t || !t->defined()) return nullptr;
+  keep = t->to(at::kInt).contiguous();
+  return keep.data_ptr<int>();
+}
+
+// host-side operand checks for the attention kernels: 16-B vector loads of head rows
+static void attn_check(const Tensor& t, int64_t rows, int64_t heads, int64_t d, const char* name) {
+  CHECK_BF16(t);
+  TORCH_CHECK(t.dim() == 2 && t.stride(-1) == 1, "attn: ", name, " must be 2-D with unit inner stride");
+  TORCH_CHECK(t.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "attn: ", name,
+              " rows must be 16-byte aligned");
+  TORCH_CHECK(t.size(0) >= rows && t.size(1) >= heads * d, "attn: ", name, " too small for the launch shape");
+}
+
+// General forward: Sq queries per batch row (absolute positions q_offs[b] + i) over Skv keys stored
+// kv_rows rows apart per batch (a KV cache), optional per-batch key lengths.
+std::vector<Tensor> attn_fwd_ext(Tensor q, Tensor k, Tensor v, optional<Tensor> kv_lens, optional<Tensor> q_offs,
+                                 int64_t B, int64_t Sq, int64_t Skv, int64_t kv_rows, int64_t hq, int64_t hkv,
+                                 int64_t d, bool causal, double scale, double p_drop, int64_t seed) {
+  TORCH_CHECK(p_drop >= 0.0 && p_drop < 1.0, "attn: dropout probability in [0, 1)");
+  TORCH_CHECK(d == 32 || d == 64 || d == 96 || d == 128, "attn: head_dim in {32, 64, 96, 128}");
+  TORCH_CHECK(hkv > 0 && hq % hkv == 0, "attn: GQA group");
+  TORCH_CHECK(Sq > 0 && Skv > 0 && kv_rows >= Skv, "attn: shape");
+  attn_check(q, B * Sq, hq, d, "q");
+  attn_check(k, (B - 1) * kv_rows + Skv, hkv, d, "k");
+  attn_check(v, (B - 1) * kv_rows + Skv, hkv, d, "v");
+  auto o = at::empty({B * Sq, hq * d}, q.options());
+  auto lse = at::empty({B, hq, Sq}, q.options().dtype(at::kFloat));
+  Tensor k1, k2;
+  const int* kl = int_ptr(kv_lens, k1);
+  const int* qo = int_ptr(q_offs, k2);
+  launch_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0), v.stride(0), kl, qo,
+                  o.data_ptr(), lse.data_ptr<float>(), B, Sq, Skv, kv_rows, hq, hkv, d, causal, scale, p_drop,
+                  (uint64_t)seed, stream());
+  return {o, lse};
+}
+
 std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, optional<Tensor> kv_lens, int64_t B, int64_t S, int64_t hq,
                              int64_t hkv, int64_t d, bool causal, double scale) {
-  CHECK_BF16(q);
-  TORCH_CHECK(q.stride(-1) == 1 && k.stride(-1) == 1 && v.stride(-1) == 1, "attn: unit inner stride");
-  TORCH_CHECK(d == 64 || d == 128, "attn: head_dim 64 or 128");
-  TORCH_CHECK(hq % hkv == 0, "attn: GQA group");
-  auto o = at::empty({B * S, hq * d}, q.options());
-  auto lse = at::empty({B, hq, S}, q.options().dtype(at::kFloat));
-  const int* kl = nullptr;
-  Tensor klc;
-  if (kv_lens && kv_lens->defined()) {
-    klc = kv_lens->to(at::kInt).contiguous();
-    kl = klc.data_ptr<int>();
-  }
-  launch_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), k.stride(0), v.stride(0), kl, o.data_ptr(),
-                  lse.data_ptr<float>(), B, S, hq, hkv, d, causal, scale, stream());
-  return {o, lse};
+  return attn_fwd_ext(q, k, v, kv_lens, c10::nullopt, B, S, S, S, hq, hkv, d, causal, scale, 0.0, 0);
 }
 
 std::vector<Tensor> attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse,
                              optional<Tensor> kv_lens, int64_t B, int64_t S, int64_t hq, int64_t hkv, int64_t d,
-                             bool causal, double scale) {
+                             bool causal, double scale, double p_drop, int64_t seed) {
   auto dq = at::empty({B * S, hq * d}, q.options());
   auto dk = at::empty({B * S, hkv * d}, q.options());
   auto dv = at::empty({B * S, hkv * d}, q.options());
-  TORCH_CHECK(S % 64 == 0, "attn_bwd: seq_len must be a multiple of 64");
+  TORCH_CHECK(d == 32 || d == 64 || d == 96 || d == 128, "attn_bwd: head_dim in {32, 64, 96, 128}");
+  attn_check(q, B * S, hq, d, "q");
+  attn_check(k, B * S, hkv, d, "k");
+  attn_check(v, B * S, hkv, d, "v");
+  attn_check(o, B * S, hq, d, "o");
+  attn_check(dout, B * S, hq, d, "dout");
+  TORCH_CHECK(dout.stride(0) == hq * d && o.stride(0) == hq * d, "attn_bwd: o / dout must be dense [T, hq*d]");
   auto delta = at::empty({B, hq, S}, q.options().dtype(at::kFloat));
   const int* kl = nullptr;
   Tensor klc;
@@ -529,7 +560,7 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o
   }
   launch_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), kl,
                   q.stride(0), k.stride(0), v.stride(0), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
-                  delta.data_ptr<float>(), B, S, hq, hkv, d, causal, scale, stream());
+                  delta.data_ptr<float>(), B, S, hq, hkv, d, causal, scale, p_drop, (uint64_t)seed, stream());
   return {dq, dk, dv};
 }
 
@@ -803,5 +834,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_bf16", &gemm_bf16);
   m.def("gemm_bf16_t", &gemm_bf16_t);
   m.def("attn_fwd", &attn_fwd);
+  m.def("attn_fwd_ext", &attn_fwd_ext);
   m.def("attn_bwd", &attn_bwd);
 }

@@ -40,6 +40,28 @@ constexpr float LOG2E = 1.4426950408889634f;
 // probability is harmless)
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// Attention-probability dropout (the teaching models' nn.MultiheadAttention(dropout=p)): a
+// counter-based keep bit per (batch·head, query, key), regenerated identically by the forward and
+// both backward kernels, never stored.  keep ⇔ hash ≥ thresh (thresh = p·2³²); kept P is scaled by
+// rinv = 1/(1-p).  The row normaliser l and the backward's delta = rowsum(dO∘O) use the
+// un-dropped P, as in FlashAttention-2.
+__device__ __forceinline__ uint32_t drop_hash(uint32_t s0, uint32_t s1, uint32_t bh, uint32_t q, uint32_t k) {
+  uint32_t x = s0 ^ (bh * 0x9E3779B9u);
+  x ^= q * 0x85EBCA6Bu + s1;
+  x ^= k * 0xC2B2AE35u;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+struct DropParams {
+  uint32_t s0, s1, thresh;  // thresh == 0: no dropout
+  float rinv;
+};
+
 // Grid (n0, n1, n2) → logical block (i0, i1, i2) with consecutive logical blocks (i0 fastest)
 // on the same XCD, so the blocks that re-read one (batch, kv-head)'s K/V (or Q/dO) share its L2.
 __device__ __forceinline__ void xcd_grid3(int& i0, int& i1, int& i2) {
@@ -52,12 +74,18 @@ __device__ __forceinline__ void xcd_grid3(int& i0, int& i1, int& i2) {
 }
 
 // ============================================================================ forward
+// Sq queries per batch row attend to Skv keys (K/V rows of batch b start at b·kv_rows: a KV cache
+// may be allocated longer than it is filled).  Query i of batch b sits at absolute position
+// q_offs[b] + i (0 without q_offs): chunked / prefix-cache suffix prefill is the same kernel with
+// the causal limit key ≤ q_off + i.  kv_lens[b] (optional) masks keys ≥ kv_lens[b] (right padding,
+// BERT key-padding masks, the filled part of a cache).
 template <int D>
 __global__ __launch_bounds__(256) void attn_fwd_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                   const bf16* __restrict__ V, int ldq, int ldk, int ldv,
-                                                  const int* __restrict__ kv_lens, bf16* __restrict__ O,
-                                                  float* __restrict__ lse, int S, int hq, int hkv, int causal,
-                                                  float scale_log2) {
+                                                  const int* __restrict__ kv_lens, const int* __restrict__ q_offs,
+                                                  bf16* __restrict__ O, float* __restrict__ lse, int Sq, int Skv,
+                                                  int kv_rows, int hq, int hkv, int causal, float scale_log2,
+                                                  DropParams dp) {
   constexpr int LDR = D + 8;        // padded LDS row (elements)
   constexpr int CH = D / 8;         // 16-B chunks per row
   constexpr int TILE = 64 * LDR;    // elements per K or V tile
@@ -66,28 +94,30 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16* __restrict__ Q, co
   constexpr int LOADS = 64 * CH / 256;
   __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // K0 V0 K1 V1
 
-  const int nqb = (S + 127) / 128;
+  const int nqb = (Sq + 127) / 128;
   int i0, h, b;
   xcd_grid3(i0, h, b);
   const int qb = nqb - 1 - i0;  // heavy (late, causal) blocks first
   const int hk = h / (hq / hkv);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   const int q0 = qb * 128 + 32 * w;
-  const int kvlen = kv_lens ? kv_lens[b] : S;
-  const size_t tok0 = (size_t)b * S;
+  const int qoff = q_offs ? q_offs[b] : 0;
+  const int kvlen = min(kv_lens ? kv_lens[b] : Skv, Skv);
+  const size_t tok0 = (size_t)b * Sq;          // query / output rows
+  const size_t ktok0 = (size_t)b * kv_rows;     // key / value rows
 
   // Q fragments (B operand of Sᵀ = K·Qᵀ): Q[q0 + 16qt + li][32s + 8g + j]
   bf16x8 qf[2][NS];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     int q = q0 + 16 * qt + li;
-    q = q < S ? q : S - 1;
+    q = q < Sq ? q : Sq - 1;
 #pragma unroll
     for (int s = 0; s < NS; ++s)
       qf[qt][s] = *reinterpret_cast<const bf16x8*>(Q + (tok0 + q) * ldq + h * D + 32 * s + 8 * g);
   }
 
-  int kend = causal ? min(S, qb * 128 + 128) : S;
+  int kend = causal ? min(Skv, qoff + qb * 128 + 128) : Skv;
   kend = min(kend, kvlen);
   const int nt = (kend + 63) / 64;
 
@@ -103,9 +133,9 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16* __restrict__ Q, co
       const int ci = p * 256 + threadIdx.x;
       const int row = ci / CH, ch = ci % CH;
       int key = t * 64 + row;
-      key = key < S ? key : S - 1;
-      kr[p] = *reinterpret_cast<const bf16x8*>(K + (tok0 + key) * ldk + hk * D + ch * 8);
-      vr[p] = *reinterpret_cast<const bf16x8*>(V + (tok0 + key) * ldv + hk * D + ch * 8);
+      key = key < Skv ? key : Skv - 1;
+      kr[p] = *reinterpret_cast<const bf16x8*>(K + (ktok0 + key) * ldk + hk * D + ch * 8);
+      vr[p] = *reinterpret_cast<const bf16x8*>(V + (ktok0 + key) * ldv + hk * D + ch * 8);
     }
   };
   auto store_tile = [&](int buf) {
@@ -141,12 +171,12 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16* __restrict__ Q, co
       }
     }
     // ---- masks + online softmax (lane owns query q0 + 16qt + li; keys k0 + 16kt + 4g + r)
-    const bool need_mask = (causal && k0 + 63 > q0) || (k0 + 64 > kvlen);
+    const bool need_mask = (causal && k0 + 63 > qoff + q0) || (k0 + 64 > kvlen);
     bf16x8 pf[2][2];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       const int qa = q0 + 16 * qt + li;
-      const int klim = min(causal ? qa : S, kvlen - 1);  // last key this query may see
+      const int klim = min(causal ? qoff + qa : Skv, kvlen - 1);  // last key this query may see
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
@@ -182,6 +212,15 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16* __restrict__ Q, co
       m_run[qt] = mn;
 #pragma unroll
       for (int dt = 0; dt < ND; ++dt) acc[dt][qt] *= alpha;
+      if (dp.thresh) {
+        const uint32_t bh = (uint32_t)(b * hq + h);
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            sc[kt][qt][r] = drop_hash(dp.s0, dp.s1, bh, qa, k0 + 16 * kt + 4 * g + r) >= dp.thresh
+                                ? sc[kt][qt][r] * dp.rinv : 0.f;
+      }
       // P as B operand, permuted key order j ↔ 32kb + 16(j>>2) + 4g + (j&3)
       pf[qt][0] = f2b8(sc[0][qt], sc[1][qt]);
       pf[qt][1] = f2b8(sc[2][qt], sc[3][qt]);
@@ -203,7 +242,7 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16* __restrict__ Q, co
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int q = q0 + 16 * qt + li;
-    if (q >= S) continue;
+    if (q >= Sq) continue;
     const float inv = l_run[qt] > 0.f ? 1.f / l_run[qt] : 0.f;
 #pragma unroll
     for (int dt = 0; dt < ND; ++dt) {
@@ -213,7 +252,7 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16* __restrict__ Q, co
       *reinterpret_cast<bf16x4*>(O + (tok0 + q) * (size_t)(hq * D) + h * D + 16 * dt + 4 * g) = o;
     }
     if (g == 0)
-      lse[((size_t)b * hq + h) * S + q] =
+      lse[((size_t)b * hq + h) * Sq + q] =
           l_run[qt] > 0.f ? (m_run[qt] + log2f(l_run[qt])) * 0.6931471805599453f : INFINITY;
   }
 }
@@ -234,20 +273,22 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16* __restrict__ dO
                                                      const bf16* __restrict__ V, const float* __restrict__ lse,
                                                      float* __restrict__ delta, const int* __restrict__ kv_lens,
                                                      int ldq, int ldk, int ldv, bf16* __restrict__ dQ, int S, int hq,
-                                                     int hkv, int causal, float scale, float scale_log2) {
+                                                     int hkv, int causal, float scale, float scale_log2,
+                                                     DropParams drp) {
   constexpr int LDR = D + 8, CH = D / 8, TILE = 64 * LDR, NS = D / 32, ND = D / 16;
   constexpr int LOADS = 64 * CH / 256;
   __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // K0 V0 K1 V1
 
-  const int nqb = S / 64;
+  const int nqb = (S + 63) / 64;
   int i0, h, b;
   xcd_grid3(i0, h, b);
   const int qb = nqb - 1 - i0;  // heavy (late, causal) blocks first
   const int hk = h / (hq / hkv);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   const int q0 = qb * 64;
-  const int qa = q0 + 16 * w + li;  // this lane's query
-  const int kvlen = kv_lens ? kv_lens[b] : S;
+  const int qa = q0 + 16 * w + li;  // this lane's query (>= S in a tail tile: computed, never stored)
+  const int qc = qa < S ? qa : S - 1;
+  const int kvlen = min(kv_lens ? kv_lens[b] : S, S);
   const size_t tok0 = (size_t)b * S;
   const size_t ldo = (size_t)hq * D;
 
@@ -255,8 +296,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16* __restrict__ dO
   float dsum = 0.f;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    const size_t off = (tok0 + qa) * ldo + h * D + 32 * s + 8 * g;
-    qf[s] = *reinterpret_cast<const bf16x8*>(Q + (tok0 + qa) * ldq + h * D + 32 * s + 8 * g);
+    const size_t off = (tok0 + qc) * ldo + h * D + 32 * s + 8 * g;
+    qf[s] = *reinterpret_cast<const bf16x8*>(Q + (tok0 + qc) * ldq + h * D + 32 * s + 8 * g);
     dof[s] = *reinterpret_cast<const bf16x8*>(dO + off);
     const bf16x8 of = *reinterpret_cast<const bf16x8*>(O + off);
 #pragma unroll
@@ -265,8 +306,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16* __restrict__ dO
   dsum += __shfl_xor(dsum, 16, 64);
   dsum += __shfl_xor(dsum, 32, 64);
   const size_t bh = ((size_t)b * hq + h) * S;
-  if (g == 0) delta[bh + qa] = dsum;
-  const float lse2 = lse[bh + qa] * LOG2E;
+  if (g == 0 && qa < S) delta[bh + qa] = dsum;
+  const float lse2 = lse[bh + qc] * LOG2E;
   const int klim = min(causal ? qa : S, kvlen - 1);  // last key this query may see
 
   int kend = causal ? min(S, q0 + 64) : S;
@@ -283,7 +324,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16* __restrict__ dO
     for (int p = 0; p < LOADS; ++p) {
       const int ci = p * 256 + threadIdx.x;
       const int row = ci / CH, ch = ci % CH;
-      const size_t key = tok0 + t * 64 + row;
+      const size_t key = tok0 + min(t * 64 + row, S - 1);
       kr[p] = *reinterpret_cast<const bf16x8*>(K + key * ldk + hk * D + ch * 8);
       vr[p] = *reinterpret_cast<const bf16x8*>(V + key * ldv + hk * D + ch * 8);
     }
@@ -332,6 +373,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16* __restrict__ dO
 #pragma unroll
         for (int r = 0; r < 4; ++r) sc[kt][r] = (k0 + 16 * kt + 4 * g + r <= klim) ? sc[kt][r] : 0.f;
     }
+    if (drp.thresh) {   // dP = M∘dP_drop/(1-p)
+      const uint32_t bh = (uint32_t)(b * hq + h);
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          dp[kt][r] = drop_hash(drp.s0, drp.s1, bh, qa, k0 + 16 * kt + 4 * g + r) >= drp.thresh ? dp[kt][r] * drp.rinv
+                                                                                              : 0.f;
+    }
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
@@ -349,6 +399,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16* __restrict__ dO
     }
   }
   // ---- dQ[q][16dt + 4g + r] = scale · acc
+  if (qa >= S) return;
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt) {
     bf16x4 o;
@@ -366,7 +417,8 @@ __global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __res
                                                       const float* __restrict__ lse, const float* __restrict__ delta,
                                                       const int* __restrict__ kv_lens, int ldq, int ldk, int ldv,
                                                       bf16* __restrict__ dK, bf16* __restrict__ dV, int S, int hq,
-                                                      int hkv, int causal, float scale, float scale_log2) {
+                                                      int hkv, int causal, float scale, float scale_log2,
+                                                      DropParams drp) {
   constexpr int LDR = D + 8, CH = D / 8, TILE = 64 * LDR, NS = D / 32, ND = D / 16;
   constexpr int LOADS = 64 * CH / 256;
   __shared__ __attribute__((aligned(16))) bf16 smem_all[HALVES * 4 * TILE];  // per half: Q0 dO0 Q1 dO1
@@ -382,15 +434,16 @@ __global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __res
   const int w = tid >> 6, lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
   const int kb0 = kbi * 64;
   const int kw = kb0 + 16 * w + li;  // this lane's key (column of the S / dP tiles)
-  const int kvlen = kv_lens ? kv_lens[b] : S;
+  const int kwc = kw < S ? kw : S - 1;
+  const int kvlen = min(kv_lens ? kv_lens[b] : S, S);
   const size_t tok0 = (size_t)b * S;
   const size_t ldo = (size_t)hq * D, ldkv = (size_t)hkv * D;
 
   bf16x8 kf[NS], vf[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    kf[s] = *reinterpret_cast<const bf16x8*>(K + (tok0 + kw) * ldk + hk * D + 32 * s + 8 * g);
-    vf[s] = *reinterpret_cast<const bf16x8*>(V + (tok0 + kw) * ldv + hk * D + 32 * s + 8 * g);
+    kf[s] = *reinterpret_cast<const bf16x8*>(K + (tok0 + kwc) * ldk + hk * D + 32 * s + 8 * g);
+    vf[s] = *reinterpret_cast<const bf16x8*>(V + (tok0 + kwc) * ldv + hk * D + 32 * s + 8 * g);
   }
   f32x4 dv[ND], dk[ND];
 #pragma unroll
@@ -398,7 +451,7 @@ __global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __res
 
   const int qt0 = causal ? kbi : 0;
   const int qmin = kw < kvlen ? (causal ? kw : 0) : 1 << 30;  // first query that sees this key
-  const int nqt = S / 64 - qt0;
+  const int nqt = (S + 63) / 64 - qt0;
   const int n_it = kb0 < kvlen ? hp * nqt : 0;  // keys past kv_len get zero gradient
 
   bf16x8 qr[LOADS], dr[LOADS];
@@ -410,12 +463,12 @@ __global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __res
     for (int p = 0; p < LOADS; ++p) {
       const int ci = p * 256 + tid;
       const int row = ci / CH, ch = ci % CH;
-      const size_t tq = tok0 + qa0 + row;
+      const size_t tq = tok0 + min(qa0 + row, S - 1);
       qr[p] = *reinterpret_cast<const bf16x8*>(Q + tq * ldq + h * D + ch * 8);
       dr[p] = *reinterpret_cast<const bf16x8*>(dO + tq * ldo + h * D + ch * 8);
     }
     if (tid < 128) {
-      const size_t bh = ((size_t)b * hq + h) * S + qa0 + (tid & 63);
+      const size_t bh = ((size_t)b * hq + h) * S + min(qa0 + (tid & 63), S - 1);
       st = tid < 64 ? lse[bh] * LOG2E : delta[bh];
     }
   };
@@ -455,7 +508,7 @@ __global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __res
         dp[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ofr, vf[s], dp[qt], 0, 0, 0);
       }
     }
-    const bool need_mask = (causal && qa0 < kb0 + 63) || (kb0 + 64 > kvlen);
+    const bool need_mask = (causal && qa0 < kb0 + 63) || (kb0 + 64 > kvlen) || (qa0 + 64 > S);
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
       const f32x4 L = *reinterpret_cast<const f32x4*>(Ls + 16 * qt + 4 * g);
@@ -464,10 +517,23 @@ __global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __res
       for (int r = 0; r < 4; ++r) sp[qt][r] = fexp2(sp[qt][r] * scale_log2 - L[r]);
       if (need_mask) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sp[qt][r] = (qa0 + 16 * qt + 4 * g + r >= qmin) ? sp[qt][r] : 0.f;
+        for (int r = 0; r < 4; ++r) {
+          const int q = qa0 + 16 * qt + 4 * g + r;
+          sp[qt][r] = (q >= qmin && q < S) ? sp[qt][r] : 0.f;
+        }
       }
+      if (drp.thresh) {   // dV takes the dropped P, dS = P∘(M∘dP/(1-p) − delta)
+        const uint32_t bh = (uint32_t)(b * hq + hk * rep + hw * hp + it / nqt);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dp[qt][r] = sp[qt][r] * (dp[qt][r] - Dl[r]);
+        for (int r = 0; r < 4; ++r) {
+          const bool keep = drop_hash(drp.s0, drp.s1, bh, qa0 + 16 * qt + 4 * g + r, kw) >= drp.thresh;
+          dp[qt][r] = sp[qt][r] * ((keep ? dp[qt][r] * drp.rinv : 0.f) - Dl[r]);
+          sp[qt][r] = keep ? sp[qt][r] * drp.rinv : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dp[qt][r] = sp[qt][r] * (dp[qt][r] - Dl[r]);
+      }
     }
     // ---- dVᵀ[d][key] += dOᵀ[d][q]·P[q][key] ; dKᵀ += Qᵀ·dS   (permuted-q operand order)
 #pragma unroll
@@ -503,6 +569,7 @@ __global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __res
     }
   }
   // ---- dK (scaled) / dV, summed over the GQA group: lane col key = kw, rows d = 16dt + 4g + r
+  if (kw >= S) return;
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt) {
     const size_t off = (tok0 + kw) * ldkv + hk * D + 16 * dt + 4 * g;
@@ -519,42 +586,56 @@ __global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __res
 
 }  // namespace
 
+static DropParams make_drop(float p, uint64_t seed) {
+  DropParams d{(uint32_t)seed, (uint32_t)(seed >> 32), 0u, 1.f};
+  if (p > 0.f) {
+    d.thresh = (uint32_t)std::min(4294967295.0, (double)p * 4294967296.0);
+    d.rinv = 1.f / (1.f - p);
+  }
+  return d;
+}
+
+#define LIPA_ATTN_D(D, ...)                 \
+  switch (D) {                              \
+    case 32: { constexpr int DD = 32; __VA_ARGS__; } break;   \
+    case 64: { constexpr int DD = 64; __VA_ARGS__; } break;   \
+    case 96: { constexpr int DD = 96; __VA_ARGS__; } break;   \
+    default: { constexpr int DD = 128; __VA_ARGS__; } break;  \
+  }
+
 void launch_attn_fwd(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv, const int* kv_lens,
-                     void* o, float* lse, int B, int S, int hq, int hkv, int D, int causal, float scale,
-                     hipStream_t st) {
-  dim3 grid((S + 127) / 128, hq, B), blk(256);
+                     const int* q_offs, void* o, float* lse, int B, int Sq, int Skv, int kv_rows, int hq, int hkv,
+                     int D, int causal, float scale, float p_drop, uint64_t seed, hipStream_t st) {
+  const DropParams dp = make_drop(p_drop, seed);
+  dim3 grid((Sq + 127) / 128, hq, B), blk(256);
   const float sl2 = scale * LOG2E;
-  if (D == 128)
-    attn_fwd_k<128><<<grid, blk, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, ldq, ldk, ldv, kv_lens,
-                                          (bf16*)o, lse, S, hq, hkv, causal, sl2);
-  else
-    attn_fwd_k<64><<<grid, blk, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, ldq, ldk, ldv, kv_lens,
-                                         (bf16*)o, lse, S, hq, hkv, causal, sl2);
+  LIPA_ATTN_D(D, attn_fwd_k<DD><<<grid, blk, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, ldq, ldk,
+                                                      ldv, kv_lens, q_offs, (bf16*)o, lse, Sq, Skv, kv_rows, hq,
+                                                      hkv, causal, sl2, dp));
   LIPA_CHECK_LAUNCH();
 }
 
 void launch_attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
                      const int* kv_lens, int ldq, int ldk, int ldv, void* dq, void* dk, void* dv, float* delta, int B,
-                     int S, int hq, int hkv, int D, int causal, float scale, hipStream_t st) {
+                     int S, int hq, int hkv, int D, int causal, float scale, float p_drop, uint64_t seed,
+                     hipStream_t st) {
   const float sl2 = scale * LOG2E;
-  dim3 gq(S / 64, hq, B), gkv(S / 64, hkv, B), blk(256);
+  const DropParams dp = make_drop(p_drop, seed);
+  const int nb = (S + 63) / 64;
+  dim3 gq(nb, hq, B), gkv(nb, hkv, B), blk(256);
 #define RUN(DD)                                                                                                    \
   attn_bwd_dq_k<DD><<<gq, blk, 0, st>>>((const bf16*)dout, (const bf16*)o, (const bf16*)q, (const bf16*)k,         \
                                         (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dq, S, hq, hkv,  \
-                                        causal, scale, sl2);                                                        \
+                                        causal, scale, sl2, dp);                                                    \
   if ((hq / hkv) % 2 == 0)                                                                                       \
     attn_bwd_dkv_k<DD, 2><<<gkv, 512, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k, (const bf16*)v,   \
                                                lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, (bf16*)dv, S, hq, hkv, \
-                                               causal, scale, sl2);                                                  \
+                                               causal, scale, sl2, dp);                                              \
   else                                                                                                             \
     attn_bwd_dkv_k<DD, 1><<<gkv, 256, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k, (const bf16*)v,   \
                                                lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, (bf16*)dv, S, hq, hkv, \
-                                               causal, scale, sl2)
-  if (D == 128) {
-    RUN(128);
-  } else {
-    RUN(64);
-  }
+                                               causal, scale, sl2, dp)
+  LIPA_ATTN_D(D, RUN(DD));
 #undef RUN
   LIPA_CHECK_LAUNCH();
 }

@@ -23,12 +23,12 @@ import os
 
 import torch
 import torch.nn as nn
-import torch.utils.checkpoint as ckpt
 
 from ..ops import reference as ref
 from ..ops.activation import swiglu_fused
-from ..ops.attention import flash_attention
+from ..ops.attention import flash_attention, flash_attention_prefix
 from ..ops.decode import decode_attention_append
+from ..ops.linear import checkpoint as lora_checkpoint
 from ..ops.loss import fused_linear_cross_entropy, shift_labels
 from ..ops.norm import RMSNorm, rms_norm, rms_norm_residual
 from ..ops.rope import apply_rope, qk_norm_rope
@@ -185,12 +185,10 @@ class Qwen3Attention(nn.Module):
             if start == 0:   # prefill: same fused kernel as training (causal + per-row key lengths)
                 o = flash_attention(q, k.reshape(B * S, -1), v.reshape(B * S, -1), B, S, self.hq, self.hkv, self.d,
                                     causal=True, kv_lens=kv_lens)
-            else:
-                Sk = kc.shape[1]
-                o = ref.attention(q.view(B, S, self.hq, self.d), kc.view(B, Sk, self.hkv, self.d),
-                                  vc.view(B, Sk, self.hkv, self.d), causal=True,
-                                  key_padding_mask=(torch.arange(Sk, device=x.device)[None] < kv_lens[:, None])
-                                  if kv_lens is not None else None).reshape(B * S, -1)
+            else:   # chunked / suffix prefill: the new queries sit at start.. over the cache prefix
+                c = cache.k[self.layer_idx]
+                o = flash_attention_prefix(q, c, cache.v[self.layer_idx], B, S, start + S, self.hq, self.hkv,
+                                           self.d, q_offs=start, kv_lens=kv_lens, kv_rows=c.shape[1])
         if self.tp_group is None:
             return project([self.o_proj], o, residual, tr)
         # row-parallel o_proj: partial sums + the residual on rank 0 only, then one all-reduce
@@ -265,7 +263,7 @@ class Qwen3Model(nn.Module):
             x = self.pp.enter(x)        # stages > 0: the previous stage's hidden states
         for layer in self.layers:
             if self.gradient_checkpointing and self.training and cache is None:
-                x = ckpt.checkpoint(layer, x, cos, sin, B, S, None, 0, kv_lens, use_reentrant=False)
+                x = lora_checkpoint(layer, x, cos, sin, B, S, None, 0, kv_lens)
             else:
                 x = layer(x, cos, sin, B, S, cache, start, kv_lens)
         if self.pp is not None:

@@ -145,6 +145,33 @@ def seed_dropout(seed: int):
     _KEY[0] = (int(seed) * 0x2545F4914F6CDD1D) & 0x7FFFFFFFFFFFFFFF
 
 
+def checkpoint(fn, *args):
+    """Activation checkpointing (non-reentrant) that replays the SAME LoRA dropout masks.
+
+    The fused LoRA kernels draw their dropout mask from the host key stream above, not from
+    torch's RNG, so torch's ``preserve_rng_state`` does not cover them: a plain
+    ``torch.utils.checkpoint`` recompute would draw fresh keys and the backward would differentiate
+    a different mask than the forward applied.  Here the key-stream position at the first (forward)
+    call is remembered and restored for the recompute, then the live stream is put back — the
+    masks match exactly and the stream advances once per real forward.  Reference:
+    ``Fine-Tuning/qwen3-8b-lora.py:123`` (gradient checkpointing + ``lora_dropout``)."""
+    import torch.utils.checkpoint as ckpt
+    state: list = []
+
+    def run(*a):
+        if not state:                      # the forward pass
+            state.append(_KEY[0])
+            return fn(*a)
+        live = _KEY[0]                     # the recompute inside backward
+        _KEY[0] = state[0]
+        try:
+            return fn(*a)
+        finally:
+            _KEY[0] = live
+
+    return ckpt.checkpoint(run, *args, use_reentrant=False)
+
+
 def bf16_view(p: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
     """The optimizer-maintained low-precision shadow of a fp32 trainable parameter
     (written by the fused AdamW kernel every step), else a cast."""

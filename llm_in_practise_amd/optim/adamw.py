@@ -25,17 +25,31 @@ from ..ops._native import native, use_native
 
 
 class FlatParams:
-    """Flatten parameters into one fp32 master buffer + one fp32 grad buffer."""
+    """Flatten parameters into one fp32 master buffer + one fp32 grad buffer.
 
-    def __init__(self, params: list[torch.nn.Parameter], align: int = 64):
-        self.params = [p for p in params if p.requires_grad]
+    ``groups`` (optional) partitions ``params`` into optimizer param groups; each group is a
+    contiguous segment of the flat buffers starting on a ``seg_align`` boundary, so a per-group
+    update is one kernel launch over a slice (the 8-bit optimizer's 256-element state blocks
+    never straddle two groups)."""
+
+    def __init__(self, params: list[torch.nn.Parameter], align: int = 64, groups: list[list] | None = None,
+                 seg_align: int = 256):
+        if groups is None:
+            groups = [list(params)]
+        groups = [[p for p in g if p.requires_grad] for g in groups]
+        self.params = [p for g in groups for p in g]
         assert self.params, "no trainable parameters"
         dev = self.params[0].device
         self.offsets = []
+        self.segments = []                       # [start, end) of each group in the flat buffers
         n = 0
-        for p in self.params:
-            self.offsets.append(n)
-            n += (p.numel() + align - 1) // align * align
+        for g in groups:
+            s0 = n
+            for p in g:
+                self.offsets.append(n)
+                n += (p.numel() + align - 1) // align * align
+            n = (n + seg_align - 1) // seg_align * seg_align
+            self.segments.append((s0, n))
         self.numel = n
         self.data = torch.zeros(n, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(n, dtype=torch.float32, device=dev)
@@ -83,22 +97,37 @@ class FlatParams:
 
 
 class _FlatOptimizer:
+    """Base of the fused flat-buffer optimizers.  ``params`` is an iterable of parameters or of
+    torch-style param-group dicts (``{"params": [...], "lr": ..., "weight_decay": ...}``, e.g. the
+    decay / no-decay split of ``temp/ddp_gpt_wikitext2.py:337-344``); every group keeps its own lr
+    and weight decay and is updated as one contiguous segment of the flat buffers."""
+
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
                  max_grad_norm: float = 0.0):
         params = list(params)
-        if params and isinstance(params[0], dict):   # param groups: single group supported
-            group = params[0]
-            params = list(group["params"])
-            lr = group.get("lr", lr)
-            weight_decay = group.get("weight_decay", weight_decay)
-        self.flat = FlatParams(params)
+        if params and isinstance(params[0], dict):
+            groups = [dict(g) for g in params]
+        else:
+            groups = [{"params": params}]
+        for g in groups:
+            g["params"] = [p for p in g["params"] if p.requires_grad]
+            g.setdefault("lr", lr)
+            g.setdefault("weight_decay", weight_decay)
+            g.setdefault("initial_lr", g["lr"])
+        groups = [g for g in groups if g["params"]]
+        self.flat = FlatParams([p for g in groups for p in g["params"]], groups=[g["params"] for g in groups])
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
         self.max_grad_norm = max_grad_norm
         self.step_count = 0
         dev = self.flat.data.device
         self.norm_out = torch.zeros(3, dtype=torch.float32, device=dev)   # [norm, clip coef, sumsq]
         self.skip_flag = None                                             # fp16 overflow flag (device)
-        self.param_groups = [{"params": self.flat.params, "lr": lr, "weight_decay": weight_decay}]
+        self.param_groups = groups
+
+    def _segments(self):
+        """(start, end, lr, weight_decay) per param group."""
+        for (s0, s1), g in zip(self.flat.segments, self.param_groups):
+            yield s0, s1, float(g["lr"]), float(g["weight_decay"])
 
     # torch.optim-like surface ----------------------------------------------------
     def zero_grad(self, set_to_none: bool = False):
@@ -157,15 +186,19 @@ class AdamW(_FlatOptimizer):
         b1, b2 = self.betas
         g = self.flat.grad
         clip = self.norm_out if self.max_grad_norm > 0 else None
+        low = self._sync_low()
         if use_native(g):
-            native().adamw(self.flat.data, g, self.exp_avg, self.exp_avg_sq, self._sync_low(), self._lr(), b1, b2,
-                           self.eps, self.weight_decay, self.step_count, clip, self.skip_flag)
+            for s0, s1, lr, wd in self._segments():
+                native().adamw(self.flat.data[s0:s1], g[s0:s1], self.exp_avg[s0:s1], self.exp_avg_sq[s0:s1],
+                               None if low is None else low[s0:s1], lr, b1, b2, self.eps, wd, self.step_count,
+                               clip, self.skip_flag)
         else:
             if self.skip_flag is not None and self.skip_flag.item() != 0:
                 return
             gg = g * (self.norm_out[1] if clip is not None else 1.0)
-            ref.adamw_step(self.flat.data, gg, self.exp_avg, self.exp_avg_sq, self.step_count, self._lr(), b1, b2,
-                           self.eps, self.weight_decay)
+            for s0, s1, lr, wd in self._segments():
+                ref.adamw_step(self.flat.data[s0:s1], gg[s0:s1], self.exp_avg[s0:s1], self.exp_avg_sq[s0:s1],
+                               self.step_count, lr, b1, b2, self.eps, wd)
             if self.flat.mixed:
                 self.flat.low.copy_(self.flat.data)
 
@@ -201,9 +234,13 @@ class AdamW8bit(_FlatOptimizer):
         g = self.flat.grad
         clip = self.norm_out if self.max_grad_norm > 0 else None
         if use_native(g):
-            native().adamw8bit(self.flat.data, g, self.qm, self.qv, self.am, self.av, self.code_s, self.code_u,
-                               self._sync_low(), self._lr(), b1, b2, self.eps, self.weight_decay, self.step_count,
-                               clip, self.skip_flag)
+            low = self._sync_low()
+            B = self.BLOCK
+            for s0, s1, lr, wd in self._segments():
+                native().adamw8bit(self.flat.data[s0:s1], g[s0:s1], self.qm[s0:s1], self.qv[s0:s1],
+                                   self.am[s0 // B:(s1 + B - 1) // B], self.av[s0 // B:(s1 + B - 1) // B],
+                                   self.code_s, self.code_u, None if low is None else low[s0:s1], lr, b1, b2,
+                                   self.eps, wd, self.step_count, clip, self.skip_flag)
             return
         # reference: dequantise states, fp32 update, requantise blockwise
         n, B = self.flat.numel, self.BLOCK
@@ -214,11 +251,16 @@ class AdamW8bit(_FlatOptimizer):
         v = blk(self.code_u[self.qv.long()]) * self.av[:, None]
         gg = blk(g * (self.norm_out[1] if clip is not None else 1.0))
         p = blk(self.flat.data)
-        p.mul_(1 - self._lr() * self.weight_decay)
+        lr_e = torch.empty(p.shape[0], 1, dtype=p.dtype, device=p.device)   # per-block lr / wd of its group
+        wd_e = torch.empty_like(lr_e)
+        for s0, s1, lr, wd in self._segments():
+            lr_e[s0 // B:(s1 + B - 1) // B] = lr
+            wd_e[s0 // B:(s1 + B - 1) // B] = wd
+        p.mul_(1 - lr_e * wd_e)
         m.mul_(b1).add_(gg, alpha=1 - b1)
         v.mul_(b2).addcmul_(gg, gg, value=1 - b2)
         bc1, bc2 = 1 - b1 ** self.step_count, 1 - b2 ** self.step_count
-        p.addcdiv_(m, (v / bc2).sqrt().add_(self.eps), value=-self._lr() / bc1)
+        p.add_(m / (v / bc2).sqrt().add_(self.eps) * (-lr_e / bc1))
         self.flat.data.copy_(p.view(-1)[:n])
         self.am.copy_(m.abs().amax(1))
         self.av.copy_(v.amax(1))
@@ -229,6 +271,22 @@ class AdamW8bit(_FlatOptimizer):
             self.flat.low.copy_(self.flat.data)
         elif self.flat.shadow is not None:
             self.flat.shadow.copy_(self.flat.data)
+
+
+NO_DECAY_DEFAULT = ("bias", "LayerNorm.weight", "norm.weight", "ln_", "ln1", "ln2", "ln_f")
+
+
+def decay_param_groups(model: torch.nn.Module, weight_decay: float, no_decay=NO_DECAY_DEFAULT) -> list[dict]:
+    """The decay / no-decay split of ``temp/ddp_gpt_wikitext2.py:337-344``: parameters whose name
+    contains one of ``no_decay`` (biases, LayerNorm weights) get ``weight_decay=0``.  Also puts
+    every 1-D parameter (norm scales of our own modules) in the no-decay group."""
+    dec, nod = [], []
+    for n, p in model.named_parameters():
+        if not p.requires_grad:
+            continue
+        (nod if (p.ndim < 2 or any(k in n for k in no_decay)) else dec).append(p)
+    return [g for g in ({"params": dec, "weight_decay": weight_decay}, {"params": nod, "weight_decay": 0.0})
+            if g["params"]]
 
 
 def build_optimizer(name: str, params, lr: float, weight_decay: float = 0.0, betas=(0.9, 0.999), eps=1e-8,
@@ -275,14 +333,16 @@ class LRScheduler:
     def _apply(self):
         lr = self.lr_at(self.last_step)
         for g in self.opt.param_groups:
-            g["lr"] = lr
+            # a group with its own lr follows the same schedule shape (torch LambdaLR semantics)
+            init = g.get("initial_lr", self.base_lr)
+            g["lr"] = lr if init == self.base_lr or self.base_lr == 0 else lr * init / self.base_lr
 
     def step(self):
         self.last_step += 1
         self._apply()
 
     def get_last_lr(self):
-        return [self.opt.param_groups[0]["lr"]]
+        return [g["lr"] for g in self.opt.param_groups]
 
     def state_dict(self):
         return {"last_step": self.last_step}

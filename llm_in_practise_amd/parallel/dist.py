@@ -8,7 +8,6 @@ running intra-node over xGMI (8×MI355X full mesh, 7 links/GPU) — or ``gloo`` 
 from __future__ import annotations
 
 import datetime
-import os
 
 import torch
 import torch.distributed as dist
@@ -24,7 +23,6 @@ def init_distributed(backend: str | None = None, timeout_s: int = 1800) -> tuple
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(env.local_rank)
-            os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         kw = dict(backend=backend, init_method="env://", timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kw["device_id"] = torch.device("cuda", env.local_rank)

@@ -29,7 +29,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..optim.adamw import LRScheduler, build_optimizer
+from ..optim.adamw import LRScheduler, build_optimizer, decay_param_groups
 from ..parallel import dist as D
 from ..utils.logging import get_logger
 
@@ -60,6 +60,7 @@ class LoopConfig:
     patience: int = 0                  # epochs without val improvement before stopping (0 = off)
     best_model: str | None = None      # path for the best-validation weights (rank 0)
     resume: bool = False               # continue from <save_dir>/latest_checkpoint.pt if present
+    no_decay_groups: bool = False      # temp/ddp_gpt_wikitext2.py:337-344: biases / LayerNorm without decay
 
 
 def lm_loss(model: nn.Module, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
@@ -125,8 +126,9 @@ def train_lm(model: nn.Module, train_ds, cfg: LoopConfig, eval_ds=None, meta: di
     else:
         if cfg.precision == "bf16":
             model.to(torch.bfloat16)
-        opt = build_optimizer("adamw", [p for p in model.parameters() if p.requires_grad], cfg.lr,
-                              cfg.weight_decay, max_grad_norm=cfg.clip_grad_norm)
+        params = (decay_param_groups(model, cfg.weight_decay) if cfg.no_decay_groups
+                  else [p for p in model.parameters() if p.requires_grad])
+        opt = build_optimizer("adamw", params, cfg.lr, cfg.weight_decay, max_grad_norm=cfg.clip_grad_norm)
         if cfg.strategy == "ddp" and world > 1:
             from ..parallel.ddp import DistributedDataParallel
             ddp = DistributedDataParallel(model, grad_buffer=opt.grad_buffer)

@@ -45,7 +45,7 @@ def main():
     o, lse = ext.attn_fwd(q, k, v, None, B, S, hq, hkv, d, True, scale)
     do = torch.randn_like(o)
     t_f = timeit(lambda: ext.attn_fwd(q, k, v, None, B, S, hq, hkv, d, True, scale))
-    t_b = timeit(lambda: ext.attn_bwd(do, q, k, v, o, lse, None, B, S, hq, hkv, d, True, scale))
+    t_b = timeit(lambda: ext.attn_bwd(do, q, k, v, o, lse, None, B, S, hq, hkv, d, True, scale, 0.0, 0))
     fl = 4 * B * hq * S * S * d / 2  # causal fwd
     qs = q.view(B, S, hq, d).transpose(1, 2)
     ks = k.reshape(B, S, hkv, d).transpose(1, 2).repeat_interleave(hq // hkv, 1).contiguous()

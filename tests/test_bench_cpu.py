@@ -19,6 +19,21 @@ def _port():
     return p
 
 
+def test_bench_self_launches_n_ranks():
+    """`python bench.py --gpus 2` (no launcher env) must start 2 ranks itself, not silently run 1."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "2"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1",
+           "--model", "qwen3-tiny", "--seq-len", "64"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["dist_world_size"] == 2
+    assert d["config"]["parallelism"] == "dp2"
+
+
 @pytest.mark.parametrize("extra", [[], ["--ga-fusion", "0"], ["--strategy", "zero3"]])
 def test_bench_json_contract_two_ranks(extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",

@@ -217,6 +217,32 @@ def test_adamw8bit_tracks_fp32(native_ext):
     assert rel_err(p8, p) < 1e-3
 
 
+@pytest.mark.parametrize("kind", ["adamw", "adamw8bit"])
+def test_fused_optimizer_param_groups(native_ext, kind):
+    """decay / no-decay groups with their own lr: every group is updated (one segment each)."""
+    from llm_in_practise_amd.optim.adamw import AdamW, AdamW8bit
+    torch.manual_seed(0)
+    shapes = [(96, 40), (40,), (1000,)]
+    a = [torch.nn.Parameter(torch.randn(s, device=DEV)) for s in shapes]
+    b = [torch.nn.Parameter(t.detach().clone()) for t in a]
+    groups = lambda ps: [{"params": [ps[0]], "weight_decay": 0.1, "lr": 1e-2},   # noqa: E731
+                         {"params": ps[1:], "weight_decay": 0.0, "lr": 3e-3}]
+    o1 = (AdamW if kind == "adamw" else AdamW8bit)(groups(a))
+    o2 = torch.optim.AdamW(groups(b))
+    before = [t.detach().clone() for t in a]
+    for _ in range(4):
+        for p1, p2 in zip(a, b):
+            g = torch.randn(p1.shape, device=DEV)
+            p1.grad.copy_(g)
+            p2.grad = g.clone()
+        o1.step()
+        o2.step()
+    tol = 1e-5 if kind == "adamw" else 5e-3
+    for p1, p2, p0 in zip(a, b, before):
+        assert not torch.equal(p1.detach(), p0)
+        assert rel_err(p1.detach() - p0, p2.detach() - p0) < tol * (1 if kind == "adamw" else 20)
+
+
 # ----------------------------------------------------------------------------- NF4
 def test_nf4_quantize_matches_reference(native_ext):
     w = torch.randn(256, 512, device=DEV).to(torch.bfloat16)
@@ -299,8 +325,30 @@ def test_gemm_bf16_lora(native_ext, M, N, K):
 
 
 # ----------------------------------------------------------------------------- attention
-@pytest.mark.parametrize("B,S,hq,hkv,d,causal", [(2, 512, 32, 8, 128, True), (1, 256, 4, 4, 64, True),
-                                                  (2, 128, 8, 2, 128, False), (1, 192, 4, 2, 64, True)])
+ATTN_CASES = [(2, 512, 32, 8, 128, True), (1, 256, 4, 4, 64, True), (2, 128, 8, 2, 128, False),
+              (1, 192, 4, 2, 64, True),
+              # any S (masked tail tiles in fwd AND bwd), every head_dim, odd GQA groups
+              (1, 87, 4, 2, 64, True), (2, 255, 8, 2, 128, True), (1, 511, 4, 4, 96, False),
+              (2, 100, 4, 1, 32, True), (1, 130, 6, 3, 128, True), (3, 33, 2, 2, 96, True)]
+
+
+def _attn_ref_grads(q, k, v, do, B, S, hq, hkv, d, causal, scale, mask=None, keep=None, rinv=1.0):
+    qr, kr, vr = [t.float().reshape(B, S, -1, d).requires_grad_(True) for t in (q, k, v)]
+    if keep is None:
+        orf = ref.attention(qr, kr, vr, causal=causal, scale=scale, key_padding_mask=mask)
+    else:   # explicit reference with the kernel's dropout mask [B, H, S, S]
+        rep = hq // hkv
+        qh, kh, vh = qr.transpose(1, 2), kr.transpose(1, 2).repeat_interleave(rep, 1), vr.transpose(1, 2).repeat_interleave(rep, 1)
+        sc = qh @ kh.transpose(-1, -2) * scale
+        if causal:
+            sc = sc.masked_fill(torch.ones(S, S, dtype=torch.bool, device=DEV).triu(1), float("-inf"))
+        p = torch.softmax(sc, -1) * keep * rinv
+        orf = (p @ vh).transpose(1, 2)
+    orf.backward(do.float().view(B, S, hq, d))
+    return orf, qr.grad, kr.grad, vr.grad
+
+
+@pytest.mark.parametrize("B,S,hq,hkv,d,causal", ATTN_CASES)
 def test_flash_attention_fwd_bwd(native_ext, B, S, hq, hkv, d, causal):
     T = B * S
     q = torch.randn(T, hq * d, device=DEV).to(torch.bfloat16)
@@ -308,28 +356,105 @@ def test_flash_attention_fwd_bwd(native_ext, B, S, hq, hkv, d, causal):
     k, v = kv[:, :hkv * d], kv[:, hkv * d:]          # strided views (fused-projection layout)
     scale = 1 / math.sqrt(d)
     o, lse = native_ext.attn_fwd(q, k, v, None, B, S, hq, hkv, d, causal, scale)
-    qr, kr, vr = [t.float().reshape(B, S, -1, d).requires_grad_(True) for t in (q, k, v)]
-    orf = ref.attention(qr, kr, vr, causal=causal, scale=scale)
-    assert rel_err(o.view(B, S, hq, d), orf) < 1e-2
     do = torch.randn_like(o)
-    dq, dk, dv = native_ext.attn_bwd(do, q, k, v, o, lse, None, B, S, hq, hkv, d, causal, scale)
-    orf.backward(do.float().view(B, S, hq, d))
-    assert rel_err(dq.view(B, S, hq, d), qr.grad) < 2e-2
-    assert rel_err(dk.view(B, S, hkv, d), kr.grad) < 2e-2
-    assert rel_err(dv.view(B, S, hkv, d), vr.grad) < 2e-2
+    orf, gq, gk, gv = _attn_ref_grads(q, k, v, do, B, S, hq, hkv, d, causal, scale)
+    assert rel_err(o.view(B, S, hq, d), orf) < 1e-2
+    dq, dk, dv = native_ext.attn_bwd(do, q, k, v, o, lse, None, B, S, hq, hkv, d, causal, scale, 0.0, 0)
+    assert rel_err(dq.view(B, S, hq, d), gq) < 2e-2
+    assert rel_err(dk.view(B, S, hkv, d), gk) < 2e-2
+    assert rel_err(dv.view(B, S, hkv, d), gv) < 2e-2
 
 
-def test_flash_attention_padding(native_ext):
-    B, S, h, d = 2, 128, 4, 64
+@pytest.mark.parametrize("S", [128, 87])
+def test_flash_attention_padding(native_ext, S):
+    """right-padded keys (kv_lens) in the forward AND backward, incl. a ragged tail tile"""
+    B, h, d = 2, 4, 64
     q = torch.randn(B * S, h * d, device=DEV).to(torch.bfloat16)
     k = torch.randn(B * S, h * d, device=DEV).to(torch.bfloat16)
     v = torch.randn(B * S, h * d, device=DEV).to(torch.bfloat16)
-    lens = torch.tensor([100, 128], device=DEV, dtype=torch.int32)
-    o, _ = native_ext.attn_fwd(q, k, v, lens, B, S, h, h, d, True, 0.125)
+    lens = torch.tensor([S - 28, S], device=DEV, dtype=torch.int32)
+    o, lse = native_ext.attn_fwd(q, k, v, lens, B, S, h, h, d, True, 0.125)
     mask = torch.arange(S, device=DEV)[None] < lens[:, None]
-    orf = ref.attention(*(t.float().view(B, S, h, d) for t in (q, k, v)), causal=True, key_padding_mask=mask,
-                        scale=0.125)
+    do = torch.randn_like(o)
+    orf, gq, gk, gv = _attn_ref_grads(q, k, v, do, B, S, h, h, d, True, 0.125, mask=mask)
     assert rel_err(o.view(B, S, h, d)[mask], orf[mask]) < 1e-2
+    dq, dk, dv = native_ext.attn_bwd(do, q, k, v, o, lse, lens, B, S, h, h, d, True, 0.125, 0.0, 0)
+    assert rel_err(dq.view(B, S, h, d)[mask], gq[mask]) < 2e-2
+    assert rel_err(dk.view(B, S, h, d)[mask], gk[mask]) < 2e-2
+    assert rel_err(dv.view(B, S, h, d)[mask], gv[mask]) < 2e-2
+    assert dk.view(B, S, h, d)[~mask].abs().max() == 0
+
+
+def _drop_keep(seed, B, H, S, p):
+    """numpy replica of attention.hip drop_hash: keep[b, h, q, k]"""
+    import numpy as np
+    M = np.uint64(0xFFFFFFFF)
+    s0, s1 = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
+    bh = np.arange(B * H, dtype=np.uint64).reshape(B, H, 1, 1)
+    q = np.arange(S, dtype=np.uint64).reshape(1, 1, S, 1)
+    k = np.arange(S, dtype=np.uint64).reshape(1, 1, 1, S)
+    with np.errstate(over="ignore"):
+        x = s0 ^ ((bh * np.uint64(0x9E3779B9)) & M)
+        x = x ^ ((q * np.uint64(0x85EBCA6B) + s1) & M)
+        x = x ^ ((k * np.uint64(0xC2B2AE35)) & M)
+        x ^= x >> np.uint64(16)
+        x = (x * np.uint64(0x7FEB352D)) & M
+        x ^= x >> np.uint64(15)
+        x = (x * np.uint64(0x846CA68B)) & M
+        x ^= x >> np.uint64(16)
+    thresh = min(4294967295, int(p * 4294967296.0))
+    return torch.from_numpy((x >= thresh).astype(np.float32)).to(DEV)
+
+
+@pytest.mark.parametrize("S,hq,hkv,d", [(128, 4, 2, 64), (95, 4, 4, 128)])
+def test_flash_attention_dropout(native_ext, S, hq, hkv, d):
+    """attention-probability dropout: fwd and bwd regenerate the same counter-RNG mask"""
+    B, p, seed = 2, 0.1, 0x1234567890AB
+    q = torch.randn(B * S, hq * d, device=DEV).to(torch.bfloat16)
+    k = torch.randn(B * S, hkv * d, device=DEV).to(torch.bfloat16)
+    v = torch.randn(B * S, hkv * d, device=DEV).to(torch.bfloat16)
+    scale = 1 / math.sqrt(d)
+    o, lse = native_ext.attn_fwd_ext(q, k, v, None, None, B, S, S, S, hq, hkv, d, True, scale, p, seed)
+    keep = _drop_keep(seed, B, hq, S, p)
+    assert 0.85 < keep.mean().item() < 0.95
+    do = torch.randn_like(o)
+    orf, gq, gk, gv = _attn_ref_grads(q, k, v, do, B, S, hq, hkv, d, True, scale, keep=keep, rinv=1 / (1 - p))
+    assert rel_err(o.view(B, S, hq, d), orf) < 1e-2
+    dq, dk, dv = native_ext.attn_bwd(do, q, k, v, o, lse, None, B, S, hq, hkv, d, True, scale, p, seed)
+    assert rel_err(dq.view(B, S, hq, d), gq) < 2e-2
+    assert rel_err(dk.view(B, S, hkv, d), gk) < 2e-2
+    assert rel_err(dv.view(B, S, hkv, d), gv) < 2e-2
+
+
+@pytest.mark.parametrize("sq,start,d", [(64, 100, 128), (37, 300, 64), (1, 17, 128)])
+def test_flash_attention_prefix_suffix(native_ext, sq, start, d):
+    """chunked / prefix-cache suffix prefill: sq new queries at positions start.. over a KV cache"""
+    from llm_in_practise_amd.ops.attention import flash_attention_prefix
+    B, hq, hkv, rows = 2, 8, 2, 512
+    kc = torch.randn(B, rows, hkv * d, device=DEV).to(torch.bfloat16)
+    vc = torch.randn(B, rows, hkv * d, device=DEV).to(torch.bfloat16)
+    q = torch.randn(B * sq, hq * d, device=DEV).to(torch.bfloat16)
+    offs = torch.tensor([start, start - 5], device=DEV, dtype=torch.int32)
+    lens = offs + sq
+    o = flash_attention_prefix(q, kc, vc, B, sq, start + sq, hq, hkv, d, q_offs=offs, kv_lens=lens)
+    import llm_in_practise_amd.ops.attention as A
+    want = A.flash_attention_prefix(q.float().cpu().to(torch.bfloat16), kc.cpu(), vc.cpu(), B, sq, start + sq,
+                                    hq, hkv, d, q_offs=offs.cpu(), kv_lens=lens.cpu())
+    assert rel_err(o.float().cpu(), want.float()) < 1e-2
+
+
+def test_sdpa_bshd_routes_to_kernel(native_ext):
+    """GPTLike / BERT-style [B,S,H,D] attention with S % 64 != 0, a right-padding key mask and fp16
+    activations runs the fused kernel (matches the fp32 reference, gradients flow)."""
+    from llm_in_practise_amd.ops.attention import sdpa_bshd
+    B, S, H, d = 2, 255, 12, 64
+    q, k, v = [torch.randn(B, S, H, d, device=DEV, dtype=torch.float16, requires_grad=True) for _ in range(3)]
+    mask = torch.arange(S, device=DEV)[None] < torch.tensor([200, 255], device=DEV)[:, None]
+    o = sdpa_bshd(q, k, v, causal=False, key_padding_mask=mask)
+    want = ref.attention(q.float(), k.float(), v.float(), causal=False, key_padding_mask=mask)
+    assert o.dtype == torch.float16 and rel_err(o.float(), want) < 1e-2
+    o.float().sum().backward()
+    assert q.grad is not None and torch.isfinite(q.grad.float()).all()
 
 
 # ----------------------------------------------------------------------------- dropout / integration

@@ -119,3 +119,53 @@ def test_token_block_loader_sharding_and_resume():
     L2 = C.TokenBlockLoader(toks, 32, 4, 0, 1, 7, True, 2, False)
     L2.start_epoch(0, 3)
     assert torch.equal(L2.next()[0], a[3])                            # exact resume
+
+
+def _two_groups(ps):
+    """decay / no-decay split with different lrs (temp/ddp_gpt_wikitext2.py:337-344 shape)"""
+    return [{"params": [ps[0]], "weight_decay": 0.1, "lr": 1e-2}, {"params": [ps[1], ps[2]], "weight_decay": 0.0, "lr": 3e-3}]
+
+
+def test_adamw_param_groups_match_torch():
+    torch.manual_seed(0)
+    shapes = [(33, 7), (7,), (300,)]
+    a = [torch.nn.Parameter(torch.randn(s)) for s in shapes]
+    b = [torch.nn.Parameter(t.detach().clone()) for t in a]
+    o1 = AdamW(_two_groups(a), lr=5e-4)
+    o2 = torch.optim.AdamW(_two_groups(b), lr=5e-4)
+    assert len(o1.param_groups) == 2 and o1.param_groups[1]["lr"] == 3e-3
+    for _ in range(4):
+        for p1, p2 in zip(a, b):
+            g = torch.randn(p1.shape)
+            p1.grad.copy_(g)
+            p2.grad = g.clone()
+        o1.step()
+        o2.step()
+    for p1, p2 in zip(a, b):
+        assert torch.allclose(p1.detach(), p2.detach(), atol=1e-6)
+
+
+def test_adamw8bit_param_groups_update_every_group():
+    torch.manual_seed(0)
+    a = [torch.nn.Parameter(torch.randn(s)) for s in [(300,), (5,), (700,)]]
+    b = [torch.nn.Parameter(t.detach().clone()) for t in a]
+    o1 = AdamW8bit(_two_groups(a))
+    o2 = AdamW(_two_groups(b))
+    for _ in range(6):
+        for p1, p2 in zip(a, b):
+            g = torch.randn(p1.shape)
+            p1.grad.copy_(g)
+            p2.grad.copy_(g)
+        o1.step()
+        o2.step()
+    for p1, p2, p0 in zip(a, b, [torch.randn(1)] * 3):
+        assert (p1 - p2).norm() / (p2.detach()).norm() < 5e-3
+
+
+def test_scheduler_scales_each_group():
+    ps = [torch.nn.Parameter(torch.randn(4)) for _ in range(3)]
+    o = AdamW(_two_groups(ps), lr=1e-2)
+    sch = LRScheduler(o, "linear", 1e-2, total_steps=10)
+    sch.step()
+    lrs = sch.get_last_lr()
+    assert abs(lrs[0] - 0.9e-2) < 1e-12 and abs(lrs[1] - 0.9 * 3e-3) < 1e-12

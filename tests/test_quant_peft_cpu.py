@@ -171,3 +171,24 @@ def test_ga_fused_pass_equals_sequential():
         grads.append([p.grad.clone() for p in pm.parameters() if p.requires_grad])
     for a, b in zip(*grads):
         assert torch.allclose(a, b, atol=1e-6, rtol=1e-4)
+
+
+def test_checkpoint_replays_dropout_key_stream():
+    """ops.linear.checkpoint restores the host dropout-key stream for the recompute, so the
+    backward sees the forward's key; the live stream advances exactly once per real forward."""
+    from llm_in_practise_amd.ops import linear as L
+    L.seed_dropout(7)
+    seen = []
+
+    def fn(x):
+        k = L.next_dropout_key()
+        seen.append(k)
+        return x * x * float(k % 997 + 1)      # saves x: backward must recompute
+
+    x = torch.ones(3, requires_grad=True)
+    y = L.checkpoint(fn, x)
+    after_fwd = L._KEY[0]
+    y.sum().backward()
+    assert len(seen) == 2 and seen[0] == seen[1]              # recompute drew the same key
+    assert L._KEY[0] == after_fwd                             # stream not advanced by the recompute
+    assert torch.allclose(x.grad, torch.full((3,), 2.0 * float(seen[0] % 997 + 1)))
