@@ -138,7 +138,7 @@ def main():
         opt = build_optimizer(args.optim, [p for p in model.parameters() if p.requires_grad], args.lr,
                               weight_decay=0.0, max_grad_norm=1.0)
         sched = LRScheduler(opt, "linear", args.lr, total_steps)
-        ddp = DistributedDataParallel(model, grad_buffer=opt.grad_buffer)
+        ddp = DistributedDataParallel(model, flat=opt.flat)
 
     gen = torch.Generator(device=device).manual_seed(1000 + rank)
     n_batches = 8

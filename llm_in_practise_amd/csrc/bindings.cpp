@@ -47,6 +47,10 @@ void launch_gemm_skinny(const void*, int, const void*, const void*, void*, float
 void set_dequant_variant(int);
 void launch_nf4_dequant(const uint8_t*, const float*, const uint8_t*, const float*, const float*, const float*, void*,
                         size_t, hipStream_t);
+bool gemm8_supported(int, int, int, int, int);
+int gemm8_splits(int, int, int);
+void launch_gemm8(const void*, int, const void*, int, const void*, const void*, int, const void*, void*, float*, int, int,
+                  int, int, hipStream_t);
 void launch_attn_fwd(const void*, const void*, const void*, int, int, int, const int*, const int*, void*, float*, int,
                      int, int, int, int, int, int, int, float, float, uint64_t, hipStream_t);
 void launch_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const int*, int,
@@ -494,6 +498,47 @@ Tensor gemm_bf16_t(Tensor dy, Tensor w, optional<Tensor> ext_a, optional<Tensor>
   return dx;
 }
 
+// ------------------------------------------------------------------ 8-phase MFMA GEMM
+// y = x·wᵀ (+ ext_a·ext_bᵀ) (+ residual);  x [M, K] (row stride any multiple of 8), w [N, K]
+Tensor gemm8(Tensor x, Tensor w, optional<Tensor> ext_a, optional<Tensor> ext_b, optional<Tensor> residual,
+             int64_t splits) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1, "gemm8: 2-D, unit inner stride");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "gemm8: K mismatch");
+  TORCH_CHECK(gemm8_supported(M, N, K, x.stride(0), w.stride(0)), "gemm8: unsupported shape / strides");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              "gemm8: 16-byte aligned operands");
+  const void* ea = nullptr;
+  const void* eb = nullptr;
+  int R = 0;
+  if (ext_a && ext_a->defined()) {
+    TORCH_CHECK(ext_b && ext_b->defined(), "gemm8: ext_b");
+    CHECK_BF16(*ext_a);
+    CHECK_BF16(*ext_b);
+    TORCH_CHECK(ext_a->is_contiguous() && ext_b->is_contiguous(), "gemm8: contiguous LoRA slices");
+    R = ext_a->size(1);
+    TORCH_CHECK(R % 32 == 0 && ext_a->size(0) == M && ext_b->size(0) == N && ext_b->size(1) == R,
+                "gemm8: LoRA K-slice shapes [M, R] / [N, R], R % 32 == 0");
+    ea = ext_a->data_ptr();
+    eb = ext_b->data_ptr();
+  }
+  const void* res = nullptr;
+  if (residual && residual->defined()) {
+    CHECK_BF16(*residual);
+    TORCH_CHECK(residual->is_contiguous() && residual->size(0) == M && residual->size(1) == N, "gemm8: residual [M, N]");
+    res = residual->data_ptr();
+  }
+  const int sp = splits > 0 ? (int)splits : gemm8_splits(M, N, K);
+  auto y = at::empty({M, N}, x.options());
+  Tensor ws;
+  if (sp > 1) ws = at::empty({sp, M, N}, x.options().dtype(at::kFloat));
+  launch_gemm8(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), ea, eb, R, res, y.data_ptr(),
+               sp > 1 ? ws.data_ptr<float>() : nullptr, M, N, K, sp, stream());
+  return y;
+}
+
 // ------------------------------------------------------------------ attention
 static const int* int_ptr(const optional<Tensor>& t, Tensor& keep) {
   if (!t || !t->defined()) return nullptr;
@@ -830,6 +875,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nf4_pack", &nf4_pack);
   m.def("nf4_absmax_t", &nf4_absmax_t);
   m.def("gemm_nf4", &gemm_nf4);
+  m.def("gemm8", &gemm8);
   m.def("gemm_nf4_t", &gemm_nf4_t);
   m.def("gemm_bf16", &gemm_bf16);
   m.def("gemm_bf16_t", &gemm_bf16_t);

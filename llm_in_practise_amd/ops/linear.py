@@ -133,6 +133,30 @@ def _base_gemm_t(dy, base, ext_a=None, ext_b=None):
 
 _KEY = [0x5DEECE66D << 20]
 
+# "gradient final" listeners (parallel/ddp.py bucket overlap): called with the parameter whose
+# flat-buffer gradient a fused backward kernel has just accumulated in place (those gradients
+# bypass autograd's AccumulateGrad, so post_accumulate_grad_hooks do not fire for them)
+_GRAD_READY: list = []
+
+
+def register_grad_ready(fn):
+    import weakref
+    ref = weakref.WeakMethod(fn) if hasattr(fn, "__self__") else (lambda f=fn: f)
+    _GRAD_READY.append(ref)
+    return ref
+
+
+def _notify_grad_ready(p):
+    dead = False
+    for r in _GRAD_READY:
+        f = r()
+        if f is None:
+            dead = True
+        else:
+            f(p)
+    if dead:
+        _GRAD_READY[:] = [r for r in _GRAD_READY if r() is not None]
+
 
 def next_dropout_key() -> int:
     """Counter-based dropout stream: every call gets a fresh 63-bit key (deterministic given
@@ -297,6 +321,8 @@ class _FusedLinearFn(torch.autograd.Function):
                     out, ret = dest(2 * i + 1)                                     # dB [n_i, r] += dy_iᵀ·xa_s
                     native().lora_acc(xa_list[i], dy, br.c0, n_i, out, True, None, None, 0.0, 0, deterministic())
                     grads_ab[2 * i + 1] = out.to(b.dtype) if ret else None
+                    if not ret:
+                        _notify_grad_ready(ctx.ab_refs[2 * i + 1])
             else:
                 dyi = dy[:, br.c0:br.c1]
                 g = (dyi @ bf16_view(b, dy.dtype)) * br.scaling      # [T, r]  = d(xa)
@@ -327,6 +353,8 @@ class _FusedLinearFn(torch.autograd.Function):
                                       bf16_view(ab[2 * i], dy.dtype) if upd is not None else None,
                                       br.dropout if key is not None else 0.0, key or 0, deterministic())
                     grads_ab[2 * i] = out.to(ab[2 * i].dtype) if (ret and ctx.needs_input_grad[5 + 2 * i]) else None
+                    if not ret and ctx.needs_input_grad[5 + 2 * i]:
+                        _notify_grad_ready(ctx.ab_refs[2 * i])
             elif dx is not None and key is not None:   # LoRA input grad through the regenerated dropout mask
                 native().dropout_bwd_add(dx, g_list[i] @ bf16_view(ab[2 * i], dy.dtype), br.dropout, key)
         dres = dy if ctx.has_residual else None

@@ -1,12 +1,24 @@
-"""Data parallel: ``DDP(model, device_ids=[local_rank])`` semantics.
+"""Data parallel: ``DDP(model, device_ids=[local_rank])`` semantics
+(``LLM_Distributed_Trainning/PyTorch/ddp_basics/ddp_gpt_wikitext2.py:274``).
 
 MI355X design: gradients live in ONE flat fp32 buffer (owned by the fused optimizer, see
 ``optim/adamw.py``), so the data-parallel reduction is bucketed over that buffer and never
-packs/unpacks.  Buckets are sized for xGMI rings (default 64 MiB, far larger than torch's
-25 MiB: intra-node RCCL rings are per-link bandwidth-bound, so fewer, larger collectives
-win); LoRA-sized buffers (15-60 MB) are a single collective.  Buckets are issued on a
-side stream in reverse layer order after the boundary micro-step's backward;
-``no_sync()`` skips the reduction on non-boundary gradient-accumulation micro-steps.
+packs/unpacks.  Buckets are contiguous ranges of the flat buffer cut at parameter boundaries
+in REVERSE parameter order (the order backward produces gradients).
+
+Overlap with the backward: every parameter reports "gradient final" — through a
+``post_accumulate_grad_hook`` for ordinary autograd leaves, and through
+:func:`ops.linear.register_grad_ready` for the LoRA adapters whose gradients the fused
+kernels accumulate in place — and the moment a bucket's last parameter reports, the bucket's
+all-reduce is issued on a side HIP stream (ordered after the producing kernels by an event),
+so RCCL over xGMI runs while the GPU computes the rest of the backward.  ``allreduce_grads()``
+(after the boundary micro-step's backward) only flushes buckets whose parameters received no
+gradient and joins the streams.  ``no_sync()`` skips the reduction on non-boundary
+gradient-accumulation micro-steps.
+
+Bucket size: xGMI rings are per-link bandwidth-bound, so buckets are large (default 32 MiB,
+never fewer than ~4 per model so the first can start early); LoRA-sized gradient sets
+(15-60 MB) become a few collectives.
 
 On start the module's parameters and buffers are broadcast from rank 0
 (``sync_module_states``).
@@ -22,23 +34,119 @@ import torch.nn as nn
 from .dist import all_reduce_mean_, is_dist
 
 
+class _Bucket:
+    __slots__ = ("start", "end", "params", "remaining", "launched")
+
+    def __init__(self, start: int, end: int, params: list[int]):
+        self.start, self.end, self.params = start, end, params
+        self.remaining = len(params)
+        self.launched = False
+
+
 class DistributedDataParallel(nn.Module):
-    def __init__(self, module: nn.Module, grad_buffer: torch.Tensor | None = None, bucket_mb: float = 64.0,
+    def __init__(self, module: nn.Module, grad_buffer: torch.Tensor | None = None, bucket_mb: float | None = None,
                  broadcast_buffers: bool = True, device_ids=None, find_unused_parameters: bool = False,
-                 overlap: bool = True, **_):
+                 overlap: bool = True, flat=None, **_):
         super().__init__()
         self.module = module
-        self.grad_buffer = grad_buffer
-        self.bucket_elems = int(bucket_mb * (1 << 20) / 4)
+        self.flat = flat
+        self.grad_buffer = flat.grad if flat is not None else grad_buffer
         self._sync = True
-        self._pending = []
-        self.overlap = overlap and grad_buffer is not None and torch.cuda.is_available()
+        self.launch_log: list[tuple[int, str]] = []      # (bucket, "hook" | "flush") for the last step
         if is_dist():
             with torch.no_grad():
                 for t in list(module.parameters()) + (list(module.buffers()) if broadcast_buffers else []):
                     dist.broadcast(t.data, src=0)
-        self._stream = torch.cuda.Stream() if self.overlap else None
+        self.overlap = overlap and flat is not None and is_dist()
+        self._cuda = self.grad_buffer is not None and self.grad_buffer.is_cuda
+        self._stream = torch.cuda.Stream(device=self.grad_buffer.device) if (self.overlap and self._cuda) else None
+        self._works: list = []
+        if self.grad_buffer is not None:
+            total = self.grad_buffer.numel()
+            cap = int((bucket_mb if bucket_mb is not None else 32.0) * (1 << 20) / 4)
+            if bucket_mb is None:
+                cap = max(1 << 20, min(cap, total // 4))
+            self.bucket_elems = max(1, cap)
+        if self.overlap:
+            self._build_buckets()
+            self._hooks = []
+            from ..ops.linear import register_grad_ready
+            self._listener = register_grad_ready(self._on_ready)
+            for p in flat.params:
+                if hasattr(p, "register_post_accumulate_grad_hook"):
+                    self._hooks.append(p.register_post_accumulate_grad_hook(self._on_accumulated))
 
+    # ------------------------------------------------------------------ buckets
+    def _build_buckets(self):
+        fp = self.flat
+        order = sorted(range(len(fp.params)), key=lambda i: fp.offsets[i], reverse=True)
+        self._bucket_of: dict[int, int] = {}
+        self._index = {id(p): i for i, p in enumerate(fp.params)}
+        self._buckets: list[_Bucket] = []
+        end = fp.numel
+        cur: list[int] = []
+        for i in order:
+            cur.append(i)
+            start = fp.offsets[i]
+            if end - start >= self.bucket_elems:
+                self._buckets.append(_Bucket(start, end, cur))
+                end, cur = start, []
+        if cur:
+            self._buckets.append(_Bucket(0, end, cur))
+        elif self._buckets:
+            self._buckets[-1].start = 0
+        for b, bk in enumerate(self._buckets):
+            for i in bk.params:
+                self._bucket_of[i] = b
+        self._ready = [False] * len(fp.params)
+
+    def buckets(self) -> list[torch.Tensor]:
+        g = self.grad_buffer
+        if self.overlap:
+            return [g[b.start:b.end] for b in self._buckets]
+        return [g[s:s + self.bucket_elems] for s in range(0, g.numel(), self.bucket_elems)]
+
+    def _launch(self, b: int, why: str):
+        bk = self._buckets[b]
+        if bk.launched:
+            return
+        bk.launched = True
+        self.launch_log.append((b, why))
+        view = self.grad_buffer[bk.start:bk.end]
+        if self._stream is not None:
+            self._stream.wait_stream(torch.cuda.current_stream(view.device))
+            with torch.cuda.stream(self._stream):
+                all_reduce_mean_(view)
+        else:       # gloo / CPU: an async collective on the process group's own thread
+            self._works.append((dist.all_reduce(view, async_op=True), view))
+
+    def _mark(self, i: int):
+        if not self._sync or self._ready[i]:
+            return
+        self._ready[i] = True
+        b = self._bucket_of[i]
+        bk = self._buckets[b]
+        bk.remaining -= 1
+        if bk.remaining == 0:
+            self._launch(b, "hook")
+
+    def _on_accumulated(self, p: torch.Tensor):
+        i = self._index.get(id(p))
+        if i is None or not self._sync:
+            return
+        o = self.flat.offsets[i]
+        if p.grad is not None and p.grad.data_ptr() != self.flat.grad_ptrs[i]:
+            # low-precision parameter: fold its separately allocated grad into the flat buffer now
+            self.flat.grad[o:o + p.numel()].add_(p.grad.reshape(-1).float())
+            p.grad = None
+        self._mark(i)
+
+    def _on_ready(self, p: torch.Tensor):
+        i = self._index.get(id(p))
+        if i is not None:
+            self._mark(i)
+
+    # ------------------------------------------------------------------ API
     def forward(self, *args, **kw):
         return self.module(*args, **kw)
 
@@ -51,10 +159,6 @@ class DistributedDataParallel(nn.Module):
         finally:
             self._sync = prev
 
-    def buckets(self) -> list[torch.Tensor]:
-        g = self.grad_buffer
-        return [g[s:s + self.bucket_elems] for s in range(0, g.numel(), self.bucket_elems)]
-
     def allreduce_grads(self):
         """Average gradients across ranks (call after the last micro-step's backward)."""
         if not is_dist() or not self._sync:
@@ -64,16 +168,26 @@ class DistributedDataParallel(nn.Module):
                 if p.grad is not None:
                     all_reduce_mean_(p.grad)
             return
-        if self.overlap:
-            cur = torch.cuda.current_stream()
-            self._stream.wait_stream(cur)
-            with torch.cuda.stream(self._stream):
-                for b in reversed(self.buckets()):
-                    all_reduce_mean_(b)
-            cur.wait_stream(self._stream)
-        else:
-            for b in self.buckets():
+        if not self.overlap:
+            for b in reversed(self.buckets()):
                 all_reduce_mean_(b)
+            return
+        for b, bk in enumerate(self._buckets):       # params that got no gradient this step
+            if not bk.launched:
+                self._launch(b, "flush")
+        if self._stream is not None:
+            torch.cuda.current_stream(self.grad_buffer.device).wait_stream(self._stream)
+        for work, view in self._works:
+            work.wait()
+            view.div_(dist.get_world_size())
+        self._works = []
+        for bk in self._buckets:
+            bk.launched = False
+            bk.remaining = len(bk.params)
+        self._ready = [False] * len(self._ready)
+
+    def reset_log(self):
+        self.launch_log = []
 
 
 DDP = DistributedDataParallel

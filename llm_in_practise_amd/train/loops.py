@@ -131,7 +131,7 @@ def train_lm(model: nn.Module, train_ds, cfg: LoopConfig, eval_ds=None, meta: di
         opt = build_optimizer("adamw", params, cfg.lr, cfg.weight_decay, max_grad_norm=cfg.clip_grad_norm)
         if cfg.strategy == "ddp" and world > 1:
             from ..parallel.ddp import DistributedDataParallel
-            ddp = DistributedDataParallel(model, grad_buffer=opt.grad_buffer)
+            ddp = DistributedDataParallel(model, flat=opt.flat)
         bs = cfg.batch_size
     n = len(train_ds)
     steps_per_epoch = max(1, (math.ceil(n / world) // bs) // cfg.grad_accum)

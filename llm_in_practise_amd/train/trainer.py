@@ -313,7 +313,8 @@ class Trainer:
         if self.engine is None and self.world > 1:
             from ..parallel.ddp import DistributedDataParallel
             gb = getattr(self.optimizer, "grad_buffer", None)
-            self.ddp = DistributedDataParallel(self.model, grad_buffer=gb if isinstance(gb, torch.Tensor) else None)
+            self.ddp = DistributedDataParallel(self.model, grad_buffer=gb if isinstance(gb, torch.Tensor) else None,
+                                               flat=getattr(self.optimizer, "flat", None))
 
     # ------------------------------------------------------------------ loss
     def _to_device(self, batch):

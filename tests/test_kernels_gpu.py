@@ -558,3 +558,31 @@ def test_lora_fused_kernels(native_ext, M, K, r, p):
     da2 = torch.zeros(r, K, device=DEV)
     native_ext.lora_acc(gg, x, 0, K, da2, False, None, None, 0.0, 0, False)
     assert rel_err(da2, gg.t() @ x.float()) < 1e-2
+
+
+# ----------------------------------------------------------------------------- 8-phase GEMM
+@pytest.mark.parametrize("M,N,K,splits,lora,resid", [(256, 256, 64, 1, False, False), (512, 768, 512, 1, True, True),
+                                                     (300, 520, 192, 1, True, False), (2048, 1024, 1024, 4, True, True),
+                                                     (257, 264, 640, 2, False, True), (64, 4096, 4096, 0, False, False)])
+def test_gemm8_matches_fp32(native_ext, M, N, K, splits, lora, resid):
+    torch.manual_seed(0)
+    x = (torch.rand(M, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    w = (torch.rand(N, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    ea = (torch.randn(M, 32, device=DEV)).to(torch.bfloat16) if lora else None
+    eb = (0.1 * torch.randn(N, 32, device=DEV)).to(torch.bfloat16) if lora else None
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16) if resid else None
+    y = native_ext.gemm8(x, w, ea, eb, res, splits)
+    want = x.float() @ w.float().t()
+    if lora:
+        want += ea.float() @ eb.float().t()
+    if resid:
+        want += res.float()
+    assert rel_err(y, want) < 1e-2
+
+
+def test_gemm8_strided_input(native_ext):
+    """x may be a column slice of a wider activation (row stride != K)"""
+    big = torch.randn(512, 1024 + 64, device=DEV).to(torch.bfloat16)
+    x = big[:, 64:]
+    w = torch.randn(256, 1024, device=DEV).to(torch.bfloat16)
+    assert rel_err(native_ext.gemm8(x, w, None, None, None, 1), x.float() @ w.float().t()) < 1e-2
