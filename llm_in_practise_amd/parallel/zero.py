@@ -9,13 +9,25 @@ MI355X, ``gloo`` on CPU):
 * stage 2: gradients ``reduce_scatter_tensor``-ed straight into the owner's shard (bucketed
   by ``reduce_bucket_size``); grad-norm from shard partial sums + one scalar all-reduce.
 * stage 3: parameters partitioned per *unit* (each block of a ModuleList, plus the root).
-  A unit's full flat weight is all-gathered in a forward pre-hook and its storage freed
-  (``resize_(0)``) after the forward unless it is under ``stage3_param_persistence_threshold``;
-  a hook on the unit's output gradient re-gathers it before its backward; once the unit's
-  gradients are accumulated they are reduce-scattered into the fp32 shard gradient and the
-  full buffers are freed again.  Frozen parameters (NF4 bases) stay replicated — only
-  trainable parameters and their optimizer state are partitioned (QLoRA + ZeRO-3, SURVEY
-  §7.5 option 2).
+  ``ds_zero3_config.json`` semantics (``Fine-Tuning/ds_zero3_config.json:13-21``):
+    - a unit's full flat weight is all-gathered in its forward pre-hook (or was PREFETCHED: when a
+      unit is used, the next units in the recorded execution order are all-gathered
+      asynchronously — ``async_op`` RCCL on its own stream — until ``stage3_prefetch_bucket_size``
+      parameters are in flight, never exceeding ``stage3_max_live_parameters`` live);
+    - after its forward a unit is freed (``resize_(0)``) unless it is persistent
+      (``stage3_param_persistence_threshold``) or will be reused by the backward within
+      ``stage3_max_reuse_distance`` parameters;
+    - a hook on the unit's output gradient re-gathers it for its backward and prefetches the
+      units the backward visits next;
+    - finished units' gradients are packed rank-major into persistent bucket buffers and
+      reduce-scattered asynchronously (``overlap_comm``) in ``reduce_bucket_size`` buckets while
+      the backward continues; ``step()`` joins them.
+  Frozen parameters (NF4 bases) stay replicated — only trainable parameters and their optimizer
+  state are partitioned (QLoRA + ZeRO-3, SURVEY §7.5 option 2).
+* no host synchronisation in ``step()`` (bf16 / fp32): the global-norm clip coefficient stays on
+  the device and feeds the fused AdamW kernel.
+* checkpoints re-partition on load when the world size changed (per-unit / flat layouts are
+  rebuilt from every old rank's shard file).
 * ``offload_optimizer: cpu``: fp32 master shard and Adam moments live in (pinned) host memory;
   the update is the native OpenMP/AVX host AdamW (``csrc/cpu/cpu_adam.cpp``); gradients
   stream D2H and the updated compute-dtype shard H2D.
@@ -88,8 +100,9 @@ class LossScaler:
 class _Unit:
     """A stage-3 partition unit: trainable params of one module, flattened and sharded."""
 
-    def __init__(self, name, module, params, world, rank, dtype, device):
+    def __init__(self, name, module, params, world, rank, dtype, device, index=0):
         self.name, self.module, self.params = name, module, params
+        self.index = index
         self.shapes = [p.shape for p in params]
         self.numels = [p.numel() for p in params]
         n = sum(self.numels)
@@ -106,6 +119,7 @@ class _Unit:
         self.shard = full[rank * self.shard_n:(rank + 1) * self.shard_n].clone()
         self.full = full
         self.gathered = True
+        self.work = None                  # in-flight async all-gather (prefetch)
         self._point_params()
         self.grads_ready = 0
 
@@ -115,18 +129,38 @@ class _Unit:
             p.data = self.full[o:o + k].view(s)
             o += k
 
-    def gather(self):
+    @property
+    def live(self) -> bool:
+        return self.gathered or self.work is not None
+
+    def gather(self, async_op: bool = False) -> bool:
+        """All-gather the full weight.  ``async_op``: issue and return (prefetch); a later
+        ``gather()`` joins it.  Returns True when a collective was issued."""
         if self.gathered:
-            return
+            return False
+        if self.work is not None:
+            if not async_op:
+                self.work.wait()
+                self.work = None
+                self.gathered = True
+            return False
         st = self.full.untyped_storage()
         st.resize_(self.npad * self.full.element_size())
         if self.world > 1:
-            dist.all_gather_into_tensor(self.full, self.shard)
+            w = dist.all_gather_into_tensor(self.full, self.shard, async_op=async_op)
+            if async_op:
+                self.work = w
+                return True
         else:
             self.full.copy_(self.shard)
         self.gathered = True
+        return True
 
     def release(self):
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+            self.gathered = True
         if not self.gathered:
             return
         self.full.untyped_storage().resize_(0)
@@ -233,7 +267,7 @@ class ZeroEngine:
             with torch.no_grad():
                 for p in self.params:
                     dist.broadcast(p.data, src=0)
-        self.units = [_Unit(f"u{i}", u, groups[id(u)], W, r, self.params[0].dtype, self.device)
+        self.units = [_Unit(f"u{i}", u, groups[id(u)], W, r, self.params[0].dtype, self.device, index=i)
                       for i, u in enumerate(order)]
         self.master = torch.cat([u.shard.float() for u in self.units])
         self.grad_shard = torch.zeros_like(self.master)
@@ -241,8 +275,26 @@ class ZeroEngine:
         for u in self.units:
             self.unit_offsets.append(o)
             o += u.shard_n
-        thr = self.cfg.zero.stage3_param_persistence_threshold
+        z = self.cfg.zero
+        thr = z.stage3_param_persistence_threshold
         self.persistent = {id(u): (u.n < thr or u.module is self.module) for u in self.units}
+        self.prefetch_bucket = int(z.stage3_prefetch_bucket_size)
+        self.max_live = int(z.stage3_max_live_parameters)
+        self.max_reuse = int(z.stage3_max_reuse_distance)
+        self.reduce_bucket = max(1, int(z.reduce_bucket_size))
+        self.overlap_comm = bool(z.overlap_comm) or True   # async collectives are always safe here
+        self.fwd_order: list[int] = [u.index for u in self.units if u.module is not self.module]
+        self._recorded: list[int] = []
+        self._recording = True
+        self.event_log: list[tuple[str, int]] = []      # ("issue" | "use_fwd" | "use_bwd", unit)
+        self.log_events = False
+        self._pending_units: list[_Unit] = []
+        self._pending_n = 0
+        self._bucket = None               # index of the open bucket in _rs_pool
+        self._bucket_cap = 0
+        self._busy: set[int] = set()      # pool entries whose reduced output is not consumed yet
+        self._rs_works: list = []
+        self._rs_pool: list = []
         for u in self.units:
             if u.module is not self.module:
                 u.module.register_forward_pre_hook(self._pre_fwd(u))
@@ -253,22 +305,76 @@ class ZeroEngine:
             if not self.persistent[id(u)]:
                 u.release()
 
+    # ---- stage-3 scheduling -------------------------------------------------------------
+    def _log(self, what, u):
+        if self.log_events:
+            self.event_log.append((what, u.index))
+
+    def _live_params(self) -> int:
+        return sum(u.n for u in self.units if u.live)
+
+    def _prefetch(self, seq: list[int], pos: int):
+        """Issue async all-gathers for the units after ``pos`` in ``seq`` (prefetch bucket /
+        max-live bounded)."""
+        if self.prefetch_bucket <= 0:
+            return
+        budget, live = 0, self._live_params()
+        for idx in seq[pos + 1:]:
+            u = self.units[idx]
+            if budget >= self.prefetch_bucket:
+                break
+            budget += u.n
+            if u.live:
+                continue
+            if live + u.n > self.max_live:
+                break
+            if u.gather(async_op=True):
+                self._log("issue", u)
+            live += u.n
+
+    def _reuse_distance(self, u) -> int:
+        """Parameters touched between this unit's forward and its backward (fwd of the later
+        units + their bwd)."""
+        seq = self.fwd_order
+        if u.index not in seq:
+            return 1 << 62
+        after = seq[seq.index(u.index) + 1:]
+        return 2 * sum(self.units[i].n for i in after)
+
     def _pre_fwd(self, u):
         def hook(mod, args):
+            self._log("use_fwd", u)
             u.gather()
+            if self._recording and torch.is_grad_enabled() and u.index not in self._recorded:
+                self._recorded.append(u.index)
+            seq = self.fwd_order
+            if u.index in seq:
+                self._prefetch(seq, seq.index(u.index))
         return hook
 
     def _post_fwd(self, u):
         def hook(mod, args, out):
-            if self.persistent[id(u)] or not torch.is_grad_enabled():
-                if not self.persistent[id(u)]:
-                    u.release()
+            if self.persistent[id(u)]:
+                return out
+            if not torch.is_grad_enabled():
+                u.release()
                 return out
             t = out[0] if isinstance(out, (tuple, list)) else out
             if isinstance(t, torch.Tensor) and t.requires_grad:
-                t.register_hook(lambda g: (u.gather(), g)[1])
-            u.release()
+                t.register_hook(self._pre_bwd(u))
+            if self._reuse_distance(u) >= self.max_reuse:
+                u.release()
             return out
+        return hook
+
+    def _pre_bwd(self, u):
+        def hook(g):
+            self._log("use_bwd", u)
+            u.gather()
+            seq = self.fwd_order[::-1]
+            if u.index in seq:
+                self._prefetch(seq, seq.index(u.index))
+            return g
         return hook
 
     def _grad_hook(self, u):
@@ -276,27 +382,102 @@ class ZeroEngine:
             u.grads_ready += 1
             if u.grads_ready == len(u.params):
                 u.grads_ready = 0
-                self._reduce_unit(u)
+                self._queue_reduce(u)
         return hook
 
-    def _reduce_unit(self, u):
-        g = torch.zeros(u.npad, dtype=torch.float32, device=self.device)
+    def _queue_reduce(self, u):
+        """Pack a finished unit's gradients (rank-major) into the open bucket at once — so its
+        full weights and grads are freed now — and reduce-scatter the bucket when it is full."""
+        W = self.world
+        cap = max(1, self.reduce_bucket // max(1, W))
+        if self._bucket is not None and self._pending_n + u.shard_n > self._bucket_cap:
+            self._flush_reduce()
+        if self._bucket is None:
+            self._bucket_cap = max(cap, u.shard_n)
+            self._bucket = self._rs_buffers(self._bucket_cap)
+        bi, _, _ = self._rs_pool[self._bucket]
+        view = bi[:W * self._bucket_cap].view(W, self._bucket_cap)
+        col = self._pending_n
+        flat = torch.zeros(u.npad, dtype=torch.float32, device=self.device)
         o = 0
         for p, k in zip(u.params, u.numels):
             if p.grad is not None:
-                g[o:o + k].copy_(p.grad.reshape(-1))
+                flat[o:o + k].copy_(p.grad.reshape(-1))
                 p.grad = None
             o += k
-        i = self.units.index(u)
-        dst = self.grad_shard[self.unit_offsets[i]:self.unit_offsets[i] + u.shard_n]
-        if self.world > 1:
-            part = torch.empty(u.shard_n, dtype=torch.float32, device=self.device)
-            dist.reduce_scatter_tensor(part, g, op=dist.ReduceOp.SUM)
-            dst.add_(part, alpha=1.0 / self.world)
-        else:
-            dst.add_(g[:u.shard_n])
+        view[:, col:col + u.shard_n].copy_(flat.view(W, u.shard_n))
+        self._pending_units.append(u)
+        self._pending_n += u.shard_n
         if not self.persistent[id(u)]:
             u.release()
+        if self._pending_n >= self._bucket_cap:
+            self._flush_reduce()
+
+    def _retire(self, block: bool = False):
+        """Fold finished reduce-scatters into the gradient shard and free their buffers
+        (``block``: also wait for the oldest one still in flight)."""
+        keep = []
+        for j, (work, out, units, i) in enumerate(self._rs_works):
+            done = work is None or work.is_completed() or (block and j == 0)
+            if not done:
+                keep.append((work, out, units, i))
+                continue
+            if work is not None:
+                work.wait()
+            col = 0
+            for u in units:
+                o = self.unit_offsets[u.index]
+                self.grad_shard[o:o + u.shard_n].add_(out[col:col + u.shard_n], alpha=1.0 / self.world)
+                col += u.shard_n
+            self._busy.discard(i)
+            bi, bo, _ = self._rs_pool[i]
+            self._rs_pool[i] = (bi, bo, None)
+        self._rs_works = keep
+
+    def _rs_buffers(self, n: int):
+        """A persistent (in, out) pair of bucket buffers with room for ``n`` shard elements per
+        rank (at most 4 pairs: beyond that the oldest in-flight reduce-scatter is joined)."""
+        self._retire()
+        while True:
+            for i, (bi, bo, work) in enumerate(self._rs_pool):
+                if bo.numel() >= n and i not in self._busy:
+                    return i
+            if len(self._rs_pool) < 4 or not self._rs_works:
+                break
+            self._retire(block=True)
+        free = [i for i in range(len(self._rs_pool)) if i not in self._busy]
+        bi = torch.zeros(self.world * n, dtype=torch.float32, device=self.device)
+        bo = torch.zeros(n, dtype=torch.float32, device=self.device)
+        if free and len(self._rs_pool) >= 4:     # replace a too-small idle pair
+            self._rs_pool[free[0]] = (bi, bo, None)
+            return free[0]
+        self._rs_pool.append((bi, bo, None))
+        return len(self._rs_pool) - 1
+
+    def _flush_reduce(self):
+        units, n, i = self._pending_units, self._pending_n, self._bucket
+        self._pending_units, self._pending_n, self._bucket = [], 0, None
+        if not units:
+            return
+        bi, bo, _ = self._rs_pool[i]
+        W, cap = self.world, self._bucket_cap
+        src = bi[:W * cap]
+        if n < cap:                       # compact the packed columns of a partial bucket
+            src = bi[:W * cap].view(W, cap)[:, :n].contiguous().view(-1)
+        out = bo[:n]
+        work = None
+        if W > 1:
+            work = dist.reduce_scatter_tensor(out, src, op=dist.ReduceOp.SUM, async_op=True)
+        else:
+            out.copy_(src[:n])
+        self._rs_pool[i] = (bi, bo, work)
+        self._busy.add(i)
+        self._rs_works.append((work, out, units, i))
+
+    def _join_reduces(self):
+        self._flush_reduce()
+        while self._rs_works:
+            self._retire(block=True)
 
     # ------------------------------------------------------------------ optimizer state
     def _init_optimizer_state(self):
@@ -396,7 +577,11 @@ class ZeroEngine:
             for u in self.units:          # units whose params did not all receive grads
                 if u.grads_ready:
                     u.grads_ready = 0
-                    self._reduce_unit(u)
+                    self._queue_reduce(u)
+            self._join_reduces()
+            if self._recording and self._recorded:      # execution order seen by the first step
+                self.fwd_order = list(self._recorded)
+                self._recording = False
             return self.grad_shard
         if self.stage == 2:
             if self.world > 1:
@@ -420,8 +605,7 @@ class ZeroEngine:
     def _optimizer_step(self):
         g = self._reduce_grads()
         inv = 1.0 / self.scaler.scale if self.scaler.enabled else 1.0
-        overflow = False
-        if self.scaler.enabled:
+        if self.scaler.enabled:           # fp16 dynamic loss scaling needs the overflow decision on the host
             bad = torch.tensor([0.0 if torch.isfinite(g).all() else 1.0], device=self.device)
             if self.world > 1:
                 dist.all_reduce(bad, op=dist.ReduceOp.MAX)
@@ -431,12 +615,14 @@ class ZeroEngine:
                 self._skipped += 1
                 self.zero_grad()
                 return
-        sumsq = self._global_sumsq(g) * inv * inv
+        sumsq = self._global_sumsq(g) * (inv * inv)
         norm = sumsq.sqrt()
         self.last_grad_norm = norm.reshape(())
-        coef = inv
+        # clip coefficient stays a device tensor: no host sync in the step (bf16 / fp32)
         if self.clip > 0:
-            coef = inv * min(1.0, self.clip / (norm.item() + 1e-6))
+            coef = torch.clamp(self.clip / (norm + 1e-6), max=1.0) * inv
+        else:
+            coef = torch.full_like(norm, inv)
         lr = self.param_groups[0]["lr"]
         self.opt_step += 1
         b1, b2 = self.betas
@@ -444,27 +630,46 @@ class ZeroEngine:
             from ..ops._native import cpu_native
             gc = g.float().cpu()
             cpu_native().adamw_step(self.master, gc, self.exp_avg, self.exp_avg_sq, lr, b1, b2, self.eps, self.wd,
-                                    self.opt_step, coef)
+                                    self.opt_step, float(coef.reshape(())))
         elif use_native(self.master):
             gg = g.float().contiguous() if g.dtype != torch.float32 or not g.is_contiguous() else g
-            if coef != 1.0:
-                gg = gg * coef
+            gs = torch.cat([norm.reshape(1), coef.reshape(1)]).float()
             native().adamw(self.master, gg, self.exp_avg, self.exp_avg_sq, None, lr, b1, b2, self.eps, self.wd,
-                           self.opt_step, None, None)
+                           self.opt_step, gs, None)
         else:
-            ref.adamw_step(self.master, g.float() * coef, self.exp_avg, self.exp_avg_sq, self.opt_step, lr, b1, b2,
-                           self.eps, self.wd)
+            ref.adamw_step(self.master, g.float() * coef.to(g.device), self.exp_avg, self.exp_avg_sq, self.opt_step,
+                           lr, b1, b2, self.eps, self.wd)
         self._publish_params()
         self.zero_grad()
 
     def _publish_params(self):
         m = self.master.to(self.device, non_blocking=True)
         if self.stage == 3:
+            pers = []
             for u, o in zip(self.units, self.unit_offsets):
                 u.shard.copy_(m[o:o + u.shard_n])
-                if u.gathered:            # persistent units keep a live full copy: refresh it
-                    u.gathered = False
-                    u.gather()
+                if self.persistent[id(u)]:
+                    pers.append(u)
+                else:
+                    u.release()           # stale full copies (kept for reuse / prefetched) are dropped
+            if not pers:
+                return
+            # persistent units refresh their full copy with ONE coalesced all-gather (rank-major)
+            S = sum(u.shard_n for u in pers)
+            send = torch.cat([u.shard for u in pers])
+            if self.world > 1:
+                recv = torch.empty(self.world * S, dtype=send.dtype, device=send.device)
+                dist.all_gather_into_tensor(recv, send)
+                view = recv.view(self.world, S)
+            else:
+                view = send.view(1, S)
+            col = 0
+            for u in pers:
+                if not u.gathered:
+                    u.full.untyped_storage().resize_(u.npad * u.full.element_size())
+                    u.gathered = True
+                u.full.view(self.world, u.shard_n).copy_(view[:, col:col + u.shard_n])
+                col += u.shard_n
             return
         self.flat_model[self.shard_slice].copy_(m)
         if self.world > 1 and self.stage > 0:
@@ -512,6 +717,7 @@ class ZeroEngine:
                        os.path.join(d, "mp_rank_00_model_states.pt"))
         torch.save({"master": self.master.cpu(), "exp_avg": self.exp_avg.cpu(), "exp_avg_sq": self.exp_avg_sq.cpu(),
                     "opt_step": self.opt_step, "zero_stage": self.stage, "rank": self.rank, "world": self.world,
+                    "layout": self._layout(),
                     "lr_scheduler": self.lr_scheduler.state_dict() if self.lr_scheduler else None},
                    os.path.join(d, f"zero_pp_rank_{self.rank}_mp_rank_00_optim_states.pt"))
         if is_dist():
@@ -527,12 +733,17 @@ class ZeroEngine:
                 tag = f.read().strip()
         d = os.path.join(load_dir, tag)
         ms = torch.load(os.path.join(d, "mp_rank_00_model_states.pt"), map_location="cpu", weights_only=True)
-        os_ = torch.load(os.path.join(d, f"zero_pp_rank_{self.rank}_mp_rank_00_optim_states.pt"),
+        os_ = torch.load(os.path.join(d, f"zero_pp_rank_{min(self.rank, ms.get('world_size', 1) - 1)}_mp_rank_00_optim_states.pt"),
                          map_location="cpu", weights_only=True)
-        assert os_["world"] == self.world, "re-partitioning across world sizes is not supported"
-        self.master.copy_(os_["master"])
-        self.exp_avg.copy_(os_["exp_avg"])
-        self.exp_avg_sq.copy_(os_["exp_avg_sq"])
+        if os_["world"] == self.world:
+            for k in ("master", "exp_avg", "exp_avg_sq"):
+                getattr(self, k).copy_(os_[k])
+        else:                             # re-partition: rebuild the full vectors from every old shard
+            old = [torch.load(os.path.join(d, f"zero_pp_rank_{r}_mp_rank_00_optim_states.pt"), map_location="cpu",
+                              weights_only=True) for r in range(os_["world"])]
+            for k in ("master", "exp_avg", "exp_avg_sq"):
+                full = self._unshard([o[k] for o in old], os_.get("layout"), os_["world"])
+                getattr(self, k).copy_(self._shard_of(full))
         self.opt_step = os_["opt_step"]
         if self.lr_scheduler is not None and os_.get("lr_scheduler"):
             self.lr_scheduler.load_state_dict(os_["lr_scheduler"])
@@ -540,6 +751,37 @@ class ZeroEngine:
         self.scaler.scale = ms["loss_scale"]
         self._publish_params()
         return d, ms.get("client_state", {})
+
+    # ------------------------------------------------------------------ re-partitioning helpers
+    def _layout(self) -> list[int]:
+        """World-independent partition layout: numel per stage-3 unit, or [n] for stages 0-2."""
+        return [u.n for u in self.units] if self.stage == 3 else [self.n]
+
+    def _unshard(self, shards: list[torch.Tensor], layout, world_old: int) -> torch.Tensor:
+        layout = layout or self._layout()
+        if self.stage == 0:               # replicated state
+            return shards[0][:layout[0]]
+        parts, offs = [], [0] * world_old
+        for n in layout:
+            sn = _pad_to(max(n, 1), world_old) // world_old
+            full = torch.cat([shards[r][offs[r]:offs[r] + sn] for r in range(world_old)])
+            parts.append(full[:n])
+            offs = [o + sn for o in offs]
+        return torch.cat(parts)
+
+    def _shard_of(self, full: torch.Tensor) -> torch.Tensor:
+        """This rank's shard of a full (unpadded) state vector in the current layout."""
+        if self.stage == 3:
+            out, o = [], 0
+            for u in self.units:
+                v = torch.zeros(u.npad, dtype=full.dtype)
+                v[:u.n] = full[o:o + u.n]
+                out.append(v[self.rank * u.shard_n:(self.rank + 1) * u.shard_n])
+                o += u.n
+            return torch.cat(out)
+        v = torch.zeros(self.npad, dtype=full.dtype)
+        v[:self.n] = full[:self.n]
+        return v[self.shard_slice]
 
     # DeepSpeed accessors used by the reference scripts
     def train_micro_batch_size_per_gpu(self):

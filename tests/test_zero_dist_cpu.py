@@ -66,9 +66,9 @@ def _worker(rank, world, port, stage, offload, ga, out):
     torch.distributed.destroy_process_group()
 
 
-def _oracle(steps=3, ga=1):
+def _oracle(steps=3, ga=1, n=3):
     torch.manual_seed(0)
-    net = Net()
+    net = Net(n=n)
     eng = ZeroEngine(net, _cfg(0, ga=ga))
     for s in range(steps):
         for mstep in range(ga):
@@ -221,3 +221,81 @@ def test_fsdp_api_full_shard_matches_single_process(tmp_path):
     want = _oracle()
     for k in want:
         assert torch.allclose(got[k], want[k], atol=2e-5), k
+
+
+# ----------------------------------------------------------------------------- stage-3 scheduling
+def _cfg3(prefetch, reuse, bucket=64):
+    c = _cfg(3)
+    c["zero_optimization"].update({"stage3_prefetch_bucket_size": prefetch, "stage3_max_reuse_distance": reuse,
+                                   "stage3_param_persistence_threshold": 0, "reduce_bucket_size": bucket,
+                                   "overlap_comm": True, "stage3_max_live_parameters": 10 ** 9})
+    return c
+
+
+def _prefetch_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    net = Net(n=5)
+    eng = ZeroEngine(net, _cfg3(prefetch=1, reuse=0))     # prefetch one unit ahead, free after every use
+    for step in range(3):                                 # step 0 records the execution order
+        eng.log_events = step > 0
+        x, y = _data(step, rank)
+        eng.backward(((eng(x) - y) ** 2).mean())
+        eng.step()
+    sd = eng.consolidated_state_dict()
+    if rank == 0:
+        torch.save({"log": eng.event_log, "order": eng.fwd_order, "sd": sd}, out)
+    torch.distributed.destroy_process_group()
+
+
+def test_stage3_prefetch_issues_gathers_ahead_of_use(tmp_path):
+    """Every block's all-gather is issued (async) while an EARLIER unit runs — before its own
+    forward / backward use — and training still matches the single-process oracle."""
+    out = str(tmp_path / "p.pt")
+    mp.spawn(_prefetch_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    r = torch.load(out, weights_only=True)
+    log, order = [tuple(e) for e in r["log"]], r["order"]
+    assert len(order) == 5
+    ahead, prev_use = 0, None
+    for pos, (what, u) in enumerate(log):
+        if what not in ("use_fwd", "use_bwd"):
+            continue
+        # prefetched = its gather was issued after the previous unit's use began, before this use
+        if prev_use is not None and ("issue", u) in log[prev_use:pos]:
+            ahead += 1
+        prev_use = pos
+    # per step: blocks 2..5 prefetched in the forward, 4..1 in the backward (2 logged steps)
+    assert ahead == 2 * (4 + 4), log
+    want = _oracle(steps=3, n=5)
+    for k in want:
+        assert torch.allclose(r["sd"][k], want[k], atol=2e-5), k
+
+
+def _repart_save(rank, world, port, d):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    for stage in (1, 3):
+        torch.manual_seed(0)
+        eng = ZeroEngine(Net(), _cfg(stage))
+        _train(eng, world, rank, steps=2)
+        eng.save_checkpoint(os.path.join(d, f"s{stage}"))
+    torch.distributed.destroy_process_group()
+
+
+def test_checkpoint_repartitions_across_world_sizes(tmp_path):
+    """A ZeRO-1 / ZeRO-3 checkpoint written by 2 ranks resumes in 1 process: the next step on the
+    concatenated batch equals the 2-rank oracle's third step."""
+    d = str(tmp_path / "ck")
+    mp.spawn(_repart_save, args=(2, _free_port(), d), nprocs=2, join=True)
+    want = _oracle(steps=3)
+    for stage in (1, 3):
+        torch.manual_seed(7)
+        eng = ZeroEngine(Net(), _cfg(stage))
+        eng.load_checkpoint(os.path.join(d, f"s{stage}"))
+        xs, ys = zip(*[_data(2, r) for r in range(2)])
+        eng.backward(((eng(torch.cat(xs)) - torch.cat(ys)) ** 2).mean())
+        eng.step()
+        got = eng.consolidated_state_dict()
+        for k in want:
+            assert torch.allclose(got[k], want[k], atol=2e-5), (stage, k)
