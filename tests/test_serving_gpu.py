@@ -132,4 +132,32 @@ def test_chunked_prefill_matches_whole_prefill(lm):
             assert all(s is None for s in e.slots)
         finally:
             e.shutdown()
-    assert outs[0] == outs[64]
+    # bf16 attention + M-dependent GEMM tiling make chunked and whole prefill agree to ~1 % (see
+    # test_chunked_prefill_hidden_states_match); greedy decoding of a random model has near-ties, so
+    # compare the first token of every request exactly and the rest statistically
+    assert [o[:1] for o in outs[0]] == [o[:1] for o in outs[64]]
+    same = sum(a == b for x, y in zip(outs[0], outs[64]) for a, b in zip(x, y))
+    total = sum(len(x) for x in outs[0])
+    assert same >= 0.6 * total, (outs[0], outs[64])
+
+
+def test_chunked_prefill_hidden_states_match(lm):
+    """Chunked prefill through the prefix/suffix attention kernel (queries at q_off over the cached
+    prefix) reproduces whole-prompt prefill hidden states to bf16 accuracy, for chunk sizes that do
+    and do not divide the 64-key tile."""
+    from llm_in_practise_amd.models.common import KVCache
+    cfg = lm.config
+    hd = cfg.hidden_size // cfg.num_attention_heads if not getattr(cfg, "head_dim", None) else cfg.head_dim
+    ids = torch.randint(0, 256, (1, 200), device="cuda", generator=torch.Generator(device="cuda").manual_seed(3))
+    with torch.no_grad():
+        c1 = KVCache(cfg.num_hidden_layers, 1, 512, cfg.num_key_value_heads, hd, torch.bfloat16, "cuda")
+        h1 = lm.model(ids, None, c1, None).float()
+        for chunk in (64, 50):
+            c2 = KVCache(cfg.num_hidden_layers, 1, 512, cfg.num_key_value_heads, hd, torch.bfloat16, "cuda")
+            hs = []
+            for s0 in range(0, 200, chunk):
+                c2.len = s0
+                hs.append(lm.model(ids[:, s0:s0 + chunk], None, c2, None))
+            h2 = torch.cat(hs).float()
+            err = (h2 - h1).norm(dim=-1) / h1.norm(dim=-1)
+            assert err.max().item() < 0.03, (chunk, err.max().item())
