@@ -241,6 +241,7 @@ class ServingEngine:
                       "batches_total": 0, "running": 0, "decode_steps_total": 0}
         self.h_latency = _Histogram([0.05, 0.1, 0.25, 0.5, 1, 2, 5, 10, 30, 60])
         self.h_ttft = _Histogram([0.01, 0.025, 0.05, 0.1, 0.2, 0.5, 1, 2, 5])
+        self.queue_time_ewma: float | None = None
         self.cache = KVCache(cfg.num_hidden_layers, max_batch, self.max_len, cfg.num_key_value_heads, cfg.head_dim,
                              self.lm.lm_head.weight.dtype, self.device)
         self.cache.pos = torch.zeros(max_batch, dtype=torch.long, device=self.device)
@@ -389,6 +390,8 @@ class ServingEngine:
                 self._held = r
                 break
             budget -= len(r.prompt_ids)
+            qt = max(0.0, time.time() - r.t_arrive)     # router load signal (llm-d queue_time_ms)
+            self.queue_time_ewma = qt if self.queue_time_ewma is None else 0.8 * self.queue_time_ewma + 0.2 * qt
             new.append((free.pop(0), r))
         return new
 
@@ -656,6 +659,16 @@ class ServingEngine:
             "# TYPE lipa_num_requests_waiting gauge", f"lipa_num_requests_waiting {self.q.qsize()}",
             "# TYPE lipa_num_requests_running gauge", f"lipa_num_requests_running {s['running']}",
         ]
+        # KV occupancy: rows held by live slots over the cache capacity (vLLM gpu_cache_usage_perc role)
+        used = 0
+        try:
+            pos = self.cache.pos.tolist() if self.cache.pos is not None else []
+            used = sum(int(pos[i]) for i, sl in enumerate(self.slots) if sl is not None and i < len(pos))
+        except Exception:
+            pass
+        cap = max(1, self.max_batch * self.cache.max_len)
+        lines += ["# TYPE lipa_gpu_cache_usage_perc gauge", f"lipa_gpu_cache_usage_perc {used / cap:.6f}",
+                  "# TYPE lipa_queue_time_seconds gauge", f"lipa_queue_time_seconds {self.queue_time_ewma or 0.0:.6f}"]
         if self.prefix is not None:
             lines += ["# TYPE lipa_prefix_cache_queries_total counter",
                       f"lipa_prefix_cache_queries_total {self.prefix.query_tokens}",

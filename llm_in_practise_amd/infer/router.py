@@ -25,11 +25,26 @@ and implements the routing behaviour in front of per-GPU ``lipa serve`` processe
   flagged requests with 400 before any model is called;
 * ``/v1/models``, ``/health``, ``/metrics`` (Prometheus text: per-deployment requests / failures /
   cooldowns, fallbacks, guard blocks).
+* prefix / load-aware strategies of the reference's routers:
+  ``load_aware_prefix`` — llm-d (``08-LLM-Router/llm-d/llm-d-config.yaml:13-25``): a load score
+  from each backend's scraped ``/metrics`` with ``load_weights`` pending_requests 0.4,
+  gpu_cache_usage 0.3, ttft_ms 0.2, queue_time_ms 0.1, minus a prefix-affinity bonus for the
+  backend that served the longest matching prompt prefix (its KV / prefix cache is warm);
+  ``prefixaware`` / ``cache_aware`` — the vLLM router's ``--routing-logic``
+  (``vLLM-Router/vllm-router-deployment.yaml:34-35``, helm ``routingLogic: cache_aware``): longest
+  prefix match wins, least-busy otherwise (``cache_aware`` gives up affinity when that backend is
+  over ``cache_aware_imbalance`` × the least loaded one).
+  Backend statistics are scraped every ``health_check_interval`` seconds (lipa or vLLM metric
+  names); a backend that fails ``failure_threshold`` scrapes in a row is treated as down.
+
+FastAPI handlers run the blocking upstream calls in the threadpool, so requests are served
+concurrently (``in_flight`` / ``max_parallel_requests`` / least-busy see real concurrency).
 """
 from __future__ import annotations
 
 import collections
 import dataclasses
+import hashlib
 import random
 import threading
 import time
@@ -37,8 +52,12 @@ from typing import Callable
 
 from fastapi import FastAPI, Request
 from fastapi.responses import JSONResponse, PlainTextResponse
+from starlette.concurrency import run_in_threadpool
 
-STRATEGIES = ("simple-shuffle", "least-busy", "usage-based-routing", "latency-based-routing", "cost-based-routing")
+STRATEGIES = ("simple-shuffle", "least-busy", "usage-based-routing", "latency-based-routing", "cost-based-routing",
+              "load_aware_prefix", "prefixaware", "cache_aware")
+LLMD_LOAD_WEIGHTS = {"pending_requests": 0.4, "gpu_cache_usage": 0.3, "ttft_ms": 0.2, "queue_time_ms": 0.1}
+PREFIX_CHUNK = 256          # characters per prompt-prefix hash block
 
 
 class UpstreamError(Exception):
@@ -66,10 +85,78 @@ class Deployment:
     requests: int = 0
     failures: int = 0
     cooldowns: int = 0
+    # scraped backend load (load_aware_prefix): pending, gpu_cache_usage [0,1], ttft_ms, queue_time_ms
+    stats: dict = dataclasses.field(default_factory=dict)
+    scrape_fails: int = 0
+    down: bool = False
 
     @property
     def name(self) -> str:
         return f"{self.group}@{self.api_base}"
+
+
+def parse_prometheus(text: str) -> dict[str, float]:
+    out: dict[str, float] = {}
+    for line in text.splitlines():
+        if not line or line.startswith("#"):
+            continue
+        parts = line.split()
+        if len(parts) >= 2:
+            name = parts[0].split("{", 1)[0]
+            try:
+                out[name] = out.get(name, 0.0) + float(parts[1])
+            except ValueError:
+                pass
+    return out
+
+
+def backend_load(metrics: dict[str, float]) -> dict[str, float]:
+    """lipa (``infer/engine.py``) or vLLM metric names → the llm-d load signals."""
+    def get(*names, default=0.0):
+        for n in names:
+            if n in metrics:
+                return metrics[n]
+        return default
+
+    def mean(prefixes):
+        for p in prefixes:
+            c = metrics.get(p + "_count")
+            if c:
+                return metrics.get(p + "_sum", 0.0) / c
+        return 0.0
+    return {"pending_requests": get("lipa_num_requests_waiting", "vllm:num_requests_waiting"),
+            "gpu_cache_usage": get("lipa_gpu_cache_usage_perc", "vllm:gpu_cache_usage_perc", "vllm:kv_cache_usage_perc"),
+            "ttft_ms": 1000.0 * mean(["lipa_time_to_first_token_seconds", "vllm:time_to_first_token_seconds"]),
+            "queue_time_ms": 1000.0 * get("lipa_queue_time_seconds", default=mean(["vllm:request_queue_time_seconds"]))}
+
+
+def http_scraper(timeout: float = 3.0) -> Callable[[Deployment], dict]:
+    """GET ``<api_base without /v1>/metrics`` → load signals (raises on failure)."""
+    import httpx
+    client = httpx.Client(timeout=timeout)
+
+    def scrape(dep: Deployment) -> dict:
+        base = dep.api_base.rstrip("/")
+        if base.endswith("/v1"):
+            base = base[:-3]
+        r = client.get(base + "/metrics")
+        r.raise_for_status()
+        return backend_load(parse_prometheus(r.text))
+    return scrape
+
+
+def prompt_prefix_hashes(body: dict, chunk: int = PREFIX_CHUNK) -> list[str]:
+    """Chained content hashes of the prompt text in ``chunk``-character blocks (the router-level
+    analogue of the engine's token-block prefix hashes)."""
+    if body.get("messages"):
+        text = "".join(f"<{m.get('role', '')}>{m.get('content', '')}" for m in body["messages"])
+    else:
+        text = str(body.get("prompt", ""))
+    out, h = [], b""
+    for i in range(0, len(text) - len(text) % chunk, chunk):
+        h = hashlib.blake2b(h + text[i:i + chunk].encode(), digest_size=12).digest()
+        out.append(h.hex())
+    return out
 
 
 def load_config(cfg: dict | str) -> dict:
@@ -135,6 +222,17 @@ class Router:
         self.rng = random.Random(seed)
         self.lock = threading.Lock()
         self.counters = collections.Counter()
+        # prefix / load-aware routing (llm-d load_aware_prefix, vLLM router prefixaware / cache_aware)
+        self.load_weights = dict(LLMD_LOAD_WEIGHTS)
+        self.load_weights.update({k: float(v) for k, v in (rs.get("load_weights") or {}).items()})
+        self.prefix_weight = float(rs.get("prefix_weight", 0.5))
+        self.imbalance = float(rs.get("cache_aware_imbalance", 2.0))
+        self.scrape_interval = float(rs.get("health_check_interval", 5))
+        self.failure_threshold = int(rs.get("failure_threshold", 2))
+        self.prefix_owner: collections.OrderedDict[str, str] = collections.OrderedDict()
+        self.prefix_capacity = int(rs.get("prefix_table_size", 100_000))
+        self.scraper: Callable[[Deployment], dict] | None = None
+        self._last_scrape = -1e18
 
     @staticmethod
     def _fallback_map(spec) -> dict[str, list[str]]:
@@ -149,9 +247,74 @@ class Router:
         now = self.clock()
         return [d for d in self.groups.get(group, []) if d.cooldown_until <= now]
 
-    def pick(self, group: str, exclude: set[str] = frozenset()) -> Deployment | None:
+    # ------------------------------------------------------------------ backend load / prefix affinity
+    def refresh_stats(self, force: bool = False):
+        """Scrape every deployment's /metrics (at most once per health-check interval)."""
+        if self.scraper is None:
+            return
+        now = self.clock()
+        if not force and now - self._last_scrape < self.scrape_interval:
+            return
+        self._last_scrape = now
+        for deps in self.groups.values():
+            for d in deps:
+                try:
+                    st = self.scraper(d)
+                except Exception:
+                    d.scrape_fails += 1
+                    d.down = d.scrape_fails >= self.failure_threshold
+                    continue
+                d.stats, d.scrape_fails, d.down = st, 0, False
+
+    def _prefix_scores(self, hashes: list[str]) -> dict[str, float]:
+        """deployment name → fraction of the prompt's leading blocks it served last."""
+        if not hashes:
+            return {}
+        run: dict[str, int] = collections.Counter()
+        for h in hashes:
+            owner = self.prefix_owner.get(h)
+            if owner is None:
+                break
+            run[owner] += 1
+        return {k: v / len(hashes) for k, v in run.items()}
+
+    def _remember_prefix(self, hashes: list[str], dep: Deployment):
+        for h in hashes:
+            self.prefix_owner[h] = dep.name
+            self.prefix_owner.move_to_end(h)
+        while len(self.prefix_owner) > self.prefix_capacity:
+            self.prefix_owner.popitem(last=False)
+
+    def load_score(self, d: Deployment, cands: list[Deployment]) -> float:
+        """llm-d weighted load: each signal normalised by its max over the candidates."""
+        st = dict(d.stats)
+        st["pending_requests"] = st.get("pending_requests", 0.0) + d.in_flight
+        score = 0.0
+        for k, w in self.load_weights.items():
+            if k == "gpu_cache_usage":
+                score += w * min(1.0, max(0.0, st.get(k, 0.0)))
+                continue
+            mx = max((c.stats.get(k, 0.0) + (c.in_flight if k == "pending_requests" else 0)) for c in cands)
+            score += w * (st.get(k, 0.0) / mx if mx > 0 else 0.0)
+        return score
+
+    def _pick_prefix(self, cands: list[Deployment], pref: dict[str, float]) -> Deployment:
+        if self.strategy == "load_aware_prefix":
+            return min(cands, key=lambda d: (self.load_score(d, cands) - self.prefix_weight * pref.get(d.name, 0.0),
+                                             d.in_flight))
+        least = min(d.in_flight for d in cands)
+        best = max(cands, key=lambda d: (pref.get(d.name, 0.0), -d.in_flight))
+        if pref.get(best.name, 0.0) > 0:
+            if self.strategy == "prefixaware" or best.in_flight <= self.imbalance * max(1, least):
+                return best
+        return self.rng.choice([d for d in cands if d.in_flight == least])
+
+    def pick(self, group: str, exclude: set[str] = frozenset(), body: dict | None = None) -> Deployment | None:
+        if self.strategy in ("load_aware_prefix", "prefixaware", "cache_aware"):
+            self.refresh_stats()
         with self.lock:
-            healthy = [d for d in self._healthy(group) if d.max_parallel is None or d.in_flight < d.max_parallel]
+            healthy = [d for d in self._healthy(group) if (d.max_parallel is None or d.in_flight < d.max_parallel)
+                       and not d.down]
             cands = [d for d in healthy if d.name not in exclude] or healthy
             if not cands:
                 if self._healthy(group):            # every deployment is at max_parallel_requests
@@ -171,6 +334,12 @@ class Router:
                 dep = min(cands, key=lambda d: d.latency_ewma)
             elif self.strategy == "cost-based-routing":
                 dep = min(cands, key=lambda d: d.cost)
+            elif self.strategy in ("load_aware_prefix", "prefixaware", "cache_aware"):
+                hashes = prompt_prefix_hashes(body or {})
+                pref = self._prefix_scores(hashes)
+                dep = self._pick_prefix(cands, pref)
+                self.counters["prefix_hits_total"] += int(pref.get(dep.name, 0.0) > 0)
+                self._remember_prefix(hashes, dep)
             else:
                 dep = self.rng.choices(cands, weights=[max(d.weight, 1e-9) for d in cands])[0]
             if dep.minute != minute:
@@ -218,7 +387,7 @@ class Router:
         used: collections.Counter = collections.Counter()
         last: UpstreamError | None = None
         while True:
-            dep = self.pick(group, tried)
+            dep = self.pick(group, tried, body)
             if dep is None:
                 raise last or UpstreamError(503, f"no healthy deployment in group {group!r}")
             t0 = self.clock()
@@ -267,7 +436,7 @@ class Router:
 
     def metrics_text(self) -> str:
         lines = []
-        for name in ("retries_total", "fallbacks_total", "guard_blocked_total"):
+        for name in ("retries_total", "fallbacks_total", "guard_blocked_total", "prefix_hits_total"):
             lines += [f"# TYPE lipa_router_{name} counter", f"lipa_router_{name} {self.counters[name]}"]
         for metric, attr in (("requests_total", "requests"), ("failures_total", "failures"),
                              ("cooldowns_total", "cooldowns"), ("in_flight", "in_flight")):
@@ -279,20 +448,22 @@ class Router:
         return "\n".join(lines) + "\n"
 
 
-def create_router_app(router: Router) -> FastAPI:
+def create_router_app(router: Router, scrape: bool = True) -> FastAPI:
     app = FastAPI(title="lipa router")
+    if scrape and router.scraper is None and router.strategy in ("load_aware_prefix", "prefixaware", "cache_aware"):
+        router.scraper = http_scraper()
 
     async def handle(path: str, request: Request):
         body = await request.json()
         if body.get("stream"):
             return JSONResponse({"error": {"message": "streaming is served by the backends directly; "
                                                       "the router proxies non-streaming requests"}}, 400)
-        flagged = router.moderate(body)
+        flagged = await run_in_threadpool(router.moderate, body)
         if flagged is not None:
             return JSONResponse({"error": {"message": "request blocked by moderation guardrail",
                                            "type": "guardrail_violation", "moderation": flagged}}, 400)
         try:
-            return JSONResponse(router.route(path, body))
+            return JSONResponse(await run_in_threadpool(router.route, path, body))
         except UpstreamError as e:
             return JSONResponse({"error": {"message": str(e.body) or str(e), "code": e.status}}, e.status)
 

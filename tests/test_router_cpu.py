@@ -149,3 +149,95 @@ def test_max_parallel_requests_caps_in_flight():
     assert ei.value.status == 429
     r._done(a, True, 0.01)
     assert r.pick("qwen3-8b") is a
+
+
+# ----------------------------------------------------------------------------- prefix / load aware
+def _prompt(sys_prompt, user):
+    return {"model": "qwen3-8b", "messages": [{"role": "system", "content": sys_prompt},
+                                              {"role": "user", "content": user}]}
+
+
+def test_prefixaware_routes_shared_prefix_to_same_backend():
+    calls = []
+    r = Router(cfg("prefixaware"), ok_sender(calls), seed=1)
+    doc = "RAG document about MI355X HBM3E. " * 40           # > several 256-char blocks
+    first = r.route("/chat/completions", _prompt(doc, "q1"))
+    owner = calls[-1][0]
+    for i in range(6):
+        r.route("/chat/completions", _prompt(doc, f"question {i}"))
+        assert calls[-1][0] == owner
+    assert r.counters["prefix_hits_total"] == 6 and first["model"] == "qwen3-8b"
+
+
+def test_load_aware_prefix_uses_scraped_backend_load():
+    """llm-d weights (pending 0.4, kv-cache 0.3, ttft 0.2, queue 0.1) over scraped /metrics; a warm
+    prefix wins only while its backend is not much more loaded."""
+    calls, clock = [], Clock()
+    r = Router(cfg("load_aware_prefix", prefix_weight=0.3), ok_sender(calls), clock=clock, seed=0)
+    load = {"http://a/v1": dict(pending_requests=8, gpu_cache_usage=0.9, ttft_ms=900, queue_time_ms=300),
+            "http://b/v1": dict(pending_requests=0, gpu_cache_usage=0.1, ttft_ms=100, queue_time_ms=0)}
+    r.scraper = lambda d: load[d.api_base]
+    r.route("/chat/completions", _prompt("x" * 600, "hi"))
+    assert calls[-1][0] == "http://b/v1"                       # idle backend
+    # b becomes busy, a idle: the shared prefix (owned by b) is outweighed by b's load
+    load["http://a/v1"], load["http://b/v1"] = load["http://b/v1"], load["http://a/v1"]
+    clock.t += 10
+    r.route("/chat/completions", _prompt("x" * 600, "again"))
+    assert calls[-1][0] == "http://a/v1"
+    # equal load: prefix affinity decides (a now owns the prefix)
+    load["http://b/v1"] = dict(load["http://a/v1"])
+    clock.t += 10
+    r.route("/chat/completions", _prompt("x" * 600, "third"))
+    assert calls[-1][0] == "http://a/v1"
+    # a scrape failure twice in a row marks a backend down
+    def flaky(d):
+        if d.api_base == "http://a/v1":
+            raise OSError("down")
+        return load[d.api_base]
+    r.scraper = flaky
+    for _ in range(2):
+        clock.t += 10
+        r.refresh_stats()
+    r.route("/chat/completions", _prompt("x" * 600, "fourth"))
+    assert calls[-1][0] == "http://b/v1"
+
+
+def test_backend_load_parses_lipa_and_vllm_metrics():
+    from llm_in_practise_amd.infer.router import backend_load, parse_prometheus
+    lipa = ("lipa_num_requests_waiting 3\nlipa_gpu_cache_usage_perc 0.25\n"
+            "lipa_time_to_first_token_seconds_sum 2.0\nlipa_time_to_first_token_seconds_count 4\n"
+            "lipa_queue_time_seconds 0.05\n")
+    assert backend_load(parse_prometheus(lipa)) == {"pending_requests": 3.0, "gpu_cache_usage": 0.25,
+                                                     "ttft_ms": 500.0, "queue_time_ms": 50.0}
+    vllm = 'vllm:num_requests_waiting{model_name="q"} 2\nvllm:gpu_cache_usage_perc{model_name="q"} 0.5\n'
+    assert backend_load(parse_prometheus(vllm))["pending_requests"] == 2.0
+
+
+def test_app_serves_requests_concurrently():
+    """Upstream calls run in the threadpool: two slow requests overlap (in_flight reaches 2)."""
+    import threading
+    import time as _t
+    peak, lock, cur = [0], threading.Lock(), [0]
+
+    def slow(dep, path, body):
+        with lock:
+            cur[0] += 1
+            peak[0] = max(peak[0], cur[0])
+        _t.sleep(0.3)
+        with lock:
+            cur[0] -= 1
+        return {"choices": [], "model": body["model"]}
+    r = Router(cfg("least-busy"), slow, seed=0)
+    app = create_router_app(r, scrape=False)
+    import asyncio
+    import httpx
+
+    async def go():
+        transport = httpx.ASGITransport(app=app)
+        async with httpx.AsyncClient(transport=transport, base_url="http://t") as c:
+            t0 = _t.time()
+            await asyncio.gather(*[c.post("/v1/chat/completions", json={"model": "qwen3-8b", "messages": []})
+                                   for _ in range(2)])
+            return _t.time() - t0
+    dt = asyncio.run(go())
+    assert peak[0] == 2 and dt < 0.55
