@@ -10,6 +10,7 @@
     lipa eval-quant --model DIR                                                  (F2b)
     lipa infer --model DIR --prompt TEXT                                        (F1b, F2c, G1)
     lipa serve --model DIR [--adapter DIR] [--port 8000]                        (G4, H1)
+               [--enable-lora --lora-modules n1=dir1 n2=dir2] [--kv-host-cache-blocks N]
     lipa guard --backend URL [--port 8099]                                      (H3)
     lipa router --config deploy/litellm/config.yaml [--port 4000]               (H2 LiteLLM router)
     lipa convert-alpaca --input self_cognition.jsonl --out alpaca.json           (E10 converter)
@@ -431,11 +432,17 @@ def cmd_serve(a):
     if a.guard_url:
         from ..infer.guard import GuardClient
         moderation = GuardClient(a.guard_url).moderate_sync
+    loras = None
+    if getattr(a, "lora_modules", None):
+        if not a.enable_lora:
+            raise SystemExit("--lora-modules needs --enable-lora (vLLM semantics)")
+        loras = dict(spec.split("=", 1) for spec in a.lora_modules)
     eng = ServingEngine(m, tok, model_name=a.served_model_name or os.path.basename(a.model.rstrip("/")),
                         max_batch=a.max_batch, system_prompt=a.system, tp_group=tp,
                         max_model_len=a.max_model_len,
                         prefix_cache_blocks=a.prefix_blocks if a.prefix_caching else 0,
-                        chunked_prefill=a.max_batched_tokens if a.chunked_prefill else 0)
+                        chunked_prefill=a.max_batched_tokens if a.chunked_prefill else 0,
+                        lora_modules=loras, host_cache_blocks=getattr(a, "host_blocks", 0))
     if tp is not None and eng.tp_rank != 0:
         eng.follower_loop()              # TP / PP followers replay rank 0's iterations
         return
@@ -781,6 +788,12 @@ def build_parser() -> argparse.ArgumentParser:
                    help="prefill long prompts in chunks interleaved with decode (vLLM flag)")
     p.add_argument("--max-num-batched-tokens", dest="max_batched_tokens", type=int, default=2048,
                    help="chunk size for --enable-chunked-prefill")
+    p.add_argument("--enable-lora", dest="enable_lora", action="store_true",
+                   help="serve LoRA adapters next to the base (vLLM flag; Fine-Tuning/README.md:346-351)")
+    p.add_argument("--lora-modules", dest="lora_modules", nargs="+", default=None, metavar="NAME=DIR",
+                   help="adapters selectable per request by `model` name")
+    p.add_argument("--kv-host-cache-blocks", dest="host_blocks", type=int, default=0,
+                   help="prefix-cache host tier (LMCache local-CPU role): 64-token chunks spilled to pinned RAM")
     _add_parallel_args(p)
     p.set_defaults(fn=cmd_serve)
 

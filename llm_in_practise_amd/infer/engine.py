@@ -58,6 +58,7 @@ class _Request:
     out: "queue.Queue[Any]"
     t_arrive: float
     rid: str = dataclasses.field(default_factory=lambda: uuid.uuid4().hex)
+    adapter: int = 0                      # multi-LoRA serving: 0 = base, i = i-th --lora-modules entry
 
 
 class PrefixCache:
@@ -71,9 +72,18 @@ class PrefixCache:
     layer in an HBM pool ``[layers][capacity, block, Hkv·D]``; a hit copies the longest cached
     chunk run into the request's KV slot (one gather per layer) and only the suffix is
     prefilled.  LRU eviction; at least one prompt token is always recomputed (its logits seed
-    the first sampled token)."""
+    the first sampled token).
 
-    def __init__(self, n_layers: int, width: int, dtype, device, block: int = 64, capacity_blocks: int = 512):
+    Host tier (LMCache ``LMCACHE_LOCAL_CPU`` / ``max_local_cpu_size`` role,
+    ``07-L1-Cache/LMCache/vllm-statefulset-lmcache.yaml:96-111``): with ``host_blocks > 0`` a chunk
+    evicted from HBM is spilled to a pinned host pool instead of dropped, and a later hit restores
+    it over PCIe into a free HBM block (its own LRU; the HBM pool holds the hot set, host memory
+    — hundreds of GB on an MI355X node — the warm set).
+
+    ``salt`` separates hash chains whose K/V differ for the same tokens (multi-LoRA adapters)."""
+
+    def __init__(self, n_layers: int, width: int, dtype, device, block: int = 64, capacity_blocks: int = 512,
+                 host_blocks: int = 0):
         import collections
         self.block, self.capacity = block, capacity_blocks
         self.k = [torch.zeros(capacity_blocks, block, width, dtype=dtype, device=device) for _ in range(n_layers)]
@@ -82,10 +92,19 @@ class PrefixCache:
         self.free = list(range(capacity_blocks))
         self.hit_tokens = 0
         self.query_tokens = 0
+        self.host_blocks = int(host_blocks)
+        self.host_hits = 0
+        self.spills = 0
+        if self.host_blocks > 0:
+            pin = torch.device(device).type == "cuda"
+            shape = (n_layers, 2, self.host_blocks, block, width)
+            self.host = torch.zeros(shape, dtype=dtype, pin_memory=pin)
+            self.hmap: "collections.OrderedDict[bytes, int]" = collections.OrderedDict()
+            self.hfree = list(range(self.host_blocks))
 
-    def _digests(self, ids: list[int], n_blocks: int) -> list[bytes]:
+    def _digests(self, ids: list[int], n_blocks: int, salt: int = 0) -> list[bytes]:
         import hashlib
-        out, prev = [], b""
+        out, prev = [], (b"" if not salt else salt.to_bytes(8, "little"))
         for i in range(n_blocks):
             h = hashlib.blake2b(prev, digest_size=16)
             h.update(torch.tensor(ids[i * self.block:(i + 1) * self.block], dtype=torch.int32).numpy().tobytes())
@@ -93,14 +112,49 @@ class PrefixCache:
             out.append(prev)
         return out
 
-    def match(self, ids: list[int]) -> list[int]:
+    # ---- host tier ---------------------------------------------------------------------
+    def _alloc_hbm(self) -> int:
+        """A free HBM block; the LRU one is spilled to the host tier (or dropped) first."""
+        if not self.free:
+            d, j = self.map.popitem(last=False)
+            if self.host_blocks > 0 and d not in self.hmap:
+                if not self.hfree:
+                    _, hj = self.hmap.popitem(last=False)
+                    self.hfree.append(hj)
+                hj = self.hfree.pop()
+                for l in range(len(self.k)):
+                    self.host[l, 0, hj].copy_(self.k[l][j], non_blocking=True)
+                    self.host[l, 1, hj].copy_(self.v[l][j], non_blocking=True)
+                self.hmap[d] = hj
+                self.spills += 1
+            self.free.append(j)
+        return self.free.pop()
+
+    def _restore(self, d: bytes) -> int | None:
+        hj = self.hmap.get(d) if self.host_blocks > 0 else None
+        if hj is None:
+            return None
+        if self.k[0].is_cuda:
+            torch.cuda.current_stream().synchronize()     # spills of the same step have landed
+        j = self._alloc_hbm()
+        for l in range(len(self.k)):
+            self.k[l][j].copy_(self.host[l, 0, hj], non_blocking=True)
+            self.v[l][j].copy_(self.host[l, 1, hj], non_blocking=True)
+        self.hmap.move_to_end(d)
+        self.map[d] = j
+        self.host_hits += 1
+        return j
+
+    def match(self, ids: list[int], salt: int = 0) -> list[int]:
         """Pool indices of the longest cached chunk run (leaving >= 1 token to prefill)."""
         n = (len(ids) - 1) // self.block
         idx = []
-        for d in self._digests(ids, n):
+        for d in self._digests(ids, n, salt):
             j = self.map.get(d)
             if j is None:
-                break
+                j = self._restore(d)
+                if j is None:
+                    break
             self.map.move_to_end(d)
             idx.append(j)
         self.query_tokens += len(ids)
@@ -114,18 +168,15 @@ class PrefixCache:
             cache.k[l][slot, :n] = self.k[l][t].reshape(n, -1)
             cache.v[l][slot, :n] = self.v[l][t].reshape(n, -1)
 
-    def store(self, ids: list[int], cache: KVCache, slot: int):
+    def store(self, ids: list[int], cache: KVCache, slot: int, salt: int = 0):
         """Insert every full prompt chunk of a freshly prefilled slot that is not cached yet."""
         n = len(ids) // self.block
         new = []
-        for i, d in enumerate(self._digests(ids, n)):
+        for i, d in enumerate(self._digests(ids, n, salt)):
             if d in self.map:
                 self.map.move_to_end(d)
                 continue
-            if not self.free:
-                _, j = self.map.popitem(last=False)          # evict LRU
-                self.free.append(j)
-            j = self.free.pop()
+            j = self._alloc_hbm()                            # evicts (spills) the LRU block if full
             self.map[d] = j
             new.append((i, j))
         if not new:
@@ -178,6 +229,10 @@ class _Histogram:
 def _unwrap_lm(model):
     m = model
     for _ in range(4):
+        bm = getattr(m, "__dict__", {}).get("_modules", {}).get("base_model")
+        if bm is not None and hasattr(bm, "model"):      # PeftModel: unwrap before duck-typing
+            m = bm.model
+            continue
         if hasattr(m, "lm_head") and hasattr(m, "model"):
             return m
         m = getattr(m, "model", None) or getattr(m, "module", None)
@@ -191,7 +246,8 @@ class ServingEngine:
                  system_prompt: str | None = None, chat_template: str = "auto", space_before_end: bool = False,
                  max_model_len: int | None = None, max_prefill_batch: int = 32, prefill_token_budget: int = 16384,
                  use_graphs: bool | None = None, tp_group=None, prefix_cache_blocks: int = 0,
-                 prefix_block: int = 64, chunked_prefill: int = 0):
+                 prefix_block: int = 64, chunked_prefill: int = 0, lora_modules: dict[str, str] | None = None,
+                 host_cache_blocks: int = 0):
         """``tp_group``: the model was sharded by ``parallel.tensor_parallel`` over this group.
         The engine then runs SPMD — group rank 0 owns the request queue and broadcasts each
         iteration's admissions; the other ranks call :meth:`follower_loop` and replay exactly the
@@ -248,7 +304,14 @@ class ServingEngine:
         self.prefix = None
         if prefix_cache_blocks > 0:
             self.prefix = PrefixCache(cfg.num_hidden_layers, cfg.num_key_value_heads * cfg.head_dim,
-                                      self.lm.lm_head.weight.dtype, self.device, prefix_block, prefix_cache_blocks)
+                                      self.lm.lm_head.weight.dtype, self.device, prefix_block, prefix_cache_blocks,
+                                      host_blocks=host_cache_blocks)
+        # multi-LoRA serving (vLLM --enable-lora --lora-modules): stacked adapters, per-row masks;
+        # built BEFORE the decode graphs are captured so the adapter term is part of every graph
+        self.mlora = None
+        if lora_modules:
+            from ..peft.multi_lora import MultiLoraManager
+            self.mlora = MultiLoraManager(self.lm, dict(lora_modules), max_rows=max_batch)
         self.slots: list[_Slot | None] = [None] * max_batch
         self.next_tok = torch.full((max_batch,), self.pad, dtype=torch.long, device=self.device)
         self.graphs = None
@@ -259,6 +322,7 @@ class ServingEngine:
             with torch.no_grad():
                 self.graphs = DecodeGraphs(self.lm, self.cache, max_batch, tokens=self.next_tok)
         self._held: _Request | None = None
+        self._admitting = None
         self._pending = None                     # (pinned host tokens, event, owners) of the in-flight step
         self.pipeline = self.device.type == "cuda"
         self._stop = False
@@ -286,15 +350,29 @@ class ServingEngine:
         return list(self.tok.encode(text, add_special_tokens=False))
 
     # ------------------------------------------------------------------ request API (thread-safe)
-    def submit(self, prompt: str, params: SamplingParams, stream: bool = False) -> _Request:
+    @property
+    def served_models(self) -> list[str]:
+        """``/v1/models``: the base model plus every LoRA adapter name."""
+        return [self.model_name] + (list(self.mlora.names) if self.mlora is not None else [])
+
+    def adapter_id(self, model: str | None) -> int:
+        """Request ``model`` → adapter index; KeyError for a model this server does not serve."""
+        if model is None or model == self.model_name:
+            return 0
+        if self.mlora is None or model not in self.mlora.index:
+            raise KeyError(model)
+        return self.mlora.index[model]
+
+    def submit(self, prompt: str, params: SamplingParams, stream: bool = False, model: str | None = None) -> _Request:
         room = self.max_len - 1 - min(params.max_tokens, self.max_len // 2)   # keep space to generate
         ids = self.encode(prompt)[-room:]
-        r = _Request(ids, params, stream, queue.Queue(), time.time())
+        r = _Request(ids, params, stream, queue.Queue(), time.time(), adapter=self.adapter_id(model))
         self.q.put(r)
         return r
 
-    def complete(self, prompt: str, params: SamplingParams, timeout: float | None = None) -> dict:
-        r = self.submit(prompt, params, stream=False)
+    def complete(self, prompt: str, params: SamplingParams, timeout: float | None = None,
+                 model: str | None = None) -> dict:
+        r = self.submit(prompt, params, stream=False, model=model)
         while True:
             kind, val = r.out.get(timeout=timeout)
             if kind == "final":
@@ -302,8 +380,8 @@ class ServingEngine:
             if kind == "error":
                 raise RuntimeError(val)
 
-    def stream(self, prompt: str, params: SamplingParams, timeout: float | None = None):
-        r = self.submit(prompt, params, stream=True)
+    def stream(self, prompt: str, params: SamplingParams, timeout: float | None = None, model: str | None = None):
+        r = self.submit(prompt, params, stream=True, model=model)
         while True:
             kind, val = r.out.get(timeout=timeout)
             if kind == "delta":
@@ -326,12 +404,18 @@ class ServingEngine:
         while not self._stop:
             try:
                 self._iteration()
-            except Exception as e:  # fail the in-flight requests, keep serving
+            except Exception as e:  # fail the in-flight requests (incl. ones being admitted), keep serving
                 self._pending = None
+                failed = set()
                 for i, s in enumerate(self.slots):
                     if s is not None:
                         s.req.out.put(("error", repr(e)))
+                        failed.add(id(s.req))
                         self.slots[i] = None
+                for _, r in (self._admitting or []):
+                    if id(r) not in failed:
+                        r.out.put(("error", repr(e)))
+                self._admitting = None
                 self.cache.pos.zero_()
 
     def _iteration(self):
@@ -345,7 +429,9 @@ class ServingEngine:
             return
         with self.lock, torch.no_grad():
             if new:
+                self._admitting = new
                 self._admit(new)
+                self._admitting = None
             if self.chunked_prefill:
                 self._prefill_chunks()
             if any(s is not None and s.prefilled < 0 for s in self.slots):
@@ -356,7 +442,7 @@ class ServingEngine:
     def _tp_sync(self, new):
         """Broadcast this iteration's admissions (slot, prompt ids, sampling params) from TP rank 0."""
         import torch.distributed as dist
-        payload = None if new is None else [(slot, r.prompt_ids, dataclasses.asdict(r.params), r.t_arrive)
+        payload = None if new is None else [(slot, r.prompt_ids, dataclasses.asdict(r.params), r.t_arrive, r.adapter)
                                             for slot, r in new]
         box = [payload]
         dist.broadcast_object_list(box, src=self.tp_src, group=self.tp_group)
@@ -364,7 +450,8 @@ class ServingEngine:
             return new
         if box[0] is None:
             return None
-        return [(slot, _Request(ids, SamplingParams(**pd), False, queue.Queue(), t)) for slot, ids, pd, t in box[0]]
+        return [(slot, _Request(ids, SamplingParams(**pd), False, queue.Queue(), t, adapter=a))
+                for slot, ids, pd, t, a in box[0]]
 
     def _collect(self):
         """Pull the requests to admit this iteration (None = shut down)."""
@@ -400,13 +487,16 @@ class ServingEngine:
         each one's first token.  With prefix caching, prompts whose leading chunks are cached
         load them and prefill only their suffix (one request at a time).  With chunked prefill,
         prompts longer than the chunk are only registered here (see :meth:`_prefill_chunks`)."""
+        if self.mlora is not None:
+            for slot, r in new:
+                self.mlora.set_slot(slot, r.adapter)
         if self.chunked_prefill:
             short = []
             for slot, r in new:
                 if len(r.prompt_ids) > self.chunked_prefill:
                     P = 0
                     if self.prefix is not None:
-                        idx = self.prefix.match(r.prompt_ids)
+                        idx = self.prefix.match(r.prompt_ids, r.adapter)
                         if idx:
                             self.prefix.load(idx, self.cache, slot)
                             P = len(idx) * self.prefix.block
@@ -420,7 +510,7 @@ class ServingEngine:
         if self.prefix is not None:
             rest = []
             for slot, r in new:
-                idx = self.prefix.match(r.prompt_ids)
+                idx = self.prefix.match(r.prompt_ids, r.adapter)
                 if idx:
                     self._admit_suffix(slot, r, idx)
                 else:
@@ -428,9 +518,18 @@ class ServingEngine:
             if rest:
                 self._admit_batch(rest)
             for slot, r in new:      # (a slot that already finished keeps its rows until reused)
-                self.prefix.store(r.prompt_ids, self.cache, slot)
+                self.prefix.store(r.prompt_ids, self.cache, slot, r.adapter)
             return
         self._admit_batch(new)
+
+    def _rows_for(self, parts: list[tuple[int, int]]):
+        """Multi-LoRA: install the per-token adapter index of a prefill batch [(adapter, n_tokens)]."""
+        if self.mlora is not None:
+            self.mlora.use_rows(torch.cat([torch.full((n,), a, dtype=torch.long) for a, n in parts]).to(self.device))
+
+    def _rows_done(self):
+        if self.mlora is not None:
+            self.mlora.use_rows(None)
 
     def _slot_view(self, slot: int, length: int) -> KVCache:
         view = KVCache.__new__(KVCache)
@@ -454,7 +553,11 @@ class ServingEngine:
         L = len(r.prompt_ids)
         C = min(self.chunked_prefill, L - P)
         ids = torch.tensor([r.prompt_ids[P:P + C]], dtype=torch.long, device=self.device)
-        h = self.lm.model(ids, None, self._slot_view(slot, P), None)
+        self._rows_for([(r.adapter, C)])
+        try:
+            h = self.lm.model(ids, None, self._slot_view(slot, P), None)
+        finally:
+            self._rows_done()
         s.prefilled = P + C
         self.cache.pos[slot] = P + C
         self.stats["batches_total"] += 1
@@ -466,7 +569,7 @@ class ServingEngine:
         dev_toks, toks = self._sample(logits, [slot])
         self.next_tok[slot] = dev_toks[0]
         if self.prefix is not None:
-            self.prefix.store(r.prompt_ids, self.cache, slot)
+            self.prefix.store(r.prompt_ids, self.cache, slot, r.adapter)
         self._accept(slot, toks[0], time.time())
 
     def _admit_suffix(self, slot, r, idx):
@@ -475,7 +578,11 @@ class ServingEngine:
         self.prefix.load(idx, self.cache, slot)
         view = self._slot_view(slot, P)
         ids = torch.tensor([r.prompt_ids[P:]], dtype=torch.long, device=self.device)
-        h = lm.model(ids, None, view, None)
+        self._rows_for([(r.adapter, len(r.prompt_ids) - P)])
+        try:
+            h = lm.model(ids, None, view, None)
+        finally:
+            self._rows_done()
         logits = h[-1:] @ lm.lm_head.weight.t()
         L = len(r.prompt_ids)
         self.cache.pos[slot] = L
@@ -493,7 +600,11 @@ class ServingEngine:
         lens = [len(r.prompt_ids) for _, r in new]
         ids = torch.tensor([[t for _, r in new for t in r.prompt_ids]], dtype=torch.long).to(self.device)
         pp = PackedPrefill(self.cache, [s for s, _ in new], lens, self.device)
-        h = lm.model(ids, pp.positions, pp, None)
+        self._rows_for([(r.adapter, n) for (_, r), n in zip(new, lens)])
+        try:
+            h = lm.model(ids, pp.positions, pp, None)
+        finally:
+            self._rows_done()
         logits = h[pp.last] @ lm.lm_head.weight.t()
         rows = torch.tensor([s for s, _ in new], device=self.device)
         self.cache.pos[rows] = torch.tensor(lens, dtype=torch.long, device=self.device)
@@ -673,7 +784,11 @@ class ServingEngine:
             lines += ["# TYPE lipa_prefix_cache_queries_total counter",
                       f"lipa_prefix_cache_queries_total {self.prefix.query_tokens}",
                       "# TYPE lipa_prefix_cache_hits_total counter",
-                      f"lipa_prefix_cache_hits_total {self.prefix.hit_tokens}"]
+                      f"lipa_prefix_cache_hits_total {self.prefix.hit_tokens}",
+                      "# TYPE lipa_prefix_cache_host_hits_total counter",
+                      f"lipa_prefix_cache_host_hits_total {self.prefix.host_hits}",
+                      "# TYPE lipa_prefix_cache_spills_total counter",
+                      f"lipa_prefix_cache_spills_total {self.prefix.spills}"]
         lines += self.h_latency.render("lipa_e2e_request_latency_seconds")
         lines += self.h_ttft.render("lipa_time_to_first_token_seconds")
         if torch.cuda.is_available():

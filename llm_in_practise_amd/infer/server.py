@@ -129,8 +129,20 @@ def create_app(engine: ServingEngine, api_key: str | None = None, moderation=Non
 
     @app.get("/v1/models")
     async def models():
-        return {"object": "list", "data": [{"id": engine.model_name, "object": "model", "created": int(time.time()),
-                                            "owned_by": "llm_in_practise_amd"}]}
+        names = getattr(engine, "served_models", None) or [engine.model_name]
+        return {"object": "list", "data": [{"id": n, "object": "model", "created": int(time.time()),
+                                            "owned_by": "llm_in_practise_amd",
+                                            **({"parent": engine.model_name} if n != engine.model_name else {})}
+                                           for n in names]}
+
+    def _target(model):
+        """Multi-LoRA serving (vLLM --lora-modules): the request's ``model`` picks the adapter;
+        with adapters loaded an unknown name is a 404, without any every name maps to the base."""
+        if getattr(engine, "mlora", None) is None:
+            return None
+        if model is None or model in engine.served_models:
+            return model
+        raise HTTPException(status_code=404, detail=f"The model `{model}` does not exist.")
 
     @app.get("/metrics")
     async def metrics():
@@ -143,10 +155,11 @@ def create_app(engine: ServingEngine, api_key: str | None = None, moderation=Non
         prompt = engine.build_chat_prompt(msgs)
         cid, created = "chatcmpl-" + uuid.uuid4().hex, int(time.time())
         name = req.model or engine.model_name
+        tgt = _target(req.model)
         if req.stream:
-            return StreamingResponse(_sse_chat(engine, prompt, _params(req), cid, created, name),
+            return StreamingResponse(_sse_chat(engine, prompt, _params(req), cid, created, name, tgt),
                                      media_type="text/event-stream")
-        res = await asyncio.to_thread(engine.complete, prompt, _params(req))
+        res = await asyncio.to_thread(_complete, engine, prompt, _params(req), tgt)
         return ChatCompletionResponse(
             id=cid, created=created, model=name,
             choices=[Choice(index=0, message=ChoiceMessage(content=res["text"]), finish_reason=res["finish_reason"])],
@@ -158,10 +171,11 @@ def create_app(engine: ServingEngine, api_key: str | None = None, moderation=Non
         await _moderate(req.prompt)
         cid, created = "cmpl-" + uuid.uuid4().hex, int(time.time())
         name = req.model or engine.model_name
+        tgt = _target(req.model)
         if req.stream:
-            return StreamingResponse(_sse_completion(engine, req.prompt, _params(req), cid, created, name),
+            return StreamingResponse(_sse_completion(engine, req.prompt, _params(req), cid, created, name, tgt),
                                      media_type="text/event-stream")
-        res = await asyncio.to_thread(engine.complete, req.prompt, _params(req))
+        res = await asyncio.to_thread(_complete, engine, req.prompt, _params(req), tgt)
         return {"id": cid, "object": "text_completion", "created": created, "model": name,
                 "choices": [{"index": 0, "text": res["text"], "finish_reason": res["finish_reason"],
                              "logprobs": None}],
@@ -171,8 +185,12 @@ def create_app(engine: ServingEngine, api_key: str | None = None, moderation=Non
     return app
 
 
-async def _aiter_stream(engine, prompt, params):
-    it = engine.stream(prompt, params)
+def _complete(engine, prompt, params, model=None):
+    return engine.complete(prompt, params, model=model) if model is not None else engine.complete(prompt, params)
+
+
+async def _aiter_stream(engine, prompt, params, model=None):
+    it = engine.stream(prompt, params, model=model) if model is not None else engine.stream(prompt, params)
     while True:
         item = await asyncio.to_thread(next, it, None)
         if item is None:
@@ -180,11 +198,11 @@ async def _aiter_stream(engine, prompt, params):
         yield item
 
 
-async def _sse_chat(engine, prompt, params, cid, created, name):
+async def _sse_chat(engine, prompt, params, cid, created, name, model=None):
     head = {"id": cid, "object": "chat.completion.chunk", "created": created, "model": name}
     yield "data: " + json.dumps({**head, "choices": [{"index": 0, "delta": {"role": "assistant"},
                                                       "finish_reason": None}]}) + "\n\n"
-    async for delta, final in _aiter_stream(engine, prompt, params):
+    async for delta, final in _aiter_stream(engine, prompt, params, model):
         if final is None:
             yield "data: " + json.dumps({**head, "choices": [{"index": 0, "delta": {"content": delta},
                                                               "finish_reason": None}]}, ensure_ascii=False) + "\n\n"
@@ -194,9 +212,9 @@ async def _sse_chat(engine, prompt, params, cid, created, name):
     yield "data: [DONE]\n\n"
 
 
-async def _sse_completion(engine, prompt, params, cid, created, name):
+async def _sse_completion(engine, prompt, params, cid, created, name, model=None):
     head = {"id": cid, "object": "text_completion", "created": created, "model": name}
-    async for delta, final in _aiter_stream(engine, prompt, params):
+    async for delta, final in _aiter_stream(engine, prompt, params, model):
         fr = None if final is None else final["finish_reason"]
         yield "data: " + json.dumps({**head, "choices": [{"index": 0, "text": delta, "finish_reason": fr}]},
                                     ensure_ascii=False) + "\n\n"

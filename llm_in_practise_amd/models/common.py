@@ -101,7 +101,23 @@ class FusedProjection:
         return out
 
     def __call__(self, x, residual=None, training: bool = True):
-        return fused_linear(x, self.base, self.bias, self.branches(training), residual, training)
+        y = fused_linear(x, self.base, self.bias, self.branches(training), residual, training)
+        return _apply_multi_lora(self.mods, self.splits, x, y)
+
+
+def _apply_multi_lora(mods, splits, x, y):
+    """Per-request adapters of multi-LoRA serving (``peft/multi_lora.py``): y[:, c0:c1] += the
+    row-masked stacked low-rank term of each projection that carries adapters."""
+    slots = [getattr(_leaf_linear(m), "_mlora", None) for m in mods]
+    if not any(s is not None for s in slots):
+        return y
+    x2, y2 = x.reshape(-1, x.shape[-1]), y.view(-1, y.shape[-1])
+    c0 = 0
+    for s, n in zip(slots, splits):
+        if s is not None:
+            s.apply_(x2, y2, c0)
+        c0 += n
+    return y
 
 
 def project(mods: list[nn.Module], x: torch.Tensor, residual: torch.Tensor | None = None,
@@ -113,13 +129,15 @@ def project(mods: list[nn.Module], x: torch.Tensor, residual: torch.Tensor | Non
         m = mods[0]
         if _trainable_base(m) or not isinstance(_leaf_linear(m), (nn.Linear, Linear4bit)):
             y = m(x)
+            y = _apply_multi_lora(mods, [y.shape[-1]], x, y)
             return y if residual is None else y + residual
         base, bias = base_of(m)
         br = [m.branch()] if isinstance(m, LoraLayer) and not m.merged else []
         if br and not training:
             br[0].dropout = 0.0
         cd = base.dtype if isinstance(base, torch.Tensor) else base.dtype
-        return fused_linear(x.to(cd), base, bias, br, residual, training)
+        y = fused_linear(x.to(cd), base, bias, br, residual, training)
+        return _apply_multi_lora(mods, [_out_features(m)], x, y)
     ys = [project([m], x, None, training) for m in mods]
     y = torch.cat(ys, -1)
     return y if residual is None else y + residual

@@ -195,3 +195,94 @@ def test_cache_gateway_exact_and_semantic_levels():
     assert len(calls) == 3
     m = c.get("/metrics").text
     assert "lipa_cache_hits_exact_total 1" in m and "lipa_cache_hits_semantic_total 1" in m
+
+
+# ----------------------------------------------------------------------------- multi-LoRA serving
+def _make_adapter(tmp, name, targets, r, seed):
+    from llm_in_practise_amd.peft.lora import LoraConfig, get_peft_model
+    base = Qwen3ForCausalLM.from_config(qwen3_config("qwen3-tiny", vocab_size=256), dtype=torch.float32, seed=0)
+    pm = get_peft_model(base, LoraConfig(r=r, lora_alpha=2 * r, target_modules=targets))
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for n, p in pm.named_parameters():
+            if "lora_" in n:
+                p.copy_(torch.randn(p.shape, generator=g) * 0.3)
+    d = str(tmp / name)
+    pm.save_pretrained(d)
+    return d
+
+
+def _greedy(engine, prompt, model=None):
+    return engine.complete(prompt, SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True), model=model)["text"]
+
+
+def test_multi_lora_per_request_adapters_match_single_adapter_models(tmp_path):
+    """vLLM --enable-lora --lora-modules: one base, two adapters (different targets / ranks), the
+    adapter picked per request by `model`; mixed batches equal dedicated single-adapter engines."""
+    from llm_in_practise_amd.peft.lora import PeftModel
+    tok = ByteTokenizer()
+    d1 = _make_adapter(tmp_path, "a1", ["q_proj", "v_proj"], 4, 1)
+    d2 = _make_adapter(tmp_path, "a2", ["q_proj", "k_proj", "v_proj", "o_proj", "down_proj"], 8, 2)
+
+    def base_model():
+        return Qwen3ForCausalLM.from_config(qwen3_config("qwen3-tiny", vocab_size=256), dtype=torch.float32,
+                                            seed=0).eval()
+    m = base_model()
+    m.fuse_projections()
+    multi = ServingEngine(m, tok, model_name="tiny", max_batch=6, lora_modules={"a1": d1, "a2": d2})
+    singles = {}
+    for name, d in (("a1", d1), ("a2", d2)):
+        pm = PeftModel.from_pretrained(base_model(), d)
+        pm.model.fuse_projections()
+        singles[name] = ServingEngine(pm, tok, model_name="tiny", max_batch=2)
+    plain = ServingEngine(base_model(), tok, model_name="tiny", max_batch=2)
+    try:
+        prompts = ["hello lora", "abc", "MI355X"]
+        want = {}
+        for p in prompts:
+            want[(p, None)] = _greedy(plain, p)
+            for name in ("a1", "a2"):
+                want[(p, name)] = _greedy(singles[name], p)
+        assert want[(prompts[0], "a1")] != want[(prompts[0], None)] != want[(prompts[0], "a2")]
+        # all nine (prompt, adapter) requests in flight together: one mixed decode batch
+        reqs = [(p, a, multi.submit(p, SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True), model=a))
+                for p in prompts for a in (None, "a1", "a2")]
+        for p, a, r in reqs:
+            while True:
+                kind, val = r.out.get(timeout=120)
+                if kind == "final":
+                    assert val["text"] == want[(p, a)], (p, a)
+                    break
+        assert multi.served_models == ["tiny", "a1", "a2"]
+        c = TestClient(create_app(multi))
+        ids = [d["id"] for d in c.get("/v1/models").json()["data"]]
+        assert ids == ["tiny", "a1", "a2"]
+        r = c.post("/v1/completions", json={"model": "a2", "prompt": "abc", "max_tokens": 8, "temperature": 0,
+                                            "ignore_eos": True})
+        assert r.status_code == 200 and r.json()["choices"][0]["text"] == want[("abc", "a2")]
+        assert c.post("/v1/completions", json={"model": "nope", "prompt": "x", "max_tokens": 2}).status_code == 404
+    finally:
+        for e in [multi, plain, *singles.values()]:
+            e.shutdown()
+
+
+def test_prefix_cache_host_tier_spills_and_restores():
+    """LMCache local-CPU role: chunks evicted from a tiny HBM pool are spilled to host memory and
+    restored on a later hit; outputs equal an engine without prefix caching."""
+    m = Qwen3ForCausalLM.from_config(qwen3_config("qwen3-tiny", vocab_size=256), dtype=torch.float32, seed=0).eval()
+    tok = ByteTokenizer()
+    p = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    docs = [("document %d " % i) * 40 for i in range(4)]              # 4 distinct ~480-token prefixes
+    ref = ServingEngine(m, tok, max_batch=2)
+    tiered = ServingEngine(m, tok, max_batch=2, prefix_cache_blocks=8, host_cache_blocks=64)
+    try:
+        want = {d: ref.complete(d + "q", p)["text"] for d in docs}
+        for rnd in range(2):
+            for d in docs:
+                assert tiered.complete(d + "q%d" % rnd, p)["text"] == ref.complete(d + "q%d" % rnd, p)["text"]
+        pc = tiered.prefix
+        assert pc.spills > 0 and pc.host_hits > 0
+        assert want[docs[0]] == tiered.complete(docs[0] + "q", p)["text"]
+    finally:
+        ref.shutdown()
+        tiered.shutdown()
