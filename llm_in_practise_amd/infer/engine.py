@@ -61,6 +61,23 @@ class _Request:
     adapter: int = 0                      # multi-LoRA serving: 0 = base, i = i-th --lora-modules entry
 
 
+class AsyncOut:
+    """Thread-safe ``put`` into an ``asyncio.Queue`` owned by an event loop: the engine thread
+    hands each streamed delta to the server's loop with one ``call_soon_threadsafe`` instead of
+    the loop polling a ``queue.Queue`` from a worker thread per token."""
+
+    def __init__(self, loop=None):
+        import asyncio
+        self.loop = loop or asyncio.get_running_loop()
+        self.q: "asyncio.Queue" = asyncio.Queue()
+
+    def put(self, item):
+        self.loop.call_soon_threadsafe(self.q.put_nowait, item)
+
+    async def get(self):
+        return await self.q.get()
+
+
 class PrefixCache:
     """Automatic prefix caching — the vLLM ``--enable-prefix-caching`` / LMCache chunk-reuse role
     (``LLM_on_Kubernetes/Inference_Platfrom/07-L1-Cache``, README "APC": system-prompt /
@@ -244,7 +261,7 @@ def _unwrap_lm(model):
 class ServingEngine:
     def __init__(self, model, tokenizer, model_name: str = "lipa-model", max_batch: int = 16,
                  system_prompt: str | None = None, chat_template: str = "auto", space_before_end: bool = False,
-                 max_model_len: int | None = None, max_prefill_batch: int = 32, prefill_token_budget: int = 16384,
+                 max_model_len: int | None = None, max_prefill_batch: int | None = None, prefill_token_budget: int = 16384,
                  use_graphs: bool | None = None, tp_group=None, prefix_cache_blocks: int = 0,
                  prefix_block: int = 64, chunked_prefill: int = 0, lora_modules: dict[str, str] | None = None,
                  host_cache_blocks: int = 0):
@@ -270,7 +287,9 @@ class ServingEngine:
         self.lm = _unwrap_lm(model)
         self.lm.eval()
         self.max_batch = max_batch
-        self.max_prefill_batch = max_prefill_batch
+        # admit a whole burst at once (one packed prefill, bounded by the token budget) rather than in
+        # waves of 32: every wave costs the waiting requests another prefill + decode iteration
+        self.max_prefill_batch = max_prefill_batch or max_batch
         self.prefill_token_budget = prefill_token_budget
         self.system_prompt = system_prompt
         self.chat_template = chat_template
@@ -323,6 +342,7 @@ class ServingEngine:
                 self.graphs = DecodeGraphs(self.lm, self.cache, max_batch, tokens=self.next_tok)
         self._held: _Request | None = None
         self._admitting = None
+        self.iteration_hook = None               # engine-process mode: flush the batched outputs
         self._pending = None                     # (pinned host tokens, event, owners) of the in-flight step
         self.pipeline = self.device.type == "cuda"
         self._stop = False
@@ -363,10 +383,15 @@ class ServingEngine:
             raise KeyError(model)
         return self.mlora.index[model]
 
-    def submit(self, prompt: str, params: SamplingParams, stream: bool = False, model: str | None = None) -> _Request:
+    def submit(self, prompt: str, params: SamplingParams, stream: bool = False, model: str | None = None,
+               out=None) -> _Request:
+        """``out``: any object with a thread-safe ``put`` (default a ``queue.Queue``); the HTTP server
+        passes an :class:`AsyncOut` so streamed deltas reach its event loop without a thread hop
+        per token."""
         room = self.max_len - 1 - min(params.max_tokens, self.max_len // 2)   # keep space to generate
         ids = self.encode(prompt)[-room:]
-        r = _Request(ids, params, stream, queue.Queue(), time.time(), adapter=self.adapter_id(model))
+        r = _Request(ids, params, stream, out if out is not None else queue.Queue(), time.time(),
+                     adapter=self.adapter_id(model))
         self.q.put(r)
         return r
 
@@ -404,6 +429,8 @@ class ServingEngine:
         while not self._stop:
             try:
                 self._iteration()
+                if self.iteration_hook is not None:
+                    self.iteration_hook()
             except Exception as e:  # fail the in-flight requests (incl. ones being admitted), keep serving
                 self._pending = None
                 failed = set()
@@ -417,6 +444,8 @@ class ServingEngine:
                         r.out.put(("error", repr(e)))
                 self._admitting = None
                 self.cache.pos.zero_()
+                if self.iteration_hook is not None:
+                    self.iteration_hook()
 
     def _iteration(self):
         new = self._collect() if self.tp_rank == 0 else []

@@ -190,12 +190,27 @@ def _complete(engine, prompt, params, model=None):
 
 
 async def _aiter_stream(engine, prompt, params, model=None):
-    it = engine.stream(prompt, params, model=model) if model is not None else engine.stream(prompt, params)
+    from .engine import AsyncOut
+    from .mp_engine import EngineClient
+    if not isinstance(engine, (ServingEngine, EngineClient)):
+        it = engine.stream(prompt, params, model=model) if model is not None else engine.stream(prompt, params)
+        while True:
+            item = await asyncio.to_thread(next, it, None)
+            if item is None:
+                return
+            yield item
+        return
+    out = AsyncOut()
+    engine.submit(prompt, params, stream=True, model=model, out=out)
     while True:
-        item = await asyncio.to_thread(next, it, None)
-        if item is None:
+        kind, val = await out.get()
+        if kind == "delta":
+            yield val, None
+        elif kind == "final":
+            yield "", val
             return
-        yield item
+        else:
+            raise RuntimeError(val)
 
 
 async def _sse_chat(engine, prompt, params, cid, created, name, model=None):

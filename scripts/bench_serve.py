@@ -122,18 +122,29 @@ class _SyntheticTokenizer:
         return "".join(chr(0x4E00 + int(i) % 20000) for i in ids)
 
 
-def start_inprocess(spec: str, port: int, max_batch: int = 64, max_model_len: int | None = None):
-    """Launch our server in a background thread with a random-init model (synthetic tokenizer)."""
+def _make_engine(spec: str, max_batch: int, max_model_len: int | None):
+    from llm_in_practise_amd.cli.main import _load_for_inference
+    from llm_in_practise_amd.infer.engine import ServingEngine
+    m = _load_for_inference(spec)
+    return ServingEngine(m, _SyntheticTokenizer(), model_name=spec, max_batch=max_batch, chat_template="chatml",
+                         max_model_len=max_model_len)
+
+
+def start_inprocess(spec: str, port: int, max_batch: int = 64, max_model_len: int | None = None,
+                    engine_process: bool = False):
+    """Launch our server in a background thread with a random-init model (synthetic tokenizer);
+    ``engine_process``: the engine runs in its own process (infer/mp_engine.py)."""
     import threading
 
     import uvicorn
 
-    from llm_in_practise_amd.cli.main import _load_for_inference
-    from llm_in_practise_amd.infer.engine import ServingEngine
     from llm_in_practise_amd.infer.server import create_app
-    m = _load_for_inference(spec)
-    eng = ServingEngine(m, _SyntheticTokenizer(), model_name=spec, max_batch=max_batch, chat_template="chatml",
-                        max_model_len=max_model_len)
+    if engine_process:
+        from llm_in_practise_amd.infer.mp_engine import EngineClient, PromptFormatter
+        eng = EngineClient(_make_engine, (spec, max_batch, max_model_len),
+                           PromptFormatter(_SyntheticTokenizer(), chat_template="chatml"))
+    else:
+        eng = _make_engine(spec, max_batch, max_model_len)
     cfg = uvicorn.Config(create_app(eng), host="127.0.0.1", port=port, log_level="warning")
     th = threading.Thread(target=uvicorn.Server(cfg).run, daemon=True)
     th.start()
@@ -157,9 +168,11 @@ def main():
     ap.add_argument("--spawn", action="store_true",
                     help="with --inprocess: run the server in a child process (client and server do not share a GIL)")
     ap.add_argument("--serve-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--engine-process", action="store_true",
+                    help="run the engine core in its own process (frontend only formats / streams)")
     a = ap.parse_args()
     if a.serve_only:                      # child of --spawn
-        start_inprocess(a.inprocess, a.port, a.max_batch, a.max_model_len)
+        start_inprocess(a.inprocess, a.port, a.max_batch, a.max_model_len, a.engine_process)
         while True:
             time.sleep(3600)
     child = None
@@ -170,6 +183,8 @@ def main():
                str(a.port), "--max-batch", str(a.max_batch)]
         if a.max_model_len:
             cmd += ["--max-model-len", str(a.max_model_len)]
+        if a.engine_process:
+            cmd += ["--engine-process"]
         child = subprocess.Popen(cmd)
         url = f"http://127.0.0.1:{a.port}"
         for _ in range(600):
@@ -181,7 +196,7 @@ def main():
                     raise RuntimeError("server process exited")
                 time.sleep(1)
     else:
-        url = a.url or start_inprocess(a.inprocess, a.port, a.max_batch, a.max_model_len)
+        url = a.url or start_inprocess(a.inprocess, a.port, a.max_batch, a.max_model_len, a.engine_process)
     if a.dataset == "mixed":
         prompts = mixed_dataset(a.num_prompts)
     elif a.dataset == "short":       # ShareGPT-like chat turns only (the reference table's workload shape)

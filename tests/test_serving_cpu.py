@@ -286,3 +286,38 @@ def test_prefix_cache_host_tier_spills_and_restores():
     finally:
         ref.shutdown()
         tiered.shutdown()
+
+
+# ----------------------------------------------------------------------------- engine process
+def _tiny_engine(seed):
+    torch.set_num_threads(2)
+    m = Qwen3ForCausalLM.from_config(qwen3_config("qwen3-tiny", vocab_size=256), dtype=torch.float32, seed=seed).eval()
+    tok = ByteTokenizer()
+    tok.eos_token_id = 10
+    return ServingEngine(m, tok, model_name="tiny", max_batch=8, system_prompt="You are helpful.")
+
+
+def test_engine_process_frontend_matches_inprocess(engine):
+    """Engine core in its own process (EngineClient): the OpenAI server streams the same tokens as
+    the in-process engine; metrics are fetched over the RPC path."""
+    from llm_in_practise_amd.infer.mp_engine import EngineClient, PromptFormatter
+    tok = ByteTokenizer()
+    client = EngineClient(_tiny_engine, (0,), PromptFormatter(tok, system_prompt="You are helpful."))
+    try:
+        p = SamplingParams(max_tokens=6, temperature=0.0)
+        assert client.complete("abc", p)["text"] == engine.complete("abc", p)["text"]
+        c = TestClient(create_app(client))
+        r = c.post("/v1/chat/completions", json={"messages": [{"role": "user", "content": "hi"}], "max_tokens": 5,
+                                                 "temperature": 0})
+        want = TestClient(create_app(engine)).post("/v1/chat/completions", json={
+            "messages": [{"role": "user", "content": "hi"}], "max_tokens": 5, "temperature": 0})
+        assert r.status_code == 200 and r.json()["choices"][0]["message"]["content"] == \
+            want.json()["choices"][0]["message"]["content"]
+        with c.stream("POST", "/v1/chat/completions", json={"messages": [{"role": "user", "content": "hey"}],
+                                                             "max_tokens": 4, "temperature": 0, "stream": True}) as s:
+            lines = [l for l in s.iter_lines() if l]
+        assert lines[-1] == "data: [DONE]" and len(lines) >= 3
+        assert "lipa_requests_total" in c.get("/metrics").text
+        assert c.get("/v1/models").json()["data"][0]["id"] == "tiny"
+    finally:
+        client.shutdown()
