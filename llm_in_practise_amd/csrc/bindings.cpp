@@ -32,11 +32,8 @@ void launch_adamw8bit(int, float*, const void*, uint8_t*, uint8_t*, float*, floa
                       size_t, float, float, float, float, float, float, float, const float*, const float*,
                       hipStream_t);
 void launch_unscale(int, void*, size_t, const float*, float*, hipStream_t);
-void set_gemm_impl(int impl);
 void launch_gemm_w4(int, const void*, int, const uint32_t*, const float*, const void*, const void*, int, const void*,
                     void*, int, int, int, hipStream_t);
-void launch_gemm_bf16w(const void*, int, const void*, const void*, const void*, int, const void*, void*, int, int, int,
-                       hipStream_t);
 void launch_pack_nf4(const uint8_t*, uint32_t*, int, int, int, hipStream_t);
 void launch_absmax_t(const float*, const uint8_t*, const float*, const float*, const float*, float*, int, int,
                      hipStream_t);
@@ -472,26 +469,29 @@ Tensor gemm_nf4_t(Tensor dy, Tensor codes_b, Tensor absmax_t, int64_t K, optiona
   return dx;
 }
 
+Tensor gemm8(Tensor x, Tensor w, optional<Tensor> ext_a, optional<Tensor> ext_b, optional<Tensor> residual,
+             int64_t splits);
+
+// y = x·wᵀ (+ LoRA K-slice) (+ residual) for a frozen bf16 base: the hand-written 8-phase MFMA GEMM
+// (gemm8.hip) whenever the shape / strides allow it, library GEMM otherwise.
 Tensor gemm_bf16(Tensor x, Tensor w, optional<Tensor> ext_a, optional<Tensor> ext_b, optional<Tensor> residual) {
   CHECK_BF16(x);
   CHECK_BF16(w);
   CHECK_CONTIG(w);
   const int M = x.size(0), K = x.size(1), N = w.size(0);
-  if (N % 32 != 0 || K % 64 != 0 || x.stride(1) != 1 || x.stride(0) % 8 != 0) {
+  const bool ext_ok = !(ext_a && ext_a->defined()) || (ext_a->is_contiguous() && ext_b->is_contiguous() &&
+                                                       ext_a->size(1) % 32 == 0);
+  const bool res_ok = !(residual && residual->defined()) || residual->is_contiguous();
+  if (x.stride(1) != 1 || !gemm8_supported(M, N, K, x.stride(0), w.stride(0)) || !ext_ok || !res_ok ||
+      reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 != 0) {
     auto y = at::matmul(x, w.t());
     if (ext_a && ext_a->defined()) y.addmm_(*ext_a, ext_b->t());
     if (residual && residual->defined()) y.add_(*residual);
     return y;
   }
-  int R_ext;
-  check_ext(ext_a, ext_b, M, N, R_ext);
-  auto y = at::empty({M, N}, x.options());
-  launch_gemm_bf16w(x.data_ptr(), x.stride(0), w.data_ptr(), optr(ext_a), optr(ext_b), R_ext, optr(residual),
-                    y.data_ptr(), M, N, K, stream());
-  return y;
+  return gemm8(x, w, ext_a, ext_b, residual, 0);
 }
 
-// bf16 base backward: plain library GEMM (hipBLASLt) + the low-rank K-slice as a rank-R update
 Tensor gemm_bf16_t(Tensor dy, Tensor w, optional<Tensor> ext_a, optional<Tensor> ext_b) {
   auto dx = at::matmul(dy, w);
   if (ext_a && ext_a->defined()) dx.addmm_(*ext_a, ext_b->t());
@@ -856,7 +856,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dropout_fwd", &dropout_fwd);
   m.def("dropout_bwd_add", &dropout_bwd_add);
   m.def("grad_norm", &grad_norm);
-  m.def("set_gemm_impl", &set_gemm_impl);
   m.def("decode_attention", &decode_attention);
   m.def("decode_attention_append", &decode_attention_append);
   m.def("lora_proj", &lora_proj);

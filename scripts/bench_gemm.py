@@ -51,11 +51,9 @@ def main():
             dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
             fl = 2 * M * N * K
             r = {}
-            for impl in a.impls:
-                C.set_gemm_impl(impl)
-                r[f"nf4_fwd_v{impl}"] = timeit(lambda: C.gemm_nf4(x, cf, at, N, None, None, None), a.iters)
-                r[f"nf4_bwd_v{impl}"] = timeit(lambda: C.gemm_nf4_t(dy, cb, at, K, None, None), a.iters)
-            C.set_gemm_impl(0)
+            r["nf4_fwd_v2"] = timeit(lambda: C.gemm_nf4(x, cf, at, N, None, None, None), a.iters)
+            r["nf4_bwd_v2"] = timeit(lambda: C.gemm_nf4_t(dy, cb, at, K, None, None), a.iters)
+            r["bf16_fwd_gemm8"] = timeit(lambda: C.gemm8(x, w, None, None, None, 0), a.iters)
             if a.quick:
                 r["bf16_fwd_hipblaslt"] = timeit(lambda: x @ w.t(), a.iters)
                 r["bf16_bwd_hipblaslt"] = timeit(lambda: dy @ w, a.iters)

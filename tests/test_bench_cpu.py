@@ -54,3 +54,17 @@ def test_bench_json_contract_two_ranks(extra):
     assert abs(d["value"] - tokens / (d["ms_per_step"] * 2 / 1000)) / d["value"] < 0.02
     assert d["config"]["global_batch"] == 8
     assert d["config"]["parallelism"] == ("zero3-dp2" if "zero3" in extra else "dp2")
+
+
+def test_scaling_harness_runs_each_world_size(tmp_path):
+    """bench/scaling.py: one bench.py job per N (gloo on CPU), efficiency vs N = 1."""
+    out = tmp_path / "scale.json"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "2"
+    r = subprocess.run([sys.executable, "-m", "llm_in_practise_amd.bench.scaling", "--gpus", "1", "2", "--steps", "1",
+                        "--warmup", "1", "--out", str(out), "--model", "qwen3-tiny", "--seq-len", "64"],
+                       capture_output=True, text=True, timeout=900, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(out.read_text())
+    assert [t["n_gpus"] for t in d["table"]] == [1, 2]
+    assert d["table"][0]["weak_scaling_efficiency"] == 1.0 and d["table"][1]["weak_scaling_efficiency"] > 0

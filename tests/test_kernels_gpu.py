@@ -273,9 +273,7 @@ def _lora_ref(x, w, ext_a=None, ext_b=None, res=None):
 
 @pytest.mark.parametrize("M,N,K", [(1024, 6144, 4096), (1000, 512, 1024), (64, 128, 256), (2048, 24576, 512)])
 @pytest.mark.parametrize("dq", [True, False])
-@pytest.mark.parametrize("impl", [1, 2])
-def test_gemm_nf4_fwd_bwd(native_ext, M, N, K, dq, impl):
-    native_ext.set_gemm_impl(impl)
+def test_gemm_nf4_fwd_bwd(native_ext, M, N, K, dq):
     w = torch.randn(N, K, device=DEV).to(torch.bfloat16)
     q = quantize_nf4(w, 64, double_quant=dq)
     wd = dequantize_nf4(q, torch.float32)
@@ -293,13 +291,10 @@ def test_gemm_nf4_fwd_bwd(native_ext, M, N, K, dq, impl):
     eb2 = (0.1 * torch.randn(K, R, device=DEV)).to(torch.bfloat16)
     dx = native_ext.gemm_nf4_t(dy, cb, at, K, ea, eb2)
     assert rel_err(dx, dy.float() @ wd + ea.float() @ eb2.float().t()) < 1e-2
-    native_ext.set_gemm_impl(0)
 
 
-@pytest.mark.parametrize("impl", [1, 2])
-def test_gemm_nf4_asymmetric_layout(native_ext, impl):
+def test_gemm_nf4_asymmetric_layout(native_ext):
     """A = I style check with an asymmetric weight catches a transposed epilogue."""
-    native_ext.set_gemm_impl(impl)
     N, K = 128, 128
     w = torch.arange(N * K, device=DEV, dtype=torch.float32).view(N, K) % 13 - 6
     q = quantize_nf4(w.to(torch.bfloat16), 64, double_quant=False)
@@ -310,11 +305,11 @@ def test_gemm_nf4_asymmetric_layout(native_ext, impl):
     assert torch.allclose(y.float(), wd.t().to(torch.bfloat16).float(), atol=1e-2)
     dx = native_ext.gemm_nf4_t(torch.eye(N, device=DEV, dtype=torch.bfloat16), cb, at, K, None, None)
     assert torch.allclose(dx.float(), wd.to(torch.bfloat16).float(), atol=1e-2)
-    native_ext.set_gemm_impl(0)
 
 
-@pytest.mark.parametrize("M,N,K", [(1024, 4096, 4096), (77, 256, 128)])
+@pytest.mark.parametrize("M,N,K", [(1024, 4096, 4096), (77, 256, 128), (77, 264, 96)])
 def test_gemm_bf16_lora(native_ext, M, N, K):
+    """gemm_bf16 = gemm8 (8-phase MFMA) where the shape allows it, library GEMM otherwise"""
     w = (0.05 * torch.randn(N, K, device=DEV)).to(torch.bfloat16)
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     ea = torch.randn(M, 32, device=DEV).to(torch.bfloat16)
