@@ -25,6 +25,7 @@ architecture with random weights for smoke runs.
 from __future__ import annotations
 
 import argparse
+import dataclasses
 import json
 import os
 import sys
@@ -516,6 +517,74 @@ def cmd_convert_alpaca(a):
     print(json.dumps({"records": len(out), "out": a.out}))
 
 
+def _nb_tokenizer(spec: str, texts: list[str]):
+    from ..train.data import ByteTokenizer, CharTokenizer, load_tokenizer
+    if spec == "char":
+        return CharTokenizer("".join(texts))
+    if spec == "bytes":
+        return ByteTokenizer()
+    return load_tokenizer(spec[3:] if spec.startswith("hf:") else spec, pad_to_eos=False)
+
+
+def cmd_minibert_imdb(a):
+    """Transformer_Basics cell 34: MiniBert sentiment classifier (IMDb in the notebook; any local
+    JSONL/JSON of {text, label} here, or a synthetic sentiment set without --data)."""
+    import random
+    from ..train.data import load_records
+    from ..train.teaching import MiniBertConfig, train_minibert_classifier
+    if a.data:
+        recs = load_records(a.data)
+        recs = [{"text": r[a.text_field], "label": int(r[a.label_field])} for r in recs]
+    else:
+        rng = random.Random(0)
+        recs = [{"text": " ".join(rng.choice(["the", "movie", "plot", "was", "acting"]) for _ in range(8)) +
+                 (" great fun" if i % 2 else " awful boring"), "label": i % 2} for i in range(600)]
+    test = load_records(a.test) if a.test else None
+    if test is None:
+        n = max(1, len(recs) // 10)
+        recs, test = recs[n:], recs[:n]
+    else:
+        test = [{"text": r[a.text_field], "label": int(r[a.label_field])} for r in test]
+    tok = _nb_tokenizer(a.tokenizer, [r["text"] for r in recs + test])
+    cfg = MiniBertConfig(hidden_size=a.hidden_size, num_layers=a.num_layers, max_len=a.max_len, epochs=a.epochs,
+                         batch_size=a.batch_size, lr=a.lr)
+    h = train_minibert_classifier(recs, test, tok, cfg, pad_id=getattr(tok, "pad_token_id", None) or 0)
+    if a.save:
+        torch.save({"model_state": h["model"].state_dict(), "config": dataclasses.asdict(cfg)}, a.save)
+    print(json.dumps({k: v for k, v in h.items() if k != "model"}))
+
+
+def cmd_nb_gpt(a):
+    """Transformer_Basics cells 39 / 41: notebook GPT on WikiText-2 (GPT-2 vocab) or the Chinese
+    CLUECorpusSmall (bert-base-chinese vocab) — any local corpus (file or directory of .txt)."""
+    from ..models.teaching import NotebookGPTConfig
+    from ..train.data import load_text_corpus
+    from ..train.teaching import train_notebook_gpt
+    if os.path.isdir(a.data):                    # CLUECorpusSmall layout: a directory of text files
+        texts = []
+        for fn in sorted(os.listdir(a.data)):
+            if fn.endswith((".txt", ".jsonl", ".json")):
+                texts += load_text_corpus(os.path.join(a.data, fn))
+    else:
+        texts = load_text_corpus(a.data)
+    tok = _nb_tokenizer(a.tokenizer, texts)
+    cfg = NotebookGPTConfig(vocab_size=int(getattr(tok, "vocab_size", 256) or len(tok)), n_embd=a.n_embd,
+                            n_head=a.n_head, n_layer=a.n_layer, max_seq_len=a.max_seq_len)
+    out = train_notebook_gpt(texts, tok, cfg, epochs=a.epochs, batch_size=a.batch_size, lr=a.lr,
+                             max_steps=a.max_steps, prompt=a.prompt, gen_tokens=a.gen_tokens)
+    if a.save:
+        torch.save({"model_state": out["model"].state_dict(), "config": dataclasses.asdict(cfg)}, a.save)
+    print(json.dumps({"final_loss": out["losses"][-1], "steps": out["steps"], "sample": out.get("sample")},
+                     ensure_ascii=False))
+
+
+def cmd_seq2seq_demo(a):
+    """Transformer_Basics cells 20-22: the encoder-decoder Transformer learns sequence reversal."""
+    from ..train.teaching import train_seq2seq
+    _, losses, acc = train_seq2seq(steps=a.steps, vocab=a.vocab, length=a.length, num_layers=a.num_layers)
+    print(json.dumps({"first_loss": losses[0], "final_loss": losses[-1], "exact_match": acc}))
+
+
 def cmd_hf_classify(a):
     """G5 ``HF_Basics/trainer_demo.py``: BERT sequence classification with the Trainer (eval and
     save per epoch, best model by accuracy)."""
@@ -839,6 +908,44 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--name", default="马哥教育AI小助手")
     p.add_argument("--author", default="马哥教育AI团队")
     p.set_defaults(fn=cmd_convert_alpaca)
+
+    p = sub.add_parser("minibert-imdb", help="Transformer_Basics cell 34: MiniBert sentiment classifier")
+    p.add_argument("--data", default=None, help="JSONL/JSON with text + label (IMDb export); synthetic if omitted")
+    p.add_argument("--test", default=None)
+    p.add_argument("--text-field", dest="text_field", default="text")
+    p.add_argument("--label-field", dest="label_field", default="label")
+    p.add_argument("--tokenizer", default="bytes", help="bytes | char | hf:<local bert-base-uncased dir>")
+    p.add_argument("--hidden-size", dest="hidden_size", type=int, default=128)
+    p.add_argument("--num-layers", dest="num_layers", type=int, default=2)
+    p.add_argument("--max-len", dest="max_len", type=int, default=256)
+    p.add_argument("--epochs", type=int, default=2)
+    p.add_argument("--batch-size", dest="batch_size", type=int, default=16)
+    p.add_argument("--lr", type=float, default=1e-3)
+    p.add_argument("--save", default=None)
+    p.set_defaults(fn=cmd_minibert_imdb)
+
+    p = sub.add_parser("nb-gpt", help="Transformer_Basics cells 39/41: notebook GPT (WikiText / Chinese GPT)")
+    p.add_argument("--data", required=True, help="text file or a directory of .txt files (CLUECorpusSmall)")
+    p.add_argument("--tokenizer", default="char", help="char | bytes | hf:<local gpt2 or bert-base-chinese dir>")
+    p.add_argument("--n-embd", dest="n_embd", type=int, default=256)
+    p.add_argument("--n-head", dest="n_head", type=int, default=8)
+    p.add_argument("--n-layer", dest="n_layer", type=int, default=6)
+    p.add_argument("--max-seq-len", dest="max_seq_len", type=int, default=128)
+    p.add_argument("--epochs", type=int, default=1)
+    p.add_argument("--batch-size", dest="batch_size", type=int, default=16)
+    p.add_argument("--lr", type=float, default=3e-4)
+    p.add_argument("--max-steps", dest="max_steps", type=int, default=-1)
+    p.add_argument("--prompt", default=None)
+    p.add_argument("--gen-tokens", dest="gen_tokens", type=int, default=50)
+    p.add_argument("--save", default=None)
+    p.set_defaults(fn=cmd_nb_gpt)
+
+    p = sub.add_parser("seq2seq-demo", help="Transformer_Basics cells 20-22: encoder-decoder on sequence reversal")
+    p.add_argument("--steps", type=int, default=400)
+    p.add_argument("--vocab", type=int, default=12)
+    p.add_argument("--length", type=int, default=6)
+    p.add_argument("--num-layers", dest="num_layers", type=int, default=2)
+    p.set_defaults(fn=cmd_seq2seq_demo)
 
     p = sub.add_parser("hf-classify")
     p.add_argument("--model-path", dest="model_path", help="local bert-base-uncased style dir")

@@ -142,3 +142,28 @@ def test_infer_tp_pp_under_torchrun(par, capsys):
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.rstrip("\n").splitlines()[-1] == single.rstrip("\n")   # (gloo logs its connects first)
+
+
+def test_teaching_notebook_commands(tmp_path):
+    """lipa seq2seq-demo / nb-gpt (Chinese corpus directory) / minibert-imdb (JSONL) run end to end."""
+    import json as _json
+    import subprocess as _sp
+    import sys as _sys
+    d = tmp_path / "clue"
+    d.mkdir()
+    (d / "part0.txt").write_text("学习大模型训练与推理。\n马哥教育AI小助手。\n" * 4, encoding="utf-8")
+    recs = tmp_path / "imdb.jsonl"
+    recs.write_text("\n".join(_json.dumps({"text": ("great fun " if i % 2 else "awful boring ") * 3, "label": i % 2})
+                              for i in range(40)))
+    cmds = [["seq2seq-demo", "--steps", "20"],
+            ["nb-gpt", "--data", str(d), "--n-layer", "1", "--n-embd", "32", "--n-head", "2", "--max-seq-len", "8",
+             "--batch-size", "2", "--prompt", "马哥", "--gen-tokens", "3", "--save", str(tmp_path / "g.pt")],
+            ["minibert-imdb", "--data", str(recs), "--epochs", "1", "--max-len", "32", "--hidden-size", "32",
+             "--save", str(tmp_path / "b.pt")]]
+    for c in cmds:
+        r = _sp.run([_sys.executable, "-m", "llm_in_practise_amd.cli.main", *c], capture_output=True, text=True,
+                    timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out = _json.loads(r.stdout.strip().splitlines()[-1])
+        assert out
+    assert (tmp_path / "g.pt").exists() and (tmp_path / "b.pt").exists()
