@@ -422,31 +422,44 @@ def cmd_eval_quant(a):
     print(json.dumps({"self_ppl": ppl, "pass": ppl < PASS_THRESHOLD, "threshold": PASS_THRESHOLD}))
 
 
-def cmd_serve(a):
+def _serving_engine_from_args(a, tp=None, tpg=None, ppg=None):
+    """Build the ServingEngine ``lipa serve`` describes (runs in the engine process by default)."""
     from ..infer.engine import ServingEngine
-    from ..infer.server import serve
     from ..train.data import load_tokenizer
-    tp, tpg, ppg = _parallel(a)
     m = _load_for_inference(a.model, a.adapter, quant=a.quant, tp_group=tpg, pp_group=ppg)
     tok = load_tokenizer(a.tokenizer or a.model)
+    loras = dict(spec.split("=", 1) for spec in a.lora_modules) if getattr(a, "lora_modules", None) else None
+    return ServingEngine(m, tok, model_name=a.served_model_name or os.path.basename(a.model.rstrip("/")),
+                         max_batch=a.max_batch, system_prompt=a.system, tp_group=tp,
+                         max_model_len=a.max_model_len,
+                         prefix_cache_blocks=a.prefix_blocks if a.prefix_caching else 0,
+                         chunked_prefill=a.max_batched_tokens if a.chunked_prefill else 0,
+                         lora_modules=loras, host_cache_blocks=getattr(a, "host_blocks", 0))
+
+
+def cmd_serve(a):
+    """OpenAI server.  Single-GPU serving runs the engine core in its own process (the HTTP
+    process only formats and streams — ``infer/mp_engine.py``); TP/PP groups and
+    ``--no-engine-process`` keep the engine in-process."""
+    from ..infer.server import serve
+    if getattr(a, "lora_modules", None) and not a.enable_lora:
+        raise SystemExit("--lora-modules needs --enable-lora (vLLM semantics)")
     moderation = None
     if a.guard_url:
         from ..infer.guard import GuardClient
         moderation = GuardClient(a.guard_url).moderate_sync
-    loras = None
-    if getattr(a, "lora_modules", None):
-        if not a.enable_lora:
-            raise SystemExit("--lora-modules needs --enable-lora (vLLM semantics)")
-        loras = dict(spec.split("=", 1) for spec in a.lora_modules)
-    eng = ServingEngine(m, tok, model_name=a.served_model_name or os.path.basename(a.model.rstrip("/")),
-                        max_batch=a.max_batch, system_prompt=a.system, tp_group=tp,
-                        max_model_len=a.max_model_len,
-                        prefix_cache_blocks=a.prefix_blocks if a.prefix_caching else 0,
-                        chunked_prefill=a.max_batched_tokens if a.chunked_prefill else 0,
-                        lora_modules=loras, host_cache_blocks=getattr(a, "host_blocks", 0))
-    if tp is not None and eng.tp_rank != 0:
-        eng.follower_loop()              # TP / PP followers replay rank 0's iterations
-        return
+    tp, tpg, ppg = _parallel(a)
+    if tp is None and getattr(a, "engine_process", True):
+        from ..infer.mp_engine import EngineClient, PromptFormatter
+        from ..train.data import load_tokenizer
+        fmt = PromptFormatter(load_tokenizer(a.tokenizer or a.model), a.system)
+        args = argparse.Namespace(**{k: v for k, v in vars(a).items() if k != "fn"})   # picklable
+        eng = EngineClient(_serving_engine_from_args, (args,), fmt)
+    else:
+        eng = _serving_engine_from_args(a, tp, tpg, ppg)
+        if tp is not None and eng.tp_rank != 0:
+            eng.follower_loop()              # TP / PP followers replay rank 0's iterations
+            return
     serve(eng, a.host, a.port, api_key=a.api_key, moderation=moderation)
 
 
@@ -490,7 +503,8 @@ def cmd_lf(a):
                                 tokenizer=a.tokenizer, quant="nf4" if int(cfg.get("quantization_bit") or 0) == 4
                                 else None, host="0.0.0.0", port=int(cfg.get("port", 7860)), max_batch=16,
                                 served_model_name=None, api_key=None, guard_url=None, system=None,
-                                prefix_caching=True, prefix_blocks=512, max_model_len=None)
+                                prefix_caching=True, prefix_blocks=512, max_model_len=None,
+                                engine_process=False)
         cmd_serve(ns)
 
 
@@ -863,6 +877,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help="adapters selectable per request by `model` name")
     p.add_argument("--kv-host-cache-blocks", dest="host_blocks", type=int, default=0,
                    help="prefix-cache host tier (LMCache local-CPU role): 64-token chunks spilled to pinned RAM")
+    p.add_argument("--no-engine-process", dest="engine_process", action="store_false",
+                   help="run the engine core in the HTTP process (default: its own process)")
     _add_parallel_args(p)
     p.set_defaults(fn=cmd_serve)
 

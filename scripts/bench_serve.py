@@ -82,6 +82,54 @@ async def one_request(client, url, model, msgs, max_tokens):
     return {"ttft": ttft or (time.perf_counter() - t0), "itl": itl, "out_tokens": n, "e2e": time.perf_counter() - t0}
 
 
+async def _run_raw(url, model, prompts, conc, max_tokens):
+    import httpx
+    sem = asyncio.Semaphore(conc)
+    limits = httpx.Limits(max_connections=None, max_keepalive_connections=None)
+    async with httpx.AsyncClient(limits=limits) as client:
+        async def task(m):
+            async with sem:
+                return await one_request(client, url, model, m, max_tokens)
+        t0 = time.perf_counter()
+        res = await asyncio.gather(*[task(m) for m in prompts])
+        return res, time.perf_counter() - t0
+
+
+def _proc_level(args):
+    url, model, prompts, conc, max_tokens, start_at = args
+    while time.time() < start_at:            # every client process starts together
+        time.sleep(0.001)
+    return asyncio.run(_run_raw(url, model, prompts, conc, max_tokens))
+
+
+def run_level_procs(url, model, prompts, conc, max_tokens, procs):
+    """The load generator itself split over ``procs`` processes (one Python event loop parsing
+    10k+ SSE events/s saturates and inflates TTFT / ITL): prompts and concurrency are divided,
+    the per-request samples merged, duration = the slowest process."""
+    import multiprocessing as mp
+    parts = [prompts[i::procs] for i in range(procs)]
+    concs = [conc // procs + (1 if i < conc % procs else 0) for i in range(procs)]
+    start = time.time() + 1.0
+    with mp.get_context("spawn").Pool(procs) as pool:
+        outs = pool.map(_proc_level, [(url, model, p, max(1, c), max_tokens, start) for p, c in zip(parts, concs)])
+    res = [r for rs, _ in outs for r in rs]
+    return _summary(res, max(d for _, d in outs), conc)
+
+
+def _summary(res, dur, conc):
+    ttft = [r["ttft"] * 1e3 for r in res]
+    itl = [x * 1e3 for r in res for x in r["itl"]]
+    toks = sum(r["out_tokens"] for r in res)
+    per_req = [r["out_tokens"] / r["e2e"] for r in res if r["e2e"] > 0]
+    return {"concurrency": conc, "requests": len(res), "duration_s": round(dur, 3),
+            "mean_ttft_ms": round(statistics.mean(ttft), 2), "p99_ttft_ms": round(pct(ttft, 99), 2),
+            "mean_itl_ms": round(statistics.mean(itl), 2) if itl else None,
+            "p99_itl_ms": round(pct(itl, 99), 2) if itl else None,
+            "req_per_s": round(len(res) / dur, 3), "output_tok_per_s": round(toks / dur, 1),
+            "mean_request_tok_per_s": round(statistics.mean(per_req), 2) if per_req else None,
+            "p50_request_tok_per_s": round(statistics.median(per_req), 2) if per_req else None}
+
+
 async def run_level(url, model, prompts, conc, max_tokens):
     import httpx
     sem = asyncio.Semaphore(conc)
@@ -168,6 +216,8 @@ def main():
     ap.add_argument("--spawn", action="store_true",
                     help="with --inprocess: run the server in a child process (client and server do not share a GIL)")
     ap.add_argument("--serve-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--client-procs", type=int, default=1,
+                    help="split the load generator over N processes (merged statistics)")
     ap.add_argument("--engine-process", action="store_true",
                     help="run the engine core in its own process (frontend only formats / streams)")
     a = ap.parse_args()
@@ -203,7 +253,11 @@ def main():
         prompts = [p for p in mixed_dataset(4 * a.num_prompts) if len(p) == 1][:a.num_prompts]
     else:
         prompts = sharegpt(a.dataset, a.num_prompts)
-    rows = [asyncio.run(run_level(url, a.model, prompts, c, a.max_tokens)) for c in a.concurrency]
+    if a.client_procs > 1:
+        rows = [run_level_procs(url, a.model, prompts, c, a.max_tokens, min(a.client_procs, c))
+                for c in a.concurrency]
+    else:
+        rows = [asyncio.run(run_level(url, a.model, prompts, c, a.max_tokens)) for c in a.concurrency]
     for r in rows:
         print(json.dumps(r))
     if a.out:
