@@ -41,6 +41,9 @@ void launch_nf4_quantize(const void*, uint8_t*, float*, size_t, hipStream_t);
 void launch_nf4_dequant2(const uint8_t*, const float*, void*, size_t, hipStream_t);
 int skinny_splits(int, int);
 void launch_gemm_skinny(const void*, int, const void*, const void*, void*, float*, int, int, int, int, hipStream_t);
+int w4_skinny_splits(int, int);
+void launch_gemm_w4_skinny(const void*, int, const uint8_t*, const float*, const float*, int, const void*, void*, float*,
+                           int, int, int, int, hipStream_t);
 void set_dequant_variant(int);
 void launch_nf4_dequant(const uint8_t*, const float*, const uint8_t*, const float*, const float*, const float*, void*,
                         size_t, hipStream_t);
@@ -78,6 +81,14 @@ void launch_decode_attention2(const void*, int, const void*, int, const void*, i
                               float*, float*, void*, int, int, int, int, int, int, float, hipStream_t);
 void launch_sample(int, const void*, const int*, int, float*, int64_t*, int, int, float, int, float, float, uint64_t,
                    hipStream_t);
+void* car_alloc(size_t, bool);
+void car_free(void*);
+bool car_ipc_handle(void*, char*);
+void* car_ipc_open(const char*);
+void car_ipc_close(void*);
+int car_max_blocks();
+void launch_custom_allreduce(int, const void* const*, void* const*, uint32_t* const*, int*, int, int, uint32_t, size_t,
+                             bool, float, void*, int, hipStream_t);
 void launch_dropout_fwd(const void*, void*, size_t, uint64_t, float, hipStream_t);
 void launch_dropout_bwd_add(void*, const void*, size_t, uint64_t, float, hipStream_t);
 
@@ -342,6 +353,37 @@ Tensor gemm_skinny(Tensor x, Tensor w, optional<Tensor> residual) {
   Tensor out = at::empty({M, N}, x.options());
   launch_gemm_skinny(x.data_ptr(), x.stride(0), w.data_ptr(), rp, out.data_ptr(), part.data_ptr<float>(), M, N, K, S,
                      stream());
+  return out;
+}
+
+// W4A16 decode GEMM: x [M<=256, K] bf16, codes u8 [N, K/2] (high nibble = even k), scales / biases fp32 [N, K/gs]
+Tensor gemm_w4_skinny(Tensor x, Tensor codes, Tensor scales, Tensor biases, int64_t N, int64_t gs,
+                      optional<Tensor> residual) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_CONTIG(codes); CHECK_CONTIG(scales); CHECK_CONTIG(biases);
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && M >= 1 && M <= 256,
+              "gemm_w4_skinny: x [M<=256, K] row-major, 16-B aligned rows");
+  TORCH_CHECK(codes.scalar_type() == at::kByte && codes.size(0) == N && codes.size(1) * 2 == K,
+              "gemm_w4_skinny: codes [N, K/2] uint8");
+  TORCH_CHECK(K % 256 == 0 && gs % 128 == 0 && K % gs == 0 && N % 16 == 0, "gemm_w4_skinny: K%256, gs%128, N%16");
+  TORCH_CHECK(scales.scalar_type() == at::kFloat && biases.scalar_type() == at::kFloat &&
+                  scales.numel() == N * (K / gs) && biases.numel() == N * (K / gs),
+              "gemm_w4_skinny: fp32 scales / biases [N, K/gs]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(codes.data_ptr()) % 16 == 0,
+              "gemm_w4_skinny: 16-B aligned operands");
+  const void* rp = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    CHECK_BF16((*residual));
+    CHECK_CONTIG((*residual));
+    TORCH_CHECK(residual->size(0) == M && residual->size(1) == N, "gemm_w4_skinny: residual shape");
+    rp = residual->data_ptr();
+  }
+  const int S = w4_skinny_splits(N, K);
+  Tensor part = at::empty({S, M, N}, x.options().dtype(at::kFloat));
+  Tensor out = at::empty({M, N}, x.options());
+  launch_gemm_w4_skinny(x.data_ptr(), x.stride(0), codes.data_ptr<uint8_t>(), scales.data_ptr<float>(),
+                        biases.data_ptr<float>(), (int)gs, rp, out.data_ptr(), part.data_ptr<float>(), M, N, K, S,
+                        stream());
   return out;
 }
 
@@ -833,6 +875,53 @@ Tensor moe_wgrad(Tensor dout, Tensor ys, Tensor pos_of, int64_t k) {
   return dw;
 }
 
+// ------------------------------------------------------------------ custom all-reduce (allreduce.hip)
+int64_t car_alloc_py(int64_t bytes, bool uncached) {
+  void* p = car_alloc((size_t)bytes, uncached);
+  TORCH_CHECK(p != nullptr, "car_alloc: device allocation of ", bytes, " B failed");
+  return reinterpret_cast<int64_t>(p);
+}
+void car_free_py(int64_t p) { car_free(reinterpret_cast<void*>(p)); }
+pybind11::bytes car_handle_py(int64_t p) {
+  char h[64] = {0};
+  TORCH_CHECK(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle larger than 64 B");
+  TORCH_CHECK(car_ipc_handle(reinterpret_cast<void*>(p), h), "hipIpcGetMemHandle failed (is HSA_ENABLE_IPC_MODE_LEGACY=0 set?)");
+  return pybind11::bytes(h, sizeof(hipIpcMemHandle_t));
+}
+int64_t car_open_py(pybind11::bytes h) {
+  std::string s = h;
+  char buf[64] = {0};
+  memcpy(buf, s.data(), std::min<size_t>(s.size(), 64));
+  void* p = car_ipc_open(buf);
+  TORCH_CHECK(p != nullptr, "hipIpcOpenMemHandle failed");
+  return reinterpret_cast<int64_t>(p);
+}
+void car_close_py(int64_t p) { car_ipc_close(reinterpret_cast<void*>(p)); }
+
+void custom_allreduce(Tensor out, std::vector<int64_t> data, std::vector<int64_t> result, std::vector<int64_t> flags,
+                      Tensor err, int64_t rank, int64_t epoch, bool two_shot, double scale, int64_t blocks) {
+  CHECK_CUDA(out); CHECK_CONTIG(out); CHECK_CUDA(err);
+  const int W = (int)data.size();
+  TORCH_CHECK(W >= 1 && W <= 8 && (int)result.size() == W && (int)flags.size() == W, "custom_allreduce: 1..8 peers");
+  TORCH_CHECK(rank >= 0 && rank < W, "custom_allreduce: rank");
+  TORCH_CHECK(err.scalar_type() == at::kInt && err.numel() >= 1, "custom_allreduce: err must be int32");
+  const size_t bytes = out.numel() * out.element_size();
+  TORCH_CHECK(bytes % 16 == 0, "custom_allreduce: byte size must be a multiple of 16");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "custom_allreduce: out must be 16-B aligned");
+  std::vector<const void*> d(W);
+  std::vector<void*> r(W);
+  std::vector<uint32_t*> f(W);
+  for (int i = 0; i < W; ++i) {
+    d[i] = reinterpret_cast<const void*>(data[i]);
+    r[i] = reinterpret_cast<void*>(result[i]);
+    f[i] = reinterpret_cast<uint32_t*>(flags[i]);
+    TORCH_CHECK(data[i] % 16 == 0 && result[i] % 16 == 0 && flags[i] % 4 == 0, "custom_allreduce: peer alignment");
+  }
+  // in place: the kernel stages `out` into this rank's data area (peers read it from there)
+  launch_custom_allreduce(dtype_code(out), d.data(), r.data(), f.data(), err.data_ptr<int>(), W, (int)rank,
+                          (uint32_t)epoch, bytes, two_shot, (float)scale, out.data_ptr(), (int)blocks, stream());
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "llm_in_practise_amd gfx950 (MI355X / CDNA4) kernels";
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
@@ -870,6 +959,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nf4_dequant", &nf4_dequant);
   m.def("nf4_dequant_fast", &nf4_dequant_fast);
   m.def("gemm_skinny", &gemm_skinny);
+  m.def("gemm_w4_skinny", &gemm_w4_skinny);
   m.def("set_dequant_variant", &set_dequant_variant);
   m.def("nf4_pack", &nf4_pack);
   m.def("nf4_absmax_t", &nf4_absmax_t);
@@ -881,4 +971,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_fwd_ext", &attn_fwd_ext);
   m.def("attn_bwd", &attn_bwd);
+  m.def("car_alloc", &car_alloc_py);
+  m.def("car_free", &car_free_py);
+  m.def("car_handle", &car_handle_py);
+  m.def("car_open", &car_open_py);
+  m.def("car_close", &car_close_py);
+  m.def("car_max_blocks", &car_max_blocks);
+  m.def("custom_allreduce", &custom_allreduce);
 }

@@ -417,12 +417,17 @@ class ServingEngine:
             elif kind == "error":
                 raise RuntimeError(val)
 
-    def shutdown(self):
+    def shutdown(self, timeout: float = 30.0):
+        """Stop the engine loop and wait for it, so no GPU work is in flight while the caller (or
+        the interpreter) tears down graphs and allocators."""
         if self.tp_group is None:
             self._stop = True
         else:   # SPMD: rank 0 must hand the stop to its followers inside the iteration protocol
             self._closing = True
         self.q.put(None)
+        w = self._worker
+        if w is not None and w is not threading.current_thread():
+            w.join(timeout)
 
     # ------------------------------------------------------------------ worker
     def _loop(self):

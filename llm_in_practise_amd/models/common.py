@@ -8,6 +8,7 @@ import torch.nn as nn
 
 from ..ops.linear import LoraBranch, fused_linear
 from ..peft.lora import Linear4bit, LoraLayer, base_of
+from ..quant.int4 import Int4Linear, Int4Weight, int4_linear
 from ..quant.nf4 import NF4Weight, concat_nf4
 
 
@@ -67,6 +68,19 @@ class FusedProjection:
                 r0 += n
                 b0 += nblk
             biases = [l.bias for l in leaves]
+        elif all(isinstance(l, Int4Linear) for l in leaves):   # W4A16 (GPTQ / AWQ / RTN): concat along N
+            codes = torch.cat([l.codes for l in leaves], 0)
+            scales = torch.cat([l.scales for l in leaves], 0)
+            zeros = torch.cat([l.zeros for l in leaves], 0)
+            self.base = Int4Weight(codes, scales, zeros, (codes.shape[0], leaves[0].in_features),
+                                   leaves[0].group_size, leaves[0].sym)
+            r0 = 0
+            for l in leaves:
+                n = l.out_features
+                l.load(Int4Weight(codes[r0:r0 + n], scales[r0:r0 + n], zeros[r0:r0 + n], (n, l.in_features),
+                                  l.group_size, l.sym))
+                r0 += n
+            biases = [l.bias for l in leaves]
         else:
             w = torch.cat([l.weight.detach() for l in leaves], 0)
             self.base = w
@@ -101,6 +115,12 @@ class FusedProjection:
         return out
 
     def __call__(self, x, residual=None, training: bool = True):
+        if isinstance(self.base, Int4Weight):
+            y = int4_linear(x, self.base, self.bias, residual)
+            for br in self.branches(False):       # inference-only base: unmerged adapters as plain low-rank adds
+                y2 = y.view(-1, y.shape[-1])
+                y2[:, br.c0:br.c1] += ((x.reshape(-1, x.shape[-1]) @ br.a.t().to(x.dtype)) @ br.b.t().to(x.dtype)) * br.scaling
+            return _apply_multi_lora(self.mods, self.splits, x, y)
         y = fused_linear(x, self.base, self.bias, self.branches(training), residual, training)
         return _apply_multi_lora(self.mods, self.splits, x, y)
 
@@ -127,6 +147,9 @@ def project(mods: list[nn.Module], x: torch.Tensor, residual: torch.Tensor | Non
         return fused(x, residual, training)
     if len(mods) == 1:
         m = mods[0]
+        if isinstance(m, Int4Linear):            # o_proj / down_proj of a W4A16 model: residual in the epilogue
+            y = int4_linear(x.to(torch.bfloat16) if x.is_cuda else x, m.int4, m.bias, residual)
+            return _apply_multi_lora(mods, [m.out_features], x, y)
         if _trainable_base(m) or not isinstance(_leaf_linear(m), (nn.Linear, Linear4bit)):
             y = m(x)
             y = _apply_multi_lora(mods, [y.shape[-1]], x, y)
@@ -150,6 +173,8 @@ def can_fuse(mods: list[nn.Module]) -> bool:
     if all(isinstance(l, Linear4bit) for l in leaves):
         k = leaves[0].in_features
         return all(l.in_features == k and (l.out_features * l.in_features // l.blocksize) % 256 == 0 for l in leaves)
+    if all(isinstance(l, Int4Linear) for l in leaves):
+        return len({(l.in_features, l.group_size, l.sym) for l in leaves}) == 1
     if all(isinstance(l, nn.Linear) for l in leaves):
         return len({l.in_features for l in leaves}) == 1 and len({l.weight.dtype for l in leaves}) == 1
     return False

@@ -20,12 +20,17 @@ Bucket size: xGMI rings are per-link bandwidth-bound, so buckets are large (defa
 never fewer than ~4 per model so the first can start early); LoRA-sized gradient sets
 (15-60 MB) become a few collectives.
 
+Small buckets can go over the intra-node peer-memory all-reduce instead of RCCL
+(``custom_allreduce=`` a :class:`~.custom_allreduce.CustomAllReduce`, or ``"auto"`` /
+``LIPA_CUSTOM_AR=1`` to build one): one- or two-shot by size, RCCL above its staging cap.
+
 On start the module's parameters and buffers are broadcast from rank 0
 (``sync_module_states``).
 """
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 import torch.distributed as dist
@@ -46,7 +51,7 @@ class _Bucket:
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, grad_buffer: torch.Tensor | None = None, bucket_mb: float | None = None,
                  broadcast_buffers: bool = True, device_ids=None, find_unused_parameters: bool = False,
-                 overlap: bool = True, flat=None, **_):
+                 overlap: bool = True, flat=None, custom_allreduce=None, **_):
         super().__init__()
         self.module = module
         self.flat = flat
@@ -61,6 +66,14 @@ class DistributedDataParallel(nn.Module):
         self._cuda = self.grad_buffer is not None and self.grad_buffer.is_cuda
         self._stream = torch.cuda.Stream(device=self.grad_buffer.device) if (self.overlap and self._cuda) else None
         self._works: list = []
+        if custom_allreduce is None and os.environ.get("LIPA_CUSTOM_AR", "0") == "1":
+            custom_allreduce = "auto"
+        if custom_allreduce == "auto":
+            custom_allreduce = None
+            if is_dist() and self.grad_buffer is not None:
+                from .custom_allreduce import CustomAllReduce
+                custom_allreduce = CustomAllReduce(device=self.grad_buffer.device)
+        self.car = custom_allreduce
         if self.grad_buffer is not None:
             total = self.grad_buffer.numel()
             cap = int((bucket_mb if bucket_mb is not None else 32.0) * (1 << 20) / 4)
@@ -116,7 +129,12 @@ class DistributedDataParallel(nn.Module):
         if self._stream is not None:
             self._stream.wait_stream(torch.cuda.current_stream(view.device))
             with torch.cuda.stream(self._stream):
-                all_reduce_mean_(view)
+                if self.car is not None and self.car.should_use(view):
+                    self.car.all_reduce_(view, average=True)
+                else:
+                    all_reduce_mean_(view)
+        elif self.car is not None and self.car.should_use(view):     # peer-memory path (host model on CPU)
+            self.car.all_reduce_(view, average=True)
         else:       # gloo / CPU: an async collective on the process group's own thread
             self._works.append((dist.all_reduce(view, async_op=True), view))
 

@@ -82,6 +82,10 @@ class Int4Weight:
             self.packed = (cf, st, bt)
         return self.packed
 
+    def skinny_ok(self) -> bool:
+        n, k = self.shape
+        return n % 16 == 0 and k % 256 == 0 and self.group_size % 128 == 0
+
     def gemv_tables(self):
         if self._gemv is None:
             self._gemv = (self.scales.float().contiguous(), self.bias_table().contiguous())
@@ -212,6 +216,12 @@ def from_awq(d: dict, group_size: int) -> Int4Weight:
 
 
 # ============================================================================ module + op
+import os as _os
+
+# decode-batch W4A16 kernel up to this many rows (profiles/w4a16_decode_gemm.txt); M = 1 stays on
+# the GEMV, larger M on the MFMA tile kernel
+_W4_SKINNY_MAX = int(_os.environ.get("LIPA_W4_SKINNY_MAX", "256"))
+
 def int4_linear(x: torch.Tensor, w: Int4Weight, bias: torch.Tensor | None = None,
                 residual: torch.Tensor | None = None) -> torch.Tensor:
     from ..ops._native import native, use_native
@@ -219,7 +229,11 @@ def int4_linear(x: torch.Tensor, w: Int4Weight, bias: torch.Tensor | None = None
     x2 = x.reshape(-1, shape[-1])
     n = w.shape[0]
     r2 = residual.reshape(-1, n).contiguous() if residual is not None else None
-    if use_native(x2) and x2.dtype == torch.bfloat16 and w.kernel_ok():
+    M = x2.shape[0]
+    if use_native(x2) and x2.dtype == torch.bfloat16 and 2 <= M <= _W4_SKINNY_MAX and w.skinny_ok():
+        s, b = w.gemv_tables()       # decode batches: split-K weight streaming, dequant in registers
+        y = native().gemm_w4_skinny(x2.contiguous(), w.codes, s, b, n, w.group_size, r2)
+    elif use_native(x2) and x2.dtype == torch.bfloat16 and w.kernel_ok():
         x2 = x2.contiguous()
         if x2.shape[0] <= 8:
             s, b = w.gemv_tables()

@@ -68,3 +68,20 @@ def test_scaling_harness_runs_each_world_size(tmp_path):
     d = json.loads(out.read_text())
     assert [t["n_gpus"] for t in d["table"]] == [1, 2]
     assert d["table"][0]["weak_scaling_efficiency"] == 1.0 and d["table"][1]["weak_scaling_efficiency"] > 0
+
+
+def test_awq_infer_bench_tiny(tmp_path):
+    """BASELINE #5 harness: merged LoRA -> AWQ int4, decode/prefill/serve on both, quality vs bf16."""
+    out = tmp_path / "awq.json"
+    r = subprocess.run([sys.executable, "-m", "llm_in_practise_amd.bench.awq_infer", "--model", "qwen3-tiny",
+                        "--batches", "1", "4", "--steps", "2", "--prefill", "2", "64", "--ppl-prompts", "2",
+                        "--ppl-new", "8", "--calib", "2", "--calib-len", "64", "--group-size", "32",
+                        "--serve-requests", "4", "--serve-tokens", "8", "--max-len", "256", "--ctx", "32",
+                        "--out", str(out)], capture_output=True, text=True, timeout=600, cwd=ROOT,
+                       env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(out.read_text())
+    assert d["int4"]["weight_bytes"] < 0.35 * d["bf16"]["weight_bytes"]
+    assert d["int4"]["kl_vs_bf16"] < 0.05 and d["int4"]["top1_agree_vs_bf16"] > 0.5
+    assert d["int4"]["serve"]["output_tok_per_s"] > 0
+    assert [x["batch"] for x in d["int4"]["decode"]] == [1, 4]

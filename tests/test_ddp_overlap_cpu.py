@@ -31,13 +31,14 @@ def _data(step, rank, n=4):
     return torch.randn(n, 8, generator=g), torch.randn(n, 1, generator=g)
 
 
-def _worker(rank, world, port, out, ga):
+def _worker(rank, world, port, out, ga, car=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(0)
     net = Net()
     opt = AdamW(net.parameters(), lr=1e-2, weight_decay=0.0)
-    ddp = DistributedDataParallel(net, flat=opt.flat, bucket_mb=0.004)   # ~1k floats: several buckets
+    ddp = DistributedDataParallel(net, flat=opt.flat, bucket_mb=0.004,   # ~1k floats: several buckets
+                                  custom_allreduce="auto" if car else None)
     logs = []
     for s in range(3):
         for m in range(ga):
@@ -50,8 +51,11 @@ def _worker(rank, world, port, out, ga):
         ddp.allreduce_grads()
         opt.step()
         opt.zero_grad()
+    calls = dict(ddp.car.calls) if ddp.car is not None else {}
+    if ddp.car is not None:
+        ddp.car.close()
     if rank == 0:
-        torch.save({"sd": net.state_dict(), "logs": logs, "nb": len(ddp._buckets)}, out)
+        torch.save({"sd": net.state_dict(), "logs": logs, "nb": len(ddp._buckets), "calls": calls}, out)
     torch.distributed.destroy_process_group()
 
 
@@ -87,3 +91,14 @@ def test_ddp_overlap_matches_oracle_and_launches_during_backward(tmp_path):
             # every bucket was issued from a gradient-ready hook inside backward, in reverse order
             assert [why for _, why in log] == ["hook"] * got["nb"]
             assert [b for b, _ in log] == list(range(got["nb"]))
+
+
+def test_ddp_buckets_over_custom_allreduce_match_oracle(tmp_path):
+    """Gradient buckets through the peer-memory all-reduce (its /dev/shm model on CPU)."""
+    out = str(tmp_path / "car.pt")
+    mp.spawn(_worker, args=(2, _port(), out, 2, True), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    want = _oracle(2)
+    for k in want:
+        assert torch.allclose(got["sd"][k], want[k], atol=1e-5), k
+    assert got["calls"]["oneshot"] + got["calls"]["twoshot"] > 0

@@ -41,9 +41,24 @@ def test_gemv_nf4_and_int4(native_ext, M, N, K):
     assert rel(y4, x.float() @ w4.dequantize().t() + res.float()) < 1e-2
 
 
+@pytest.mark.parametrize("M", [1, 2, 8, 17, 40, 64, 100, 256])
+@pytest.mark.parametrize("N,K,gs", [(4096, 4096, 128), (1024, 12288, 128), (48, 512, 256)])
+def test_gemm_w4_skinny(native_ext, M, N, K, gs):
+    """Decode-batch W4A16 (skinny.hip): split-K weight streaming, in-register dequant, vs fp32."""
+    torch.manual_seed(2)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w4 = quantize_rtn(torch.randn(N, K, device=DEV), gs, False)
+    s, b = w4.gemv_tables()
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    y = native_ext.gemm_w4_skinny(x, w4.codes, s, b, N, gs, res)
+    assert rel(y, x.float() @ w4.dequantize().t() + res.float()) < 1e-2
+    y0 = native_ext.gemm_w4_skinny(x, w4.codes, s, b, N, gs, None)
+    assert rel(y0, x.float() @ w4.dequantize().t()) < 1e-2
+
+
 def test_int4_linear_dispatch(native_ext):
     w = quantize_rtn(torch.randn(256, 512, device=DEV), 128)
-    for M in (1, 300):
+    for M in (1, 8, 64, 300):
         x = torch.randn(M, 512, device=DEV).to(torch.bfloat16)
         assert rel(int4_linear(x, w), x.float() @ w.dequantize().t()) < 1e-2
 
