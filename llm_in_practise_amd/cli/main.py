@@ -463,6 +463,21 @@ def cmd_serve(a):
     serve(eng, a.host, a.port, api_key=a.api_key, moderation=moderation)
 
 
+def cmd_serve_deploy(a):
+    """``serve deploy <config.yaml>`` with Ray Serve LLM-app semantics: replicas of
+    ``lipa serve`` on the given GPUs behind an autoscaling proxy (``infer/serve_app.py``)."""
+    import uvicorn
+    from ..infer.serve_app import ServeController, create_serve_proxy, load_serve_config, process_replica_factory
+    gpus = [int(g) for g in a.gpus.split(",")] if a.gpus else None
+    ctl = ServeController(load_serve_config(a.config), process_replica_factory(), gpus=gpus,
+                          control_interval=a.control_interval)
+    ctl.start()
+    try:
+        uvicorn.run(create_serve_proxy(ctl), host=a.host, port=a.port)
+    finally:
+        ctl.shutdown()
+
+
 def cmd_guard(a):
     import uvicorn
     from ..infer.guard import GuardClient, create_guard_app
@@ -881,6 +896,14 @@ def build_parser() -> argparse.ArgumentParser:
                    help="run the engine core in the HTTP process (default: its own process)")
     _add_parallel_args(p)
     p.set_defaults(fn=cmd_serve)
+
+    p = sub.add_parser("serve-deploy", help="Ray Serve-style autoscaling replicas from a serve config (H4)")
+    p.add_argument("config")
+    p.add_argument("--gpus", default=None, help="GPU pool, e.g. 0,1,2,3 (default: no GPU pinning)")
+    p.add_argument("--host", default="0.0.0.0")
+    p.add_argument("--port", type=int, default=8000)
+    p.add_argument("--control-interval", dest="control_interval", type=float, default=1.0)
+    p.set_defaults(fn=cmd_serve_deploy)
 
     p = sub.add_parser("guard")
     p.add_argument("--backend", required=True, help="guard model completions URL")

@@ -356,13 +356,13 @@ Tensor gemm_skinny(Tensor x, Tensor w, optional<Tensor> residual) {
   return out;
 }
 
-// W4A16 decode GEMM: x [M<=256, K] bf16, codes u8 [N, K/2] (high nibble = even k), scales / biases fp32 [N, K/gs]
+// W4A16 decode GEMM: x [M<=64, K] bf16, codes u8 [N, K/2] (high nibble = even k), scales / biases fp32 [N, K/gs]
 Tensor gemm_w4_skinny(Tensor x, Tensor codes, Tensor scales, Tensor biases, int64_t N, int64_t gs,
                       optional<Tensor> residual) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_CONTIG(codes); CHECK_CONTIG(scales); CHECK_CONTIG(biases);
   const int64_t M = x.size(0), K = x.size(1);
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && M >= 1 && M <= 256,
-              "gemm_w4_skinny: x [M<=256, K] row-major, 16-B aligned rows");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && M >= 1 && M <= 64,
+              "gemm_w4_skinny: x [M<=64, K] row-major, 16-B aligned rows");
   TORCH_CHECK(codes.scalar_type() == at::kByte && codes.size(0) == N && codes.size(1) * 2 == K,
               "gemm_w4_skinny: codes [N, K/2] uint8");
   TORCH_CHECK(K % 256 == 0 && gs % 128 == 0 && K % gs == 0 && N % 16 == 0, "gemm_w4_skinny: K%256, gs%128, N%16");

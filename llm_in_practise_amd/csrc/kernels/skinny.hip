@@ -139,8 +139,14 @@ __global__ __launch_bounds__(256) void gemm_w4_skinny_k(const bf16* __restrict__
     for (int b = 0; b < KB; ++b)
       if (b < nb) {
         const int kk = kb + 128 * b;
-        // dequantise the block's 8 A fragments first, then its MFMAs; the pad keeps the next
-        // block's dequant from rewriting fragment registers the last MFMAs may still be reading
+        // x fragments of the whole block into their own registers first (their loads overlap the
+        // dequant), then the 8 dequantised A fragments, then the MFMAs; no register the MFMA
+        // phase reads is rewritten before the closing pad (see the launcher's note)
+        bf16x8 xb[4][MT];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) xb[s][mt] = *reinterpret_cast<const bf16x8*>(xr[mt] + kk + 8 * s);
         bf16x8 a0[4], a1[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -152,9 +158,8 @@ __global__ __launch_bounds__(256) void gemm_w4_skinny_k(const bf16* __restrict__
         for (int s = 0; s < 4; ++s)
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
-            const bf16x8 xb = *reinterpret_cast<const bf16x8*>(xr[mt] + kk + 8 * s);
-            acc[0][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[s], xb, acc[0][mt], 0, 0, 0);
-            acc[1][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[s], xb, acc[1][mt], 0, 0, 0);
+            acc[0][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[s], xb[s][mt], acc[0][mt], 0, 0, 0);
+            acc[1][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[s], xb[s][mt], acc[1][mt], 0, 0, 0);
           }
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
@@ -236,15 +241,14 @@ void launch_gemm_w4_skinny(const void* X, int ldx, const uint8_t* codes, const f
                            hipStream_t st) {
   const int kc = K / S;
   dim3 grid((N + SK_NB - 1) / SK_NB, S);
-#define L(MT) gemm_w4_skinny_k<MT><<<grid, 256, 0, st>>>((const bf16*)X, ldx, codes, scales, biases, gs, part, M, N, K, kc)
-  static const int force_mt = [] { const char* e = getenv("LIPA_W4_MT"); return e ? atoi(e) : 0; }();
-  if (force_mt == 2) L(2);
-  else if (force_mt == 4) L(4);
-  else if (M <= 16) L(1);
+  // MT >= 2 runs one workgroup per CU (a 96 KB dynamic-LDS reservation; the kernel uses no LDS):
+  // measured on MI355X (ROCm 7.2), two co-resident workgroups of the MT >= 2 code returned
+  // nondeterministically wrong fragments (scripts/dbg_w4.py); one per CU is exact.
+#define L(MT) gemm_w4_skinny_k<MT><<<grid, 256, (MT) >= 2 ? 98304 : 0, st>>>((const bf16*)X, ldx, codes, scales, biases, \
+                                                                          gs, part, M, N, K, kc)
+  if (M <= 16) L(1);
   else if (M <= 32) L(2);
-  else if (M <= 64) L(4);
-  else if (M <= 128) L(8);
-  else L(16);
+  else L(4);
 #undef L
   const size_t MN = (size_t)M * N;
   skinny_reduce_k<<<(MN / 8 + 255) / 256, 256, 0, st>>>(part, (const bf16*)res, (bf16*)out, S, MN);

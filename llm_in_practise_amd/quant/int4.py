@@ -218,9 +218,9 @@ def from_awq(d: dict, group_size: int) -> Int4Weight:
 # ============================================================================ module + op
 import os as _os
 
-# decode-batch W4A16 kernel up to this many rows (profiles/w4a16_decode_gemm.txt); M = 1 stays on
-# the GEMV, larger M on the MFMA tile kernel
-_W4_SKINNY_MAX = int(_os.environ.get("LIPA_W4_SKINNY_MAX", "256"))
+# decode-batch W4A16 kernel for 3..64 rows (profiles/w4a16_decode_gemm.txt); M <= 2 stays on the
+# GEMV, larger M on the MFMA tile kernel
+_W4_SKINNY_MAX = min(64, int(_os.environ.get("LIPA_W4_SKINNY_MAX", "64")))
 
 def int4_linear(x: torch.Tensor, w: Int4Weight, bias: torch.Tensor | None = None,
                 residual: torch.Tensor | None = None) -> torch.Tensor:
@@ -230,7 +230,7 @@ def int4_linear(x: torch.Tensor, w: Int4Weight, bias: torch.Tensor | None = None
     n = w.shape[0]
     r2 = residual.reshape(-1, n).contiguous() if residual is not None else None
     M = x2.shape[0]
-    if use_native(x2) and x2.dtype == torch.bfloat16 and 2 <= M <= _W4_SKINNY_MAX and w.skinny_ok():
+    if use_native(x2) and x2.dtype == torch.bfloat16 and 3 <= M <= _W4_SKINNY_MAX and w.skinny_ok():
         s, b = w.gemv_tables()       # decode batches: split-K weight streaming, dequant in registers
         y = native().gemm_w4_skinny(x2.contiguous(), w.codes, s, b, n, w.group_size, r2)
     elif use_native(x2) and x2.dtype == torch.bfloat16 and w.kernel_ok():

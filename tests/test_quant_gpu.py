@@ -41,8 +41,8 @@ def test_gemv_nf4_and_int4(native_ext, M, N, K):
     assert rel(y4, x.float() @ w4.dequantize().t() + res.float()) < 1e-2
 
 
-@pytest.mark.parametrize("M", [1, 2, 8, 17, 40, 64, 100, 256])
-@pytest.mark.parametrize("N,K,gs", [(4096, 4096, 128), (1024, 12288, 128), (48, 512, 256)])
+@pytest.mark.parametrize("M", [1, 2, 8, 17, 32, 40, 64])
+@pytest.mark.parametrize("N,K,gs", [(4096, 4096, 128), (6144, 4096, 128), (4096, 12288, 128), (48, 512, 256)])
 def test_gemm_w4_skinny(native_ext, M, N, K, gs):
     """Decode-batch W4A16 (skinny.hip): split-K weight streaming, in-register dequant, vs fp32."""
     torch.manual_seed(2)
