@@ -426,15 +426,17 @@ def _serving_engine_from_args(a, tp=None, tpg=None, ppg=None):
     """Build the ServingEngine ``lipa serve`` describes (runs in the engine process by default)."""
     from ..infer.engine import ServingEngine
     from ..train.data import load_tokenizer
-    m = _load_for_inference(a.model, a.adapter, quant=a.quant, tp_group=tpg, pp_group=ppg)
-    tok = load_tokenizer(a.tokenizer or a.model)
-    loras = dict(spec.split("=", 1) for spec in a.lora_modules) if getattr(a, "lora_modules", None) else None
-    return ServingEngine(m, tok, model_name=a.served_model_name or os.path.basename(a.model.rstrip("/")),
-                         max_batch=a.max_batch, system_prompt=a.system, tp_group=tp,
-                         max_model_len=a.max_model_len,
-                         prefix_cache_blocks=a.prefix_blocks if a.prefix_caching else 0,
-                         chunked_prefill=a.max_batched_tokens if a.chunked_prefill else 0,
-                         lora_modules=loras, host_cache_blocks=getattr(a, "host_blocks", 0))
+    g = lambda k, d=None: getattr(a, k, d)      # noqa: E731  (namespaces built by other commands)
+    m = _load_for_inference(a.model, g("adapter"), quant=g("quant"), tp_group=tpg, pp_group=ppg)
+    tok = load_tokenizer(g("tokenizer") or a.model)
+    loras = dict(spec.split("=", 1) for spec in g("lora_modules")) if g("lora_modules") else None
+    return ServingEngine(m, tok, model_name=g("served_model_name") or os.path.basename(a.model.rstrip("/")),
+                         max_batch=g("max_batch", 32), system_prompt=g("system"), tp_group=tp,
+                         max_model_len=g("max_model_len"),
+                         prefix_cache_blocks=g("prefix_blocks", 1024) if g("prefix_caching") else 0,
+                         chunked_prefill=g("max_batched_tokens", 2048) if g("chunked_prefill") else 0,
+                         lora_modules=loras, host_cache_blocks=g("host_blocks", 0),
+                         kv_remote_url=g("kv_remote_url"))
 
 
 def cmd_serve(a):
@@ -476,6 +478,13 @@ def cmd_serve_deploy(a):
         uvicorn.run(create_serve_proxy(ctl), host=a.host, port=a.port)
     finally:
         ctl.shutdown()
+
+
+def cmd_kv_server(a):
+    """LMCache-server role: the remote prefix-KV chunk store shared by serving replicas."""
+    import uvicorn
+    from ..infer.kv_server import create_kv_server
+    uvicorn.run(create_kv_server(int(a.max_gib * (1 << 30))), host=a.host, port=a.port)
 
 
 def cmd_guard(a):
@@ -892,6 +901,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help="adapters selectable per request by `model` name")
     p.add_argument("--kv-host-cache-blocks", dest="host_blocks", type=int, default=0,
                    help="prefix-cache host tier (LMCache local-CPU role): 64-token chunks spilled to pinned RAM")
+    p.add_argument("--kv-remote-url", dest="kv_remote_url", default=None,
+                   help="shared remote KV-chunk store (LMCache server role; `lipa kv-server`)")
     p.add_argument("--no-engine-process", dest="engine_process", action="store_false",
                    help="run the engine core in the HTTP process (default: its own process)")
     _add_parallel_args(p)
@@ -904,6 +915,12 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--port", type=int, default=8000)
     p.add_argument("--control-interval", dest="control_interval", type=float, default=1.0)
     p.set_defaults(fn=cmd_serve_deploy)
+
+    p = sub.add_parser("kv-server", help="remote KV-chunk store shared by replicas (LMCache server role)")
+    p.add_argument("--host", default="0.0.0.0")
+    p.add_argument("--port", type=int, default=8100)
+    p.add_argument("--max-gib", dest="max_gib", type=float, default=64.0)
+    p.set_defaults(fn=cmd_kv_server)
 
     p = sub.add_parser("guard")
     p.add_argument("--backend", required=True, help="guard model completions URL")

@@ -97,11 +97,18 @@ class PrefixCache:
     it over PCIe into a free HBM block (its own LRU; the HBM pool holds the hot set, host memory
     — hundreds of GB on an MI355X node — the warm set).
 
+    Remote tier (LMCache server role, ``07-L1-Cache/LMCache/lmcache-deployment.yaml``): with a
+    :class:`~.kv_server.RemoteKV`, every newly computed chunk is written through to a store shared
+    by all replicas (write-behind, off the engine loop), and a chunk missing from HBM and host is
+    fetched from it before giving up — a prefix prefilled on one replica is warm on all of them.
+
     ``salt`` separates hash chains whose K/V differ for the same tokens (multi-LoRA adapters)."""
 
     def __init__(self, n_layers: int, width: int, dtype, device, block: int = 64, capacity_blocks: int = 512,
-                 host_blocks: int = 0):
+                 host_blocks: int = 0, remote=None):
         import collections
+        self.remote = remote
+        self.remote_hits = 0
         self.block, self.capacity = block, capacity_blocks
         self.k = [torch.zeros(capacity_blocks, block, width, dtype=dtype, device=device) for _ in range(n_layers)]
         self.v = [torch.zeros(capacity_blocks, block, width, dtype=dtype, device=device) for _ in range(n_layers)]
@@ -162,6 +169,50 @@ class PrefixCache:
         self.host_hits += 1
         return j
 
+    # ---- remote tier ---------------------------------------------------------------------
+    def _chunk_shape(self):
+        return (len(self.k), 2, self.block, self.k[0].shape[-1])
+
+    def _remote_fetch(self, d: bytes) -> int | None:
+        if self.remote is None:
+            return None
+        data = self.remote.get(d)
+        L, _, B, W = self._chunk_shape()
+        esz = self.k[0].element_size()
+        if data is None or len(data) != L * 2 * B * W * esz:
+            return None
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8).view(self.k[0].dtype).view(L, 2, B, W)
+        if self.k[0].is_cuda:
+            t = t.pin_memory()
+        j = self._alloc_hbm()
+        for l in range(L):
+            self.k[l][j].copy_(t[l, 0], non_blocking=True)
+            self.v[l][j].copy_(t[l, 1], non_blocking=True)
+        if self.k[0].is_cuda:
+            torch.cuda.current_stream().synchronize()     # the pinned staging buffer dies here
+        self.map[d] = j
+        self.remote_hits += 1
+        return j
+
+    def _remote_write(self, digests: list[bytes], dst: "torch.Tensor"):
+        """Write-through of freshly stored chunks: one D2H gather into pinned memory on the current
+        stream, bytes produced and uploaded on the client's writer thread after the copy lands."""
+        L = len(self.k)
+        stacked = torch.stack([torch.stack([self.k[l][dst], self.v[l][dst]]) for l in range(L)])   # [L,2,n,B,W]
+        if stacked.is_cuda:
+            host = torch.empty(stacked.shape, dtype=stacked.dtype, pin_memory=True)
+            host.copy_(stacked, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host, ev = stacked.clone(), None
+        for i, d in enumerate(digests):
+            def payload(i=i):
+                if ev is not None:
+                    ev.synchronize()
+                return host[:, :, i].contiguous().view(torch.uint8).numpy().tobytes()
+            self.remote.put(d, payload)
+
     def match(self, ids: list[int], salt: int = 0) -> list[int]:
         """Pool indices of the longest cached chunk run (leaving >= 1 token to prefill)."""
         n = (len(ids) - 1) // self.block
@@ -170,6 +221,8 @@ class PrefixCache:
             j = self.map.get(d)
             if j is None:
                 j = self._restore(d)
+                if j is None:
+                    j = self._remote_fetch(d)
                 if j is None:
                     break
             self.map.move_to_end(d)
@@ -189,7 +242,8 @@ class PrefixCache:
         """Insert every full prompt chunk of a freshly prefilled slot that is not cached yet."""
         n = len(ids) // self.block
         new = []
-        for i, d in enumerate(self._digests(ids, n, salt)):
+        digests = self._digests(ids, n, salt)
+        for i, d in enumerate(digests):
             if d in self.map:
                 self.map.move_to_end(d)
                 continue
@@ -204,6 +258,8 @@ class PrefixCache:
         for l in range(len(self.k)):
             self.k[l][dst] = cache.k[l][slot, :n * B].view(n, B, -1)[src]
             self.v[l][dst] = cache.v[l][slot, :n * B].view(n, B, -1)[src]
+        if self.remote is not None:
+            self._remote_write([digests[i] for i, _ in new], dst)
 
 
 @dataclasses.dataclass
@@ -264,7 +320,7 @@ class ServingEngine:
                  max_model_len: int | None = None, max_prefill_batch: int | None = None, prefill_token_budget: int = 16384,
                  use_graphs: bool | None = None, tp_group=None, prefix_cache_blocks: int = 0,
                  prefix_block: int = 64, chunked_prefill: int = 0, lora_modules: dict[str, str] | None = None,
-                 host_cache_blocks: int = 0):
+                 host_cache_blocks: int = 0, kv_remote_url: str | None = None):
         """``tp_group``: the model was sharded by ``parallel.tensor_parallel`` over this group.
         The engine then runs SPMD — group rank 0 owns the request queue and broadcasts each
         iteration's admissions; the other ranks call :meth:`follower_loop` and replay exactly the
@@ -321,10 +377,14 @@ class ServingEngine:
                              self.lm.lm_head.weight.dtype, self.device)
         self.cache.pos = torch.zeros(max_batch, dtype=torch.long, device=self.device)
         self.prefix = None
+        remote = None
+        if kv_remote_url and prefix_cache_blocks > 0:
+            from .kv_server import RemoteKV
+            remote = RemoteKV(kv_remote_url)
         if prefix_cache_blocks > 0:
             self.prefix = PrefixCache(cfg.num_hidden_layers, cfg.num_key_value_heads * cfg.head_dim,
                                       self.lm.lm_head.weight.dtype, self.device, prefix_block, prefix_cache_blocks,
-                                      host_blocks=host_cache_blocks)
+                                      host_blocks=host_cache_blocks, remote=remote)
         # multi-LoRA serving (vLLM --enable-lora --lora-modules): stacked adapters, per-row masks;
         # built BEFORE the decode graphs are captured so the adapter term is part of every graph
         self.mlora = None
@@ -822,7 +882,9 @@ class ServingEngine:
                       "# TYPE lipa_prefix_cache_host_hits_total counter",
                       f"lipa_prefix_cache_host_hits_total {self.prefix.host_hits}",
                       "# TYPE lipa_prefix_cache_spills_total counter",
-                      f"lipa_prefix_cache_spills_total {self.prefix.spills}"]
+                      f"lipa_prefix_cache_spills_total {self.prefix.spills}",
+                      "# TYPE lipa_prefix_cache_remote_hits_total counter",
+                      f"lipa_prefix_cache_remote_hits_total {self.prefix.remote_hits}"]
         lines += self.h_latency.render("lipa_e2e_request_latency_seconds")
         lines += self.h_ttft.render("lipa_time_to_first_token_seconds")
         if torch.cuda.is_available():

@@ -159,6 +159,12 @@ def prompt_prefix_hashes(body: dict, chunk: int = PREFIX_CHUNK) -> list[str]:
     return out
 
 
+def resolve_service(host: str, port: int) -> list[str]:
+    """IPv4 addresses behind a DNS name (a headless Service resolves to its ready pods)."""
+    import socket
+    return sorted({ai[4][0] for ai in socket.getaddrinfo(host, port, socket.AF_INET, socket.SOCK_STREAM)})
+
+
 def load_config(cfg: dict | str) -> dict:
     if isinstance(cfg, str):
         import yaml
@@ -191,7 +197,8 @@ def http_sender(timeout: float = 600.0) -> Callable[[Deployment, str, dict], dic
 
 class Router:
     def __init__(self, cfg: dict | str, send: Callable[[Deployment, str, dict], dict] | None = None,
-                 clock: Callable[[], float] = time.time, seed: int | None = None):
+                 clock: Callable[[], float] = time.time, seed: int | None = None,
+                 resolver: Callable[[str, int], list[str]] | None = None):
         cfg = load_config(cfg)
         rs = cfg.get("router_settings", {}) or {}
         self.strategy = rs.get("routing_strategy", "simple-shuffle")
@@ -233,6 +240,42 @@ class Router:
         self.prefix_capacity = int(rs.get("prefix_table_size", 100_000))
         self.scraper: Callable[[Deployment], dict] | None = None
         self._last_scrape = -1e18
+        # Kubernetes discovery (the llm-d / vLLM-router RBAC pod watch role): the A records of a
+        # headless Service are the replica pods; re-resolved every `interval` seconds
+        self.discovery = [dict(d) for d in (rs.get("discovery") or [])]
+        self.resolver: Callable[[str, int], list[str]] = resolver or resolve_service
+        self._last_discovery = -1e18
+        if self.discovery:
+            self.refresh_discovery(force=True)
+
+    def refresh_discovery(self, force: bool = False):
+        """Sync each discovered group's deployments with the pod IPs behind its Service name:
+        new pods join (fresh stats), vanished pods leave; existing deployments keep their state."""
+        if not self.discovery:
+            return
+        now = self.clock()
+        interval = min(float(d.get("interval", 10)) for d in self.discovery)
+        if not force and now - self._last_discovery < interval:
+            return
+        self._last_discovery = now
+        for spec in self.discovery:
+            group, port = spec["model_name"], int(spec.get("port", 8000))
+            try:
+                ips = self.resolver(spec["service"], port)
+            except OSError:
+                continue                          # DNS hiccup: keep the last known set
+            scheme = spec.get("scheme", "http")
+            want = {f"{scheme}://{ip}:{port}/v1" for ip in ips}
+            with self.lock:
+                cur = self.groups.get(group, [])
+                keep = [d for d in cur if d.api_base in want]
+                have = {d.api_base for d in keep}
+                for base in sorted(want - have):
+                    keep.append(Deployment(group=group, model=spec.get("model", group), api_base=base,
+                                           api_key=spec.get("api_key"),
+                                           max_parallel=spec.get("max_parallel_requests")))
+                self.groups[group] = keep
+                self.counters["discovery_refreshes"] += 1
 
     @staticmethod
     def _fallback_map(spec) -> dict[str, list[str]]:
@@ -310,6 +353,7 @@ class Router:
         return self.rng.choice([d for d in cands if d.in_flight == least])
 
     def pick(self, group: str, exclude: set[str] = frozenset(), body: dict | None = None) -> Deployment | None:
+        self.refresh_discovery()
         if self.strategy in ("load_aware_prefix", "prefixaware", "cache_aware"):
             self.refresh_stats()
         with self.lock:

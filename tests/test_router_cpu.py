@@ -241,3 +241,33 @@ def test_app_serves_requests_concurrently():
             return _t.time() - t0
     dt = asyncio.run(go())
     assert peak[0] == 2 and dt < 0.55
+
+
+def test_kubernetes_headless_service_discovery():
+    """router_settings.discovery: the pod IPs behind a headless Service become the group's
+    deployments, re-resolved on an interval (pods joining / leaving)."""
+    from llm_in_practise_amd.infer.router import Router, resolve_service
+    assert resolve_service("localhost", 8000) == ["127.0.0.1"]
+    t = [0.0]
+    ips = [["10.0.0.1", "10.0.0.2"]]
+    sent = []
+
+    def send(dep, path, body):
+        sent.append(dep.api_base)
+        return {"choices": [{"text": "x"}]}
+
+    cfg = {"model_list": [], "router_settings": {"routing_strategy": "least-busy", "discovery": [
+        {"model_name": "qwen3-8b", "service": "lipa-headless.llm-inference.svc", "port": 8000, "interval": 10}]}}
+    r = Router(cfg, send=send, clock=lambda: t[0], seed=0, resolver=lambda host, port: list(ips[0]))
+    assert sorted(d.api_base for d in r.groups["qwen3-8b"]) == ["http://10.0.0.1:8000/v1", "http://10.0.0.2:8000/v1"]
+    r.route("/completions", {"model": "qwen3-8b", "prompt": "hi"})
+    first = r.groups["qwen3-8b"]
+    ips[0] = ["10.0.0.2", "10.0.0.3"]
+    t[0] = 5.0                               # inside the interval: no re-resolve
+    r.route("/completions", {"model": "qwen3-8b", "prompt": "hi"})
+    assert len(r.groups["qwen3-8b"]) == 2 and r.groups["qwen3-8b"][0].api_base == first[0].api_base
+    t[0] = 11.0
+    r.route("/completions", {"model": "qwen3-8b", "prompt": "hi"})
+    bases = sorted(d.api_base for d in r.groups["qwen3-8b"])
+    assert bases == ["http://10.0.0.2:8000/v1", "http://10.0.0.3:8000/v1"]
+    assert sent[-1] in bases

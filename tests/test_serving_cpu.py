@@ -321,3 +321,50 @@ def test_engine_process_frontend_matches_inprocess(engine):
         assert c.get("/v1/models").json()["data"][0]["id"] == "tiny"
     finally:
         client.shutdown()
+
+
+def test_remote_kv_tier_shares_prefix_chunks_across_replicas():
+    """LMCache-server role: replica A writes its computed chunks through to the shared store;
+    replica B (cold HBM and host) fetches them instead of recomputing — identical K/V rows."""
+    import socket
+    import threading
+    import time
+
+    import uvicorn
+
+    from llm_in_practise_amd.infer.engine import PrefixCache
+    from llm_in_practise_amd.infer.kv_server import RemoteKV, create_kv_server
+    from llm_in_practise_amd.models.common import KVCache
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    srv = uvicorn.Server(uvicorn.Config(create_kv_server(1 << 26), host="127.0.0.1", port=port, log_level="error"))
+    threading.Thread(target=srv.run, daemon=True).start()
+    while not srv.started:
+        time.sleep(0.02)
+    try:
+        L, W, B = 3, 16, 8
+        ra, rb = RemoteKV(f"http://127.0.0.1:{port}"), RemoteKV(f"http://127.0.0.1:{port}")
+        a = PrefixCache(L, W, torch.float32, "cpu", block=B, capacity_blocks=8, remote=ra)
+        b = PrefixCache(L, W, torch.float32, "cpu", block=B, capacity_blocks=8, remote=rb)
+        cache_a = KVCache(L, 2, 64, 2, 8, torch.float32, "cpu")
+        for l in range(L):
+            cache_a.k[l].normal_()
+            cache_a.v[l].normal_()
+        ids = list(range(100, 133))                     # 4 full chunks + 1 token
+        a.store(ids, cache_a, slot=0)
+        ra.flush()
+        idx = b.match(ids)                              # cold B: all 4 chunks from the remote store
+        assert len(idx) == 4 and b.remote_hits == 4 and rb.stats["hits"] == 4
+        cache_b = KVCache(L, 2, 64, 2, 8, torch.float32, "cpu")
+        b.load(idx, cache_b, slot=1)
+        for l in range(L):
+            assert torch.equal(cache_b.k[l][1, :32], cache_a.k[l][0, :32])
+            assert torch.equal(cache_b.v[l][1, :32], cache_a.v[l][0, :32])
+        assert b.match(ids) == idx and b.remote_hits == 4      # now served from B's own HBM pool
+        assert b.match(list(range(7, 40))) == [] and rb.stats["misses"] >= 1
+        ra.close()
+        rb.close()
+    finally:
+        srv.should_exit = True
