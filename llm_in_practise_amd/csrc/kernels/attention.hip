@@ -79,8 +79,8 @@ __device__ __forceinline__ void xcd_grid3(int& i0, int& i1, int& i2) {
 // q_offs[b] + i (0 without q_offs): chunked / prefix-cache suffix prefill is the same kernel with
 // the causal limit key ≤ q_off + i.  kv_lens[b] (optional) masks keys ≥ kv_lens[b] (right padding,
 // BERT key-padding masks, the filled part of a cache).
-template <int D>
-__global__ __launch_bounds__(256) void attn_fwd_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
+template <int D, int PF, int QT>
+__global__ __launch_bounds__(256, 2) void attn_fwd_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                   const bf16* __restrict__ V, int ldq, int ldk, int ldv,
                                                   const int* __restrict__ kv_lens, const int* __restrict__ q_offs,
                                                   bf16* __restrict__ O, float* __restrict__ lse, int Sq, int Skv,
@@ -94,22 +94,23 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16* __restrict__ Q, co
   constexpr int LOADS = 64 * CH / 256;
   __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // K0 V0 K1 V1
 
-  const int nqb = (Sq + 127) / 128;
+  constexpr int QB = 64 * QT;       // queries per workgroup (QT 16-query subtiles per wave)
+  const int nqb = (Sq + QB - 1) / QB;
   int i0, h, b;
   xcd_grid3(i0, h, b);
   const int qb = nqb - 1 - i0;  // heavy (late, causal) blocks first
   const int hk = h / (hq / hkv);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
-  const int q0 = qb * 128 + 32 * w;
+  const int q0 = qb * QB + 16 * QT * w;
   const int qoff = q_offs ? q_offs[b] : 0;
   const int kvlen = min(kv_lens ? kv_lens[b] : Skv, Skv);
   const size_t tok0 = (size_t)b * Sq;          // query / output rows
   const size_t ktok0 = (size_t)b * kv_rows;     // key / value rows
 
   // Q fragments (B operand of Sᵀ = K·Qᵀ): Q[q0 + 16qt + li][32s + 8g + j]
-  bf16x8 qf[2][NS];
+  bf16x8 qf[QT][NS];
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
+  for (int qt = 0; qt < QT; ++qt) {
     int q = q0 + 16 * qt + li;
     q = q < Sq ? q : Sq - 1;
 #pragma unroll
@@ -117,64 +118,80 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16* __restrict__ Q, co
       qf[qt][s] = *reinterpret_cast<const bf16x8*>(Q + (tok0 + q) * ldq + h * D + 32 * s + 8 * g);
   }
 
-  int kend = causal ? min(Skv, qoff + qb * 128 + 128) : Skv;
+  int kend = causal ? min(Skv, qoff + qb * QB + QB) : Skv;
   kend = min(kend, kvlen);
   const int nt = (kend + 63) / 64;
 
-  f32x4 acc[ND][2];
+  f32x4 acc[ND][QT];
+  float m_run[QT], l_run[QT];
 #pragma unroll
-  for (int dt = 0; dt < ND; ++dt) acc[dt][0] = acc[dt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+  for (int qt = 0; qt < QT; ++qt) {
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) acc[dt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    m_run[qt] = -INFINITY;
+    l_run[qt] = 0.f;
+  }
 
-  bf16x8 kr[LOADS], vr[LOADS];
-  auto load_tile = [&](int t) {
+  // K/V tiles are register-staged PF tiles ahead (PF register sets, the loop unrolled by 2 so
+  // each set is static): with PF = 2 a tile's global loads get two tile-computations of latency
+  // budget before their LDS store.
+  bf16x8 kr[PF][LOADS], vr[PF][LOADS];
+  auto load_tile = [&](int set, int t) {
 #pragma unroll
     for (int p = 0; p < LOADS; ++p) {
       const int ci = p * 256 + threadIdx.x;
       const int row = ci / CH, ch = ci % CH;
       int key = t * 64 + row;
       key = key < Skv ? key : Skv - 1;
-      kr[p] = *reinterpret_cast<const bf16x8*>(K + (ktok0 + key) * ldk + hk * D + ch * 8);
-      vr[p] = *reinterpret_cast<const bf16x8*>(V + (ktok0 + key) * ldv + hk * D + ch * 8);
+      kr[set][p] = *reinterpret_cast<const bf16x8*>(K + (ktok0 + key) * ldk + hk * D + ch * 8);
+      vr[set][p] = *reinterpret_cast<const bf16x8*>(V + (ktok0 + key) * ldv + hk * D + ch * 8);
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int set, int buf) {
     bf16* Kl = smem + buf * 2 * TILE;
     bf16* Vl = Kl + TILE;
 #pragma unroll
     for (int p = 0; p < LOADS; ++p) {
       const int ci = p * 256 + threadIdx.x;
       const int row = ci / CH, ch = ci % CH;
-      *reinterpret_cast<bf16x8*>(Kl + row * LDR + ch * 8) = kr[p];
-      *reinterpret_cast<bf16x8*>(Vl + row * LDR + ch * 8) = vr[p];
+      *reinterpret_cast<bf16x8*>(Kl + row * LDR + ch * 8) = kr[set][p];
+      *reinterpret_cast<bf16x8*>(Vl + row * LDR + ch * 8) = vr[set][p];
     }
   };
 
-  if (nt > 0) load_tile(0);
-  for (int t = 0; t < nt; ++t) {
-    store_tile(t & 1);
+  if (nt > 0) load_tile(0, 0);
+  if (PF == 2 && nt > 1) load_tile(PF - 1, 1);
+  for (int t2 = 0; t2 < nt; t2 += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+    const int t = t2 + u;
+    if (t >= nt) break;
+    const int set = PF == 2 ? u : 0;
+    store_tile(set, u);
     __syncthreads();
-    if (t + 1 < nt) load_tile(t + 1);
-    const bf16* Kl = smem + (t & 1) * 2 * TILE;
+    if (t + PF < nt) load_tile(set, t + PF);
+    const bf16* Kl = smem + u * 2 * TILE;
     const bf16* Vl = Kl + TILE;
     const int k0 = t * 64;
     // ---- Sᵀ[key][q] for 4 key-subtiles × 2 query-subtiles
-    f32x4 sc[4][2];
+    f32x4 sc[4][QT];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
-      sc[kt][0] = sc[kt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) sc[kt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kl + (16 * kt + li) * LDR + 32 * s + 8 * g);
-        sc[kt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][s], sc[kt][0], 0, 0, 0);
-        sc[kt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][s], sc[kt][1], 0, 0, 0);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+          sc[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][s], sc[kt][qt], 0, 0, 0);
       }
     }
     // ---- masks + online softmax (lane owns query q0 + 16qt + li; keys k0 + 16kt + 4g + r)
     const bool need_mask = (causal && k0 + 63 > qoff + q0) || (k0 + 64 > kvlen);
-    bf16x8 pf[2][2];
+    bf16x8 pf[QT][2];
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
+    for (int qt = 0; qt < QT; ++qt) {
       const int qa = q0 + 16 * qt + li;
       const int klim = min(causal ? qoff + qa : Skv, kvlen - 1);  // last key this query may see
 #pragma unroll
@@ -233,14 +250,16 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16* __restrict__ Q, co
         // lane 4q'+p' of each 16-group addresses row r0+q', cols 16dt+4p'..+3
         const bf16* p0 = Vl + (32 * kb + 4 * g + (li >> 2)) * LDR + 16 * dt + 4 * (li & 3);
         const bf16x8 vf = cat8(tr_read(p0), tr_read(p0 + 16 * LDR));
-        acc[dt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[0][kb], acc[dt][0], 0, 0, 0);
-        acc[dt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[1][kb], acc[dt][1], 0, 0, 0);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+          acc[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt][kb], acc[dt][qt], 0, 0, 0);
       }
+    }
     }
   }
   // ---- epilogue: O[q][16dt + 4g + r] = acc / l ; lse = (m + log2 l) * ln2
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
+  for (int qt = 0; qt < QT; ++qt) {
     const int q = q0 + 16 * qt + li;
     if (q >= Sq) continue;
     const float inv = l_run[qt] > 0.f ? 1.f / l_run[qt] : 0.f;
@@ -267,8 +286,8 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const bf16* __restrict__ Q, co
 //    registers) that sweeps every q-head of its GQA group × 64-query tiles, so the group's
 //    dK/dV sum stays in registers: no fp32 partials, no finalize pass.  Q/dO tiles (plus
 //    their lse/delta) are register-prefetched one tile ahead into double-buffered LDS.
-template <int D>
-__global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16* __restrict__ dO, const bf16* __restrict__ O,
+template <int D, int PF>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(const bf16* __restrict__ dO, const bf16* __restrict__ O,
                                                      const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ V, const float* __restrict__ lse,
                                                      float* __restrict__ delta, const int* __restrict__ kv_lens,
@@ -318,35 +337,41 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16* __restrict__ dO
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 kr[LOADS], vr[LOADS];
-  auto load_tile = [&](int t) {
+  bf16x8 kr[PF][LOADS], vr[PF][LOADS];   // two tiles ahead, as the forward
+  auto load_tile = [&](int set, int t) {
 #pragma unroll
     for (int p = 0; p < LOADS; ++p) {
       const int ci = p * 256 + threadIdx.x;
       const int row = ci / CH, ch = ci % CH;
       const size_t key = tok0 + min(t * 64 + row, S - 1);
-      kr[p] = *reinterpret_cast<const bf16x8*>(K + key * ldk + hk * D + ch * 8);
-      vr[p] = *reinterpret_cast<const bf16x8*>(V + key * ldv + hk * D + ch * 8);
+      kr[set][p] = *reinterpret_cast<const bf16x8*>(K + key * ldk + hk * D + ch * 8);
+      vr[set][p] = *reinterpret_cast<const bf16x8*>(V + key * ldv + hk * D + ch * 8);
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int set, int buf) {
     bf16* Kl = smem + buf * 2 * TILE;
     bf16* Vl = Kl + TILE;
 #pragma unroll
     for (int p = 0; p < LOADS; ++p) {
       const int ci = p * 256 + threadIdx.x;
       const int row = ci / CH, ch = ci % CH;
-      *reinterpret_cast<bf16x8*>(Kl + row * LDR + ch * 8) = kr[p];
-      *reinterpret_cast<bf16x8*>(Vl + row * LDR + ch * 8) = vr[p];
+      *reinterpret_cast<bf16x8*>(Kl + row * LDR + ch * 8) = kr[set][p];
+      *reinterpret_cast<bf16x8*>(Vl + row * LDR + ch * 8) = vr[set][p];
     }
   };
 
-  if (nt > 0) load_tile(0);
-  for (int t = 0; t < nt; ++t) {
-    store_tile(t & 1);
+  if (nt > 0) load_tile(0, 0);
+  if (PF == 2 && nt > 1) load_tile(PF - 1, 1);
+  for (int t2 = 0; t2 < nt; t2 += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+    const int t = t2 + u;
+    if (t >= nt) break;
+    const int set = PF == 2 ? u : 0;
+    store_tile(set, u);
     __syncthreads();
-    if (t + 1 < nt) load_tile(t + 1);
-    const bf16* Kl = smem + (t & 1) * 2 * TILE;
+    if (t + PF < nt) load_tile(set, t + PF);
+    const bf16* Kl = smem + u * 2 * TILE;
     const bf16* Vl = Kl + TILE;
     const int k0 = t * 64;
     // ---- Sᵀ[key][q], dPᵀ[key][q] for 4 key-subtiles (lane: query li, keys 16kt + 4g + r)
@@ -397,6 +422,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16* __restrict__ dO
         acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ktf, dsf, acc[dt], 0, 0, 0);
       }
     }
+    }
   }
   // ---- dQ[q][16dt + 4g + r] = scale · acc
   if (qa >= S) return;
@@ -411,7 +437,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_k(const bf16* __restrict__ dO
 
 // HALVES = 2: a 512-thread workgroup, the two 4-wave halves sweep different q-heads of the GQA
 // group over the SAME 64 keys (2 waves per SIMD instead of 1) and meet in LDS at the end.
-template <int D, int HALVES>
+template <int D, int HALVES, int PF>
 __global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __restrict__ dO, const bf16* __restrict__ Q,
                                                       const bf16* __restrict__ K, const bf16* __restrict__ V,
                                                       const float* __restrict__ lse, const float* __restrict__ delta,
@@ -454,9 +480,9 @@ __global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __res
   const int nqt = (S + 63) / 64 - qt0;
   const int n_it = kb0 < kvlen ? hp * nqt : 0;  // keys past kv_len get zero gradient
 
-  bf16x8 qr[LOADS], dr[LOADS];
-  float st = 0.f;
-  auto load_it = [&](int it) {
+  bf16x8 qr[PF][LOADS], dr[PF][LOADS];   // PF query tiles ahead, as the forward
+  float st[PF];
+  auto load_it = [&](int set, int it) {
     const int h = hk * rep + hw * hp + it / nqt;
     const int qa0 = (qt0 + it % nqt) * 64;
 #pragma unroll
@@ -464,36 +490,42 @@ __global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __res
       const int ci = p * 256 + tid;
       const int row = ci / CH, ch = ci % CH;
       const size_t tq = tok0 + min(qa0 + row, S - 1);
-      qr[p] = *reinterpret_cast<const bf16x8*>(Q + tq * ldq + h * D + ch * 8);
-      dr[p] = *reinterpret_cast<const bf16x8*>(dO + tq * ldo + h * D + ch * 8);
+      qr[set][p] = *reinterpret_cast<const bf16x8*>(Q + tq * ldq + h * D + ch * 8);
+      dr[set][p] = *reinterpret_cast<const bf16x8*>(dO + tq * ldo + h * D + ch * 8);
     }
     if (tid < 128) {
       const size_t bh = ((size_t)b * hq + h) * S + min(qa0 + (tid & 63), S - 1);
-      st = tid < 64 ? lse[bh] * LOG2E : delta[bh];
+      st[set] = tid < 64 ? lse[bh] * LOG2E : delta[bh];
     }
   };
-  auto store_it = [&](int buf) {
+  auto store_it = [&](int set, int buf) {
     bf16* Ql = smem + buf * 2 * TILE;
     bf16* dOl = Ql + TILE;
 #pragma unroll
     for (int p = 0; p < LOADS; ++p) {
       const int ci = p * 256 + tid;
       const int row = ci / CH, ch = ci % CH;
-      *reinterpret_cast<bf16x8*>(Ql + row * LDR + ch * 8) = qr[p];
-      *reinterpret_cast<bf16x8*>(dOl + row * LDR + ch * 8) = dr[p];
+      *reinterpret_cast<bf16x8*>(Ql + row * LDR + ch * 8) = qr[set][p];
+      *reinterpret_cast<bf16x8*>(dOl + row * LDR + ch * 8) = dr[set][p];
     }
-    if (tid < 128) stat[buf][tid >> 6][tid & 63] = st;
+    if (tid < 128) stat[buf][tid >> 6][tid & 63] = st[set];
   };
 
-  if (n_it > 0) load_it(0);
-  for (int it = 0; it < n_it; ++it) {
-    store_it(it & 1);
+  if (n_it > 0) load_it(0, 0);
+  if (PF == 2 && n_it > 1) load_it(PF - 1, 1);
+  for (int i2 = 0; i2 < n_it; i2 += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+    const int it = i2 + u;
+    if (it >= n_it) break;
+    const int set = PF == 2 ? u : 0;
+    store_it(set, u);
     __syncthreads();
-    if (it + 1 < n_it) load_it(it + 1);
-    const bf16* Ql = smem + (it & 1) * 2 * TILE;
+    if (it + PF < n_it) load_it(set, it + PF);
+    const bf16* Ql = smem + u * 2 * TILE;
     const bf16* dOl = Ql + TILE;
-    const float* Ls = stat[it & 1][0];
-    const float* Dls = stat[it & 1][1];
+    const float* Ls = stat[u][0];
+    const float* Dls = stat[u][1];
     const int qa0 = (qt0 + it % nqt) * 64;
     // ---- S[q][key], dP[q][key]: rows q = 16qt + 4g + r, col key = kw
     f32x4 sp[4], dp[4];
@@ -549,6 +581,7 @@ __global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __res
         dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qfr, dsf, dk[dt], 0, 0, 0);
       }
     }
+    }
   }
   if constexpr (HALVES == 2) {  // half 1 hands its partial sums to half 0 through LDS
     __syncthreads();
@@ -603,15 +636,34 @@ static DropParams make_drop(float p, uint64_t seed) {
     default: { constexpr int DD = 128; __VA_ARGS__; } break;  \
   }
 
+// register prefetch depth per kernel (measured, profiles/attention_fwd_bwd.txt): fwd 1 (2 waves per
+// SIMD at 244 VGPRs; depth 2 spills), dQ 2 (236 VGPRs), dK/dV 1; LIPA_ATTN_PF=1|2 forces all
+static int attn_pf(int dflt) {
+  static const int pf = [] { const char* e = getenv("LIPA_ATTN_PF"); return e ? atoi(e) : 0; }();
+  return pf == 1 || pf == 2 ? pf : dflt;
+}
+
 void launch_attn_fwd(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv, const int* kv_lens,
                      const int* q_offs, void* o, float* lse, int B, int Sq, int Skv, int kv_rows, int hq, int hkv,
                      int D, int causal, float scale, float p_drop, uint64_t seed, hipStream_t st) {
   const DropParams dp = make_drop(p_drop, seed);
-  dim3 grid((Sq + 127) / 128, hq, B), blk(256);
+  // 128-query workgroups (32 queries per wave, QT = 2) reuse each K/V tile for twice the queries;
+  // 64-query ones (QT = 1) give the causal grid more, smaller blocks to balance — measured slower at
+  // S = 512 / 8192 and equal at 2048 (profiles/attention_fwd_bwd.txt).  LIPA_ATTN_QT=1|2 forces one.
+  static const int qt_env = [] { const char* e = getenv("LIPA_ATTN_QT"); return e ? atoi(e) : 0; }();
+  const int qt = qt_env == 1 || qt_env == 2 ? qt_env : 2;
+  dim3 grid((Sq + 64 * qt - 1) / (64 * qt), hq, B), blk(256);
   const float sl2 = scale * LOG2E;
-  LIPA_ATTN_D(D, attn_fwd_k<DD><<<grid, blk, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, ldq, ldk,
-                                                      ldv, kv_lens, q_offs, (bf16*)o, lse, Sq, Skv, kv_rows, hq,
-                                                      hkv, causal, sl2, dp));
+#define FWD(PFV, QTV)                                                                                      \
+  LIPA_ATTN_D(D, attn_fwd_k<DD, PFV, QTV><<<grid, blk, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,  \
+                                                           ldq, ldk, ldv, kv_lens, q_offs, (bf16*)o, lse, Sq, Skv, \
+                                                           kv_rows, hq, hkv, causal, sl2, dp))
+  if (qt == 1) {
+    FWD(1, 1);
+  } else {
+    FWD(1, 2);
+  }
+#undef FWD
   LIPA_CHECK_LAUNCH();
 }
 
@@ -623,19 +675,26 @@ void launch_attn_bwd(const void* dout, const void* q, const void* k, const void*
   const DropParams dp = make_drop(p_drop, seed);
   const int nb = (S + 63) / 64;
   dim3 gq(nb, hq, B), gkv(nb, hkv, B), blk(256);
-#define RUN(DD)                                                                                                    \
-  attn_bwd_dq_k<DD><<<gq, blk, 0, st>>>((const bf16*)dout, (const bf16*)o, (const bf16*)q, (const bf16*)k,         \
-                                        (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dq, S, hq, hkv,  \
-                                        causal, scale, sl2, dp);                                                    \
+#define RUN(DD, PFQ, PFKV)                                                                                        \
+  attn_bwd_dq_k<DD, PFQ><<<gq, blk, 0, st>>>((const bf16*)dout, (const bf16*)o, (const bf16*)q, (const bf16*)k,    \
+                                             (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dq, S, hq,  \
+                                             hkv, causal, scale, sl2, dp);                                          \
   if ((hq / hkv) % 2 == 0)                                                                                       \
-    attn_bwd_dkv_k<DD, 2><<<gkv, 512, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k, (const bf16*)v,   \
-                                               lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, (bf16*)dv, S, hq, hkv, \
-                                               causal, scale, sl2, dp);                                              \
-  else                                                                                                             \
-    attn_bwd_dkv_k<DD, 1><<<gkv, 256, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k, (const bf16*)v,   \
-                                               lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, (bf16*)dv, S, hq, hkv, \
-                                               causal, scale, sl2, dp)
-  LIPA_ATTN_D(D, RUN(DD));
+    attn_bwd_dkv_k<DD, 2, PFKV><<<gkv, 512, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k,            \
+                                                     (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, \
+                                                     (bf16*)dv, S, hq, hkv, causal, scale, sl2, dp);               \
+  else                                                                                                           \
+    attn_bwd_dkv_k<DD, 1, PFKV><<<gkv, 256, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k,            \
+                                                     (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, \
+                                                     (bf16*)dv, S, hq, hkv, causal, scale, sl2, dp)
+  const int pfq = attn_pf(2), pfkv = attn_pf(1);
+  if (pfq == 2 && pfkv == 1) {
+    LIPA_ATTN_D(D, RUN(DD, 2, 1));
+  } else if (pfq == 1) {
+    LIPA_ATTN_D(D, RUN(DD, 1, 1));
+  } else {
+    LIPA_ATTN_D(D, RUN(DD, 2, 2));
+  }
 #undef RUN
   LIPA_CHECK_LAUNCH();
 }
