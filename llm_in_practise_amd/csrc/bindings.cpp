@@ -71,6 +71,11 @@ void launch_moe_gather(int, const void*, const int*, const float*, void*, int, i
 void launch_moe_combine(int, const void*, const int*, const float*, const void*, void*, int, int, int, hipStream_t);
 void launch_moe_wgrad(int, const void*, const void*, const int*, float*, int, int, int, hipStream_t);
 int lora_acc_chunks(int M, int K);
+void launch_lora_proj2(const void*, int, const void*, const void*, int, int, int, float*, int, void*, int, int, uint64_t, float, float,
+                       uint64_t, float, float, size_t, hipStream_t);
+void launch_lora_acc2(const float*, int, int, const float*, int, int, const void*, int, void*, int, const void*,
+                      const void*, int, float*, float*, int64_t, int64_t, int64_t, int64_t, int, uint64_t, float,
+                      uint64_t, float, size_t, hipStream_t);
 void launch_lora_acc(const float*, int, int, const void*, int, void*, int, const void*, int, float*, int64_t, int64_t,
                      float*, int, uint64_t, float, size_t, hipStream_t);
 void launch_decode_attention(const void*, const void*, const void*, const int*, float*, float*, float*, void*, int, int,
@@ -679,6 +684,59 @@ Tensor lora_proj(Tensor x, int64_t c0, int64_t K, Tensor w, optional<Tensor> out
 }
 
 // out (fp32, 2-D, [r, K] or its transpose view [K, r]) += gᵀ·D(x[:, c0:c0+K]); with dx: dx += D(g·w)
+// two LoRA branches sharing x (q_proj + v_proj): A0 [r0, K], A1 [r1, K] bf16, r0 + r1 <= 16
+Tensor lora_proj2(Tensor x, Tensor a0, Tensor a1, optional<Tensor> outb, bool want_f32, double p0, int64_t key0,
+                  double scale0, double p1, int64_t key1, double scale1) {
+  CHECK_BF16(x);
+  CHECK_BF16(a0);
+  CHECK_BF16(a1);
+  const int64_t K = x.size(1);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "lora_proj2: x layout");
+  TORCH_CHECK(a0.is_contiguous() && a1.is_contiguous() && a0.size(1) == K && a1.size(1) == K &&
+                  a0.size(0) + a1.size(0) <= 16 && K % 32 == 0, "lora_proj2: A_i [r_i, K], r0 + r1 <= 16");
+  const int M = x.size(0), r0 = a0.size(0), r = r0 + a1.size(0);
+  Tensor of;
+  if (want_f32) of = at::empty({M, r}, x.options().dtype(at::kFloat));
+  void* ob = nullptr;
+  int ldob = 0;
+  if (outb) {
+    TORCH_CHECK(outb->scalar_type() == at::kBFloat16 && outb->stride(1) == 1 && outb->size(0) == M &&
+                    outb->size(1) == r, "lora_proj2: outb");
+    ob = outb->data_ptr();
+    ldob = outb->stride(0);
+  }
+  TORCH_CHECK(ob || want_f32, "lora_proj2: no output");
+  launch_lora_proj2(x.data_ptr(), x.stride(0), a0.data_ptr(), a1.data_ptr(), r0, r, K, want_f32 ? of.data_ptr<float>() : nullptr, r,
+                    ob, ldob, M, (uint64_t)key0, (float)p0, (float)scale0, (uint64_t)key1, (float)p1, (float)scale1,
+                    (size_t)x.stride(0), stream());
+  return want_f32 ? of : Tensor();
+}
+
+// dA_i [r_i, K] += G_iᵀ·D_i(x), dx += Σ_i D_i(G_i·A_i) for two branches in one pass (r_i <= 8)
+void lora_acc2(Tensor g0, Tensor g1, Tensor x, Tensor dx, Tensor a0, Tensor a1, Tensor out0, Tensor out1, double p0,
+               int64_t key0, double p1, int64_t key1) {
+  for (const Tensor* g : {&g0, &g1})
+    TORCH_CHECK(g->scalar_type() == at::kFloat && g->dim() == 2 && g->stride(1) == 1 && g->size(1) <= 8 &&
+                    g->stride(0) % 4 == 0 && g->stride(0) >= 8 && reinterpret_cast<uintptr_t>(g->data_ptr()) % 16 == 0,
+                "lora_acc2: g fp32 [M, r<=8], row stride >= 8, 16-B aligned rows");
+  CHECK_BF16(x);
+  CHECK_BF16(dx);
+  const int M = x.size(0), K = x.size(1), r0 = g0.size(1), r1 = g1.size(1);
+  TORCH_CHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && K % 128 == 0 && g0.size(0) == M && g1.size(0) == M,
+              "lora_acc2: x layout");
+  TORCH_CHECK(dx.stride(1) == 1 && dx.size(0) == M && dx.size(1) == K, "lora_acc2: dx");
+  TORCH_CHECK(a0.is_contiguous() && a0.size(0) == r0 && a0.size(1) == K && a1.is_contiguous() && a1.size(0) == r1 &&
+                  a1.size(1) == K && a0.scalar_type() == at::kBFloat16 && a1.scalar_type() == at::kBFloat16,
+              "lora_acc2: A [r, K] bf16");
+  TORCH_CHECK(out0.scalar_type() == at::kFloat && out0.size(0) == r0 && out0.size(1) == K &&
+                  out1.scalar_type() == at::kFloat && out1.size(0) == r1 && out1.size(1) == K,
+              "lora_acc2: out [r, K] fp32");
+  launch_lora_acc2(g0.data_ptr<float>(), g0.stride(0), r0, g1.data_ptr<float>(), g1.stride(0), r1, x.data_ptr(),
+                   x.stride(0), dx.data_ptr(), dx.stride(0), a0.data_ptr(), a1.data_ptr(), K, out0.data_ptr<float>(),
+                   out1.data_ptr<float>(), out0.stride(0), out0.stride(1), out1.stride(0), out1.stride(1), M,
+                   (uint64_t)key0, (float)p0, (uint64_t)key1, (float)p1, (size_t)x.stride(0), stream());
+}
+
 void lora_acc(Tensor g, Tensor x, int64_t c0, int64_t K, Tensor out, bool out_transposed, optional<Tensor> dx,
               optional<Tensor> w, double p, int64_t key, bool deterministic) {
   TORCH_CHECK(g.scalar_type() == at::kFloat && g.dim() == 2 && g.stride(1) == 1 && g.size(1) <= 16, "lora_acc: g");
@@ -949,6 +1007,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_attention_append", &decode_attention_append);
   m.def("lora_proj", &lora_proj);
   m.def("lora_acc", &lora_acc);
+  m.def("lora_proj2", &lora_proj2);
+  m.def("lora_acc2", &lora_acc2);
   m.def("gemm_int4", &gemm_int4);
   m.def("gemv_w4", &gemv_w4);
   m.def("sample", &sample);

@@ -304,6 +304,205 @@ __global__ __launch_bounds__(256) void lora_acc_mfma_k(const float* __restrict__
     atomicAdd(out + j * sj + (int64_t)(kb + kk) * sk, v);
   }
 }
+
+// ---- two branches sharing one input (q_proj + v_proj of a fused q|k|v projection) -------------
+// Each pass over x serves BOTH adapters: the x fragment is loaded once and masked twice (the two
+// branches' independent dropout streams), so the activations are read once per projection instead
+// of once per adapter.
+
+// lora_proj for two branches: A0 [r0, K], A1 [r1, K] (r0 + r1 <= 16); output columns j < r0 are
+// branch 0 (its mask, scale), the rest branch 1.  Two MFMAs per k-step, each against the rows of
+// its own branch (the other branch's B rows are zero), accumulate into one 16-column tile.
+template <int NW, int RW>
+__global__ __launch_bounds__(NW * 64) void lora_proj2_k(const bf16* __restrict__ X, int ldx, const bf16* __restrict__ W0,
+                                                       const bf16* __restrict__ W1, int r0, int r, int K, float* __restrict__ outf, int ldof,
+                                                       bf16* __restrict__ outb, int ldob, int M, uint64_t key0,
+                                                       uint64_t key1, uint32_t thr0, uint32_t thr1, float ds0,
+                                                       float ds1, float scale0, float scale1, size_t mask_ld) {
+  __shared__ f32x4 red[NW][64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int m0 = blockIdx.x * RW;
+  const bool rv = (lane & 15) < RW;
+  const int row = min(m0 + (lane & 15), M - 1);
+  const int kw = K / NW;
+  const int kbeg = w * kw;
+  const bf16* xr = X + (size_t)row * ldx;
+  const int n = lane & 15;
+  const bf16* wr = n < r0 ? W0 + (size_t)n * K : (n < r ? W1 + (size_t)(n - r0) * K : W0);
+  const bool in0 = n < r0, in1 = n >= r0 && n < r;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = kbeg; k0 < kbeg + kw; k0 += 8 * 32) {
+    bf16x8 av[8], bv[8];
+    const int ns = min(8, (kbeg + kw - k0) / 32);
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      if (s < ns) {
+        const int k = k0 + s * 32 + 8 * (lane >> 4);
+        av[s] = rv ? *reinterpret_cast<const bf16x8*>(xr + k) : bf16x8{};
+        bv[s] = *reinterpret_cast<const bf16x8*>(wr + k);
+      }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      if (s < ns) {
+        const int k = k0 + s * 32 + 8 * (lane >> 4);
+        const size_t v8 = ((size_t)row * mask_ld + k) >> 3;
+        const uint32_t keep0 = thr0 ? dropout_keep8(key0, v8, thr0) : 0xFFu;
+        const uint32_t keep1 = thr1 ? dropout_keep8(key1, v8, thr1) : 0xFFu;
+        const float d0 = thr0 ? ds0 : 1.f, d1 = thr1 ? ds1 : 1.f;
+        bf16x8 a0, a1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float xv = (float)av[s][i];
+          a0[i] = ((keep0 >> i) & 1) ? (bf16)(xv * d0) : (bf16)0.f;
+          a1[i] = ((keep1 >> i) & 1) ? (bf16)(xv * d1) : (bf16)0.f;
+        }
+        const bf16x8 b0 = in0 ? bv[s] : bf16x8{};
+        const bf16x8 b1 = in1 ? bv[s] : bf16x8{};
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc, 0, 0, 0);
+      }
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w != 0) return;
+  f32x4 t = red[0][lane];
+#pragma unroll
+  for (int i = 1; i < NW; ++i) t += red[i][lane];
+  const int j = lane & 15;
+  if (j >= r) return;
+  const float sc = j < r0 ? scale0 : scale1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ml = 4 * (lane >> 4) + i, m = m0 + ml;
+    if (ml >= RW || m >= M) continue;
+    const float v = t[i] * sc;
+    if (outf) outf[(size_t)m * ldof + j] = v;
+    if (outb) outb[(size_t)m * ldob + j] = (bf16)v;
+  }
+}
+
+// lora_acc (matrix cores) for two dropout branches over the same x / dx, R = 8 rows each:
+//   out_i[j, k] += Σ_m G_i[m, j]·D_i(X)[m, k]          (dA of each adapter)
+//   DX[m, k]    += Σ_i D_i(Σ_j G_i[m, j]·A_i[j, k])    (both adapters' input gradients, one RW of dx)
+// — the single-branch kernel above run twice read x twice and dx twice; this reads each once.
+template <int SUB>
+__global__ __launch_bounds__(256) void lora_acc2_mfma_k(const float* __restrict__ G0, int ldg0, int r0,
+                                                       const float* __restrict__ G1, int ldg1, int r1,
+                                                       const bf16* __restrict__ X, int ldx, bf16* __restrict__ DX,
+                                                       int lddx, const bf16* __restrict__ W0,
+                                                       const bf16* __restrict__ W1, int K, float* __restrict__ out0,
+                                                       float* __restrict__ out1, int64_t sj0, int64_t sk0, int64_t sj1,
+                                                       int64_t sk1, int M, uint64_t key0, uint64_t key1, uint32_t thr0,
+                                                       uint32_t thr1, float ds0, float ds1, size_t mask_ld) {
+  constexpr int R = 8;
+  __shared__ float red[4][64][33];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int q = lane >> 4, n = lane & 15;
+  const int kb = blockIdx.x * 128;
+  const int k8 = kb + 8 * n;
+  const int mw = blockIdx.y * (128 * SUB) + w * (32 * SUB);
+  bf16x8 wv0[R], wv1[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    wv0[j] = j < r0 ? *reinterpret_cast<const bf16x8*>(W0 + (size_t)j * K + k8) : bf16x8{};
+    wv1[j] = j < r1 ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)j * K + k8) : bf16x8{};
+  }
+  f32x4 acc0[8], acc1[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) acc0[c] = acc1[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float d0 = thr0 ? ds0 : 1.f, d1 = thr1 ? ds1 : 1.f;
+#pragma unroll
+  for (int s = 0; s < SUB; ++s) {
+    const int m0 = mw + 32 * s + 8 * q;
+    bf16x8 xb[8], db[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int m = min(m0 + e, M - 1);
+      xb[e] = *reinterpret_cast<const bf16x8*>(X + (size_t)m * ldx + k8);
+      db[e] = *reinterpret_cast<const bf16x8*>(DX + (size_t)m * lddx + k8);
+    }
+    bf16x8 a0, a1;   // Gᵀ fragments: rows j = n (< 8 used), k = the lane group's 8 m
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int m = m0 + e;
+      a0[e] = (bf16)((m < M && n < r0) ? G0[(size_t)m * ldg0 + n] : 0.f);
+      a1[e] = (bf16)((m < M && n < r1) ? G1[(size_t)m * ldg1 + n] : 0.f);
+    }
+    uint32_t keep0[8], keep1[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int m = m0 + e;
+      const size_t v8 = ((size_t)m * mask_ld + k8) >> 3;
+      keep0[e] = m >= M ? 0u : (thr0 ? dropout_keep8(key0, v8, thr0) : 0xFFu);
+      keep1[e] = m >= M ? 0u : (thr1 ? dropout_keep8(key1, v8, thr1) : 0xFFu);
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      bf16x8 b0, b1;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        b0[e] = ((keep0[e] >> c) & 1) ? xb[e][c] : (bf16)0.f;
+        b1[e] = ((keep1[e] >> c) & 1) ? xb[e][c] : (bf16)0.f;
+      }
+      acc0[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc0[c], 0, 0, 0);
+      acc1[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc1[c], 0, 0, 0);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int m = m0 + e;
+      if (m >= M) continue;
+      float g0[R], g1[R];
+#pragma unroll
+      for (int j = 0; j < R; j += 4) {
+        const f32x4 t0 = *reinterpret_cast<const f32x4*>(G0 + (size_t)m * ldg0 + j);
+        const f32x4 t1 = *reinterpret_cast<const f32x4*>(G1 + (size_t)m * ldg1 + j);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          g0[j + u] = j + u < r0 ? t0[u] : 0.f;
+          g1[j + u] = j + u < r1 ? t1[u] : 0.f;
+        }
+      }
+      float t0[8], t1[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t0[i] = t1[i] = 0.f;
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          t0[i] += g0[j] * (float)wv0[j][i];
+          t1[i] += g1[j] * (float)wv1[j][i];
+        }
+      bf16x8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        o[i] = (bf16)((float)db[e][i] + (((keep0[e] >> i) & 1) ? t0[i] * d0 : 0.f) +
+                      (((keep1[e] >> i) & 1) ? t1[i] * d1 : 0.f));
+      *reinterpret_cast<bf16x8*>(DX + (size_t)m * lddx + k8) = o;
+    }
+  }
+  // reduce the 4 waves' partials branch by branch through the one LDS array
+#pragma unroll
+  for (int br = 0; br < 2; ++br) {
+    const f32x4* acc = br == 0 ? acc0 : acc1;
+    const int r = br == 0 ? r0 : r1;
+    const int64_t sj = br == 0 ? sj0 : sj1, sk = br == 0 ? sk0 : sk1;
+    float* out = br == 0 ? out0 : out1;
+    const float ds = br == 0 ? d0 : d1;
+    if (br == 1) __syncthreads();        // branch 0's reads of red are done
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) red[w][lane][c * 4 + t] = acc[c][t];
+    __syncthreads();
+    const bool jfast = sj == 1;
+    for (int idx = threadIdx.x; idx < r * 128; idx += 256) {
+      const int j = jfast ? idx % r : idx / 128, kk = jfast ? idx / r : idx % 128;
+      const int ln = 16 * (j >> 2) + (kk >> 3), slot = (kk & 7) * 4 + (j & 3);
+      const float v = (red[0][ln][slot] + red[1][ln][slot] + red[2][ln][slot] + red[3][ln][slot]) * ds;
+      atomicAdd(out + j * sj + (int64_t)(kb + kk) * sk, v);
+    }
+  }
+}
 }  // namespace
 
 // X row stride ldx (elements), W [r, K] bf16 contiguous; K % 32 == 0; outf/outb may each be null.
@@ -389,5 +588,42 @@ void launch_lora_acc(const float* G, int ldg, int r, const void* X, int ldx, voi
   }
 #undef B
 #undef A
+  LIPA_CHECK_LAUNCH();
+}
+
+// two branches sharing x: W = [A0; A1] ([r0 + r1 <= 16, K]); outputs [M, r0 + r1] (fp32 and/or bf16)
+void launch_lora_proj2(const void* X, int ldx, const void* W0, const void* W1, int r0, int r, int K, float* outf, int ldof, void* outb,
+                       int ldob, int M, uint64_t key0, float p0, float scale0, uint64_t key1, float p1, float scale1,
+                       size_t mask_ld, hipStream_t st) {
+  const uint32_t thr0 = p0 > 0.f ? (uint32_t)(p0 * 65536.0f + 0.5f) : 0u;
+  const uint32_t thr1 = p1 > 0.f ? (uint32_t)(p1 * 65536.0f + 0.5f) : 0u;
+  const float ds0 = p0 > 0.f ? 1.f / (1.f - p0) : 1.f, ds1 = p1 > 0.f ? 1.f / (1.f - p1) : 1.f;
+  const int rw = M < 4096 ? 8 : 16;
+  const int grid = (M + rw - 1) / rw;
+  if (K % (16 * 32) == 0 && rw == 8)
+    lora_proj2_k<16, 8><<<grid, 1024, 0, st>>>((const bf16*)X, ldx, (const bf16*)W0, (const bf16*)W1, r0, r, K, outf, ldof,
+                                               (bf16*)outb, ldob, M, key0, key1, thr0, thr1, ds0, ds1, scale0, scale1, mask_ld);
+  else if (K % (16 * 32) == 0)
+    lora_proj2_k<16, 16><<<grid, 1024, 0, st>>>((const bf16*)X, ldx, (const bf16*)W0, (const bf16*)W1, r0, r, K, outf, ldof,
+                                                (bf16*)outb, ldob, M, key0, key1, thr0, thr1, ds0, ds1, scale0, scale1, mask_ld);
+  else
+    lora_proj2_k<1, 16><<<(M + 15) / 16, 64, 0, st>>>((const bf16*)X, ldx, (const bf16*)W0, (const bf16*)W1, r0, r, K, outf,
+                                                      ldof, (bf16*)outb, ldob, M, key0, key1, thr0, thr1, ds0, ds1, scale0,
+                                                      scale1, mask_ld);
+  LIPA_CHECK_LAUNCH();
+}
+
+// two dropout branches over the same x / dx (r0, r1 <= 8, K % 128 == 0)
+void launch_lora_acc2(const float* G0, int ldg0, int r0, const float* G1, int ldg1, int r1, const void* X, int ldx,
+                      void* DX, int lddx, const void* W0, const void* W1, int K, float* out0, float* out1, int64_t sj0,
+                      int64_t sk0, int64_t sj1, int64_t sk1, int M, uint64_t key0, float p0, uint64_t key1, float p1,
+                      size_t mask_ld, hipStream_t st) {
+  const uint32_t thr0 = p0 > 0.f ? (uint32_t)(p0 * 65536.0f + 0.5f) : 0u;
+  const uint32_t thr1 = p1 > 0.f ? (uint32_t)(p1 * 65536.0f + 0.5f) : 0u;
+  const float ds0 = p0 > 0.f ? 1.f / (1.f - p0) : 1.f, ds1 = p1 > 0.f ? 1.f / (1.f - p1) : 1.f;
+  dim3 g2(K / 128, (M + 127) / 128);
+  lora_acc2_mfma_k<1><<<g2, 256, 0, st>>>(G0, ldg0, r0, G1, ldg1, r1, (const bf16*)X, ldx, (bf16*)DX, lddx,
+                                          (const bf16*)W0, (const bf16*)W1, K, out0, out1, sj0, sk0, sj1, sk1, M, key0,
+                                          key1, thr0, thr1, ds0, ds1, mask_ld);
   LIPA_CHECK_LAUNCH();
 }

@@ -230,6 +230,12 @@ def _zero_buffer(tag: str, rows: int, cols: int, like: torch.Tensor) -> torch.Te
     return t
 
 
+def _pair_ok(x, branches) -> bool:
+    """Two rank-<=8 adapters on one fused projection (q_proj + v_proj): the two-branch kernels."""
+    return (len(branches) == 2 and x.is_cuda and all(br.a.shape[0] <= 8 for br in branches)
+            and __import__("os").environ.get("LIPA_LORA_PAIR", "1") != "0")
+
+
 def _fast_lora_ok(x, branches) -> bool:
     """Shapes the fused LoRA branch kernels (csrc/kernels/lora.hip) take."""
     K = x.shape[1]
@@ -257,9 +263,25 @@ class _FusedLinearFn(torch.autograd.Function):
                 ext_b = x.new_zeros(N, rp)
                 ext_a = x.new_zeros(x.shape[0], rp) if fast else None
             cols, r0 = [], 0
-            for br, (a, b) in zip(branches, zip(ab[0::2], ab[1::2])):
+            pair = fast and _pair_ok(x, branches)
+            if pair:   # q_proj + v_proj: ONE pass over x for both adapters (lora_proj2)
+                ps = [br.dropout if training else 0.0 for br in branches]
+                pair_keys = [next_dropout_key() if p > 0 else None for p in ps]
+                a0, a1 = bf16_view(ab[0], x.dtype), bf16_view(ab[2], x.dtype)
+                rr = a0.shape[0] + a1.shape[0]
+                xa2 = native().lora_proj2(x, a0, a1, ext_a[:, :rr], need_xa, ps[0], pair_keys[0] or 0,
+                                          branches[0].scaling, ps[1], pair_keys[1] or 0, branches[1].scaling)
+            for bi, (br, (a, b)) in enumerate(zip(branches, zip(ab[0::2], ab[1::2]))):
                 r = a.shape[0]
                 p = br.dropout if training else 0.0
+                if pair:
+                    key = pair_keys[bi]
+                    xa = xa2[:, r0:r0 + r] if need_xa else None
+                    ext_b[br.c0:br.c1, r0:r0 + r] = bf16_view(b, x.dtype)
+                    xa_list.append(xa)
+                    keys.append(key)
+                    r0 += r
+                    continue
                 key = next_dropout_key() if p > 0 else None
                 if fast:   # one MFMA pass: s·D(x)·Aᵀ into the ext slice (bf16) + fp32 copy for dB
                     xa = native().lora_proj(x, 0, x.shape[1], bf16_view(a, x.dtype), ext_a[:, r0:r0 + r],
@@ -284,6 +306,7 @@ class _FusedLinearFn(torch.autograd.Function):
         ctx.meta = meta
         ctx.keys = keys
         ctx.fast = fast
+        ctx.pair = bool(branches) and fast and _pair_ok(x, branches)
         ctx.ab_refs = ab          # the parameters themselves: fused kernels accumulate into their .grad
         ctx.has_residual = residual is not None
         ctx.save_for_backward(x, weight, *ab, *[t for t in xa_list if t is not None])
@@ -343,7 +366,21 @@ class _FusedLinearFn(torch.autograd.Function):
             wb = ctx.wdq if ctx.wdq is not None else (base if not dense else weight)
             dx = _base_gemm_t(dy, wb, ext_a, ext_b)
         ctx.wdq = None
-        for i, br in enumerate(branches):
+        if (ctx.pair and dx is not None and all(k is not None for k in ctx.keys) and not deterministic()
+                and ctx.needs_input_grad[5] and ctx.needs_input_grad[7]):
+            # both adapters' dA and their dx terms in ONE pass over x and dx (lora_acc2)
+            (o0, ret0), (o1, ret1) = dest(0), dest(2)
+            native().lora_acc2(g_list[0], g_list[1], x, dx, bf16_view(ab[0], dy.dtype), bf16_view(ab[2], dy.dtype),
+                               o0, o1, branches[0].dropout, ctx.keys[0], branches[1].dropout, ctx.keys[1])
+            for i, (o, ret) in ((0, (o0, ret0)), (1, (o1, ret1))):
+                if ret:
+                    grads_ab[2 * i] = o.to(ab[2 * i].dtype)
+                else:
+                    _notify_grad_ready(ctx.ab_refs[2 * i])
+            branches_acc = ()
+        else:
+            branches_acc = branches
+        for i, br in enumerate(branches_acc):
             key = ctx.keys[i]
             if fast:   # dA += gᵀ·D(x) and (dropout branches) dx += D(g·A), one pass over x / dx
                 upd = dx if (dx is not None and key is not None) else None

@@ -555,6 +555,36 @@ def test_lora_fused_kernels(native_ext, M, K, r, p):
     assert rel_err(da2, gg.t() @ x.float()) < 1e-2
 
 
+@pytest.mark.parametrize("M,K,p0,p1", [(2048, 4096, 0.1, 0.1), (1000, 1024, 0.05, 0.0), (77, 512, 0.0, 0.2)])
+def test_lora_two_branch_kernels(native_ext, M, K, p0, p1):
+    """lora_proj2 / lora_acc2 (q_proj + v_proj over one x pass) vs fp32 with each branch's own
+    regenerated dropout mask."""
+    torch.manual_seed(1)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    a0 = (0.05 * torch.randn(8, K, device=DEV)).to(torch.bfloat16)
+    a1 = (0.05 * torch.randn(8, K, device=DEV)).to(torch.bfloat16)
+    k0, k1 = 777, 991
+    xd0 = native_ext.dropout_fwd(x, p0, k0) if p0 > 0 else x
+    xd1 = native_ext.dropout_fwd(x, p1, k1) if p1 > 0 else x
+    outb = torch.zeros(M, 32, device=DEV, dtype=torch.bfloat16)
+    xa = native_ext.lora_proj2(x, a0, a1, outb[:, :16], True, p0, k0, 2.0, p1, k1, 0.5)
+    ref = torch.cat([2.0 * xd0.float() @ a0.float().t(), 0.5 * xd1.float() @ a1.float().t()], 1)
+    assert rel_err(xa, ref) < 1e-2 and rel_err(outb[:, :16], ref) < 1e-2 and outb[:, 16:].abs().sum() == 0
+    g0 = torch.randn(M, 8, device=DEV)
+    g1 = torch.randn(M, 8, device=DEV)
+    dx = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    dx0 = dx.float().clone()
+    da0 = torch.ones(8, K, device=DEV)
+    da1 = torch.zeros(8, K, device=DEV)
+    native_ext.lora_acc2(g0, g1, x, dx, a0, a1, da0, da1, p0, k0, p1, k1)
+    assert rel_err(da0 - 1, g0.t() @ xd0.float()) < 1e-2
+    assert rel_err(da1, g1.t() @ xd1.float()) < 1e-2
+    m0 = ((xd0 != 0) | (x == 0)).float() * (1 / (1 - p0)) if p0 > 0 else torch.ones_like(dx0)
+    m1 = ((xd1 != 0) | (x == 0)).float() * (1 / (1 - p1)) if p1 > 0 else torch.ones_like(dx0)
+    want = dx0 + m0 * (g0 @ a0.float()) + m1 * (g1 @ a1.float())
+    assert rel_err(dx, want) < 1e-2
+
+
 # ----------------------------------------------------------------------------- 8-phase GEMM
 @pytest.mark.parametrize("M,N,K,splits,lora,resid", [(256, 256, 64, 1, False, False), (512, 768, 512, 1, True, True),
                                                      (300, 520, 192, 1, True, False), (2048, 1024, 1024, 4, True, True),

@@ -101,3 +101,25 @@ def test_grad_ckpt_lora_dropout_same_gradients(native_ext, monkeypatch, targets)
     for n in grads[0]:
         a, b = grads[0][n], grads[1][n]
         assert (a - b).norm() <= 2e-3 * a.norm() + 1e-6, n
+
+
+def test_lora_pair_kernels_match_single_branch_path(native_ext, monkeypatch):
+    """q_proj + v_proj through the two-branch kernels (one x / dx pass) give the same loss and
+    LoRA gradients as the per-adapter kernels, dropout 0.1 included (same counter-RNG keys)."""
+    from llm_in_practise_amd.ops.linear import seed_dropout
+    torch.manual_seed(0)
+    ids = torch.randint(0, 1000, (2, 64), device="cuda")
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("LIPA_LORA_PAIR", mode)
+        pm = _qlora(seed=0)
+        pm.train()
+        seed_dropout(42)
+        out = pm(input_ids=ids, labels=ids)
+        out.loss.backward()
+        res[mode] = (out.loss.item(), {n: p.grad.float().clone() for n, p in pm.named_parameters() if p.requires_grad})
+    (l0, g0), (l1, g1) = res["0"], res["1"]
+    assert abs(l0 - l1) < 1e-3 * abs(l0)
+    for n in g0:
+        err = (g0[n] - g1[n]).norm() / g0[n].norm().clamp(min=1e-12)
+        assert err < 2e-2, (n, float(err))
