@@ -34,6 +34,9 @@ def main():
     bv = torch.randn(r, 1024, device=dev, dtype=torch.bfloat16) * 0.02
     ext = torch.zeros(M, 16, device=dev, dtype=torch.bfloat16)
     g = torch.randn(M, r, device=dev, dtype=torch.float32)
+    g2 = torch.randn(M, r, device=dev, dtype=torch.float32)
+    a2 = torch.randn(r, H, device=dev, dtype=torch.bfloat16) * 0.02
+    outA2 = torch.zeros(r, H, device=dev, dtype=torch.float32)
     outA = torch.zeros(r, H, device=dev, dtype=torch.float32)
     outBq = torch.zeros(4096, r, device=dev, dtype=torch.float32)
     outBv = torch.zeros(1024, r, device=dev, dtype=torch.float32)
@@ -50,7 +53,13 @@ def main():
         "acc_dA_drop_nodx": (lambda: N.lora_acc(g, x, 0, H, outA, False, None, None, 0.1, 7, False), M * H * 2),
         "dropout_fwd": (lambda: N.dropout_fwd(x, 0.1, 7), 2 * M * H * 2),
         "acc_dA_nodx": (lambda: N.lora_acc(g, x, 0, H, outA, False, None, None, 0.0, 0, False), M * H * 2),
+        "pair_proj2_fwd_drop": (lambda: N.lora_proj2(x, a, a2, ext, True, 0.1, 7, 2.0, 0.1, 9, 2.0), M * H * 2),
+        "pair_acc2_dA_dx_drop": (lambda: N.lora_acc2(g, g2, x, dx, a, a2, outA, outA2, 0.1, 7, 0.1, 9), 3 * M * H * 2),
     }
+    import os
+    only = os.environ.get("LORA_CASES")
+    if only:
+        cases = {k: v for k, v in cases.items() if any(o in k for o in only.split(","))}
     for name, (fn, nbytes) in cases.items():
         us = timeit(fn)
         print(json.dumps({"case": name, "us": round(us, 2), "TB_s": round(nbytes / us / 1e6, 2)}), flush=True)
