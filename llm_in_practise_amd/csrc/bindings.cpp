@@ -76,6 +76,8 @@ void launch_lora_proj2(const void*, int, const void*, const void*, int, int, int
 void launch_lora_acc2(const float*, int, int, const float*, int, int, const void*, int, void*, int, const void*,
                       const void*, int, float*, float*, int64_t, int64_t, int64_t, int64_t, int, uint64_t, float,
                       uint64_t, float, size_t, hipStream_t);
+void launch_lora_apply(void*, int, int, int, const float* const*, const int*, const void* const*, const int*, const int*,
+                       const int*, hipStream_t);
 void launch_lora_acc(const float*, int, int, const void*, int, void*, int, const void*, int, float*, int64_t, int64_t,
                      float*, int, uint64_t, float, size_t, hipStream_t);
 void launch_decode_attention(const void*, const void*, const void*, const int*, float*, float*, float*, void*, int, int,
@@ -737,6 +739,36 @@ void lora_acc2(Tensor g0, Tensor g1, Tensor x, Tensor dx, Tensor a0, Tensor a1, 
                    (uint64_t)key0, (float)p0, (uint64_t)key1, (float)p1, (size_t)x.stride(0), stream());
 }
 
+// y[:, c0_i : c0_i + n_i] += xa_i · B_iᵀ in place (xa_i fp32 [M, r_i], scale folded in; B_i bf16 [n_i, r_i])
+void lora_apply(Tensor y, std::vector<Tensor> xas, std::vector<Tensor> bs, std::vector<int64_t> c0s) {
+  CHECK_CUDA(y);
+  CHECK_BF16(y);
+  const int nb = (int)xas.size();
+  TORCH_CHECK(nb >= 1 && nb <= 4 && (int)bs.size() == nb && (int)c0s.size() == nb, "lora_apply: 1..4 branches");
+  TORCH_CHECK(y.dim() == 2 && y.stride(1) == 1 && y.stride(0) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0, "lora_apply: y [M, N] 16-B aligned rows");
+  const int M = y.size(0);
+  std::vector<const float*> xp(nb);
+  std::vector<const void*> bp(nb);
+  std::vector<int> ld(nb), c0(nb), n(nb), r(nb);
+  for (int i = 0; i < nb; ++i) {
+    TORCH_CHECK(xas[i].scalar_type() == at::kFloat && xas[i].dim() == 2 && xas[i].stride(1) == 1 &&
+                    xas[i].size(0) == M && xas[i].size(1) <= 16, "lora_apply: xa fp32 [M, r<=16]");
+    TORCH_CHECK(bs[i].scalar_type() == at::kBFloat16 && bs[i].is_contiguous() && bs[i].size(1) == xas[i].size(1),
+                "lora_apply: B bf16 [n, r] contiguous");
+    TORCH_CHECK(c0s[i] % 8 == 0 && bs[i].size(0) % 8 == 0 && c0s[i] + bs[i].size(0) <= y.size(1),
+                "lora_apply: column block");
+    xp[i] = xas[i].data_ptr<float>();
+    ld[i] = xas[i].stride(0);
+    bp[i] = bs[i].data_ptr();
+    c0[i] = c0s[i];
+    n[i] = bs[i].size(0);
+    r[i] = bs[i].size(1);
+  }
+  launch_lora_apply(y.data_ptr(), y.stride(0), M, nb, xp.data(), ld.data(), bp.data(), c0.data(), n.data(), r.data(),
+                    stream());
+}
+
 void lora_acc(Tensor g, Tensor x, int64_t c0, int64_t K, Tensor out, bool out_transposed, optional<Tensor> dx,
               optional<Tensor> w, double p, int64_t key, bool deterministic) {
   TORCH_CHECK(g.scalar_type() == at::kFloat && g.dim() == 2 && g.stride(1) == 1 && g.size(1) <= 16, "lora_acc: g");
@@ -1009,6 +1041,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lora_acc", &lora_acc);
   m.def("lora_proj2", &lora_proj2);
   m.def("lora_acc2", &lora_acc2);
+  m.def("lora_apply", &lora_apply);
   m.def("gemm_int4", &gemm_int4);
   m.def("gemv_w4", &gemv_w4);
   m.def("sample", &sample);

@@ -503,6 +503,80 @@ __global__ __launch_bounds__(256) void lora_acc2_mfma_k(const float* __restrict_
     }
   }
 }
+
+// ---- y[:, c0_i : c0_i + n_i] += xa_i · B_iᵀ for up to 4 branches, in place on the base GEMM's output ----
+// (replaces the rank-Σr addmm over ALL N columns of a fused q|k|v output plus the per-call copies of
+// each B into a zero-padded [N, 32] K-slice buffer: only the adapters' own column blocks are read and
+// written, B is read in its natural [n, r] layout.)  xa_i is fp32 [M, r_i] and already carries the
+// branch scale.  Tile: 64 rows × 256 columns per workgroup; a thread owns 8 consecutive columns
+// (their 8 × r B values are 128 contiguous bytes) of 8 rows.
+struct LoraApplyArgs {
+  const float* xa[4];
+  int ldxa[4];
+  const bf16* B[4];
+  int c0[4], n[4], r[4];
+  int blk0[5];    // first column block of each branch (prefix sums), blk0[nb] = total
+  int nb;
+};
+
+template <int R>
+__global__ __launch_bounds__(256) void lora_apply_k(bf16* __restrict__ Y, int ldy, int M, LoraApplyArgs a) {
+  __shared__ __attribute__((aligned(16))) float xs[64][R];
+  int br = 0;
+#pragma unroll
+  for (int i = 1; i < 4; ++i)
+    if (i < a.nb && (int)blockIdx.x >= a.blk0[i]) br = i;
+  const int r = a.r[br];
+  const int m0 = blockIdx.y * 64;
+  const int cb = (blockIdx.x - a.blk0[br]) * 256;
+  const float* xa = a.xa[br];
+  for (int i = threadIdx.x; i < 64 * R; i += 256) {
+    const int rr = i / R, j = i % R, m = m0 + rr;
+    xs[rr][j] = (m < M && j < r) ? xa[(size_t)m * a.ldxa[br] + j] : 0.f;
+  }
+  __syncthreads();
+  const int cl = cb + 8 * (threadIdx.x & 31);
+  if (cl >= a.n[br]) return;
+  // B rows of this thread's 8 columns: [8][R] bf16, contiguous when r == R (vector loads)
+  float bw[8][R];
+  const bf16* Bp = a.B[br] + (size_t)cl * r;
+  if (r == R) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int j0 = 0; j0 < R; j0 += 8) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(Bp + c * R + j0);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bw[c][j0 + e] = (float)v[e];
+      }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int j = 0; j < R; ++j) bw[c][j] = (j < r) ? (float)Bp[c * r + j] : 0.f;
+  }
+  bf16* yc = Y + a.c0[br] + cl;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int rr = (threadIdx.x >> 5) + 8 * i, m = m0 + rr;
+    if (m >= M) break;
+    float xv[R];
+#pragma unroll
+    for (int j0 = 0; j0 < R; j0 += 4) {
+      const f32x4 t = *reinterpret_cast<const f32x4*>(&xs[rr][j0]);
+      xv[j0] = t[0]; xv[j0 + 1] = t[1]; xv[j0 + 2] = t[2]; xv[j0 + 3] = t[3];
+    }
+    bf16x8 y = *reinterpret_cast<const bf16x8*>(yc + (size_t)m * ldy);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float acc = (float)y[c];
+#pragma unroll
+      for (int j = 0; j < R; ++j) acc += xv[j] * bw[c][j];
+      y[c] = (bf16)acc;
+    }
+    *reinterpret_cast<bf16x8*>(yc + (size_t)m * ldy) = y;
+  }
+}
 }  // namespace
 
 // X row stride ldx (elements), W [r, K] bf16 contiguous; K % 32 == 0; outf/outb may each be null.
@@ -625,5 +699,32 @@ void launch_lora_acc2(const float* G0, int ldg0, int r0, const float* G1, int ld
   lora_acc2_mfma_k<1><<<g2, 256, 0, st>>>(G0, ldg0, r0, G1, ldg1, r1, (const bf16*)X, ldx, (bf16*)DX, lddx,
                                           (const bf16*)W0, (const bf16*)W1, K, out0, out1, sj0, sk0, sj1, sk1, M, key0,
                                           key1, thr0, thr1, ds0, ds1, mask_ld);
+  LIPA_CHECK_LAUNCH();
+}
+
+void launch_lora_apply(void* Y, int ldy, int M, int nb, const float* const* xa, const int* ldxa, const void* const* B,
+                       const int* c0, const int* n, const int* r, hipStream_t st) {
+  LoraApplyArgs a{};
+  a.nb = nb;
+  int tot = 0;
+  for (int i = 0; i < nb; ++i) {
+    a.xa[i] = xa[i];
+    a.ldxa[i] = ldxa[i];
+    a.B[i] = static_cast<const bf16*>(B[i]);
+    a.c0[i] = c0[i];
+    a.n[i] = n[i];
+    a.r[i] = r[i];
+    a.blk0[i] = tot;
+    tot += (n[i] + 255) / 256;
+  }
+  a.blk0[nb] = tot;
+  for (int i = nb + 1; i < 5; ++i) a.blk0[i] = tot;
+  dim3 grid(tot, (M + 63) / 64);
+  int rmax = 0;
+  for (int i = 0; i < nb; ++i) rmax = r[i] > rmax ? r[i] : rmax;
+  if (rmax <= 8)
+    lora_apply_k<8><<<grid, 256, 0, st>>>(static_cast<bf16*>(Y), ldy, M, a);
+  else
+    lora_apply_k<16><<<grid, 256, 0, st>>>(static_cast<bf16*>(Y), ldy, M, a);
   LIPA_CHECK_LAUNCH();
 }

@@ -39,6 +39,8 @@ _NATIVE_DENSE = __import__("os").environ.get("LIPA_DENSE_GEMM", "") == "native"
 #  "fused" — the register-dequant MFMA GEMMs (gemm_w4v2, LoRA K-slice + residual epilogue):
 #    no bf16 copy at all, for memory-bound deployments.
 _NF4_MODE = __import__("os").environ.get("LIPA_NF4_GEMM", "dequant")
+# LoRA B term as an in-place column-block update after the base GEMM (LIPA_LORA_APPLY=0: K-slice form)
+_APPLY = __import__("os").environ.get("LIPA_LORA_APPLY", "1") != "0"
 
 
 def _nf4_dequant_bf16(q: NF4Weight) -> torch.Tensor:
@@ -251,7 +253,28 @@ class _FusedLinearFn(torch.autograd.Function):
         ext_a = ext_b = None
         fast = bool(branches) and _fast_lora_ok(x, branches)
         need_xa = any(ctx.needs_input_grad[5:])     # (grad mode is off inside forward: ask autograd)
-        if branches:
+        # "apply" form: the base GEMM runs alone, then lora_apply adds xa_i·B_iᵀ into ONLY the adapters'
+        # column blocks of its output (no K-slice buffers, no per-call B copies, no rank-Σr addmm over
+        # all N columns)
+        apply = fast and x.is_cuda and len(branches) <= 4 and _APPLY
+        if apply:
+            pair = _pair_ok(x, branches)
+            if pair:
+                ps = [br.dropout if training else 0.0 for br in branches]
+                keys = [next_dropout_key() if p > 0 else None for p in ps]
+                a0, a1 = bf16_view(ab[0], x.dtype), bf16_view(ab[2], x.dtype)
+                xa2 = native().lora_proj2(x, a0, a1, None, True, ps[0], keys[0] or 0, branches[0].scaling,
+                                          ps[1], keys[1] or 0, branches[1].scaling)
+                r0 = a0.shape[0]
+                xa_list = [xa2[:, :r0], xa2[:, r0:]]
+            else:
+                for br, a in zip(branches, ab[0::2]):
+                    p = br.dropout if training else 0.0
+                    key = next_dropout_key() if p > 0 else None
+                    xa_list.append(native().lora_proj(x, 0, x.shape[1], bf16_view(a, x.dtype), None, True, p,
+                                                      key or 0, br.scaling))
+                    keys.append(key)
+        elif branches:
             N = base.shape[0]
             rtot = sum(br.a.shape[0] for br in branches)
             rp = (rtot + EXT_ALIGN - 1) // EXT_ALIGN * EXT_ALIGN
@@ -300,6 +323,10 @@ class _FusedLinearFn(torch.autograd.Function):
         if not dense and _NF4_MODE == "dequant" and x.shape[0] > 8 and base.kernel_ok():
             wdq = _nf4_dequant_bf16(base)
         y = _base_gemm(x, wdq if wdq is not None else (base if not dense else weight), ext_a, ext_b, residual)
+        if apply:
+            native().lora_apply(y, xa_list, [bf16_view(b, x.dtype) for b in ab[1::2]], [br.c0 for br in branches])
+            if not need_xa:
+                xa_list = [None] * len(xa_list)
         ctx.wdq = wdq if ctx.needs_input_grad[0] else None
         if bias is not None:
             y = y + bias

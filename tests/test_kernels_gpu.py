@@ -611,3 +611,19 @@ def test_gemm8_strided_input(native_ext):
     x = big[:, 64:]
     w = torch.randn(256, 1024, device=DEV).to(torch.bfloat16)
     assert rel_err(native_ext.gemm8(x, w, None, None, None, 1), x.float() @ w.float().t()) < 1e-2
+
+
+def test_lora_apply_column_blocks(native_ext):
+    """lora_apply: y[:, c0_i:c0_i+n_i] += xa_i·B_iᵀ in place for several branches, other columns untouched."""
+    torch.manual_seed(3)
+    M, N = 333, 6144
+    y = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    y0 = y.float().clone()
+    specs = [(0, 4096, 8), (5120, 1024, 8), (4096, 1024, 16)]
+    xas = [torch.randn(M, r, device=DEV) for _, _, r in specs]
+    bs = [(0.1 * torch.randn(n, r, device=DEV)).to(torch.bfloat16) for _, n, r in specs]
+    native_ext.lora_apply(y, xas, bs, [c0 for c0, _, _ in specs])
+    want = y0.clone()
+    for (c0, n, _), xa, b in zip(specs, xas, bs):
+        want[:, c0:c0 + n] += xa @ b.float().t()
+    assert rel_err(y, want) < 1e-2
