@@ -40,6 +40,10 @@ void launch_absmax_t(const float*, const uint8_t*, const float*, const float*, c
 void launch_nf4_quantize(const void*, uint8_t*, float*, size_t, hipStream_t);
 void launch_nf4_dequant2(const uint8_t*, const float*, void*, size_t, hipStream_t);
 int skinny_splits(int, int);
+bool lt_gemm(bool, bool, long, long, long, const void*, long, const void*, long, const void*, void*, long, int, long,
+             long, long, void*, size_t, hipStream_t);
+void lt_reset();
+void launch_sum_slices(const void*, void*, int, size_t, size_t, hipStream_t);
 void launch_gemm_skinny(const void*, int, const void*, const void*, void*, float*, int, int, int, int, hipStream_t);
 int w4_skinny_splits(int, int);
 void launch_gemm_w4_skinny(const void*, int, const uint8_t*, const float*, const float*, int, const void*, void*, float*,
@@ -337,6 +341,70 @@ std::vector<Tensor> nf4_quantize(Tensor w, int64_t blocksize) {
 }
 
 // decode-shaped y = x·Wᵀ (+ residual): x [M <= 64, K] row-strided, W [N, K] contiguous bf16
+// ---- hipBLASLt frozen-base GEMMs (csrc/kernels/blaslt.hip)
+static void* lt_workspace(size_t& bytes) {
+  static std::vector<Tensor> ws(16);
+  const int dev = at::hip::current_device();
+  bytes = (size_t)64 << 20;
+  if (!ws[dev].defined())
+    ws[dev] = at::empty({(int64_t)bytes}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, dev));
+  return ws[dev].data_ptr();
+}
+
+// y = x·wᵀ (+ residual): x [M, K] (unit column stride), w [N, K] contiguous bf16
+Tensor lt_linear(Tensor x, Tensor w, optional<Tensor> residual) {
+  CHECK_CUDA(x);
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && w.dim() == 2 && w.size(1) == x.size(1), "lt_linear: shapes");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  const void* cp = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    CHECK_BF16((*residual));
+    CHECK_CONTIG((*residual));
+    TORCH_CHECK(residual->size(0) == M && residual->size(1) == N, "lt_linear: residual shape");
+    cp = residual->data_ptr();
+  }
+  Tensor out = at::empty({M, N}, x.options());
+  size_t wsb;
+  void* ws = lt_workspace(wsb);
+  if (!lt_gemm(true, false, N, M, K, w.data_ptr(), K, x.data_ptr(), x.stride(0), cp, out.data_ptr(), N, 1, 0, 0, 0,
+               ws, wsb, stream()))
+    return cp ? at::addmm(*residual, x, w.t()) : at::mm(x, w.t());
+  return out;
+}
+
+// dx = dy·w: dy [M, N] contiguous, w [N, K] contiguous; split > 1: K-slices of the reduction dim
+// as one strided-batched GEMM into bf16 partials + an fp32 slice sum
+Tensor lt_dx(Tensor dy, Tensor w, int64_t split) {
+  CHECK_CUDA(dy);
+  CHECK_BF16(dy);
+  CHECK_BF16(w);
+  CHECK_CONTIG(dy);
+  CHECK_CONTIG(w);
+  const int64_t M = dy.size(0), N = dy.size(1), K = w.size(1);
+  TORCH_CHECK(w.size(0) == N, "lt_dx: shapes");
+  TORCH_CHECK(split == 1 || ((split == 2 || split == 3 || split == 4 || split == 8) && N % split == 0 && K % 8 == 0),
+              "lt_dx: split");
+  size_t wsb;
+  void* ws = lt_workspace(wsb);
+  Tensor out = at::empty({M, K}, dy.options());
+  if (split == 1) {
+    if (!lt_gemm(false, false, K, M, N, w.data_ptr(), K, dy.data_ptr(), N, nullptr, out.data_ptr(), K, 1, 0, 0, 0, ws,
+                 wsb, stream()))
+      return at::mm(dy, w);
+    return out;
+  }
+  const int64_t Ns = N / split;
+  Tensor part = at::empty({split, M, K}, dy.options());
+  if (!lt_gemm(false, false, K, M, Ns, w.data_ptr(), K, dy.data_ptr(), N, nullptr, part.data_ptr(), K, (int)split,
+               Ns * K, Ns, M * K, ws, wsb, stream()))
+    return at::mm(dy, w);
+  launch_sum_slices(part.data_ptr(), out.data_ptr(), (int)split, (size_t)(M * K), (size_t)(M * K), stream());
+  return out;
+}
+
 Tensor gemm_skinny(Tensor x, Tensor w, optional<Tensor> residual) {
   CHECK_CUDA(x);
   CHECK_BF16(x);
@@ -1052,6 +1120,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nf4_dequant", &nf4_dequant);
   m.def("nf4_dequant_fast", &nf4_dequant_fast);
   m.def("gemm_skinny", &gemm_skinny);
+  m.def("lt_linear", &lt_linear);
+  m.def("lt_dx", &lt_dx);
+  m.def("lt_reset", &lt_reset);
   m.def("gemm_w4_skinny", &gemm_w4_skinny);
   m.def("set_dequant_variant", &set_dequant_variant);
   m.def("nf4_pack", &nf4_pack);

@@ -85,7 +85,7 @@ def build_hip_extension(jobs: int | None = None, verbose: bool = True) -> str:
     out = os.path.join(PKG, f"_C{EXT_SUFFIX}")
     link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out + ".tmp"] + objs
     link += [f"-L{p}" for p in libs] + [f"-Wl,-rpath,{p}" for p in libs]
-    link += ["-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip", "-lamdhip64"]
+    link += ["-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip", "-lamdhip64", "-lhipblaslt"]
     _run(link)
     os.replace(out + ".tmp", out)
     if verbose:

@@ -65,6 +65,24 @@ __global__ __launch_bounds__(256) void gelu_bwd_k(const T* __restrict__ dy, cons
   }
 }
 
+// y[n] = Σ_s x[s·stride + ·] (fp32 sum of S bf16 slices: the split-K partials of a batched GEMM)
+template <int S>
+__global__ __launch_bounds__(256) void sum_slices_k(const bf16* __restrict__ x, bf16* __restrict__ y, size_t n8,
+                                                    size_t stride) {
+  for (size_t v = (size_t)blockIdx.x * 256 + threadIdx.x; v < n8; v += (size_t)gridDim.x * 256) {
+    float a[S][8], o[8];
+#pragma unroll
+    for (int s = 0; s < S; ++s) load8(x + s * stride + v * 8, a[s]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      o[i] = a[0][i];
+#pragma unroll
+      for (int s = 1; s < S; ++s) o[i] += a[s][i];
+    }
+    store8(y + v * 8, o);
+  }
+}
+
 inline int grid_for(size_t work) {
   size_t g = (work + 255) / 256;
   return (int)(g < 2048 ? (g ? g : 1) : 2048);
@@ -88,5 +106,16 @@ void launch_gelu_fwd(int dtype, const void* x, void* y, size_t n, hipStream_t st
 void launch_gelu_bwd(int dtype, const void* dy, const void* x, void* dx, size_t n, hipStream_t st) {
   if (dtype == 1) gelu_bwd_k<bf16><<<grid_for(n), 256, 0, st>>>((const bf16*)dy, (const bf16*)x, (bf16*)dx, n);
   else gelu_bwd_k<float><<<grid_for(n), 256, 0, st>>>((const float*)dy, (const float*)x, (float*)dx, n);
+  LIPA_CHECK_LAUNCH();
+}
+void launch_sum_slices(const void* x, void* y, int S, size_t n, size_t stride, hipStream_t st) {
+  const size_t n8 = n / 8;
+  const int g = grid_for(n8);
+  switch (S) {
+    case 2: sum_slices_k<2><<<g, 256, 0, st>>>((const bf16*)x, (bf16*)y, n8, stride); break;
+    case 3: sum_slices_k<3><<<g, 256, 0, st>>>((const bf16*)x, (bf16*)y, n8, stride); break;
+    case 4: sum_slices_k<4><<<g, 256, 0, st>>>((const bf16*)x, (bf16*)y, n8, stride); break;
+    default: sum_slices_k<8><<<g, 256, 0, st>>>((const bf16*)x, (bf16*)y, n8, stride); break;
+  }
   LIPA_CHECK_LAUNCH();
 }

@@ -41,6 +41,11 @@ _NATIVE_DENSE = __import__("os").environ.get("LIPA_DENSE_GEMM", "") == "native"
 _NF4_MODE = __import__("os").environ.get("LIPA_NF4_GEMM", "dequant")
 # LoRA B term as an in-place column-block update after the base GEMM (LIPA_LORA_APPLY=0: K-slice form)
 _APPLY = __import__("os").environ.get("LIPA_LORA_APPLY", "1") != "0"
+# training-sized bf16 base GEMMs through direct hipBLASLt calls (csrc/kernels/blaslt.hip): the
+# residual as a separate C matrix (no copy into the output first) and a per-shape kernel choice
+# timed in the running step; LIPA_LT=0: torch.addmm / torch.mm / torch.bmm
+_LT = __import__("os").environ.get("LIPA_LT", "1") != "0"
+_LT_MIN_M = 256
 
 
 def _nf4_dequant_bf16(q: NF4Weight) -> torch.Tensor:
@@ -93,6 +98,10 @@ def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
         # the residual; the wide gate|up / long-K down stay on hipBLASLt (≥ 5 TB/s there)
         y = native().gemm_skinny(x, base, residual)
         return y if ext_a is None else y.addmm_(ext_a, ext_b.t())
+    if _LT and M >= _LT_MIN_M and x.is_cuda and x.dtype == torch.bfloat16 and x.stride(1) == 1 \
+            and not _NATIVE_DENSE:
+        y = native().lt_linear(x, base.contiguous(), None if residual is None else residual.contiguous())
+        return y if ext_a is None else y.addmm_(ext_a, ext_b.t())
     if not _NATIVE_DENSE:
         # a bf16 base is a plain library GEMM: hipBLASLt's tuned kernels run it at 1.1-1.5
         # PFLOP/s at the Qwen3 shapes (profiles/gemm_nf4_v1_v2_hipblaslt_ab.txt) and its split-K
@@ -113,8 +122,11 @@ def _dense_dx(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     sum fill it (491 → 328 µs, profiles/nf4_dequant_vs_fused_ab.txt)."""
     M, N = dy.shape
     K = w.shape[1]
-    if N % 4 == 0 and N >= 4 * K and M >= 256 and (M // 256) * max(1, K // 256) < 256:
-        s = 4
+    split = 4 if N % 4 == 0 and N >= 4 * K and M >= 256 and (M // 256) * max(1, K // 256) < 256 else 1
+    if _LT and M >= _LT_MIN_M and dy.is_cuda and dy.dtype == torch.bfloat16 and K % 8 == 0:
+        return native().lt_dx(dy.contiguous(), w.contiguous(), split)
+    if split > 1:
+        s = split
         return torch.bmm(dy.view(M, s, N // s).transpose(0, 1), w.view(s, N // s, K)).sum(0)
     return dy @ w
 

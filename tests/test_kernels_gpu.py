@@ -627,3 +627,30 @@ def test_lora_apply_column_blocks(native_ext):
     for (c0, n, _), xa, b in zip(specs, xas, bs):
         want[:, c0:c0 + n] += xa @ b.float().t()
     assert rel_err(y, want) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K,res", [(512, 768, 512, False), (512, 1024, 768, True), (300, 640, 256, True)])
+def test_lt_linear(native_ext, M, N, K, res):
+    """Direct hipBLASLt frozen-base GEMM (separate C = residual), over the in-step candidate
+    timing phase and after it, vs an fp32 reference."""
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / K ** 0.5
+    r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16) if res else None
+    want = x.float() @ w.float().t() + (r.float() if res else 0)
+    for _ in range(20):          # candidate rotation (4 x 3 timed calls), then the chosen kernel
+        y = native_ext.lt_linear(x, w, r)
+        assert (y.float() - want).abs().max().item() < 0.05 * want.abs().max().item()
+    if res:
+        assert r is not y
+
+
+@pytest.mark.parametrize("split", [1, 2, 4])
+def test_lt_dx_split(native_ext, split):
+    M, N, K = 512, 2048, 512
+    dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / N ** 0.5
+    want = dy.float() @ w.float()
+    for _ in range(16):
+        dx = native_ext.lt_dx(dy, w, split)
+        err = (dx.float() - want).abs().max().item()
+        assert err < 0.03 * want.abs().max().item(), err
