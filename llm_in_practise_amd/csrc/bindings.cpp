@@ -80,7 +80,7 @@ void launch_lora_proj2(const void*, int, const void*, const void*, int, int, int
 void launch_lora_acc2(const float*, int, int, const float*, int, int, const void*, int, void*, int, const void*,
                       const void*, int, float*, float*, int64_t, int64_t, int64_t, int64_t, int, uint64_t, float,
                       uint64_t, float, size_t, hipStream_t);
-void launch_lora_apply(void*, int, int, int, const float* const*, const int*, const void* const*, const int*, const int*,
+void launch_lora_apply(void*, int, int, int, const float* const*, const int*, const void* const*, void* const*, const int*, const int*,
                        const int*, hipStream_t);
 void launch_lora_acc(const float*, int, int, const void*, int, void*, int, const void*, int, float*, int64_t, int64_t,
                      float*, int, uint64_t, float, size_t, hipStream_t);
@@ -808,7 +808,8 @@ void lora_acc2(Tensor g0, Tensor g1, Tensor x, Tensor dx, Tensor a0, Tensor a1, 
 }
 
 // y[:, c0_i : c0_i + n_i] += xa_i · B_iᵀ in place (xa_i fp32 [M, r_i], scale folded in; B_i bf16 [n_i, r_i])
-void lora_apply(Tensor y, std::vector<Tensor> xas, std::vector<Tensor> bs, std::vector<int64_t> c0s) {
+void lora_apply(Tensor y, std::vector<Tensor> xas, std::vector<Tensor> bs, std::vector<int64_t> c0s,
+                std::vector<Tensor> bts) {
   CHECK_CUDA(y);
   CHECK_BF16(y);
   const int nb = (int)xas.size();
@@ -818,6 +819,8 @@ void lora_apply(Tensor y, std::vector<Tensor> xas, std::vector<Tensor> bs, std::
   const int M = y.size(0);
   std::vector<const float*> xp(nb);
   std::vector<const void*> bp(nb);
+  std::vector<void*> btp(nb, nullptr);
+  TORCH_CHECK(bts.empty() || (int)bts.size() == nb, "lora_apply: one Bt output per branch");
   std::vector<int> ld(nb), c0(nb), n(nb), r(nb);
   for (int i = 0; i < nb; ++i) {
     TORCH_CHECK(xas[i].scalar_type() == at::kFloat && xas[i].dim() == 2 && xas[i].stride(1) == 1 &&
@@ -829,12 +832,18 @@ void lora_apply(Tensor y, std::vector<Tensor> xas, std::vector<Tensor> bs, std::
     xp[i] = xas[i].data_ptr<float>();
     ld[i] = xas[i].stride(0);
     bp[i] = bs[i].data_ptr();
+    if (!bts.empty()) {
+      TORCH_CHECK(bts[i].scalar_type() == at::kBFloat16 && bts[i].is_contiguous() && bts[i].size(0) == bs[i].size(1) &&
+                      bts[i].size(1) == bs[i].size(0) && reinterpret_cast<uintptr_t>(bts[i].data_ptr()) % 16 == 0,
+                  "lora_apply: Bt bf16 [r, n] contiguous, 16-B aligned");
+      btp[i] = bts[i].data_ptr();
+    }
     c0[i] = c0s[i];
     n[i] = bs[i].size(0);
     r[i] = bs[i].size(1);
   }
-  launch_lora_apply(y.data_ptr(), y.stride(0), M, nb, xp.data(), ld.data(), bp.data(), c0.data(), n.data(), r.data(),
-                    stream());
+  launch_lora_apply(y.data_ptr(), y.stride(0), M, nb, xp.data(), ld.data(), bp.data(), bts.empty() ? nullptr : btp.data(),
+                    c0.data(), n.data(), r.data(), stream());
 }
 
 void lora_acc(Tensor g, Tensor x, int64_t c0, int64_t K, Tensor out, bool out_transposed, optional<Tensor> dx,

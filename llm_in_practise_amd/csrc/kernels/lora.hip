@@ -514,6 +514,7 @@ struct LoraApplyArgs {
   const float* xa[4];
   int ldxa[4];
   const bf16* B[4];
+  bf16* Bt[4];    // optional [r, n] copy of B for the backward's dy·B projection (row-0 workgroups write it)
   int c0[4], n[4], r[4];
   int blk0[5];    // first column block of each branch (prefix sums), blk0[nb] = total
   int nb;
@@ -554,6 +555,17 @@ __global__ __launch_bounds__(256) void lora_apply_k(bf16* __restrict__ Y, int ld
     for (int c = 0; c < 8; ++c)
 #pragma unroll
       for (int j = 0; j < R; ++j) bw[c][j] = (j < r) ? (float)Bp[c * r + j] : 0.f;
+  }
+  if (a.Bt[br] && blockIdx.y == 0 && threadIdx.x < 32) {
+    bf16* bt = a.Bt[br] + cl;
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+      if (j < r) {
+        bf16x8 v;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = (bf16)bw[c][j];
+        *reinterpret_cast<bf16x8*>(bt + (size_t)j * a.n[br]) = v;
+      }
   }
   bf16* yc = Y + a.c0[br] + cl;
 #pragma unroll
@@ -703,7 +715,7 @@ void launch_lora_acc2(const float* G0, int ldg0, int r0, const float* G1, int ld
 }
 
 void launch_lora_apply(void* Y, int ldy, int M, int nb, const float* const* xa, const int* ldxa, const void* const* B,
-                       const int* c0, const int* n, const int* r, hipStream_t st) {
+                       void* const* Bt, const int* c0, const int* n, const int* r, hipStream_t st) {
   LoraApplyArgs a{};
   a.nb = nb;
   int tot = 0;
@@ -711,6 +723,7 @@ void launch_lora_apply(void* Y, int ldy, int M, int nb, const float* const* xa, 
     a.xa[i] = xa[i];
     a.ldxa[i] = ldxa[i];
     a.B[i] = static_cast<const bf16*>(B[i]);
+    a.Bt[i] = Bt ? static_cast<bf16*>(Bt[i]) : nullptr;
     a.c0[i] = c0[i];
     a.n[i] = n[i];
     a.r[i] = r[i];

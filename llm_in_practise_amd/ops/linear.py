@@ -335,8 +335,13 @@ class _FusedLinearFn(torch.autograd.Function):
         if not dense and _NF4_MODE == "dequant" and x.shape[0] > 8 and base.kernel_ok():
             wdq = _nf4_dequant_bf16(base)
         y = _base_gemm(x, wdq if wdq is not None else (base if not dense else weight), ext_a, ext_b, residual)
+        ctx.bts = None
         if apply:
-            native().lora_apply(y, xa_list, [bf16_view(b, x.dtype) for b in ab[1::2]], [br.c0 for br in branches])
+            bs = [bf16_view(b, x.dtype) for b in ab[1::2]]
+            # training: the same pass writes Bᵀ [r, n] for the backward's dy·B projection (no transpose kernel)
+            bts = [torch.empty(b.shape[1], b.shape[0], dtype=x.dtype, device=x.device) for b in bs] if need_xa else []
+            native().lora_apply(y, xa_list, bs, [br.c0 for br in branches], bts)
+            ctx.bts = bts or None
             if not need_xa:
                 xa_list = [None] * len(xa_list)
         ctx.wdq = wdq if ctx.needs_input_grad[0] else None
@@ -377,7 +382,7 @@ class _FusedLinearFn(torch.autograd.Function):
             a, b = ab[2 * i], ab[2 * i + 1]
             n_i = br.c1 - br.c0
             if fast:
-                bt = bf16_view(b, dy.dtype).t().contiguous()                      # [r, n_i]
+                bt = ctx.bts[i] if ctx.bts is not None else bf16_view(b, dy.dtype).t().contiguous()   # [r, n_i]
                 g = native().lora_proj(dy, br.c0, n_i, bt, None, True, 0.0, 0, br.scaling)   # s·dy_i·B, fp32
                 if ctx.needs_input_grad[5 + 2 * i + 1]:
                     out, ret = dest(2 * i + 1)                                     # dB [n_i, r] += dy_iᵀ·xa_s
@@ -405,6 +410,7 @@ class _FusedLinearFn(torch.autograd.Function):
             wb = ctx.wdq if ctx.wdq is not None else (base if not dense else weight)
             dx = _base_gemm_t(dy, wb, ext_a, ext_b)
         ctx.wdq = None
+        ctx.bts = None
         if (ctx.pair and dx is not None and all(k is not None for k in ctx.keys) and not deterministic()
                 and ctx.needs_input_grad[5] and ctx.needs_input_grad[7]):
             # both adapters' dA and their dx terms in ONE pass over x and dx (lora_acc2)

@@ -1,11 +1,10 @@
 #!/bin/bash
-# kernel tests (subset by -k expr) then N bench runs.  usage: scripts/gpu_quick.sh "<-k expr>" <nbench>
-set -u
-export HSA_ENABLE_IPC_MODE_LEGACY=0
+# tests touching the LoRA / linear path + 2 bench runs + kernel trace.  usage: scripts/gpu_quick.sh <tag>
+export PYTHONPATH=.
+TAG=${1:-q}
 mkdir -p gpurun_out
-timeout -k 10 400 python -m pytest tests -m gpu -q -x -k "$1" --timeout 120 --timeout-method thread > gpurun_out/q_tests.log 2>&1 || { tail -30 gpurun_out/q_tests.log; exit 1; }
-tail -1 gpurun_out/q_tests.log
-for i in $(seq 1 $2); do
-timeout -k 10 300 python bench.py --steps 8 --warmup 2 > gpurun_out/q_bench.log 2>&1 || { tail -20 gpurun_out/q_bench.log; exit 1; }
-echo "$(grep -o '[0-9.]* ms/step  [0-9,]* tok/s' gpurun_out/q_bench.log)"
-done
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "lt_ or lora" tests/test_trainer_gpu.py > gpurun_out/${TAG}_tests.log 2>&1 &&
+timeout -k 10 300 python bench.py --steps 20 --warmup 3 > gpurun_out/bench_${TAG}1.json 2>>gpurun_out/bench_${TAG}.err &&
+timeout -k 10 300 python bench.py --steps 20 --warmup 3 > gpurun_out/bench_${TAG}2.json 2>>gpurun_out/bench_${TAG}.err &&
+bash scripts/gpu_prof.sh $TAG > /dev/null 2>&1
+rc=$?; tail -2 gpurun_out/${TAG}_tests.log; grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench_${TAG}1.json gpurun_out/bench_${TAG}2.json; exit $rc

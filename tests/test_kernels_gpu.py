@@ -622,11 +622,16 @@ def test_lora_apply_column_blocks(native_ext):
     specs = [(0, 4096, 8), (5120, 1024, 8), (4096, 1024, 16)]
     xas = [torch.randn(M, r, device=DEV) for _, _, r in specs]
     bs = [(0.1 * torch.randn(n, r, device=DEV)).to(torch.bfloat16) for _, n, r in specs]
-    native_ext.lora_apply(y, xas, bs, [c0 for c0, _, _ in specs])
+    bts = [torch.empty(r, n, device=DEV, dtype=torch.bfloat16) for _, n, r in specs]
+    native_ext.lora_apply(y, xas, bs, [c0 for c0, _, _ in specs], bts)
     want = y0.clone()
-    for (c0, n, _), xa, b in zip(specs, xas, bs):
+    for (c0, n, _), xa, b, bt in zip(specs, xas, bs, bts):
         want[:, c0:c0 + n] += xa @ b.float().t()
+        assert torch.equal(bt, b.t())          # the backward's [r, n] copy of B
     assert rel_err(y, want) < 1e-2
+    y2 = y0.to(torch.bfloat16)
+    native_ext.lora_apply(y2, xas, bs, [c0 for c0, _, _ in specs], [])   # no Bt outputs
+    assert rel_err(y2, want) < 1e-2
 
 
 @pytest.mark.parametrize("M,N,K,res", [(512, 768, 512, False), (512, 1024, 768, True), (300, 640, 256, True)])
