@@ -17,7 +17,7 @@ void launch_layernorm_bwd(int, const void*, const void*, const void*, const floa
 int norm_partial_rows(int M);
 void launch_qk_norm_rope_fwd(const void*, const void*, const void*, const float*, const float*, void*, void*, float*,
                              float*, int, int, int, int, float, hipStream_t);
-void launch_qk_norm_rope_bwd(const void*, const void*, const void*, const void*, const void*, const float*,
+void launch_qk_norm_rope_bwd(const void*, const void*, const void*, const void*, const void*, const void*, const float*,
                              const float*, const float*, const float*, void*, int, int, int, int, hipStream_t);
 void launch_rope(int, const void*, const float*, const float*, void*, int, int, int, int, int, hipStream_t);
 void launch_swiglu_fwd(const void*, void*, int, int, hipStream_t);
@@ -76,10 +76,10 @@ void launch_moe_combine(int, const void*, const int*, const float*, const void*,
 void launch_moe_wgrad(int, const void*, const void*, const int*, float*, int, int, int, hipStream_t);
 int lora_acc_chunks(int M, int K);
 void launch_lora_proj2(const void*, int, const void*, const void*, int, int, int, float*, int, void*, int, int, uint64_t, float, float,
-                       uint64_t, float, float, size_t, hipStream_t);
+                       uint64_t, float, float, size_t, uint8_t*, hipStream_t);
 void launch_lora_acc2(const float*, int, int, const float*, int, int, const void*, int, void*, int, const void*,
                       const void*, int, float*, float*, int64_t, int64_t, int64_t, int64_t, int, uint64_t, float,
-                      uint64_t, float, size_t, hipStream_t);
+                      uint64_t, float, size_t, const uint8_t*, hipStream_t);
 void launch_lora_apply(void*, int, int, int, const float* const*, const int*, const void* const*, void* const*, const int*, const int*,
                        const int*, hipStream_t);
 void launch_lora_acc(const float*, int, int, const void*, int, void*, int, const void*, int, float*, int64_t, int64_t,
@@ -222,12 +222,17 @@ Tensor qk_norm_rope_bwd(Tensor dq, Tensor dk, optional<Tensor> dv, Tensor qkv, o
                         int64_t d) {
   const int T = qkv.size(0);
   auto dqkv = at::empty_like(qkv);
-  launch_qk_norm_rope_bwd(dq.data_ptr(), dk.data_ptr(), qkv.data_ptr(), optr(qw), optr(kw), cos.data_ptr<float>(),
-                          sin.data_ptr<float>(), rq.data_ptr<float>(), rk.data_ptr<float>(), dqkv.data_ptr(), T, hq,
-                          hkv, d, stream());
-  auto vslice = dqkv.narrow(1, (hq + hkv) * d, hkv * d);
-  if (dv && dv->defined()) vslice.copy_(*dv);
-  else vslice.zero_();
+  const void* dvp = nullptr;
+  if (dv && dv->defined()) {
+    CHECK_BF16((*dv));
+    CHECK_CONTIG((*dv));
+    TORCH_CHECK(dv->numel() == (int64_t)T * hkv * d, "qk_norm_rope_bwd: dv [T, hkv*d]");
+    dvp = dv->data_ptr();
+  }
+  // the kernel writes all three parts of dqkv (the v rows: dv copied through, zeros without one)
+  launch_qk_norm_rope_bwd(dq.data_ptr(), dk.data_ptr(), dvp, qkv.data_ptr(), optr(qw), optr(kw),
+                          cos.data_ptr<float>(), sin.data_ptr<float>(), rq.data_ptr<float>(), rk.data_ptr<float>(),
+                          dqkv.data_ptr(), T, hq, hkv, d, stream());
   return dqkv;
 }
 
@@ -755,8 +760,16 @@ Tensor lora_proj(Tensor x, int64_t c0, int64_t K, Tensor w, optional<Tensor> out
 
 // out (fp32, 2-D, [r, K] or its transpose view [K, r]) += gᵀ·D(x[:, c0:c0+K]); with dx: dx += D(g·w)
 // two LoRA branches sharing x (q_proj + v_proj): A0 [r0, K], A1 [r1, K] bf16, r0 + r1 <= 16
+static uint8_t* keep_bits_ptr(const optional<Tensor>& m, int64_t M, int64_t K, const char* who) {
+  if (!m || !m->defined()) return nullptr;
+  TORCH_CHECK(m->scalar_type() == at::kByte && m->is_contiguous() && m->numel() == 2 * M * (K / 8),
+              who, ": keep bits uint8 [2, M, K/8] contiguous");
+  return m->data_ptr<uint8_t>();
+}
+
+// masks (optional, uint8 [2, M, K/8]): the two branches' dropout keep bits, written for lora_acc2
 Tensor lora_proj2(Tensor x, Tensor a0, Tensor a1, optional<Tensor> outb, bool want_f32, double p0, int64_t key0,
-                  double scale0, double p1, int64_t key1, double scale1) {
+                  double scale0, double p1, int64_t key1, double scale1, optional<Tensor> masks) {
   CHECK_BF16(x);
   CHECK_BF16(a0);
   CHECK_BF16(a1);
@@ -778,13 +791,13 @@ Tensor lora_proj2(Tensor x, Tensor a0, Tensor a1, optional<Tensor> outb, bool wa
   TORCH_CHECK(ob || want_f32, "lora_proj2: no output");
   launch_lora_proj2(x.data_ptr(), x.stride(0), a0.data_ptr(), a1.data_ptr(), r0, r, K, want_f32 ? of.data_ptr<float>() : nullptr, r,
                     ob, ldob, M, (uint64_t)key0, (float)p0, (float)scale0, (uint64_t)key1, (float)p1, (float)scale1,
-                    (size_t)x.stride(0), stream());
+                    (size_t)x.stride(0), keep_bits_ptr(masks, M, K, "lora_proj2"), stream());
   return want_f32 ? of : Tensor();
 }
 
 // dA_i [r_i, K] += G_iᵀ·D_i(x), dx += Σ_i D_i(G_i·A_i) for two branches in one pass (r_i <= 8)
 void lora_acc2(Tensor g0, Tensor g1, Tensor x, Tensor dx, Tensor a0, Tensor a1, Tensor out0, Tensor out1, double p0,
-               int64_t key0, double p1, int64_t key1) {
+               int64_t key0, double p1, int64_t key1, optional<Tensor> masks) {
   for (const Tensor* g : {&g0, &g1})
     TORCH_CHECK(g->scalar_type() == at::kFloat && g->dim() == 2 && g->stride(1) == 1 && g->size(1) <= 8 &&
                     g->stride(0) % 4 == 0 && g->stride(0) >= 8 && reinterpret_cast<uintptr_t>(g->data_ptr()) % 16 == 0,
@@ -804,7 +817,8 @@ void lora_acc2(Tensor g0, Tensor g1, Tensor x, Tensor dx, Tensor a0, Tensor a1, 
   launch_lora_acc2(g0.data_ptr<float>(), g0.stride(0), r0, g1.data_ptr<float>(), g1.stride(0), r1, x.data_ptr(),
                    x.stride(0), dx.data_ptr(), dx.stride(0), a0.data_ptr(), a1.data_ptr(), K, out0.data_ptr<float>(),
                    out1.data_ptr<float>(), out0.stride(0), out0.stride(1), out1.stride(0), out1.stride(1), M,
-                   (uint64_t)key0, (float)p0, (uint64_t)key1, (float)p1, (size_t)x.stride(0), stream());
+                   (uint64_t)key0, (float)p0, (uint64_t)key1, (float)p1, (size_t)x.stride(0),
+                   keep_bits_ptr(masks, M, K, "lora_acc2"), stream());
 }
 
 // y[:, c0_i : c0_i + n_i] += xa_i · B_iᵀ in place (xa_i fp32 [M, r_i], scale folded in; B_i bf16 [n_i, r_i])

@@ -318,7 +318,8 @@ __global__ __launch_bounds__(NW * 64) void lora_proj2_k(const bf16* __restrict__
                                                        const bf16* __restrict__ W1, int r0, int r, int K, float* __restrict__ outf, int ldof,
                                                        bf16* __restrict__ outb, int ldob, int M, uint64_t key0,
                                                        uint64_t key1, uint32_t thr0, uint32_t thr1, float ds0,
-                                                       float ds1, float scale0, float scale1, size_t mask_ld) {
+                                                       float ds1, float scale0, float scale1, size_t mask_ld,
+                                                       uint8_t* __restrict__ mko) {
   __shared__ f32x4 red[NW][64];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int m0 = blockIdx.x * RW;
@@ -346,8 +347,14 @@ __global__ __launch_bounds__(NW * 64) void lora_proj2_k(const bf16* __restrict__
       if (s < ns) {
         const int k = k0 + s * 32 + 8 * (lane >> 4);
         const size_t v8 = ((size_t)row * mask_ld + k) >> 3;
-        const uint32_t keep0 = thr0 ? dropout_keep8(key0, v8, thr0) : 0xFFu;
-        const uint32_t keep1 = thr1 ? dropout_keep8(key1, v8, thr1) : 0xFFu;
+        // padding rows (RW = 8: lanes 8..15) draw no mask: their x fragment is zero anyway
+        const uint32_t keep0 = thr0 && rv ? dropout_keep8(key0, v8, thr0) : 0xFFu;
+        const uint32_t keep1 = thr1 && rv ? dropout_keep8(key1, v8, thr1) : 0xFFu;
+        if (mko && rv && m0 + (lane & 15) < M) {   // the keep bits for the backward (1 bit / element)
+          const size_t mi = (size_t)row * (K >> 3) + (k >> 3);
+          mko[mi] = (uint8_t)keep0;
+          mko[(size_t)M * (K >> 3) + mi] = (uint8_t)keep1;
+        }
         const float d0 = thr0 ? ds0 : 1.f, d1 = thr1 ? ds1 : 1.f;
         bf16x8 a0, a1;
 #pragma unroll
@@ -393,7 +400,8 @@ __global__ __launch_bounds__(256) void lora_acc2_mfma_k(const float* __restrict_
                                                        const bf16* __restrict__ W1, int K, float* __restrict__ out0,
                                                        float* __restrict__ out1, int64_t sj0, int64_t sk0, int64_t sj1,
                                                        int64_t sk1, int M, uint64_t key0, uint64_t key1, uint32_t thr0,
-                                                       uint32_t thr1, float ds0, float ds1, size_t mask_ld) {
+                                                       uint32_t thr1, float ds0, float ds1, size_t mask_ld,
+                                                       const uint8_t* __restrict__ mki) {
   constexpr int R = 8;
   __shared__ float red[4][64][33];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -433,8 +441,14 @@ __global__ __launch_bounds__(256) void lora_acc2_mfma_k(const float* __restrict_
     for (int e = 0; e < 8; ++e) {
       const int m = m0 + e;
       const size_t v8 = ((size_t)m * mask_ld + k8) >> 3;
-      keep0[e] = m >= M ? 0u : (thr0 ? dropout_keep8(key0, v8, thr0) : 0xFFu);
-      keep1[e] = m >= M ? 0u : (thr1 ? dropout_keep8(key1, v8, thr1) : 0xFFu);
+      if (mki) {   // keep bits stored by the forward's lora_proj2 (no hash regeneration)
+        const size_t mi = (size_t)min(m, M - 1) * (K >> 3) + (k8 >> 3);
+        keep0[e] = m >= M ? 0u : (thr0 ? (uint32_t)mki[mi] : 0xFFu);
+        keep1[e] = m >= M ? 0u : (thr1 ? (uint32_t)mki[(size_t)M * (K >> 3) + mi] : 0xFFu);
+      } else {
+        keep0[e] = m >= M ? 0u : (thr0 ? dropout_keep8(key0, v8, thr0) : 0xFFu);
+        keep1[e] = m >= M ? 0u : (thr1 ? dropout_keep8(key1, v8, thr1) : 0xFFu);
+      }
     }
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
@@ -680,7 +694,7 @@ void launch_lora_acc(const float* G, int ldg, int r, const void* X, int ldx, voi
 // two branches sharing x: W = [A0; A1] ([r0 + r1 <= 16, K]); outputs [M, r0 + r1] (fp32 and/or bf16)
 void launch_lora_proj2(const void* X, int ldx, const void* W0, const void* W1, int r0, int r, int K, float* outf, int ldof, void* outb,
                        int ldob, int M, uint64_t key0, float p0, float scale0, uint64_t key1, float p1, float scale1,
-                       size_t mask_ld, hipStream_t st) {
+                       size_t mask_ld, uint8_t* mko, hipStream_t st) {
   const uint32_t thr0 = p0 > 0.f ? (uint32_t)(p0 * 65536.0f + 0.5f) : 0u;
   const uint32_t thr1 = p1 > 0.f ? (uint32_t)(p1 * 65536.0f + 0.5f) : 0u;
   const float ds0 = p0 > 0.f ? 1.f / (1.f - p0) : 1.f, ds1 = p1 > 0.f ? 1.f / (1.f - p1) : 1.f;
@@ -688,14 +702,14 @@ void launch_lora_proj2(const void* X, int ldx, const void* W0, const void* W1, i
   const int grid = (M + rw - 1) / rw;
   if (K % (16 * 32) == 0 && rw == 8)
     lora_proj2_k<16, 8><<<grid, 1024, 0, st>>>((const bf16*)X, ldx, (const bf16*)W0, (const bf16*)W1, r0, r, K, outf, ldof,
-                                               (bf16*)outb, ldob, M, key0, key1, thr0, thr1, ds0, ds1, scale0, scale1, mask_ld);
+                                               (bf16*)outb, ldob, M, key0, key1, thr0, thr1, ds0, ds1, scale0, scale1, mask_ld, mko);
   else if (K % (16 * 32) == 0)
     lora_proj2_k<16, 16><<<grid, 1024, 0, st>>>((const bf16*)X, ldx, (const bf16*)W0, (const bf16*)W1, r0, r, K, outf, ldof,
-                                                (bf16*)outb, ldob, M, key0, key1, thr0, thr1, ds0, ds1, scale0, scale1, mask_ld);
+                                                (bf16*)outb, ldob, M, key0, key1, thr0, thr1, ds0, ds1, scale0, scale1, mask_ld, mko);
   else
     lora_proj2_k<1, 16><<<(M + 15) / 16, 64, 0, st>>>((const bf16*)X, ldx, (const bf16*)W0, (const bf16*)W1, r0, r, K, outf,
                                                       ldof, (bf16*)outb, ldob, M, key0, key1, thr0, thr1, ds0, ds1, scale0,
-                                                      scale1, mask_ld);
+                                                      scale1, mask_ld, mko);
   LIPA_CHECK_LAUNCH();
 }
 
@@ -703,14 +717,14 @@ void launch_lora_proj2(const void* X, int ldx, const void* W0, const void* W1, i
 void launch_lora_acc2(const float* G0, int ldg0, int r0, const float* G1, int ldg1, int r1, const void* X, int ldx,
                       void* DX, int lddx, const void* W0, const void* W1, int K, float* out0, float* out1, int64_t sj0,
                       int64_t sk0, int64_t sj1, int64_t sk1, int M, uint64_t key0, float p0, uint64_t key1, float p1,
-                      size_t mask_ld, hipStream_t st) {
+                      size_t mask_ld, const uint8_t* mki, hipStream_t st) {
   const uint32_t thr0 = p0 > 0.f ? (uint32_t)(p0 * 65536.0f + 0.5f) : 0u;
   const uint32_t thr1 = p1 > 0.f ? (uint32_t)(p1 * 65536.0f + 0.5f) : 0u;
   const float ds0 = p0 > 0.f ? 1.f / (1.f - p0) : 1.f, ds1 = p1 > 0.f ? 1.f / (1.f - p1) : 1.f;
   dim3 g2(K / 128, (M + 127) / 128);
   lora_acc2_mfma_k<1><<<g2, 256, 0, st>>>(G0, ldg0, r0, G1, ldg1, r1, (const bf16*)X, ldx, (bf16*)DX, lddx,
                                           (const bf16*)W0, (const bf16*)W1, K, out0, out1, sj0, sk0, sj1, sk1, M, key0,
-                                          key1, thr0, thr1, ds0, ds1, mask_ld);
+                                          key1, thr0, thr1, ds0, ds1, mask_ld, mki);
   LIPA_CHECK_LAUNCH();
 }
 

@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void qk_norm_rope_fwd_k(const bf16* __restrict
 
 template <int D>
 __global__ __launch_bounds__(256) void qk_norm_rope_bwd_k(const bf16* __restrict__ dq, const bf16* __restrict__ dk,
-                                                          const bf16* __restrict__ qkv, const bf16* __restrict__ qw,
+                                                          const bf16* __restrict__ dv, const bf16* __restrict__ qkv, const bf16* __restrict__ qw,
                                                           const bf16* __restrict__ kw, const float* __restrict__ cosb,
                                                           const float* __restrict__ sinb, const float* __restrict__ rq,
                                                           const float* __restrict__ rk, bf16* __restrict__ dqkv, int T,
@@ -98,7 +98,21 @@ __global__ __launch_bounds__(256) void qk_norm_rope_bwd_k(const bf16* __restrict
   const int gid = blockIdx.x * 256 + threadIdx.x;
   const int row = gid / P, j = gid % P;
   const int nq = T * hq, nrows = nq + T * hkv;
-  if (row >= nrows) return;
+  if (row >= nrows) {
+    // rows past q and k: the v head rows of dqkv (dv passes through, or zeros without a dv)
+    const int vr = row - nrows;
+    if (vr >= T * hkv) return;
+    const int t = vr / hkv, h = vr % hkv;
+    bf16* o = dqkv + (size_t)t * (hq + 2 * hkv) * D + (hq + hkv + h) * D;
+    float va[4] = {0.f, 0.f, 0.f, 0.f}, vb[4] = {0.f, 0.f, 0.f, 0.f};
+    if (dv) {
+      ld4(dv + (size_t)vr * D + 4 * j, va);
+      ld4(dv + (size_t)vr * D + H + 4 * j, vb);
+    }
+    st4(o + 4 * j, va);
+    st4(o + H + 4 * j, vb);
+    return;
+  }
   const bool isq = row < nq;
   const int t = isq ? row / hq : (row - nq) / hkv;
   const int h = isq ? row % hq : (row - nq) % hkv;
@@ -188,14 +202,14 @@ void launch_qk_norm_rope_fwd(const void* qkv, const void* qw, const void* kw, co
   LIPA_CHECK_LAUNCH();
 }
 
-void launch_qk_norm_rope_bwd(const void* dq, const void* dk, const void* qkv, const void* qw, const void* kw,
-                             const float* cosb, const float* sinb, const float* rq, const float* rk, void* dqkv, int T,
-                             int hq, int hkv, int D, hipStream_t st) {
-  const long rows = (long)T * (hq + hkv);
+void launch_qk_norm_rope_bwd(const void* dq, const void* dk, const void* dv, const void* qkv, const void* qw,
+                             const void* kw, const float* cosb, const float* sinb, const float* rq, const float* rk,
+                             void* dqkv, int T, int hq, int hkv, int D, hipStream_t st) {
+  const long rows = (long)T * (hq + 2 * hkv);
   const long threads = rows * (D / 8);
   dim3 g((threads + 255) / 256), b(256);
 #define F(DD)                                                                                                  \
-  qk_norm_rope_bwd_k<DD><<<g, b, 0, st>>>((const bf16*)dq, (const bf16*)dk, (const bf16*)qkv, (const bf16*)qw, \
+  qk_norm_rope_bwd_k<DD><<<g, b, 0, st>>>((const bf16*)dq, (const bf16*)dk, (const bf16*)dv, (const bf16*)qkv, (const bf16*)qw, \
                                           (const bf16*)kw, cosb, sinb, rq, rk, (bf16*)dqkv, T, hq, hkv)
   switch (D) {
     case 32: F(32); break;

@@ -46,6 +46,9 @@ _APPLY = __import__("os").environ.get("LIPA_LORA_APPLY", "1") != "0"
 # timed in the running step; LIPA_LT=0: torch.addmm / torch.mm / torch.bmm
 _LT = __import__("os").environ.get("LIPA_LT", "1") != "0"
 _LT_MIN_M = 256
+# q_proj + v_proj with dropout: the forward's lora_proj2 stores the keep bits (1 bit per element and
+# branch) and lora_acc2 reads them instead of re-hashing; LIPA_LORA_KEEP_BITS=0: regenerate
+_KEEP_BITS = __import__("os").environ.get("LIPA_LORA_KEEP_BITS", "1") != "0"
 
 
 def _nf4_dequant_bf16(q: NF4Weight) -> torch.Tensor:
@@ -263,6 +266,7 @@ class _FusedLinearFn(torch.autograd.Function):
         dense = not isinstance(base, NF4Weight)
         xa_list, keys = [], []
         ext_a = ext_b = None
+        ctx.masks = None
         fast = bool(branches) and _fast_lora_ok(x, branches)
         need_xa = any(ctx.needs_input_grad[5:])     # (grad mode is off inside forward: ask autograd)
         # "apply" form: the base GEMM runs alone, then lora_apply adds xa_i·B_iᵀ into ONLY the adapters'
@@ -275,8 +279,12 @@ class _FusedLinearFn(torch.autograd.Function):
                 ps = [br.dropout if training else 0.0 for br in branches]
                 keys = [next_dropout_key() if p > 0 else None for p in ps]
                 a0, a1 = bf16_view(ab[0], x.dtype), bf16_view(ab[2], x.dtype)
+                # training with dropout on both: keep the masks' bits (2 bits / element of x) for lora_acc2
+                masks = (torch.empty(2, x.shape[0], x.shape[1] // 8, dtype=torch.uint8, device=x.device)
+                         if need_xa and all(k is not None for k in keys) and _KEEP_BITS else None)
                 xa2 = native().lora_proj2(x, a0, a1, None, True, ps[0], keys[0] or 0, branches[0].scaling,
-                                          ps[1], keys[1] or 0, branches[1].scaling)
+                                          ps[1], keys[1] or 0, branches[1].scaling, masks)
+                ctx.masks = masks
                 r0 = a0.shape[0]
                 xa_list = [xa2[:, :r0], xa2[:, r0:]]
             else:
@@ -305,7 +313,7 @@ class _FusedLinearFn(torch.autograd.Function):
                 a0, a1 = bf16_view(ab[0], x.dtype), bf16_view(ab[2], x.dtype)
                 rr = a0.shape[0] + a1.shape[0]
                 xa2 = native().lora_proj2(x, a0, a1, ext_a[:, :rr], need_xa, ps[0], pair_keys[0] or 0,
-                                          branches[0].scaling, ps[1], pair_keys[1] or 0, branches[1].scaling)
+                                          branches[0].scaling, ps[1], pair_keys[1] or 0, branches[1].scaling, None)
             for bi, (br, (a, b)) in enumerate(zip(branches, zip(ab[0::2], ab[1::2]))):
                 r = a.shape[0]
                 p = br.dropout if training else 0.0
@@ -416,7 +424,8 @@ class _FusedLinearFn(torch.autograd.Function):
             # both adapters' dA and their dx terms in ONE pass over x and dx (lora_acc2)
             (o0, ret0), (o1, ret1) = dest(0), dest(2)
             native().lora_acc2(g_list[0], g_list[1], x, dx, bf16_view(ab[0], dy.dtype), bf16_view(ab[2], dy.dtype),
-                               o0, o1, branches[0].dropout, ctx.keys[0], branches[1].dropout, ctx.keys[1])
+                               o0, o1, branches[0].dropout, ctx.keys[0], branches[1].dropout, ctx.keys[1], ctx.masks)
+            ctx.masks = None
             for i, (o, ret) in ((0, (o0, ret0)), (1, (o1, ret1))):
                 if ret:
                     grads_ab[2 * i] = o.to(ab[2 * i].dtype)

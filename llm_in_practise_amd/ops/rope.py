@@ -53,7 +53,7 @@ class _QKNormRopeFn(torch.autograd.Function):
         qkv, qw, kw, cos, sin, rq, rk = ctx.saved_tensors
         hq, hkv, d = ctx.dims
         dqkv = native().qk_norm_rope_bwd(dq.contiguous(), dk.contiguous(),
-                                         None if dv is None else dv, qkv, qw, kw, cos, sin, rq, rk, hq, hkv, d)
+                                         None if dv is None else dv.contiguous(), qkv, qw, kw, cos, sin, rq, rk, hq, hkv, d)
         return dqkv, None, None, None, None, None, None, None, None
 
 

@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
     ap.add_argument("--filter", default="")
+    ap.add_argument("--raw", action="store_true", help="also print every counter's mean per dispatch")
     a = ap.parse_args()
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     meta = {}
@@ -47,6 +48,8 @@ def main():
                 if c in m:
                     line.append(f"{c[3:].lower()}/wave_cyc={m[c] / m['SQ_WAVE_CYCLES']:.3f}")
         print(" | ".join(line))
+        if a.raw:
+            print("    " + "  ".join(f"{c}={v:.4g}" for c, v in sorted(m.items())))
 
 
 if __name__ == "__main__":

@@ -101,6 +101,10 @@ def test_qk_norm_rope(native_ext, hq, hkv, d):
     g = x.grad.clone()
     g[:, (hq + hkv) * d:] = dv.float()
     assert rel_err(dqkv, g) < 2e-2
+    assert torch.equal(dqkv[:, (hq + hkv) * d:], dv)          # v rows pass through exactly
+    d0 = native_ext.qk_norm_rope_bwd(dq, dk, None, qkv, qw, kw, cos, sin, rq, rk, hq, hkv, d)
+    assert torch.equal(d0[:, :(hq + hkv) * d], dqkv[:, :(hq + hkv) * d])
+    assert not d0[:, (hq + hkv) * d:].any()                    # no dv: zeros
 
 
 def test_rope_generic(native_ext):
@@ -567,7 +571,15 @@ def test_lora_two_branch_kernels(native_ext, M, K, p0, p1):
     xd0 = native_ext.dropout_fwd(x, p0, k0) if p0 > 0 else x
     xd1 = native_ext.dropout_fwd(x, p1, k1) if p1 > 0 else x
     outb = torch.zeros(M, 32, device=DEV, dtype=torch.bfloat16)
-    xa = native_ext.lora_proj2(x, a0, a1, outb[:, :16], True, p0, k0, 2.0, p1, k1, 0.5)
+    masks = torch.zeros(2, M, K // 8, device=DEV, dtype=torch.uint8)
+    xa = native_ext.lora_proj2(x, a0, a1, outb[:, :16], True, p0, k0, 2.0, p1, k1, 0.5, masks)
+    assert torch.equal(native_ext.lora_proj2(x, a0, a1, None, True, p0, k0, 2.0, p1, k1, 0.5, None), xa)
+    # the stored keep bits are the dropout masks (bit i of byte k/8 = element k + i kept)
+    bits = torch.arange(8, device=DEV, dtype=torch.uint8)
+    for mk, xd, p in ((masks[0], xd0, p0), (masks[1], xd1, p1)):
+        if p > 0:
+            keep = ((mk.unsqueeze(-1) >> bits) & 1).reshape(M, K).bool()
+            assert torch.equal(keep | (x == 0), (xd != 0) | (x == 0))
     ref = torch.cat([2.0 * xd0.float() @ a0.float().t(), 0.5 * xd1.float() @ a1.float().t()], 1)
     assert rel_err(xa, ref) < 1e-2 and rel_err(outb[:, :16], ref) < 1e-2 and outb[:, 16:].abs().sum() == 0
     g0 = torch.randn(M, 8, device=DEV)
@@ -576,7 +588,10 @@ def test_lora_two_branch_kernels(native_ext, M, K, p0, p1):
     dx0 = dx.float().clone()
     da0 = torch.ones(8, K, device=DEV)
     da1 = torch.zeros(8, K, device=DEV)
-    native_ext.lora_acc2(g0, g1, x, dx, a0, a1, da0, da1, p0, k0, p1, k1)
+    dx_b, da0_b, da1_b = dx.clone(), da0.clone(), da1.clone()
+    native_ext.lora_acc2(g0, g1, x, dx, a0, a1, da0, da1, p0, k0, p1, k1, None)
+    native_ext.lora_acc2(g0, g1, x, dx_b, a0, a1, da0_b, da1_b, p0, k0, p1, k1, masks)   # stored keep bits
+    assert torch.equal(dx_b, dx) and rel_err(da0_b, da0) < 1e-5 and rel_err(da1_b, da1) < 1e-5
     assert rel_err(da0 - 1, g0.t() @ xd0.float()) < 1e-2
     assert rel_err(da1, g1.t() @ xd1.float()) < 1e-2
     m0 = ((xd0 != 0) | (x == 0)).float() * (1 / (1 - p0)) if p0 > 0 else torch.ones_like(dx0)
