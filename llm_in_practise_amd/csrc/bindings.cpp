@@ -80,6 +80,10 @@ void launch_lora_proj2(const void*, int, const void*, const void*, int, int, int
 void launch_lora_acc2(const float*, int, int, const float*, int, int, const void*, int, void*, int, const void*,
                       const void*, int, float*, float*, int64_t, int64_t, int64_t, int64_t, int, uint64_t, float,
                       uint64_t, float, size_t, const uint8_t*, hipStream_t);
+void launch_lora_proj_pair(const void*, const void*, int, const void*, const void*, int, int, int, float*, float*, float,
+                           float, int, hipStream_t);
+void launch_lora_acc_pair(const float*, const float*, int, int, const void*, const void*, int, int, int, float*, float*,
+                          int, hipStream_t);
 void launch_lora_apply(void*, int, int, int, const float* const*, const int*, const void* const*, void* const*, const int*, const int*,
                        const int*, hipStream_t);
 void launch_lora_acc(const float*, int, int, const void*, int, void*, int, const void*, int, float*, int64_t, int64_t,
@@ -899,6 +903,47 @@ void lora_acc(Tensor g, Tensor x, int64_t c0, int64_t K, Tensor out, bool out_tr
   }
 }
 
+// backward of a q_proj + v_proj pair, one launch per product:
+//   g_i = s_i · dy[:, c0_i : c0_i + n_i] · B_i   (B_i passed as Bᵀ [r, n_i] bf16) -> fp32 [M, r]
+std::vector<Tensor> lora_proj_pair(Tensor dy, int64_t c0a, Tensor bta, double sa, int64_t c0b, Tensor btb, double sb) {
+  CHECK_BF16(dy);
+  CHECK_BF16(bta);
+  CHECK_BF16(btb);
+  TORCH_CHECK(dy.dim() == 2 && dy.stride(1) == 1 && dy.stride(0) % 8 == 0 && c0a % 8 == 0 && c0b % 8 == 0,
+              "lora_proj_pair: dy layout");
+  TORCH_CHECK(bta.is_contiguous() && btb.is_contiguous() && bta.size(0) == btb.size(0) && bta.size(0) <= 16 &&
+                  bta.size(1) % 512 == 0 && btb.size(1) % 512 == 0 && c0a + bta.size(1) <= dy.size(1) &&
+                  c0b + btb.size(1) <= dy.size(1),
+              "lora_proj_pair: Bt_i [r, n_i % 512] within dy");
+  const int M = dy.size(0), r = bta.size(0);
+  Tensor ga = at::empty({M, r}, dy.options().dtype(at::kFloat)), gb = at::empty({M, r}, dy.options().dtype(at::kFloat));
+  const char* base = (const char*)dy.data_ptr();
+  launch_lora_proj_pair(base + c0a * 2, base + c0b * 2, dy.stride(0), bta.data_ptr(), btb.data_ptr(), r, bta.size(1),
+                        btb.size(1), ga.data_ptr<float>(), gb.data_ptr<float>(), (float)sa, (float)sb, M, stream());
+  return {ga, gb};
+}
+
+//   dB_i [n_i, r] += (dy[:, c0_i : c0_i + n_i])ᵀ · xa_i   (xa_i fp32 [M, r], one row stride for both)
+void lora_acc_pair(Tensor xa, Tensor xb, Tensor dy, int64_t c0a, Tensor outa, int64_t c0b, Tensor outb) {
+  for (const Tensor* g : {&xa, &xb})
+    TORCH_CHECK(g->scalar_type() == at::kFloat && g->dim() == 2 && g->stride(1) == 1 && g->size(1) <= 8 &&
+                    g->stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(g->data_ptr()) % 16 == 0,
+                "lora_acc_pair: xa fp32 [M, r<=8], 16-B aligned rows");
+  TORCH_CHECK(xa.stride(0) == xb.stride(0) && xa.size(1) == xb.size(1), "lora_acc_pair: one layout for both xa");
+  CHECK_BF16(dy);
+  TORCH_CHECK(dy.stride(1) == 1 && dy.stride(0) % 8 == 0 && c0a % 8 == 0 && c0b % 8 == 0, "lora_acc_pair: dy layout");
+  const int M = dy.size(0), r = xa.size(1);
+  for (const Tensor* o : {&outa, &outb})
+    TORCH_CHECK(o->scalar_type() == at::kFloat && o->is_contiguous() && o->dim() == 2 && o->size(1) == r &&
+                    o->size(0) % 128 == 0, "lora_acc_pair: out fp32 [n_i % 128, r] contiguous");
+  TORCH_CHECK(xa.size(0) == M && xb.size(0) == M && c0a + outa.size(0) <= dy.size(1) &&
+                  c0b + outb.size(0) <= dy.size(1), "lora_acc_pair: shapes");
+  const char* base = (const char*)dy.data_ptr();
+  launch_lora_acc_pair(xa.data_ptr<float>(), xb.data_ptr<float>(), xa.stride(0), r, base + c0a * 2, base + c0b * 2,
+                       dy.stride(0), outa.size(0), outb.size(0), outa.data_ptr<float>(), outb.data_ptr<float>(), M,
+                       stream());
+}
+
 // ------------------------------------------------------------------ generation (K16, K17)
 // q [B, hq*d] bf16; kc/vc [B, Smax, hkv*d] bf16 contiguous; lens [B] int32 (valid keys per row);
 // max_len >= max(lens) bounds the split count without a host sync.
@@ -1132,6 +1177,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lora_acc", &lora_acc);
   m.def("lora_proj2", &lora_proj2);
   m.def("lora_acc2", &lora_acc2);
+  m.def("lora_proj_pair", &lora_proj_pair);
+  m.def("lora_acc_pair", &lora_acc_pair);
   m.def("lora_apply", &lora_apply);
   m.def("gemm_int4", &gemm_int4);
   m.def("gemv_w4", &gemv_w4);

@@ -31,13 +31,13 @@ namespace {
 // flight at once), partials meet in LDS and the result is written once (fp32 and/or bf16) — no
 // atomics, no zero-initialised output, no follow-up cast kernel.
 template <int NW, int RW>
-__global__ __launch_bounds__(NW * 64) void lora_proj_k(const bf16* __restrict__ X, int ldx, const bf16* __restrict__ W,
-                                                      int r, int K, float* __restrict__ outf, int ldof,
-                                                      bf16* __restrict__ outb, int ldob, int M, uint64_t key,
-                                                      uint32_t thr16, float dscale, float scale, size_t mask_ld) {
+__device__ __forceinline__ void lora_proj_body(const bf16* __restrict__ X, int ldx, const bf16* __restrict__ W, int r,
+                                               int K, float* __restrict__ outf, int ldof, bf16* __restrict__ outb,
+                                               int ldob, int M, uint64_t key, uint32_t thr16, float dscale,
+                                               float scale, size_t mask_ld, int bx) {
   __shared__ f32x4 red[NW][64];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int m0 = blockIdx.x * RW;
+  const int m0 = bx * RW;
   const bool rv = (lane & 15) < RW;   // RW = 8: MFMA rows 8..15 are zero padding (twice the workgroups)
   const int row = min(m0 + (lane & 15), M - 1);
   const int kw = K / NW;
@@ -87,6 +87,30 @@ __global__ __launch_bounds__(NW * 64) void lora_proj_k(const bf16* __restrict__ 
     if (outf) outf[(size_t)m * ldof + j] = v;
     if (outb) outb[(size_t)m * ldob + j] = (bf16)v;
   }
+}
+
+template <int NW, int RW>
+__global__ __launch_bounds__(NW * 64) void lora_proj_k(const bf16* __restrict__ X, int ldx, const bf16* __restrict__ W,
+                                                      int r, int K, float* __restrict__ outf, int ldof,
+                                                      bf16* __restrict__ outb, int ldob, int M, uint64_t key,
+                                                      uint32_t thr16, float dscale, float scale, size_t mask_ld) {
+  lora_proj_body<NW, RW>(X, ldx, W, r, K, outf, ldof, outb, ldob, M, key, thr16, dscale, scale, mask_ld, blockIdx.x);
+}
+
+// two independent projections of one launch (blockIdx.y = branch): the backward's s·dy_i·B_i of
+// q_proj and v_proj, each over its own column range of dy — one launch, one tail
+struct ProjPair {
+  const bf16* X[2];
+  const bf16* W[2];
+  float* out[2];
+  int K[2];
+  float scale[2];
+};
+template <int NW, int RW>
+__global__ __launch_bounds__(NW * 64) void lora_proj_pair_k(ProjPair p, int ldx, int r, int M) {
+  const int b = blockIdx.y;
+  lora_proj_body<NW, RW>(p.X[b], ldx, p.W[b], r, p.K[b], p.out[b], r, nullptr, 0, M, 0, 0u, 1.f, p.scale[b], 0,
+                         blockIdx.x);
 }
 
 // NRL row-lanes × 64 k-threads (8 consecutive k each); a chunk of ROWS rows is walked in passes of
@@ -211,17 +235,18 @@ __global__ __launch_bounds__(NRL * 64) void lora_acc_k(const float* __restrict__
 // partials meet in LDS and leave as one fp32 atomic per output per workgroup.  With DXU, each lane
 // also applies dx[m, k8..k8+7] += D(Σ_j G[m,j]·W[j,k]) to the rows it holds (VALU, R FMAs/element).
 template <int R, bool DXU, int SUB>
-__global__ __launch_bounds__(256) void lora_acc_mfma_k(const float* __restrict__ G, int ldg, int r,
-                                                      const bf16* __restrict__ X, int ldx, bf16* __restrict__ DX,
-                                                      int lddx, const bf16* __restrict__ W, int K,
-                                                      float* __restrict__ out, int64_t sj, int64_t sk, int M,
-                                                      uint64_t key, uint32_t thr16, float dscale, size_t mask_ld) {
+__device__ __forceinline__ void lora_acc_mfma_body(const float* __restrict__ G, int ldg, int r,
+                                                   const bf16* __restrict__ X, int ldx, bf16* __restrict__ DX,
+                                                   int lddx, const bf16* __restrict__ W, int K,
+                                                   float* __restrict__ out, int64_t sj, int64_t sk, int M,
+                                                   uint64_t key, uint32_t thr16, float dscale, size_t mask_ld, int bx,
+                                                   int by) {
   __shared__ float red[4][64][33];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int q = lane >> 4, n = lane & 15;
-  const int kb = blockIdx.x * 128;
+  const int kb = bx * 128;
   const int k8 = kb + 8 * n;
-  const int mw = blockIdx.y * (128 * SUB) + w * (32 * SUB);
+  const int mw = by * (128 * SUB) + w * (32 * SUB);
   bf16x8 wv[DXU ? R : 1];
   if constexpr (DXU) {
 #pragma unroll
@@ -303,6 +328,33 @@ __global__ __launch_bounds__(256) void lora_acc_mfma_k(const float* __restrict__
     const float v = (red[0][ln][slot] + red[1][ln][slot] + red[2][ln][slot] + red[3][ln][slot]) * ds;
     atomicAdd(out + j * sj + (int64_t)(kb + kk) * sk, v);
   }
+}
+
+template <int R, bool DXU, int SUB>
+__global__ __launch_bounds__(256) void lora_acc_mfma_k(const float* __restrict__ G, int ldg, int r,
+                                                      const bf16* __restrict__ X, int ldx, bf16* __restrict__ DX,
+                                                      int lddx, const bf16* __restrict__ W, int K,
+                                                      float* __restrict__ out, int64_t sj, int64_t sk, int M,
+                                                      uint64_t key, uint32_t thr16, float dscale, size_t mask_ld) {
+  lora_acc_mfma_body<R, DXU, SUB>(G, ldg, r, X, ldx, DX, lddx, W, K, out, sj, sk, M, key, thr16, dscale, mask_ld,
+                                  blockIdx.x, blockIdx.y);
+}
+
+// dB_i [n_i, r] += (dy[:, c0_i : c0_i + n_i])ᵀ · xa_i for two branches in one launch (the k-blocks of
+// branch 1 follow those of branch 0 along blockIdx.x)
+struct AccPair {
+  const float* G[2];
+  const bf16* X[2];
+  float* out[2];
+  int K[2];
+  int nblk0;
+};
+template <int SUB>
+__global__ __launch_bounds__(256) void lora_acc_pair_k(AccPair a, int ldg, int r, int ldx, int M) {
+  const int b = (int)blockIdx.x >= a.nblk0;
+  const int bx = blockIdx.x - (b ? a.nblk0 : 0);
+  lora_acc_mfma_body<8, false, SUB>(a.G[b], ldg, r, a.X[b], ldx, nullptr, 0, nullptr, a.K[b], a.out[b], 1, r, M, 0,
+                                    0u, 1.f, 0, bx, blockIdx.y);
 }
 
 // ---- two branches sharing one input (q_proj + v_proj of a fused q|k|v projection) -------------
@@ -753,5 +805,28 @@ void launch_lora_apply(void* Y, int ldy, int M, int nb, const float* const* xa, 
     lora_apply_k<8><<<grid, 256, 0, st>>>(static_cast<bf16*>(Y), ldy, M, a);
   else
     lora_apply_k<16><<<grid, 256, 0, st>>>(static_cast<bf16*>(Y), ldy, M, a);
+  LIPA_CHECK_LAUNCH();
+}
+
+// the backward's two-branch projections g_i = s_i·dy[:, c0_i : c0_i + K_i]·B_i (fp32 [M, r]), B_i given as
+// Bᵀ [r, K_i]; both branches have the same rank r
+void launch_lora_proj_pair(const void* X0, const void* X1, int ldx, const void* W0, const void* W1, int r, int K0,
+                           int K1, float* out0, float* out1, float s0, float s1, int M, hipStream_t st) {
+  ProjPair p{{(const bf16*)X0, (const bf16*)X1}, {(const bf16*)W0, (const bf16*)W1}, {out0, out1}, {K0, K1}, {s0, s1}};
+  const int rw = M < 4096 ? 8 : 16;
+  dim3 grid((M + rw - 1) / rw, 2);
+  if (rw == 8)
+    lora_proj_pair_k<16, 8><<<grid, 1024, 0, st>>>(p, ldx, r, M);
+  else
+    lora_proj_pair_k<16, 16><<<grid, 1024, 0, st>>>(p, ldx, r, M);
+  LIPA_CHECK_LAUNCH();
+}
+
+// dB_i [K_i, r] (row-major, i.e. out[k * r + j]) += Σ_m X_i[m, k]·G_i[m, j] for two branches, r <= 8
+void launch_lora_acc_pair(const float* G0, const float* G1, int ldg, int r, const void* X0, const void* X1, int ldx,
+                          int K0, int K1, float* out0, float* out1, int M, hipStream_t st) {
+  AccPair a{{G0, G1}, {(const bf16*)X0, (const bf16*)X1}, {out0, out1}, {K0, K1}, K0 / 128};
+  dim3 g(K0 / 128 + K1 / 128, (M + 127) / 128);
+  lora_acc_pair_k<1><<<g, 256, 0, st>>>(a, ldg, r, ldx, M);
   LIPA_CHECK_LAUNCH();
 }

@@ -49,6 +49,8 @@ _LT_MIN_M = 256
 # q_proj + v_proj with dropout: the forward's lora_proj2 stores the keep bits (1 bit per element and
 # branch) and lora_acc2 reads them instead of re-hashing; LIPA_LORA_KEEP_BITS=0: regenerate
 _KEEP_BITS = __import__("os").environ.get("LIPA_LORA_KEEP_BITS", "1") != "0"
+# two-branch backward launches (lora_proj_pair / lora_acc_pair); LIPA_LORA_PAIR_BWD=0: per-branch
+_PAIR_BWD = __import__("os").environ.get("LIPA_LORA_PAIR_BWD", "1") != "0"
 
 
 def _nf4_dequant_bf16(q: NF4Weight) -> torch.Tensor:
@@ -386,7 +388,33 @@ class _FusedLinearFn(torch.autograd.Function):
                 return gr, False
             return torch.zeros(prm.shape, dtype=torch.float32, device=dy.device), True
 
-        for i, br in enumerate(branches):
+        # q_proj + v_proj: both adapters' s·dy_i·B_i in one launch, both dB_i in another
+        pair_g = (fast and nb == 2 and ctx.bts is not None and ctx.bts[0].shape[0] == ctx.bts[1].shape[0]
+                  and all(bt.shape[1] % 512 == 0 for bt in ctx.bts) and _PAIR_BWD)
+        if pair_g:
+            g_list = list(native().lora_proj_pair(dy, branches[0].c0, ctx.bts[0], branches[0].scaling,
+                                                  branches[1].c0, ctx.bts[1], branches[1].scaling))
+            xs = xa_list
+            if (ctx.needs_input_grad[6] and ctx.needs_input_grad[8] and not deterministic() and xs[0] is not None
+                    and xs[1] is not None and xs[0].stride(0) == xs[1].stride(0) and xs[0].shape[1] <= 8
+                    and all((br.c1 - br.c0) % 128 == 0 for br in branches)):
+                (o0, ret0), (o1, ret1) = dest(1), dest(3)
+                native().lora_acc_pair(xs[0], xs[1], dy, branches[0].c0, o0, branches[1].c0, o1)
+                for i, (o, ret) in ((0, (o0, ret0)), (1, (o1, ret1))):
+                    if ret:
+                        grads_ab[2 * i + 1] = o.to(ab[2 * i + 1].dtype)
+                    else:
+                        _notify_grad_ready(ctx.ab_refs[2 * i + 1])
+            else:
+                for i, br in enumerate(branches):
+                    if ctx.needs_input_grad[5 + 2 * i + 1]:
+                        out, ret = dest(2 * i + 1)
+                        native().lora_acc(xa_list[i], dy, br.c0, br.c1 - br.c0, out, True, None, None, 0.0, 0,
+                                          deterministic())
+                        grads_ab[2 * i + 1] = out.to(ab[2 * i + 1].dtype) if ret else None
+                        if not ret:
+                            _notify_grad_ready(ctx.ab_refs[2 * i + 1])
+        for i, br in enumerate(branches if not pair_g else ()):
             a, b = ab[2 * i], ab[2 * i + 1]
             n_i = br.c1 - br.c0
             if fast:

@@ -674,3 +674,23 @@ def test_lt_dx_split(native_ext, split):
         dx = native_ext.lt_dx(dy, w, split)
         err = (dx.float() - want).abs().max().item()
         assert err < 0.03 * want.abs().max().item(), err
+
+
+@pytest.mark.parametrize("M", [2048, 300])
+def test_lora_backward_pair_kernels(native_ext, M):
+    """lora_proj_pair (s_i·dy_i·B_i for two column blocks of dy) and lora_acc_pair (dB_i += dy_iᵀ·xa_i)
+    vs fp32."""
+    torch.manual_seed(4)
+    N, r = 6144, 8
+    dy = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    specs = [(0, 4096, 2.0), (5120, 1024, 0.5)]
+    bts = [(0.05 * torch.randn(r, n, device=DEV)).to(torch.bfloat16) for _, n, _ in specs]
+    ga, gb = native_ext.lora_proj_pair(dy, specs[0][0], bts[0], specs[0][2], specs[1][0], bts[1], specs[1][2])
+    for g, (c0, n, s), bt in zip((ga, gb), specs, bts):
+        assert rel_err(g, s * dy[:, c0:c0 + n].float() @ bt.float().t()) < 1e-2
+    xa2 = torch.randn(M, 16, device=DEV)
+    xs = [xa2[:, :8], xa2[:, 8:]]
+    outs = [torch.full((n, r), 0.25, device=DEV) for _, n, _ in specs]
+    native_ext.lora_acc_pair(xs[0], xs[1], dy, specs[0][0], outs[0], specs[1][0], outs[1])
+    for o, (c0, n, _), xa in zip(outs, specs, xs):
+        assert rel_err(o - 0.25, dy[:, c0:c0 + n].float().t() @ xa) < 1e-2
