@@ -243,7 +243,7 @@ void launch_gemm_w4_skinny(const void* X, int ldx, const uint8_t* codes, const f
   dim3 grid((N + SK_NB - 1) / SK_NB, S);
   // MT >= 2 runs one workgroup per CU (a 96 KB dynamic-LDS reservation; the kernel uses no LDS):
   // measured on MI355X (ROCm 7.2), two co-resident workgroups of the MT >= 2 code returned
-  // nondeterministically wrong fragments (scripts/dbg_w4.py); one per CU is exact.
+  // nondeterministically wrong fragments (scripts/experiments/dbg_w4.py); one per CU is exact.
 #define L(MT) gemm_w4_skinny_k<MT><<<grid, 256, (MT) >= 2 ? 98304 : 0, st>>>((const bf16*)X, ldx, codes, scales, biases, \
                                                                           gs, part, M, N, K, kc)
   if (M <= 16) L(1);

@@ -33,6 +33,7 @@ from ..ops.loss import fused_linear_cross_entropy, shift_labels
 from ..ops.norm import RMSNorm, rms_norm, rms_norm_residual
 from ..ops.rope import apply_rope, qk_norm_rope
 from ..parallel.tensor_parallel import tp_all_reduce
+from ..peft.lora import base_of
 from .common import CausalLMOutput, FusedProjection, KVCache, PackedPrefill, can_fuse, project
 
 
@@ -159,7 +160,7 @@ class Qwen3Attention(nn.Module):
         self._qkv = FusedProjection(mods) if can_fuse(mods) else None
 
     def forward(self, x, cos, sin, B, S, residual=None, cache: KVCache | None = None, start: int = 0,
-                kv_lens=None):
+                kv_lens=None, before_attn=None):
         tr = self.training
         qkv = project([self.q_proj, self.k_proj, self.v_proj], x, None, tr, self._qkv)
         if self.q_norm is not None:
@@ -172,6 +173,8 @@ class Qwen3Attention(nn.Module):
             k = apply_rope(qkv[:, nq:nq + nk].reshape(T, self.hkv, self.d), cos, sin).reshape(T, nk)
             v = qkv[:, nq + nk:]
         if cache is None:
+            if before_attn is not None:
+                before_attn()
             o = flash_attention(q, k, v, B, S, self.hq, self.hkv, self.d, causal=True, kv_lens=kv_lens)
         elif isinstance(cache, PackedPrefill):
             o = cache.attend(self.layer_idx, q, k, v, self.hq, self.hkv, self.d, flash_attention)
@@ -218,6 +221,11 @@ class Qwen3MLP(nn.Module):
         return tp_all_reduce(y, self.tp_group)
 
 
+def _overlap_on() -> bool:
+    from ..ops.linear import _OVERLAP
+    return bool(_OVERLAP)
+
+
 class Qwen3DecoderLayer(nn.Module):
     def __init__(self, cfg: Qwen3Config, layer_idx: int):
         super().__init__()
@@ -226,9 +234,27 @@ class Qwen3DecoderLayer(nn.Module):
         self.input_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
         self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
 
+    def _prefetch(self):
+        """NF4 training step: expand this layer's o / gate|up / down weights on a side stream while
+        the attention forward (latency-bound, light on HBM) runs (ops/linear.py prefetch_dequant)."""
+        from ..ops.linear import _OVERLAP, prefetch_dequant
+        pick = {"o": [self.self_attn.o_proj], "gu": [self.mlp.gate_proj, self.mlp.up_proj],
+                "down": [self.mlp.down_proj]}
+        bases = []
+        for key in _OVERLAP:
+            mods = pick.get(key, [])
+            if key == "gu" and self.mlp._gu is not None:
+                bases.append(self.mlp._gu.base)
+            else:
+                bases += [base_of(m)[0] for m in mods]
+        prefetch_dequant(bases)
+
     def forward(self, x, cos, sin, B, S, cache=None, start=0, kv_lens=None):
         xn, skip = rms_norm_residual(x, self.input_layernorm.weight, self.input_layernorm.eps)
-        h = self.self_attn(xn, cos, sin, B, S, residual=skip, cache=cache, start=start, kv_lens=kv_lens)
+        pre = self._prefetch if (_overlap_on() and self.training and cache is None and torch.is_grad_enabled()) \
+            else None
+        h = self.self_attn(xn, cos, sin, B, S, residual=skip, cache=cache, start=start, kv_lens=kv_lens,
+                           before_attn=pre)
         hn, skip = rms_norm_residual(h, self.post_attention_layernorm.weight, self.post_attention_layernorm.eps)
         return self.mlp(hn, residual=skip)
 

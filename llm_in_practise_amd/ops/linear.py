@@ -54,8 +54,48 @@ _PAIR_BWD = __import__("os").environ.get("LIPA_LORA_PAIR_BWD", "1") != "0"
 
 
 def _nf4_dequant_bf16(q: NF4Weight) -> torch.Tensor:
+    pre = _PREFETCHED.pop(id(q), None)
+    if pre is not None:                       # expanded on the side stream (prefetch_dequant)
+        t, ev = pre
+        cur = torch.cuda.current_stream(t.device)
+        cur.wait_event(ev)
+        t.record_stream(cur)
+        return t
     n, k = q.shape
     return native().nf4_dequant_fast(q.codes, q.gemv_scales(), n, k)
+
+
+# NF4 weights expanded ahead of use on a side stream: {id(NF4Weight): (bf16 tensor, ready event)}
+_PREFETCHED: dict = {}
+_SIDE: dict = {}
+# which of a decoder layer's projections prefetch_dequant expands while attention runs
+# (LIPA_NF4_OVERLAP: comma list of o,gu,down; empty = off)
+_OVERLAP = tuple(t for t in __import__("os").environ.get("LIPA_NF4_OVERLAP", "").split(",") if t)
+
+
+def prefetch_dequant(bases, after: torch.Tensor | None = None):
+    """Expand ``bases`` (NF4Weights) to bf16 on a side stream that starts once the current stream
+    reaches this point: the memory-bound expansion then runs beside a latency-bound kernel (the
+    attention forward) instead of serially before its GEMM.  The GEMM's forward picks the copy up
+    (and waits for its event) in :func:`_nf4_dequant_bf16`."""
+    bases = [b for b in bases if isinstance(b, NF4Weight) and b.kernel_ok()]
+    if not bases or _NF4_MODE != "dequant" or not bases[0].codes.is_cuda:
+        return
+    dev = bases[0].codes.device
+    side = _SIDE.get(dev)
+    if side is None:
+        side = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    cur = torch.cuda.current_stream(dev)
+    start = torch.cuda.Event()
+    start.record(cur)
+    side.wait_event(start)
+    with torch.cuda.stream(side):
+        for b in bases:
+            n, k = b.shape
+            t = native().nf4_dequant_fast(b.codes, b.gemv_scales(), n, k)
+            ev = torch.cuda.Event()
+            ev.record(side)
+            _PREFETCHED[id(b)] = (t, ev)
 
 
 @dataclasses.dataclass

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box A/B of one Python source file: alternates bench runs with $1 (old copy) swapped in for $2.
-# usage: scripts/gpu_ab_env_file.sh <old_copy> <tracked_file>
+# usage: scripts/experiments/gpu_ab_env_file.sh <old_copy> <tracked_file>
 set -u
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box A/B of the NF4 GEMM generations: gemm tests, then alternating full-bench runs.
-# usage: scripts/gpu_ab_impl.sh <impl> <impl> ...
+# usage: scripts/experiments/gpu_ab_impl.sh <impl> <impl> ...
 set -u
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out

@@ -1,5 +1,5 @@
 #!/bin/bash
-# attention numerics + microbenchmark + short bench.  usage: scripts/gpu_attn.sh
+# attention numerics + microbenchmark + short bench.  usage: scripts/experiments/gpu_attn.sh
 set -u
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0

@@ -11,4 +11,4 @@ tail -2 gpurun_out/dec2_tests.log
 timeout -k 10 300 python3 scripts/bench_decode.py --model qwen3-8b --batches 8 64 128 256 --ctx 512 --max-len 1024 \
   > gpurun_out/decode_big2.log 2>&1 || { tail -20 gpurun_out/decode_big2.log; exit 1; }
 grep batch gpurun_out/decode_big2.log
-bash scripts/gpu_serve_ref.sh
+bash scripts/experiments/gpu_serve_ref.sh

@@ -1,5 +1,5 @@
 #!/bin/bash
-# NF4 GEMM numerics + A/B microbenchmark.  usage: scripts/gpu_gemm3.sh <impls...>
+# NF4 GEMM numerics + A/B microbenchmark.  usage: scripts/experiments/gpu_gemm3.sh <impls...>
 set -u
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC counters of the GEMM microbench (own run: --pmc only, no trace domains).
-# usage: scripts/gpu_pmc_gemm.sh <tag> [bench_gemm args]
+# usage: scripts/experiments/gpu_pmc_gemm.sh <tag> [bench_gemm args]
 set -u
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
