@@ -41,7 +41,7 @@ void launch_nf4_quantize(const void*, uint8_t*, float*, size_t, hipStream_t);
 void launch_nf4_dequant2(const uint8_t*, const float*, void*, size_t, hipStream_t);
 int skinny_splits(int, int);
 bool lt_gemm(bool, bool, long, long, long, const void*, long, const void*, long, const void*, void*, long, int, long,
-             long, long, void*, size_t, hipStream_t);
+             long, long, void*, size_t, hipStream_t, bool);
 void lt_reset();
 void launch_sum_slices(const void*, void*, int, size_t, size_t, hipStream_t);
 void launch_gemm_skinny(const void*, int, const void*, const void*, void*, float*, int, int, int, int, hipStream_t);
@@ -361,7 +361,7 @@ static void* lt_workspace(size_t& bytes) {
 }
 
 // y = x·wᵀ (+ residual): x [M, K] (unit column stride), w [N, K] contiguous bf16
-Tensor lt_linear(Tensor x, Tensor w, optional<Tensor> residual) {
+Tensor lt_linear(Tensor x, Tensor w, optional<Tensor> residual, bool tune) {
   CHECK_CUDA(x);
   CHECK_BF16(x);
   CHECK_BF16(w);
@@ -379,14 +379,14 @@ Tensor lt_linear(Tensor x, Tensor w, optional<Tensor> residual) {
   size_t wsb;
   void* ws = lt_workspace(wsb);
   if (!lt_gemm(true, false, N, M, K, w.data_ptr(), K, x.data_ptr(), x.stride(0), cp, out.data_ptr(), N, 1, 0, 0, 0,
-               ws, wsb, stream()))
+               ws, wsb, stream(), tune))
     return cp ? at::addmm(*residual, x, w.t()) : at::mm(x, w.t());
   return out;
 }
 
 // dx = dy·w: dy [M, N] contiguous, w [N, K] contiguous; split > 1: K-slices of the reduction dim
 // as one strided-batched GEMM into bf16 partials + an fp32 slice sum
-Tensor lt_dx(Tensor dy, Tensor w, int64_t split) {
+Tensor lt_dx(Tensor dy, Tensor w, int64_t split, bool tune) {
   CHECK_CUDA(dy);
   CHECK_BF16(dy);
   CHECK_BF16(w);
@@ -401,14 +401,14 @@ Tensor lt_dx(Tensor dy, Tensor w, int64_t split) {
   Tensor out = at::empty({M, K}, dy.options());
   if (split == 1) {
     if (!lt_gemm(false, false, K, M, N, w.data_ptr(), K, dy.data_ptr(), N, nullptr, out.data_ptr(), K, 1, 0, 0, 0, ws,
-                 wsb, stream()))
+                 wsb, stream(), tune))
       return at::mm(dy, w);
     return out;
   }
   const int64_t Ns = N / split;
   Tensor part = at::empty({split, M, K}, dy.options());
   if (!lt_gemm(false, false, K, M, Ns, w.data_ptr(), K, dy.data_ptr(), N, nullptr, part.data_ptr(), K, (int)split,
-               Ns * K, Ns, M * K, ws, wsb, stream()))
+               Ns * K, Ns, M * K, ws, wsb, stream(), tune))
     return at::mm(dy, w);
   launch_sum_slices(part.data_ptr(), out.data_ptr(), (int)split, (size_t)(M * K), (size_t)(M * K), stream());
   return out;

@@ -104,10 +104,11 @@ bool make_plan(Plan& p, bool ta, bool tb, long m, long n, long k, long lda, long
 }  // namespace
 
 // D = op(A)·op(B) (+ C when C != nullptr; beta = 1), column-major, bf16 in/out, fp32 accumulate.
+// tune: time the heuristic's top candidates on the first calls of the shape and keep the fastest.
 // Returns false when hipBLASLt has no plan for the problem (the caller falls back).
 bool lt_gemm(bool ta, bool tb, long m, long n, long k, const void* A, long lda, const void* B, long ldb,
              const void* C, void* D, long ldc, int batch, long sa, long sb, long sc, void* ws, size_t ws_bytes,
-             hipStream_t st) {
+             hipStream_t st, bool tune) {
   Plan* p;
   {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -124,8 +125,10 @@ bool lt_gemm(bool ta, bool tb, long m, long n, long k, const void* A, long lda, 
   const float alpha = 1.f, beta = C ? 1.f : 0.f;
   int idx = p->chosen;
   bool timed = false;
-  if (idx < 0 && getenv("LIPA_DETERMINISTIC") && atoi(getenv("LIPA_DETERMINISTIC"))) {
-    idx = 0;  // reproducible runs: the heuristic's first choice, no candidate rotation
+  if (idx < 0 && (!tune || (getenv("LIPA_DETERMINISTIC") && atoi(getenv("LIPA_DETERMINISTIC"))))) {
+    // reproducible runs, or a shape called once per step (timing would stall the host behind the
+    // device for a dozen steps): the heuristic's first choice, no candidate rotation
+    idx = 0;
   } else if (idx < 0) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     hipStreamIsCapturing(st, &cs);

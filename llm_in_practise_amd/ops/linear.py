@@ -145,7 +145,7 @@ def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
         return y if ext_a is None else y.addmm_(ext_a, ext_b.t())
     if _LT and M >= _LT_MIN_M and x.is_cuda and x.dtype == torch.bfloat16 and x.stride(1) == 1 \
             and not _NATIVE_DENSE:
-        y = native().lt_linear(x, base.contiguous(), None if residual is None else residual.contiguous())
+        y = native().lt_linear(x, base.contiguous(), None if residual is None else residual.contiguous(), True)
         return y if ext_a is None else y.addmm_(ext_a, ext_b.t())
     if not _NATIVE_DENSE:
         # a bf16 base is a plain library GEMM: hipBLASLt's tuned kernels run it at 1.1-1.5
@@ -160,7 +160,7 @@ def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
     return native().gemm_bf16(x, base, ext_a, ext_b, residual)
 
 
-def _dense_dx(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+def _dense_dx(dy: torch.Tensor, w: torch.Tensor, tune: bool = True) -> torch.Tensor:
     """dX = dY·W for a bf16 [N, K] weight.  A long reduction into a small output (gate|up:
     N = 24576 → K = 4096 at M = 2048 is 128 output tiles for 256 CUs) leaves half the chip idle
     in hipBLASLt's non-split-K kernel; four K-slices as one batched GEMM + an fp32-accumulated
@@ -169,7 +169,7 @@ def _dense_dx(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     K = w.shape[1]
     split = 4 if N % 4 == 0 and N >= 4 * K and M >= 256 and (M // 256) * max(1, K // 256) < 256 else 1
     if _LT and M >= _LT_MIN_M and dy.is_cuda and dy.dtype == torch.bfloat16 and K % 8 == 0:
-        return native().lt_dx(dy.contiguous(), w.contiguous(), split)
+        return native().lt_dx(dy.contiguous(), w.contiguous(), split, tune)
     if split > 1:
         s = split
         return torch.bmm(dy.view(M, s, N // s).transpose(0, 1), w.view(s, N // s, K)).sum(0)

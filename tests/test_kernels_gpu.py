@@ -658,7 +658,7 @@ def test_lt_linear(native_ext, M, N, K, res):
     r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16) if res else None
     want = x.float() @ w.float().t() + (r.float() if res else 0)
     for _ in range(20):          # candidate rotation (4 x 3 timed calls), then the chosen kernel
-        y = native_ext.lt_linear(x, w, r)
+        y = native_ext.lt_linear(x, w, r, True)
         assert (y.float() - want).abs().max().item() < 0.05 * want.abs().max().item()
     if res:
         assert r is not y
@@ -671,7 +671,7 @@ def test_lt_dx_split(native_ext, split):
     w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / N ** 0.5
     want = dy.float() @ w.float()
     for _ in range(16):
-        dx = native_ext.lt_dx(dy, w, split)
+        dx = native_ext.lt_dx(dy, w, split, True)
         err = (dx.float() - want).abs().max().item()
         assert err < 0.03 * want.abs().max().item(), err
 
