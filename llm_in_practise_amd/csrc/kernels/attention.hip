@@ -73,6 +73,34 @@ __device__ __forceinline__ void xcd_grid3(int& i0, int& i1, int& i2) {
   i2 = id / (n0 * n1);
 }
 
+// Causal grids (i0 = query block, work grows with it): the same XCD grouping, but inside each run of
+// n0·G consecutive logical blocks (G (head, batch) pairs — one XCD's share at the training shapes)
+// the block index varies SLOWEST, so every XCD dispatches all its heavy blocks before any light one
+// (longest-first: the light blocks then fill the slots the heavy ones leave).  LIPA_ATTN_LPT=0: the
+// plain xcd_grid3 order.
+__device__ __forceinline__ void xcd_grid3_lpt(int& i0, int& i1, int& i2, int lpt) {
+  if (!lpt) {
+    xcd_grid3(i0, i1, i2);
+    return;
+  }
+  const int n0 = gridDim.x, n1 = gridDim.y;
+  const int npair = n1 * gridDim.z;
+  const int nwg = n0 * npair;
+  const int id = xcd_remap(blockIdx.x + n0 * (blockIdx.y + n1 * blockIdx.z), nwg);
+  const int G = max(1, min(npair, 128 / n0));   // pairs per run
+  const int run = id / (n0 * G), t = id % (n0 * G);
+  const int g = min(G, npair - run * G);       // the last run may hold fewer pairs
+  i0 = t / g;
+  const int pr = run * G + t % g;
+  i1 = pr % n1;
+  i2 = pr / n1;
+}
+
+static int attn_lpt() {
+  static const int v = [] { const char* e = getenv("LIPA_ATTN_LPT"); return e ? (atoi(e) != 0) : 1; }();
+  return v;
+}
+
 // ============================================================================ forward
 // Sq queries per batch row attend to Skv keys (K/V rows of batch b start at b·kv_rows: a KV cache
 // may be allocated longer than it is filled).  Query i of batch b sits at absolute position
@@ -97,7 +125,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const bf16* __restrict__ Q,
   constexpr int QB = 64 * QT;       // queries per workgroup (QT 16-query subtiles per wave)
   const int nqb = (Sq + QB - 1) / QB;
   int i0, h, b;
-  xcd_grid3(i0, h, b);
+  xcd_grid3_lpt(i0, h, b, causal >> 1);   // causal bit 1: longest-first order
   const int qb = nqb - 1 - i0;  // heavy (late, causal) blocks first
   const int hk = h / (hq / hkv);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
@@ -300,7 +328,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(const bf16* __restrict__
 
   const int nqb = (S + 63) / 64;
   int i0, h, b;
-  xcd_grid3(i0, h, b);
+  xcd_grid3_lpt(i0, h, b, causal >> 1);   // causal bit 1: longest-first order
   const int qb = nqb - 1 - i0;  // heavy (late, causal) blocks first
   const int hk = h / (hq / hkv);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
@@ -657,7 +685,7 @@ void launch_attn_fwd(const void* q, const void* k, const void* v, int ldq, int l
 #define FWD(PFV, QTV)                                                                                      \
   LIPA_ATTN_D(D, attn_fwd_k<DD, PFV, QTV><<<grid, blk, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,  \
                                                            ldq, ldk, ldv, kv_lens, q_offs, (bf16*)o, lse, Sq, Skv, \
-                                                           kv_rows, hq, hkv, causal, sl2, dp))
+                                                           kv_rows, hq, hkv, causal ? 1 | (attn_lpt() << 1) : 0, sl2, dp))
   if (qt == 1) {
     FWD(1, 1);
   } else {
@@ -678,7 +706,7 @@ void launch_attn_bwd(const void* dout, const void* q, const void* k, const void*
 #define RUN(DD, PFQ, PFKV)                                                                                        \
   attn_bwd_dq_k<DD, PFQ><<<gq, blk, 0, st>>>((const bf16*)dout, (const bf16*)o, (const bf16*)q, (const bf16*)k,    \
                                              (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dq, S, hq,  \
-                                             hkv, causal, scale, sl2, dp);                                          \
+                                             hkv, causal ? 1 | (attn_lpt() << 1) : 0, scale, sl2, dp);              \
   if ((hq / hkv) % 2 == 0)                                                                                       \
     attn_bwd_dkv_k<DD, 2, PFKV><<<gkv, 512, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k,            \
                                                      (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, \
