@@ -292,12 +292,134 @@ struct ChTag {};
     else { fprintf(stderr, "norm: N=%d too large\n", (int)(N)); }  \
   } while (0)
 
+
+// ---- split rows (bf16, no weight gradient): WPR waves share one row, so a 2048-row activation is
+// 4096 waves (4 per SIMD) with half the registers each — the single-wave-per-row form leaves the
+// memory latency of its one round trip exposed at 2 waves per SIMD.  Partial sums meet in LDS.
+template <int CH, int WPR>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_split_k(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                           bf16* __restrict__ y, float* __restrict__ rstd_out, int M,
+                                                           int N, float eps) {
+  constexpr int RPB = 4 / WPR;  // rows per workgroup
+  __shared__ float part[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int row = blockIdx.x * RPB + wid / WPR, pw = wid % WPR;
+  const bool valid = row < M;
+  const bf16* xr = x + (size_t)(valid ? row : 0) * N;
+  float v[CH][8];
+  bf16x8 wb[CH];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = ((c * WPR + pw) * 64 + lane) * 8;
+    load8(xr + col, v[c]);
+    if (w) wb[c] = *reinterpret_cast<const bf16x8*>(w + col);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ss += v[c][i] * v[c][i];
+  }
+  ss = wave_sum(ss);
+  if (lane == 0) part[wid] = ss;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int p = 0; p < WPR; ++p) tot += part[(wid / WPR) * WPR + p];
+  if (!valid) return;
+  const float r = rsqrtf(tot / N + eps);
+  if (lane == 0 && pw == 0) rstd_out[row] = r;
+  bf16* yr = y + (size_t)row * N;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = ((c * WPR + pw) * 64 + lane) * 8;
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = v[c][i] * r * (w ? (float)wb[c][i] : 1.f);
+    store8(yr + col, o);
+  }
+}
+
+template <int CH, int WPR>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_split_k(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                           const bf16* __restrict__ w, const float* __restrict__ rstd,
+                                                           bf16* __restrict__ dx, int M, int N,
+                                                           const bf16* __restrict__ dres) {
+  constexpr int RPB = 4 / WPR;
+  __shared__ float part[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int row = blockIdx.x * RPB + wid / WPR, pw = wid % WPR;
+  const bool valid = row < M;
+  const size_t ro = (size_t)(valid ? row : 0) * N;
+  const float r = rstd[valid ? row : 0];
+  float xv[CH][8], gv[CH][8];
+  bf16x8 rb[CH], wb[CH];
+  float dot = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = ((c * WPR + pw) * 64 + lane) * 8;
+    load8(x + ro + col, xv[c]);
+    load8(dy + ro + col, gv[c]);
+    if (dres) rb[c] = *reinterpret_cast<const bf16x8*>(dres + ro + col);
+    if (w) wb[c] = *reinterpret_cast<const bf16x8*>(w + col);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      xv[c][i] *= r;
+      dot += xv[c][i] * gv[c][i] * (w ? (float)wb[c][i] : 1.f);
+    }
+  }
+  dot = wave_sum(dot);
+  if (lane == 0) part[wid] = dot;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int p = 0; p < WPR; ++p) tot += part[(wid / WPR) * WPR + p];
+  if (!valid) return;
+  tot /= N;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = ((c * WPR + pw) * 64 + lane) * 8;
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      o[i] = r * (gv[c][i] * (w ? (float)wb[c][i] : 1.f) - xv[c][i] * tot);
+      if (dres) o[i] += (float)rb[c][i];
+    }
+    store8(dx + ro + col, o);
+  }
+}
+
+// waves per row (LIPA_NORM_WPR = 2 | 4; 4 needs N >= 2048); the template's CH is N / (512·WPR)
+static int norm_wpr(int ch) {
+  static const int v = [] { const char* e = getenv("LIPA_NORM_WPR"); return e ? atoi(e) : 2; }();
+  return v == 4 && ch >= 2 ? 4 : 2;
+}
+
+// split-row form for bf16 rows of N = 1024·{1, 2, 4, 8}; LIPA_NORM_SPLIT=0 keeps one wave per row
+static int norm_split_ch(int dtype, int N) {
+  static const bool off = [] { const char* e = getenv("LIPA_NORM_SPLIT"); return e && atoi(e) == 0; }();
+  if (off || dtype != 1 || N % 1024) return 0;
+  const int ch = N / 1024;
+  return (ch == 1 || ch == 2 || ch == 4 || ch == 8) ? ch : 0;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------ launchers
 // dtype: 0 = fp32, 1 = bf16 (activations and weight share the dtype)
 void launch_rmsnorm_fwd(int dtype, const void* x, const void* w, void* y, float* rstd, int M, int N, float eps,
                         hipStream_t st) {
+  if (const int ch = norm_split_ch(dtype, N)) {
+    const int wpr = norm_wpr(ch);
+    dim3 g2((M * wpr + 3) / 4), b2(256);
+#define S(CH_, W_)                                                                                                \
+  rmsnorm_fwd_split_k<CH_, W_><<<g2, b2, 0, st>>>((const bf16*)x, (const bf16*)w, (bf16*)y, rstd, M, N, eps)
+    if (wpr == 4) {
+      if (ch == 2) S(1, 4); else if (ch == 4) S(2, 4); else S(4, 4);
+    } else {
+      if (ch == 1) S(1, 2); else if (ch == 2) S(2, 2); else if (ch == 4) S(4, 2); else S(8, 2);
+    }
+#undef S
+    LIPA_CHECK_LAUNCH();
+    return;
+  }
   dim3 g((M + ROWS - 1) / ROWS), b(256);
 #define F(CH)                                                                                                  \
   if (dtype == 1)                                                                                              \
@@ -311,6 +433,21 @@ void launch_rmsnorm_fwd(int dtype, const void* x, const void* w, void* y, float*
 
 void launch_rmsnorm_bwd(int dtype, const void* dy, const void* x, const void* w, const float* rstd, void* dx,
                         float* dw_part, float* dw, int M, int N, const void* dres, hipStream_t st) {
+  if (const int ch = dw_part ? 0 : norm_split_ch(dtype, N)) {
+    const int wpr = norm_wpr(ch);
+    dim3 g2((M * wpr + 3) / 4), b2(256);
+#define S(CH_, W_)                                                                                          \
+  rmsnorm_bwd_split_k<CH_, W_><<<g2, b2, 0, st>>>((const bf16*)dy, (const bf16*)x, (const bf16*)w, rstd, \
+                                                 (bf16*)dx, M, N, (const bf16*)dres)
+    if (wpr == 4) {
+      if (ch == 2) S(1, 4); else if (ch == 4) S(2, 4); else S(4, 4);
+    } else {
+      if (ch == 1) S(1, 2); else if (ch == 2) S(2, 2); else if (ch == 4) S(4, 2); else S(8, 2);
+    }
+#undef S
+    LIPA_CHECK_LAUNCH();
+    return;
+  }
   dim3 g((M + ROWS - 1) / ROWS), b(256);
 #define F(CH)                                                                                               \
   if (dtype == 1)                                                                                           \
