@@ -84,6 +84,10 @@ void launch_lora_proj_pair(const void*, const void*, int, const void*, const voi
                            float, int, hipStream_t);
 void launch_lora_acc_pair(const float*, const float*, int, int, const void*, const void*, int, int, int, float*, float*,
                           int, hipStream_t);
+void launch_lora_dA_pair(const float*, const float*, int, int, const void*, int, int, float*, float*, int64_t, int64_t,
+                         int64_t, int64_t, const uint8_t*, const uint8_t*, float, float, int, hipStream_t);
+void launch_lora_dx2(const float*, const float*, int, const void*, const void*, int, int, const uint8_t*,
+                     const uint8_t*, float, float, void*, int, int, hipStream_t);
 void launch_lora_apply(void*, int, int, int, const float* const*, const int*, const void* const*, void* const*, const int*, const int*,
                        const int*, hipStream_t);
 void launch_lora_acc(const float*, int, int, const void*, int, void*, int, const void*, int, float*, int64_t, int64_t,
@@ -386,7 +390,7 @@ Tensor lt_linear(Tensor x, Tensor w, optional<Tensor> residual, bool tune) {
 
 // dx = dy·w: dy [M, N] contiguous, w [N, K] contiguous; split > 1: K-slices of the reduction dim
 // as one strided-batched GEMM into bf16 partials + an fp32 slice sum
-Tensor lt_dx(Tensor dy, Tensor w, int64_t split, bool tune) {
+Tensor lt_dx(Tensor dy, Tensor w, int64_t split, bool tune, optional<Tensor> c) {
   CHECK_CUDA(dy);
   CHECK_BF16(dy);
   CHECK_BF16(w);
@@ -399,10 +403,17 @@ Tensor lt_dx(Tensor dy, Tensor w, int64_t split, bool tune) {
   size_t wsb;
   void* ws = lt_workspace(wsb);
   Tensor out = at::empty({M, K}, dy.options());
+  const void* cp = nullptr;
+  if (c.has_value() && c->defined()) {   // dx = dy·w + c (c: the LoRA input-gradient term)
+    CHECK_BF16((*c));
+    CHECK_CONTIG((*c));
+    TORCH_CHECK(c->size(0) == M && c->size(1) == K && split == 1, "lt_dx: c [M, K], no split");
+    cp = c->data_ptr();
+  }
   if (split == 1) {
-    if (!lt_gemm(false, false, K, M, N, w.data_ptr(), K, dy.data_ptr(), N, nullptr, out.data_ptr(), K, 1, 0, 0, 0, ws,
+    if (!lt_gemm(false, false, K, M, N, w.data_ptr(), K, dy.data_ptr(), N, cp, out.data_ptr(), K, 1, 0, 0, 0, ws,
                  wsb, stream(), tune))
-      return at::mm(dy, w);
+      return cp ? at::addmm(*c, dy, w) : at::mm(dy, w);
     return out;
   }
   const int64_t Ns = N / split;
@@ -944,6 +955,51 @@ void lora_acc_pair(Tensor xa, Tensor xb, Tensor dy, int64_t c0a, Tensor outa, in
                        stream());
 }
 
+//   dA_i [r, K] += D_i(x)ᵀ-weighted G_i (keep bits from lora_proj2, masks [2, M, K/8])
+void lora_dA_pair(Tensor g0, Tensor g1, Tensor x, Tensor out0, Tensor out1, Tensor masks, double p0, double p1) {
+  for (const Tensor* g : {&g0, &g1})
+    TORCH_CHECK(g->scalar_type() == at::kFloat && g->dim() == 2 && g->stride(1) == 1 && g->size(1) <= 8 &&
+                    g->stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(g->data_ptr()) % 16 == 0,
+                "lora_dA_pair: g fp32 [M, r<=8], 16-B aligned rows");
+  TORCH_CHECK(g0.stride(0) == g1.stride(0) && g0.size(1) == g1.size(1), "lora_dA_pair: one layout for both g");
+  CHECK_BF16(x);
+  const int M = x.size(0), K = x.size(1), r = g0.size(1);
+  TORCH_CHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && K % 128 == 0, "lora_dA_pair: x layout");
+  for (const Tensor* o : {&out0, &out1})
+    TORCH_CHECK(o->scalar_type() == at::kFloat && o->dim() == 2 && o->size(0) == r && o->size(1) == K,
+                "lora_dA_pair: out fp32 [r, K]");
+  const uint8_t* kb = keep_bits_ptr(masks, M, K, "lora_dA_pair");
+  TORCH_CHECK(kb, "lora_dA_pair: keep bits required");
+  const size_t plane = (size_t)M * (K / 8);
+  launch_lora_dA_pair(g0.data_ptr<float>(), g1.data_ptr<float>(), g0.stride(0), r, x.data_ptr(), x.stride(0), K,
+                      out0.data_ptr<float>(), out1.data_ptr<float>(), out0.stride(0), out0.stride(1), out1.stride(0),
+                      out1.stride(1), p0 > 0 ? kb : nullptr, p1 > 0 ? kb + plane : nullptr,
+                      p0 > 0 ? (float)(1.0 / (1.0 - p0)) : 1.f, p1 > 0 ? (float)(1.0 / (1.0 - p1)) : 1.f, M, stream());
+}
+
+//   dx_lora [M, K] bf16 = Σ_i D_i(G_i·A_i)·ds_i  — the dX GEMM's C matrix
+Tensor lora_dx2(Tensor g0, Tensor g1, Tensor a0, Tensor a1, Tensor masks, double p0, double p1) {
+  TORCH_CHECK(g0.scalar_type() == at::kFloat && g1.scalar_type() == at::kFloat && g0.stride(0) == g1.stride(0) &&
+                  g0.stride(1) == 1 && g1.stride(1) == 1 && g0.stride(0) % 4 == 0 &&
+                  reinterpret_cast<uintptr_t>(g0.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(g1.data_ptr()) % 16 == 0 && g0.size(1) <= 8 && g1.size(1) <= 8,
+              "lora_dx2: g fp32 [M, r<=8], one row stride, 16-B aligned");
+  CHECK_BF16(a0);
+  CHECK_BF16(a1);
+  const int M = g0.size(0), K = a0.size(1);
+  TORCH_CHECK(a0.is_contiguous() && a1.is_contiguous() && a1.size(1) == K && a0.size(0) == g0.size(1) &&
+                  a1.size(0) == g1.size(1) && K % 8 == 0 && g1.size(0) == M, "lora_dx2: A_i [r_i, K]");
+  const uint8_t* kb = keep_bits_ptr(masks, M, K, "lora_dx2");
+  TORCH_CHECK(kb, "lora_dx2: keep bits required");
+  const size_t plane = (size_t)M * (K / 8);
+  Tensor out = at::empty({M, K}, a0.options());
+  launch_lora_dx2(g0.data_ptr<float>(), g1.data_ptr<float>(), g0.stride(0), a0.data_ptr(), a1.data_ptr(), a0.size(0),
+                  a1.size(0), p0 > 0 ? kb : nullptr, p1 > 0 ? kb + plane : nullptr,
+                  p0 > 0 ? (float)(1.0 / (1.0 - p0)) : 1.f, p1 > 0 ? (float)(1.0 / (1.0 - p1)) : 1.f, out.data_ptr(),
+                  M, K, stream());
+  return out;
+}
+
 // ------------------------------------------------------------------ generation (K16, K17)
 // q [B, hq*d] bf16; kc/vc [B, Smax, hkv*d] bf16 contiguous; lens [B] int32 (valid keys per row);
 // max_len >= max(lens) bounds the split count without a host sync.
@@ -1179,6 +1235,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lora_acc2", &lora_acc2);
   m.def("lora_proj_pair", &lora_proj_pair);
   m.def("lora_acc_pair", &lora_acc_pair);
+  m.def("lora_dA_pair", &lora_dA_pair);
+  m.def("lora_dx2", &lora_dx2);
   m.def("lora_apply", &lora_apply);
   m.def("gemm_int4", &gemm_int4);
   m.def("gemv_w4", &gemv_w4);

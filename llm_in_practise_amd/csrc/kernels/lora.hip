@@ -240,7 +240,7 @@ __device__ __forceinline__ void lora_acc_mfma_body(const float* __restrict__ G, 
                                                    int lddx, const bf16* __restrict__ W, int K,
                                                    float* __restrict__ out, int64_t sj, int64_t sk, int M,
                                                    uint64_t key, uint32_t thr16, float dscale, size_t mask_ld, int bx,
-                                                   int by) {
+                                                   int by, const uint8_t* __restrict__ kbits = nullptr) {
   __shared__ float red[4][64][33];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int q = lane >> 4, n = lane & 15;
@@ -276,7 +276,9 @@ __device__ __forceinline__ void lora_acc_mfma_body(const float* __restrict__ G, 
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int m = m0 + e;
-      keep[e] = m >= M ? 0u : (thr16 ? dropout_keep8(key, ((size_t)m * mask_ld + k8) >> 3, thr16) : 0xFFu);
+      keep[e] = m >= M ? 0u
+                       : kbits ? (uint32_t)kbits[(size_t)m * (K >> 3) + (k8 >> 3)]   // stored by lora_proj2
+                               : (thr16 ? dropout_keep8(key, ((size_t)m * mask_ld + k8) >> 3, thr16) : 0xFFu);
     }
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
@@ -348,13 +350,71 @@ struct AccPair {
   float* out[2];
   int K[2];
   int nblk0;
+  int64_t sj[2], sk[2];
+  float ds[2];            // dropout rescale 1/(1-p) (1: no dropout)
+  const uint8_t* kb[2];   // keep bits [M, K/8] (null: no dropout)
 };
 template <int SUB>
 __global__ __launch_bounds__(256) void lora_acc_pair_k(AccPair a, int ldg, int r, int ldx, int M) {
   const int b = (int)blockIdx.x >= a.nblk0;
   const int bx = blockIdx.x - (b ? a.nblk0 : 0);
-  lora_acc_mfma_body<8, false, SUB>(a.G[b], ldg, r, a.X[b], ldx, nullptr, 0, nullptr, a.K[b], a.out[b], 1, r, M, 0,
-                                    0u, 1.f, 0, bx, blockIdx.y);
+  lora_acc_mfma_body<8, false, SUB>(a.G[b], ldg, r, a.X[b], ldx, nullptr, 0, nullptr, a.K[b], a.out[b], a.sj[b],
+                                    a.sk[b], M, 0, a.kb[b] ? 1u : 0u, a.ds[b], 0, bx, blockIdx.y, a.kb[b]);
+}
+
+// dx_lora[m, k] = Σ_i D_i[m, k]·ds_i·Σ_j G_i[m, j]·A_i[j, k] for the two branches (bf16 [M, K]): the LoRA
+// input-gradient term, written once and handed to the dX GEMM as its C matrix (no read-modify-write
+// pass over dx).  A thread owns 8 consecutive k of 8 rows; A's 8 k-columns are loaded once per thread.
+__global__ __launch_bounds__(256) void lora_dx2_k(const float* __restrict__ G0, const float* __restrict__ G1, int ldg,
+                                                  const bf16* __restrict__ A0, const bf16* __restrict__ A1, int r0,
+                                                  int r1, const uint8_t* __restrict__ kb0,
+                                                  const uint8_t* __restrict__ kb1, float ds0, float ds1,
+                                                  bf16* __restrict__ out, int M, int K) {
+  const int kv = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int k8 = kv * 8;
+  if (k8 >= K) return;
+  const int m0 = (blockIdx.y * 4 + (threadIdx.x >> 6)) * 8;
+  float a0[8][8], a1[8][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const bf16x8 v0 = j < r0 ? *reinterpret_cast<const bf16x8*>(A0 + (size_t)j * K + k8) : bf16x8{};
+    const bf16x8 v1 = j < r1 ? *reinterpret_cast<const bf16x8*>(A1 + (size_t)j * K + k8) : bf16x8{};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a0[j][i] = (float)v0[i];
+      a1[j][i] = (float)v1[i];
+    }
+  }
+#pragma unroll 2
+  for (int e = 0; e < 8; ++e) {
+    const int m = m0 + e;
+    if (m >= M) break;
+    float g0[8], g1[8];
+#pragma unroll
+    for (int j = 0; j < 8; j += 4) {
+      const f32x4 t0 = *reinterpret_cast<const f32x4*>(G0 + (size_t)m * ldg + j);
+      const f32x4 t1 = *reinterpret_cast<const f32x4*>(G1 + (size_t)m * ldg + j);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        g0[j + u] = j + u < r0 ? t0[u] * ds0 : 0.f;
+        g1[j + u] = j + u < r1 ? t1[u] * ds1 : 0.f;
+      }
+    }
+    const uint32_t k0 = kb0 ? kb0[(size_t)m * (K >> 3) + kv] : 0xFFu;
+    const uint32_t k1 = kb1 ? kb1[(size_t)m * (K >> 3) + kv] : 0xFFu;
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float t0 = 0.f, t1 = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        t0 += g0[j] * a0[j][i];
+        t1 += g1[j] * a1[j][i];
+      }
+      o[i] = (((k0 >> i) & 1) ? t0 : 0.f) + (((k1 >> i) & 1) ? t1 : 0.f);
+    }
+    store8(out + (size_t)m * K + k8, o);
+  }
 }
 
 // ---- two branches sharing one input (q_proj + v_proj of a fused q|k|v projection) -------------
@@ -825,8 +885,30 @@ void launch_lora_proj_pair(const void* X0, const void* X1, int ldx, const void* 
 // dB_i [K_i, r] (row-major, i.e. out[k * r + j]) += Σ_m X_i[m, k]·G_i[m, j] for two branches, r <= 8
 void launch_lora_acc_pair(const float* G0, const float* G1, int ldg, int r, const void* X0, const void* X1, int ldx,
                           int K0, int K1, float* out0, float* out1, int M, hipStream_t st) {
-  AccPair a{{G0, G1}, {(const bf16*)X0, (const bf16*)X1}, {out0, out1}, {K0, K1}, K0 / 128};
+  AccPair a{{G0, G1}, {(const bf16*)X0, (const bf16*)X1}, {out0, out1}, {K0, K1}, K0 / 128, {1, 1}, {r, r},
+            {1.f, 1.f}, {nullptr, nullptr}};
   dim3 g(K0 / 128 + K1 / 128, (M + 127) / 128);
   lora_acc_pair_k<1><<<g, 256, 0, st>>>(a, ldg, r, ldx, M);
+  LIPA_CHECK_LAUNCH();
+}
+
+// backward of a dropout q_proj + v_proj pair from the forward's keep bits:
+//   dA_i [r, K] += Σ_m G_i[m, j]·D_i(x)[m, k]·ds_i  (one launch, both branches, fp32 atomics)
+void launch_lora_dA_pair(const float* G0, const float* G1, int ldg, int r, const void* X, int ldx, int K, float* out0,
+                         float* out1, int64_t sj0, int64_t sk0, int64_t sj1, int64_t sk1, const uint8_t* kb0,
+                         const uint8_t* kb1, float ds0, float ds1, int M, hipStream_t st) {
+  AccPair a{{G0, G1}, {(const bf16*)X, (const bf16*)X}, {out0, out1}, {K, K}, K / 128, {sj0, sj1}, {sk0, sk1},
+            {ds0, ds1}, {kb0, kb1}};
+  dim3 g(2 * (K / 128), (M + 127) / 128);
+  lora_acc_pair_k<1><<<g, 256, 0, st>>>(a, ldg, r, ldx, M);
+  LIPA_CHECK_LAUNCH();
+}
+
+void launch_lora_dx2(const float* G0, const float* G1, int ldg, const void* A0, const void* A1, int r0, int r1,
+                     const uint8_t* kb0, const uint8_t* kb1, float ds0, float ds1, void* out, int M, int K,
+                     hipStream_t st) {
+  dim3 g((K / 8 + 63) / 64, (M + 31) / 32);
+  lora_dx2_k<<<g, 256, 0, st>>>(G0, G1, ldg, (const bf16*)A0, (const bf16*)A1, r0, r1, kb0, kb1, ds0, ds1, (bf16*)out,
+                                M, K);
   LIPA_CHECK_LAUNCH();
 }

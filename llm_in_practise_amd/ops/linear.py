@@ -51,6 +51,9 @@ _LT_MIN_M = 256
 _KEEP_BITS = __import__("os").environ.get("LIPA_LORA_KEEP_BITS", "1") != "0"
 # two-branch backward launches (lora_proj_pair / lora_acc_pair); LIPA_LORA_PAIR_BWD=0: per-branch
 _PAIR_BWD = __import__("os").environ.get("LIPA_LORA_PAIR_BWD", "1") != "0"
+# q+v dropout pair backward: the LoRA dx term as the dX GEMM's C matrix + a separate dA launch
+# (LIPA_LORA_DX_C=0: the fused read-modify-write lora_acc2 pass over dx)
+_DX_C = __import__("os").environ.get("LIPA_LORA_DX_C", "1") != "0"
 
 
 def _nf4_dequant_bf16(q: NF4Weight) -> torch.Tensor:
@@ -160,6 +163,12 @@ def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
     return native().gemm_bf16(x, base, ext_a, ext_b, residual)
 
 
+def _dx_split(dy: torch.Tensor, w: torch.Tensor) -> int:
+    M, N = dy.shape
+    K = w.shape[1]
+    return 4 if N % 4 == 0 and N >= 4 * K and M >= 256 and (M // 256) * max(1, K // 256) < 256 else 1
+
+
 def _dense_dx(dy: torch.Tensor, w: torch.Tensor, tune: bool = True) -> torch.Tensor:
     """dX = dY·W for a bf16 [N, K] weight.  A long reduction into a small output (gate|up:
     N = 24576 → K = 4096 at M = 2048 is 128 output tiles for 256 CUs) leaves half the chip idle
@@ -167,9 +176,9 @@ def _dense_dx(dy: torch.Tensor, w: torch.Tensor, tune: bool = True) -> torch.Ten
     sum fill it (491 → 328 µs, profiles/nf4_dequant_vs_fused_ab.txt)."""
     M, N = dy.shape
     K = w.shape[1]
-    split = 4 if N % 4 == 0 and N >= 4 * K and M >= 256 and (M // 256) * max(1, K // 256) < 256 else 1
+    split = _dx_split(dy, w)
     if _LT and M >= _LT_MIN_M and dy.is_cuda and dy.dtype == torch.bfloat16 and K % 8 == 0:
-        return native().lt_dx(dy.contiguous(), w.contiguous(), split, tune)
+        return native().lt_dx(dy.contiguous(), w.contiguous(), split, tune, None)
     if split > 1:
         s = split
         return torch.bmm(dy.view(M, s, N // s).transpose(0, 1), w.view(s, N // s, K)).sum(0)
@@ -484,10 +493,38 @@ class _FusedLinearFn(torch.autograd.Function):
                 ext_b = torch.cat([bf16_view(ab[2 * i], dy.dtype) for i in fold], 0)            # [R, K]
                 ext_b = F.pad(ext_b, (0, 0, 0, ext_a.shape[1] - ext_b.shape[0])).t().contiguous()  # [K, Rp]
             wb = ctx.wdq if ctx.wdq is not None else (base if not dense else weight)
-            dx = _base_gemm_t(dy, wb, ext_a, ext_b)
+            pair_ok = (ctx.pair and all(k is not None for k in ctx.keys) and not deterministic()
+                       and ctx.needs_input_grad[5] and ctx.needs_input_grad[7])
+            if (pair_ok and _DX_C and ctx.masks is not None and not fold and isinstance(wb, torch.Tensor)
+                    and _LT and not _NATIVE_DENSE and dy.shape[0] >= _LT_MIN_M and _dx_split(dy, wb) == 1):
+                # the LoRA input-gradient term written once (lora_dx2, from the stored keep bits) and
+                # added by the dX GEMM as its C matrix; dA from x in a separate launch — no
+                # read-modify-write pass over dx (lora_acc2)
+                a0, a1 = bf16_view(ab[0], dy.dtype), bf16_view(ab[2], dy.dtype)
+                p0, p1 = branches[0].dropout, branches[1].dropout
+                c = native().lora_dx2(g_list[0], g_list[1], a0, a1, ctx.masks, p0, p1)
+                dx = native().lt_dx(dy.contiguous(), wb.contiguous(), 1, True, c)
+                del c
+                (o0, ret0), (o1, ret1) = dest(0), dest(2)
+                native().lora_dA_pair(g_list[0], g_list[1], x, o0, o1, ctx.masks, p0, p1)
+                ctx.masks = None
+                for i, (o, ret) in ((0, (o0, ret0)), (1, (o1, ret1))):
+                    if ret:
+                        grads_ab[2 * i] = o.to(ab[2 * i].dtype)
+                    else:
+                        _notify_grad_ready(ctx.ab_refs[2 * i])
+                pair_ok = False
+                done_dA = True
+            else:
+                dx = _base_gemm_t(dy, wb, ext_a, ext_b)
+                done_dA = False
+        else:
+            pair_ok = done_dA = False
         ctx.wdq = None
         ctx.bts = None
-        if (ctx.pair and dx is not None and all(k is not None for k in ctx.keys) and not deterministic()
+        if done_dA:
+            branches_acc = ()
+        elif (ctx.pair and dx is not None and all(k is not None for k in ctx.keys) and not deterministic()
                 and ctx.needs_input_grad[5] and ctx.needs_input_grad[7]):
             # both adapters' dA and their dx terms in ONE pass over x and dx (lora_acc2)
             (o0, ret0), (o1, ret1) = dest(0), dest(2)

@@ -615,6 +615,17 @@ def test_lora_two_branch_kernels(native_ext, M, K, p0, p1):
     m1 = ((xd1 != 0) | (x == 0)).float() * (1 / (1 - p1)) if p1 > 0 else torch.ones_like(dx0)
     want = dx0 + m0 * (g0 @ a0.float()) + m1 * (g1 @ a1.float())
     assert rel_err(dx, want) < 1e-2
+    # split form: the dx term alone (the dX GEMM's C matrix) + dA from the stored keep bits
+    c = native_ext.lora_dx2(g0, g1, a0, a1, masks, p0, p1)
+    assert rel_err(c, want - dx0) < 1e-2
+    da0c, da1c = torch.zeros(8, K, device=DEV), torch.zeros(8, K, device=DEV)
+    native_ext.lora_dA_pair(g0, g1, x, da0c, da1c, masks, p0, p1)
+    assert rel_err(da0c, g0.t() @ xd0.float()) < 1e-2 and rel_err(da1c, g1.t() @ xd1.float()) < 1e-2
+    # dx = dy·W + c in one hipBLASLt call
+    dyw = torch.randn(M, 1024, device=DEV).to(torch.bfloat16)
+    w = (0.03 * torch.randn(1024, K, device=DEV)).to(torch.bfloat16)
+    dxc = native_ext.lt_dx(dyw, w, 1, True, c)
+    assert rel_err(dxc, dyw.float() @ w.float() + c.float()) < 1e-2
 
 
 # ----------------------------------------------------------------------------- 8-phase GEMM
@@ -688,7 +699,7 @@ def test_lt_dx_split(native_ext, split):
     w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) / N ** 0.5
     want = dy.float() @ w.float()
     for _ in range(16):
-        dx = native_ext.lt_dx(dy, w, split, True)
+        dx = native_ext.lt_dx(dy, w, split, True, None)
         err = (dx.float() - want).abs().max().item()
         assert err < 0.03 * want.abs().max().item(), err
 
