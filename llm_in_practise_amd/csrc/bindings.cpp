@@ -980,10 +980,10 @@ void lora_dA_pair(Tensor g0, Tensor g1, Tensor x, Tensor out0, Tensor out1, Tens
 //   dx_lora [M, K] bf16 = Σ_i D_i(G_i·A_i)·ds_i  — the dX GEMM's C matrix
 Tensor lora_dx2(Tensor g0, Tensor g1, Tensor a0, Tensor a1, Tensor masks, double p0, double p1) {
   TORCH_CHECK(g0.scalar_type() == at::kFloat && g1.scalar_type() == at::kFloat && g0.stride(0) == g1.stride(0) &&
-                  g0.stride(1) == 1 && g1.stride(1) == 1 && g0.stride(0) % 4 == 0 &&
+                  g0.stride(1) == 1 && g1.stride(1) == 1 && g0.stride(0) % 4 == 0 && g0.stride(0) >= 8 &&
                   reinterpret_cast<uintptr_t>(g0.data_ptr()) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(g1.data_ptr()) % 16 == 0 && g0.size(1) <= 8 && g1.size(1) <= 8,
-              "lora_dx2: g fp32 [M, r<=8], one row stride, 16-B aligned");
+              "lora_dx2: g fp32 [M, r<=8], one row stride >= 8, 16-B aligned");
   CHECK_BF16(a0);
   CHECK_BF16(a1);
   const int M = g0.size(0), K = a0.size(1);

@@ -365,6 +365,7 @@ __global__ __launch_bounds__(256) void lora_acc_pair_k(AccPair a, int ldg, int r
 // dx_lora[m, k] = Σ_i D_i[m, k]·ds_i·Σ_j G_i[m, j]·A_i[j, k] for the two branches (bf16 [M, K]): the LoRA
 // input-gradient term, written once and handed to the dX GEMM as its C matrix (no read-modify-write
 // pass over dx).  A thread owns 8 consecutive k of 8 rows; A's 8 k-columns are loaded once per thread.
+template <int RPT>
 __global__ __launch_bounds__(256) void lora_dx2_k(const float* __restrict__ G0, const float* __restrict__ G1, int ldg,
                                                   const bf16* __restrict__ A0, const bf16* __restrict__ A1, int r0,
                                                   int r1, const uint8_t* __restrict__ kb0,
@@ -373,46 +374,49 @@ __global__ __launch_bounds__(256) void lora_dx2_k(const float* __restrict__ G0, 
   const int kv = blockIdx.x * 64 + (threadIdx.x & 63);
   const int k8 = kv * 8;
   if (k8 >= K) return;
-  const int m0 = (blockIdx.y * 4 + (threadIdx.x >> 6)) * 8;
-  float a0[8][8], a1[8][8];
+  const int m0 = (blockIdx.y * 4 + (threadIdx.x >> 6)) * RPT;
+  // every load of the thread issued up front (A columns stay packed bf16; G rows and keep bytes of
+  // all RPT rows), then the math: one exposed memory round trip per thread
+  bf16x8 av0[8], av1[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const bf16x8 v0 = j < r0 ? *reinterpret_cast<const bf16x8*>(A0 + (size_t)j * K + k8) : bf16x8{};
-    const bf16x8 v1 = j < r1 ? *reinterpret_cast<const bf16x8*>(A1 + (size_t)j * K + k8) : bf16x8{};
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      a0[j][i] = (float)v0[i];
-      a1[j][i] = (float)v1[i];
-    }
+    av0[j] = j < r0 ? *reinterpret_cast<const bf16x8*>(A0 + (size_t)j * K + k8) : bf16x8{};
+    av1[j] = j < r1 ? *reinterpret_cast<const bf16x8*>(A1 + (size_t)j * K + k8) : bf16x8{};
   }
-#pragma unroll 2
-  for (int e = 0; e < 8; ++e) {
+  f32x4 gq0[RPT][2], gq1[RPT][2];
+  uint32_t kp0[RPT], kp1[RPT];
+#pragma unroll
+  for (int e = 0; e < RPT; ++e) {
+    const int m = min(m0 + e, M - 1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      gq0[e][h] = *reinterpret_cast<const f32x4*>(G0 + (size_t)m * ldg + 4 * h);
+      gq1[e][h] = *reinterpret_cast<const f32x4*>(G1 + (size_t)m * ldg + 4 * h);
+    }
+    kp0[e] = kb0 ? kb0[(size_t)m * (K >> 3) + kv] : 0xFFu;
+    kp1[e] = kb1 ? kb1[(size_t)m * (K >> 3) + kv] : 0xFFu;
+  }
+#pragma unroll
+  for (int e = 0; e < RPT; ++e) {
     const int m = m0 + e;
     if (m >= M) break;
-    float g0[8], g1[8];
+    float t0[8], t1[8];
 #pragma unroll
-    for (int j = 0; j < 8; j += 4) {
-      const f32x4 t0 = *reinterpret_cast<const f32x4*>(G0 + (size_t)m * ldg + j);
-      const f32x4 t1 = *reinterpret_cast<const f32x4*>(G1 + (size_t)m * ldg + j);
+    for (int i = 0; i < 8; ++i) t0[i] = t1[i] = 0.f;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        g0[j + u] = j + u < r0 ? t0[u] * ds0 : 0.f;
-        g1[j + u] = j + u < r1 ? t1[u] * ds1 : 0.f;
+    for (int j = 0; j < 8; ++j) {
+      const float g0 = j < r0 ? gq0[e][j >> 2][j & 3] : 0.f;
+      const float g1 = j < r1 ? gq1[e][j >> 2][j & 3] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        t0[i] += g0 * (float)av0[j][i];
+        t1[i] += g1 * (float)av1[j][i];
       }
     }
-    const uint32_t k0 = kb0 ? kb0[(size_t)m * (K >> 3) + kv] : 0xFFu;
-    const uint32_t k1 = kb1 ? kb1[(size_t)m * (K >> 3) + kv] : 0xFFu;
     float o[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float t0 = 0.f, t1 = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        t0 += g0[j] * a0[j][i];
-        t1 += g1[j] * a1[j][i];
-      }
-      o[i] = (((k0 >> i) & 1) ? t0 : 0.f) + (((k1 >> i) & 1) ? t1 : 0.f);
-    }
+    for (int i = 0; i < 8; ++i)
+      o[i] = (((kp0[e] >> i) & 1) ? t0[i] * ds0 : 0.f) + (((kp1[e] >> i) & 1) ? t1[i] * ds1 : 0.f);
     store8(out + (size_t)m * K + k8, o);
   }
 }
@@ -907,8 +911,16 @@ void launch_lora_dA_pair(const float* G0, const float* G1, int ldg, int r, const
 void launch_lora_dx2(const float* G0, const float* G1, int ldg, const void* A0, const void* A1, int r0, int r1,
                      const uint8_t* kb0, const uint8_t* kb1, float ds0, float ds1, void* out, int M, int K,
                      hipStream_t st) {
-  dim3 g((K / 8 + 63) / 64, (M + 31) / 32);
-  lora_dx2_k<<<g, 256, 0, st>>>(G0, G1, ldg, (const bf16*)A0, (const bf16*)A1, r0, r1, kb0, kb1, ds0, ds1, (bf16*)out,
+  static const int rpt = [] { const char* e = getenv("LIPA_LORA_DX_RPT"); return e ? atoi(e) : 4; }();
+  if (rpt == 8) {
+    dim3 g8((K / 8 + 63) / 64, (M + 31) / 32);
+    lora_dx2_k<8><<<g8, 256, 0, st>>>(G0, G1, ldg, (const bf16*)A0, (const bf16*)A1, r0, r1, kb0, kb1, ds0, ds1,
+                                      (bf16*)out, M, K);
+    LIPA_CHECK_LAUNCH();
+    return;
+  }
+  dim3 g((K / 8 + 63) / 64, (M + 15) / 16);
+  lora_dx2_k<4><<<g, 256, 0, st>>>(G0, G1, ldg, (const bf16*)A0, (const bf16*)A1, r0, r1, kb0, kb1, ds0, ds1, (bf16*)out,
                                 M, K);
   LIPA_CHECK_LAUNCH();
 }
