@@ -163,17 +163,30 @@ def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
     return native().gemm_bf16(x, base, ext_a, ext_b, residual)
 
 
+_SPLIT_ENV = int(__import__("os").environ.get("LIPA_DX_SPLIT", "0"))   # 0: auto; 1, 2, 4, 8: forced
+
+
 def _dx_split(dy: torch.Tensor, w: torch.Tensor) -> int:
     M, N = dy.shape
     K = w.shape[1]
-    return 4 if N % 4 == 0 and N >= 4 * K and M >= 256 and (M // 256) * max(1, K // 256) < 256 else 1
+    tiles = (M // 256) * max(1, K // 256)
+    if not (N >= 4 * K and M >= 256 and tiles < 256):
+        return 1
+    # the fewest K-slices that give every CU an output tile (gate|up dX at M = 2048: 128 tiles -> 2;
+    # 2 slices beat 4 by 0.5 ms/step: same GEMM time, half the partial bytes to sum)
+    s = 2
+    while tiles * s < 256 and s < 8:
+        s *= 2
+    if _SPLIT_ENV in (1, 2, 4, 8):
+        s = _SPLIT_ENV
+    return s if N % s == 0 else 1
 
 
 def _dense_dx(dy: torch.Tensor, w: torch.Tensor, tune: bool = True) -> torch.Tensor:
     """dX = dY·W for a bf16 [N, K] weight.  A long reduction into a small output (gate|up:
     N = 24576 → K = 4096 at M = 2048 is 128 output tiles for 256 CUs) leaves half the chip idle
-    in hipBLASLt's non-split-K kernel; four K-slices as one batched GEMM + an fp32-accumulated
-    sum fill it (491 → 328 µs, profiles/nf4_dequant_vs_fused_ab.txt)."""
+    in hipBLASLt's non-split-K kernel (491 µs; its best in-step candidate 365 µs); K-slices as one
+    batched GEMM + an fp32 slice sum fill it (2 slices: 301 + 8 µs; profiles/hipblaslt_direct_ab.txt)."""
     M, N = dy.shape
     K = w.shape[1]
     split = _dx_split(dy, w)
