@@ -4,7 +4,8 @@
 // GEMM with beta = 1 (one extra 16 MB copy per o_proj / down_proj call, 72 per Qwen3-8B step);
 // hipBLASLt itself takes C and D as separate matrices.  The plan cache also lets a shape pick its
 // kernel from the measured time of the heuristic's top candidates IN the running step (cold
-// weights just written by the NF4 dequant, the real L2 / MALL state) instead of the heuristic's
+// weights just written by the NF4 dequant, the real L2 / MALL state; timed with events read back on
+// later calls, so the host never waits) instead of the heuristic's
 // first choice or an isolated-loop tuner (profiles/tunableop_ab.txt: isolated tuning predicted
 // 10-20 % per GEMM and delivered 0.8 % in the step).
 //
@@ -39,9 +40,53 @@ struct Plan {
   hipblasLtMatrixLayout_t a = nullptr, b = nullptr, c = nullptr, d = nullptr;
   std::vector<hipblasLtMatmulHeuristicResult_t> cand;
   std::vector<float> best;  // per-candidate best time (ms) while tuning
+  std::vector<int> seen;    // timings collected per candidate
   int calls = 0, chosen = -1;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
+  // timings in flight: read back with hipEventQuery on later calls, never waited for (no host stall)
+  struct Pending {
+    int idx;
+    hipEvent_t e0, e1;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> pool;
 };
+
+hipEvent_t take_event(Plan& p) {
+  if (!p.pool.empty()) {
+    hipEvent_t e = p.pool.back();
+    p.pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  hipEventCreate(&e);
+  return e;
+}
+
+// fold finished timings in; choose once every candidate has tune_reps() of them
+void poll_timings(Plan& p, int reps) {
+  for (size_t i = 0; i < p.pending.size();) {
+    Plan::Pending& t = p.pending[i];
+    if (hipEventQuery(t.e1) != hipSuccess) {
+      ++i;
+      continue;
+    }
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, t.e0, t.e1);
+    if (ms < p.best[t.idx]) p.best[t.idx] = ms;
+    ++p.seen[t.idx];
+    p.pool.push_back(t.e0);
+    p.pool.push_back(t.e1);
+    p.pending[i] = p.pending.back();
+    p.pending.pop_back();
+  }
+  if (p.chosen >= 0) return;
+  for (size_t i = 0; i < p.cand.size(); ++i)
+    if (p.seen[i] < reps) return;
+  int bi = 0;
+  for (int i = 1; i < (int)p.cand.size(); ++i)
+    if (p.best[i] < p.best[bi]) bi = i;
+  p.chosen = bi;
+}
 
 hipblasLtHandle_t g_handle = nullptr;
 std::map<Key, Plan> g_plans;
@@ -97,6 +142,7 @@ bool make_plan(Plan& p, bool ta, bool tb, long m, long n, long k, long lda, long
     if (res[i].state == HIPBLAS_STATUS_SUCCESS && res[i].workspaceSize <= ws) p.cand.push_back(res[i]);
   if (p.cand.empty()) return false;
   p.best.assign(p.cand.size(), 1e30f);
+  p.seen.assign(p.cand.size(), 0);
   if (p.cand.size() == 1) p.chosen = 0;
   return true;
 }
@@ -123,26 +169,31 @@ bool lt_gemm(bool ta, bool tb, long m, long n, long k, const void* A, long lda, 
     p = &it->second;
   }
   const float alpha = 1.f, beta = C ? 1.f : 0.f;
+  if (p->chosen < 0 && !p->pending.empty()) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    const int before = p->chosen;
+    poll_timings(*p, tune_reps());
+    if (before < 0 && p->chosen >= 0 && env_int("LIPA_LT_VERBOSE", 0))
+      fprintf(stderr, "[lt] m=%ld n=%ld k=%ld b=%d C=%d: candidate %d of %zu (%.1f us; first %.1f us)\n", m, n, k,
+              batch, C != nullptr, p->chosen, p->cand.size(), 1e3f * p->best[p->chosen], 1e3f * p->best[0]);
+  }
   int idx = p->chosen;
-  bool timed = false;
+  Plan::Pending timing{-1, nullptr, nullptr};
   if (idx < 0 && (!tune || (getenv("LIPA_DETERMINISTIC") && atoi(getenv("LIPA_DETERMINISTIC"))))) {
-    // reproducible runs, or a shape called once per step (timing would stall the host behind the
-    // device for a dozen steps): the heuristic's first choice, no candidate rotation
+    // reproducible runs, or a shape called once per step: the heuristic's first choice, no rotation
     idx = 0;
   } else if (idx < 0) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     hipStreamIsCapturing(st, &cs);
-    if (cs != hipStreamCaptureStatusNone) {
-      idx = 0;  // no host timing inside a graph capture
-    } else {
+    idx = 0;   // no timing inside a graph capture
+    if (cs == hipStreamCaptureStatusNone) {
       const int nc = (int)p->cand.size();
-      idx = p->calls % nc;
-      timed = true;
-      if (!p->e0) {
-        hipEventCreate(&p->e0);
-        hipEventCreate(&p->e1);
+      idx = p->calls++ % nc;
+      if (p->pending.size() < 64) {
+        std::lock_guard<std::mutex> lk(g_mu);
+        timing = {idx, take_event(*p), take_event(*p)};
+        hipEventRecord(timing.e0, st);
       }
-      hipEventRecord(p->e0, st);
     }
   }
   const hipblasStatus_t s =
@@ -152,21 +203,10 @@ bool lt_gemm(bool ta, bool tb, long m, long n, long k, const void* A, long lda, 
     fprintf(stderr, "hipBLASLt matmul failed (%d) m=%ld n=%ld k=%ld\n", (int)s, m, n, k);
     return false;
   }
-  if (timed) {
-    hipEventRecord(p->e1, st);
-    hipEventSynchronize(p->e1);
-    float ms = 0.f;
-    hipEventElapsedTime(&ms, p->e0, p->e1);
-    if (ms < p->best[idx]) p->best[idx] = ms;
-    if (++p->calls >= (int)p->cand.size() * tune_reps()) {
-      int bi = 0;
-      for (int i = 1; i < (int)p->cand.size(); ++i)
-        if (p->best[i] < p->best[bi]) bi = i;
-      p->chosen = bi;
-      if (env_int("LIPA_LT_VERBOSE", 0))
-        fprintf(stderr, "[lt] m=%ld n=%ld k=%ld b=%d C=%d: candidate %d of %zu (%.1f us; first %.1f us)\n", m, n,
-                k, batch, C != nullptr, bi, p->cand.size(), 1e3f * p->best[bi], 1e3f * p->best[0]);
-    }
+  if (timing.idx >= 0) {
+    hipEventRecord(timing.e1, st);
+    std::lock_guard<std::mutex> lk(g_mu);
+    p->pending.push_back(timing);
   }
   return true;
 }
@@ -181,8 +221,11 @@ void lt_reset() {
     hipblasLtMatrixLayoutDestroy(p.b);
     hipblasLtMatrixLayoutDestroy(p.c);
     hipblasLtMatrixLayoutDestroy(p.d);
-    if (p.e0) hipEventDestroy(p.e0);
-    if (p.e1) hipEventDestroy(p.e1);
+    for (auto& t : p.pending) {
+      hipEventDestroy(t.e0);
+      hipEventDestroy(t.e1);
+    }
+    for (hipEvent_t e : p.pool) hipEventDestroy(e);
   }
   g_plans.clear();
 }
