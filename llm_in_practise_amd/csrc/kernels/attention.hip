@@ -222,10 +222,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const bf16* __restrict__ Q,
     for (int qt = 0; qt < QT; ++qt) {
       const int qa = q0 + 16 * qt + li;
       const int klim = min(causal ? qoff + qa : Skv, kvlen - 1);  // last key this query may see
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sc[kt][qt][r] *= scale_log2;
+      // raw scores: the log2(e)/√D scale is folded into the exponent's FMA below
       if (need_mask) {
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt)
@@ -241,13 +238,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const bf16* __restrict__ Q,
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mn = fmaxf(m_run[qt], mx);
-      const float alpha = (mn == -INFINITY) ? 1.f : fexp2(m_run[qt] - mn);
+      const bool dead = mn == -INFINITY;   // every key so far masked for this query
+      const float alpha = dead ? 1.f : fexp2((m_run[qt] - mn) * scale_log2);
+      const float mc = dead ? 0.f : mn * scale_log2;
       float rs = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = (mn == -INFINITY) ? 0.f : fexp2(sc[kt][qt][r] - mn);
+          const float p = dead ? 0.f : fexp2(fmaf(sc[kt][qt][r], scale_log2, -mc));
           sc[kt][qt][r] = p;
           rs += p;
         }
@@ -255,8 +254,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const bf16* __restrict__ Q,
       rs += __shfl_xor(rs, 32, 64);
       l_run[qt] = l_run[qt] * alpha + rs;
       m_run[qt] = mn;
+      if (__any(alpha != 1.f)) {   // the running max moved for some query of the wave: rescale O
 #pragma unroll
-      for (int dt = 0; dt < ND; ++dt) acc[dt][qt] *= alpha;
+        for (int dt = 0; dt < ND; ++dt) acc[dt][qt] *= alpha;
+      }
       if (dp.thresh) {
         const uint32_t bh = (uint32_t)(b * hq + h);
 #pragma unroll
@@ -300,7 +301,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const bf16* __restrict__ Q,
     }
     if (g == 0)
       lse[((size_t)b * hq + h) * Sq + q] =
-          l_run[qt] > 0.f ? (m_run[qt] + log2f(l_run[qt])) * 0.6931471805599453f : INFINITY;
+          l_run[qt] > 0.f ? (m_run[qt] * scale_log2 + log2f(l_run[qt])) * 0.6931471805599453f : INFINITY;
   }
 }
 
