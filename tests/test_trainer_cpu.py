@@ -143,3 +143,15 @@ def test_trainer_zero3_saves_gathered_adapter(tmp_path):
     sd = load_file(str(tmp_path / "checkpoint-2" / "adapter_model.safetensors"))
     assert sd and all(v.numel() > 0 for v in sd.values())
     assert os.path.isdir(tmp_path / "checkpoint-2" / "global_step2")
+
+
+def test_dx_split_policy():
+    """K-slices for the dX GEMM: only long reductions into an output that leaves CUs idle, and the
+    fewest slices that give every CU a 256x256 tile (gate|up dX at M = 2048 -> 2)."""
+    from llm_in_practise_amd.ops.linear import _dx_split
+    t = lambda m, n, k: (torch.empty(m, n), torch.empty(n, k))  # noqa: E731  (dy [M, N], W [N, K])
+    assert _dx_split(*t(2048, 24576, 4096)) == 2      # gate|up: 128 tiles
+    assert _dx_split(*t(2048, 6144, 4096)) == 1       # qkv: reduction not 4x the output width
+    assert _dx_split(*t(2048, 4096, 12288)) == 1      # down: 384 tiles
+    assert _dx_split(*t(1024, 24576, 4096)) == 4      # 64 tiles -> 4 slices
+    assert _dx_split(*t(128, 24576, 4096)) == 1       # small M: no split
