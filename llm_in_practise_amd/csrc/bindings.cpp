@@ -88,6 +88,10 @@ void launch_lora_dA_pair(const float*, const float*, int, int, const void*, int,
                          int64_t, int64_t, const uint8_t*, const uint8_t*, float, float, int, hipStream_t);
 void launch_lora_dx2(const float*, const float*, int, const void*, const void*, int, int, const uint8_t*,
                      const uint8_t*, float, float, void*, int, int, hipStream_t);
+void launch_lora_dA_multi(int, const float* const*, const int*, float* const*, const int*, const uint64_t*, const float*,
+                          const void*, int, int, int, size_t, hipStream_t);
+void launch_lora_dx_multi(int, const float* const*, const int*, const void* const*, const int*, const uint64_t*,
+                          const float*, void*, int, int, size_t, hipStream_t);
 void launch_lora_apply(void*, int, int, int, const float* const*, const int*, const void* const*, void* const*, const int*, const int*,
                        const int*, hipStream_t);
 void launch_lora_acc(const float*, int, int, const void*, int, void*, int, const void*, int, float*, int64_t, int64_t,
@@ -1000,6 +1004,72 @@ Tensor lora_dx2(Tensor g0, Tensor g1, Tensor a0, Tensor a1, Tensor masks, double
   return out;
 }
 
+// up to 4 adapters on one input x [M, K] (keys / p: each branch's dropout; masks regenerated from the counter RNG
+// over x's row stride, as in the forward's lora_proj):
+//   lora_dx_multi: Σ_i D_i(G_i·A_i)·ds_i -> bf16 [M, K] (the dX GEMM's C matrix)
+//   lora_dA_multi: dA_i [r_i, K] += G_iᵀ·D_i(x)·ds_i (fp32 atomics), one launch
+static void multi_common(const std::vector<Tensor>& gs, int64_t M, std::vector<const float*>& gp, std::vector<int>& ld,
+                         std::vector<int>& r, const char* who) {
+  TORCH_CHECK(gs.size() >= 1 && gs.size() <= 4, who, ": 1..4 branches");
+  for (const Tensor& g : gs) {
+    TORCH_CHECK(g.scalar_type() == at::kFloat && g.dim() == 2 && g.stride(1) == 1 && g.size(0) == M && g.size(1) <= 16 &&
+                    g.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0,
+                who, ": g fp32 [M, r<=16], 16-B aligned rows");
+    gp.push_back(g.data_ptr<float>());
+    ld.push_back(g.stride(0));
+    r.push_back(g.size(1));
+  }
+}
+
+Tensor lora_dx_multi(std::vector<Tensor> gs, std::vector<Tensor> as, std::vector<double> ps, std::vector<int64_t> keys,
+                     int64_t mask_ld) {
+  const int nb = gs.size();
+  TORCH_CHECK((int)as.size() == nb && (int)ps.size() == nb && (int)keys.size() == nb, "lora_dx_multi: per-branch lists");
+  const int64_t M = gs[0].size(0), K = as[0].size(1);
+  std::vector<const float*> gp;
+  std::vector<int> ld, r;
+  multi_common(gs, M, gp, ld, r, "lora_dx_multi");
+  std::vector<const void*> ap;
+  std::vector<float> pf;
+  std::vector<uint64_t> kf;
+  for (int i = 0; i < nb; ++i) {
+    CHECK_BF16(as[i]);
+    TORCH_CHECK(as[i].is_contiguous() && as[i].size(0) == r[i] && as[i].size(1) == K && K % 8 == 0,
+                "lora_dx_multi: A_i [r_i, K]");
+    ap.push_back(as[i].data_ptr());
+    pf.push_back((float)ps[i]);
+    kf.push_back((uint64_t)keys[i]);
+  }
+  Tensor out = at::empty({M, K}, as[0].options());
+  launch_lora_dx_multi(nb, gp.data(), ld.data(), ap.data(), r.data(), kf.data(), pf.data(), out.data_ptr(), M, K,
+                       (size_t)mask_ld, stream());
+  return out;
+}
+
+void lora_dA_multi(std::vector<Tensor> gs, Tensor x, std::vector<Tensor> outs, std::vector<double> ps,
+                   std::vector<int64_t> keys) {
+  const int nb = gs.size();
+  TORCH_CHECK((int)outs.size() == nb && (int)ps.size() == nb && (int)keys.size() == nb, "lora_dA_multi: per-branch lists");
+  CHECK_BF16(x);
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && K % 128 == 0, "lora_dA_multi: x layout");
+  std::vector<const float*> gp;
+  std::vector<int> ld, r;
+  multi_common(gs, M, gp, ld, r, "lora_dA_multi");
+  std::vector<float*> op;
+  std::vector<float> pf;
+  std::vector<uint64_t> kf;
+  for (int i = 0; i < nb; ++i) {
+    TORCH_CHECK(outs[i].scalar_type() == at::kFloat && outs[i].is_contiguous() && outs[i].size(0) == r[i] &&
+                    outs[i].size(1) == K, "lora_dA_multi: out fp32 [r_i, K] contiguous");
+    op.push_back(outs[i].data_ptr<float>());
+    pf.push_back((float)ps[i]);
+    kf.push_back((uint64_t)keys[i]);
+  }
+  launch_lora_dA_multi(nb, gp.data(), ld.data(), op.data(), r.data(), kf.data(), pf.data(), x.data_ptr(), x.stride(0), K,
+                       M, (size_t)x.stride(0), stream());
+}
+
 // ------------------------------------------------------------------ generation (K16, K17)
 // q [B, hq*d] bf16; kc/vc [B, Smax, hkv*d] bf16 contiguous; lens [B] int32 (valid keys per row);
 // max_len >= max(lens) bounds the split count without a host sync.
@@ -1236,6 +1306,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lora_proj_pair", &lora_proj_pair);
   m.def("lora_acc_pair", &lora_acc_pair);
   m.def("lora_dA_pair", &lora_dA_pair);
+  m.def("lora_dx_multi", &lora_dx_multi);
+  m.def("lora_dA_multi", &lora_dA_multi);
   m.def("lora_dx2", &lora_dx2);
   m.def("lora_apply", &lora_apply);
   m.def("gemm_int4", &gemm_int4);

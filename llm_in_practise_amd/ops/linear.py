@@ -501,10 +501,13 @@ class _FusedLinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             fold = [i for i in range(nb) if ctx.keys[i] is None]
             ext_a = ext_b = None
-            if fold:
-                ext_a = _pad_cols(torch.cat([g_list[i].to(dy.dtype) for i in fold], 1))
-                ext_b = torch.cat([bf16_view(ab[2 * i], dy.dtype) for i in fold], 0)            # [R, K]
-                ext_b = F.pad(ext_b, (0, 0, 0, ext_a.shape[1] - ext_b.shape[0])).t().contiguous()  # [K, Rp]
+
+            def fold_ext():   # no-dropout adapters' dx terms as an extra K-slice of the dX GEMM
+                if not fold:
+                    return None, None
+                ea = _pad_cols(torch.cat([g_list[i].to(dy.dtype) for i in fold], 1))
+                eb = torch.cat([bf16_view(ab[2 * i], dy.dtype) for i in fold], 0)            # [R, K]
+                return ea, F.pad(eb, (0, 0, 0, ea.shape[1] - eb.shape[0])).t().contiguous()  # [K, Rp]
             wb = ctx.wdq if ctx.wdq is not None else (base if not dense else weight)
             pair_ok = (ctx.pair and all(k is not None for k in ctx.keys) and not deterministic()
                        and ctx.needs_input_grad[5] and ctx.needs_input_grad[7])
@@ -528,7 +531,29 @@ class _FusedLinearFn(torch.autograd.Function):
                         _notify_grad_ready(ctx.ab_refs[2 * i])
                 pair_ok = False
                 done_dA = True
+            elif (fast and _DX_C and not pair_ok and isinstance(wb, torch.Tensor) and _LT and not _NATIVE_DENSE
+                    and dy.shape[0] >= _LT_MIN_M and _dx_split(dy, wb) == 1 and not deterministic()
+                    and nb <= 4 and all(ab[2 * i].shape[0] <= 16 for i in range(nb)) and x.shape[1] % 128 == 0
+                    and all(ctx.needs_input_grad[5 + 2 * i] for i in range(nb))):
+                # any adapters on this input (q/k/v of a fused projection, an o_proj adapter): their dx
+                # terms summed into ONE bf16 matrix (masks regenerated) that the dX GEMM adds as C, and
+                # every dA in one launch — no per-adapter read-modify-write pass over dx
+                ps = [br.dropout if k is not None else 0.0 for br, k in zip(branches, ctx.keys)]
+                ks = [k or 0 for k in ctx.keys]
+                c = native().lora_dx_multi(list(g_list), [bf16_view(ab[2 * i], dy.dtype) for i in range(nb)], ps, ks,
+                                           x.stride(0))
+                dx = native().lt_dx(dy.contiguous(), wb.contiguous(), 1, True, c)
+                del c
+                dsts = [dest(2 * i) for i in range(nb)]
+                native().lora_dA_multi(list(g_list), x, [o for o, _ in dsts], ps, ks)
+                for i, (o, ret) in enumerate(dsts):
+                    if ret:
+                        grads_ab[2 * i] = o.to(ab[2 * i].dtype)
+                    else:
+                        _notify_grad_ready(ctx.ab_refs[2 * i])
+                done_dA = True
             else:
+                ext_a, ext_b = fold_ext()
                 dx = _base_gemm_t(dy, wb, ext_a, ext_b)
                 done_dA = False
         else:

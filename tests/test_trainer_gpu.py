@@ -123,3 +123,35 @@ def test_lora_pair_kernels_match_single_branch_path(native_ext, monkeypatch):
     for n in g0:
         err = (g0[n] - g1[n]).norm() / g0[n].norm().clamp(min=1e-12)
         assert err < 2e-2, (n, float(err))
+
+
+@pytest.mark.parametrize("targets,r,quant", [(["q_proj", "v_proj"], 8, True), (["q_proj", "k_proj", "v_proj", "o_proj"], 16, True),
+                                             (["q_proj", "k_proj", "v_proj", "o_proj"], 16, False)])
+def test_lora_dx_as_gemm_c_matches_read_modify_write(native_ext, monkeypatch, targets, r, quant):
+    """At training sizes (M >= 256) the adapters' dx terms are summed into one matrix that the dX GEMM
+    adds as C (lora_dx2 / lora_dx_multi) and dA runs in one launch; the loss and LoRA gradients match
+    the per-adapter read-modify-write path (LIPA_LORA_DX_C=0), dropout 0.1 included."""
+    import llm_in_practise_amd.ops.linear as L
+    torch.manual_seed(0)
+    ids = torch.randint(0, 1000, (2, 256), device="cuda")
+    res = {}
+    for mode in (False, True):
+        monkeypatch.setattr(L, "_DX_C", mode)
+        m = Qwen3ForCausalLM.from_config(qwen3_config("qwen3-small"), dtype=torch.bfloat16, device="cuda", seed=0)
+        if quant:
+            quantize_model_nf4(m)
+        pm = get_peft_model(m, LoraConfig(r=r, lora_alpha=2 * r, lora_dropout=0.1, target_modules=targets))
+        pm.fuse_projections()
+        pm.train()
+        for n, p in pm.named_parameters():       # non-zero B so the dx / dA terms carry the masks
+            if p.requires_grad and "lora_B" in n:
+                torch.nn.init.normal_(p, std=0.02, generator=torch.Generator(device="cuda").manual_seed(hash(n) % 1000))
+        L.seed_dropout(42)
+        out = pm(input_ids=ids, labels=ids)
+        out.loss.backward()
+        res[mode] = (out.loss.item(), {n: p.grad.float().clone() for n, p in pm.named_parameters() if p.requires_grad})
+    (l0, g0), (l1, g1) = res[False], res[True]
+    assert abs(l0 - l1) < 1e-3 * abs(l0)
+    for n in g0:
+        err = (g0[n] - g1[n]).norm() / g0[n].norm().clamp(min=1e-12)
+        assert err < 2e-2, (n, float(err))
