@@ -54,6 +54,10 @@ _PAIR_BWD = __import__("os").environ.get("LIPA_LORA_PAIR_BWD", "1") != "0"
 # q+v dropout pair backward: the LoRA dx term as the dX GEMM's C matrix + a separate dA launch
 # (LIPA_LORA_DX_C=0: the fused read-modify-write lora_acc2 pass over dx)
 _DX_C = __import__("os").environ.get("LIPA_LORA_DX_C", "1") != "0"
+# the same for any 1-4 adapters with the masks regenerated (lora_dx_multi + lora_dA_multi): opt-in —
+# re-hashing every mask twice made BASELINE #2 (q,k,v,o r16) 116.7 -> 120.9 ms/step vs the per-adapter
+# fused read-modify-write kernels (LIPA_LORA_DX_MULTI=1 to enable)
+_DX_MULTI = __import__("os").environ.get("LIPA_LORA_DX_MULTI", "0") == "1"
 
 
 def _nf4_dequant_bf16(q: NF4Weight) -> torch.Tensor:
@@ -531,7 +535,7 @@ class _FusedLinearFn(torch.autograd.Function):
                         _notify_grad_ready(ctx.ab_refs[2 * i])
                 pair_ok = False
                 done_dA = True
-            elif (fast and _DX_C and not pair_ok and isinstance(wb, torch.Tensor) and _LT and not _NATIVE_DENSE
+            elif (fast and _DX_MULTI and not pair_ok and isinstance(wb, torch.Tensor) and _LT and not _NATIVE_DENSE
                     and dy.shape[0] >= _LT_MIN_M and _dx_split(dy, wb) == 1 and not deterministic()
                     and nb <= 4 and all(ab[2 * i].shape[0] <= 16 for i in range(nb)) and x.shape[1] % 128 == 0
                     and all(ctx.needs_input_grad[5 + 2 * i] for i in range(nb))):

@@ -137,6 +137,7 @@ def test_lora_dx_as_gemm_c_matches_read_modify_write(native_ext, monkeypatch, ta
     res = {}
     for mode in (False, True):
         monkeypatch.setattr(L, "_DX_C", mode)
+        monkeypatch.setattr(L, "_DX_MULTI", mode)
         m = Qwen3ForCausalLM.from_config(qwen3_config("qwen3-small"), dtype=torch.bfloat16, device="cuda", seed=0)
         if quant:
             quantize_model_nf4(m)
