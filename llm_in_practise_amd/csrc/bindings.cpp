@@ -4,6 +4,7 @@
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
 
+#include <map>
 #include <vector>
 
 // ---- launcher declarations (csrc/kernels/*.hip)
@@ -360,12 +361,12 @@ std::vector<Tensor> nf4_quantize(Tensor w, int64_t blocksize) {
 // decode-shaped y = x·Wᵀ (+ residual): x [M <= 64, K] row-strided, W [N, K] contiguous bf16
 // ---- hipBLASLt frozen-base GEMMs (csrc/kernels/blaslt.hip)
 static void* lt_workspace(size_t& bytes) {
-  static std::vector<Tensor> ws(16);
+  static std::map<int, Tensor> ws;   // one 64 MiB hipBLASLt workspace per device, kept for the process
   const int dev = at::hip::current_device();
   bytes = (size_t)64 << 20;
-  if (!ws[dev].defined())
-    ws[dev] = at::empty({(int64_t)bytes}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, dev));
-  return ws[dev].data_ptr();
+  Tensor& t = ws[dev];
+  if (!t.defined()) t = at::empty({(int64_t)bytes}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, dev));
+  return t.data_ptr();
 }
 
 // y = x·wᵀ (+ residual): x [M, K] (unit column stride), w [N, K] contiguous bf16
