@@ -77,7 +77,8 @@ void launch_moe_combine(int, const void*, const int*, const float*, const void*,
 void launch_moe_wgrad(int, const void*, const void*, const int*, float*, int, int, int, hipStream_t);
 int lora_acc_chunks(int M, int K);
 void launch_lora_proj2(const void*, int, const void*, const void*, int, int, int, float*, int, void*, int, int, uint64_t, float, float,
-                       uint64_t, float, float, size_t, uint8_t*, hipStream_t);
+                       uint64_t, float, float, size_t, uint8_t*, float*, hipStream_t);
+int lora_proj2_ws_floats(int, int);
 void launch_lora_acc2(const float*, int, int, const float*, int, int, const void*, int, void*, int, const void*,
                       const void*, int, float*, float*, int64_t, int64_t, int64_t, int64_t, int, uint64_t, float,
                       uint64_t, float, size_t, const uint8_t*, hipStream_t);
@@ -809,9 +810,13 @@ Tensor lora_proj2(Tensor x, Tensor a0, Tensor a1, optional<Tensor> outb, bool wa
     ldob = outb->stride(0);
   }
   TORCH_CHECK(ob || want_f32, "lora_proj2: no output");
+  const int wsf = lora_proj2_ws_floats(M, K);
+  Tensor ws;
+  if (wsf) ws = at::empty({wsf}, x.options().dtype(at::kFloat));
   launch_lora_proj2(x.data_ptr(), x.stride(0), a0.data_ptr(), a1.data_ptr(), r0, r, K, want_f32 ? of.data_ptr<float>() : nullptr, r,
                     ob, ldob, M, (uint64_t)key0, (float)p0, (float)scale0, (uint64_t)key1, (float)p1, (float)scale1,
-                    (size_t)x.stride(0), keep_bits_ptr(masks, M, K, "lora_proj2"), stream());
+                    (size_t)x.stride(0), keep_bits_ptr(masks, M, K, "lora_proj2"),
+                    wsf ? ws.data_ptr<float>() : nullptr, stream());
   return want_f32 ? of : Tensor();
 }
 

@@ -504,6 +504,138 @@ __global__ __launch_bounds__(NW * 64) void lora_proj2_k(const bf16* __restrict__
   }
 }
 
+// Split-K form of lora_proj2 (the default when K is a multiple of 128).  lora_proj2_k above gives a
+// workgroup 8 rows × all of K, so every workgroup re-reads all of [A0; A1] (128 KB at K = 4096) for
+// 64 KB of x: 3× the compulsory traffic and one exposed round trip — 14 µs without dropout, 23 µs
+// with it and the keep bits (rocprofv3, wait_any 0.63 of wave cycles).  Here a workgroup is 64 rows
+// × KC = 4·NS·32 of K (grid K/KC × M/64 = 256 workgroups at the bench shape): each wave holds its
+// NS B fragments of [A0; A1] for four 16-row MFMA blocks (A traffic 1/4 of x), every load of the
+// wave is issued before the first MFMA, and the 4 waves' partials meet in LDS and leave as one
+// fp32 [M, 16] slab per K chunk; lora_proj2_sum_k adds the slabs in a fixed order (deterministic).
+// Lane (g = lane/16) owns NS·8 CONSECUTIVE k (MFMA step s, k-slot g ↔ k = kl + 8s): the MFMA sum
+// over k is order-free, and the lane's keep bytes are contiguous → one NS-byte store per branch.
+// Dropout masks the bf16 x fragment with a bitwise AND (no convert / multiply / re-round); the
+// 1/(1-p) factor is folded into the output scale.
+template <int NS>
+__global__ __launch_bounds__(256) void lora_proj2s_k(const bf16* __restrict__ X, int ldx, const bf16* __restrict__ W0,
+                                                    const bf16* __restrict__ W1, int r0, int r, int K, int M,
+                                                    uint64_t key0, uint64_t key1, uint32_t thr0, uint32_t thr1,
+                                                    size_t mask_ld, uint8_t* __restrict__ mko, float* __restrict__ ws) {
+  constexpr int KW = NS * 32, KC = 4 * KW;
+  __shared__ f32x4 red[4][4][64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = lane >> 4, n = lane & 15;
+  const int kc = blockIdx.x, m0 = blockIdx.y * 64;
+  const int kl = kc * KC + w * KW + g * (NS * 8);
+  const bool in0 = n < r0, in1 = n >= r0 && n < r;
+  const bf16* wr = in0 ? W0 + (size_t)n * K : (in1 ? W1 + (size_t)(n - r0) * K : W0);
+  bf16x8 bv[NS], xv[4][NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) bv[s] = *reinterpret_cast<const bf16x8*>(wr + kl + 8 * s);
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int row = min(m0 + 16 * b + n, M - 1);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) xv[b][s] = *reinterpret_cast<const bf16x8*>(X + (size_t)row * ldx + kl + 8 * s);
+  }
+  f32x4 acc[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if ((thr0 | thr1) == 0) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const bf16x8 bb = (in0 || in1) ? bv[s] : bf16x8{};
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xv[b][s], bb, acc[b], 0, 0, 0);
+    }
+  } else {
+    // every keep byte first: the hash is independent of the loads in flight, so it runs under them
+    uint32_t kp0[4], kp1[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int row = min(m0 + 16 * b + n, M - 1);
+      kp0[b] = 0;
+      kp1[b] = 0;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const size_t v8 = ((size_t)row * mask_ld + kl + 8 * s) >> 3;
+        kp0[b] |= (thr0 ? dropout_keep8(key0, v8, thr0) : 0xFFu) << (8 * s);
+        kp1[b] |= (thr1 ? dropout_keep8(key1, v8, thr1) : 0xFFu) << (8 * s);
+      }
+      const int mg = m0 + 16 * b + n;
+      if (mko && mg < M) {   // the keep bits for the backward (1 bit / element), NS bytes per branch
+        const size_t mi = (size_t)mg * (K >> 3) + (kl >> 3);
+        if constexpr (NS == 4) {
+          *reinterpret_cast<uint32_t*>(mko + mi) = kp0[b];
+          *reinterpret_cast<uint32_t*>(mko + (size_t)M * (K >> 3) + mi) = kp1[b];
+        } else if constexpr (NS == 2) {
+          *reinterpret_cast<uint16_t*>(mko + mi) = (uint16_t)kp0[b];
+          *reinterpret_cast<uint16_t*>(mko + (size_t)M * (K >> 3) + mi) = (uint16_t)kp1[b];
+        } else {
+          mko[mi] = (uint8_t)kp0[b];
+          mko[(size_t)M * (K >> 3) + mi] = (uint8_t)kp1[b];
+        }
+      }
+    }
+    bf16x8 b0[NS], b1[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      b0[s] = in0 ? bv[s] : bf16x8{};
+      b1[s] = in1 ? bv[s] : bf16x8{};
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const uint32_t k0 = kp0[b] >> (8 * s), k1 = kp1[b] >> (8 * s);
+        const u32x4 xw = __builtin_bit_cast(u32x4, xv[b][s]);
+        u32x4 a0, a1;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const uint32_t m0w = (0u - ((k0 >> (2 * p)) & 1u)) & 0xFFFFu, m0h = (0u - ((k0 >> (2 * p + 1)) & 1u)) << 16;
+          const uint32_t m1w = (0u - ((k1 >> (2 * p)) & 1u)) & 0xFFFFu, m1h = (0u - ((k1 >> (2 * p + 1)) & 1u)) << 16;
+          a0[p] = xw[p] & (m0w | m0h);
+          a1[p] = xw[p] & (m1w | m1h);
+        }
+        acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a0), b0[s], acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a1), b1[s], acc[b], 0, 0, 0);
+      }
+  }
+#pragma unroll
+  for (int b = 0; b < 4; ++b) red[w][b][lane] = acc[b];
+  __syncthreads();
+  // wave w sums row block w over the 4 waves' K ranges; D layout: col j = lane & 15, rows 4g + i
+  f32x4 t = red[0][w][lane];
+#pragma unroll
+  for (int v = 1; v < 4; ++v) t += red[v][w][lane];
+  if (n >= r) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + 16 * w + 4 * g + i;
+    if (m < M) ws[((size_t)kc * M + m) * 16 + n] = t[i];
+  }
+}
+
+// out[m, j] = sc_j · Σ_c ws[c][m][j] (fixed order), fp32 and / or bf16
+__global__ __launch_bounds__(256) void lora_proj2_sum_k(const float* __restrict__ ws, int nkc, int M, int r, int r0,
+                                                       float sc0, float sc1, float* __restrict__ outf, int ldof,
+                                                       bf16* __restrict__ outb, int ldob) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  const int m = idx >> 4, j = idx & 15;
+  if (m >= M || j >= r) return;
+  // all slab loads in flight at once (a runtime-trip loop issues them one round trip apart)
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < nkc; c0 += 8) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      if (c0 + c < nkc) v[c] += ws[((size_t)(c0 + c) * M + m) * 16 + j];
+  }
+  float t = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+  t *= j < r0 ? sc0 : sc1;
+  if (outf) outf[(size_t)m * ldof + j] = t;
+  if (outb) outb[(size_t)m * ldob + j] = (bf16)t;
+}
+
 // lora_acc (matrix cores) for two dropout branches over the same x / dx, R = 8 rows each:
 //   out_i[j, k] += Σ_m G_i[m, j]·D_i(X)[m, k]          (dA of each adapter)
 //   DX[m, k]    += Σ_i D_i(Σ_j G_i[m, j]·A_i[j, k])    (both adapters' input gradients, one RW of dx)
@@ -878,13 +1010,40 @@ void launch_lora_acc(const float* G, int ldg, int r, const void* X, int ldx, voi
   LIPA_CHECK_LAUNCH();
 }
 
+// split-K lora_proj2s_k: NS (K per wave / 32) giving >= 256 workgroups, 0 = not applicable (old kernel)
+int lora_proj2_ns(int M, int K) {
+  static const int impl = [] { const char* e = getenv("LIPA_PROJ2_IMPL"); return e ? atoi(e) : 1; }();
+  if (impl == 0 || M <= 0) return 0;
+  const int nrb = (M + 63) / 64;
+  for (int ns = 4; ns >= 1; ns /= 2)
+    if (K % (128 * ns) == 0 && (nrb * (K / (128 * ns)) >= 256 || ns == 1)) return ns;
+  return 0;
+}
+int lora_proj2_ws_floats(int M, int K) {
+  const int ns = lora_proj2_ns(M, K);
+  return ns ? (K / (128 * ns)) * M * 16 : 0;
+}
+
 // two branches sharing x: W = [A0; A1] ([r0 + r1 <= 16, K]); outputs [M, r0 + r1] (fp32 and/or bf16)
 void launch_lora_proj2(const void* X, int ldx, const void* W0, const void* W1, int r0, int r, int K, float* outf, int ldof, void* outb,
                        int ldob, int M, uint64_t key0, float p0, float scale0, uint64_t key1, float p1, float scale1,
-                       size_t mask_ld, uint8_t* mko, hipStream_t st) {
+                       size_t mask_ld, uint8_t* mko, float* ws, hipStream_t st) {
   const uint32_t thr0 = p0 > 0.f ? (uint32_t)(p0 * 65536.0f + 0.5f) : 0u;
   const uint32_t thr1 = p1 > 0.f ? (uint32_t)(p1 * 65536.0f + 0.5f) : 0u;
   const float ds0 = p0 > 0.f ? 1.f / (1.f - p0) : 1.f, ds1 = p1 > 0.f ? 1.f / (1.f - p1) : 1.f;
+  const int ns = lora_proj2_ns(M, K);
+  if (ws && ns) {
+    dim3 grid(K / (128 * ns), (M + 63) / 64);
+#define P(NS_)                                                                                                      \
+  lora_proj2s_k<NS_><<<grid, 256, 0, st>>>((const bf16*)X, ldx, (const bf16*)W0, (const bf16*)W1, r0, r, K, M, key0, \
+                                           key1, thr0, thr1, mask_ld, mko, ws)
+    if (ns == 4) P(4); else if (ns == 2) P(2); else P(1);
+#undef P
+    lora_proj2_sum_k<<<(M * 16 + 255) / 256, 256, 0, st>>>(ws, grid.x, M, r, r0, scale0 * ds0, scale1 * ds1, outf, ldof,
+                                                          (bf16*)outb, ldob);
+    LIPA_CHECK_LAUNCH();
+    return;
+  }
   const int rw = M < 4096 ? 8 : 16;
   const int grid = (M + rw - 1) / rw;
   if (K % (16 * 32) == 0 && rw == 8)

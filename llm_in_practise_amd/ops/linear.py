@@ -75,6 +75,18 @@ def _nf4_dequant_bf16(q: NF4Weight) -> torch.Tensor:
 # NF4 weights expanded ahead of use on a side stream: {id(NF4Weight): (bf16 tensor, ready event)}
 _PREFETCHED: dict = {}
 _SIDE: dict = {}
+# LIPA_LORA_SIDE=1: the q+v LoRA projection (lora_proj2: VALU-bound dropout hashing + a skinny MFMA
+# reduction) runs on a side stream beside the NF4 expansion and the base GEMM of the same projection;
+# the main stream joins it before lora_apply
+_LORA_SIDE = __import__("os").environ.get("LIPA_LORA_SIDE", "0") == "1"
+_LSIDE: dict = {}
+
+
+def _lora_side_stream(dev):
+    s = _LSIDE.get(dev)
+    if s is None:
+        s = _LSIDE[dev] = torch.cuda.Stream(device=dev)
+    return s
 # which of a decoder layer's projections prefetch_dequant expands while attention runs
 # (LIPA_NF4_OVERLAP: comma list of o,gu,down; empty = off)
 _OVERLAP = tuple(t for t in __import__("os").environ.get("LIPA_NF4_OVERLAP", "").split(",") if t)
@@ -334,6 +346,7 @@ class _FusedLinearFn(torch.autograd.Function):
         dense = not isinstance(base, NF4Weight)
         xa_list, keys = [], []
         ext_a = ext_b = None
+        side_join = None
         ctx.masks = None
         fast = bool(branches) and _fast_lora_ok(x, branches)
         need_xa = any(ctx.needs_input_grad[5:])     # (grad mode is off inside forward: ask autograd)
@@ -350,8 +363,21 @@ class _FusedLinearFn(torch.autograd.Function):
                 # training with dropout on both: keep the masks' bits (2 bits / element of x) for lora_acc2
                 masks = (torch.empty(2, x.shape[0], x.shape[1] // 8, dtype=torch.uint8, device=x.device)
                          if need_xa and all(k is not None for k in keys) and _KEEP_BITS else None)
-                xa2 = native().lora_proj2(x, a0, a1, None, True, ps[0], keys[0] or 0, branches[0].scaling,
-                                          ps[1], keys[1] or 0, branches[1].scaling, masks)
+                if _LORA_SIDE and not torch.cuda.is_current_stream_capturing():
+                    main = torch.cuda.current_stream(x.device)
+                    side = _lora_side_stream(x.device)
+                    side.wait_stream(main)
+                    with torch.cuda.stream(side):
+                        xa2 = native().lora_proj2(x, a0, a1, None, True, ps[0], keys[0] or 0, branches[0].scaling,
+                                                  ps[1], keys[1] or 0, branches[1].scaling, masks)
+                    xa2.record_stream(main)
+                    if masks is not None:
+                        masks.record_stream(side)
+                    x.record_stream(side)
+                    side_join = side
+                else:
+                    xa2 = native().lora_proj2(x, a0, a1, None, True, ps[0], keys[0] or 0, branches[0].scaling,
+                                              ps[1], keys[1] or 0, branches[1].scaling, masks)
                 ctx.masks = masks
                 r0 = a0.shape[0]
                 xa_list = [xa2[:, :r0], xa2[:, r0:]]
@@ -416,6 +442,8 @@ class _FusedLinearFn(torch.autograd.Function):
             bs = [bf16_view(b, x.dtype) for b in ab[1::2]]
             # training: the same pass writes Bᵀ [r, n] for the backward's dy·B projection (no transpose kernel)
             bts = [torch.empty(b.shape[1], b.shape[0], dtype=x.dtype, device=x.device) for b in bs] if need_xa else []
+            if side_join is not None:
+                torch.cuda.current_stream(x.device).wait_stream(side_join)
             native().lora_apply(y, xa_list, bs, [br.c0 for br in branches], bts)
             ctx.bts = bts or None
             if not need_xa:

@@ -576,7 +576,8 @@ def test_lora_fused_kernels(native_ext, M, K, r, p):
     assert rel_err(da2, gg.t() @ x.float()) < 1e-2
 
 
-@pytest.mark.parametrize("M,K,p0,p1", [(2048, 4096, 0.1, 0.1), (1000, 1024, 0.05, 0.0), (77, 512, 0.0, 0.2)])
+@pytest.mark.parametrize("M,K,p0,p1", [(2048, 4096, 0.1, 0.1), (1000, 1024, 0.05, 0.0), (77, 512, 0.0, 0.2),
+                                       (640, 2048, 0.0, 0.0), (96, 640, 0.1, 0.1)])
 def test_lora_two_branch_kernels(native_ext, M, K, p0, p1):
     """lora_proj2 / lora_acc2 (q_proj + v_proj over one x pass) vs fp32 with each branch's own
     regenerated dropout mask."""
