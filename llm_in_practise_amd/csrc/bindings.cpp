@@ -115,6 +115,9 @@ int car_max_blocks();
 void launch_custom_allreduce(int, const void* const*, void* const*, uint32_t* const*, int*, int, int, uint32_t, size_t,
                              bool, float, void*, int, hipStream_t);
 void launch_dropout_fwd(const void*, void*, size_t, uint64_t, float, hipStream_t);
+bool embedding_supported(int64_t, int64_t);
+void launch_embedding_fwd(const void*, const int64_t*, void*, int64_t, int64_t, int64_t, int64_t, hipStream_t);
+void launch_embedding_bwd(const void*, int, const int64_t*, float*, int64_t, int64_t, int64_t, int64_t, hipStream_t);
 void launch_dropout_bwd_add(void*, const void*, size_t, uint64_t, float, hipStream_t);
 
 namespace {
@@ -281,6 +284,31 @@ Tensor gelu_bwd(Tensor dy, Tensor x) {
 }
 
 // ------------------------------------------------------------------ dropout (counter RNG)
+// embedding gather: weight [V, D] (any dtype, D·elem % 16 == 0), ids int64 (any shape) → [*ids, D]
+Tensor embedding_fwd(Tensor weight, Tensor ids) {
+  CHECK_CONTIG(weight);
+  TORCH_CHECK(weight.dim() == 2 && ids.scalar_type() == at::kLong, "embedding_fwd: weight [V, D], int64 ids");
+  const int64_t V = weight.size(0), D = weight.size(1), el = weight.element_size();
+  TORCH_CHECK(embedding_supported(D, el), "embedding_fwd: row bytes % 16");
+  Tensor idc = ids.contiguous();
+  auto sizes = idc.sizes().vec();
+  sizes.push_back(D);
+  Tensor out = at::empty(sizes, weight.options());
+  launch_embedding_fwd(weight.data_ptr(), idc.data_ptr<int64_t>(), out.data_ptr(), idc.numel(), D, el, V, stream());
+  return out;
+}
+// gradient of the gather: fp32 [V, D] (scatter-add of dout rows; padding_idx < 0: none)
+Tensor embedding_bwd(Tensor dout, Tensor ids, int64_t V, int64_t padding_idx) {
+  TORCH_CHECK(dout.scalar_type() == at::kBFloat16 || dout.scalar_type() == at::kFloat, "embedding_bwd: bf16/fp32");
+  Tensor d = dout.contiguous(), idc = ids.contiguous();
+  const int64_t D = d.size(-1);
+  TORCH_CHECK(D % 8 == 0 && d.numel() == idc.numel() * D, "embedding_bwd: shapes");
+  Tensor gw = at::zeros({V, D}, d.options().dtype(at::kFloat));
+  launch_embedding_bwd(d.data_ptr(), d.scalar_type() == at::kFloat ? 1 : 0, idc.data_ptr<int64_t>(), gw.data_ptr<float>(),
+                       idc.numel(), D, V, padding_idx, stream());
+  return gw;
+}
+
 Tensor dropout_fwd(Tensor x, double p, int64_t key) {
   CHECK_BF16(x);
   CHECK_CONTIG(x);
@@ -1301,6 +1329,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_bwd", &gelu_bwd);
   m.def("ce_fwd_bwd", &ce_fwd_bwd);
   m.def("dropout_fwd", &dropout_fwd);
+  m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_bwd", &embedding_bwd);
   m.def("dropout_bwd_add", &dropout_bwd_add);
   m.def("grad_norm", &grad_norm);
   m.def("decode_attention", &decode_attention);

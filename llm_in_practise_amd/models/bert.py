@@ -21,6 +21,7 @@ import torch.nn.functional as F
 from ..ops.activation import gelu
 from ..ops.attention import sdpa_bshd
 from ..ops.norm import LayerNorm
+from ..ops.embedding import Embedding
 
 
 @dataclasses.dataclass
@@ -50,9 +51,9 @@ class BertConfig:
 class _Embeddings(nn.Module):
     def __init__(self, c: BertConfig):
         super().__init__()
-        self.word_embeddings = nn.Embedding(c.vocab_size, c.hidden_size, padding_idx=c.pad_token_id)
-        self.position_embeddings = nn.Embedding(c.max_position_embeddings, c.hidden_size)
-        self.token_type_embeddings = nn.Embedding(c.type_vocab_size, c.hidden_size)
+        self.word_embeddings = Embedding(c.vocab_size, c.hidden_size, padding_idx=c.pad_token_id)
+        self.position_embeddings = Embedding(c.max_position_embeddings, c.hidden_size)
+        self.token_type_embeddings = Embedding(c.type_vocab_size, c.hidden_size)
         self.LayerNorm = LayerNorm(c.hidden_size, eps=c.layer_norm_eps)
         self.dropout = nn.Dropout(c.hidden_dropout_prob)
 

@@ -22,6 +22,7 @@ from ..ops.attention import sdpa_bshd
 from ..ops.loss import fused_linear_cross_entropy
 from ..ops.norm import LayerNorm
 from ..ops.rope import apply_rope
+from ..ops.embedding import Embedding
 from .layers import MoEFeedForward
 
 
@@ -78,7 +79,7 @@ class DeepSeekLike(nn.Module):
     def __init__(self, vocab_size=30000, block_size=256, n_layer=6, n_head=8, d_model=768, dropout=0.1,
                  latent_dim=None, num_experts=8, top_k=2, num_shared=2, rope_theta=10000.0, moe_dispatch="sparse"):
         super().__init__()
-        self.tok_emb = nn.Embedding(vocab_size, d_model)
+        self.tok_emb = Embedding(vocab_size, d_model)
         self.drop = nn.Dropout(dropout)
         self.blocks = nn.ModuleList([
             TransformerBlock(d_model, n_head, 4.0, dropout, latent_dim, num_experts, top_k, num_shared, moe_dispatch)

@@ -4,7 +4,7 @@
 (causal), GELU 4× MLP, tied head, and one of:
   * ``pos="sinusoidal"``: fixed table registered as ``pos_emb`` buffer [1, block, d]
     (``ddp_gpt_wikitext2.py:134-139``, ``GPTLike_wikitext2_fixed_pe.py``);
-  * ``pos="learned"``: ``pos_emb = nn.Embedding(block, d)`` (``GPTLike_wikitext2_learned_pe.py:166``,
+  * ``pos="learned"``: ``pos_emb = Embedding(block, d)`` (``GPTLike_wikitext2_learned_pe.py:166``,
     ``temp/ddp_gpt_wikitext2.py:176``).
 ``init="xavier"`` is the C/D family (``ddp_gpt_wikitext2.py:147-155``), ``init="normal"`` the
 B family / temp scripts (N(0, 0.02)).  State-dict keys are the reference's, so
@@ -24,6 +24,7 @@ import torch.nn as nn
 
 from ..ops.loss import fused_linear_cross_entropy
 from ..ops.norm import LayerNorm
+from ..ops.embedding import Embedding
 from .layers import MultiheadAttention, TransformerEncoderLayer, sinusoidal_pe
 
 
@@ -77,7 +78,7 @@ class GPTLike(nn.Module):
         super().__init__()
         self.config = dict(vocab_size=vocab_size, block_size=block_size, n_layer=n_layer, n_head=n_head,
                            d_model=d_model, dropout=dropout, pos=pos, init=init, tie=tie)
-        self.tok_emb = nn.Embedding(vocab_size, d_model)
+        self.tok_emb = Embedding(vocab_size, d_model)
         self.drop = nn.Dropout(dropout)
         self.blocks = nn.ModuleList([TransformerBlock(d_model, n_head, dropout) for _ in range(n_layer)])
         self.ln_f = LayerNorm(d_model)
@@ -86,7 +87,7 @@ class GPTLike(nn.Module):
             self.head.weight = self.tok_emb.weight
         self.block_size, self.d_model, self.pos = block_size, d_model, pos
         if pos == "learned":
-            self.pos_emb = nn.Embedding(block_size, d_model)
+            self.pos_emb = Embedding(block_size, d_model)
         else:
             self.register_buffer("pos_emb", sinusoidal_pe(block_size, d_model).unsqueeze(0), persistent=True)
         self.init = init
@@ -113,7 +114,7 @@ class GPTLike(nn.Module):
     def resize_token_embeddings(self, n: int):
         """Grow/shrink the vocabulary keeping the tie (``temp/ddp_gpt_bpe_tokenizer.py:215-247``)."""
         old = self.tok_emb
-        new = nn.Embedding(n, self.d_model, device=old.weight.device, dtype=old.weight.dtype)
+        new = Embedding(n, self.d_model, device=old.weight.device, dtype=old.weight.dtype)
         nn.init.normal_(new.weight, 0.0, 0.02)
         k = min(n, old.num_embeddings)
         with torch.no_grad():
@@ -157,7 +158,7 @@ class SimpleTransformer(nn.Module):
     def __init__(self, vocab_size, d_model=256, nhead=4, num_layers=6, max_len=64, dropout=0.1, causal=False):
         super().__init__()
         self.d_model, self.max_len, self.causal = d_model, max_len, causal
-        self.token_embedding = nn.Embedding(vocab_size, d_model)
+        self.token_embedding = Embedding(vocab_size, d_model)
         self.register_buffer("pos_embedding", sinusoidal_pe(max_len, d_model).unsqueeze(0))
         self.transformer = _Stack(d_model, nhead, num_layers, dropout)
         self.output_layer = nn.Linear(d_model, vocab_size)

@@ -19,6 +19,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.norm import LayerNorm
+from ..ops.embedding import Embedding
 from .layers import TransformerDecoderLayer, TransformerEncoderLayer
 
 
@@ -26,8 +27,8 @@ class MiniGPT(nn.Module):
     def __init__(self, vocab_size, embed_dim=64, n_heads=2, n_layers=2, dropout=0.1, seq_len=16,
                  reference_layout: bool = True, causal: bool = False, dim_feedforward: int = 2048):
         super().__init__()
-        self.token_embed = nn.Embedding(vocab_size, embed_dim)
-        self.pos_embed = nn.Embedding(seq_len, embed_dim)
+        self.token_embed = Embedding(vocab_size, embed_dim)
+        self.pos_embed = Embedding(seq_len, embed_dim)
         self.layers = nn.ModuleList([
             TransformerDecoderLayer(embed_dim, n_heads, dim_feedforward, dropout, batch_first=not reference_layout)
             for _ in range(n_layers)])
@@ -70,7 +71,7 @@ class MiniGPT2(nn.Module):
         super().__init__()
         c = config
         self.config, self.causal = c, causal
-        self.embed = nn.Embedding(c.vocab_size, c.embed_dim)
+        self.embed = Embedding(c.vocab_size, c.embed_dim)
         self.pos_embed = nn.Parameter(torch.zeros(1, c.seq_len, c.embed_dim))
         self.transformer = _Encoder(c)
         self.ln = LayerNorm(c.embed_dim)

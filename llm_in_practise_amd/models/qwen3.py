@@ -34,6 +34,7 @@ from ..ops.norm import RMSNorm, rms_norm, rms_norm_residual
 from ..ops.rope import apply_rope, qk_norm_rope
 from ..parallel.tensor_parallel import tp_all_reduce
 from ..peft.lora import base_of
+from ..ops.embedding import Embedding
 from .common import CausalLMOutput, FusedProjection, KVCache, PackedPrefill, can_fuse, project
 
 
@@ -263,7 +264,7 @@ class Qwen3Model(nn.Module):
     def __init__(self, cfg: Qwen3Config):
         super().__init__()
         self.cfg = cfg
-        self.embed_tokens = nn.Embedding(cfg.vocab_size, cfg.hidden_size)
+        self.embed_tokens = Embedding(cfg.vocab_size, cfg.hidden_size)
         self.layers = nn.ModuleList([Qwen3DecoderLayer(cfg, i) for i in range(cfg.num_hidden_layers)])
         self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
         inv, attn_factor = ref.rope_inv_freq(cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)

@@ -24,6 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.norm import LayerNorm
+from ..ops.embedding import Embedding
 from .layers import MultiheadAttention, sinusoidal_pe
 
 
@@ -32,7 +33,7 @@ class ScaledEmbedding(nn.Module):
 
     def __init__(self, vocab_size: int, d_model: int):
         super().__init__()
-        self.emb = nn.Embedding(vocab_size, d_model)
+        self.emb = Embedding(vocab_size, d_model)
         self.scale = math.sqrt(d_model)
 
     def forward(self, x):
@@ -162,8 +163,8 @@ class MiniBert(nn.Module):
     def __init__(self, vocab_size: int, hidden_size: int = 128, num_heads: int = 4, num_layers: int = 2,
                  ffn_size: int = 256, max_len: int = 256, num_classes: int = 2, dropout: float = 0.1):
         super().__init__()
-        self.token_emb = nn.Embedding(vocab_size, hidden_size)
-        self.pos_emb = nn.Embedding(max_len, hidden_size)
+        self.token_emb = Embedding(vocab_size, hidden_size)
+        self.pos_emb = Embedding(max_len, hidden_size)
         self.dropout = nn.Dropout(dropout)
         self.layers = nn.ModuleList([_BertLayer(hidden_size, num_heads, ffn_size, dropout) for _ in range(num_layers)])
         self.norm = LayerNorm(hidden_size)
@@ -211,8 +212,8 @@ class NotebookGPT(nn.Module):
     def __init__(self, config: NotebookGPTConfig):
         super().__init__()
         self.config = c = config
-        self.tok_emb = nn.Embedding(c.vocab_size, c.n_embd)
-        self.pos_emb = nn.Embedding(c.max_seq_len, c.n_embd)
+        self.tok_emb = Embedding(c.vocab_size, c.n_embd)
+        self.pos_emb = Embedding(c.max_seq_len, c.n_embd)
         self.drop = nn.Dropout(c.dropout)
         self.blocks = nn.ModuleList([_GPTBlock(c) for _ in range(c.n_layer)])
         self.ln_f = LayerNorm(c.n_embd)

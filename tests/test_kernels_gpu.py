@@ -748,3 +748,28 @@ def test_lora_multi_branch_backward(native_ext, M, K, rs, ps):
     native_ext.lora_dA_multi(gs, x, outs, ps, keys)
     for o, g, xd in zip(outs, gs, xds):
         assert rel_err(o - 0.5, g.t() @ xd.float()) < 1e-2
+
+
+# ----------------------------------------------------------------------------- embedding (K6)
+@pytest.mark.parametrize("V,D,dtype,pad", [(1000, 128, torch.bfloat16, None), (50, 64, torch.float32, 3),
+                                           (151, 4096, torch.bfloat16, 0)])
+def test_embedding_gather_scatter_add(native_ext, V, D, dtype, pad):
+    """ops.Embedding (embedding.hip) vs torch F.embedding: forward bit-exact, weight gradient vs the
+    fp32 scatter-add (repeated ids, padding_idx rows get no gradient)."""
+    from llm_in_practise_amd.ops.embedding import Embedding
+    torch.manual_seed(0)
+    emb = Embedding(V, D, padding_idx=pad).to(DEV, dtype)
+    ids = torch.randint(0, V, (4, 37), device=DEV)
+    ids[0, :5] = 7                                       # repeated ids accumulate
+    if pad is not None:
+        ids[1, :3] = pad
+    out = emb(ids)
+    ref = torch.nn.functional.embedding(ids, emb.weight.detach(), pad)
+    assert out.shape == (4, 37, D) and torch.equal(out, ref)
+    g = torch.randn(4, 37, D, device=DEV, dtype=dtype)
+    out.backward(g)
+    want = torch.zeros(V, D, device=DEV).index_add_(0, ids.reshape(-1), g.reshape(-1, D).float())
+    if pad is not None:
+        want[pad] = 0
+    assert emb.weight.grad.dtype == dtype
+    assert rel_err(emb.weight.grad, want) < 1e-2
