@@ -40,6 +40,8 @@ void launch_absmax_t(const float*, const uint8_t*, const float*, const float*, c
                      hipStream_t);
 void launch_nf4_quantize(const void*, uint8_t*, float*, size_t, hipStream_t);
 void launch_nf4_dequant2(const uint8_t*, const float*, void*, size_t, hipStream_t);
+void launch_nf4_dequant_bg(int, const uint8_t* const*, const float* const*, void* const*, const size_t*, int,
+                           hipStream_t);
 int skinny_splits(int, int);
 bool lt_gemm(bool, bool, long, long, long, const void*, long, const void*, long, const void*, void*, long, int, long,
              long, long, void*, size_t, hipStream_t, bool);
@@ -527,6 +529,34 @@ Tensor nf4_dequant_fast(Tensor codes, Tensor absmax, int64_t N, int64_t K) {
   auto w = at::empty({N, K}, codes.options().dtype(at::kBFloat16));
   launch_nf4_dequant2(codes.data_ptr<uint8_t>(), absmax.data_ptr<float>(), w.data_ptr(), N * K, stream());
   return w;
+}
+
+// background expansion of up to 4 NF4 weights in one small persistent grid (see gemm.hip)
+std::vector<Tensor> nf4_dequant_bg(std::vector<Tensor> codes, std::vector<Tensor> absmax, std::vector<int64_t> N,
+                                   std::vector<int64_t> K, int64_t grid) {
+  const int nj = (int)codes.size();
+  TORCH_CHECK(nj >= 1 && nj <= 4 && (int)absmax.size() == nj && (int)N.size() == nj && (int)K.size() == nj && grid > 0,
+              "nf4_dequant_bg: 1-4 jobs");
+  std::vector<Tensor> out;
+  const uint8_t* cp[4];
+  const float* ap[4];
+  void* wp[4];
+  size_t ne[4];
+  for (int j = 0; j < nj; ++j) {
+    CHECK_CUDA(codes[j]);
+    CHECK_CONTIG(codes[j]);
+    CHECK_CONTIG(absmax[j]);
+    TORCH_CHECK(codes[j].numel() * 2 == N[j] * K[j] && K[j] % 64 == 0 && absmax[j].scalar_type() == at::kFloat &&
+                    absmax[j].numel() * 64 == N[j] * K[j] && reinterpret_cast<uintptr_t>(codes[j].data_ptr()) % 16 == 0,
+                "nf4_dequant_bg: job shapes");
+    out.push_back(at::empty({N[j], K[j]}, codes[j].options().dtype(at::kBFloat16)));
+    cp[j] = codes[j].data_ptr<uint8_t>();
+    ap[j] = absmax[j].data_ptr<float>();
+    wp[j] = out.back().data_ptr();
+    ne[j] = (size_t)(N[j] * K[j]);
+  }
+  launch_nf4_dequant_bg(nj, cp, ap, wp, ne, (int)grid, stream());
+  return out;
 }
 
 Tensor nf4_dequant(Tensor codes, optional<Tensor> absmax, optional<Tensor> qabs, optional<Tensor> absmax2,
@@ -1355,6 +1385,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequant", &nf4_dequant);
   m.def("nf4_dequant_fast", &nf4_dequant_fast);
+  m.def("nf4_dequant_bg", &nf4_dequant_bg);
   m.def("gemm_skinny", &gemm_skinny);
   m.def("lt_linear", &lt_linear);
   m.def("lt_dx", &lt_dx);

@@ -227,6 +227,11 @@ def _overlap_on() -> bool:
     return bool(_OVERLAP)
 
 
+def _nf4_bg_on() -> bool:
+    from ..ops.linear import _NF4_BG
+    return _NF4_BG > 0
+
+
 class Qwen3DecoderLayer(nn.Module):
     def __init__(self, cfg: Qwen3Config, layer_idx: int):
         super().__init__()
@@ -249,6 +254,18 @@ class Qwen3DecoderLayer(nn.Module):
             else:
                 bases += [base_of(m)[0] for m in mods]
         prefetch_dequant(bases)
+
+    def prefetch_nf4_bg(self):
+        """Queue this layer's NF4 expansions (fused q|k|v, o, fused gate|up, down) on the background
+        grid (ops/linear.py prefetch_dequant_bg)."""
+        from ..ops.linear import prefetch_dequant_bg
+        a, m = self.self_attn, self.mlp
+        bases = [a._qkv.base] if a._qkv is not None else [base_of(p)[0] for p in (a.q_proj, a.k_proj, a.v_proj)]
+        bases += [base_of(a.o_proj)[0]]
+        bases += [m._gu.base] if m._gu is not None else [base_of(p)[0] for p in (m.gate_proj, m.up_proj)]
+        bases += [base_of(m.down_proj)[0]]
+        for i in range(0, len(bases), 4):
+            prefetch_dequant_bg(bases[i:i + 4])
 
     def forward(self, x, cos, sin, B, S, cache=None, start=0, kv_lens=None):
         xn, skip = rms_norm_residual(x, self.input_layernorm.weight, self.input_layernorm.eps)
@@ -288,7 +305,11 @@ class Qwen3Model(nn.Module):
         x = self.embed_tokens(input_ids).reshape(B * S, -1)
         if self.pp is not None:
             x = self.pp.enter(x)        # stages > 0: the previous stage's hidden states
-        for layer in self.layers:
+        bg = _nf4_bg_on() and self.training and cache is None and torch.is_grad_enabled() \
+            and not self.gradient_checkpointing and x.is_cuda and not torch.cuda.is_current_stream_capturing()
+        for i, layer in enumerate(self.layers):
+            if bg and i + 1 < len(self.layers):
+                self.layers[i + 1].prefetch_nf4_bg()   # expanded beside this layer's kernels
             if self.gradient_checkpointing and self.training and cache is None:
                 x = lora_checkpoint(layer, x, cos, sin, B, S, None, 0, kv_lens)
             else:

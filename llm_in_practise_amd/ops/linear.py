@@ -117,6 +117,33 @@ def prefetch_dequant(bases, after: torch.Tensor | None = None):
             _PREFETCHED[id(b)] = (t, ev)
 
 
+# LIPA_NF4_BG=G (> 0): the NEXT decoder layer's NF4 weights are expanded by ONE small persistent grid
+# of G workgroups (nf4_dequant_bg_k) on a side stream while this layer runs; the GEMMs (compute-bound,
+# one workgroup per CU, little HBM traffic) leave room for it, where the full-size expansion grid
+# (one workgroup per 8 K elements) would take their CU slots.  0 = off (each GEMM expands its own).
+_NF4_BG = int(__import__("os").environ.get("LIPA_NF4_BG", "0"))
+
+
+def prefetch_dequant_bg(bases, grid: int = 0):
+    """Queue the background expansion of ``bases`` (one layer's NF4Weights, <= 4) behind the
+    current stream's work so far; :func:`_nf4_dequant_bf16` picks each copy up."""
+    bases = [b for b in bases if isinstance(b, NF4Weight) and b.kernel_ok() and id(b) not in _PREFETCHED]
+    if not bases or _NF4_MODE != "dequant" or not bases[0].codes.is_cuda:
+        return
+    dev = bases[0].codes.device
+    side = _SIDE.get(dev)
+    if side is None:
+        side = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        outs = native().nf4_dequant_bg([b.codes for b in bases], [b.gemv_scales() for b in bases],
+                                       [b.shape[0] for b in bases], [b.shape[1] for b in bases], grid or _NF4_BG)
+        ev = torch.cuda.Event()
+        ev.record(side)
+    for b, t in zip(bases, outs):
+        _PREFETCHED[id(b)] = (t, ev)
+
+
 @dataclasses.dataclass
 class LoraBranch:
     a: torch.Tensor          # [r, K]
