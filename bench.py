@@ -117,7 +117,7 @@ def main():
     rank, local_rank, world = D.init_distributed()
     if world != args.gpus:
         raise SystemExit(f"[bench] --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
-    device = torch.device("cuda", local_rank) if torch.cuda.is_available() else torch.device("cpu")
+    device = torch.device("cuda", D.local_device_index(local_rank)) if torch.cuda.is_available() else torch.device("cpu")
     cfg, model = build(args, device)
     total_steps = args.warmup + args.steps
     engine = None

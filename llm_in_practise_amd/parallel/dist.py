@@ -8,6 +8,7 @@ running intra-node over xGMI (8×MI355X full mesh, 7 links/GPU) — or ``gloo`` 
 from __future__ import annotations
 
 import datetime
+import os
 
 import torch
 import torch.distributed as dist
@@ -15,24 +16,35 @@ import torch.distributed as dist
 from ..runtime.env import dist_env
 
 
+def local_device_index(local_rank: int) -> int:
+    """GPU of this rank: ``local_rank``, or ``local_rank % device_count`` under ``LIPA_SHARE_GPU=1``
+    (a multi-rank rehearsal of the distributed path on a box with fewer GPUs than ranks; pair it with
+    ``LIPA_DIST_BACKEND=gloo``, since RCCL refuses two ranks on one device)."""
+    if os.environ.get("LIPA_SHARE_GPU", "0") == "1" and torch.cuda.is_available():
+        return local_rank % max(1, torch.cuda.device_count())
+    return local_rank
+
+
 def init_distributed(backend: str | None = None, timeout_s: int = 1800) -> tuple[int, int, int]:
-    """Initialise the default group from torchrun env vars.  Returns (rank, local_rank, world)."""
+    """Initialise the default group from torchrun env vars.  Returns (rank, local_rank, world).
+    ``LIPA_DIST_BACKEND`` overrides the backend (default: nccl = RCCL with GPUs, else gloo)."""
     env = dist_env()
+    dev = local_device_index(env.local_rank)
     if env.world_size > 1 and not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
-            torch.cuda.set_device(env.local_rank)
+            backend = os.environ.get("LIPA_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        if torch.cuda.is_available():
+            torch.cuda.set_device(dev)
         kw = dict(backend=backend, init_method="env://", timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
-            kw["device_id"] = torch.device("cuda", env.local_rank)
+            kw["device_id"] = torch.device("cuda", dev)
         try:
             dist.init_process_group(**kw)
         except TypeError:
             kw.pop("device_id", None)
             dist.init_process_group(**kw)
     elif torch.cuda.is_available():
-        torch.cuda.set_device(env.local_rank)
+        torch.cuda.set_device(dev)
     return env.rank, env.local_rank, env.world_size
 
 

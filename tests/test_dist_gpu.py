@@ -1,0 +1,25 @@
+"""Multi-rank rehearsal of the distributed bench on one GPU: 2 ranks share cuda:0 (LIPA_SHARE_GPU=1)
+over gloo (RCCL refuses two ranks on one device), so DDP's gradient-ready bucket hooks and the ZeRO-3
+engine run with the real HIP kernels; the RCCL transport itself is exercised by the driver's 8-GPU run."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy", ["ddp", "zero3"])
+def test_bench_two_ranks_share_one_gpu(strategy):
+    env = dict(os.environ, LIPA_DIST_BACKEND="gloo", LIPA_SHARE_GPU="1", HSA_ENABLE_IPC_MODE_LEGACY="0",
+               PYTHONPATH=ROOT)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", "qwen3-small",
+                          "--steps", "2", "--warmup", "1", "--strategy", strategy],
+                         env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["n_gpus"] == 2 and rec["config"]["dist_world_size"] == 2 and rec["config"]["dist_backend"] == "gloo"
+    assert rec["value"] > 0 and rec["config"]["parallelism"].endswith("dp2")
