@@ -62,7 +62,8 @@ void launch_attn_fwd(const void*, const void*, const void*, int, int, int, const
                      int, int, int, int, int, int, int, float, float, uint64_t, hipStream_t);
 void launch_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const int*, int,
                      int, int, void*, void*, void*, float*, int, int, int, int, int, int, float, float, uint64_t,
-                     hipStream_t);
+                     float*, hipStream_t);
+int attn_dkv_nsplit(int, int, int, int);
 
 void launch_gemm_int4_any(const void*, int, const uint32_t*, const float*, const float*, const void*, const void*, int,
                       const void*, void*, int, int, int, hipStream_t);
@@ -798,6 +799,8 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o
   attn_check(dout, B * S, hq, d, "dout");
   TORCH_CHECK(dout.stride(0) == hq * d && o.stride(0) == hq * d, "attn_bwd: o / dout must be dense [T, hq*d]");
   auto delta = at::empty({B, hq, S}, q.options().dtype(at::kFloat));
+  Tensor ws;   // split causal dK/dV blocks: fp32 partial planes [2 parts][dK | dV][T][hkv·d]
+  if (attn_dkv_nsplit(B, S, hkv, causal) > 0) ws = at::empty({4, B * S, hkv * d}, q.options().dtype(at::kFloat));
   const int* kl = nullptr;
   Tensor klc;
   if (kv_lens && kv_lens->defined()) {
@@ -806,7 +809,8 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o
   }
   launch_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), kl,
                   q.stride(0), k.stride(0), v.stride(0), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
-                  delta.data_ptr<float>(), B, S, hq, hkv, d, causal, scale, p_drop, (uint64_t)seed, stream());
+                  delta.data_ptr<float>(), B, S, hq, hkv, d, causal, scale, p_drop, (uint64_t)seed,
+                  ws.defined() ? ws.data_ptr<float>() : nullptr, stream());
   return {dq, dk, dv};
 }
 

@@ -515,14 +515,26 @@ __global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __res
                                                       const int* __restrict__ kv_lens, int ldq, int ldk, int ldv,
                                                       bf16* __restrict__ dK, bf16* __restrict__ dV, int S, int hq,
                                                       int hkv, int causal, float scale, float scale_log2,
-                                                      DropParams drp) {
+                                                      DropParams drp, float* __restrict__ ws, int nsplit) {
   constexpr int LDR = D + 8, CH = D / 8, TILE = 64 * LDR, NS = D / 32, ND = D / 16;
   constexpr int LOADS = 64 * CH / 256;
   __shared__ __attribute__((aligned(16))) bf16 smem_all[HALVES * 4 * TILE];  // per half: Q0 dO0 Q1 dO1
   __shared__ __attribute__((aligned(16))) float stat_all[HALVES][2][2][64];  // [half][buf][lse|delta][q]
 
-  int kbi, hk, b;  // causal: block 0 (most query tiles) first
-  xcd_grid3(kbi, hk, b);
+  // causal work per key block falls off linearly (block 0 sweeps every query tile, the last one);
+  // with nsplit > 0 the first nsplit blocks are each split over two workgroups by query-tile range
+  // (units 2kb, 2kb+1: fp32 partials into ws, summed by attn_dkv_fin_k), the rest are whole (units
+  // 2·nsplit + ...): the longest workgroup sweeps ~half as many tiles
+  int ui, hk, b;
+  xcd_grid3(ui, hk, b);
+  int kbi, part;
+  if (ui < 2 * nsplit) {
+    kbi = ui >> 1;
+    part = ui & 1;
+  } else {
+    kbi = ui - nsplit;
+    part = -1;
+  }
   const int rep = hq / hkv;
   const int tid = threadIdx.x & 255, hw = threadIdx.x >> 8;       // thread within half, half index
   const int hp = rep / HALVES;                                    // q-heads per half
@@ -546,9 +558,18 @@ __global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __res
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt) dv[dt] = dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int qt0 = causal ? kbi : 0;
+  int qt0 = causal ? kbi : 0;
   const int qmin = kw < kvlen ? (causal ? kw : 0) : 1 << 30;  // first query that sees this key
-  const int nqt = (S + 63) / 64 - qt0;
+  int nqt = (S + 63) / 64 - qt0;
+  if (part >= 0) {   // this workgroup's half of the block's query tiles
+    const int h1 = (nqt + 1) / 2;
+    if (part == 0) {
+      nqt = h1;
+    } else {
+      qt0 += h1;
+      nqt -= h1;
+    }
+  }
   const int n_it = kb0 < kvlen ? hp * nqt : 0;  // keys past kv_len get zero gradient
 
   bf16x8 qr[PF][LOADS], dr[PF][LOADS];   // PF query tiles ahead, as the forward
@@ -674,6 +695,18 @@ __global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __res
   }
   // ---- dK (scaled) / dV, summed over the GQA group: lane col key = kw, rows d = 16dt + 4g + r
   if (kw >= S) return;
+  if (part >= 0) {   // split block: raw fp32 partials, planes [part][dK | dV][T][hkv·D]
+    const size_t plane = (size_t)gridDim.z * S * ldkv;
+    float* wk = ws + (size_t)(2 * part) * plane;
+    float* wv = wk + plane;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {
+      const size_t off = (tok0 + kw) * ldkv + hk * D + 16 * dt + 4 * g;
+      *reinterpret_cast<f32x4*>(wk + off) = dk[dt];
+      *reinterpret_cast<f32x4*>(wv + off) = dv[dt];
+    }
+    return;
+  }
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt) {
     const size_t off = (tok0 + kw) * ldkv + hk * D + 16 * dt + 4 * g;
@@ -688,7 +721,43 @@ __global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __res
   }
 }
 
+// dK = scale·(P0 + P1), dV = P0 + P1 for the keys of the split blocks (keys < nsplit·64 of every batch)
+__global__ __launch_bounds__(256) void attn_dkv_fin_k(const float* __restrict__ ws, bf16* __restrict__ dK,
+                                                     bf16* __restrict__ dV, int B, int S, int ldkv, int rows,
+                                                     float scale) {
+  const size_t per_b = (size_t)rows * ldkv;
+  const size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= (size_t)B * per_b) return;
+  const size_t b = i / per_b, r = i - b * per_b;
+  const size_t off = b * (size_t)S * ldkv + r;
+  const size_t plane = (size_t)B * S * ldkv;
+  const f32x4 k = *reinterpret_cast<const f32x4*>(ws + off) + *reinterpret_cast<const f32x4*>(ws + 2 * plane + off);
+  const f32x4 v = *reinterpret_cast<const f32x4*>(ws + plane + off) +
+                  *reinterpret_cast<const f32x4*>(ws + 3 * plane + off);
+  bf16x4 ok, ov;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    ok[e] = (bf16)(k[e] * scale);
+    ov[e] = (bf16)v[e];
+  }
+  *reinterpret_cast<bf16x4*>(dK + off) = ok;
+  *reinterpret_cast<bf16x4*>(dV + off) = ov;
+}
+
 }  // namespace
+
+// key blocks of the causal dK/dV grid split over two workgroups (0: none).  Split when the grid is
+// at most ~2 workgroups per CU (larger grids already balance over several waves of workgroups) and
+// S >= 1024: blocks whose query-tile count exceeds half the blocks.  Measured (same box, interleaved,
+// scripts/experiments/gpu_dkv_split_ab.sh): [1, 2048, 32, 8, 128] bwd 283 -> 260 us; at the bench
+// shape [4, 512, ...] the 4-tile units' fixed cost and the fp32 partial round trip lose (92 -> 102 us),
+// hence the S threshold.  LIPA_ATTN_DKV_SPLIT=0 disables, =2 also splits S < 1024.
+int attn_dkv_nsplit(int B, int S, int hkv, int causal) {
+  static const int env = [] { const char* e = getenv("LIPA_ATTN_DKV_SPLIT"); return e ? atoi(e) : 1; }();
+  const int nb = (S + 63) / 64;
+  if (!env || !causal || nb < (env == 2 ? 4 : 16) || (long)B * hkv * nb > 512) return 0;
+  return nb - (nb + 1) / 2;   // kb with nb - kb > ceil(nb / 2)
+}
 
 static DropParams make_drop(float p, uint64_t seed) {
   DropParams d{(uint32_t)seed, (uint32_t)(seed >> 32), 0u, 1.f};
@@ -776,12 +845,13 @@ void launch_attn_fwd(const void* q, const void* k, const void* v, int ldq, int l
 
 void launch_attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
                      const int* kv_lens, int ldq, int ldk, int ldv, void* dq, void* dk, void* dv, float* delta, int B,
-                     int S, int hq, int hkv, int D, int causal, float scale, float p_drop, uint64_t seed,
+                     int S, int hq, int hkv, int D, int causal, float scale, float p_drop, uint64_t seed, float* ws,
                      hipStream_t st) {
   const float sl2 = scale * LOG2E;
   const DropParams dp = make_drop(p_drop, seed);
   const int nb = (S + 63) / 64;
-  dim3 gq(nb, hq, B), gkv(nb, hkv, B), blk(256);
+  const int nsplit = ws ? attn_dkv_nsplit(B, S, hkv, causal) : 0;
+  dim3 gq(nb, hq, B), gkv(nb + nsplit, hkv, B), blk(256);
   // Two streams (causal): the dK/dV grid is one 8-wave workgroup per 64-key block and its work falls
   // off linearly with the block index (block 0 sweeps every query tile, the last one tile), so most
   // CUs go idle long before it ends.  With delta computed up front, the dK/dV kernel runs on a side
@@ -804,11 +874,11 @@ void launch_attn_bwd(const void* dout, const void* q, const void* k, const void*
   if ((hq / hkv) % 2 == 0)                                                                                       \
     attn_bwd_dkv_k<DD, 2, PFKV><<<gkv, 512, 0, kst>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k,           \
                                                       (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, \
-                                                      (bf16*)dv, S, hq, hkv, causal, scale, sl2, dp);               \
+                                                      (bf16*)dv, S, hq, hkv, causal, scale, sl2, dp, ws, nsplit);   \
   else                                                                                                           \
     attn_bwd_dkv_k<DD, 1, PFKV><<<gkv, 256, 0, kst>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k,           \
                                                       (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, \
-                                                      (bf16*)dv, S, hq, hkv, causal, scale, sl2, dp)
+                                                      (bf16*)dv, S, hq, hkv, causal, scale, sl2, dp, ws, nsplit)
 // two streams: dK/dV first on the side stream (delta is ready), dQ beside it; one stream: dQ first
 // (it writes delta), then dK/dV
 #define RUN(DD, PFQ, PFKV)                                                                                        \
@@ -834,6 +904,11 @@ void launch_attn_bwd(const void* dout, const void* q, const void* k, const void*
   }
 #undef RUN
 #undef DKV
+  if (nsplit > 0) {
+    const int ldkv = hkv * D, rows = std::min(nsplit * 64, S);
+    const size_t n4 = (size_t)B * rows * ldkv / 4;
+    attn_dkv_fin_k<<<(unsigned)((n4 + 255) / 256), 256, 0, kst>>>(ws, (bf16*)dk, (bf16*)dv, B, S, ldkv, rows, scale);
+  }
   if (two) {
     hipEventRecord(ev_join, kst);
     hipStreamWaitEvent(st, ev_join, 0);

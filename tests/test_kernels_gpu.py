@@ -345,7 +345,9 @@ ATTN_CASES = [(2, 512, 32, 8, 128, True), (1, 256, 4, 4, 64, True), (2, 128, 8, 
               (1, 192, 4, 2, 64, True),
               # any S (masked tail tiles in fwd AND bwd), every head_dim, odd GQA groups
               (1, 87, 4, 2, 64, True), (2, 255, 8, 2, 128, True), (1, 511, 4, 4, 96, False),
-              (2, 100, 4, 1, 32, True), (1, 130, 6, 3, 128, True), (3, 33, 2, 2, 96, True)]
+              (2, 100, 4, 1, 32, True), (1, 130, 6, 3, 128, True), (3, 33, 2, 2, 96, True),
+              # S >= 1024: the causal dK/dV grid splits its heavy key blocks over two workgroups
+              (1, 1100, 4, 2, 128, True), (2, 1024, 4, 4, 64, True)]
 
 
 def _attn_ref_grads(q, k, v, do, B, S, hq, hkv, d, causal, scale, mask=None, keep=None, rinv=1.0):
