@@ -1,0 +1,37 @@
+"""The measured-and-kept-off scheduling variants stay numerically equivalent to the default path, so
+their A/B records (profiles/) compare like with like: side-stream LoRA projection (LIPA_LORA_SIDE),
+two-stream attention backward with the standalone delta kernel (LIPA_ATTN_BWD_STREAMS), background
+next-layer NF4 expansion (LIPA_NF4_BG), the single-kernel lora_proj2 (LIPA_PROJ2_IMPL=0).  Each runs the
+bench step on a small Qwen3 in a subprocess (the switches are read once per process)."""
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _losses(extra_env):
+    env = dict(os.environ, PYTHONPATH=ROOT, HSA_ENABLE_IPC_MODE_LEGACY="0", **extra_env)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", "qwen3-small", "--steps", "3",
+                          "--warmup", "1"], env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-3000:]
+    return [float(x) for x in re.findall(r"loss=([0-9.]+)", out.stderr)]
+
+
+@pytest.fixture(scope="module")
+def base_losses():
+    got = _losses({})
+    assert len(got) == 2
+    return got
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{"LIPA_LORA_SIDE": "1"}, {"LIPA_ATTN_BWD_STREAMS": "1"}, {"LIPA_NF4_BG": "64"},
+                                 {"LIPA_PROJ2_IMPL": "0"}], ids=lambda e: ",".join(e))
+def test_opt_in_schedule_matches_default(base_losses, env):
+    got = _losses(env)
+    assert len(got) == 2 and all(abs(a - b) <= 2e-3 * abs(b) for a, b in zip(got, base_losses)), (env, got,
+                                                                                                   base_losses)
