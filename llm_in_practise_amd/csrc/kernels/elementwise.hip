@@ -9,41 +9,39 @@ namespace {
 __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
 
 // gu [M, 2F] -> y [M, F];  F % 8 == 0
+// One 8-element vector per thread on a (row, column-chunk) grid: no index division (the grid-stride
+// form spent most of its VALU on a 64-bit e / F, e % F per vector) and every load in flight at once.
 __global__ __launch_bounds__(256) void swiglu_fwd_k(const bf16* __restrict__ gu, bf16* __restrict__ y, int M, int F) {
-  const size_t nvec = (size_t)M * F / 8;
-  for (size_t v = (size_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (size_t)gridDim.x * 256) {
-    const size_t e = v * 8;
-    const size_t m = e / F, f = e % F;
-    float g[8], u[8], o[8];
-    load8(gu + m * 2 * F + f, g);
-    load8(gu + m * 2 * F + F + f, u);
+  const int f = (blockIdx.y * 256 + threadIdx.x) * 8;
+  if (f >= F) return;
+  const size_t m = blockIdx.x;
+  float g[8], u[8], o[8];
+  load8(gu + m * 2 * F + f, g);
+  load8(gu + m * 2 * F + F + f, u);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = silu(g[i]) * u[i];
-    store8(y + e, o);
-  }
+  for (int i = 0; i < 8; ++i) o[i] = silu(g[i]) * u[i];
+  store8(y + m * F + f, o);
 }
 
 // dgu = [dy*u*silu'(g) | dy*silu(g)]
 __global__ __launch_bounds__(256) void swiglu_bwd_k(const bf16* __restrict__ dy, const bf16* __restrict__ gu,
                                                     bf16* __restrict__ dgu, int M, int F) {
-  const size_t nvec = (size_t)M * F / 8;
-  for (size_t v = (size_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (size_t)gridDim.x * 256) {
-    const size_t e = v * 8;
-    const size_t m = e / F, f = e % F;
-    float g[8], u[8], d[8], dg[8], du[8];
-    load8(gu + m * 2 * F + f, g);
-    load8(gu + m * 2 * F + F + f, u);
-    load8(dy + e, d);
+  const int f = (blockIdx.y * 256 + threadIdx.x) * 8;
+  if (f >= F) return;
+  const size_t m = blockIdx.x;
+  float g[8], u[8], d[8], dg[8], du[8];
+  load8(gu + m * 2 * F + f, g);
+  load8(gu + m * 2 * F + F + f, u);
+  load8(dy + m * F + f, d);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float sg = 1.f / (1.f + __expf(-g[i]));
-      const float s = g[i] * sg;
-      du[i] = d[i] * s;
-      dg[i] = d[i] * u[i] * (sg * (1.f + g[i] * (1.f - sg)));
-    }
-    store8(dgu + m * 2 * F + f, dg);
-    store8(dgu + m * 2 * F + F + f, du);
+  for (int i = 0; i < 8; ++i) {
+    const float sg = 1.f / (1.f + __expf(-g[i]));
+    const float s = g[i] * sg;
+    du[i] = d[i] * s;
+    dg[i] = d[i] * u[i] * (sg * (1.f + g[i] * (1.f - sg)));
   }
+  store8(dgu + m * 2 * F + f, dg);
+  store8(dgu + m * 2 * F + F + f, du);
 }
 
 template <typename T>
@@ -91,11 +89,15 @@ inline int grid_for(size_t work) {
 }  // namespace
 
 void launch_swiglu_fwd(const void* gu, void* y, int M, int F, hipStream_t st) {
-  swiglu_fwd_k<<<grid_for((size_t)M * F / 8), 256, 0, st>>>((const bf16*)gu, (bf16*)y, M, F);
+  if (M <= 0) return;
+  const dim3 g(M, (F / 8 + 255) / 256);
+  swiglu_fwd_k<<<g, 256, 0, st>>>((const bf16*)gu, (bf16*)y, M, F);
   LIPA_CHECK_LAUNCH();
 }
 void launch_swiglu_bwd(const void* dy, const void* gu, void* dgu, int M, int F, hipStream_t st) {
-  swiglu_bwd_k<<<grid_for((size_t)M * F / 8), 256, 0, st>>>((const bf16*)dy, (const bf16*)gu, (bf16*)dgu, M, F);
+  if (M <= 0) return;
+  const dim3 g(M, (F / 8 + 255) / 256);
+  swiglu_bwd_k<<<g, 256, 0, st>>>((const bf16*)dy, (const bf16*)gu, (bf16*)dgu, M, F);
   LIPA_CHECK_LAUNCH();
 }
 void launch_gelu_fwd(int dtype, const void* x, void* y, size_t n, hipStream_t st) {
