@@ -21,6 +21,8 @@
 //              reads X and DX once; the per-chunk (64-row) partials are summed by the caller.
 #include <cstdlib>
 
+#include <algorithm>
+
 #include "common.h"
 
 using namespace lipa;
@@ -407,6 +409,68 @@ __global__ __launch_bounds__(256) void lora_dx2_k(const float* __restrict__ G0, 
     for (int j = 0; j < 8; ++j) {
       const float g0 = j < r0 ? gq0[e][j >> 2][j & 3] : 0.f;
       const float g1 = j < r1 ? gq1[e][j >> 2][j & 3] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        t0[i] += g0 * (float)av0[j][i];
+        t1[i] += g1 * (float)av1[j][i];
+      }
+    }
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      o[i] = (((kp0[e] >> i) & 1) ? t0[i] * ds0 : 0.f) + (((kp1[e] >> i) & 1) ? t1[i] * ds1 : 0.f);
+    store8(out + (size_t)m * K + k8, o);
+  }
+}
+
+// lora_dx2 with A read once per 16 rows: a thread owns 8 consecutive k of 16 rows (workgroup = 2048 k ×
+// 16 rows), the 16 rows' G values (both branches) are staged once in LDS, and every keep byte of the
+// thread is loaded up front.  The 4-row form above re-read A's 8 k-columns (both adapters: 256 B per
+// thread) for every 4 rows — 64 MB of L2 reads per call at the bench shape for 16 MB of output.
+__global__ __launch_bounds__(256) void lora_dx2_r16_k(const float* __restrict__ G0, const float* __restrict__ G1,
+                                                      int ldg, const bf16* __restrict__ A0,
+                                                      const bf16* __restrict__ A1, int r0, int r1,
+                                                      const uint8_t* __restrict__ kb0,
+                                                      const uint8_t* __restrict__ kb1, float ds0, float ds1,
+                                                      bf16* __restrict__ out, int M, int K) {
+  __shared__ float gs[16][2][8];
+  const int m0 = blockIdx.y * 16;
+  {
+    const int t = threadIdx.x, e = t >> 4, br = (t >> 3) & 1, j = t & 7;
+    const int m = min(m0 + e, M - 1);
+    const int rr = br ? r1 : r0;
+    gs[e][br][j] = j < rr ? (br ? G1 : G0)[(size_t)m * ldg + j] : 0.f;
+  }
+  const int kv = blockIdx.x * 256 + threadIdx.x;
+  const int k8 = kv * 8;
+  const bool live = k8 < K;
+  bf16x8 av0[8], av1[8];
+  uint32_t kp0[16], kp1[16];
+  if (live) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      av0[j] = j < r0 ? *reinterpret_cast<const bf16x8*>(A0 + (size_t)j * K + k8) : bf16x8{};
+      av1[j] = j < r1 ? *reinterpret_cast<const bf16x8*>(A1 + (size_t)j * K + k8) : bf16x8{};
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int m = min(m0 + e, M - 1);
+      kp0[e] = kb0 ? kb0[(size_t)m * (K >> 3) + kv] : 0xFFu;
+      kp1[e] = kb1 ? kb1[(size_t)m * (K >> 3) + kv] : 0xFFu;
+    }
+  }
+  __syncthreads();
+  if (!live) return;
+#pragma unroll 4
+  for (int e = 0; e < 16; ++e) {
+    const int m = m0 + e;
+    if (m >= M) break;
+    float t0[8], t1[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t0[i] = t1[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float g0 = gs[e][0][j], g1 = gs[e][1][j];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         t0[i] += g0 * (float)av0[j][i];
@@ -1107,6 +1171,7 @@ void launch_lora_apply(void* Y, int ldy, int M, int nb, const float* const* xa, 
 void launch_lora_proj_pair(const void* X0, const void* X1, int ldx, const void* W0, const void* W1, int r, int K0,
                            int K1, float* out0, float* out1, float s0, float s1, int M, hipStream_t st) {
   ProjPair p{{(const bf16*)X0, (const bf16*)X1}, {(const bf16*)W0, (const bf16*)W1}, {out0, out1}, {K0, K1}, {s0, s1}};
+  // (a split-K form like lora_proj2s_k measured slower here: 10.4 + 5.2 us slab sum vs 11.1 us)
   const int rw = M < 4096 ? 8 : 16;
   dim3 grid((M + rw - 1) / rw, 2);
   if (rw == 8)
@@ -1141,7 +1206,14 @@ void launch_lora_dA_pair(const float* G0, const float* G1, int ldg, int r, const
 void launch_lora_dx2(const float* G0, const float* G1, int ldg, const void* A0, const void* A1, int r0, int r1,
                      const uint8_t* kb0, const uint8_t* kb1, float ds0, float ds1, void* out, int M, int K,
                      hipStream_t st) {
-  static const int rpt = [] { const char* e = getenv("LIPA_LORA_DX_RPT"); return e ? atoi(e) : 4; }();
+  static const int rpt = [] { const char* e = getenv("LIPA_LORA_DX_RPT"); return e ? atoi(e) : 16; }();
+  if (rpt == 16 && r0 <= 8 && r1 <= 8) {
+    dim3 g16((K / 8 + 255) / 256, (M + 15) / 16);
+    lora_dx2_r16_k<<<g16, 256, 0, st>>>(G0, G1, ldg, (const bf16*)A0, (const bf16*)A1, r0, r1, kb0, kb1, ds0, ds1,
+                                       (bf16*)out, M, K);
+    LIPA_CHECK_LAUNCH();
+    return;
+  }
   if (rpt == 8) {
     dim3 g8((K / 8 + 63) / 64, (M + 31) / 32);
     lora_dx2_k<8><<<g8, 256, 0, st>>>(G0, G1, ldg, (const bf16*)A0, (const bf16*)A1, r0, r1, kb0, kb1, ds0, ds1,

@@ -11,4 +11,4 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 $R/bench.py --steps 3 --warmup 1 > $OUT/kt.log 2>&1 || exit 1
 python3 $R/scripts/step_timeline.py $(find $OUT/kt -name "*kernel_trace.csv" | head -1) --marker adamw8bit > $OUT/timeline.txt
 rm -rf $OUT/kt
-grep -E "step [01]|swiglu|rmsnorm|qk_norm" $OUT/timeline.txt
+grep -E "step [01]|swiglu|rmsnorm|qk_norm|lora" $OUT/timeline.txt
