@@ -90,17 +90,29 @@ __device__ __forceinline__ void xcd_grid3_lpt(int& i0, int& i1, int& i2, int lpt
   const int npair = n1 * gridDim.z;
   const int nwg = n0 * npair;
   const int id = xcd_remap(blockIdx.x + n0 * (blockIdx.y + n1 * blockIdx.z), nwg);
-  const int G = max(1, min(npair, 128 / n0));   // pairs per run
+  // pairs per run = one XCD's share of the grid (xcd_remap gives XCD x the contiguous logical range
+  // [x·nwg/8, (x+1)·nwg/8)), so every XCD holds the whole heavy-to-light range of its pairs: a run
+  // spanning two XCDs hands one of them only heavy blocks (the 128-query forward at [4, 512, 32, 8]:
+  // 448 vs 192 tile-sweeps per XCD)
+  const int G = max(1, min(npair, (nwg / 8) / n0));
   const int run = id / (n0 * G), t = id % (n0 * G);
   const int g = min(G, npair - run * G);       // the last run may hold fewer pairs
   i0 = t / g;
+  if (lpt == 1 && nwg <= 8 * 64) {
+    // the whole grid is resident at once (2 workgroups per CU): the first 32 of an XCD's blocks take
+    // one slot of each CU, the next 32 the other, so a snake order (heavy half descending, light half
+    // ascending) gives every CU one heavy + one light block instead of two of the heaviest
+    const int m = (n0 + 1) / 2;
+    i0 = i0 < m ? i0 : n0 - 1 - (i0 - m);
+  }
   const int pr = run * G + t % g;
   i1 = pr % n1;
   i2 = pr / n1;
 }
 
 static int attn_lpt() {
-  static const int v = [] { const char* e = getenv("LIPA_ATTN_LPT"); return e ? (atoi(e) != 0) : 1; }();
+  // 0: plain XCD-grouped order; 1: longest-first (+ snake when the grid is resident); 2: longest-first only
+  static const int v = [] { const char* e = getenv("LIPA_ATTN_LPT"); return e ? atoi(e) : 1; }();
   return v;
 }
 
