@@ -177,9 +177,10 @@ def main():
                 ctx = ddp.no_sync() if micro < args.grad_accum - 1 else contextlib.nullcontext()
                 with ctx:
                     out = model(ids, labels=ids)
+                    spent[0] = None         # the previous micro-step's graph, torn down under this forward
                     (out.loss / args.grad_accum).backward()
                 loss = out.loss.detach()
-                del out
+                spent[0] = out
         ddp.allreduce_grads()
         opt.clip_grad_norm_(1.0)
         opt.step()

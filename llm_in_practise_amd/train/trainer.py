@@ -467,6 +467,8 @@ class Trainer:
             for i, b in enumerate(batches):
                 last = i == len(batches) - 1
                 loss = self.compute_loss(self.model, b)
+                if i == 0:
+                    self._spent_graph = None   # previous step's last graph, torn down under this forward
                 if self.engine is not None:
                     self.engine.backward(loss)
                     if not last:
@@ -476,6 +478,7 @@ class Trainer:
                     with ctx:
                         (loss / len(batches)).backward()
                 total = total + loss.detach() / len(batches)
+            self._spent_graph = loss
             poison = self.faults.check(self.state.global_step + 1) if self.faults else None
             if poison == "nan":
                 total = total * float("nan")
