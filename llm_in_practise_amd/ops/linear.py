@@ -293,8 +293,14 @@ def seed_dropout(seed: int):
     _KEY[0] = (int(seed) * 0x2545F4914F6CDD1D) & 0x7FFFFFFFFFFFFFFF
 
 
+_CKPT_REENTRANT = __import__("os").environ.get("LIPA_CKPT_REENTRANT", "1") == "1"
+
+
 def checkpoint(fn, *args):
-    """Activation checkpointing (non-reentrant) that replays the SAME LoRA dropout masks.
+    """Activation checkpointing that replays the SAME LoRA dropout masks.  Reentrant by default
+    (``LIPA_CKPT_REENTRANT=0``: the non-reentrant form): the reference-faithful QLoRA step
+    (checkpointing on, sequential GA) is partly host-bound and the non-reentrant form's saved-tensor
+    pack hooks cost it 10-15 ms per step (129-135 -> 120 ms, profiles/baseline_configs_r2_end.txt).
 
     The fused LoRA kernels draw their dropout mask from the host key stream above, not from
     torch's RNG, so torch's ``preserve_rng_state`` does not cover them: a plain
@@ -317,6 +323,14 @@ def checkpoint(fn, *args):
         finally:
             _KEY[0] = live
 
+    if _CKPT_REENTRANT:
+        # reentrant form: the first forward runs without building a graph (no saved-tensor pack hooks:
+        # ~2k per step at Qwen3-8B, the host-side cost of the checkpointed step); it needs an input
+        # that requires grad for the recompute to reach the LoRA parameters (layer 0's input is the
+        # frozen embedding) — the role of HF's enable_input_require_grads()
+        args = tuple(a.detach().requires_grad_() if isinstance(a, torch.Tensor) and i == 0 and
+                     a.is_floating_point() and not a.requires_grad else a for i, a in enumerate(args))
+        return ckpt.checkpoint(run, *args, use_reentrant=True)
     return ckpt.checkpoint(run, *args, use_reentrant=False)
 
 

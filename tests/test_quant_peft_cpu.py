@@ -192,3 +192,27 @@ def test_checkpoint_replays_dropout_key_stream():
     assert len(seen) == 2 and seen[0] == seen[1]              # recompute drew the same key
     assert L._KEY[0] == after_fwd                             # stream not advanced by the recompute
     assert torch.allclose(x.grad, torch.full((3,), 2.0 * float(seen[0] % 997 + 1)))
+
+
+def test_checkpointed_qwen3_lora_grads_match_including_layer0():
+    """Gradient checkpointing (reentrant default) gives the same LoRA gradients as the plain pass —
+    including layer 0, whose input (the frozen embedding's output) does not require grad (the
+    reentrant form needs the input marked, as HF's enable_input_require_grads() does)."""
+    from llm_in_practise_amd.models.qwen3 import Qwen3ForCausalLM, qwen3_config
+    from llm_in_practise_amd.peft.lora import LoraConfig, get_peft_model
+    grads = []
+    for ck in (False, True):
+        m = Qwen3ForCausalLM.from_config(qwen3_config("qwen3-tiny"), dtype=torch.float32, device="cpu", seed=3)
+        pm = get_peft_model(m, LoraConfig(r=4, lora_alpha=8, lora_dropout=0.0, target_modules=["q_proj", "v_proj"]))
+        for n, p in pm.named_parameters():
+            if p.requires_grad and "lora_B" in n:
+                torch.nn.init.normal_(p, std=0.02, generator=torch.Generator().manual_seed(len(n)))
+        if ck:
+            pm.gradient_checkpointing_enable()
+        pm.train()
+        ids = torch.randint(0, 100, (2, 16), generator=torch.Generator().manual_seed(1))
+        pm(ids, labels=ids).loss.backward()
+        grads.append({n: p.grad.clone() for n, p in pm.named_parameters() if p.requires_grad and p.grad is not None})
+    assert grads[0].keys() == grads[1].keys() and any(".0." in n for n in grads[1])
+    for n in grads[0]:
+        assert torch.allclose(grads[0][n], grads[1][n], rtol=1e-4, atol=1e-6), n
