@@ -393,9 +393,10 @@ std::vector<Tensor> nf4_quantize(Tensor w, int64_t blocksize) {
 // decode-shaped y = x·Wᵀ (+ residual): x [M <= 64, K] row-strided, W [N, K] contiguous bf16
 // ---- hipBLASLt frozen-base GEMMs (csrc/kernels/blaslt.hip)
 static void* lt_workspace(size_t& bytes) {
-  static std::map<int, Tensor> ws;   // one 64 MiB hipBLASLt workspace per device, kept for the process
+  static std::map<int, Tensor> ws;   // one hipBLASLt workspace per device (64 MiB; LIPA_LT_WS_MB), kept for the process
+  static const size_t mb = [] { const char* e = getenv("LIPA_LT_WS_MB"); return (size_t)(e && atoi(e) > 0 ? atoi(e) : 64); }();
   const int dev = at::hip::current_device();
-  bytes = (size_t)64 << 20;
+  bytes = mb << 20;
   Tensor& t = ws[dev];
   if (!t.defined()) t = at::empty({(int64_t)bytes}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, dev));
   return t.data_ptr();

@@ -45,7 +45,9 @@ def embedding(ids: torch.Tensor, weight: torch.Tensor, padding_idx: int | None =
     if _native_ok(ids, weight):
         if not torch.is_grad_enabled() or not weight.requires_grad:
             return native().embedding_fwd(weight, ids)
-        return _EmbeddingFn.apply(ids, weight, padding_idx)
+        from .linear import deterministic
+        if not deterministic():   # the scatter-add's fp32 atomics sum in arrival order
+            return _EmbeddingFn.apply(ids, weight, padding_idx)
     return F.embedding(ids, weight, padding_idx)
 
 
