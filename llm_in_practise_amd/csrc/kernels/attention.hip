@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const bf16* __restrict__ Q,
                                                   const int* __restrict__ kv_lens, const int* __restrict__ q_offs,
                                                   bf16* __restrict__ O, float* __restrict__ lse, int Sq, int Skv,
                                                   int kv_rows, int hq, int hkv, int causal, float scale_log2,
-                                                  DropParams dp) {
+                                                  DropParams dp, float defer_thr) {
   constexpr int LDR = D + 8;        // padded LDS row (elements)
   constexpr int CH = D / 8;         // 16-B chunks per row
   constexpr int TILE = 64 * LDR;    // elements per K or V tile
@@ -252,7 +252,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const bf16* __restrict__ Q,
         for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sc[kt][qt][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m_run[qt], mx);
+      // deferred max (defer_thr > 0, cdna guide T13): the running max moves only when some query of
+      // the wave grew by more than defer_thr in the exponent's log2 units; P is then bounded by
+      // 2^defer_thr instead of 1 and most tiles skip the O rescale.  defer_thr = 0: exact update.
+      const bool upd = __any((mx - m_run[qt]) * scale_log2 > defer_thr);
+      const float mn = upd ? fmaxf(m_run[qt], mx) : m_run[qt];
       const bool dead = mn == -INFINITY;   // every key so far masked for this query
       const float alpha = dead ? 1.f : fexp2((m_run[qt] - mn) * scale_log2);
       const float mc = dead ? 0.f : mn * scale_log2;
@@ -840,12 +844,14 @@ void launch_attn_fwd(const void* q, const void* k, const void* v, int ldq, int l
   // S = 512 / 8192 and equal at 2048 (profiles/attention_fwd_bwd.txt).  LIPA_ATTN_QT=1|2 forces one.
   static const int qt_env = [] { const char* e = getenv("LIPA_ATTN_QT"); return e ? atoi(e) : 0; }();
   const int qt = qt_env == 1 || qt_env == 2 ? qt_env : 2;
+  static const float defer = [] { const char* e = getenv("LIPA_ATTN_DEFER"); return e ? (float)atof(e) : 0.f; }();
   dim3 grid((Sq + 64 * qt - 1) / (64 * qt), hq, B), blk(256);
   const float sl2 = scale * LOG2E;
 #define FWD(PFV, QTV)                                                                                      \
   LIPA_ATTN_D(D, attn_fwd_k<DD, PFV, QTV><<<grid, blk, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,  \
                                                            ldq, ldk, ldv, kv_lens, q_offs, (bf16*)o, lse, Sq, Skv, \
-                                                           kv_rows, hq, hkv, causal ? 1 | (attn_lpt() << 1) : 0, sl2, dp))
+                                                           kv_rows, hq, hkv, causal ? 1 | (attn_lpt() << 1) : 0, sl2, dp, \
+                                                           defer))
   if (qt == 1) {
     FWD(1, 1);
   } else {
