@@ -9,11 +9,14 @@ in REVERSE parameter order (the order backward produces gradients).
 Overlap with the backward: every parameter reports "gradient final" — through a
 ``post_accumulate_grad_hook`` for ordinary autograd leaves, and through
 :func:`ops.linear.register_grad_ready` for the LoRA adapters whose gradients the fused
-kernels accumulate in place — and the moment a bucket's last parameter reports, the bucket's
-all-reduce is issued on a side HIP stream (ordered after the producing kernels by an event),
-so RCCL over xGMI runs while the GPU computes the rest of the backward.  ``allreduce_grads()``
-(after the boundary micro-step's backward) only flushes buckets whose parameters received no
-gradient and joins the streams.  ``no_sync()`` skips the reduction on non-boundary
+kernels accumulate in place — and once a bucket's last parameter has reported AND every bucket
+before it has been issued, the bucket's all-reduce is issued on a side HIP stream (ordered
+after the producing kernels by an event), so RCCL over xGMI runs while the GPU computes the rest
+of the backward.  Buckets are issued strictly in index order (torch DDP's rule): collectives pair
+up by call order, so a bucket that completes early on one rank must not overtake a bucket whose
+parameter got no gradient on that rank (an MoE expert that received zero tokens) — it waits, and
+``allreduce_grads()`` (after the boundary micro-step's backward) flushes the unfinished tail in
+the same order on every rank, then joins the streams.  ``no_sync()`` skips the reduction on non-boundary
 gradient-accumulation micro-steps.
 
 Bucket size: xGMI rings are per-link bandwidth-bound, so buckets are large (default 32 MiB,
@@ -112,6 +115,7 @@ class DistributedDataParallel(nn.Module):
             for i in bk.params:
                 self._bucket_of[i] = b
         self._ready = [False] * len(fp.params)
+        self._next = 0          # the next bucket index allowed to launch (strict index order)
 
     def buckets(self) -> list[torch.Tensor]:
         g = self.grad_buffer
@@ -145,8 +149,11 @@ class DistributedDataParallel(nn.Module):
         b = self._bucket_of[i]
         bk = self._buckets[b]
         bk.remaining -= 1
-        if bk.remaining == 0:
-            self._launch(b, "hook")
+        # issue every complete bucket at the head of the order; a complete bucket behind an
+        # incomplete one waits (collectives must be called in the same order on every rank)
+        while self._next < len(self._buckets) and self._buckets[self._next].remaining == 0:
+            self._launch(self._next, "hook")
+            self._next += 1
 
     def _on_accumulated(self, p: torch.Tensor):
         i = self._index.get(id(p))
@@ -190,9 +197,9 @@ class DistributedDataParallel(nn.Module):
             for b in reversed(self.buckets()):
                 all_reduce_mean_(b)
             return
-        for b, bk in enumerate(self._buckets):       # params that got no gradient this step
-            if not bk.launched:
-                self._launch(b, "flush")
+        for b in range(self._next, len(self._buckets)):   # the tail, in order (some param got no gradient)
+            self._launch(b, "flush")
+        self._next = 0
         if self._stream is not None:
             torch.cuda.current_stream(self.grad_buffer.device).wait_stream(self._stream)
         for work, view in self._works:

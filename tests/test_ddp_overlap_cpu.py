@@ -102,3 +102,60 @@ def test_ddp_buckets_over_custom_allreduce_match_oracle(tmp_path):
     for k in want:
         assert torch.allclose(got["sd"][k], want[k], atol=1e-5), k
     assert got["calls"]["oneshot"] + got["calls"]["twoshot"] > 0
+
+
+class SkipNet(Net):
+    """A block that one rank never runs (an MoE expert that got zero tokens on that rank)."""
+
+    def forward(self, x, skip=None):
+        h = self.inp(x)
+        for i, b in enumerate(self.blocks):
+            if i != skip:
+                h = h + torch.tanh(b(h))
+        return self.out(h)
+
+
+def _skip_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    net = SkipNet()
+    opt = AdamW(net.parameters(), lr=1e-2, weight_decay=0.0)
+    ddp = DistributedDataParallel(net, flat=opt.flat, bucket_mb=0.004)
+    logs = []
+    for s in range(3):
+        x, y = _data(s, rank)
+        # the last block (the FIRST bucket in backward order) is unused on rank 1
+        ((ddp(x, skip=5 if rank == 1 else None) - y) ** 2).mean().backward()
+        logs.append(list(ddp.launch_log))
+        ddp.reset_log()
+        ddp.allreduce_grads()
+        logs[-1] += list(ddp.launch_log)
+        ddp.reset_log()
+        opt.step()
+        opt.zero_grad()
+    torch.save({"sd": net.state_dict(), "logs": logs, "nb": len(ddp._buckets)}, out.format(rank))
+    torch.distributed.destroy_process_group()
+
+
+def test_ddp_unused_param_on_one_rank_keeps_collective_order(tmp_path):
+    """with a parameter unused on one rank, buckets must still be issued in the same
+    (index) order on every rank; gradients equal the per-rank-average oracle."""
+    out = str(tmp_path / "skip{}.pt")
+    mp.spawn(_skip_worker, args=(2, _port(), out), nprocs=2, join=True)
+    torch.manual_seed(0)
+    net = SkipNet()
+    opt = AdamW(net.parameters(), lr=1e-2, weight_decay=0.0)
+    for s in range(3):
+        loss = sum(((net(_data(s, r)[0], skip=5 if r == 1 else None) - _data(s, r)[1]) ** 2).mean() for r in range(2))
+        (loss / 2).backward()
+        opt.step()
+        opt.zero_grad()
+    for r in range(2):
+        got = torch.load(out.format(r), weights_only=True)
+        for k, v in net.state_dict().items():
+            assert torch.allclose(got["sd"][k], v, atol=1e-5), (r, k)
+        for log in got["logs"]:
+            assert [b for b, _ in log] == list(range(got["nb"]))      # identical order on both ranks
+        if r == 1:   # the unused block holds back its bucket and everything after it until the flush
+            assert all(log[0][1] == "flush" for log in got["logs"])
