@@ -119,7 +119,7 @@ void launch_custom_allreduce(int, const void* const*, void* const*, uint32_t* co
                              bool, float, void*, int, hipStream_t);
 void launch_dropout_fwd(const void*, void*, size_t, uint64_t, float, hipStream_t);
 bool embedding_supported(int64_t, int64_t);
-void launch_embedding_fwd(const void*, const int64_t*, void*, int64_t, int64_t, int64_t, int64_t, hipStream_t);
+void launch_embedding_fwd(const void*, const int64_t*, void*, int64_t, int64_t, int64_t, int64_t, int*, hipStream_t);
 void launch_embedding_bwd(const void*, int, const int64_t*, float*, int64_t, int64_t, int64_t, int64_t, hipStream_t);
 void launch_dropout_bwd_add(void*, const void*, size_t, uint64_t, float, hipStream_t);
 
@@ -288,7 +288,8 @@ Tensor gelu_bwd(Tensor dy, Tensor x) {
 
 // ------------------------------------------------------------------ dropout (counter RNG)
 // embedding gather: weight [V, D] (any dtype, D·elem % 16 == 0), ids int64 (any shape) → [*ids, D]
-Tensor embedding_fwd(Tensor weight, Tensor ids) {
+// oob (optional int32 [1] on the device): set to 1 when an id is outside [0, V) (that row reads clamped)
+Tensor embedding_fwd(Tensor weight, Tensor ids, c10::optional<Tensor> oob) {
   CHECK_CONTIG(weight);
   TORCH_CHECK(weight.dim() == 2 && ids.scalar_type() == at::kLong, "embedding_fwd: weight [V, D], int64 ids");
   const int64_t V = weight.size(0), D = weight.size(1), el = weight.element_size();
@@ -297,7 +298,12 @@ Tensor embedding_fwd(Tensor weight, Tensor ids) {
   auto sizes = idc.sizes().vec();
   sizes.push_back(D);
   Tensor out = at::empty(sizes, weight.options());
-  launch_embedding_fwd(weight.data_ptr(), idc.data_ptr<int64_t>(), out.data_ptr(), idc.numel(), D, el, V, stream());
+  int* flag = nullptr;
+  if (oob.has_value() && oob->defined()) {
+    TORCH_CHECK(oob->scalar_type() == at::kInt && oob->is_cuda(), "embedding_fwd: oob int32 device tensor");
+    flag = oob->data_ptr<int>();
+  }
+  launch_embedding_fwd(weight.data_ptr(), idc.data_ptr<int64_t>(), out.data_ptr(), idc.numel(), D, el, V, flag, stream());
   return out;
 }
 // gradient of the gather: fp32 [V, D] (scatter-add of dout rows; padding_idx < 0: none)
@@ -1364,7 +1370,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_bwd", &gelu_bwd);
   m.def("ce_fwd_bwd", &ce_fwd_bwd);
   m.def("dropout_fwd", &dropout_fwd);
-  m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_fwd", &embedding_fwd, py::arg("weight"), py::arg("ids"), py::arg("oob") = py::none());
   m.def("embedding_bwd", &embedding_bwd);
   m.def("dropout_bwd_add", &dropout_bwd_add);
   m.def("grad_norm", &grad_norm);

@@ -16,13 +16,16 @@ namespace {
 
 __global__ __launch_bounds__(256) void embedding_fwd_k(const char* __restrict__ W, const int64_t* __restrict__ ids,
                                                        char* __restrict__ out, int64_t N, int row_chunks,
-                                                       int64_t V) {
+                                                       int64_t V, int* __restrict__ oob) {
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;   // global 16-B chunk index
   const int64_t n = c / row_chunks;
   if (n >= N) return;
   const int ch = (int)(c - n * row_chunks);
   int64_t id = ids[n];
-  id = id < 0 ? 0 : (id >= V ? V - 1 : id);   // clamped: a device-side range check would cost a host sync
+  if (id < 0 || id >= V) {   // out-of-range id: flag it (the host checks the word lazily) and read a valid row
+    if (oob) oob[0] = 1;
+    id = id < 0 ? 0 : V - 1;
+  }
   const u32x4 v = *reinterpret_cast<const u32x4*>(W + (id * row_chunks + ch) * 16);
   *reinterpret_cast<u32x4*>(out + (n * row_chunks + ch) * 16) = v;
 }
@@ -50,11 +53,11 @@ __global__ __launch_bounds__(256) void embedding_bwd_k(const T* __restrict__ dou
 bool embedding_supported(int64_t D, int64_t elem) { return (D * elem) % 16 == 0 && D % 8 == 0; }
 
 void launch_embedding_fwd(const void* W, const int64_t* ids, void* out, int64_t N, int64_t D, int64_t elem, int64_t V,
-                          hipStream_t st) {
+                          int* oob, hipStream_t st) {
   if (N == 0) return;
   const int row_chunks = (int)(D * elem / 16);
   const int64_t chunks = N * row_chunks;
-  embedding_fwd_k<<<(unsigned)((chunks + 255) / 256), 256, 0, st>>>((const char*)W, ids, (char*)out, N, row_chunks, V);
+  embedding_fwd_k<<<(unsigned)((chunks + 255) / 256), 256, 0, st>>>((const char*)W, ids, (char*)out, N, row_chunks, V, oob);
   LIPA_CHECK_LAUNCH();
 }
 

@@ -102,11 +102,18 @@ class PrefixCache:
     by all replicas (write-behind, off the engine loop), and a chunk missing from HBM and host is
     fetched from it before giving up — a prefix prefilled on one replica is warm on all of them.
 
-    ``salt`` separates hash chains whose K/V differ for the same tokens (multi-LoRA adapters)."""
+    ``namespace`` seeds every chain: the engine derives it from the model identity (name, a
+    fingerprint of the weights, dtype, layer count, KV width, block size, TP rank), so two
+    deployments sharing one remote store (a base and a fine-tuned model of the same shape) never
+    read each other's K/V — LMCache's keys carry the model name and format for the same reason.
+    ``salt`` separates hash chains whose K/V differ for the same tokens (multi-LoRA adapters); the
+    engine passes the adapter's NAME and path, not its slot index (which depends on the order of
+    ``--lora-modules``)."""
 
     def __init__(self, n_layers: int, width: int, dtype, device, block: int = 64, capacity_blocks: int = 512,
-                 host_blocks: int = 0, remote=None):
+                 host_blocks: int = 0, remote=None, namespace: bytes = b""):
         import collections
+        self.namespace = bytes(namespace)
         self.remote = remote
         self.remote_hits = 0
         self.block, self.capacity = block, capacity_blocks
@@ -126,9 +133,14 @@ class PrefixCache:
             self.hmap: "collections.OrderedDict[bytes, int]" = collections.OrderedDict()
             self.hfree = list(range(self.host_blocks))
 
-    def _digests(self, ids: list[int], n_blocks: int, salt: int = 0) -> list[bytes]:
+    def _digests(self, ids: list[int], n_blocks: int, salt: bytes | int = 0) -> list[bytes]:
         import hashlib
-        out, prev = [], (b"" if not salt else salt.to_bytes(8, "little"))
+        if isinstance(salt, int):
+            salt = b"" if not salt else salt.to_bytes(8, "little")
+        prev = self.namespace + (b"|" + salt if salt else b"")
+        if prev:
+            prev = hashlib.blake2b(prev, digest_size=16).digest()
+        out = []
         for i in range(n_blocks):
             h = hashlib.blake2b(prev, digest_size=16)
             h.update(torch.tensor(ids[i * self.block:(i + 1) * self.block], dtype=torch.int32).numpy().tobytes())
@@ -213,7 +225,7 @@ class PrefixCache:
                 return host[:, :, i].contiguous().view(torch.uint8).numpy().tobytes()
             self.remote.put(d, payload)
 
-    def match(self, ids: list[int], salt: int = 0) -> list[int]:
+    def match(self, ids: list[int], salt: bytes | int = 0) -> list[int]:
         """Pool indices of the longest cached chunk run (leaving >= 1 token to prefill)."""
         n = (len(ids) - 1) // self.block
         idx = []
@@ -238,7 +250,7 @@ class PrefixCache:
             cache.k[l][slot, :n] = self.k[l][t].reshape(n, -1)
             cache.v[l][slot, :n] = self.v[l][t].reshape(n, -1)
 
-    def store(self, ids: list[int], cache: KVCache, slot: int, salt: int = 0):
+    def store(self, ids: list[int], cache: KVCache, slot: int, salt: bytes | int = 0):
         """Insert every full prompt chunk of a freshly prefilled slot that is not cached yet."""
         n = len(ids) // self.block
         new = []
@@ -384,13 +396,20 @@ class ServingEngine:
         if prefix_cache_blocks > 0:
             self.prefix = PrefixCache(cfg.num_hidden_layers, cfg.num_key_value_heads * cfg.head_dim,
                                       self.lm.lm_head.weight.dtype, self.device, prefix_block, prefix_cache_blocks,
-                                      host_blocks=host_cache_blocks, remote=remote)
+                                      host_blocks=host_cache_blocks, remote=remote,
+                                      namespace=self._kv_namespace(prefix_block))
         # multi-LoRA serving (vLLM --enable-lora --lora-modules): stacked adapters, per-row masks;
         # built BEFORE the decode graphs are captured so the adapter term is part of every graph
         self.mlora = None
         if lora_modules:
             from ..peft.multi_lora import MultiLoraManager
             self.mlora = MultiLoraManager(self.lm, dict(lora_modules), max_rows=max_batch)
+        # prefix-cache chain salt per adapter slot: its name and path (slot 0 = the base model)
+        self._adapter_salt = [b""] + [f"{n}={p}".encode() for n, p in (lora_modules or {}).items()]
+        if self.mlora is not None:
+            self._adapter_salt = [b""] * (1 + len(self.mlora.names))
+            for n, i in self.mlora.index.items():
+                self._adapter_salt[i] = f"{n}={(lora_modules or {}).get(n, '')}".encode()
         self.slots: list[_Slot | None] = [None] * max_batch
         self.next_tok = torch.full((max_batch,), self.pad, dtype=torch.long, device=self.device)
         self.graphs = None
@@ -428,6 +447,25 @@ class ServingEngine:
 
     def encode(self, text: str) -> list[int]:
         return list(self.tok.encode(text, add_special_tokens=False))
+
+    def _kv_namespace(self, block: int) -> bytes:
+        """Model identity for the prefix-cache keys: served name, dims, dtype, block size, TP rank and
+        a fingerprint of the weights (a few rows of the embedding, the head and the last layer's
+        parameters — enough to tell a base model from its fine-tune of the same architecture)."""
+        import hashlib
+        cfg = self.lm.config
+        h = hashlib.blake2b(digest_size=16)
+        h.update(f"{self.model_name}|{cfg.num_hidden_layers}|{cfg.num_key_value_heads}|{cfg.head_dim}|"
+                 f"{self.lm.lm_head.weight.dtype}|{block}|tp{self.tp_rank}".encode())
+        params = list(self.lm.parameters())
+        with torch.no_grad():
+            for p in (params[0], params[-1], self.lm.lm_head.weight):
+                t = p.detach().reshape(-1)[:4096].float().cpu()
+                h.update(t.numpy().tobytes())
+        return h.digest()
+
+    def _salt(self, adapter: int) -> bytes:
+        return self._adapter_salt[adapter] if 0 <= adapter < len(self._adapter_salt) else str(adapter).encode()
 
     # ------------------------------------------------------------------ request API (thread-safe)
     @property
@@ -590,7 +628,7 @@ class ServingEngine:
                 if len(r.prompt_ids) > self.chunked_prefill:
                     P = 0
                     if self.prefix is not None:
-                        idx = self.prefix.match(r.prompt_ids, r.adapter)
+                        idx = self.prefix.match(r.prompt_ids, self._salt(r.adapter))
                         if idx:
                             self.prefix.load(idx, self.cache, slot)
                             P = len(idx) * self.prefix.block
@@ -604,7 +642,7 @@ class ServingEngine:
         if self.prefix is not None:
             rest = []
             for slot, r in new:
-                idx = self.prefix.match(r.prompt_ids, r.adapter)
+                idx = self.prefix.match(r.prompt_ids, self._salt(r.adapter))
                 if idx:
                     self._admit_suffix(slot, r, idx)
                 else:
@@ -612,7 +650,7 @@ class ServingEngine:
             if rest:
                 self._admit_batch(rest)
             for slot, r in new:      # (a slot that already finished keeps its rows until reused)
-                self.prefix.store(r.prompt_ids, self.cache, slot, r.adapter)
+                self.prefix.store(r.prompt_ids, self.cache, slot, self._salt(r.adapter))
             return
         self._admit_batch(new)
 
@@ -663,7 +701,7 @@ class ServingEngine:
         dev_toks, toks = self._sample(logits, [slot])
         self.next_tok[slot] = dev_toks[0]
         if self.prefix is not None:
-            self.prefix.store(r.prompt_ids, self.cache, slot, r.adapter)
+            self.prefix.store(r.prompt_ids, self.cache, slot, self._salt(r.adapter))
         self._accept(slot, toks[0], time.time())
 
     def _admit_suffix(self, slot, r, idx):

@@ -245,6 +245,37 @@ class CustomAllReduce:
         if self.backend == "hip" and self.peers is not None:
             self.peers.check()
 
+    def poll(self):
+        """Off-the-hot-path timeout check, once per optimizer step (DDP calls it after joining the
+        gradient buckets): the device error word copied at the PREVIOUS call — long finished by now —
+        is examined, then a fresh non-blocking copy is queued behind this step's reductions.  A
+        kernel-side barrier timeout (a peer that never arrived: its staging was stale) therefore
+        raises at the next step boundary instead of letting training continue on corrupted
+        gradients; the word is reset so a caller that handles the error can go on."""
+        peers = self.peers
+        if self.backend != "hip" or peers is None:
+            return
+        err = peers.err
+        pend = getattr(peers, "pending", None)
+        if pend is not None:
+            ev, host = pend
+            if ev is not None:
+                ev.synchronize()
+            if int(host[0]):
+                peers.pending = None
+                err.zero_()
+                raise RuntimeError("custom all-reduce: a peer missed a kernel-side barrier (timeout); "
+                                   "the reduced gradients of that step are not valid")
+        host = getattr(peers, "host_err", None)
+        if host is None:
+            host = peers.host_err = torch.zeros(1, dtype=torch.int32, pin_memory=err.is_cuda)
+        host.copy_(err, non_blocking=err.is_cuda)
+        ev = None
+        if err.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+        peers.pending = (ev, host)
+
     def close(self):
         if self.peers is not None:
             if self.backend == "hip":

@@ -202,6 +202,8 @@ class DistributedDataParallel(nn.Module):
         self._next = 0
         if self._stream is not None:
             torch.cuda.current_stream(self.grad_buffer.device).wait_stream(self._stream)
+        if self.car is not None:
+            self.car.poll()         # raises if a peer-memory reduction of the previous step timed out
         for work, view in self._works:
             work.wait()
             view.div_(dist.get_world_size())

@@ -97,6 +97,14 @@ class LossScaler:
                 self.cur_hyst = self.hysteresis
 
 
+def _in_backward() -> bool:
+    """True inside an autograd backward pass (e.g. a reentrant checkpoint's recompute)."""
+    try:
+        return torch._C._current_graph_task_id() != -1
+    except AttributeError:      # pragma: no cover - older torch
+        return False
+
+
 class _Unit:
     """A stage-3 partition unit: trainable params of one module, flattened and sharded."""
 
@@ -345,9 +353,12 @@ class ZeroEngine:
         def hook(mod, args):
             self._log("use_fwd", u)
             u.gather()
-            if self._recording and torch.is_grad_enabled() and u.index not in self._recorded:
+            recompute = _in_backward()      # an activation-checkpoint recompute inside the backward
+            # the execution order is recorded from the real forward whether or not it builds a graph
+            # (reentrant checkpointing runs it under no_grad); a recompute runs the units in reverse
+            if self._recording and not recompute and u.index not in self._recorded:
                 self._recorded.append(u.index)
-            seq = self.fwd_order
+            seq = self.fwd_order[::-1] if recompute else self.fwd_order
             if u.index in seq:
                 self._prefetch(seq, seq.index(u.index))
         return hook

@@ -75,3 +75,25 @@ def test_host_protocol_matches_sum(world):
         else:
             assert calls["oneshot"] == 4 and calls["twoshot"] == 6
     assert not [f for f in os.listdir("/dev/shm") if f.startswith("lipa_car_")]
+
+
+def test_poll_raises_on_kernel_timeout_word_and_resets():
+    """the kernel's timeout word is checked off the hot path (one step later) and reset."""
+    import types
+
+    import pytest
+    import torch
+
+    from llm_in_practise_amd.parallel.custom_allreduce import CustomAllReduce
+    car = CustomAllReduce.__new__(CustomAllReduce)
+    car.backend = "hip"
+    car.peers = types.SimpleNamespace(err=torch.zeros(1, dtype=torch.int32))
+    car.poll()                      # queues a copy of a clean word
+    car.poll()                      # clean -> no error
+    car.peers.err[0] = 1            # a kernel-side barrier timed out during this step
+    car.poll()                      # examines the previous (clean) copy, queues this one
+    with pytest.raises(RuntimeError, match="missed a kernel-side barrier"):
+        car.poll()
+    assert int(car.peers.err[0]) == 0
+    car.poll()
+    car.poll()

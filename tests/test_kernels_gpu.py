@@ -775,3 +775,21 @@ def test_embedding_gather_scatter_add(native_ext, V, D, dtype, pad):
         want[pad] = 0
     assert emb.weight.grad.dtype == dtype
     assert rel_err(emb.weight.grad, want) < 1e-2
+
+
+def test_embedding_out_of_range_id_raises(native_ext):
+    """F.embedding raises on an id >= V; the gather kernel flags it and the op raises
+    (lazily: at the next call, or at ops.embedding.check_ids())."""
+    from llm_in_practise_amd.ops.embedding import Embedding, check_ids
+    emb = Embedding(100, 64).to(DEV, torch.bfloat16)
+    with torch.no_grad():
+        emb(torch.randint(0, 100, (2, 8), device=DEV))
+        check_ids()                                   # clean
+        emb(torch.tensor([[5, 100]], device=DEV))     # 100 is out of range
+        with pytest.raises(IndexError, match="out of range"):
+            emb(torch.zeros(1, 4, dtype=torch.long, device=DEV))
+        emb(torch.zeros(1, 4, dtype=torch.long, device=DEV))   # reported once, then reset
+        emb(torch.tensor([[-3]], device=DEV))
+        with pytest.raises(IndexError, match="out of range"):
+            check_ids()
+        emb(torch.zeros(1, 4, dtype=torch.long, device=DEV))   # word was reset

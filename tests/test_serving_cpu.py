@@ -364,6 +364,11 @@ def test_remote_kv_tier_shares_prefix_chunks_across_replicas():
             assert torch.equal(cache_b.v[l][1, :32], cache_a.v[l][0, :32])
         assert b.match(ids) == idx and b.remote_hits == 4      # now served from B's own HBM pool
         assert b.match(list(range(7, 40))) == [] and rb.stats["misses"] >= 1
+        # another deployment of the same shape (different weights -> different namespace)
+        # on the same store must NOT read A's chunks; nor may a different adapter of A's model
+        other = PrefixCache(L, W, torch.float32, "cpu", block=B, capacity_blocks=8, remote=rb, namespace=b"ft-model")
+        assert other.match(ids) == [] and other.remote_hits == 0
+        assert a._digests(ids, 4, b"sql=/ad/sql") != a._digests(ids, 4, b"chat=/ad/chat") != a._digests(ids, 4)
         ra.close()
         rb.close()
     finally:

@@ -299,3 +299,35 @@ def test_checkpoint_repartitions_across_world_sizes(tmp_path):
         got = eng.consolidated_state_dict()
         for k in want:
             assert torch.allclose(got[k], want[k], atol=2e-5), (stage, k)
+
+
+class CkptNet(Net):
+    def forward(self, x):
+        import torch.utils.checkpoint as ckpt
+        h = self.inp(x)
+        for b in self.blocks:
+            h = h + ckpt.checkpoint(b, h, use_reentrant=True)
+        return self.out(h)
+
+
+def test_stage3_forward_order_recorded_under_reentrant_checkpointing():
+    """the first forward of a reentrant-checkpointed model runs under no_grad; the
+    prefetch order must still be the forward order (not the reversed recompute order), and the
+    engine trains identically to the un-checkpointed model."""
+    outs = []
+    for cls in (CkptNet, Net):
+        torch.manual_seed(0)
+        net = cls(d=32, n=4)
+        eng = ZeroEngine(net, {"zero_optimization": {"stage": 3, "stage3_param_persistence_threshold": 10},
+                               "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}}})
+        blocks = [u.index for u in eng.units if u.module in list(net.blocks)]
+        for s in range(3):
+            x, y = _data(s, 0)
+            x.requires_grad_(True)
+            eng.backward(((eng(x) - y) ** 2).mean())
+            eng.step()
+            pos = [eng.fwd_order.index(i) for i in blocks]
+            assert pos == sorted(pos), (cls.__name__, s, eng.fwd_order)
+        outs.append(eng.consolidated_state_dict())
+    for k in outs[1]:
+        assert torch.allclose(outs[0][k], outs[1][k], atol=1e-6), k
