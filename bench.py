@@ -132,7 +132,7 @@ def main():
             ds["train_micro_batch_size_per_gpu"] = args.micro_batch * args.grad_accum
             ds["train_batch_size"] = args.micro_batch * args.grad_accum * world
         engine = ZeroEngine(model, ds, lr=args.lr, weight_decay=0.0, hidden_size=cfg.hidden_size,
-                            total_steps=total_steps)
+                            total_steps=total_steps, optim=args.optim)
         opt = sched = ddp = None
     else:
         opt = build_optimizer(args.optim, [p for p in model.parameters() if p.requires_grad], args.lr,
@@ -239,7 +239,7 @@ def main():
                 "grad_accum": args.grad_accum,
                 "quant": "nf4+double_quant" if args.mode == "qlora" else "none",
                 "lora": f"r{args.lora_r}/a{args.lora_alpha}/drop{args.lora_dropout}/{args.targets}",
-                "optimizer": args.optim if engine is None else "zero3-adamw",
+                "optimizer": args.optim if engine is None else f"zero3-{engine.optim_name}",
                 "gradient_checkpointing": bool(args.grad_ckpt),
                 "ga_execution": "fused-pass" if args.ga_fusion else "sequential",
                 "weights": "random-init",

@@ -243,34 +243,51 @@ class AdamW8bit(_FlatOptimizer):
                                    self.eps, wd, self.step_count, clip, self.skip_flag)
             return
         # reference: dequantise states, fp32 update, requantise blockwise
-        n, B = self.flat.numel, self.BLOCK
-        pad = (-n) % B
-        blk = lambda t: torch.cat([t, t.new_zeros(pad)]).view(-1, B)  # noqa: E731
-        m = (self.code_s[self.qm.long()].view(-1) if not pad else self.code_s[self.qm.long()])
-        m = blk(m) * self.am[:, None]
-        v = blk(self.code_u[self.qv.long()]) * self.av[:, None]
-        gg = blk(g * (self.norm_out[1] if clip is not None else 1.0))
-        p = blk(self.flat.data)
-        lr_e = torch.empty(p.shape[0], 1, dtype=p.dtype, device=p.device)   # per-block lr / wd of its group
+        B = self.BLOCK
+        lr_e = torch.empty((self.flat.numel + B - 1) // B, 1, dtype=torch.float32, device=g.device)
         wd_e = torch.empty_like(lr_e)
-        for s0, s1, lr, wd in self._segments():
+        for s0, s1, lr, wd in self._segments():       # per-block lr / wd of its group
             lr_e[s0 // B:(s1 + B - 1) // B] = lr
             wd_e[s0 // B:(s1 + B - 1) // B] = wd
-        p.mul_(1 - lr_e * wd_e)
-        m.mul_(b1).add_(gg, alpha=1 - b1)
-        v.mul_(b2).addcmul_(gg, gg, value=1 - b2)
-        bc1, bc2 = 1 - b1 ** self.step_count, 1 - b2 ** self.step_count
-        p.add_(m / (v / bc2).sqrt().add_(self.eps) * (-lr_e / bc1))
-        self.flat.data.copy_(p.view(-1)[:n])
-        self.am.copy_(m.abs().amax(1))
-        self.av.copy_(v.amax(1))
-        from ..quant.nf4 import _nearest
-        self.qm.copy_(_nearest((m / self.am[:, None].clamp_min(1e-30)).view(-1)[:n], self.code_s))
-        self.qv.copy_(_nearest((v / self.av[:, None].clamp_min(1e-30)).view(-1)[:n], self.code_u))
+        adamw8bit_reference(self.flat.data, g * (self.norm_out[1] if clip is not None else 1.0), self.qm, self.qv,
+                            self.am, self.av, self.code_s, self.code_u, self.step_count, lr_e, b1, b2, self.eps, wd_e)
         if self.flat.mixed:
             self.flat.low.copy_(self.flat.data)
         elif self.flat.shadow is not None:
             self.flat.shadow.copy_(self.flat.data)
+
+
+def adamw8bit_reference(p, g, qm, qv, am, av, code_s, code_u, step, lr, b1, b2, eps, wd, block: int = 256):
+    """Blockwise 8-bit AdamW step in plain torch (the CPU twin of ``adamw8bit_k``): dequantise the
+    signed first / unsigned second moment with their per-block absmax, fp32 update, requantise to
+    the nearest dynamic-map code.  ``lr`` / ``wd``: floats or per-block [nb, 1] tensors; ``g`` is
+    already clip-scaled.  Updates p, qm, qv, am, av in place."""
+    from ..quant.nf4 import _nearest
+    n, B = p.numel(), block
+    pad = (-n) % B
+    blk = lambda t: torch.cat([t, t.new_zeros(pad)]).view(-1, B) if pad else t.view(-1, B)  # noqa: E731
+    m = blk(code_s[qm.long()]) * am[:, None]
+    v = blk(code_u[qv.long()]) * av[:, None]
+    gg = blk(g.float())
+    pp = blk(p.float())
+    pp.mul_(1 - lr * wd)
+    m.mul_(b1).add_(gg, alpha=1 - b1)
+    v.mul_(b2).addcmul_(gg, gg, value=1 - b2)
+    bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
+    if isinstance(lr, torch.Tensor):
+        pp.add_(m / (v / bc2).sqrt().add_(eps) * (-lr / bc1))
+    else:
+        pp.add_(m / (v / bc2).sqrt().add_(eps), alpha=-lr / bc1)
+    p.copy_(pp.view(-1)[:n])
+    am.copy_(m.abs().amax(1))
+    av.copy_(v.amax(1))
+    qm.copy_(_nearest((m / am[:, None].clamp_min(1e-30)).view(-1)[:n], code_s))
+    qv.copy_(_nearest((v / av[:, None].clamp_min(1e-30)).view(-1)[:n], code_u))
+
+
+def is_8bit(name: str) -> bool:
+    """HF ``optim`` names served by the blockwise 8-bit AdamW."""
+    return name.lower() in ("paged_adamw_8bit", "adamw_8bit", "adamw_bnb_8bit")
 
 
 NO_DECAY_DEFAULT = ("bias", "LayerNorm.weight", "norm.weight", "ln_", "ln1", "ln2", "ln_f")

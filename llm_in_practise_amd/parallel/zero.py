@@ -108,14 +108,14 @@ def _in_backward() -> bool:
 class _Unit:
     """A stage-3 partition unit: trainable params of one module, flattened and sharded."""
 
-    def __init__(self, name, module, params, world, rank, dtype, device, index=0):
+    def __init__(self, name, module, params, world, rank, dtype, device, index=0, block=1):
         self.name, self.module, self.params = name, module, params
         self.index = index
         self.shapes = [p.shape for p in params]
         self.numels = [p.numel() for p in params]
         n = sum(self.numels)
         self.n = n
-        self.npad = _pad_to(max(n, 1), world)
+        self.npad = _pad_to(max(n, 1), world * block)     # block: shards hold whole 8-bit state blocks
         self.shard_n = self.npad // world
         self.world, self.rank = world, rank
         self.dtype, self.device = dtype, device
@@ -179,8 +179,17 @@ class ZeroEngine:
     def __init__(self, model: nn.Module, config, lr: float | None = None, weight_decay: float | None = None,
                  betas=(0.9, 0.999), eps: float = 1e-8, hidden_size: int | None = None,
                  micro_batch: int | None = None, grad_accum: int | None = None, units: list[nn.Module] | None = None,
-                 total_steps: int = 10 ** 9):
+                 total_steps: int = 10 ** 9, optim: str | None = None):
+        """``optim``: a client optimizer by HF ``TrainingArguments.optim`` name.  ``"paged_adamw_8bit"`` /
+        ``"adamw_8bit"`` (``Fine-Tuning/qwen3-14b-qlora-dist-deepspeed.py:151,164``: the client 8-bit
+        paged AdamW under ``deepspeed=ds_zero3_config.json``) keeps blockwise-8-bit moments on each
+        rank's partition — every shard is a whole number of 256-element state blocks, so the blocks
+        (and the update) are the same at any world size; default / ``adamw_torch``: fp32 moments."""
+        from ..optim.adamw import is_8bit
         self.world, self.rank = _world(), _rank()
+        self.opt8 = bool(optim) and is_8bit(optim)
+        self.block = 256 if self.opt8 else 1
+        self.optim_name = "paged_adamw_8bit" if self.opt8 else "adamw"
         self.cfg: DSConfig = load_ds_config(config, self.world, micro_batch, grad_accum, hidden_size)
         self.module = model
         self.stage = self.cfg.zero.stage
@@ -229,7 +238,7 @@ class ZeroEngine:
         dtype = self.params[0].dtype
         n = sum(p.numel() for p in self.params)
         self.n = n
-        self.npad = _pad_to(n, W)
+        self.npad = _pad_to(n, W * self.block)
         self.shard_n = self.npad // W
         self.flat_model = torch.zeros(self.npad, dtype=dtype, device=self.device)
         self.flat_grad = torch.zeros(self.npad, dtype=torch.float32, device=self.device)
@@ -275,8 +284,8 @@ class ZeroEngine:
             with torch.no_grad():
                 for p in self.params:
                     dist.broadcast(p.data, src=0)
-        self.units = [_Unit(f"u{i}", u, groups[id(u)], W, r, self.params[0].dtype, self.device, index=i)
-                      for i, u in enumerate(order)]
+        self.units = [_Unit(f"u{i}", u, groups[id(u)], W, r, self.params[0].dtype, self.device, index=i,
+                            block=self.block) for i, u in enumerate(order)]
         self.master = torch.cat([u.shard.float() for u in self.units])
         self.grad_shard = torch.zeros_like(self.master)
         self.unit_offsets, o = [], 0
@@ -496,8 +505,18 @@ class ZeroEngine:
         if self.offload:
             self.master = self.master.cpu().pin_memory() if (self.cfg.zero.pin_memory and torch.cuda.is_available()) \
                 else self.master.cpu()
-        self.exp_avg = torch.zeros(self.master.numel(), dtype=torch.float32, device=dev)
-        self.exp_avg_sq = torch.zeros_like(self.exp_avg)
+        if self.opt8:      # blockwise 8-bit moments (bitsandbytes dynamic maps) on this rank's partition
+            from ..quant.nf4 import create_dynamic_map
+            n, nb = self.master.numel(), self.master.numel() // 256
+            self.code_s = create_dynamic_map(True).to(dev)
+            self.code_u = create_dynamic_map(False).to(dev)
+            self.qm = torch.full((n,), int(torch.argmin(self.code_s.abs())), dtype=torch.uint8, device=dev)
+            self.qv = torch.full((n,), int(torch.argmin(self.code_u.abs())), dtype=torch.uint8, device=dev)
+            self.am = torch.zeros(nb, dtype=torch.float32, device=dev)
+            self.av = torch.zeros(nb, dtype=torch.float32, device=dev)
+        else:
+            self.exp_avg = torch.zeros(self.master.numel(), dtype=torch.float32, device=dev)
+            self.exp_avg_sq = torch.zeros_like(self.exp_avg)
         self.opt_step = 0
 
     def _build_scheduler(self, total_steps):
@@ -637,7 +656,9 @@ class ZeroEngine:
         lr = self.param_groups[0]["lr"]
         self.opt_step += 1
         b1, b2 = self.betas
-        if self.offload:
+        if self.opt8:
+            self._step_8bit(g, norm, coef, lr, b1, b2)
+        elif self.offload:
             from ..ops._native import cpu_native
             gc = g.float().cpu()
             cpu_native().adamw_step(self.master, gc, self.exp_avg, self.exp_avg_sq, lr, b1, b2, self.eps, self.wd,
@@ -652,6 +673,24 @@ class ZeroEngine:
                            lr, b1, b2, self.eps, self.wd)
         self._publish_params()
         self.zero_grad()
+
+    def _step_8bit(self, g, norm, coef, lr, b1, b2):
+        gg = g.float().contiguous()
+        if self.offload:
+            gg = gg.cpu()
+        if use_native(self.master):
+            gs = torch.cat([norm.reshape(1), coef.reshape(1)]).float()
+            native().adamw8bit(self.master, gg, self.qm, self.qv, self.am, self.av, self.code_s, self.code_u, None, lr,
+                               b1, b2, self.eps, self.wd, self.opt_step, gs, None)
+        else:
+            from ..optim.adamw import adamw8bit_reference
+            adamw8bit_reference(self.master, gg * coef.to(gg.device), self.qm, self.qv, self.am, self.av, self.code_s,
+                                self.code_u, self.opt_step, lr, b1, b2, self.eps, self.wd)
+
+    def _state_tensors(self) -> dict:
+        if self.opt8:
+            return {"master": self.master, "qm": self.qm, "qv": self.qv, "am": self.am, "av": self.av}
+        return {"master": self.master, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}
 
     def _publish_params(self):
         m = self.master.to(self.device, non_blocking=True)
@@ -726,9 +765,9 @@ class ZeroEngine:
                         "loss_scale": self.scaler.scale, "client_state": client_state or {},
                         "ds_config": self.cfg.raw, "zero_stage": self.stage, "world_size": self.world},
                        os.path.join(d, "mp_rank_00_model_states.pt"))
-        torch.save({"master": self.master.cpu(), "exp_avg": self.exp_avg.cpu(), "exp_avg_sq": self.exp_avg_sq.cpu(),
+        torch.save({**{k: v.cpu() for k, v in self._state_tensors().items()}, "optim": self.optim_name,
                     "opt_step": self.opt_step, "zero_stage": self.stage, "rank": self.rank, "world": self.world,
-                    "layout": self._layout(),
+                    "layout": self._layout(), "block": self.block,
                     "lr_scheduler": self.lr_scheduler.state_dict() if self.lr_scheduler else None},
                    os.path.join(d, f"zero_pp_rank_{self.rank}_mp_rank_00_optim_states.pt"))
         if is_dist():
@@ -746,15 +785,24 @@ class ZeroEngine:
         ms = torch.load(os.path.join(d, "mp_rank_00_model_states.pt"), map_location="cpu", weights_only=True)
         os_ = torch.load(os.path.join(d, f"zero_pp_rank_{min(self.rank, ms.get('world_size', 1) - 1)}_mp_rank_00_optim_states.pt"),
                          map_location="cpu", weights_only=True)
+        if os_.get("optim", "adamw") != self.optim_name:
+            raise ValueError(f"checkpoint optimizer {os_.get('optim', 'adamw')!r} != engine optimizer {self.optim_name!r}")
+        st = self._state_tensors()
         if os_["world"] == self.world:
-            for k in ("master", "exp_avg", "exp_avg_sq"):
-                getattr(self, k).copy_(os_[k])
+            for k, t in st.items():
+                t.copy_(os_[k])
         else:                             # re-partition: rebuild the full vectors from every old shard
             old = [torch.load(os.path.join(d, f"zero_pp_rank_{r}_mp_rank_00_optim_states.pt"), map_location="cpu",
                               weights_only=True) for r in range(os_["world"])]
-            for k in ("master", "exp_avg", "exp_avg_sq"):
-                full = self._unshard([o[k] for o in old], os_.get("layout"), os_["world"])
-                getattr(self, k).copy_(self._shard_of(full))
+            ob = os_.get("block", 1)
+            for k, t in st.items():
+                if k in ("am", "av"):     # per-256-block scales: the same layout, counted in blocks
+                    lay = [(_pad_to(max(n, 1), 256)) // 256 for n in (os_.get("layout") or self._layout())]
+                    full = self._unshard([o[k] for o in old], lay, os_["world"], ob // 256 if ob >= 256 else 1)
+                    t.copy_(self._shard_of(full, block_units=True))
+                else:
+                    full = self._unshard([o[k] for o in old], os_.get("layout"), os_["world"], ob)
+                    t.copy_(self._shard_of(full))
         self.opt_step = os_["opt_step"]
         if self.lr_scheduler is not None and os_.get("lr_scheduler"):
             self.lr_scheduler.load_state_dict(os_["lr_scheduler"])
@@ -768,31 +816,38 @@ class ZeroEngine:
         """World-independent partition layout: numel per stage-3 unit, or [n] for stages 0-2."""
         return [u.n for u in self.units] if self.stage == 3 else [self.n]
 
-    def _unshard(self, shards: list[torch.Tensor], layout, world_old: int) -> torch.Tensor:
+    def _unshard(self, shards: list[torch.Tensor], layout, world_old: int, block_old: int = 1) -> torch.Tensor:
         layout = layout or self._layout()
         if self.stage == 0:               # replicated state
             return shards[0][:layout[0]]
         parts, offs = [], [0] * world_old
         for n in layout:
-            sn = _pad_to(max(n, 1), world_old) // world_old
+            sn = _pad_to(max(n, 1), world_old * block_old) // world_old
             full = torch.cat([shards[r][offs[r]:offs[r] + sn] for r in range(world_old)])
             parts.append(full[:n])
             offs = [o + sn for o in offs]
         return torch.cat(parts)
 
-    def _shard_of(self, full: torch.Tensor) -> torch.Tensor:
-        """This rank's shard of a full (unpadded) state vector in the current layout."""
+    def _shard_of(self, full: torch.Tensor, block_units: bool = False) -> torch.Tensor:
+        """This rank's shard of a full (unpadded) state vector in the current layout
+        (``block_units``: the vector counts 256-element blocks — the 8-bit state scales)."""
+        d = 256 if block_units else 1
         if self.stage == 3:
             out, o = [], 0
             for u in self.units:
-                v = torch.zeros(u.npad, dtype=full.dtype)
-                v[:u.n] = full[o:o + u.n]
-                out.append(v[self.rank * u.shard_n:(self.rank + 1) * u.shard_n])
-                o += u.n
+                n = (_pad_to(max(u.n, 1), 256) // 256) if block_units else u.n
+                v = torch.zeros(u.npad // d, dtype=full.dtype)
+                v[:n] = full[o:o + n]
+                sn = u.shard_n // d
+                out.append(v[self.rank * sn:(self.rank + 1) * sn])
+                o += n
             return torch.cat(out)
-        v = torch.zeros(self.npad, dtype=full.dtype)
-        v[:self.n] = full[:self.n]
-        return v[self.shard_slice]
+        n = (_pad_to(max(self.n, 1), 256) // 256) if block_units else self.n
+        v = torch.zeros(self.npad // d, dtype=full.dtype)
+        v[:n] = full[:n]
+        sn = self.shard_n // d
+        r0 = self.shard_slice.start // self.shard_n if self.shard_n else 0
+        return v[r0 * sn:(r0 + 1) * sn]
 
     # DeepSpeed accessors used by the reference scripts
     def train_micro_batch_size_per_gpu(self):

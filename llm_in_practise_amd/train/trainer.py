@@ -295,7 +295,8 @@ class Trainer:
             self.engine = ZeroEngine(self.model, a.deepspeed, lr=a.learning_rate, weight_decay=a.weight_decay,
                                      betas=(a.adam_beta1, a.adam_beta2), eps=a.adam_epsilon, hidden_size=hidden,
                                      micro_batch=a.per_device_train_batch_size,
-                                     grad_accum=a.gradient_accumulation_steps, total_steps=total_steps)
+                                     grad_accum=a.gradient_accumulation_steps, total_steps=total_steps,
+                                     optim=a.optim)     # client optimizer (paged_adamw_8bit) under ZeRO
             if self.engine.cfg.gradient_clipping == 0 and a.max_grad_norm > 0:
                 self.engine.clip = a.max_grad_norm
             self.optimizer = self.engine

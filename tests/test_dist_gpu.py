@@ -23,3 +23,5 @@ def test_bench_two_ranks_share_one_gpu(strategy):
     rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["n_gpus"] == 2 and rec["config"]["dist_world_size"] == 2 and rec["config"]["dist_backend"] == "gloo"
     assert rec["value"] > 0 and rec["config"]["parallelism"].endswith("dp2")
+    if strategy == "zero3":      # the client 8-bit AdamW runs on each rank's partition (E6)
+        assert rec["config"]["optimizer"] == "zero3-paged_adamw_8bit"

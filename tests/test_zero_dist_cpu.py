@@ -331,3 +331,67 @@ def test_stage3_forward_order_recorded_under_reentrant_checkpointing():
         outs.append(eng.consolidated_state_dict())
     for k in outs[1]:
         assert torch.allclose(outs[0][k], outs[1][k], atol=1e-6), k
+
+
+# ----------------------------------------------------------------------------- ZeRO + client 8-bit AdamW
+def _w8(rank, world, port, stage, out, steps=4, ckpt=None, load=None):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    net = Net(d=40, n=3)            # 40x40 blocks: units are not multiples of 256 (uneven padded shards)
+    eng = ZeroEngine(net, _cfg(stage), optim="paged_adamw_8bit")
+    start = 0
+    if load:
+        eng.load_checkpoint(load)
+        start = eng.global_steps
+    for s in range(start, start + steps):
+        xs, ys = zip(*[_data(s, r) for r in range(4)])
+        per = 8 // world            # the same global batch of 8 rows at every world size
+        x = torch.cat(xs)[:8].view(world, per, 8)[rank]
+        y = torch.cat(ys)[:8].view(world, per, 1)[rank]
+        eng.backward(((eng(x) - y) ** 2).mean())
+        eng.step()
+    if ckpt:
+        eng.save_checkpoint(ckpt)
+    sd = eng.consolidated_state_dict()
+    if rank == 0:
+        torch.save({"sd": sd, "am": eng.am.clone(), "optim": eng.optim_name}, out)
+    torch.distributed.destroy_process_group()
+
+
+def _w8_oracle(steps=4, stage=0):
+    """Single process, same 8-bit blocking: the flat layout (stages 0-2) or the per-unit layout (3)."""
+    torch.manual_seed(0)
+    net = Net(d=40, n=3)
+    eng = ZeroEngine(net, _cfg(stage), optim="paged_adamw_8bit")
+    for s in range(steps):
+        xs, ys = zip(*[_data(s, r) for r in range(4)])
+        eng.backward(((eng(torch.cat(xs)[:8]) - torch.cat(ys)[:8]) ** 2).mean())
+        eng.step()
+    return net.state_dict()
+
+
+@pytest.mark.parametrize("stage,world", [(3, 2), (3, 4), (2, 4), (1, 2)])
+def test_zero_with_client_8bit_adamw_matches_single_process(tmp_path, stage, world):
+    """E6 (qwen3-14b-qlora-dist-deepspeed.py:151,164): optim=paged_adamw_8bit under ZeRO keeps
+    blockwise-8-bit moments on each rank's partition; shards are whole 256-element blocks, so the
+    update equals the single-process 8-bit update at world 2 and 4 (to fp32 reduction-order noise)."""
+    out = str(tmp_path / "w8.pt")
+    mp.spawn(_w8, args=(world, _free_port(), stage, out), nprocs=world, join=True)
+    got = torch.load(out, weights_only=True)
+    assert got["optim"] == "paged_adamw_8bit"
+    want = _w8_oracle(stage=3 if stage == 3 else 0)
+    for k in want:
+        assert torch.allclose(got["sd"][k], want[k], atol=1e-4), (stage, world, k, (got["sd"][k] - want[k]).abs().max())
+
+
+def test_zero3_8bit_checkpoint_repartitions_4_to_2(tmp_path):
+    """8-bit states in the zero_pp_rank_* shards, re-partitioned on load (world 4 -> 2): training
+    resumed at world 2 equals uninterrupted training."""
+    ck = str(tmp_path / "ck")
+    mp.spawn(_w8, args=(4, _free_port(), 3, str(tmp_path / "a.pt"), 2, ck), nprocs=4, join=True)
+    mp.spawn(_w8, args=(2, _free_port(), 3, str(tmp_path / "b.pt"), 2, None, ck), nprocs=2, join=True)
+    resumed = torch.load(str(tmp_path / "b.pt"), weights_only=True)["sd"]
+    want = _w8_oracle(steps=4, stage=3)
+    for k in want:
+        assert torch.allclose(resumed[k], want[k], atol=1e-4), (k, (resumed[k] - want[k]).abs().max())
