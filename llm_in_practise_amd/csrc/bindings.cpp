@@ -40,8 +40,6 @@ void launch_absmax_t(const float*, const uint8_t*, const float*, const float*, c
                      hipStream_t);
 void launch_nf4_quantize(const void*, uint8_t*, float*, size_t, hipStream_t);
 void launch_nf4_dequant2(const uint8_t*, const float*, void*, size_t, hipStream_t);
-void launch_nf4_dequant_bg(int, const uint8_t* const*, const float* const*, void* const*, const size_t*, int,
-                           hipStream_t);
 int skinny_splits(int, int);
 bool lt_gemm(bool, bool, long, long, long, const void*, long, const void*, long, const void*, void*, long, int, long,
              long, long, void*, size_t, hipStream_t, bool);
@@ -55,6 +53,9 @@ void set_dequant_variant(int);
 void launch_nf4_dequant(const uint8_t*, const float*, const uint8_t*, const float*, const float*, const float*, void*,
                         size_t, hipStream_t);
 bool gemm8_supported(int, int, int, int, int);
+bool gemm4w_supported(int, int, int, int, int);
+int gemm4w_splits(int, int, int);
+void launch_gemm4w(const void*, int, const void*, int, const void*, void*, float*, int, int, int, int, hipStream_t);
 int gemm8_splits(int, int, int);
 void launch_gemm8(const void*, int, const void*, int, const void*, const void*, int, const void*, void*, float*, int, int,
                   int, int, hipStream_t);
@@ -93,10 +94,6 @@ void launch_lora_dA_pair(const float*, const float*, int, int, const void*, int,
                          int64_t, int64_t, const uint8_t*, const uint8_t*, float, float, int, hipStream_t);
 void launch_lora_dx2(const float*, const float*, int, const void*, const void*, int, int, const uint8_t*,
                      const uint8_t*, float, float, void*, int, int, hipStream_t);
-void launch_lora_dA_multi(int, const float* const*, const int*, float* const*, const int*, const uint64_t*, const float*,
-                          const void*, int, int, int, size_t, hipStream_t);
-void launch_lora_dx_multi(int, const float* const*, const int*, const void* const*, const int*, const uint64_t*,
-                          const float*, void*, int, int, size_t, hipStream_t);
 void launch_lora_apply(void*, int, int, int, const float* const*, const int*, const void* const*, void* const*, const int*, const int*,
                        const int*, hipStream_t);
 void launch_lora_acc(const float*, int, int, const void*, int, void*, int, const void*, int, float*, int64_t, int64_t,
@@ -540,32 +537,6 @@ Tensor nf4_dequant_fast(Tensor codes, Tensor absmax, int64_t N, int64_t K) {
 }
 
 // background expansion of up to 4 NF4 weights in one small persistent grid (see gemm.hip)
-std::vector<Tensor> nf4_dequant_bg(std::vector<Tensor> codes, std::vector<Tensor> absmax, std::vector<int64_t> N,
-                                   std::vector<int64_t> K, int64_t grid) {
-  const int nj = (int)codes.size();
-  TORCH_CHECK(nj >= 1 && nj <= 4 && (int)absmax.size() == nj && (int)N.size() == nj && (int)K.size() == nj && grid > 0,
-              "nf4_dequant_bg: 1-4 jobs");
-  std::vector<Tensor> out;
-  const uint8_t* cp[4];
-  const float* ap[4];
-  void* wp[4];
-  size_t ne[4];
-  for (int j = 0; j < nj; ++j) {
-    CHECK_CUDA(codes[j]);
-    CHECK_CONTIG(codes[j]);
-    CHECK_CONTIG(absmax[j]);
-    TORCH_CHECK(codes[j].numel() * 2 == N[j] * K[j] && K[j] % 64 == 0 && absmax[j].scalar_type() == at::kFloat &&
-                    absmax[j].numel() * 64 == N[j] * K[j] && reinterpret_cast<uintptr_t>(codes[j].data_ptr()) % 16 == 0,
-                "nf4_dequant_bg: job shapes");
-    out.push_back(at::empty({N[j], K[j]}, codes[j].options().dtype(at::kBFloat16)));
-    cp[j] = codes[j].data_ptr<uint8_t>();
-    ap[j] = absmax[j].data_ptr<float>();
-    wp[j] = out.back().data_ptr();
-    ne[j] = (size_t)(N[j] * K[j]);
-  }
-  launch_nf4_dequant_bg(nj, cp, ap, wp, ne, (int)grid, stream());
-  return out;
-}
 
 Tensor nf4_dequant(Tensor codes, optional<Tensor> absmax, optional<Tensor> qabs, optional<Tensor> absmax2,
                    optional<Tensor> offset, optional<Tensor> dcode, int64_t N, int64_t K) {
@@ -680,6 +651,33 @@ Tensor gemm_nf4_t(Tensor dy, Tensor codes_b, Tensor absmax_t, int64_t K, optiona
 
 Tensor gemm8(Tensor x, Tensor w, optional<Tensor> ext_a, optional<Tensor> ext_b, optional<Tensor> residual,
              int64_t splits);
+
+
+// y = x·wᵀ (+ residual) through the one-wave-per-SIMD AGPR-accumulator MFMA GEMM (gemm4w.hip);
+// x [M, K] (row stride any multiple of 8), w [N, K] contiguous rows.  splits <= 0: auto split-K
+Tensor gemm4w(Tensor x, Tensor w, optional<Tensor> residual, int64_t splits) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1, "gemm4w: 2-D, unit inner stride");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "gemm4w: K mismatch");
+  TORCH_CHECK(gemm4w_supported(M, N, K, x.stride(0), w.stride(0)), "gemm4w: unsupported shape / strides");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              "gemm4w: 16-byte aligned operands");
+  const void* res = nullptr;
+  if (residual && residual->defined()) {
+    CHECK_BF16(*residual);
+    TORCH_CHECK(residual->is_contiguous() && residual->size(0) == M && residual->size(1) == N, "gemm4w: residual [M, N]");
+    res = residual->data_ptr();
+  }
+  const int sp = splits > 0 ? (int)splits : gemm4w_splits(M, N, K);
+  auto y = at::empty({M, N}, x.options());
+  Tensor ws;
+  if (sp > 1) ws = at::empty({sp, M, N}, x.options().dtype(at::kFloat));
+  launch_gemm4w(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), res, y.data_ptr(),
+                sp > 1 ? ws.data_ptr<float>() : nullptr, M, N, K, sp, stream());
+  return y;
+}
 
 // y = x·wᵀ (+ LoRA K-slice) (+ residual) for a frozen bf16 base: the hand-written 8-phase MFMA GEMM
 // (gemm8.hip) whenever the shape / strides allow it, library GEMM otherwise.
@@ -1079,72 +1077,6 @@ Tensor lora_dx2(Tensor g0, Tensor g1, Tensor a0, Tensor a1, Tensor masks, double
   return out;
 }
 
-// up to 4 adapters on one input x [M, K] (keys / p: each branch's dropout; masks regenerated from the counter RNG
-// over x's row stride, as in the forward's lora_proj):
-//   lora_dx_multi: Σ_i D_i(G_i·A_i)·ds_i -> bf16 [M, K] (the dX GEMM's C matrix)
-//   lora_dA_multi: dA_i [r_i, K] += G_iᵀ·D_i(x)·ds_i (fp32 atomics), one launch
-static void multi_common(const std::vector<Tensor>& gs, int64_t M, std::vector<const float*>& gp, std::vector<int>& ld,
-                         std::vector<int>& r, const char* who) {
-  TORCH_CHECK(gs.size() >= 1 && gs.size() <= 4, who, ": 1..4 branches");
-  for (const Tensor& g : gs) {
-    TORCH_CHECK(g.scalar_type() == at::kFloat && g.dim() == 2 && g.stride(1) == 1 && g.size(0) == M && g.size(1) <= 16 &&
-                    g.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0,
-                who, ": g fp32 [M, r<=16], 16-B aligned rows");
-    gp.push_back(g.data_ptr<float>());
-    ld.push_back(g.stride(0));
-    r.push_back(g.size(1));
-  }
-}
-
-Tensor lora_dx_multi(std::vector<Tensor> gs, std::vector<Tensor> as, std::vector<double> ps, std::vector<int64_t> keys,
-                     int64_t mask_ld) {
-  const int nb = gs.size();
-  TORCH_CHECK((int)as.size() == nb && (int)ps.size() == nb && (int)keys.size() == nb, "lora_dx_multi: per-branch lists");
-  const int64_t M = gs[0].size(0), K = as[0].size(1);
-  std::vector<const float*> gp;
-  std::vector<int> ld, r;
-  multi_common(gs, M, gp, ld, r, "lora_dx_multi");
-  std::vector<const void*> ap;
-  std::vector<float> pf;
-  std::vector<uint64_t> kf;
-  for (int i = 0; i < nb; ++i) {
-    CHECK_BF16(as[i]);
-    TORCH_CHECK(as[i].is_contiguous() && as[i].size(0) == r[i] && as[i].size(1) == K && K % 8 == 0,
-                "lora_dx_multi: A_i [r_i, K]");
-    ap.push_back(as[i].data_ptr());
-    pf.push_back((float)ps[i]);
-    kf.push_back((uint64_t)keys[i]);
-  }
-  Tensor out = at::empty({M, K}, as[0].options());
-  launch_lora_dx_multi(nb, gp.data(), ld.data(), ap.data(), r.data(), kf.data(), pf.data(), out.data_ptr(), M, K,
-                       (size_t)mask_ld, stream());
-  return out;
-}
-
-void lora_dA_multi(std::vector<Tensor> gs, Tensor x, std::vector<Tensor> outs, std::vector<double> ps,
-                   std::vector<int64_t> keys) {
-  const int nb = gs.size();
-  TORCH_CHECK((int)outs.size() == nb && (int)ps.size() == nb && (int)keys.size() == nb, "lora_dA_multi: per-branch lists");
-  CHECK_BF16(x);
-  const int64_t M = x.size(0), K = x.size(1);
-  TORCH_CHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && K % 128 == 0, "lora_dA_multi: x layout");
-  std::vector<const float*> gp;
-  std::vector<int> ld, r;
-  multi_common(gs, M, gp, ld, r, "lora_dA_multi");
-  std::vector<float*> op;
-  std::vector<float> pf;
-  std::vector<uint64_t> kf;
-  for (int i = 0; i < nb; ++i) {
-    TORCH_CHECK(outs[i].scalar_type() == at::kFloat && outs[i].is_contiguous() && outs[i].size(0) == r[i] &&
-                    outs[i].size(1) == K, "lora_dA_multi: out fp32 [r_i, K] contiguous");
-    op.push_back(outs[i].data_ptr<float>());
-    pf.push_back((float)ps[i]);
-    kf.push_back((uint64_t)keys[i]);
-  }
-  launch_lora_dA_multi(nb, gp.data(), ld.data(), op.data(), r.data(), kf.data(), pf.data(), x.data_ptr(), x.stride(0), K,
-                       M, (size_t)x.stride(0), stream());
-}
-
 // ------------------------------------------------------------------ generation (K16, K17)
 // q [B, hq*d] bf16; kc/vc [B, Smax, hkv*d] bf16 contiguous; lens [B] int32 (valid keys per row);
 // max_len >= max(lens) bounds the split count without a host sync.
@@ -1383,8 +1315,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lora_proj_pair", &lora_proj_pair);
   m.def("lora_acc_pair", &lora_acc_pair);
   m.def("lora_dA_pair", &lora_dA_pair);
-  m.def("lora_dx_multi", &lora_dx_multi);
-  m.def("lora_dA_multi", &lora_dA_multi);
   m.def("lora_dx2", &lora_dx2);
   m.def("lora_apply", &lora_apply);
   m.def("gemm_int4", &gemm_int4);
@@ -1396,7 +1326,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequant", &nf4_dequant);
   m.def("nf4_dequant_fast", &nf4_dequant_fast);
-  m.def("nf4_dequant_bg", &nf4_dequant_bg);
   m.def("gemm_skinny", &gemm_skinny);
   m.def("lt_linear", &lt_linear);
   m.def("lt_dx", &lt_dx);
@@ -1407,6 +1336,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nf4_absmax_t", &nf4_absmax_t);
   m.def("gemm_nf4", &gemm_nf4);
   m.def("gemm8", &gemm8);
+  m.def("gemm4w", &gemm4w);
   m.def("gemm_nf4_t", &gemm_nf4_t);
   m.def("gemm_bf16", &gemm_bf16);
   m.def("gemm_bf16_t", &gemm_bf16_t);

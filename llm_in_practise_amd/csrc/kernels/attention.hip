@@ -16,8 +16,6 @@
 // query tiles (no atomics), P is recomputed from the saved log-sum-exp, dQ is accumulated
 // with fp32 atomics (the dQ sum spans key blocks).  GQA partial dK/dV per q-head are summed
 // in a finalize pass (deterministic).
-#include <map>
-#include <mutex>
 
 #include "common.h"
 
@@ -128,7 +126,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const bf16* __restrict__ Q,
                                                   const int* __restrict__ kv_lens, const int* __restrict__ q_offs,
                                                   bf16* __restrict__ O, float* __restrict__ lse, int Sq, int Skv,
                                                   int kv_rows, int hq, int hkv, int causal, float scale_log2,
-                                                  DropParams dp, float defer_thr) {
+                                                  DropParams dp) {
   constexpr int LDR = D + 8;        // padded LDS row (elements)
   constexpr int CH = D / 8;         // 16-B chunks per row
   constexpr int TILE = 64 * LDR;    // elements per K or V tile
@@ -252,11 +250,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const bf16* __restrict__ Q,
         for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sc[kt][qt][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      // deferred max (defer_thr > 0, cdna guide T13): the running max moves only when some query of
-      // the wave grew by more than defer_thr in the exponent's log2 units; P is then bounded by
-      // 2^defer_thr instead of 1 and most tiles skip the O rescale.  defer_thr = 0: exact update.
-      const bool upd = __any((mx - m_run[qt]) * scale_log2 > defer_thr);
-      const float mn = upd ? fmaxf(m_run[qt], mx) : m_run[qt];
+      const float mn = fmaxf(m_run[qt], mx);
       const bool dead = mn == -INFINITY;   // every key so far masked for this query
       const float alpha = dead ? 1.f : fexp2((m_run[qt] - mn) * scale_log2);
       const float mc = dead ? 0.f : mn * scale_log2;
@@ -334,7 +328,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const bf16* __restrict__ Q,
 //    registers) that sweeps every q-head of its GQA group × 64-query tiles, so the group's
 //    dK/dV sum stays in registers: no fp32 partials, no finalize pass.  Q/dO tiles (plus
 //    their lse/delta) are register-prefetched one tile ahead into double-buffered LDS.
-template <int D, int PF, bool DIN>
+template <int D, int PF>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(const bf16* __restrict__ dO, const bf16* __restrict__ O,
                                                      const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ V, const float* __restrict__ lse,
@@ -367,19 +361,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(const bf16* __restrict__
     const size_t off = (tok0 + qc) * ldo + h * D + 32 * s + 8 * g;
     qf[s] = *reinterpret_cast<const bf16x8*>(Q + (tok0 + qc) * ldq + h * D + 32 * s + 8 * g);
     dof[s] = *reinterpret_cast<const bf16x8*>(dO + off);
-    if constexpr (!DIN) {
-      const bf16x8 of = *reinterpret_cast<const bf16x8*>(O + off);
+    const bf16x8 of = *reinterpret_cast<const bf16x8*>(O + off);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dsum += (float)dof[s][j] * (float)of[j];
-    }
+    for (int j = 0; j < 8; ++j) dsum += (float)dof[s][j] * (float)of[j];
   }
-  if constexpr (DIN) {   // delta precomputed by attn_delta_k (the dK/dV kernel runs beside this one)
-    dsum = delta[bh + qc];
-  } else {
-    dsum += __shfl_xor(dsum, 16, 64);
-    dsum += __shfl_xor(dsum, 32, 64);
-    if (g == 0 && qa < S) delta[bh + qa] = dsum;
-  }
+  dsum += __shfl_xor(dsum, 16, 64);
+  dsum += __shfl_xor(dsum, 32, 64);
+  if (g == 0 && qa < S) delta[bh + qa] = dsum;
   const float lse2 = lse[bh + qc] * LOG2E;
   const int klim = min(causal ? qa : S, kvlen - 1);  // last key this query may see
 
@@ -489,38 +477,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(const bf16* __restrict__
   }
 }
 
-// delta[b, h, q] = Σ_d dO·O (fp32) on its own, so the dQ and dK/dV kernels can run side by side:
-// 16 lanes per (token, head) row of D (D / 16 elements each), a wave covers 4 rows.
-template <int D>
-__global__ __launch_bounds__(256) void attn_delta_k(const bf16* __restrict__ dO, const bf16* __restrict__ O,
-                                                   float* __restrict__ delta, int B, int S, int hq) {
-  constexpr int EL = D / 16;   // elements per lane (2 .. 8)
-  const int64_t rowi = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;   // (token, head) row
-  const int sub = threadIdx.x & 15;
-  const int64_t T = (int64_t)B * S;
-  const bool live = rowi < T * hq;
-  const int64_t r = live ? rowi : 0;
-  const int64_t tok = r / hq;
-  const int h = (int)(r - tok * hq);
-  const size_t off = (size_t)tok * hq * D + (size_t)h * D + sub * EL;
-  float acc = 0.f;
-  if constexpr (EL == 8) {
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(dO + off), o = *reinterpret_cast<const bf16x8*>(O + off);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc += (float)a[j] * (float)o[j];
-  } else {
-#pragma unroll
-    for (int j = 0; j < EL; ++j) acc += (float)dO[off + j] * (float)O[off + j];
-  }
-  acc += __shfl_xor(acc, 1, 64);
-  acc += __shfl_xor(acc, 2, 64);
-  acc += __shfl_xor(acc, 4, 64);
-  acc += __shfl_xor(acc, 8, 64);
-  if (live && sub == 0) {
-    const int b = (int)(tok / S), q = (int)(tok - (int64_t)b * S);
-    delta[((size_t)b * hq + h) * S + q] = acc;
-  }
-}
 
 // HALVES = 2: a 512-thread workgroup, the two 4-wave halves sweep different q-heads of the GQA
 // group over the SAME 64 keys (2 waves per SIMD instead of 1) and meet in LDS at the end.
@@ -799,42 +755,6 @@ static int attn_pf(int dflt) {
   return pf == 1 || pf == 2 ? pf : dflt;
 }
 
-static int attn_two_streams() {
-  static const int v = [] { const char* e = getenv("LIPA_ATTN_BWD_STREAMS"); return e ? atoi(e) : 0; }();
-  return v;
-}
-
-static bool stream_capturing(hipStream_t st) {
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  return hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
-}
-
-// one side stream + fork / join events per device (created on first use, never destroyed); the
-// side stream gets the higher priority so the dK/dV kernel's heavy blocks are dispatched first
-static bool side_stream(hipStream_t* s, hipEvent_t* fork, hipEvent_t* join) {
-  struct Side { hipStream_t s; hipEvent_t f, j; };
-  static std::mutex mu;
-  static std::map<int, Side> sides;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = sides.find(dev);
-  if (it == sides.end()) {
-    Side sd{};
-    int lo = 0, hi = 0;
-    hipDeviceGetStreamPriorityRange(&lo, &hi);
-    if (hipStreamCreateWithPriority(&sd.s, hipStreamNonBlocking, hi) != hipSuccess) return false;
-    if (hipEventCreateWithFlags(&sd.f, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&sd.j, hipEventDisableTiming) != hipSuccess)
-      return false;
-    it = sides.emplace(dev, sd).first;
-  }
-  *s = it->second.s;
-  *fork = it->second.f;
-  *join = it->second.j;
-  return true;
-}
-
 void launch_attn_fwd(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv, const int* kv_lens,
                      const int* q_offs, void* o, float* lse, int B, int Sq, int Skv, int kv_rows, int hq, int hkv,
                      int D, int causal, float scale, float p_drop, uint64_t seed, hipStream_t st) {
@@ -844,14 +764,12 @@ void launch_attn_fwd(const void* q, const void* k, const void* v, int ldq, int l
   // S = 512 / 8192 and equal at 2048 (profiles/attention_fwd_bwd.txt).  LIPA_ATTN_QT=1|2 forces one.
   static const int qt_env = [] { const char* e = getenv("LIPA_ATTN_QT"); return e ? atoi(e) : 0; }();
   const int qt = qt_env == 1 || qt_env == 2 ? qt_env : 2;
-  static const float defer = [] { const char* e = getenv("LIPA_ATTN_DEFER"); return e ? (float)atof(e) : 0.f; }();
   dim3 grid((Sq + 64 * qt - 1) / (64 * qt), hq, B), blk(256);
   const float sl2 = scale * LOG2E;
 #define FWD(PFV, QTV)                                                                                      \
   LIPA_ATTN_D(D, attn_fwd_k<DD, PFV, QTV><<<grid, blk, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,  \
                                                            ldq, ldk, ldv, kv_lens, q_offs, (bf16*)o, lse, Sq, Skv, \
-                                                           kv_rows, hq, hkv, causal ? 1 | (attn_lpt() << 1) : 0, sl2, dp, \
-                                                           defer))
+                                                           kv_rows, hq, hkv, causal ? 1 | (attn_lpt() << 1) : 0, sl2, dp))
   if (qt == 1) {
     FWD(1, 1);
   } else {
@@ -870,48 +788,21 @@ void launch_attn_bwd(const void* dout, const void* q, const void* k, const void*
   const int nb = (S + 63) / 64;
   const int nsplit = ws ? attn_dkv_nsplit(B, S, hkv, causal) : 0;
   dim3 gq(nb, hq, B), gkv(nb + nsplit, hkv, B), blk(256);
-  // Two streams (causal): the dK/dV grid is one 8-wave workgroup per 64-key block and its work falls
-  // off linearly with the block index (block 0 sweeps every query tile, the last one tile), so most
-  // CUs go idle long before it ends.  With delta computed up front, the dK/dV kernel runs on a side
-  // stream (launched first: its heavy blocks start at once) while the dQ grid fills the CUs its light
-  // blocks release; the caller's stream waits for both.  Opt-in (LIPA_ATTN_BWD_STREAMS=1): measured
-  // SLOWER at the bench shape (bwd 92.5 -> 117.9 us, step +0.9 ms; profiles/attention_fwd_bwd.txt) —
-  // the dQ grid's 1024 workgroups take the CUs first and stretch the dK/dV critical path.
-  hipStream_t kst = st;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  const bool two = causal && attn_two_streams() && !stream_capturing(st) &&
-                   side_stream(&kst, &ev_fork, &ev_join);
-  if (two) {
-    const int64_t rows = (int64_t)B * S * hq;
-    LIPA_ATTN_D(D, attn_delta_k<DD><<<(unsigned)((rows * 16 + 255) / 256), 256, 0, st>>>((const bf16*)dout,
-                                                                                        (const bf16*)o, delta, B, S, hq));
-    hipEventRecord(ev_fork, st);
-    hipStreamWaitEvent(kst, ev_fork, 0);
-  }
 #define DKV(DD, PFKV)                                                                                             \
   if ((hq / hkv) % 2 == 0)                                                                                       \
-    attn_bwd_dkv_k<DD, 2, PFKV><<<gkv, 512, 0, kst>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k,           \
+    attn_bwd_dkv_k<DD, 2, PFKV><<<gkv, 512, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k,           \
                                                       (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, \
                                                       (bf16*)dv, S, hq, hkv, causal, scale, sl2, dp, ws, nsplit);   \
   else                                                                                                           \
-    attn_bwd_dkv_k<DD, 1, PFKV><<<gkv, 256, 0, kst>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k,           \
+    attn_bwd_dkv_k<DD, 1, PFKV><<<gkv, 256, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k,           \
                                                       (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, \
                                                       (bf16*)dv, S, hq, hkv, causal, scale, sl2, dp, ws, nsplit)
-// two streams: dK/dV first on the side stream (delta is ready), dQ beside it; one stream: dQ first
-// (it writes delta), then dK/dV
+// dQ first (it writes delta), then dK/dV
 #define RUN(DD, PFQ, PFKV)                                                                                        \
-  if (two) {                                                                                                     \
-    DKV(DD, PFKV);                                                                                               \
-    attn_bwd_dq_k<DD, PFQ, true><<<gq, blk, 0, st>>>((const bf16*)dout, (const bf16*)o, (const bf16*)q,          \
-                                                     (const bf16*)k, (const bf16*)v, lse, delta, kv_lens, ldq, ldk, \
-                                                     ldv, (bf16*)dq, S, hq, hkv, 1 | (attn_lpt() << 1), scale, sl2, dp); \
-  } else {                                                                                                       \
-    attn_bwd_dq_k<DD, PFQ, false><<<gq, blk, 0, st>>>((const bf16*)dout, (const bf16*)o, (const bf16*)q,         \
-                                                      (const bf16*)k, (const bf16*)v, lse, delta, kv_lens, ldq, ldk, \
-                                                      ldv, (bf16*)dq, S, hq, hkv, causal ? 1 | (attn_lpt() << 1) : 0, \
-                                                      scale, sl2, dp);                                            \
-    DKV(DD, PFKV);                                                                                               \
-  }
+  attn_bwd_dq_k<DD, PFQ><<<gq, blk, 0, st>>>((const bf16*)dout, (const bf16*)o, (const bf16*)q, (const bf16*)k,   \
+                                             (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dq, S, hq, \
+                                             hkv, causal ? 1 | (attn_lpt() << 1) : 0, scale, sl2, dp);            \
+  DKV(DD, PFKV);
   const int pfq = attn_pf(2), pfkv = attn_pf(1);
   if (pfq == 2 && pfkv == 1) {
     LIPA_ATTN_D(D, RUN(DD, 2, 1));
@@ -925,11 +816,7 @@ void launch_attn_bwd(const void* dout, const void* q, const void* k, const void*
   if (nsplit > 0) {
     const int ldkv = hkv * D, rows = std::min(nsplit * 64, S);
     const size_t n4 = (size_t)B * rows * ldkv / 4;
-    attn_dkv_fin_k<<<(unsigned)((n4 + 255) / 256), 256, 0, kst>>>(ws, (bf16*)dk, (bf16*)dv, B, S, ldkv, rows, scale);
-  }
-  if (two) {
-    hipEventRecord(ev_join, kst);
-    hipStreamWaitEvent(st, ev_join, 0);
+    attn_dkv_fin_k<<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(ws, (bf16*)dk, (bf16*)dv, B, S, ldkv, rows, scale);
   }
   LIPA_CHECK_LAUNCH();
 }

@@ -180,58 +180,6 @@ __global__ __launch_bounds__(256) void nf4_dequant3_k(const uint32_t* __restrict
   }
 }
 
-// Background form of variant 3 for the next layer's weights (up to 4 tensors in one launch): a
-// small persistent grid (G workgroups, 2 KB LDS, few VGPRs) walks the 1024-vector chunks of all jobs,
-// so it can sit beside a GEMM that holds one workgroup per CU without taking the slots the GEMM
-// needs (the full-size grid of variant 3 floods every CU).
-struct DqJobs {
-  const uint32_t* codes[4];
-  const float* absmax[4];
-  bf16* w[4];
-  size_t n8[4];
-  size_t chunk0[5];   // prefix sums of ceil(n8 / BG_CHUNK)
-  int njobs;
-};
-
-// BG_ITEMS 8-element vectors per thread per chunk (all loads of a chunk in flight together: a small
-// grid needs the per-workgroup memory parallelism the full-size grid gets from its workgroup count)
-constexpr int BG_ITEMS = 16, BG_CHUNK = 256 * BG_ITEMS;
-__global__ __launch_bounds__(256) void nf4_dequant_bg_k(DqJobs jb) {
-  __shared__ float2 tab[256];
-  tab[threadIdx.x] = make_float2(kNF4[threadIdx.x >> 4], kNF4[threadIdx.x & 15]);
-  __syncthreads();
-  const size_t total = jb.chunk0[jb.njobs];
-  int j = 0;
-  for (size_t ch = blockIdx.x; ch < total; ch += gridDim.x) {
-    while (ch >= jb.chunk0[j + 1]) ++j;   // chunks only grow along the loop
-    const uint32_t* codes = jb.codes[j];
-    const float* absmax = jb.absmax[j];
-    bf16* w = jb.w[j];
-    const size_t n8 = jb.n8[j];
-    const size_t base = (ch - jb.chunk0[j]) * BG_CHUNK + threadIdx.x;
-    uint32_t c[BG_ITEMS];
-    float a[BG_ITEMS];
-#pragma unroll
-    for (int q = 0; q < BG_ITEMS; ++q) {
-      const size_t i = base + 256 * q;
-      c[q] = i < n8 ? codes[i] : 0u;
-      a[q] = i < n8 ? absmax[i >> 3] : 0.f;
-    }
-#pragma unroll
-    for (int q = 0; q < BG_ITEMS; ++q) {
-      const size_t i = base + 256 * q;
-      if (i >= n8) break;
-      bf16x8 o;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const float2 t = tab[(c[q] >> (8 * b)) & 0xff];
-        o[2 * b] = (bf16)(t.x * a[q]);
-        o[2 * b + 1] = (bf16)(t.y * a[q]);
-      }
-      *reinterpret_cast<bf16x8*>(w + i * 8) = o;
-    }
-  }
-}
 
 // bnb-layout codes → bf16 (reference / merge path)
 __global__ __launch_bounds__(256) void nf4_dequant_k(const uint8_t* __restrict__ codes, const float* __restrict__ absmax,
@@ -311,22 +259,6 @@ void launch_nf4_dequant2(const uint8_t* codes, const float* absmax, void* w, siz
   LIPA_CHECK_LAUNCH();
 }
 
-void launch_nf4_dequant_bg(int njobs, const uint8_t* const* codes, const float* const* absmax, void* const* w,
-                           const size_t* nelem, int grid, hipStream_t st) {
-  DqJobs jb{};
-  jb.njobs = njobs;
-  jb.chunk0[0] = 0;
-  for (int j = 0; j < njobs; ++j) {
-    jb.codes[j] = (const uint32_t*)codes[j];
-    jb.absmax[j] = absmax[j];
-    jb.w[j] = (bf16*)w[j];
-    jb.n8[j] = nelem[j] / 8;
-    jb.chunk0[j + 1] = jb.chunk0[j] + (jb.n8[j] + BG_CHUNK - 1) / BG_CHUNK;
-  }
-  if (njobs == 0 || jb.chunk0[njobs] == 0) return;
-  nf4_dequant_bg_k<<<grid, 256, 0, st>>>(jb);
-  LIPA_CHECK_LAUNCH();
-}
 
 void launch_nf4_dequant(const uint8_t* codes, const float* absmax, const uint8_t* qabs, const float* absmax2,
                         const float* offset, const float* dcode, void* w, size_t nelem, hipStream_t st) {

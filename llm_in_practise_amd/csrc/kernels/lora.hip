@@ -916,75 +916,6 @@ __global__ __launch_bounds__(256) void lora_apply_k(bf16* __restrict__ Y, int ld
   }
 }
 
-// ---- up to 4 adapters sharing one input x (q/k/v of a fused projection, or a single o_proj adapter)
-struct LoraMulti {
-  const float* G[4];    // s_i·dy_i·B_i, fp32 [M, r_i] (row stride ldg[i])
-  int ldg[4];
-  const bf16* A[4];     // [r_i, K] bf16
-  float* out[4];        // dA_i [r_i, K] fp32 (accumulated)
-  int r[4];
-  uint64_t key[4];
-  uint32_t thr[4];      // 0: no dropout on that branch
-  float ds[4];          // 1/(1-p_i)
-  int nb;
-};
-
-// dA_i += Σ_m G_i[m, :]ᵀ·D_i(x)[m, :] for every branch in one launch (blockIdx.z = branch)
-__global__ __launch_bounds__(256) void lora_dA_multi_k(LoraMulti a, const bf16* __restrict__ X, int ldx, int K, int M,
-                                                       size_t mask_ld) {
-  const int b = blockIdx.z;
-  if (a.r[b] <= 8)
-    lora_acc_mfma_body<8, false, 1>(a.G[b], a.ldg[b], a.r[b], X, ldx, nullptr, 0, nullptr, K, a.out[b], K, 1, M,
-                                    a.key[b], a.thr[b], a.ds[b], mask_ld, blockIdx.x, blockIdx.y);
-  else
-    lora_acc_mfma_body<16, false, 1>(a.G[b], a.ldg[b], a.r[b], X, ldx, nullptr, 0, nullptr, K, a.out[b], K, 1, M,
-                                     a.key[b], a.thr[b], a.ds[b], mask_ld, blockIdx.x, blockIdx.y);
-}
-
-// dx_lora[m, k] = Σ_i D_i[m, k]·ds_i·Σ_j G_i[m, j]·A_i[j, k] (bf16 [M, K]) for all branches, masks regenerated
-// from the counter RNG; the dX GEMM adds it as its C matrix.  A thread owns 8 k of 4 rows and walks the
-// branches, holding one branch's A columns at a time.
-__global__ __launch_bounds__(256) void lora_dx_multi_k(LoraMulti a, bf16* __restrict__ out, int M, int K,
-                                                       size_t mask_ld) {
-  constexpr int RPT = 4;
-  const int kv = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int k8 = kv * 8;
-  if (k8 >= K) return;
-  const int m0 = (blockIdx.y * 4 + (threadIdx.x >> 6)) * RPT;
-  float o[RPT][8];
-#pragma unroll
-  for (int e = 0; e < RPT; ++e)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) o[e][i] = 0.f;
-  for (int b = 0; b < a.nb; ++b) {
-    const int r = a.r[b];
-    bf16x8 av[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) av[j] = j < r ? *reinterpret_cast<const bf16x8*>(a.A[b] + (size_t)j * K + k8) : bf16x8{};
-    const float ds = a.thr[b] ? a.ds[b] : 1.f;
-#pragma unroll
-    for (int e = 0; e < RPT; ++e) {
-      const int m = min(m0 + e, M - 1);
-      const float* gr = a.G[b] + (size_t)m * a.ldg[b];
-      float g[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) g[j] = j < r ? gr[j] * ds : 0.f;
-      const uint32_t keep = a.thr[b] ? dropout_keep8(a.key[b], ((size_t)m * mask_ld + k8) >> 3, a.thr[b]) : 0xFFu;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        float t = 0.f;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) t += g[j] * (float)av[j][i];
-        o[e][i] += ((keep >> i) & 1) ? t : 0.f;
-      }
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < RPT; ++e) {
-    const int m = m0 + e;
-    if (m < M) store8(out + (size_t)m * K + k8, o[e]);
-  }
-}
 
 }  // namespace
 
@@ -1227,38 +1158,3 @@ void launch_lora_dx2(const float* G0, const float* G1, int ldg, const void* A0, 
   LIPA_CHECK_LAUNCH();
 }
 
-static LoraMulti make_multi(int nb, const float* const* G, const int* ldg, const void* const* A, float* const* out,
-                            const int* r, const uint64_t* key, const float* p) {
-  LoraMulti a{};
-  a.nb = nb;
-  for (int i = 0; i < nb; ++i) {
-    a.G[i] = G[i];
-    a.ldg[i] = ldg[i];
-    a.A[i] = static_cast<const bf16*>(A[i]);
-    a.out[i] = out ? out[i] : nullptr;
-    a.r[i] = r[i];
-    a.key[i] = key[i];
-    a.thr[i] = p[i] > 0.f ? (uint32_t)(p[i] * 65536.0f + 0.5f) : 0u;
-    a.ds[i] = p[i] > 0.f ? 1.f / (1.f - p[i]) : 1.f;
-  }
-  return a;
-}
-
-void launch_lora_dA_multi(int nb, const float* const* G, const int* ldg, float* const* out, const int* r,
-                          const uint64_t* key, const float* p, const void* X, int ldx, int K, int M, size_t mask_ld,
-                          hipStream_t st) {
-  const void* A[4] = {nullptr, nullptr, nullptr, nullptr};
-  LoraMulti a = make_multi(nb, G, ldg, A, out, r, key, p);
-  dim3 g(K / 128, (M + 127) / 128, nb);
-  lora_dA_multi_k<<<g, 256, 0, st>>>(a, (const bf16*)X, ldx, K, M, mask_ld);
-  LIPA_CHECK_LAUNCH();
-}
-
-void launch_lora_dx_multi(int nb, const float* const* G, const int* ldg, const void* const* A, const int* r,
-                          const uint64_t* key, const float* p, void* out, int M, int K, size_t mask_ld,
-                          hipStream_t st) {
-  LoraMulti a = make_multi(nb, G, ldg, A, nullptr, r, key, p);
-  dim3 g((K / 8 + 63) / 64, (M + 15) / 16);
-  lora_dx_multi_k<<<g, 256, 0, st>>>(a, (bf16*)out, M, K, mask_ld);
-  LIPA_CHECK_LAUNCH();
-}

@@ -161,7 +161,7 @@ class Qwen3Attention(nn.Module):
         self._qkv = FusedProjection(mods) if can_fuse(mods) else None
 
     def forward(self, x, cos, sin, B, S, residual=None, cache: KVCache | None = None, start: int = 0,
-                kv_lens=None, before_attn=None):
+                kv_lens=None):
         tr = self.training
         qkv = project([self.q_proj, self.k_proj, self.v_proj], x, None, tr, self._qkv)
         if self.q_norm is not None:
@@ -174,8 +174,6 @@ class Qwen3Attention(nn.Module):
             k = apply_rope(qkv[:, nq:nq + nk].reshape(T, self.hkv, self.d), cos, sin).reshape(T, nk)
             v = qkv[:, nq + nk:]
         if cache is None:
-            if before_attn is not None:
-                before_attn()
             o = flash_attention(q, k, v, B, S, self.hq, self.hkv, self.d, causal=True, kv_lens=kv_lens)
         elif isinstance(cache, PackedPrefill):
             o = cache.attend(self.layer_idx, q, k, v, self.hq, self.hkv, self.d, flash_attention)
@@ -222,16 +220,6 @@ class Qwen3MLP(nn.Module):
         return tp_all_reduce(y, self.tp_group)
 
 
-def _overlap_on() -> bool:
-    from ..ops.linear import _OVERLAP
-    return bool(_OVERLAP)
-
-
-def _nf4_bg_on() -> bool:
-    from ..ops.linear import _NF4_BG
-    return _NF4_BG > 0
-
-
 class Qwen3DecoderLayer(nn.Module):
     def __init__(self, cfg: Qwen3Config, layer_idx: int):
         super().__init__()
@@ -240,39 +228,9 @@ class Qwen3DecoderLayer(nn.Module):
         self.input_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
         self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
 
-    def _prefetch(self):
-        """NF4 training step: expand this layer's o / gate|up / down weights on a side stream while
-        the attention forward (latency-bound, light on HBM) runs (ops/linear.py prefetch_dequant)."""
-        from ..ops.linear import _OVERLAP, prefetch_dequant
-        pick = {"o": [self.self_attn.o_proj], "gu": [self.mlp.gate_proj, self.mlp.up_proj],
-                "down": [self.mlp.down_proj]}
-        bases = []
-        for key in _OVERLAP:
-            mods = pick.get(key, [])
-            if key == "gu" and self.mlp._gu is not None:
-                bases.append(self.mlp._gu.base)
-            else:
-                bases += [base_of(m)[0] for m in mods]
-        prefetch_dequant(bases)
-
-    def prefetch_nf4_bg(self):
-        """Queue this layer's NF4 expansions (fused q|k|v, o, fused gate|up, down) on the background
-        grid (ops/linear.py prefetch_dequant_bg)."""
-        from ..ops.linear import prefetch_dequant_bg
-        a, m = self.self_attn, self.mlp
-        bases = [a._qkv.base] if a._qkv is not None else [base_of(p)[0] for p in (a.q_proj, a.k_proj, a.v_proj)]
-        bases += [base_of(a.o_proj)[0]]
-        bases += [m._gu.base] if m._gu is not None else [base_of(p)[0] for p in (m.gate_proj, m.up_proj)]
-        bases += [base_of(m.down_proj)[0]]
-        for i in range(0, len(bases), 4):
-            prefetch_dequant_bg(bases[i:i + 4])
-
     def forward(self, x, cos, sin, B, S, cache=None, start=0, kv_lens=None):
         xn, skip = rms_norm_residual(x, self.input_layernorm.weight, self.input_layernorm.eps)
-        pre = self._prefetch if (_overlap_on() and self.training and cache is None and torch.is_grad_enabled()) \
-            else None
-        h = self.self_attn(xn, cos, sin, B, S, residual=skip, cache=cache, start=start, kv_lens=kv_lens,
-                           before_attn=pre)
+        h = self.self_attn(xn, cos, sin, B, S, residual=skip, cache=cache, start=start, kv_lens=kv_lens)
         hn, skip = rms_norm_residual(h, self.post_attention_layernorm.weight, self.post_attention_layernorm.eps)
         return self.mlp(hn, residual=skip)
 
@@ -305,11 +263,7 @@ class Qwen3Model(nn.Module):
         x = self.embed_tokens(input_ids).reshape(B * S, -1)
         if self.pp is not None:
             x = self.pp.enter(x)        # stages > 0: the previous stage's hidden states
-        bg = _nf4_bg_on() and self.training and cache is None and torch.is_grad_enabled() \
-            and not self.gradient_checkpointing and x.is_cuda and not torch.cuda.is_current_stream_capturing()
-        for i, layer in enumerate(self.layers):
-            if bg and i + 1 < len(self.layers):
-                self.layers[i + 1].prefetch_nf4_bg()   # expanded beside this layer's kernels
+        for layer in self.layers:
             if self.gradient_checkpointing and self.training and cache is None:
                 x = lora_checkpoint(layer, x, cos, sin, B, S, None, 0, kv_lens)
             else:

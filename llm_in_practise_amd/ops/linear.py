@@ -54,94 +54,11 @@ _PAIR_BWD = __import__("os").environ.get("LIPA_LORA_PAIR_BWD", "1") != "0"
 # q+v dropout pair backward: the LoRA dx term as the dX GEMM's C matrix + a separate dA launch
 # (LIPA_LORA_DX_C=0: the fused read-modify-write lora_acc2 pass over dx)
 _DX_C = __import__("os").environ.get("LIPA_LORA_DX_C", "1") != "0"
-# the same for any 1-4 adapters with the masks regenerated (lora_dx_multi + lora_dA_multi): opt-in —
-# re-hashing every mask twice made BASELINE #2 (q,k,v,o r16) 116.7 -> 120.9 ms/step vs the per-adapter
-# fused read-modify-write kernels (LIPA_LORA_DX_MULTI=1 to enable)
-_DX_MULTI = __import__("os").environ.get("LIPA_LORA_DX_MULTI", "0") == "1"
 
 
 def _nf4_dequant_bf16(q: NF4Weight) -> torch.Tensor:
-    pre = _PREFETCHED.pop(id(q), None)
-    if pre is not None:                       # expanded on the side stream (prefetch_dequant)
-        t, ev = pre
-        cur = torch.cuda.current_stream(t.device)
-        cur.wait_event(ev)
-        t.record_stream(cur)
-        return t
     n, k = q.shape
     return native().nf4_dequant_fast(q.codes, q.gemv_scales(), n, k)
-
-
-# NF4 weights expanded ahead of use on a side stream: {id(NF4Weight): (bf16 tensor, ready event)}
-_PREFETCHED: dict = {}
-_SIDE: dict = {}
-# LIPA_LORA_SIDE=1: the q+v LoRA projection (lora_proj2: VALU-bound dropout hashing + a skinny MFMA
-# reduction) runs on a side stream beside the NF4 expansion and the base GEMM of the same projection;
-# the main stream joins it before lora_apply
-_LORA_SIDE = __import__("os").environ.get("LIPA_LORA_SIDE", "0") == "1"
-_LSIDE: dict = {}
-
-
-def _lora_side_stream(dev):
-    s = _LSIDE.get(dev)
-    if s is None:
-        s = _LSIDE[dev] = torch.cuda.Stream(device=dev)
-    return s
-# which of a decoder layer's projections prefetch_dequant expands while attention runs
-# (LIPA_NF4_OVERLAP: comma list of o,gu,down; empty = off)
-_OVERLAP = tuple(t for t in __import__("os").environ.get("LIPA_NF4_OVERLAP", "").split(",") if t)
-
-
-def prefetch_dequant(bases, after: torch.Tensor | None = None):
-    """Expand ``bases`` (NF4Weights) to bf16 on a side stream that starts once the current stream
-    reaches this point: the memory-bound expansion then runs beside a latency-bound kernel (the
-    attention forward) instead of serially before its GEMM.  The GEMM's forward picks the copy up
-    (and waits for its event) in :func:`_nf4_dequant_bf16`."""
-    bases = [b for b in bases if isinstance(b, NF4Weight) and b.kernel_ok()]
-    if not bases or _NF4_MODE != "dequant" or not bases[0].codes.is_cuda:
-        return
-    dev = bases[0].codes.device
-    side = _SIDE.get(dev)
-    if side is None:
-        side = _SIDE[dev] = torch.cuda.Stream(device=dev)
-    cur = torch.cuda.current_stream(dev)
-    start = torch.cuda.Event()
-    start.record(cur)
-    side.wait_event(start)
-    with torch.cuda.stream(side):
-        for b in bases:
-            n, k = b.shape
-            t = native().nf4_dequant_fast(b.codes, b.gemv_scales(), n, k)
-            ev = torch.cuda.Event()
-            ev.record(side)
-            _PREFETCHED[id(b)] = (t, ev)
-
-
-# LIPA_NF4_BG=G (> 0): the NEXT decoder layer's NF4 weights are expanded by ONE small persistent grid
-# of G workgroups (nf4_dequant_bg_k) on a side stream while this layer runs; the GEMMs (compute-bound,
-# one workgroup per CU, little HBM traffic) leave room for it, where the full-size expansion grid
-# (one workgroup per 8 K elements) would take their CU slots.  0 = off (each GEMM expands its own).
-_NF4_BG = int(__import__("os").environ.get("LIPA_NF4_BG", "0"))
-
-
-def prefetch_dequant_bg(bases, grid: int = 0):
-    """Queue the background expansion of ``bases`` (one layer's NF4Weights, <= 4) behind the
-    current stream's work so far; :func:`_nf4_dequant_bf16` picks each copy up."""
-    bases = [b for b in bases if isinstance(b, NF4Weight) and b.kernel_ok() and id(b) not in _PREFETCHED]
-    if not bases or _NF4_MODE != "dequant" or not bases[0].codes.is_cuda:
-        return
-    dev = bases[0].codes.device
-    side = _SIDE.get(dev)
-    if side is None:
-        side = _SIDE[dev] = torch.cuda.Stream(device=dev)
-    side.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(side):
-        outs = native().nf4_dequant_bg([b.codes for b in bases], [b.gemv_scales() for b in bases],
-                                       [b.shape[0] for b in bases], [b.shape[1] for b in bases], grid or _NF4_BG)
-        ev = torch.cuda.Event()
-        ev.record(side)
-    for b, t in zip(bases, outs):
-        _PREFETCHED[id(b)] = (t, ev)
 
 
 @dataclasses.dataclass
@@ -387,7 +304,6 @@ class _FusedLinearFn(torch.autograd.Function):
         dense = not isinstance(base, NF4Weight)
         xa_list, keys = [], []
         ext_a = ext_b = None
-        side_join = None
         ctx.masks = None
         fast = bool(branches) and _fast_lora_ok(x, branches)
         need_xa = any(ctx.needs_input_grad[5:])     # (grad mode is off inside forward: ask autograd)
@@ -404,21 +320,8 @@ class _FusedLinearFn(torch.autograd.Function):
                 # training with dropout on both: keep the masks' bits (2 bits / element of x) for lora_acc2
                 masks = (torch.empty(2, x.shape[0], x.shape[1] // 8, dtype=torch.uint8, device=x.device)
                          if need_xa and all(k is not None for k in keys) and _KEEP_BITS else None)
-                if _LORA_SIDE and not torch.cuda.is_current_stream_capturing():
-                    main = torch.cuda.current_stream(x.device)
-                    side = _lora_side_stream(x.device)
-                    side.wait_stream(main)
-                    with torch.cuda.stream(side):
-                        xa2 = native().lora_proj2(x, a0, a1, None, True, ps[0], keys[0] or 0, branches[0].scaling,
-                                                  ps[1], keys[1] or 0, branches[1].scaling, masks)
-                    xa2.record_stream(main)
-                    if masks is not None:
-                        masks.record_stream(side)
-                    x.record_stream(side)
-                    side_join = side
-                else:
-                    xa2 = native().lora_proj2(x, a0, a1, None, True, ps[0], keys[0] or 0, branches[0].scaling,
-                                              ps[1], keys[1] or 0, branches[1].scaling, masks)
+                xa2 = native().lora_proj2(x, a0, a1, None, True, ps[0], keys[0] or 0, branches[0].scaling,
+                                          ps[1], keys[1] or 0, branches[1].scaling, masks)
                 ctx.masks = masks
                 r0 = a0.shape[0]
                 xa_list = [xa2[:, :r0], xa2[:, r0:]]
@@ -483,8 +386,6 @@ class _FusedLinearFn(torch.autograd.Function):
             bs = [bf16_view(b, x.dtype) for b in ab[1::2]]
             # training: the same pass writes Bᵀ [r, n] for the backward's dy·B projection (no transpose kernel)
             bts = [torch.empty(b.shape[1], b.shape[0], dtype=x.dtype, device=x.device) for b in bs] if need_xa else []
-            if side_join is not None:
-                torch.cuda.current_stream(x.device).wait_stream(side_join)
             native().lora_apply(y, xa_list, bs, [br.c0 for br in branches], bts)
             ctx.bts = bts or None
             if not need_xa:
@@ -603,27 +504,6 @@ class _FusedLinearFn(torch.autograd.Function):
                     else:
                         _notify_grad_ready(ctx.ab_refs[2 * i])
                 pair_ok = False
-                done_dA = True
-            elif (fast and _DX_MULTI and not pair_ok and isinstance(wb, torch.Tensor) and _LT and not _NATIVE_DENSE
-                    and dy.shape[0] >= _LT_MIN_M and _dx_split(dy, wb) == 1 and not deterministic()
-                    and nb <= 4 and all(ab[2 * i].shape[0] <= 16 for i in range(nb)) and x.shape[1] % 128 == 0
-                    and all(ctx.needs_input_grad[5 + 2 * i] for i in range(nb))):
-                # any adapters on this input (q/k/v of a fused projection, an o_proj adapter): their dx
-                # terms summed into ONE bf16 matrix (masks regenerated) that the dX GEMM adds as C, and
-                # every dA in one launch — no per-adapter read-modify-write pass over dx
-                ps = [br.dropout if k is not None else 0.0 for br, k in zip(branches, ctx.keys)]
-                ks = [k or 0 for k in ctx.keys]
-                c = native().lora_dx_multi(list(g_list), [bf16_view(ab[2 * i], dy.dtype) for i in range(nb)], ps, ks,
-                                           x.stride(0))
-                dx = native().lt_dx(dy.contiguous(), wb.contiguous(), 1, True, c)
-                del c
-                dsts = [dest(2 * i) for i in range(nb)]
-                native().lora_dA_multi(list(g_list), x, [o for o, _ in dsts], ps, ks)
-                for i, (o, ret) in enumerate(dsts):
-                    if ret:
-                        grads_ab[2 * i] = o.to(ab[2 * i].dtype)
-                    else:
-                        _notify_grad_ready(ctx.ab_refs[2 * i])
                 done_dA = True
             else:
                 ext_a, ext_b = fold_ext()

@@ -15,11 +15,6 @@ import torch.nn.functional as F
 
 from . import reference as ref
 from ._native import native, use_native
-from .linear import _dense_dx
-
-# LM head logits / dX through the direct hipBLASLt calls (LIPA_LT_HEAD=1; A/B on MI355X: no change,
-# 68.4 vs 68.4 ms/step, so torch.mm / torch.matmul stay the default)
-_LT_HEAD = __import__("os").environ.get("LIPA_LT_HEAD", "0") == "1"
 
 
 def cross_entropy(logits, labels, ignore_index: int = -100):
@@ -41,19 +36,13 @@ class _FusedLinearCEFn(torch.autograd.Function):
         dh = torch.empty_like(h)
         dw = torch.zeros(weight.shape, dtype=torch.float32, device=h.device) if need_wgrad else None
         loss = torch.zeros((), dtype=torch.float32, device=h.device)
-        lt = _LT_HEAD and h.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and weight.is_contiguous()
         for s in range(0, T, chunk):
             hc = h[s:s + chunk]
-            # [c, V] bf16 logits and dlogits·W through the direct hipBLASLt path (ops/linear.py: in-step
-            # kernel choice; the dX as 4 K-slices + slice sum: 128 output tiles would leave half the CUs idle)
-            logits = native().lt_linear(hc, weight, None, False) if lt else hc @ weight.t()
+            logits = hc @ weight.t()
             g0, g1 = s // rows_g, (s + hc.shape[0]) // rows_g
             row_loss = native().ce_fwd_bwd(logits, labels[s:s + chunk], ignore_index, inv[g0:g1])
             loss += (row_loss.view(g1 - g0, -1).sum(1) * inv[g0:g1]).sum()
-            if lt and hc.shape[0] == T:
-                dh = _dense_dx(logits, weight, tune=False)         # dlogits @ W (one call per step: no timing)
-            else:
-                torch.matmul(logits, weight, out=dh[s:s + chunk])
+            torch.matmul(logits, weight, out=dh[s:s + chunk])
             if need_wgrad:
                 dw.add_(logits.t().float() @ hc.float())
         ctx.save_for_backward(dh, dw)

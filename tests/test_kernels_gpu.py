@@ -727,31 +727,6 @@ def test_lora_backward_pair_kernels(native_ext, M):
         assert rel_err(o - 0.25, dy[:, c0:c0 + n].float().t() @ xa) < 1e-2
 
 
-@pytest.mark.parametrize("M,K,rs,ps", [(512, 1024, [16, 16, 16], [0.1, 0.0, 0.05]), (300, 512, [16], [0.2]),
-                                      (256, 4096, [8, 8], [0.1, 0.1])])
-def test_lora_multi_branch_backward(native_ext, M, K, rs, ps):
-    """lora_dx_multi (Σ_i D_i(G_i·A_i)/(1-p_i) as one bf16 matrix) and lora_dA_multi (every dA_i in one
-    launch) vs fp32 with each branch's regenerated dropout mask."""
-    torch.manual_seed(6)
-    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
-    keys = [101 + 7 * i for i in range(len(rs))]
-    gs = [torch.randn(M, r, device=DEV) for r in rs]
-    As = [(0.05 * torch.randn(r, K, device=DEV)).to(torch.bfloat16) for r in rs]
-    want_c = torch.zeros(M, K, device=DEV)
-    xds = []
-    for g, a, p, k in zip(gs, As, ps, keys):
-        xd = native_ext.dropout_fwd(x, p, k) if p > 0 else x
-        m = (((xd != 0) | (x == 0)).float() / (1 - p)) if p > 0 else torch.ones(M, K, device=DEV)
-        want_c += m * (g @ a.float())
-        xds.append(xd)
-    c = native_ext.lora_dx_multi(gs, As, ps, keys, K)
-    assert rel_err(c, want_c) < 1e-2
-    outs = [torch.full((r, K), 0.5, device=DEV) for r in rs]
-    native_ext.lora_dA_multi(gs, x, outs, ps, keys)
-    for o, g, xd in zip(outs, gs, xds):
-        assert rel_err(o - 0.5, g.t() @ xd.float()) < 1e-2
-
-
 # ----------------------------------------------------------------------------- embedding (K6)
 @pytest.mark.parametrize("V,D,dtype,pad", [(1000, 128, torch.bfloat16, None), (50, 64, torch.float32, 3),
                                            (151, 4096, torch.bfloat16, 0)])

@@ -129,7 +129,7 @@ def test_lora_pair_kernels_match_single_branch_path(native_ext, monkeypatch):
                                              (["q_proj", "k_proj", "v_proj", "o_proj"], 16, False)])
 def test_lora_dx_as_gemm_c_matches_read_modify_write(native_ext, monkeypatch, targets, r, quant):
     """At training sizes (M >= 256) the adapters' dx terms are summed into one matrix that the dX GEMM
-    adds as C (lora_dx2 / lora_dx_multi) and dA runs in one launch; the loss and LoRA gradients match
+    adds as C (lora_dx2, q+v pair) and dA runs in one launch; the loss and LoRA gradients match
     the per-adapter read-modify-write path (LIPA_LORA_DX_C=0), dropout 0.1 included."""
     import llm_in_practise_amd.ops.linear as L
     torch.manual_seed(0)
@@ -137,7 +137,6 @@ def test_lora_dx_as_gemm_c_matches_read_modify_write(native_ext, monkeypatch, ta
     res = {}
     for mode in (False, True):
         monkeypatch.setattr(L, "_DX_C", mode)
-        monkeypatch.setattr(L, "_DX_MULTI", mode)
         m = Qwen3ForCausalLM.from_config(qwen3_config("qwen3-small"), dtype=torch.bfloat16, device="cuda", seed=0)
         if quant:
             quantize_model_nf4(m)
