@@ -108,6 +108,11 @@ def main():
     ap.add_argument("--ga-fusion", type=int, default=1,
                     help="1: execute the grad-accum micro-batches in one pass (per-micro-batch loss "
                          "normalisation, identical gradient); 0: sequential micro-steps")
+    ap.add_argument("--faithful-steps", type=int, default=5,
+                    help="after the headline timing, time this many steps of the reference-faithful config "
+                         "(gradient checkpointing on, sequential GA micro-steps) in the same process and report "
+                         "them as the JSON's 'faithful' sub-record (0: skip; ddp strategy only)")
+    ap.add_argument("--faithful-warmup", type=int, default=2)
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -147,7 +152,8 @@ def main():
     it = [0]
     spent = [None]
 
-    def step():
+    def step(fused=None):
+        fused = args.ga_fusion if fused is None else fused
         if engine is not None:      # ZeRO-3: reduce-scatter / optimizer partition / clip inside step()
             ids = torch.cat([data[(it[0] + g) % n_batches] for g in range(args.grad_accum)])
             it[0] += args.grad_accum
@@ -157,7 +163,7 @@ def main():
             del out                 # tear the autograd graph down while the GPU still runs the backward
             engine.step()
             return loss
-        if args.ga_fusion:
+        if fused:
             # the GA micro-batches are independent given the (frozen-during-the-step) weights:
             # run them as one pass with per-micro-batch loss normalisation (same gradient)
             ids = torch.cat([data[(it[0] + g) % n_batches] for g in range(args.grad_accum)])
@@ -215,6 +221,28 @@ def main():
     mem = torch.cuda.max_memory_allocated(device) / 2 ** 30 if device.type == "cuda" else 0.0
     log(f"[bench] loss={loss.item():.4f} {ms:.1f} ms/step  {tps:,.0f} tok/s  "
         f"~{tps * fl_per_tok / world / 1e12:.0f} TFLOP/s/GPU (matmul)  peak HBM {mem:.1f} GiB")
+
+    faithful = None
+    if args.faithful_steps > 0 and engine is None and not (args.grad_ckpt and not args.ga_fusion):
+        # BASELINE.md's config exactly as the reference runs it (Fine-Tuning/qwen3-8b-qlora-dist.py:137-138,
+        # 162-163): gradient_checkpointing=True and the GA micro-steps one after another (no_sync on all but
+        # the last), same model / optimizer / data, timed the same way as the headline
+        model.gradient_checkpointing_enable()
+        for _ in range(args.faithful_warmup):
+            step(fused=0)
+        sync()
+        tf0 = time.perf_counter()
+        for _ in range(args.faithful_steps):
+            floss = step(fused=0)
+        sync()
+        fel = D.all_reduce_max(time.perf_counter() - tf0)
+        fms = 1000 * fel / args.faithful_steps
+        ftps = args.micro_batch * args.seq_len * args.grad_accum * world * args.faithful_steps / fel
+        log(f"[bench] faithful (grad ckpt + sequential GA): loss={floss.item():.4f} {fms:.1f} ms/step  {ftps:,.0f} tok/s")
+        faithful = {"value": round(ftps, 1), "unit": "tokens/s", "ms_per_step": round(fms, 2),
+                    "steps": args.faithful_steps, "warmup": args.faithful_warmup,
+                    "gradient_checkpointing": True, "ga_execution": "sequential",
+                    "micro_batch": args.micro_batch, "grad_accum": args.grad_accum}
     if D.is_main():
         rec = {
             "metric": f"tokens/sec (whole node) {MODEL_NAMES.get(args.model, args.model)} "
@@ -252,6 +280,8 @@ def main():
                 "tokens_per_s_nonpad": round(tps * nonpad_frac, 1),
             },
         }
+        if faithful is not None:
+            rec["faithful"] = faithful
         print(json.dumps(rec), flush=True)
     D.destroy()
 

@@ -9,6 +9,11 @@
 //  * 256 threads = 4 waves as 2 (M) × 2 (N); each wave owns a 128×128 output block: 8×8
 //    v_mfma_f32_16x16x32_bf16 accumulators = 256 fp32 per lane, held in AGPRs (the unified
 //    512-entry register file at one wave per SIMD), so LDS read traffic is 128 KB per K-tile.
+//    The MFMAs are one-instruction asm statements with the accumulator a tied "+a" operand: with
+//    the builtin, hipcc split the accumulator phis between the two K-halves and shuffled ~48
+//    v_accvgpr_mov/read/write per K-tile through the MFMA results (each a dependent stall).
+//    Hazards the asm hides from hipcc: none in the loop (a fragment register is rewritten ≥ 8
+//    MFMAs after its last reader); the epilogue's AGPR reads sit behind 16 wait states.
 //  * in-wave software pipeline over the two 32-deep halves of a 64-deep K-tile: the fragments of
 //    the next half are read from LDS while the 64 MFMAs of the current half run; ONE barrier per
 //    K-tile, in the middle, after which the next-next K-tile's LDS-DMA is issued, so a tile's DMA
@@ -18,6 +23,8 @@
 //    (slot 8r + (c ^ (r & 6)), measured conflict-free), swizzle applied on the SOURCE address.
 //  * XCD-aware tile order: consecutive m-tiles of one weight panel share an XCD's L2.
 //  * split-K (tile grids smaller than the chip): fp32 slabs + one reduce kernel (+ residual).
+#include <type_traits>
+
 #include "common.h"
 
 using namespace lipa;
@@ -29,8 +36,8 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int NT = 256;
-constexpr int IMG = 32768;          // one 256 × 64 bf16 operand image: 32 subtiles of 8 rows × 128 B
-constexpr int LDS_BYTES = 5 * IMG;  // a ring of five operand images: 160 KB
+constexpr int IMG = 32768;
+constexpr int LDS_BYTES = 5 * IMG;
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint64_t bytes) {
   const uint64_t p = reinterpret_cast<uint64_t>(base);
@@ -43,19 +50,55 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint64_t bytes) {
 
 __device__ __forceinline__ int slot_of(int r8, int c) { return 8 * r8 + (c ^ (r8 & 6)); }
 
-struct Loader {
-  rsrc_t rs;
-  uint32_t voff[8];   // per-lane source byte offsets of this wave's 8 subtiles (row clamp + chunk swizzle)
+struct Frags {
+  bf16x8 a[8];
+  bf16x8 b[8];
 };
 
-struct Frags {
-  bf16x8 a[8];   // m fragments (rows wr*128 + 16i)
-  bf16x8 b[8];   // n fragments (rows wc*128 + 16j)
+// compile-time unrolled k-loop: f(std::integral_constant<int, k>) for k in [K, N)
+template <int K, int N>
+struct Unroll {
+  template <typename F>
+  __device__ __forceinline__ static void run(F&& f) {
+    f(std::integral_constant<int, K>{});
+    Unroll<K + 1, N>::run(f);
+  }
 };
+template <int N>
+struct Unroll<N, N> {
+  template <typename F>
+  __device__ __forceinline__ static void run(F&&) {}
+};
+
+// MFMA order of a 64-MFMA K-half: shells of max(i, j) — shell s is (s, 0..s) then (0..s-1, s), so
+// it needs only fragments a[0..s], b[0..s]
+struct ShellOrder {
+  int i[64], j[64];
+};
+constexpr ShellOrder make_shell_order() {
+  ShellOrder o{};
+  int k = 0;
+  for (int s = 0; s < 8; ++s) {
+    for (int j = 0; j <= s; ++j) { o.i[k] = s; o.j[k] = j; ++k; }
+    for (int i = 0; i < s; ++i) { o.i[k] = i; o.j[k] = s; ++k; }
+  }
+  return o;
+}
+constexpr ShellOrder kShell = make_shell_order();
 
 __device__ __forceinline__ bf16x8 lds_frag(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
-template <bool SPLIT>
+// accumulator pinned to AGPRs, D == C (tied): no allocator copies between the two K-halves
+__device__ __forceinline__ void mfma_acc(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_zero(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
+}
+
+// VAR: diagnostic ablations (scripts/experiments/gemm4w_var.py; wrong results by design):
+//   1 = no LDS-DMA in the K-loop, 2 = no fragment reads in the K-loop, 4 = no mid-tile wait + barrier
+template <bool SPLIT, int VAR = 0>
 __global__ __launch_bounds__(NT, 1) void gemm4w_nt_k(const bf16* __restrict__ A, int lda, const bf16* __restrict__ B,
                                                      int ldb, const bf16* __restrict__ residual, void* __restrict__ out,
                                                      int M, int N, int K, int splits) {
@@ -77,9 +120,9 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_nt_k(const bf16* __restrict__ A,
   const int kt0 = sp * per;
   const int nk = max(0, min(nk_all, kt0 + per) - kt0);
 
-  Loader la, lb;
-  la.rs = make_rsrc(A, (uint64_t)((size_t)(M - 1) * lda + K) * 2);
-  lb.rs = make_rsrc(B, (uint64_t)((size_t)(N - 1) * ldb + K) * 2);
+  const rsrc_t rsa = make_rsrc(A, (uint64_t)((size_t)(M - 1) * lda + K) * 2);
+  const rsrc_t rsb = make_rsrc(B, (uint64_t)((size_t)(N - 1) * ldb + K) * 2);
+  uint32_t va[8], vb[8];
   {
     const int r8 = lane >> 3, c = (lane & 7) ^ (r8 & 6);
 #pragma unroll
@@ -88,13 +131,11 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_nt_k(const bf16* __restrict__ A,
       ra = ra < M ? ra : M - 1;
       int rb = n0 + w * 64 + i * 8 + r8;
       rb = rb < N ? rb : N - 1;
-      la.voff[i] = ((uint32_t)ra * (uint32_t)lda + (uint32_t)(kt0 * BK + c * 8)) * 2u;
-      lb.voff[i] = ((uint32_t)rb * (uint32_t)ldb + (uint32_t)(kt0 * BK + c * 8)) * 2u;
+      va[i] = ((uint32_t)ra * (uint32_t)lda + (uint32_t)(kt0 * BK + c * 8)) * 2u;
+      vb[i] = ((uint32_t)rb * (uint32_t)ldb + (uint32_t)(kt0 * BK + c * 8)) * 2u;
     }
   }
 
-  // fragment read offsets: 16-row fragment = subtiles 2f, 2f+1; lane reads row lane & 15 of it
-  // (subtile (lane >> 3) & 1, row lane & 7) at chunk 4s + (lane >> 4) for K-half s
   int lo[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) lo[s] = ((lane >> 3) & 1) * 1024 + 16 * slot_of(lane & 7, 4 * s + (lane >> 4));
@@ -102,87 +143,172 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_nt_k(const bf16* __restrict__ A,
   const int b_off = wc * 8 * 2048;
 
   f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // Operand images live in a ring of 5 slots of 32 KB: image i (A_t = 2t, B_t = 2t + 1) in slot
-  // i mod 5.  A_{t+2} reuses B_{t-1}'s slot (free since the barrier of iteration t-1) and is
-  // DMA'd during the first half of iteration t; B_{t+2} reuses A_t's slot (free after iteration
-  // t's barrier) and is DMA'd during the second half.  So every MFMA group of either half issues
-  // ONE LDS-DMA per wave (TA and LDS-write load spread evenly), and each image has ≥ one half
-  // (≈1k cycles) to land before the barrier that publishes it.
-  auto img = [&](int i) -> char* { return lds + (i % 5) * IMG; };
   Frags f0, f1;
-  auto read_q = [&](Frags& f, const char* ia, const char* ib, int s, int q) {
-    f.a[q] = lds_frag(ia + a_off + q * 2048 + lo[s]);
-    f.b[q] = lds_frag(ib + b_off + q * 2048 + lo[s]);
+
+  // producer order inside a half: group g (0..7) reads a[2g], a[2g+1] (g < 4) or b[2g-8], b[2g-7];
+  // consumer order: column j of 8 MFMAs needs b[j] and every a[i] — the a's land first
+  auto read_g = [&](Frags& f, const char* ia, const char* ib, int s, int g) {
+    if (g < 4) {
+      f.a[2 * g] = lds_frag(ia + a_off + (2 * g) * 2048 + lo[s]);
+      f.a[2 * g + 1] = lds_frag(ia + a_off + (2 * g + 1) * 2048 + lo[s]);
+    } else {
+      const int j = 2 * (g - 4);
+      f.b[j] = lds_frag(ib + b_off + j * 2048 + lo[s]);
+      f.b[j + 1] = lds_frag(ib + b_off + (j + 1) * 2048 + lo[s]);
+    }
   };
-  auto mma_row = [&](const Frags& f, int i) {
+  auto mma_col = [&](const Frags& f, int j) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.b[j], f.a[i], acc[i][j], 0, 0, 0);
+    for (int i = 0; i < 8; ++i) mfma_acc(acc[i][j], f.b[j], f.a[i]);
   };
-  // one LDS-DMA: subtile 8w + q of K-tile t's A (or B) image
-  auto dma = [&](const Loader& L, char* im, int t, int q) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(L.rs, (lds_ptr_t)(im + w * 8192 + q * 1024), 16, L.voff[q],
+  auto mma_col0 = [&](const Frags& f, int j) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) mfma_zero(acc[i][j], f.b[j], f.a[i]);
+  };
+  auto dma = [&](const rsrc_t& rs, const uint32_t* voff, char* im, int t, int q) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(im + w * 8192 + q * 1024), 16, voff[q],
                                              (uint32_t)t * (BK * 2), 0, 0);
   };
 
-  if (nk > 0) {
+  if (nk <= 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  } else if constexpr (VAR == 8) {
+    // Double-buffered form: two 64 KB stages (A image + B image each).  Per K-tile t, one
+    // 128-MFMA stream: MFMAs 0-63 on the first K-half (fA), 64-127 on the second (fB);
+    //   MFMA  0-15: + one fragment read each of tile t's second half (into fB)
+    //   after 25  : lgkmcnt(0) + barrier 1 — nobody reads stage t&1 any more
+    //   MFMA 26-101, every 5th: one LDS-DMA of tile t+2 into stage t&1 (8 A, then 8 B)
+    //   after 111 : vmcnt(16) (tile t+1 landed; t+2's 16 in flight) + barrier 2
+    //   MFMA 112-127: + one fragment read each of tile t+1's first half (into fA)
+    // The first half's MFMAs walk (i, j) in shells of max(i, j): shell s needs reads 2s, 2s+1 only.
     const int t1 = nk > 1 ? 1 : 0;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) dma(la, img(0), 0, q);
+    for (int q = 0; q < 8; ++q) dma(rsa, va, lds + 0 * IMG, 0, q);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) dma(lb, img(1), 0, q);
+    for (int q = 0; q < 8; ++q) dma(rsb, vb, lds + 1 * IMG, 0, q);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) dma(la, img(2), t1, q);
+    for (int q = 0; q < 8; ++q) dma(rsa, va, lds + 2 * IMG, t1, q);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) dma(lb, img(3), t1, q);
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // tile 0 landed (tile 1's 16 DMAs may fly)
+    for (int q = 0; q < 8; ++q) dma(rsb, vb, lds + 3 * IMG, t1, q);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    auto read_r = [&](Frags& f, const char* ia, const char* ib, int s, int r) {
+      if ((r & 1) == 0) f.a[r >> 1] = lds_frag(ia + a_off + (r >> 1) * 2048 + lo[s]);
+      else f.b[r >> 1] = lds_frag(ib + b_off + (r >> 1) * 2048 + lo[s]);
+    };
+#pragma unroll
+    for (int r = 0; r < 16; ++r) read_r(f0, lds, lds + IMG, 0, r);
+    int cur = 0;
+    auto body = [&](auto first, int t) {
+      const int t2 = t + 2 < nk ? t + 2 : nk - 1;
+      char* const ca = lds + cur;
+      char* const cb = ca + IMG;
+      char* const na = lds + (cur ^ (2 * IMG));
+      char* const nb = na + IMG;
+      Unroll<0, 128>::run([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        constexpr int i = kShell.i[k & 63], j = kShell.j[k & 63];
+        if constexpr (k < 64) {
+          if constexpr (decltype(first)::value) mfma_zero(acc[i][j], f0.b[j], f0.a[i]);
+          else mfma_acc(acc[i][j], f0.b[j], f0.a[i]);
+        } else {
+          mfma_acc(acc[i][j], f1.b[j], f1.a[i]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (k < 16) read_r(f1, ca, cb, 1, k);
+        if constexpr (k == 25) {
+          __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+          __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (k >= 26 && k <= 101 && (k - 26) % 5 == 0) {
+          constexpr int d = (k - 26) / 5;
+          if constexpr (d < 8) dma(rsa, va, ca, t2, d);
+          else dma(rsb, vb, cb, t2, d - 8);
+        }
+        if constexpr (k == 111) {
+          __builtin_amdgcn_s_waitcnt(0x4F70);   // vmcnt(16)
+          __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (k >= 112) read_r(f0, na, nb, 0, k - 112);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      cur ^= 2 * IMG;
+    };
+    body(std::integral_constant<bool, true>{}, 0);
+    for (int t = 1; t < nk; ++t) body(std::integral_constant<bool, false>{}, t);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  } else {
+    const int t1 = nk > 1 ? 1 : 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma(rsa, va, lds + 0 * IMG, 0, q);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma(rsb, vb, lds + 1 * IMG, 0, q);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma(rsa, va, lds + 2 * IMG, t1, q);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma(rsb, vb, lds + 3 * IMG, t1, q);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     __builtin_amdgcn_s_barrier();
 #pragma unroll
-    for (int q = 0; q < 8; ++q) read_q(f0, img(0), img(1), 0, q);
-  }
-  // Per K-tile t (F0 = its first K-half in registers):
-  //   [64 MFMAs on F0 ∥ read F1 (second half) ∥ DMA A_{t+2}] → vmcnt(8) lgkmcnt(0) barrier →
-  //   [64 MFMAs on F1 ∥ read F0 of tile t+1 ∥ DMA B_{t+2}]
-  // Branch-free: past the last K-tile the DMAs re-stage tile nk-1 into slots nobody reads again and
-  // the last F0 reads are discarded.  Waits are compiler-visible s_waitcnt builtins
-  // (0xC07F = lgkmcnt(0), 0x0F78 = vmcnt(8)) so the waitcnt pass adds none of its own.
-  for (int t = 0; t < nk; ++t) {
-    const int t2 = t + 2 < nk ? t + 2 : nk - 1;
-    char* const ia = img(2 * t);
-    char* const ib = img(2 * t + 1);
-    char* const na = img(2 * t + 2);
-    char* const nb = img(2 * t + 3);
-    char* const da = img(2 * t + 4);
-    char* const db = img(2 * t + 5);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      mma_row(f0, q);
-      __builtin_amdgcn_sched_barrier(0);
-      read_q(f1, ia, ib, 1, q);
-      dma(la, da, t2, q);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    __builtin_amdgcn_s_waitcnt(0x0F78);   // all but this half's 8 DMAs landed: tile t+1 is complete
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // this wave's reads of tile t are done
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      read_q(f0, na, nb, 0, q);
-      dma(lb, db, t2, q);
-      __builtin_amdgcn_sched_barrier(0);
-      mma_row(f1, q);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int g = 0; g < 8; ++g) read_g(f0, lds, lds + IMG, 0, g);
+    if constexpr ((VAR & 2) != 0) f1 = f0;
 
-  // ---- epilogue: lane holds C[m = col][n = 4·(lane>>4) + r … +3] of each 16×16 block
+    // ring slots of the images A_t = 2t, B_t = 2t + 1 (mod 5), advanced incrementally
+    int s_ia = 0;   // slot of A_t
+    for (int t = 0; t < nk; ++t) {
+      const int t2 = t + 2 < nk ? t + 2 : nk - 1;
+      const int s_ib = s_ia + 1 >= 5 ? s_ia - 4 : s_ia + 1;
+      const int s_na = s_ib + 1 >= 5 ? s_ib - 4 : s_ib + 1;
+      const int s_nb = s_na + 1 >= 5 ? s_na - 4 : s_na + 1;
+      const int s_da = s_nb + 1 >= 5 ? s_nb - 4 : s_nb + 1;   // == slot of B_{t-1}
+      const int s_db = s_ia;                                   // A_t's slot, free after the mid barrier
+      char* const ia = lds + s_ia * IMG;
+      char* const ib = lds + s_ib * IMG;
+      char* const na = lds + s_na * IMG;
+      char* const nb = lds + s_nb * IMG;
+      char* const da = lds + s_da * IMG;
+      char* const db = lds + s_db * IMG;
+      if (t == 0) {
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+          mma_col0(f0, g);
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr ((VAR & 2) == 0) read_g(f1, ia, ib, 1, g);
+          if constexpr ((VAR & 1) == 0) dma(rsa, va, da, t2, g);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+          mma_col(f0, g);
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr ((VAR & 2) == 0) read_g(f1, ia, ib, 1, g);
+          if constexpr ((VAR & 1) == 0) dma(rsa, va, da, t2, g);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if constexpr ((VAR & 4) == 0) {
+        __builtin_amdgcn_s_waitcnt(0x0F78);   // vmcnt(8): tile t+1 complete
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        if constexpr ((VAR & 2) == 0) read_g(f0, na, nb, 0, g);
+        if constexpr ((VAR & 1) == 0) dma(rsb, vb, db, t2, g);
+        __builtin_amdgcn_sched_barrier(0);
+        mma_col(f1, g);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      s_ia = s_na;
+    }
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  }
+
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = m0 + wr * 128 + i * 16 + (lane & 15);
@@ -253,9 +379,23 @@ int gemm4w_splits(int M, int N, int K) {
 void launch_gemm4w(const void* A, int lda, const void* B, int ldb, const void* residual, void* out, float* ws, int M,
                    int N, int K, int splits, hipStream_t st) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  static const int var = [] {
+    const char* e = getenv("LIPA_GEMM4W_VAR");
+    return e ? atoi(e) : 0;
+  }();
   if (splits <= 1) {
-    gemm4w_nt_k<false><<<tiles, NT, 0, st>>>((const bf16*)A, lda, (const bf16*)B, ldb, (const bf16*)residual, out, M,
-                                             N, K, 1);
+#define G4W_VAR(V)                                                                                                 \
+  case V:                                                                                                          \
+    gemm4w_nt_k<false, V><<<tiles, NT, 0, st>>>((const bf16*)A, lda, (const bf16*)B, ldb, (const bf16*)residual, out, \
+                                                M, N, K, 1);                                                        \
+    break;
+    switch (var) {
+      G4W_VAR(1) G4W_VAR(2) G4W_VAR(3) G4W_VAR(4) G4W_VAR(5) G4W_VAR(7) G4W_VAR(8)
+      default:
+        gemm4w_nt_k<false><<<tiles, NT, 0, st>>>((const bf16*)A, lda, (const bf16*)B, ldb, (const bf16*)residual, out,
+                                                 M, N, K, 1);
+    }
+#undef G4W_VAR
   } else {
     gemm4w_nt_k<true><<<tiles * splits, NT, 0, st>>>((const bf16*)A, lda, (const bf16*)B, ldb, nullptr, ws, M, N, K,
                                                      splits);
