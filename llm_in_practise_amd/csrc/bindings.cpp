@@ -53,9 +53,12 @@ void set_dequant_variant(int);
 void launch_nf4_dequant(const uint8_t*, const float*, const uint8_t*, const float*, const float*, const float*, void*,
                         size_t, hipStream_t);
 bool gemm8_supported(int, int, int, int, int);
-bool gemm4w_supported(int, int, int, int, int);
-int gemm4w_splits(int, int, int);
-void launch_gemm4w(const void*, int, const void*, int, const void*, void*, float*, int, int, int, int, hipStream_t);
+bool gemm4w_supported(int, int, int, int, int, bool);
+int gemm4w_plan(int, int, int, bool, int, int, int*);
+void launch_gemm4w_swiglu(const void*, int, const void*, void*, void*, int, int, int, int, hipStream_t);
+void launch_gemm4w_dswiglu(const void*, int, const void*, const void*, void*, int, int, int, int, hipStream_t);
+void launch_gemm4w(const void*, int, const void*, int, const void*, void*, float*, int, int, int, int, bool, int,
+                   hipStream_t);
 int gemm8_splits(int, int, int);
 void launch_gemm8(const void*, int, const void*, int, const void*, const void*, int, const void*, void*, float*, int, int,
                   int, int, hipStream_t);
@@ -654,14 +657,16 @@ Tensor gemm8(Tensor x, Tensor w, optional<Tensor> ext_a, optional<Tensor> ext_b,
 
 
 // y = x·wᵀ (+ residual) through the one-wave-per-SIMD AGPR-accumulator MFMA GEMM (gemm4w.hip);
-// x [M, K] (row stride any multiple of 8), w [N, K] contiguous rows.  splits <= 0: auto split-K
-Tensor gemm4w(Tensor x, Tensor w, optional<Tensor> residual, int64_t splits) {
+// x [M, K] (row stride any multiple of 8), w [N, K] contiguous rows.  bt: y = x·w with w [K, N]
+// (the dX = dY·W of a frozen [N_w, K_w] weight, no transpose copy).  splits <= 0: auto split-K;
+// bn: tile width 128 / 256 / 192 (NT only), 0 = auto
+Tensor gemm4w(Tensor x, Tensor w, optional<Tensor> residual, int64_t splits, bool bt, int64_t bn) {
   CHECK_BF16(x);
   CHECK_BF16(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1, "gemm4w: 2-D, unit inner stride");
-  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K, "gemm4w: K mismatch");
-  TORCH_CHECK(gemm4w_supported(M, N, K, x.stride(0), w.stride(0)), "gemm4w: unsupported shape / strides");
+  const int64_t M = x.size(0), K = x.size(1), N = bt ? w.size(1) : w.size(0);
+  TORCH_CHECK((bt ? w.size(0) : w.size(1)) == K, "gemm4w: K mismatch");
+  TORCH_CHECK(gemm4w_supported(M, N, K, x.stride(0), w.stride(0), bt), "gemm4w: unsupported shape / strides");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
               "gemm4w: 16-byte aligned operands");
   const void* res = nullptr;
@@ -670,13 +675,55 @@ Tensor gemm4w(Tensor x, Tensor w, optional<Tensor> residual, int64_t splits) {
     TORCH_CHECK(residual->is_contiguous() && residual->size(0) == M && residual->size(1) == N, "gemm4w: residual [M, N]");
     res = residual->data_ptr();
   }
-  const int sp = splits > 0 ? (int)splits : gemm4w_splits(M, N, K);
+  TORCH_CHECK(bn == 0 || bn == 128 || bn == 256 || (bn == 192 && !bt), "gemm4w: bn 0 / 128 / 256 / 192 (not bt)");
+  int bn_used = 0;
+  const int sp = gemm4w_plan(M, N, K, bt, (int)bn, (int)splits, &bn_used);
   auto y = at::empty({M, N}, x.options());
   Tensor ws;
   if (sp > 1) ws = at::empty({sp, M, N}, x.options().dtype(at::kFloat));
   launch_gemm4w(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), res, y.data_ptr(),
-                sp > 1 ? ws.data_ptr<float>() : nullptr, M, N, K, sp, stream());
+                sp > 1 ? ws.data_ptr<float>() : nullptr, M, N, K, sp, bt, bn_used, stream());
   return y;
+}
+
+// Fused MLP GEMMs (gemm4w.hip EPI 1 / 2).  gemm4w_swiglu: x [M, K], w_gu [2F, K] ([gate | up] rows)
+// → (gu [M, 2F], h = silu(gate)·up [M, F]).  gemm4w_dswiglu: dy [M, N_w], w_down [N_w, F], gu [M, 2F]
+// → dgu [M, 2F] = SwiGLU-backward(dy·w_down).
+std::vector<Tensor> gemm4w_swiglu(Tensor x, Tensor w) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && w.dim() == 2 && w.size(1) == x.size(1), "gemm4w_swiglu: shapes");
+  const int64_t M = x.size(0), K = x.size(1), F = w.size(0) / 2;
+  TORCH_CHECK(w.size(0) == 2 * F && F % 16 == 0 && gemm4w_supported(M, 2 * F, K, x.stride(0), K, false) &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              "gemm4w_swiglu: unsupported shape / alignment");
+  int bn = 0;
+  gemm4w_plan(M, 2 * F, K, false, 0, 1, &bn);
+  auto gu = at::empty({M, 2 * F}, x.options());
+  auto h = at::empty({M, F}, x.options());
+  launch_gemm4w_swiglu(x.data_ptr(), x.stride(0), w.data_ptr(), gu.data_ptr(), h.data_ptr(), M, F, K, bn, stream());
+  return {gu, h};
+}
+
+Tensor gemm4w_dswiglu(Tensor dy, Tensor w, Tensor gu) {
+  CHECK_BF16(dy);
+  CHECK_BF16(w);
+  CHECK_BF16(gu);
+  CHECK_CONTIG(w);
+  CHECK_CONTIG(gu);
+  TORCH_CHECK(dy.dim() == 2 && dy.stride(1) == 1 && w.dim() == 2 && w.size(0) == dy.size(1), "gemm4w_dswiglu: shapes");
+  const int64_t M = dy.size(0), Nw = dy.size(1), F = w.size(1);
+  TORCH_CHECK(gu.size(0) == M && gu.size(1) == 2 * F && F % 16 == 0 &&
+                  gemm4w_supported(M, F, Nw, dy.stride(0), F, true) &&
+                  reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              "gemm4w_dswiglu: unsupported shape / alignment");
+  int bn = 0;
+  gemm4w_plan(M, F, Nw, true, 0, 1, &bn);
+  auto dgu = at::empty({M, 2 * F}, dy.options());
+  launch_gemm4w_dswiglu(dy.data_ptr(), dy.stride(0), w.data_ptr(), gu.data_ptr(), dgu.data_ptr(), M, F, Nw, bn,
+                        stream());
+  return dgu;
 }
 
 // y = x·wᵀ (+ LoRA K-slice) (+ residual) for a frozen bf16 base: the hand-written 8-phase MFMA GEMM
@@ -1336,7 +1383,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nf4_absmax_t", &nf4_absmax_t);
   m.def("gemm_nf4", &gemm_nf4);
   m.def("gemm8", &gemm8);
-  m.def("gemm4w", &gemm4w);
+  m.def("gemm4w", &gemm4w, py::arg("x"), py::arg("w"), py::arg("residual") = py::none(), py::arg("splits") = 0,
+        py::arg("bt") = false, py::arg("bn") = 0);
+  m.def("gemm4w_swiglu", &gemm4w_swiglu);
+  m.def("gemm4w_dswiglu", &gemm4w_dswiglu);
   m.def("gemm_nf4_t", &gemm_nf4_t);
   m.def("gemm_bf16", &gemm_bf16);
   m.def("gemm_bf16_t", &gemm_bf16_t);

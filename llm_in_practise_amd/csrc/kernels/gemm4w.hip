@@ -1,28 +1,35 @@
-// One-wave-per-SIMD 256×256 MFMA GEMM for gfx950: C = A·Bᵀ (+ residual)
+// One-wave-per-SIMD MFMA GEMM for gfx950 — the frozen-base GEMMs of the QLoRA step:
 //
-//   A [M, K] bf16, row stride lda (activations, K contiguous)
-//   B [N, K] bf16, row stride ldb (a frozen weight, K contiguous)
+//   forward   y  = x·Wᵀ (+ residual)      A = x [M, K],  B = W  [N, K]   (NT)
+//   backward  dX = dY·W (+ C)             A = dY [M, K], B = W  [K, N]   (BT: W used as stored)
 //
-// Why this shape (profiles/gemm8_pmc_vs_hipblaslt.txt): the 8-wave ping-pong kernel (gemm8.hip)
-// re-reads every fragment from LDS for a 128×64 wave tile (192 KB of ds_read per K-tile per CU —
-// the LDS port is saturated) and parks one wave group per phase.  Here:
-//  * 256 threads = 4 waves as 2 (M) × 2 (N); each wave owns a 128×128 output block: 8×8
-//    v_mfma_f32_16x16x32_bf16 accumulators = 256 fp32 per lane, held in AGPRs (the unified
-//    512-entry register file at one wave per SIMD), so LDS read traffic is 128 KB per K-tile.
-//    The MFMAs are one-instruction asm statements with the accumulator a tied "+a" operand: with
-//    the builtin, hipcc split the accumulator phis between the two K-halves and shuffled ~48
-//    v_accvgpr_mov/read/write per K-tile through the MFMA results (each a dependent stall).
-//    Hazards the asm hides from hipcc: none in the loop (a fragment register is rewritten ≥ 8
-//    MFMAs after its last reader); the epilogue's AGPR reads sit behind 16 wait states.
-//  * in-wave software pipeline over the two 32-deep halves of a 64-deep K-tile: the fragments of
-//    the next half are read from LDS while the 64 MFMAs of the current half run; ONE barrier per
-//    K-tile, in the middle, after which the next-next K-tile's LDS-DMA is issued, so a tile's DMA
-//    has two MFMA halves (≈2k cycles) to land before its `vmcnt(0)`.
-//  * all global→LDS traffic is LDS-DMA (buffer_load … lds, 1 KB per wave-instruction, whole 128-B
-//    lines); LDS image = 1 KB subtiles of 8 rows × 64 k with the chunk permutation of gemm8.hip
-//    (slot 8r + (c ^ (r & 6)), measured conflict-free), swizzle applied on the SOURCE address.
-//  * XCD-aware tile order: consecutive m-tiles of one weight panel share an XCD's L2.
-//  * split-K (tile grids smaller than the chip): fp32 slabs + one reduce kernel (+ residual).
+// Design (profiles/gemm4w_*.txt):
+//  * 256 threads = 4 waves as 2 (M) × 2 (N), one wave per SIMD; a wave owns a 128 × BN/2 output block
+//    of v_mfma_f32_16x16x32_bf16 accumulators (256 or 128 fp32 per lane) held in AGPRs.  The MFMAs
+//    are one-instruction asm statements with the accumulator a tied "+a" operand: with the builtin,
+//    hipcc split the accumulator phis between the two K-halves and shuffled ~48 v_accvgpr_mov/read/
+//    write per K-tile through the MFMA results.  Hazards the asm hides from hipcc: none in the loop
+//    (a fragment register is rewritten ≥ 16 MFMAs after its last reader; a single wave per SIMD, so
+//    no partner's MFMAs sit between); the epilogue's AGPR reads sit behind 16 wait states.
+//  * BN = 256 (grids of ≥ 256 tiles: gate|up forward, the LM head) or BN = 128 (the M = 2048 × 4096
+//    shapes — o / down forward and every dX to d_model: 256 tiles fill the chip without split-K).
+//  * global → LDS only by LDS-DMA (buffer_load … lds, 1 KB per wave-instruction, whole 128-B lines),
+//    STAGES K-tile stages (2 for BN = 256: 128 KB; 3 for BN = 128: 144 KB).  Per K-tile one
+//    compile-time-unrolled stream of 16·BN/32 MFMAs (first K-half on fA, second on fB):
+//      - the first R MFMAs each carry one fragment read of this tile's second half (into fB);
+//      - barrier 1 (lgkmcnt(0)): nobody reads stage t % STAGES any more → its LDS-DMA refill with
+//        tile t + STAGES is spread over the middle MFMAs;
+//      - barrier 2 (vmcnt((STAGES − 1)·D)): tile t + 1 has landed;
+//      - the last R MFMAs each carry one fragment read of tile t + 1's first half (into fA).
+//    The first half walks (i, j) in shells of max(i, j), so MFMA k waits only on reads issued ≥ 14
+//    MFMAs earlier.
+//  * NT images: 1 KB subtiles of 8 rows × 64 k, 16-B chunk c of row r at slot 8r + (c ^ (r & 6))
+//    (conflict-free ds_read_b128).  BT image: 64 k-rows × 2·BN bytes with the 32-B column pairs XOR-
+//    permuted by h(k) = (k & 3) | ((k >> 1) & 4), read as the B operand by two ds_read_b64_tr_b16 per
+//    fragment (a 32-lane half reads rows {0-3, 8-11} (+4) of a 16-row group: 8 distinct h → conflict-
+//    free).  Every swizzle is applied on the DMA SOURCE address (the LDS side is lane-linear).
+//  * XCD-aware tile order: the m-tiles of one weight panel are consecutive ids and share an XCD's L2.
+//  * split-K (grids still smaller than the chip): fp32 slabs + one reduce kernel (+ residual).
 #include <type_traits>
 
 #include "common.h"
@@ -32,12 +39,11 @@ using namespace lipa;
 namespace {
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
-constexpr int BM = 256, BN = 256, BK = 64;
-constexpr int NT = 256;
-constexpr int IMG = 32768;
-constexpr int LDS_BYTES = 5 * IMG;
+constexpr int BM = 64 * 4, BK = 64, NT = 256;
+constexpr int IMG_A = 32768;   // 256 rows × 64 k bf16
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint64_t bytes) {
   const uint64_t p = reinterpret_cast<uint64_t>(base);
@@ -50,12 +56,41 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint64_t bytes) {
 
 __device__ __forceinline__ int slot_of(int r8, int c) { return 8 * r8 + (c ^ (r8 & 6)); }
 
-struct Frags {
-  bf16x8 a[8];
-  bf16x8 b[8];
-};
+__device__ __forceinline__ bf16x8 lds_frag(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
-// compile-time unrolled k-loop: f(std::integral_constant<int, k>) for k in [K, N)
+__device__ __forceinline__ void mfma_acc(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_zero(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
+}
+
+// s_waitcnt immediate for lgkmcnt(0) (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14)
+constexpr int WAIT_LGKM0 = 0 | (7 << 4) | (0 << 8) | (3 << 14);
+
+// vmcnt wait as an asm statement (the DMAs it counts are asm too, invisible to hipcc's counters)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// one wave-instruction of LDS-DMA: 64 lanes × 16 B from rs + voff + soff into LDS [dst, dst + 1 KB);
+// M0 (the LDS base, compiler-reserved) is written and restored inside the statement.  dst and soff
+// are SALU values (never fresh from v_readfirstlane, so no VALU→SGPR→VMEM wait states are needed)
+__device__ __forceinline__ void dma_lds(const rsrc_t& rs, uint32_t dst, uint32_t voff, uint32_t soff) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(dst), "v"(voff), "s"(rs), "s"(soff)
+      : "memory");
+}
+
+// compile-time unrolled loop: f(std::integral_constant<int, k>) for k in [K, N)
 template <int K, int N>
 struct Unroll {
   template <typename F>
@@ -70,39 +105,78 @@ struct Unroll<N, N> {
   __device__ __forceinline__ static void run(F&&) {}
 };
 
-// MFMA order of a 64-MFMA K-half: shells of max(i, j) — shell s is (s, 0..s) then (0..s-1, s), so
-// it needs only fragments a[0..s], b[0..s]
-struct ShellOrder {
-  int i[64], j[64];
+// Per-BN schedule tables: MFMA order of a K-half (shells of max(i, j), then the rows i ≥ NB) and the
+// fragment-read order (a0 b0 a1 b1 …, then the remaining a's)
+template <int NB>
+struct Sched {
+  int i[8 * NB], j[8 * NB];
+  int rd_a[8 + NB], rd_i[8 + NB];   // read item r: a fragment? index
 };
-constexpr ShellOrder make_shell_order() {
-  ShellOrder o{};
+template <int NB>
+constexpr Sched<NB> make_sched() {
+  Sched<NB> o{};
   int k = 0;
-  for (int s = 0; s < 8; ++s) {
+  for (int s = 0; s < NB; ++s) {
     for (int j = 0; j <= s; ++j) { o.i[k] = s; o.j[k] = j; ++k; }
     for (int i = 0; i < s; ++i) { o.i[k] = i; o.j[k] = s; ++k; }
   }
+  for (int i = NB; i < 8; ++i)
+    for (int j = 0; j < NB; ++j) { o.i[k] = i; o.j[k] = j; ++k; }
+  int r = 0;
+  for (int s = 0; s < NB; ++s) {
+    o.rd_a[r] = 1; o.rd_i[r] = s; ++r;
+    o.rd_a[r] = 0; o.rd_i[r] = s; ++r;
+  }
+  for (int i = NB; i < 8; ++i) { o.rd_a[r] = 1; o.rd_i[r] = i; ++r; }
   return o;
 }
-constexpr ShellOrder kShell = make_shell_order();
+constexpr Sched<8> kSched8 = make_sched<8>();
+constexpr Sched<4> kSched4 = make_sched<4>();
+constexpr Sched<6> kSched6 = make_sched<6>();
+template <int NB>
+__host__ __device__ constexpr const Sched<NB>& sched_of();
+template <>
+__host__ __device__ constexpr const Sched<8>& sched_of<8>() { return kSched8; }
+template <>
+__host__ __device__ constexpr const Sched<4>& sched_of<4>() { return kSched4; }
+template <>
+__host__ __device__ constexpr const Sched<6>& sched_of<6>() { return kSched6; }
 
-__device__ __forceinline__ bf16x8 lds_frag(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g)); }
 
-// accumulator pinned to AGPRs, D == C (tied): no allocator copies between the two K-halves
-__device__ __forceinline__ void mfma_acc(f32x4& acc, const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-__device__ __forceinline__ void mfma_zero(f32x4& acc, const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(a), "v"(b));
-}
-
-// VAR: diagnostic ablations (scripts/experiments/gemm4w_var.py; wrong results by design):
-//   1 = no LDS-DMA in the K-loop, 2 = no fragment reads in the K-loop, 4 = no mid-tile wait + barrier
-template <bool SPLIT, int VAR = 0>
-__global__ __launch_bounds__(NT, 1) void gemm4w_nt_k(const bf16* __restrict__ A, int lda, const bf16* __restrict__ B,
-                                                     int ldb, const bf16* __restrict__ residual, void* __restrict__ out,
-                                                     int M, int N, int K, int splits) {
-  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+// EPI (fused MLP epilogues; SURVEY.md K5 "activation in the GEMM epilogue"):
+//   1  SwiGLU forward on the gate|up projection (NT, no split).  B = W_gu [2F, K] as stored ([gate | up]
+//      rows); the tile's B rows are gathered so that fragment pair (2c, 2c+1) of a wave is gate rows
+//      16c'…+15 and the matching up rows — every lane then holds g and u of the same (m, col).  Writes
+//      gu [M, 2F] in the [gate | up] layout (saved for backward) and h = silu(g)·u [M, F] to aux_out.
+//      N = 2F (virtual columns).
+//   2  SwiGLU backward fused into the down projection's dX (BT, no split): the GEMM tile is dh [M, F];
+//      the epilogue reads g, u from aux = gu [M, 2F] and writes dgu = [dh·u·silu'(g) | dh·silu(g)].
+//      N = F.
+// Both round the GEMM result to bf16 first, exactly where the unfused path stores it.
+template <int BN, bool BT, bool SPLIT, int EPI = 0>
+__global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, int lda, const bf16* __restrict__ B,
+                                                  int ldb, const bf16* __restrict__ residual, void* __restrict__ out,
+                                                  int M, int N, int K, int splits, const bf16* __restrict__ aux,
+                                                  bf16* __restrict__ aux_out, int F) {
+  static_assert(EPI == 0 || !SPLIT, "fused epilogues run on whole-K tiles");
+  static_assert(EPI != 1 || !BT, "SwiGLU forward epilogue: NT only");
+  static_assert(EPI != 2 || BT, "SwiGLU backward epilogue: the transposed-B dX only");
+  constexpr int NB = BN / 32;                  // b fragments per wave per K-half
+  constexpr int STAGES = BN == 128 ? 3 : 2;
+  static_assert(BN == 128 || BN == 256 || (BN == 192 && !BT), "tile widths: 128, 256 (NT / BT), 192 (NT)");
+  constexpr int IMG_B = BN * BK * 2;
+  constexpr int STAGE = IMG_A + IMG_B;
+  constexpr int KT = 16 * NB;                  // MFMAs per K-tile per wave
+  constexpr int H = KT / 2;
+  constexpr int R = 8 + NB;                    // fragment-read items per K-half
+  constexpr int DB = BN / 32;                  // B DMAs per wave per K-tile
+  constexpr int D = 8 + DB;                    // all DMAs per wave per K-tile
+  constexpr int K1 = R + 9;                    // barrier 1 after this MFMA
+  constexpr int K2 = KT - R - 1;               // barrier 2 after this MFMA
+  constexpr int DSP = (K2 - 10 - (K1 + 1)) / D;   // DMA spacing
+  static_assert(DSP >= 1, "schedule");
+  __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE];
 
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   const int nwg = tiles_m * tiles_n * splits;
@@ -120,207 +194,202 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_nt_k(const bf16* __restrict__ A,
   const int kt0 = sp * per;
   const int nk = max(0, min(nk_all, kt0 + per) - kt0);
 
+  // ---- DMA sources (per-lane byte offsets; the K-tile step goes in the scalar offset)
   const rsrc_t rsa = make_rsrc(A, (uint64_t)((size_t)(M - 1) * lda + K) * 2);
-  const rsrc_t rsb = make_rsrc(B, (uint64_t)((size_t)(N - 1) * ldb + K) * 2);
-  uint32_t va[8], vb[8];
+  const rsrc_t rsb = BT ? make_rsrc(B, (uint64_t)((size_t)(K - 1) * ldb + N) * 2)
+                        : make_rsrc(B, (uint64_t)((size_t)(N - 1) * ldb + K) * 2);
+  uint32_t va[8], vb[8];   // (fixed sizes: a lambda capturing a template-sized local array drops the
+                          // kernel's host-side instantiation — hipcc / clang, ROCm 7.2)
   {
     const int r8 = lane >> 3, c = (lane & 7) ^ (r8 & 6);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      int ra = m0 + w * 64 + i * 8 + r8;
-      ra = ra < M ? ra : M - 1;
-      int rb = n0 + w * 64 + i * 8 + r8;
-      rb = rb < N ? rb : N - 1;
+    for (int i = 0; i < 8; ++i) {   // A: wave w, DMA i → rows 64w + 8i + r8
+      const int ra = min(m0 + w * 64 + i * 8 + r8, M - 1);
       va[i] = ((uint32_t)ra * (uint32_t)lda + (uint32_t)(kt0 * BK + c * 8)) * 2u;
-      vb[i] = ((uint32_t)rb * (uint32_t)ldb + (uint32_t)(kt0 * BK + c * 8)) * 2u;
+    }
+    if constexpr (!BT) {
+#pragma unroll
+      for (int i = 0; i < DB; ++i) {   // B rows (BN/4)·w + 8i + r8
+        int rb;
+        if constexpr (EPI == 1) {   // tile row rt → gate row or up row of h-column block 16·(rt / 32)
+          const int rt = w * (BN / 4) + i * 8 + r8;
+          const int hr = min(tn * (BN / 2) + 16 * (rt >> 5) + (rt & 15), F - 1);
+          rb = (rt & 16) ? F + hr : hr;
+        } else {
+          rb = min(n0 + w * (BN / 4) + i * 8 + r8, N - 1);
+        }
+        vb[i] = ((uint32_t)rb * (uint32_t)ldb + (uint32_t)(kt0 * BK + c * 8)) * 2u;
+      }
+    } else {
+      constexpr int CPR = BN / 8;             // 16-B chunks per k-row (32 or 16)
+      constexpr int RPD = 64 / CPR;            // k-rows per DMA (2 or 4)
+#pragma unroll
+      for (int i = 0; i < DB; ++i) {   // k-rows (16)·w + RPD·i + lane / CPR
+        const int kr = 16 * w + RPD * i + lane / CPR;
+        const int hk = (kr & 3) | ((kr >> 1) & 4);
+        const int cc = (lane % CPR) ^ (2 * hk);
+        vb[i] = ((uint32_t)(kt0 * BK + kr) * (uint32_t)ldb + (uint32_t)(n0 + 8 * cc)) * 2u;
+      }
     }
   }
+  const uint32_t b_step = BT ? (uint32_t)BK * (uint32_t)ldb * 2u : (uint32_t)(BK * 2);
 
+  // ---- fragment read offsets
   int lo[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) lo[s] = ((lane >> 3) & 1) * 1024 + 16 * slot_of(lane & 7, 4 * s + (lane >> 4));
   const int a_off = wr * 8 * 2048;
-  const int b_off = wc * 8 * 2048;
+  const int b_off = wc * NB * 2048;
+  int boff_t[8];
+  if constexpr (BT) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int hk = q | ((g & 1) << 2);
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+      boff_t[j] = (8 * g + q) * (2 * BN) + 32 * ((wc * NB + j) ^ hk) + 16 * (p >> 1) + 8 * (p & 1);
+  }
 
-  f32x4 acc[8][8];
-  Frags f0, f1;
+  f32x4 acc[8][8];   // [.][NB..7] unused when BN = 128
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
 
-  // producer order inside a half: group g (0..7) reads a[2g], a[2g+1] (g < 4) or b[2g-8], b[2g-7];
-  // consumer order: column j of 8 MFMAs needs b[j] and every a[i] — the a's land first
-  auto read_g = [&](Frags& f, const char* ia, const char* ib, int s, int g) {
-    if (g < 4) {
-      f.a[2 * g] = lds_frag(ia + a_off + (2 * g) * 2048 + lo[s]);
-      f.a[2 * g + 1] = lds_frag(ia + a_off + (2 * g + 1) * 2048 + lo[s]);
+  // LDS-DMA as asm statements: hipcc then tracks no LDS-DMA and does not drain the whole queue
+  // (vmcnt(0)) in front of the first ds_read_b64_tr_b16 of the next tile, which it cannot prove
+  // disjoint from the in-flight stages (measured: the dX kernel waited 33 % of its cycles there).
+  // Every ordering of DMA'd data is by the explicit vmcnt + barrier pairs below.
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)lds);
+  const uint32_t wa = lds_base + (uint32_t)w * 8192u, wb = lds_base + IMG_A + (uint32_t)w * (IMG_B / 4);
+  auto dma_a = [&](uint32_t st, int t, int q) {
+    dma_lds(rsa, wa + st + q * 1024, va[q], (uint32_t)t * (BK * 2));
+  };
+  auto dma_b = [&](uint32_t st, int t, int q) {
+    dma_lds(rsb, wb + st + q * 1024, vb[q], (uint32_t)t * b_step);
+  };
+  auto dma_tile = [&](uint32_t st, int t) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dma_a(st, t, q);
+#pragma unroll
+    for (int q = 0; q < DB; ++q) dma_b(st, t, q);
+  };
+  // read item r of K-half s of the stage at st into (fa, fb)
+  auto read_item = [&](bf16x8* fa, bf16x8* fb, const char* st, int s, int r) {
+    if (sched_of<NB>().rd_a[r]) {
+      fa[sched_of<NB>().rd_i[r]] = lds_frag(st + a_off + sched_of<NB>().rd_i[r] * 2048 + lo[s]);
+    } else if constexpr (BT) {
+      const char* pb = st + IMG_A + s * (32 * 2 * BN) + boff_t[sched_of<NB>().rd_i[r]];
+      const bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)pb);
+      const bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(pb + 4 * 2 * BN));
+      fb[sched_of<NB>().rd_i[r]] = bf16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
     } else {
-      const int j = 2 * (g - 4);
-      f.b[j] = lds_frag(ib + b_off + j * 2048 + lo[s]);
-      f.b[j + 1] = lds_frag(ib + b_off + (j + 1) * 2048 + lo[s]);
+      fb[sched_of<NB>().rd_i[r]] = lds_frag(st + IMG_A + b_off + sched_of<NB>().rd_i[r] * 2048 + lo[s]);
     }
-  };
-  auto mma_col = [&](const Frags& f, int j) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) mfma_acc(acc[i][j], f.b[j], f.a[i]);
-  };
-  auto mma_col0 = [&](const Frags& f, int j) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) mfma_zero(acc[i][j], f.b[j], f.a[i]);
-  };
-  auto dma = [&](const rsrc_t& rs, const uint32_t* voff, char* im, int t, int q) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(im + w * 8192 + q * 1024), 16, voff[q],
-                                             (uint32_t)t * (BK * 2), 0, 0);
   };
 
   if (nk <= 0) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  } else if constexpr (VAR == 8) {
-    // Double-buffered form: two 64 KB stages (A image + B image each).  Per K-tile t, one
-    // 128-MFMA stream: MFMAs 0-63 on the first K-half (fA), 64-127 on the second (fB);
-    //   MFMA  0-15: + one fragment read each of tile t's second half (into fB)
-    //   after 25  : lgkmcnt(0) + barrier 1 — nobody reads stage t&1 any more
-    //   MFMA 26-101, every 5th: one LDS-DMA of tile t+2 into stage t&1 (8 A, then 8 B)
-    //   after 111 : vmcnt(16) (tile t+1 landed; t+2's 16 in flight) + barrier 2
-    //   MFMA 112-127: + one fragment read each of tile t+1's first half (into fA)
-    // The first half's MFMAs walk (i, j) in shells of max(i, j): shell s needs reads 2s, 2s+1 only.
-    const int t1 = nk > 1 ? 1 : 0;
+      for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  } else {
+    // prologue: tiles 0 .. STAGES-1 (clamped: past the last tile the DMAs re-stage tile nk-1 into
+    // stages nobody reads again), wait for tile 0, read its first half
 #pragma unroll
-    for (int q = 0; q < 8; ++q) dma(rsa, va, lds + 0 * IMG, 0, q);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dma(rsb, vb, lds + 1 * IMG, 0, q);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dma(rsa, va, lds + 2 * IMG, t1, q);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dma(rsb, vb, lds + 3 * IMG, t1, q);
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    for (int s = 0; s < STAGES; ++s) dma_tile(s * STAGE, min(s, nk - 1));
+    wait_vmcnt<(STAGES - 1) * D>();
     __builtin_amdgcn_s_barrier();
-    auto read_r = [&](Frags& f, const char* ia, const char* ib, int s, int r) {
-      if ((r & 1) == 0) f.a[r >> 1] = lds_frag(ia + a_off + (r >> 1) * 2048 + lo[s]);
-      else f.b[r >> 1] = lds_frag(ib + b_off + (r >> 1) * 2048 + lo[s]);
-    };
 #pragma unroll
-    for (int r = 0; r < 16; ++r) read_r(f0, lds, lds + IMG, 0, r);
-    int cur = 0;
+    for (int r = 0; r < R; ++r) read_item(fa0, fb0, lds, 0, r);
+
+    int cur = 0;   // stage of tile t (byte offset)
     auto body = [&](auto first, int t) {
-      const int t2 = t + 2 < nk ? t + 2 : nk - 1;
-      char* const ca = lds + cur;
-      char* const cb = ca + IMG;
-      char* const na = lds + (cur ^ (2 * IMG));
-      char* const nb = na + IMG;
-      Unroll<0, 128>::run([&](auto kc) {
+      const int tn_ = t + STAGES < nk ? t + STAGES : nk - 1;
+      char* const cs = lds + cur;
+      char* const ns = lds + (cur + STAGE == STAGES * STAGE ? 0 : cur + STAGE);
+      Unroll<0, KT>::run([&](auto kc) {
         constexpr int k = decltype(kc)::value;
-        constexpr int i = kShell.i[k & 63], j = kShell.j[k & 63];
-        if constexpr (k < 64) {
-          if constexpr (decltype(first)::value) mfma_zero(acc[i][j], f0.b[j], f0.a[i]);
-          else mfma_acc(acc[i][j], f0.b[j], f0.a[i]);
+        constexpr int i = sched_of<NB>().i[k % H], j = sched_of<NB>().j[k % H];
+        if constexpr (k < H) {
+          if constexpr (decltype(first)::value) mfma_zero(acc[i][j], fb0[j], fa0[i]);
+          else mfma_acc(acc[i][j], fb0[j], fa0[i]);
         } else {
-          mfma_acc(acc[i][j], f1.b[j], f1.a[i]);
+          mfma_acc(acc[i][j], fb1[j], fa1[i]);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (k < 16) read_r(f1, ca, cb, 1, k);
-        if constexpr (k == 25) {
-          __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+        if constexpr (k < R) read_item(fa1, fb1, cs, 1, k);
+        if constexpr (k == K1) {
+          __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
           __builtin_amdgcn_s_barrier();
         }
-        if constexpr (k >= 26 && k <= 101 && (k - 26) % 5 == 0) {
-          constexpr int d = (k - 26) / 5;
-          if constexpr (d < 8) dma(rsa, va, ca, t2, d);
-          else dma(rsb, vb, cb, t2, d - 8);
+        if constexpr (k > K1 && (k - K1 - 1) % DSP == 0 && (k - K1 - 1) / DSP < D) {
+          constexpr int d = (k - K1 - 1) / DSP;
+          if constexpr (d < 8) dma_a(cur, tn_, d);
+          else dma_b(cur, tn_, d - 8);
         }
-        if constexpr (k == 111) {
-          __builtin_amdgcn_s_waitcnt(0x4F70);   // vmcnt(16)
+        if constexpr (k == K2) {
+          wait_vmcnt<(STAGES - 1) * D>();
           __builtin_amdgcn_s_barrier();
         }
-        if constexpr (k >= 112) read_r(f0, na, nb, 0, k - 112);
+        if constexpr (k > K2) read_item(fa0, fb0, ns, 0, k - K2 - 1);
         __builtin_amdgcn_sched_barrier(0);
       });
-      cur ^= 2 * IMG;
+      cur = cur + STAGE == STAGES * STAGE ? 0 : cur + STAGE;
     };
     body(std::integral_constant<bool, true>{}, 0);
     for (int t = 1; t < nk; ++t) body(std::integral_constant<bool, false>{}, t);
     asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-  } else {
-    const int t1 = nk > 1 ? 1 : 0;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dma(rsa, va, lds + 0 * IMG, 0, q);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dma(rsb, vb, lds + 1 * IMG, 0, q);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dma(rsa, va, lds + 2 * IMG, t1, q);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) dma(rsb, vb, lds + 3 * IMG, t1, q);
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-#pragma unroll
-    for (int g = 0; g < 8; ++g) read_g(f0, lds, lds + IMG, 0, g);
-    if constexpr ((VAR & 2) != 0) f1 = f0;
-
-    // ring slots of the images A_t = 2t, B_t = 2t + 1 (mod 5), advanced incrementally
-    int s_ia = 0;   // slot of A_t
-    for (int t = 0; t < nk; ++t) {
-      const int t2 = t + 2 < nk ? t + 2 : nk - 1;
-      const int s_ib = s_ia + 1 >= 5 ? s_ia - 4 : s_ia + 1;
-      const int s_na = s_ib + 1 >= 5 ? s_ib - 4 : s_ib + 1;
-      const int s_nb = s_na + 1 >= 5 ? s_na - 4 : s_na + 1;
-      const int s_da = s_nb + 1 >= 5 ? s_nb - 4 : s_nb + 1;   // == slot of B_{t-1}
-      const int s_db = s_ia;                                   // A_t's slot, free after the mid barrier
-      char* const ia = lds + s_ia * IMG;
-      char* const ib = lds + s_ib * IMG;
-      char* const na = lds + s_na * IMG;
-      char* const nb = lds + s_nb * IMG;
-      char* const da = lds + s_da * IMG;
-      char* const db = lds + s_db * IMG;
-      if (t == 0) {
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-          mma_col0(f0, g);
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr ((VAR & 2) == 0) read_g(f1, ia, ib, 1, g);
-          if constexpr ((VAR & 1) == 0) dma(rsa, va, da, t2, g);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      } else {
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-          mma_col(f0, g);
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr ((VAR & 2) == 0) read_g(f1, ia, ib, 1, g);
-          if constexpr ((VAR & 1) == 0) dma(rsa, va, da, t2, g);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      if constexpr ((VAR & 4) == 0) {
-        __builtin_amdgcn_s_waitcnt(0x0F78);   // vmcnt(8): tile t+1 complete
-        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-        __builtin_amdgcn_s_barrier();
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        if constexpr ((VAR & 2) == 0) read_g(f0, na, nb, 0, g);
-        if constexpr ((VAR & 1) == 0) dma(rsb, vb, db, t2, g);
-        __builtin_amdgcn_sched_barrier(0);
-        mma_col(f1, g);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      s_ia = s_na;
-    }
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   }
 
+  // ---- epilogue: lane holds C[m = col][n = 4·(lane>>4) + r … +3] of each 16×16 block
+  if constexpr (EPI == 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + wr * 128 + i * 16 + (lane & 15);
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < NB; j += 2) {
+        const int hc = tn * (BN / 2) + 16 * (wc * (NB / 2) + j / 2) + 4 * (lane >> 4);
+        if (hc >= F) continue;
+        bf16x4 g, u, h;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          g[e] = (bf16)acc[i][j][e];
+          u[e] = (bf16)acc[i][j + 1][e];
+          h[e] = (bf16)(silu_f((float)g[e]) * (float)u[e]);
+        }
+        bf16* gu = reinterpret_cast<bf16*>(out) + (size_t)m * 2 * F + hc;
+        *reinterpret_cast<bf16x4*>(gu) = g;
+        *reinterpret_cast<bf16x4*>(gu + F) = u;
+        *reinterpret_cast<bf16x4*>(aux_out + (size_t)m * F + hc) = h;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = m0 + wr * 128 + i * 16 + (lane & 15);
     if (m >= M) continue;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int n = n0 + wc * 128 + j * 16 + 4 * (lane >> 4);
+    for (int j = 0; j < NB; ++j) {
+      const int n = n0 + wc * (BN / 2) + j * 16 + 4 * (lane >> 4);
       if (n >= N) continue;
       f32x4 v = acc[i][j];
       if constexpr (SPLIT) {
         float* ws = reinterpret_cast<float*>(out) + ((size_t)sp * M + m) * N + n;
         *reinterpret_cast<f32x4*>(ws) = v;
+      } else if constexpr (EPI == 2) {
+        const bf16* gp = aux + (size_t)m * 2 * F + n;
+        const bf16x4 g4 = *reinterpret_cast<const bf16x4*>(gp);
+        const bf16x4 u4 = *reinterpret_cast<const bf16x4*>(gp + F);
+        bf16x4 dg, du;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = (float)(bf16)v[e], g = (float)g4[e], uu = (float)u4[e];
+          const float sg = 1.f / (1.f + __expf(-g));
+          du[e] = (bf16)(d * (g * sg));
+          dg[e] = (bf16)(d * uu * (sg * (1.f + g * (1.f - sg))));
+        }
+        bf16* dp = reinterpret_cast<bf16*>(out) + (size_t)m * 2 * F + n;
+        *reinterpret_cast<bf16x4*>(dp) = dg;
+        *reinterpret_cast<bf16x4*>(dp + F) = du;
       } else {
         if (residual) {
           const bf16x4 rr = *reinterpret_cast<const bf16x4*>(residual + (size_t)m * N + n);
@@ -355,53 +424,126 @@ __global__ __launch_bounds__(256) void splitk_sum_k(const float* __restrict__ ws
   }
 }
 
+int tiles_of(int M, int N, int bn) { return ((M + BM - 1) / BM) * ((N + bn - 1) / bn); }
+
 }  // namespace
 
-bool gemm4w_supported(int M, int N, int K, int lda, int ldb) {
+// bt: B given as [K, N] (row stride ldb) instead of [N, K]
+bool gemm4w_supported(int M, int N, int K, int lda, int ldb, bool bt) {
   return M > 0 && K % BK == 0 && K >= BK && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
-         (uint64_t)M * lda * 2 < 0xFFFFFFFFull && (uint64_t)N * ldb * 2 < 0xFFFFFFFFull;
+         (uint64_t)M * lda * 2 < 0xFFFFFFFFull &&
+         (bt ? (uint64_t)K * ldb * 2 < 0xFFFFFFFFull : (uint64_t)N * ldb * 2 < 0xFFFFFFFFull);
 }
 
-// K-splits for a tile grid smaller than the chip (M = 2048 × N = 4096 is 128 tiles for 256 CUs)
-int gemm4w_splits(int M, int N, int K) {
-  static const int forced = [] {
+// Tile width and K-splits from one cost model: (rounds of 256 workgroups) × (K-tiles per workgroup)
+// × the measured in-step time of one K-tile at that width (256: 1.5 µs / 1.62 transposed-B, 192: 1.22,
+// 128: 0.92) + the
+// split-K reduce pass (its fp32 slabs: M·N·(8s + 2) bytes at ≈12 TB/s effective + a launch).  At
+// M = 2048 this picks: q|k|v fwd 192 (256 tiles); gate|up fwd / LM head 256; o fwd, every dX to
+// d_model and down dX (768 tiles = 3 full rounds) 128; down fwd 256 with 2 splits.
+// LIPA_GEMM4W_BN / LIPA_GEMM4W_SPLITS force either.
+struct G4wCfg {
+  int bn, splits;
+};
+G4wCfg gemm4w_cfg(int M, int N, int K, bool bt, int bn_req, int sp_req) {
+  static const int forced_bn = [] {
+    const char* e = getenv("LIPA_GEMM4W_BN");
+    return e ? atoi(e) : 0;
+  }();
+  static const int forced_sp = [] {
     const char* e = getenv("LIPA_GEMM4W_SPLITS");
     return e ? atoi(e) : 0;
   }();
-  if (forced > 0) return forced;
-  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (bn_req == 0) bn_req = forced_bn;
+  if (sp_req <= 0) sp_req = forced_sp;
   const int nk = K / BK;
-  int s = 1;
-  while (tiles * s < 200 && nk / (2 * s) >= 16) s *= 2;
-  return s;
+  G4wCfg best{128, 1};
+  double best_t = 1e30;
+  for (int bn : {256, 192, 128}) {
+    if (bn == 192 && bt) continue;
+    if (bn_req && bn != bn_req) continue;
+    const int tiles = tiles_of(M, N, bn);
+    const double kt_us = bn == 256 ? (bt ? 1.62 : 1.5) : bn == 192 ? 1.22 : 0.92;
+    for (int s = 1; s <= 8; s *= 2) {
+      if (sp_req > 0 && s != sp_req) continue;
+      if (s > 1 && sp_req <= 0 && nk / s < 8) break;
+      double t = (double)((tiles * s + 255) / 256) * ((nk + s - 1) / s) * kt_us;
+      if (s > 1) t += (double)M * N * (8.0 * s + 2.0) / 12e6 + 2.0;
+      if (t < best_t - 1e-9) {
+        best_t = t;
+        best = G4wCfg{bn, s};
+      }
+    }
+  }
+  if (sp_req > 0) best.splits = sp_req;
+  return best;
+}
+
+// bn / splits: 0 = chosen by gemm4w_cfg.  Returns the split count used (the caller's fp32 workspace
+// must hold splits·M·N floats when it is > 1).
+int gemm4w_plan(int M, int N, int K, bool bt, int bn, int splits, int* bn_out) {
+  const G4wCfg c = gemm4w_cfg(M, N, K, bt, bn, splits);
+  if (bn_out) *bn_out = c.bn;
+  return c.splits;
 }
 
 void launch_gemm4w(const void* A, int lda, const void* B, int ldb, const void* residual, void* out, float* ws, int M,
-                   int N, int K, int splits, hipStream_t st) {
-  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  static const int var = [] {
-    const char* e = getenv("LIPA_GEMM4W_VAR");
-    return e ? atoi(e) : 0;
-  }();
-  if (splits <= 1) {
-#define G4W_VAR(V)                                                                                                 \
-  case V:                                                                                                          \
-    gemm4w_nt_k<false, V><<<tiles, NT, 0, st>>>((const bf16*)A, lda, (const bf16*)B, ldb, (const bf16*)residual, out, \
-                                                M, N, K, 1);                                                        \
-    break;
-    switch (var) {
-      G4W_VAR(1) G4W_VAR(2) G4W_VAR(3) G4W_VAR(4) G4W_VAR(5) G4W_VAR(7) G4W_VAR(8)
-      default:
-        gemm4w_nt_k<false><<<tiles, NT, 0, st>>>((const bf16*)A, lda, (const bf16*)B, ldb, (const bf16*)residual, out,
-                                                 M, N, K, 1);
-    }
-#undef G4W_VAR
+                   int N, int K, int splits, bool bt, int bn, hipStream_t st) {
+  // callers pass the (bn, splits) that gemm4w_plan returned
+  const int tiles = tiles_of(M, N, bn);
+  const bool split = splits > 1;
+  const bf16* a = (const bf16*)A;
+  const bf16* b = (const bf16*)B;
+  const bf16* r = split ? nullptr : (const bf16*)residual;
+  void* o = split ? (void*)ws : out;
+  const int grid = tiles * (split ? splits : 1), sp = split ? splits : 1;
+#define G4W(BN_, BT_, SP_) \
+  gemm4w_k<BN_, BT_, SP_><<<grid, NT, 0, st>>>(a, lda, b, ldb, r, o, M, N, K, sp, nullptr, nullptr, 0)
+  if (bn == 256) {
+    if (bt) { if (split) G4W(256, true, true); else G4W(256, true, false); }
+    else { if (split) G4W(256, false, true); else G4W(256, false, false); }
+  } else if (bn == 192) {
+    if (split) G4W(192, false, true); else G4W(192, false, false);
   } else {
-    gemm4w_nt_k<true><<<tiles * splits, NT, 0, st>>>((const bf16*)A, lda, (const bf16*)B, ldb, nullptr, ws, M, N, K,
-                                                     splits);
+    if (bt) { if (split) G4W(128, true, true); else G4W(128, true, false); }
+    else { if (split) G4W(128, false, true); else G4W(128, false, false); }
+  }
+#undef G4W
+  if (split) {
     const size_t MN = (size_t)M * N;
     const int blocks = (int)std::min<size_t>((MN / 8 + 255) / 256, 2048);
     splitk_sum_k<<<blocks, 256, 0, st>>>(ws, (const bf16*)residual, (bf16*)out, MN, splits);
   }
+  LIPA_CHECK_LAUNCH();
+}
+
+// gu [M, 2F] and h = silu(gate)·up [M, F] from x [M, K] and W_gu [2F, K] ([gate | up] rows), one launch
+void launch_gemm4w_swiglu(const void* X, int ldx, const void* W, void* gu, void* h, int M, int F, int K, int bn,
+                          hipStream_t st) {
+  const int N = 2 * F;
+  const int tiles = tiles_of(M, N, bn);
+  const bf16* a = (const bf16*)X;
+  const bf16* b = (const bf16*)W;
+#define G4S(BN_) \
+  gemm4w_k<BN_, false, false, 1><<<tiles, NT, 0, st>>>(a, ldx, b, K, nullptr, gu, M, N, K, 1, nullptr, (bf16*)h, F)
+  if (bn == 256) G4S(256);
+  else if (bn == 192) G4S(192);
+  else G4S(128);
+#undef G4S
+  LIPA_CHECK_LAUNCH();
+}
+
+// dgu [M, 2F] = SwiGLU-backward(dh = dY·W_down, gu) with W_down [N_w, F] used as stored, one launch
+void launch_gemm4w_dswiglu(const void* DY, int lddy, const void* W, const void* gu, void* dgu, int M, int F, int Nw,
+                           int bn, hipStream_t st) {
+  const int tiles = tiles_of(M, F, bn);
+  const bf16* a = (const bf16*)DY;
+  const bf16* b = (const bf16*)W;
+  if (bn == 256)
+    gemm4w_k<256, true, false, 2><<<tiles, NT, 0, st>>>(a, lddy, b, F, nullptr, dgu, M, F, Nw, 1, (const bf16*)gu,
+                                                        nullptr, F);
+  else
+    gemm4w_k<128, true, false, 2><<<tiles, NT, 0, st>>>(a, lddy, b, F, nullptr, dgu, M, F, Nw, 1, (const bf16*)gu,
+                                                        nullptr, F);
   LIPA_CHECK_LAUNCH();
 }

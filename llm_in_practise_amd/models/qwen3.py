@@ -26,6 +26,7 @@ import torch.nn as nn
 
 from ..ops import reference as ref
 from ..ops.activation import swiglu_fused
+from ..ops.mlp import fusable as mlp_fusable, swiglu_mlp
 from ..ops.attention import flash_attention, flash_attention_prefix
 from ..ops.decode import decode_attention_append
 from ..ops.linear import checkpoint as lora_checkpoint
@@ -33,9 +34,12 @@ from ..ops.loss import fused_linear_cross_entropy, shift_labels
 from ..ops.norm import RMSNorm, rms_norm, rms_norm_residual
 from ..ops.rope import apply_rope, qk_norm_rope
 from ..parallel.tensor_parallel import tp_all_reduce
-from ..peft.lora import base_of
+from ..peft.lora import LoraLayer, base_of
 from ..ops.embedding import Embedding
-from .common import CausalLMOutput, FusedProjection, KVCache, PackedPrefill, can_fuse, project
+from .common import CausalLMOutput, FusedProjection, KVCache, PackedPrefill, _leaf_linear, can_fuse, project
+
+# LIPA_FUSED_MLP=0: run the SwiGLU MLP as separate projections + activation kernels
+_FUSED_MLP = os.environ.get("LIPA_FUSED_MLP", "1") != "0"
 
 
 @dataclasses.dataclass
@@ -211,8 +215,28 @@ class Qwen3MLP(nn.Module):
         mods = [self.gate_proj, self.up_proj]
         self._gu = FusedProjection(mods) if can_fuse(mods) else None
 
+    def _fused_bases(self, x):
+        """(gate|up base, down base) when the whole block can run as the epilogue-fused SwiGLU
+        MLP (ops/mlp.py): fused gate|up, no adapters or TP on the block, bias-free frozen bases."""
+        if self._gu is None or self.tp_group is not None or not _FUSED_MLP:
+            return None
+        mods = (self.gate_proj, self.up_proj, self.down_proj)
+        if any((isinstance(m, LoraLayer) and not m.merged) or getattr(_leaf_linear(m), "_mlora", None) is not None
+               for m in mods):
+            return None
+        down_base, down_bias = base_of(self.down_proj)
+        if self._gu.bias is not None or down_bias is not None:
+            return None
+        leaf = _leaf_linear(self.gate_proj)
+        if not mlp_fusable(x, self._gu.base, down_base, leaf.out_features, leaf.in_features):
+            return None
+        return self._gu.base, down_base
+
     def forward(self, x, residual=None):
         tr = self.training
+        bases = self._fused_bases(x)
+        if bases is not None:
+            return swiglu_mlp(x, bases[0], bases[1], residual)
         gu = project([self.gate_proj, self.up_proj], x, None, tr, self._gu)
         if self.tp_group is None:
             return project([self.down_proj], swiglu_fused(gu), residual, tr)

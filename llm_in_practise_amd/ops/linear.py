@@ -46,6 +46,21 @@ _APPLY = __import__("os").environ.get("LIPA_LORA_APPLY", "1") != "0"
 # timed in the running step; LIPA_LT=0: torch.addmm / torch.mm / torch.bmm
 _LT = __import__("os").environ.get("LIPA_LT", "1") != "0"
 _LT_MIN_M = 256
+# training-sized frozen-base GEMMs (forward x·Wᵀ and backward dY·W) through the hand-written
+# one-wave-per-SIMD MFMA kernel (csrc/kernels/gemm4w.hip); LIPA_GEMM=lt: direct hipBLASLt
+_G4W = __import__("os").environ.get("LIPA_GEMM", "native") == "native"
+
+
+def _g4w_ok(a: torch.Tensor, w: torch.Tensor, bt: bool) -> bool:
+    """Shapes / strides the gemm4w kernel takes: a [M, K] row-major (row stride % 8), w [N, K]
+    (or [K, N] when bt) contiguous, K % 64, N % 8, 16-B aligned, training-sized M."""
+    if not (_G4W and a.is_cuda and a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and a.dim() == 2
+            and a.shape[0] >= _LT_MIN_M and a.stride(1) == 1 and a.stride(0) % 8 == 0 and w.is_contiguous()):
+        return False
+    K = a.shape[1]
+    N = w.shape[1] if bt else w.shape[0]
+    return ((w.shape[0] if bt else w.shape[1]) == K and K % 64 == 0 and N % 8 == 0 and a.data_ptr() % 16 == 0
+            and w.data_ptr() % 16 == 0)
 # q_proj + v_proj with dropout: the forward's lora_proj2 stores the keep bits (1 bit per element and
 # branch) and lora_acc2 reads them instead of re-hashing; LIPA_LORA_KEEP_BITS=0: regenerate
 _KEEP_BITS = __import__("os").environ.get("LIPA_LORA_KEEP_BITS", "1") != "0"
@@ -106,6 +121,9 @@ def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
         # the residual; the wide gate|up / long-K down stay on hipBLASLt (≥ 5 TB/s there)
         y = native().gemm_skinny(x, base, residual)
         return y if ext_a is None else y.addmm_(ext_a, ext_b.t())
+    if _g4w_ok(x, base, False) and not _NATIVE_DENSE:
+        y = native().gemm4w(x, base, None if residual is None else residual.contiguous(), 0, False)
+        return y if ext_a is None else y.addmm_(ext_a, ext_b.t())
     if _LT and M >= _LT_MIN_M and x.is_cuda and x.dtype == torch.bfloat16 and x.stride(1) == 1 \
             and not _NATIVE_DENSE:
         y = native().lt_linear(x, base.contiguous(), None if residual is None else residual.contiguous(), True)
@@ -149,6 +167,8 @@ def _dense_dx(dy: torch.Tensor, w: torch.Tensor, tune: bool = True) -> torch.Ten
     batched GEMM + an fp32 slice sum fill it (2 slices: 301 + 8 µs; profiles/hipblaslt_direct_ab.txt)."""
     M, N = dy.shape
     K = w.shape[1]
+    if _g4w_ok(dy, w, True):
+        return native().gemm4w(dy, w, None, 0, True)
     split = _dx_split(dy, w)
     if _LT and M >= _LT_MIN_M and dy.is_cuda and dy.dtype == torch.bfloat16 and K % 8 == 0:
         return native().lt_dx(dy.contiguous(), w.contiguous(), split, tune, None)
@@ -485,15 +505,17 @@ class _FusedLinearFn(torch.autograd.Function):
             wb = ctx.wdq if ctx.wdq is not None else (base if not dense else weight)
             pair_ok = (ctx.pair and all(k is not None for k in ctx.keys) and not deterministic()
                        and ctx.needs_input_grad[5] and ctx.needs_input_grad[7])
+            g4w = _g4w_ok(dy, wb, True) if isinstance(wb, torch.Tensor) else False
             if (pair_ok and _DX_C and ctx.masks is not None and not fold and isinstance(wb, torch.Tensor)
-                    and _LT and not _NATIVE_DENSE and dy.shape[0] >= _LT_MIN_M and _dx_split(dy, wb) == 1):
+                    and not _NATIVE_DENSE and dy.shape[0] >= _LT_MIN_M and (g4w or (_LT and _dx_split(dy, wb) == 1))):
                 # the LoRA input-gradient term written once (lora_dx2, from the stored keep bits) and
                 # added by the dX GEMM as its C matrix; dA from x in a separate launch — no
                 # read-modify-write pass over dx (lora_acc2)
                 a0, a1 = bf16_view(ab[0], dy.dtype), bf16_view(ab[2], dy.dtype)
                 p0, p1 = branches[0].dropout, branches[1].dropout
                 c = native().lora_dx2(g_list[0], g_list[1], a0, a1, ctx.masks, p0, p1)
-                dx = native().lt_dx(dy.contiguous(), wb.contiguous(), 1, True, c)
+                dx = (native().gemm4w(dy, wb, c, 0, True) if g4w else
+                      native().lt_dx(dy.contiguous(), wb.contiguous(), 1, True, c))
                 del c
                 (o0, ret0), (o1, ret1) = dest(0), dest(2)
                 native().lora_dA_pair(g_list[0], g_list[1], x, o0, o1, ctx.masks, p0, p1)

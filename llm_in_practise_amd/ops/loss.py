@@ -1,8 +1,8 @@
 """Cross-entropy (K7) and the fused, chunked LM-head + cross-entropy.
 
 ``fused_linear_cross_entropy`` never materialises the full ``[T, V]`` fp32 logits (1.2 GB
-per 2 K tokens at V=151,936): per token chunk it runs the head GEMM (hipBLASLt, plain
-library GEMM), then ONE HIP kernel computes the row log-sum-exp, the loss and overwrites
+per 2 K tokens at V=151,936): per token chunk it runs the head GEMM (the hand-written MFMA
+kernel of csrc/kernels/gemm4w.hip), then ONE HIP kernel computes the row log-sum-exp, the loss and overwrites
 the bf16 logits with dlogits in place; ``dX`` for the chunk is one more GEMM.  The
 gradient is produced during the forward (the loss is terminal), so the backward only
 scales it.  Matches HF's causal-LM loss: labels shifted by one, ``ignore_index=-100``,
@@ -15,6 +15,7 @@ import torch.nn.functional as F
 
 from . import reference as ref
 from ._native import native, use_native
+from .linear import _g4w_ok
 
 
 def cross_entropy(logits, labels, ignore_index: int = -100):
@@ -38,11 +39,19 @@ class _FusedLinearCEFn(torch.autograd.Function):
         loss = torch.zeros((), dtype=torch.float32, device=h.device)
         for s in range(0, T, chunk):
             hc = h[s:s + chunk]
-            logits = hc @ weight.t()
+            g4w = _g4w_ok(hc, weight, False)
+            logits = native().gemm4w(hc, weight, None, 0, False) if g4w else hc @ weight.t()
             g0, g1 = s // rows_g, (s + hc.shape[0]) // rows_g
             row_loss = native().ce_fwd_bwd(logits, labels[s:s + chunk], ignore_index, inv[g0:g1])
             loss += (row_loss.view(g1 - g0, -1).sum(1) * inv[g0:g1]).sum()
-            torch.matmul(logits, weight, out=dh[s:s + chunk])
+            if g4w and _g4w_ok(logits, weight, True):
+                dhc = native().gemm4w(logits, weight, None, 0, True)
+                if hc.shape[0] == T:
+                    dh = dhc
+                else:
+                    dh[s:s + chunk] = dhc
+            else:
+                torch.matmul(logits, weight, out=dh[s:s + chunk])
             if need_wgrad:
                 dw.add_(logits.t().float() @ hc.float())
         ctx.save_for_backward(dh, dw)

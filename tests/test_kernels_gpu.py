@@ -659,6 +659,69 @@ def test_gemm8_strided_input(native_ext):
     assert rel_err(native_ext.gemm8(x, w, None, None, None, 1), x.float() @ w.float().t()) < 1e-2
 
 
+# ----------------------------------------------------------------------------- one-wave-per-SIMD GEMM
+@pytest.mark.parametrize("M,N,K,splits,bt,resid", [(256, 256, 64, 1, False, False), (512, 768, 512, 1, False, True),
+                                                   (300, 520, 192, 1, False, False), (2048, 1024, 1024, 4, False, True),
+                                                   (257, 264, 640, 2, False, True), (256, 256, 64, 1, True, False),
+                                                   (512, 768, 512, 1, True, True), (300, 520, 192, 1, True, False),
+                                                   (2048, 1024, 2048, 2, True, True), (257, 264, 640, 4, True, False),
+                                                   (1000, 1536, 1024, 0, True, False)])
+@pytest.mark.parametrize("bn", [128, 192, 256])
+def test_gemm4w_matches_fp32(native_ext, M, N, K, splits, bt, resid, bn):
+    """y = x·wᵀ (w [N, K]) or, bt, y = x·w (w [K, N], the dX form), + residual, split-K or not, every
+    tile width (192: forward only)"""
+    if bt and bn == 192:
+        pytest.skip("the 192-wide tile is forward-only")
+    torch.manual_seed(0)
+    x = (torch.rand(M, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    w = (torch.rand(K, N, device=DEV) * 2 - 1).to(torch.bfloat16) if bt else \
+        (torch.rand(N, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16) if resid else None
+    y = native_ext.gemm4w(x, w, res, splits, bt, bn)
+    want = x.float() @ (w.float() if bt else w.float().t())
+    if resid:
+        want += res.float()
+    assert y.shape == (M, N)
+    assert rel_err(y, want) < 1e-2
+
+
+def test_gemm4w_asymmetric_operands(native_ext):
+    """integer-valued, asymmetric operands (exact in fp32): a transposed fragment map or a swapped
+    C-write shows as a large error (cdna_hip_programming.md §3)"""
+    torch.manual_seed(1)
+    for bt in (False, True):
+        for bn in ((128, 256) if bt else (128, 192, 256)):
+            M, N, K = 256, 512, 128
+            x = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
+            w = torch.randint(-3, 4, (K, N) if bt else (N, K), device=DEV).to(torch.bfloat16)
+            y = native_ext.gemm4w(x, w, None, 1, bt, bn).float()
+            want = x.float() @ (w.float() if bt else w.float().t())
+            assert torch.equal(y, want), f"bt={bt} bn={bn}: max |err| {(y - want).abs().max().item()}"
+
+
+@pytest.mark.parametrize("M,Fd,K", [(256, 256, 128), (300, 1024, 512), (2048, 3072, 1024), (2048, 12288, 512)])
+def test_gemm4w_swiglu_epilogues(native_ext, M, Fd, K):
+    """gate|up GEMM with the SwiGLU forward epilogue (gu and h in one launch) and the down dX GEMM with
+    the SwiGLU backward epilogue, vs fp32 (the unfused path rounds gu / dh to bf16 at the same points)"""
+    torch.manual_seed(4)
+    x = (torch.rand(M, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    w = (0.05 * torch.randn(2 * Fd, K, device=DEV)).to(torch.bfloat16)
+    gu, h = native_ext.gemm4w_swiglu(x, w)
+    gu_ref = x.float() @ w.float().t()
+    assert rel_err(gu, gu_ref) < 1e-2
+    g, u = gu.float()[:, :Fd], gu.float()[:, Fd:]
+    assert rel_err(h, F.silu(g) * u) < 1e-2
+    Nw = K
+    wd = (0.05 * torch.randn(Nw, Fd, device=DEV)).to(torch.bfloat16)
+    dy = torch.randn(M, Nw, device=DEV).to(torch.bfloat16)
+    dgu = native_ext.gemm4w_dswiglu(dy, wd, gu)
+    dh = (dy.float() @ wd.float()).to(torch.bfloat16).float()
+    gr = g.clone().requires_grad_(True)
+    ur = u.clone().requires_grad_(True)
+    (F.silu(gr) * ur).backward(dh)
+    assert rel_err(dgu[:, :Fd], gr.grad) < 1e-2 and rel_err(dgu[:, Fd:], ur.grad) < 1e-2
+
+
 def test_lora_apply_column_blocks(native_ext):
     """lora_apply: y[:, c0_i:c0_i+n_i] += xa_i·B_iᵀ in place for several branches, other columns untouched."""
     torch.manual_seed(3)

@@ -1,6 +1,7 @@
 """The kept opt-in variants stay numerically equivalent to the default path, so their A/B records
 (profiles/) compare like with like: the single-kernel lora_proj2 (LIPA_PROJ2_IMPL=0) and the per-step
-bf16 NF4 expansion + hipBLASLt (LIPA_NF4_GEMM=dequant).  Each runs the bench step on a small Qwen3 in a
+bf16 NF4 expansion + hipBLASLt (LIPA_NF4_GEMM=dequant), the unfused SwiGLU MLP (LIPA_FUSED_MLP=0) and
+hipBLASLt in place of the hand-written gemm4w GEMMs (LIPA_GEMM=lt).  Each runs the bench step on a small Qwen3 in a
 subprocess (the switches are read once per process).  The measured-slower scheduling variants of
 round 2 (side-stream LoRA projection, two-stream attention backward, background NF4 expansion,
 deferred attention max, multi-adapter dx-as-C) were deleted; their records stay in profiles/."""
@@ -17,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _losses(extra_env):
     env = dict(os.environ, PYTHONPATH=ROOT, HSA_ENABLE_IPC_MODE_LEGACY="0", **extra_env)
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", "qwen3-small", "--steps", "3",
-                          "--warmup", "1"], env=env, capture_output=True, text=True, timeout=110)
+                          "--warmup", "1", "--faithful-steps", "0"], env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-3000:]
     return [float(x) for x in re.findall(r"loss=([0-9.]+)", out.stderr)]
 
@@ -30,7 +31,8 @@ def base_losses():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{"LIPA_PROJ2_IMPL": "0"}], ids=lambda e: ",".join(e))
+@pytest.mark.parametrize("env", [{"LIPA_PROJ2_IMPL": "0"}, {"LIPA_FUSED_MLP": "0"}, {"LIPA_GEMM": "lt"}],
+                         ids=lambda e: ",".join(e))
 def test_opt_in_schedule_matches_default(base_losses, env):
     got = _losses(env)
     assert len(got) == 2 and all(abs(a - b) <= 2e-3 * abs(b) for a, b in zip(got, base_losses)), (env, got,
