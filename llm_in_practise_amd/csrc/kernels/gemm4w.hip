@@ -363,43 +363,78 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
     }
     return;
   }
+  if constexpr (SPLIT) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wr * 128 + i * 16 + (lane & 15);
-    if (m >= M) continue;
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + wr * 128 + i * 16 + (lane & 15);
+      if (m >= M) continue;
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const int n = n0 + wc * (BN / 2) + j * 16 + 4 * (lane >> 4);
-      if (n >= N) continue;
-      f32x4 v = acc[i][j];
-      if constexpr (SPLIT) {
-        float* ws = reinterpret_cast<float*>(out) + ((size_t)sp * M + m) * N + n;
-        *reinterpret_cast<f32x4*>(ws) = v;
-      } else if constexpr (EPI == 2) {
-        const bf16* gp = aux + (size_t)m * 2 * F + n;
-        const bf16x4 g4 = *reinterpret_cast<const bf16x4*>(gp);
-        const bf16x4 u4 = *reinterpret_cast<const bf16x4*>(gp + F);
-        bf16x4 dg, du;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float d = (float)(bf16)v[e], g = (float)g4[e], uu = (float)u4[e];
-          const float sg = 1.f / (1.f + __expf(-g));
-          du[e] = (bf16)(d * (g * sg));
-          dg[e] = (bf16)(d * uu * (sg * (1.f + g * (1.f - sg))));
-        }
-        bf16* dp = reinterpret_cast<bf16*>(out) + (size_t)m * 2 * F + n;
-        *reinterpret_cast<bf16x4*>(dp) = dg;
-        *reinterpret_cast<bf16x4*>(dp + F) = du;
-      } else {
-        if (residual) {
-          const bf16x4 rr = *reinterpret_cast<const bf16x4*>(residual + (size_t)m * N + n);
-          v[0] += (float)rr[0]; v[1] += (float)rr[1]; v[2] += (float)rr[2]; v[3] += (float)rr[3];
-        }
-        bf16x4 o;
-        o[0] = (bf16)v[0]; o[1] = (bf16)v[1]; o[2] = (bf16)v[2]; o[3] = (bf16)v[3];
-        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(out) + (size_t)m * N + n) = o;
+      for (int j = 0; j < NB; ++j) {
+        const int n = n0 + wc * (BN / 2) + j * 16 + 4 * (lane >> 4);
+        if (n < N) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + ((size_t)sp * M + m) * N + n) = acc[i][j];
       }
     }
+    return;
+  }
+  // Epilogues that read global memory (residual; EPI 2's g / u) issue every load of four accumulator
+  // rows before the first use, from clamped (always valid) addresses — one latency per four rows, not
+  // one per 16×16 block (a load behind a per-block bounds branch waits vmcnt(0) each time)
+  const bool has_res = EPI == 0 && residual != nullptr;
+  auto rows4 = [&](auto hh_c, auto res_c) {
+    constexpr int i0 = 4 * decltype(hh_c)::value;
+    constexpr bool RES = decltype(res_c)::value;
+    bf16x4 la[4][8], lb[4][8];
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int m = min(m0 + wr * 128 + (i0 + ii) * 16 + (lane & 15), M - 1);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int n = min(n0 + wc * (BN / 2) + j * 16 + 4 * (lane >> 4), N - 4);
+        if constexpr (EPI == 2) {
+          const bf16* gp = aux + (size_t)m * 2 * F + n;
+          la[ii][j] = *reinterpret_cast<const bf16x4*>(gp);
+          lb[ii][j] = *reinterpret_cast<const bf16x4*>(gp + F);
+        } else if constexpr (RES) {
+          la[ii][j] = *reinterpret_cast<const bf16x4*>(residual + (size_t)m * N + n);
+        }
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int m = m0 + wr * 128 + (i0 + ii) * 16 + (lane & 15);
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int n = n0 + wc * (BN / 2) + j * 16 + 4 * (lane >> 4);
+        if (n >= N) continue;
+        const f32x4 v = acc[i0 + ii][j];
+        if constexpr (EPI == 2) {
+          bf16x4 dg, du;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float d = (float)(bf16)v[e], g = (float)la[ii][j][e], uu = (float)lb[ii][j][e];
+            const float sg = 1.f / (1.f + __expf(-g));
+            du[e] = (bf16)(d * (g * sg));
+            dg[e] = (bf16)(d * uu * (sg * (1.f + g * (1.f - sg))));
+          }
+          bf16* dp = reinterpret_cast<bf16*>(out) + (size_t)m * 2 * F + n;
+          *reinterpret_cast<bf16x4*>(dp) = dg;
+          *reinterpret_cast<bf16x4*>(dp + F) = du;
+        } else {
+          bf16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = (bf16)(RES ? v[e] + (float)la[ii][j][e] : v[e]);
+          *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(out) + (size_t)m * N + n) = o;
+        }
+      }
+    }
+  };
+  if (has_res) {
+    rows4(std::integral_constant<int, 0>{}, std::true_type{});
+    rows4(std::integral_constant<int, 1>{}, std::true_type{});
+  } else {
+    rows4(std::integral_constant<int, 0>{}, std::false_type{});
+    rows4(std::integral_constant<int, 1>{}, std::false_type{});
   }
 }
 

@@ -71,9 +71,33 @@ _PAIR_BWD = __import__("os").environ.get("LIPA_LORA_PAIR_BWD", "1") != "0"
 _DX_C = __import__("os").environ.get("LIPA_LORA_DX_C", "1") != "0"
 
 
+# NF4-aware activation checkpointing: inside a checkpointed layer (its forward AND its backward
+# recompute) the bf16 expansion of each frozen NF4 base is made once per optimizer step and reused —
+# the reference-faithful step (gradient checkpointing + sequential GA micro-steps) otherwise expands
+# every weight 2 × GA times per step instead of once.  The optimizer's step() advances the epoch
+# (optim/adamw.py, parallel/zero.py), dropping the step's copies.  LIPA_CKPT_NF4_CACHE=0: off.
+_CKPT_CACHE = __import__("os").environ.get("LIPA_CKPT_NF4_CACHE", "1") != "0"
+_IN_CKPT = [0]
+_EPOCH = [0]
+
+
+def nf4_cache_advance():
+    """Called by the optimizers at every step: the expanded copies of the finished step are released."""
+    _EPOCH[0] += 1
+
+
 def _nf4_dequant_bf16(q: NF4Weight) -> torch.Tensor:
+    if _CKPT_CACHE and _IN_CKPT[0]:
+        hit = getattr(q, "_lipa_bf16", None)
+        if hit is not None and hit[0] == _EPOCH[0]:
+            return hit[1]
     n, k = q.shape
-    return native().nf4_dequant_fast(q.codes, q.gemv_scales(), n, k)
+    w = native().nf4_dequant_fast(q.codes, q.gemv_scales(), n, k)
+    if _CKPT_CACHE and _IN_CKPT[0]:
+        q._lipa_bf16 = (_EPOCH[0], w)
+    elif getattr(q, "_lipa_bf16", None) is not None:
+        q._lipa_bf16 = None
+    return w
 
 
 @dataclasses.dataclass
@@ -250,15 +274,19 @@ def checkpoint(fn, *args):
     state: list = []
 
     def run(*a):
-        if not state:                      # the forward pass
-            state.append(_KEY[0])
-            return fn(*a)
-        live = _KEY[0]                     # the recompute inside backward
-        _KEY[0] = state[0]
+        _IN_CKPT[0] += 1
         try:
-            return fn(*a)
+            if not state:                      # the forward pass
+                state.append(_KEY[0])
+                return fn(*a)
+            live = _KEY[0]                     # the recompute inside backward
+            _KEY[0] = state[0]
+            try:
+                return fn(*a)
+            finally:
+                _KEY[0] = live
         finally:
-            _KEY[0] = live
+            _IN_CKPT[0] -= 1
 
     if _CKPT_REENTRANT:
         # reentrant form: the first forward runs without building a graph (no saved-tensor pack hooks:

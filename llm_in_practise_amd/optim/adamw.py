@@ -24,6 +24,9 @@ from ..ops import reference as ref
 from ..ops._native import native, use_native
 
 
+from ..ops.linear import nf4_cache_advance  # noqa: E402
+
+
 class FlatParams:
     """Flatten parameters into one fp32 master buffer + one fp32 grad buffer.
 
@@ -181,6 +184,7 @@ class AdamW(_FlatOptimizer):
 
     @torch.no_grad()
     def step(self, closure=None):
+        nf4_cache_advance()
         self.flat.sync_grads()
         self.step_count += 1
         b1, b2 = self.betas
@@ -228,6 +232,7 @@ class AdamW8bit(_FlatOptimizer):
 
     @torch.no_grad()
     def step(self, closure=None):
+        nf4_cache_advance()
         self.flat.sync_grads()
         self.step_count += 1
         b1, b2 = self.betas

@@ -587,6 +587,8 @@ class ZeroEngine:
         self.micro_steps += 1
         if not boundary:
             return
+        from ..ops.linear import nf4_cache_advance
+        nf4_cache_advance()        # the step's NF4 expansions (checkpointed layers) are released
         self._optimizer_step()
         self.global_steps += 1
         if self.lr_scheduler is not None:
