@@ -1,4 +1,4 @@
-"""Frozen-base linear with LoRA fused into the base GEMM (K8) and NF4 dequant-GEMM (K9).
+"""Frozen-base linear with LoRA branches (K8) over NF4 or bf16 bases (K9).
 
 One op covers every projection of the stack:
 
@@ -7,13 +7,18 @@ One op covers every projection of the stack:
 * ``base`` is a bf16 ``[N, K]`` tensor (LoRA / full fine-tune) or an :class:`NF4Weight`
   (QLoRA).  Several projections that share an input (q|k|v, gate|up) are row-concatenated
   into one base and one GEMM; each LoRA branch owns a column range ``[c0, c1)``.
-* On gfx950 the LoRA low-rank product is not a separate GEMM: ``s·x·Aᵀ`` ([T, Σr]) and the
-  block-placed ``B`` ([N, Σr]) enter the MFMA kernel as an extra K-slice of the same tile
-  loop (``gemm_nf4`` / ``gemm_bf16`` in ``csrc/kernels/gemm_*.hip``), and the residual add
-  is the epilogue.  Backward ``dX = dY·deq(W)`` is the transposed-operand variant of the
-  same kernel over a second fragment-native packing of the same NF4 codes, with the LoRA
-  ``(s·dY·B)·A`` term again an extra K-slice when the branch has no dropout (with dropout
-  the counter-RNG mask is regenerated in a fused ``dx += mask·t`` kernel — never stored).
+* What runs at training / prefill sizes (M ≥ 256), the default:
+  - an NF4 base is expanded to bf16 once per call (``nf4_dequant3_k``, HBM speed; inside
+    checkpointed layers once per optimizer step) and the copy is kept for the backward;
+  - the base GEMM is the hand-written one-wave-per-SIMD MFMA kernel ``gemm4w`` (forward x·Wᵀ with
+    the residual in its epilogue; backward dY·W reading W as stored — the transposed-B form);
+  - the LoRA branches run in ``lora.hip``: ``lora_proj2`` (both q/v adapters' s·D(x)·Aᵀ in one pass,
+    keep bits stored), ``lora_apply`` (xa·Bᵀ added into the adapters' column blocks of the GEMM
+    output), and in backward ``lora_proj_pair`` / ``lora_acc_pair`` / ``lora_dx2`` (the LoRA dX term
+    enters the dX GEMM as its C matrix) / ``lora_dA_pair``.
+  ``LIPA_GEMM=lt`` swaps the base GEMMs for direct hipBLASLt calls; decode sizes (M ≤ 16) use the
+  split-K weight-streaming kernels (``skinny.hip``, ``gemv_w4``).
+* The SwiGLU MLP block bypasses this op when it carries no adapters (``ops/mlp.py``).
 
 Reference parity: PEFT ``LoraConfig(r, lora_alpha, lora_dropout, target_modules)``
 (``Fine-Tuning/qwen3-8b-qlora.py:107-114``), scaling = alpha / r.
