@@ -55,6 +55,8 @@ void launch_nf4_dequant(const uint8_t*, const float*, const uint8_t*, const floa
 bool gemm8_supported(int, int, int, int, int);
 bool gemm4w_supported(int, int, int, int, int, bool);
 int gemm4w_plan(int, int, int, bool, int, int, int*);
+void launch_mlora_apply(const void*, int, const void*, const void*, const int64_t*, const void*, int, void*, int, int, int,
+                        int, int, int, hipStream_t);
 void launch_gemm4w_swiglu(const void*, int, const void*, void*, void*, int, int, int, int, hipStream_t);
 void launch_gemm4w_dswiglu(const void*, int, const void*, const void*, void*, int, int, int, int, hipStream_t);
 void launch_gemm4w(const void*, int, const void*, int, const void*, void*, float*, int, int, int, int, bool, int,
@@ -726,6 +728,23 @@ Tensor gemm4w_dswiglu(Tensor dy, Tensor w, Tensor gu) {
   return dgu;
 }
 
+// Multi-adapter LoRA (mlora.hip): y[:, c0:c0+N] += per-row s_a·(x·A_aᵀ)·B_aᵀ, a = ids[row] (0 = base).
+// x [T, K] bf16, A_all [R, K], B_all [N, R] bf16, ids [>= T] int64, seg int32 [n_adapters + 1, 3] =
+// {offset, rank, float bits of the scale}; ranks / offsets multiples of 8, ranks <= 64.
+void mlora_apply(Tensor x, Tensor A, Tensor B, Tensor ids, Tensor seg, Tensor y, int64_t c0) {
+  CHECK_BF16(x); CHECK_BF16(A); CHECK_BF16(B); CHECK_BF16(y);
+  CHECK_CONTIG(A); CHECK_CONTIG(B); CHECK_CONTIG(seg);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && y.dim() == 2 && y.stride(1) == 1, "mlora_apply: 2-D rows");
+  const int64_t T = x.size(0), K = x.size(1), R = A.size(0), N = B.size(0);
+  TORCH_CHECK(A.size(1) == K && B.size(1) == R && y.size(0) == T && c0 >= 0 && c0 + N <= y.size(1) && K % 8 == 0 &&
+                  N % 8 == 0 && R % 8 == 0 && x.stride(0) % 8 == 0 && y.stride(0) % 8 == 0 && c0 % 8 == 0,
+              "mlora_apply: shapes");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.numel() >= T && ids.is_contiguous(), "mlora_apply: ids int64");
+  TORCH_CHECK(seg.scalar_type() == at::kInt && seg.dim() == 2 && seg.size(1) == 3, "mlora_apply: seg [n, 3] int32");
+  launch_mlora_apply(x.data_ptr(), x.stride(0), A.data_ptr(), B.data_ptr(), ids.data_ptr<int64_t>(), seg.data_ptr(),
+                     (int)seg.size(0), y.data_ptr(), y.stride(0), (int)c0, (int)T, (int)K, (int)N, (int)R, stream());
+}
+
 // y = x·wᵀ (+ LoRA K-slice) (+ residual) for a frozen bf16 base: the hand-written 8-phase MFMA GEMM
 // (gemm8.hip) whenever the shape / strides allow it, library GEMM otherwise.
 Tensor gemm_bf16(Tensor x, Tensor w, optional<Tensor> ext_a, optional<Tensor> ext_b, optional<Tensor> residual) {
@@ -1386,6 +1405,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm4w", &gemm4w, py::arg("x"), py::arg("w"), py::arg("residual") = py::none(), py::arg("splits") = 0,
         py::arg("bt") = false, py::arg("bn") = 0);
   m.def("gemm4w_swiglu", &gemm4w_swiglu);
+  m.def("mlora_apply", &mlora_apply);
   m.def("gemm4w_dswiglu", &gemm4w_dswiglu);
   m.def("gemm_nf4_t", &gemm_nf4_t);
   m.def("gemm_bf16", &gemm_bf16);

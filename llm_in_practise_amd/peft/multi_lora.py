@@ -9,7 +9,9 @@ adapters' LoRA factors are stacked once at load time:
     A_all [Σr, K]   (adapter a owns rows [o_a, o_a + r_a))
     B_all [N, Σr]   (the matching columns)
 
-and a step computes ``y += ((x · A_allᵀ) ⊙ S[ids]) · B_allᵀ`` where ``S`` is a tiny
+and on the GPU one segment kernel per projection (``csrc/kernels/mlora.hip``) computes, for every
+row, only its own adapter's ``s_a·(x·A_aᵀ)·B_aᵀ`` — ``r_a·(K + N)`` MACs per row however many adapters
+are loaded.  The portable form (CPU, odd ranks) computes ``y += ((x · A_allᵀ) ⊙ S[ids]) · B_allᵀ`` where ``S`` is a tiny
 ``[n_adapters + 1, Σr]`` table holding ``alpha_a / r_a`` on adapter a's columns (row 0 = the base,
 all zeros) and ``ids`` the per-row adapter index.  That is the same low-rank K-slice the fused
 training kernels use, segment-by-adapter through a column mask instead of a gather, so the step
@@ -32,8 +34,17 @@ import torch.nn as nn
 class MultiLoraSlot:
     """Stacked LoRA factors of every adapter for one projection."""
 
-    def __init__(self, mgr: "MultiLoraManager", a_all: torch.Tensor, b_all: torch.Tensor, col_scale: torch.Tensor):
+    def __init__(self, mgr: "MultiLoraManager", a_all: torch.Tensor, b_all: torch.Tensor, col_scale: torch.Tensor,
+                 seg: list[tuple[int, int, float]] | None = None):
         self.mgr, self.A, self.B, self.col_scale = mgr, a_all, b_all, col_scale
+        # per-adapter (offset, rank, scale) for the segment kernel (csrc/kernels/mlora.hip): each row
+        # computes only its own adapter's rank-r_a term — cost independent of how many are loaded
+        self.seg = None
+        if seg is not None and a_all.is_cuda and all(r % 8 == 0 and r <= 64 and o % 8 == 0 for o, r, _ in seg) \
+                and a_all.shape[0] % 8 == 0 and a_all.shape[1] % 8 == 0 and b_all.shape[0] % 8 == 0:
+            import struct
+            rows = [[o, r, struct.unpack("<i", struct.pack("<f", float(sc)))[0]] for o, r, sc in seg]
+            self.seg = torch.tensor(rows, dtype=torch.int32, device=a_all.device)
 
     def delta(self, x: torch.Tensor) -> torch.Tensor:
         ids = self.mgr.row_ids(x.shape[0])
@@ -42,6 +53,11 @@ class MultiLoraSlot:
         return xa @ self.B.t()                                           # [T, N]
 
     def apply_(self, x: torch.Tensor, y: torch.Tensor, c0: int = 0) -> torch.Tensor:
+        if (self.seg is not None and x.dtype == torch.bfloat16 and y.dtype == torch.bfloat16 and x.stride(-1) == 1
+                and y.stride(-1) == 1 and x.stride(0) % 8 == 0 and y.stride(0) % 8 == 0 and c0 % 8 == 0):
+            from ..ops._native import native
+            native().mlora_apply(x, self.A, self.B, self.mgr.row_ids(x.shape[0]), self.seg, y, c0)
+            return y
         d = self.delta(x).to(y.dtype)
         if c0 == 0 and d.shape[1] == y.shape[1]:
             return y.add_(d)
@@ -96,15 +112,17 @@ class MultiLoraManager:
             a_all = torch.zeros(R, K, dtype=dtype, device=dev)
             b_all = torch.zeros(N, R, dtype=dtype, device=dev)
             col_scale = torch.zeros(len(self.names) + 1, R, dtype=dtype, device=dev)
+            seg = [(0, 0, 0.0)]                     # adapter 0 = the bare base
             o = 0
             for i, (ab, r, s) in enumerate(zip(parts, cols, scales)):
+                seg.append((o, r, s))
                 if ab is None:
                     continue
                 a_all[o:o + r] = ab[0].to(dev, dtype)
                 b_all[:, o:o + r] = ab[1].to(dev, dtype)
                 col_scale[i + 1, o:o + r] = s
                 o += r
-            slot = MultiLoraSlot(self, a_all, b_all, col_scale)
+            slot = MultiLoraSlot(self, a_all, b_all, col_scale, seg)
             leaf._mlora = slot
             self.slots[tname] = slot
         self._buf = torch.zeros(max_rows, dtype=torch.long, device=dev)   # per-row adapter index

@@ -831,3 +831,39 @@ def test_embedding_out_of_range_id_raises(native_ext):
         with pytest.raises(IndexError, match="out of range"):
             check_ids()
         emb(torch.zeros(1, 4, dtype=torch.long, device=DEV))   # word was reset
+
+
+# ----------------------------------------------------------------------------- multi-LoRA segment kernel
+def test_mlora_apply_per_row_adapter(native_ext):
+    """y[:, c0:c0+N] += s_a·(x·A_aᵀ)·B_aᵀ for each row's own adapter a (0 = base: untouched), 8 adapters
+    of ranks 8/16/64 stacked; vs per-adapter fp32"""
+    import struct
+    torch.manual_seed(5)
+    T, K, N, c0 = 37, 512, 768, 256
+    ranks = [8, 16, 64, 8, 16, 8, 64, 8]
+    scales = [2.0, 1.0, 0.5, 2.0, 1.0, 2.0, 0.25, 2.0]
+    R = sum(ranks)
+    A = (0.05 * torch.randn(R, K, device=DEV)).to(torch.bfloat16)
+    B = (0.05 * torch.randn(N, R, device=DEV)).to(torch.bfloat16)
+    seg, o = [[0, 0, 0]], 0
+    for r, s in zip(ranks, scales):
+        seg.append([o, r, struct.unpack("<i", struct.pack("<f", s))[0]])
+        o += r
+    seg = torch.tensor(seg, dtype=torch.int32, device=DEV)
+    ids = torch.randint(0, len(ranks) + 1, (T,), device=DEV)
+    x = torch.randn(T, K, device=DEV).to(torch.bfloat16)
+    y = torch.randn(T, c0 + N + 64, device=DEV).to(torch.bfloat16)
+    want = y.float().clone()
+    offs = [0] + list(torch.tensor(ranks).cumsum(0).tolist())
+    for t in range(T):
+        a = int(ids[t])
+        if a == 0:
+            continue
+        o0, r = offs[a - 1], ranks[a - 1]
+        xa = (x[t].float() @ A[o0:o0 + r].float().t()) * scales[a - 1]
+        want[t, c0:c0 + N] += xa @ B[:, o0:o0 + r].float().t()
+    native_ext.mlora_apply(x, A, B, ids, seg, y, c0)
+    assert rel_err(y, want) < 1e-2
+    base_rows = ids == 0
+    assert torch.equal(y[base_rows].float(), want[base_rows])           # base rows untouched
+    assert torch.equal(y[:, :c0].float(), want[:, :c0])                 # other columns untouched
