@@ -59,7 +59,7 @@ void launch_mlora_apply(const void*, int, const void*, const void*, const int64_
                         int, int, int, hipStream_t);
 void launch_gemm4w_swiglu(const void*, int, const void*, void*, void*, int, int, int, int, hipStream_t);
 void launch_gemm4w_dswiglu(const void*, int, const void*, const void*, void*, int, int, int, int, hipStream_t);
-void launch_gemm4w(const void*, int, const void*, int, const void*, void*, float*, int, int, int, int, bool, int,
+void launch_gemm4w(const void*, int, const void*, int, const void*, void*, float*, int*, int, int, int, int, bool, int,
                    hipStream_t);
 int gemm8_splits(int, int, int);
 void launch_gemm8(const void*, int, const void*, int, const void*, const void*, int, const void*, void*, float*, int, int,
@@ -658,6 +658,17 @@ Tensor gemm8(Tensor x, Tensor w, optional<Tensor> ext_a, optional<Tensor> ext_b,
              int64_t splits);
 
 
+// Split-K tickets of gemm4w (one int per output tile): zeroed once when allocated, reset by each
+// tile's last-arriving split; one buffer per (device, stream) so concurrent streams never share.
+static int* split_tickets(const at::Device& dev, int64_t tiles) {
+  static std::map<std::pair<int, hipStream_t>, Tensor> bufs;
+  auto key = std::make_pair((int)dev.index(), stream());
+  Tensor& t = bufs[key];
+  if (!t.defined() || t.numel() < tiles)
+    t = at::zeros({std::max<int64_t>(tiles, 4096)}, at::TensorOptions().device(dev).dtype(at::kInt));
+  return t.data_ptr<int>();
+}
+
 // y = x·wᵀ (+ residual) through the one-wave-per-SIMD AGPR-accumulator MFMA GEMM (gemm4w.hip);
 // x [M, K] (row stride any multiple of 8), w [N, K] contiguous rows.  bt: y = x·w with w [K, N]
 // (the dX = dY·W of a frozen [N_w, K_w] weight, no transpose copy).  splits <= 0: auto split-K;
@@ -682,9 +693,14 @@ Tensor gemm4w(Tensor x, Tensor w, optional<Tensor> residual, int64_t splits, boo
   const int sp = gemm4w_plan(M, N, K, bt, (int)bn, (int)splits, &bn_used);
   auto y = at::empty({M, N}, x.options());
   Tensor ws;
-  if (sp > 1) ws = at::empty({sp, M, N}, x.options().dtype(at::kFloat));
+  int* cnt = nullptr;
+  if (sp > 1) {
+    ws = at::empty({sp, M, N}, x.options().dtype(at::kFloat));
+    const int64_t tiles = ((M + 255) / 256) * ((N + bn_used - 1) / bn_used);
+    cnt = split_tickets(x.device(), tiles);
+  }
   launch_gemm4w(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), res, y.data_ptr(),
-                sp > 1 ? ws.data_ptr<float>() : nullptr, M, N, K, sp, bt, bn_used, stream());
+                sp > 1 ? ws.data_ptr<float>() : nullptr, cnt, M, N, K, sp, bt, bn_used, stream());
   return y;
 }
 

@@ -29,7 +29,8 @@
 //    fragment (a 32-lane half reads rows {0-3, 8-11} (+4) of a 16-row group: 8 distinct h → conflict-
 //    free).  Every swizzle is applied on the DMA SOURCE address (the LDS side is lane-linear).
 //  * XCD-aware tile order: the m-tiles of one weight panel are consecutive ids and share an XCD's L2.
-//  * split-K (grids still smaller than the chip): fp32 slabs + one reduce kernel (+ residual).
+//  * split-K (grids still smaller than the chip): fp32 slabs reduced in the same launch by the tile's
+//    last-arriving split (agent-scope release / ticket / acquire), which also runs the epilogue.
 #include <type_traits>
 
 #include "common.h"
@@ -158,7 +159,8 @@ template <int BN, bool BT, bool SPLIT, int EPI = 0>
 __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, int lda, const bf16* __restrict__ B,
                                                   int ldb, const bf16* __restrict__ residual, void* __restrict__ out,
                                                   int M, int N, int K, int splits, const bf16* __restrict__ aux,
-                                                  bf16* __restrict__ aux_out, int F) {
+                                                  bf16* __restrict__ aux_out, int F, float* __restrict__ ws,
+                                                  int* __restrict__ cnt) {
   static_assert(EPI == 0 || !SPLIT, "fused epilogues run on whole-K tiles");
   static_assert(EPI != 1 || !BT, "SwiGLU forward epilogue: NT only");
   static_assert(EPI != 2 || BT, "SwiGLU backward epilogue: the transposed-B dX only");
@@ -364,6 +366,13 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
     return;
   }
   if constexpr (SPLIT) {
+    // Split-K, reduced in this launch by the LAST arriving split of the tile
+    // (cdna_hip_programming.md §5 "Projection GEMM" item 2): every split stores its fp32 slab, drains
+    // it (vmcnt(0) in every wave, barrier), and one lane releases at agent scope and takes a ticket;
+    // the split that draws splits-1 acquires at agent scope, adds the other slabs to its registers and
+    // runs the normal bf16 epilogue (residual included).  Correct for any placement of a tile's
+    // splits over XCDs; the ticket is reset by the last arriver (zeroed once at allocation).
+    float* wsf = ws;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int m = m0 + wr * 128 + i * 16 + (lane & 15);
@@ -371,21 +380,44 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         const int n = n0 + wc * (BN / 2) + j * 16 + 4 * (lane >> 4);
-        if (n < N) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + ((size_t)sp * M + m) * N + n) = acc[i][j];
+        if (n < N) *reinterpret_cast<f32x4*>(wsf + ((size_t)sp * M + m) * N + n) = acc[i][j];
       }
     }
-    return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(lds);   // the one LDS array (free: every DMA has landed)
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int old = __hip_atomic_fetch_add(cnt + tid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == splits - 1;
+      if (last) {
+        __hip_atomic_store(cnt + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *flag = last;
+    }
+    __syncthreads();
+    if (*reinterpret_cast<volatile int*>(flag) == 0) return;
   }
   // Epilogues that read global memory (residual; EPI 2's g / u) issue every load of four accumulator
   // rows before the first use, from clamped (always valid) addresses — one latency per four rows, not
   // one per 16×16 block (a load behind a per-block bounds branch waits vmcnt(0) each time)
   const bool has_res = EPI == 0 && residual != nullptr;
-  auto rows4 = [&](auto hh_c, auto res_c) {
-    constexpr int i0 = 4 * decltype(hh_c)::value;
+  // rows per chunk: 4 (2 when a 256-wide tile also sums split-K slabs: register budget)
+  constexpr int RC = (SPLIT && NB >= 6) ? 2 : 4;
+  auto rows = [&](auto hh_c, auto res_c) {
+    constexpr int i0 = RC * decltype(hh_c)::value;
     constexpr bool RES = decltype(res_c)::value;
-    bf16x4 la[4][8], lb[4][8];
+    bf16x4 la[RC][8], lb[RC][8];
+    f32x4 tot[RC][8];
 #pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
+    for (int ii = 0; ii < RC; ++ii)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) tot[ii][j] = acc[i0 + ii][j];
+#pragma unroll
+    for (int ii = 0; ii < RC; ++ii) {
       const int m = min(m0 + wr * 128 + (i0 + ii) * 16 + (lane & 15), M - 1);
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
@@ -399,15 +431,34 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
         }
       }
     }
+    if constexpr (SPLIT) {   // the last arriver adds the other splits' slabs
+      for (int s2 = 0; s2 < splits; ++s2) {
+        if (s2 == sp) continue;
+        f32x4 pv[RC][8];
 #pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
+        for (int ii = 0; ii < RC; ++ii) {
+          const int m = min(m0 + wr * 128 + (i0 + ii) * 16 + (lane & 15), M - 1);
+#pragma unroll
+          for (int j = 0; j < NB; ++j) {
+            const int n = min(n0 + wc * (BN / 2) + j * 16 + 4 * (lane >> 4), N - 4);
+            pv[ii][j] = *reinterpret_cast<const f32x4*>(ws + ((size_t)s2 * M + m) * N + n);
+          }
+        }
+#pragma unroll
+        for (int ii = 0; ii < RC; ++ii)
+#pragma unroll
+          for (int j = 0; j < NB; ++j) tot[ii][j] += pv[ii][j];
+      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < RC; ++ii) {
       const int m = m0 + wr * 128 + (i0 + ii) * 16 + (lane & 15);
       if (m >= M) continue;
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         const int n = n0 + wc * (BN / 2) + j * 16 + 4 * (lane >> 4);
         if (n >= N) continue;
-        const f32x4 v = acc[i0 + ii][j];
+        const f32x4 v = tot[ii][j];
         if constexpr (EPI == 2) {
           bf16x4 dg, du;
 #pragma unroll
@@ -430,32 +481,9 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
     }
   };
   if (has_res) {
-    rows4(std::integral_constant<int, 0>{}, std::true_type{});
-    rows4(std::integral_constant<int, 1>{}, std::true_type{});
+    Unroll<0, 8 / RC>::run([&](auto hc) { rows(hc, std::true_type{}); });
   } else {
-    rows4(std::integral_constant<int, 0>{}, std::false_type{});
-    rows4(std::integral_constant<int, 1>{}, std::false_type{});
-  }
-}
-
-__global__ __launch_bounds__(256) void splitk_sum_k(const float* __restrict__ ws, const bf16* __restrict__ residual,
-                                                    bf16* __restrict__ out, size_t MN, int splits) {
-  for (size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 8; i < MN; i += (size_t)gridDim.x * 256 * 8) {
-    float v[8];
-    load8(ws + i, v);
-    for (int s = 1; s < splits; ++s) {
-      float u[8];
-      load8(ws + (size_t)s * MN + i, u);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += u[j];
-    }
-    if (residual) {
-      float r[8];
-      load8(residual + i, r);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += r[j];
-    }
-    store8(out + i, v);
+    Unroll<0, 8 / RC>::run([&](auto hc) { rows(hc, std::false_type{}); });
   }
 }
 
@@ -522,18 +550,19 @@ int gemm4w_plan(int M, int N, int K, bool bt, int bn, int splits, int* bn_out) {
   return c.splits;
 }
 
-void launch_gemm4w(const void* A, int lda, const void* B, int ldb, const void* residual, void* out, float* ws, int M,
-                   int N, int K, int splits, bool bt, int bn, hipStream_t st) {
+// ws: splits·M·N fp32 slabs, cnt: one zero-initialised int per tile (both only when splits > 1)
+void launch_gemm4w(const void* A, int lda, const void* B, int ldb, const void* residual, void* out, float* ws,
+                   int* cnt, int M, int N, int K, int splits, bool bt, int bn, hipStream_t st) {
   // callers pass the (bn, splits) that gemm4w_plan returned
   const int tiles = tiles_of(M, N, bn);
   const bool split = splits > 1;
   const bf16* a = (const bf16*)A;
   const bf16* b = (const bf16*)B;
-  const bf16* r = split ? nullptr : (const bf16*)residual;
-  void* o = split ? (void*)ws : out;
+  const bf16* r = (const bf16*)residual;
+  void* o = out;
   const int grid = tiles * (split ? splits : 1), sp = split ? splits : 1;
 #define G4W(BN_, BT_, SP_) \
-  gemm4w_k<BN_, BT_, SP_><<<grid, NT, 0, st>>>(a, lda, b, ldb, r, o, M, N, K, sp, nullptr, nullptr, 0)
+  gemm4w_k<BN_, BT_, SP_><<<grid, NT, 0, st>>>(a, lda, b, ldb, r, o, M, N, K, sp, nullptr, nullptr, 0, ws, cnt)
   if (bn == 256) {
     if (bt) { if (split) G4W(256, true, true); else G4W(256, true, false); }
     else { if (split) G4W(256, false, true); else G4W(256, false, false); }
@@ -544,11 +573,6 @@ void launch_gemm4w(const void* A, int lda, const void* B, int ldb, const void* r
     else { if (split) G4W(128, false, true); else G4W(128, false, false); }
   }
 #undef G4W
-  if (split) {
-    const size_t MN = (size_t)M * N;
-    const int blocks = (int)std::min<size_t>((MN / 8 + 255) / 256, 2048);
-    splitk_sum_k<<<blocks, 256, 0, st>>>(ws, (const bf16*)residual, (bf16*)out, MN, splits);
-  }
   LIPA_CHECK_LAUNCH();
 }
 
@@ -560,7 +584,8 @@ void launch_gemm4w_swiglu(const void* X, int ldx, const void* W, void* gu, void*
   const bf16* a = (const bf16*)X;
   const bf16* b = (const bf16*)W;
 #define G4S(BN_) \
-  gemm4w_k<BN_, false, false, 1><<<tiles, NT, 0, st>>>(a, ldx, b, K, nullptr, gu, M, N, K, 1, nullptr, (bf16*)h, F)
+  gemm4w_k<BN_, false, false, 1><<<tiles, NT, 0, st>>>(a, ldx, b, K, nullptr, gu, M, N, K, 1, nullptr, (bf16*)h, F, \
+                                                       nullptr, nullptr)
   if (bn == 256) G4S(256);
   else if (bn == 192) G4S(192);
   else G4S(128);
@@ -576,9 +601,9 @@ void launch_gemm4w_dswiglu(const void* DY, int lddy, const void* W, const void* 
   const bf16* b = (const bf16*)W;
   if (bn == 256)
     gemm4w_k<256, true, false, 2><<<tiles, NT, 0, st>>>(a, lddy, b, F, nullptr, dgu, M, F, Nw, 1, (const bf16*)gu,
-                                                        nullptr, F);
+                                                        nullptr, F, nullptr, nullptr);
   else
     gemm4w_k<128, true, false, 2><<<tiles, NT, 0, st>>>(a, lddy, b, F, nullptr, dgu, M, F, Nw, 1, (const bf16*)gu,
-                                                        nullptr, F);
+                                                        nullptr, F, nullptr, nullptr);
   LIPA_CHECK_LAUNCH();
 }
