@@ -697,7 +697,13 @@ Tensor gemm4w(Tensor x, Tensor w, optional<Tensor> residual, int64_t splits, boo
   if (sp > 1) {
     ws = at::empty({sp, M, N}, x.options().dtype(at::kFloat));
     const int64_t tiles = ((M + 255) / 256) * ((N + bn_used - 1) / bn_used);
-    cnt = split_tickets(x.device(), tiles);
+    static const bool inlaunch = [] {
+      // measured 1.1-1.2 ms/step SLOWER than the separate reduce launch (profiles/r3/README.md): the
+      // last arriver's serial slab read + the agent fences sit on every split tile's critical path
+      const char* e = getenv("LIPA_GEMM4W_INLAUNCH_REDUCE");
+      return e && atoi(e) != 0;
+    }();
+    if (inlaunch) cnt = split_tickets(x.device(), tiles);
   }
   launch_gemm4w(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), res, y.data_ptr(),
                 sp > 1 ? ws.data_ptr<float>() : nullptr, cnt, M, N, K, sp, bt, bn_used, stream());

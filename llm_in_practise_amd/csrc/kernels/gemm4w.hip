@@ -29,8 +29,9 @@
 //    fragment (a 32-lane half reads rows {0-3, 8-11} (+4) of a 16-row group: 8 distinct h → conflict-
 //    free).  Every swizzle is applied on the DMA SOURCE address (the LDS side is lane-linear).
 //  * XCD-aware tile order: the m-tiles of one weight panel are consecutive ids and share an XCD's L2.
-//  * split-K (grids still smaller than the chip): fp32 slabs reduced in the same launch by the tile's
-//    last-arriving split (agent-scope release / ticket / acquire), which also runs the epilogue.
+//  * split-K (grids still smaller than the chip): fp32 slabs + one reduce launch (+ residual); the
+//    in-launch form (the tile's last-arriving split sums the slabs after an agent release / ticket /
+//    acquire) is kept behind LIPA_GEMM4W_INLAUNCH_REDUCE=1 — measured 1.1 ms/step slower.
 #include <type_traits>
 
 #include "common.h"
@@ -383,6 +384,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
         if (n < N) *reinterpret_cast<f32x4*>(wsf + ((size_t)sp * M + m) * N + n) = acc[i][j];
       }
     }
+    if (cnt == nullptr) return;                // slabs only: splitk_sum_k reduces them
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int* flag = reinterpret_cast<int*>(lds);   // the one LDS array (free: every DMA has landed)
@@ -487,6 +489,28 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   }
 }
 
+__global__ __launch_bounds__(256) void splitk_sum_k(const float* __restrict__ ws, const bf16* __restrict__ residual,
+                                                    bf16* __restrict__ out, size_t MN, int splits) {
+  for (size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 8; i < MN; i += (size_t)gridDim.x * 256 * 8) {
+    float v[8];
+    load8(ws + i, v);
+    for (int s = 1; s < splits; ++s) {
+      float u[8];
+      load8(ws + (size_t)s * MN + i, u);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += u[j];
+    }
+    if (residual) {
+      float r[8];
+      load8(residual + i, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += r[j];
+    }
+    store8(out + i, v);
+  }
+}
+
+
 int tiles_of(int M, int N, int bn) { return ((M + BM - 1) / BM) * ((N + bn - 1) / bn); }
 
 }  // namespace
@@ -550,7 +574,8 @@ int gemm4w_plan(int M, int N, int K, bool bt, int bn, int splits, int* bn_out) {
   return c.splits;
 }
 
-// ws: splits·M·N fp32 slabs, cnt: one zero-initialised int per tile (both only when splits > 1)
+// ws: splits·M·N fp32 slabs, cnt: one zero-initialised int per tile (both only when splits > 1);
+// cnt == nullptr: the slabs are summed by a separate splitk_sum_k launch instead of the last arriver
 void launch_gemm4w(const void* A, int lda, const void* B, int ldb, const void* residual, void* out, float* ws,
                    int* cnt, int M, int N, int K, int splits, bool bt, int bn, hipStream_t st) {
   // callers pass the (bn, splits) that gemm4w_plan returned
@@ -573,6 +598,11 @@ void launch_gemm4w(const void* A, int lda, const void* B, int ldb, const void* r
     else { if (split) G4W(128, false, true); else G4W(128, false, false); }
   }
 #undef G4W
+  if (split && cnt == nullptr) {
+    const size_t MN = (size_t)M * N;
+    const int blocks = (int)std::min<size_t>((MN / 8 + 255) / 256, 2048);
+    splitk_sum_k<<<blocks, 256, 0, st>>>(ws, (const bf16*)residual, (bf16*)out, MN, splits);
+  }
   LIPA_CHECK_LAUNCH();
 }
 
