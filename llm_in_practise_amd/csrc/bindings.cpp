@@ -54,13 +54,14 @@ void launch_nf4_dequant(const uint8_t*, const float*, const uint8_t*, const floa
                         size_t, hipStream_t);
 bool gemm8_supported(int, int, int, int, int);
 bool gemm4w_supported(int, int, int, int, int, bool);
-int gemm4w_plan(int, int, int, bool, int, int, int*);
+int gemm4w_plan(int, int, int, bool, int, int, int*, int, int*);
+int gemm4w_tiles(int, int, int, int);
 void launch_mlora_apply(const void*, int, const void*, const void*, const int64_t*, const void*, int, void*, int, int, int,
                         int, int, int, hipStream_t);
-void launch_gemm4w_swiglu(const void*, int, const void*, void*, void*, int, int, int, int, hipStream_t);
-void launch_gemm4w_dswiglu(const void*, int, const void*, const void*, void*, int, int, int, int, hipStream_t);
+void launch_gemm4w_swiglu(const void*, int, const void*, void*, void*, int, int, int, int, int, hipStream_t);
+void launch_gemm4w_dswiglu(const void*, int, const void*, const void*, void*, int, int, int, int, int, hipStream_t);
 void launch_gemm4w(const void*, int, const void*, int, const void*, void*, float*, int*, int, int, int, int, bool, int,
-                   hipStream_t);
+                   int, hipStream_t);
 int gemm8_splits(int, int, int);
 void launch_gemm8(const void*, int, const void*, int, const void*, const void*, int, const void*, void*, float*, int, int,
                   int, int, hipStream_t);
@@ -673,7 +674,7 @@ static int* split_tickets(const at::Device& dev, int64_t tiles) {
 // x [M, K] (row stride any multiple of 8), w [N, K] contiguous rows.  bt: y = x·w with w [K, N]
 // (the dX = dY·W of a frozen [N_w, K_w] weight, no transpose copy).  splits <= 0: auto split-K;
 // bn: tile width 128 / 256 / 192 (NT only), 0 = auto
-Tensor gemm4w(Tensor x, Tensor w, optional<Tensor> residual, int64_t splits, bool bt, int64_t bn) {
+Tensor gemm4w(Tensor x, Tensor w, optional<Tensor> residual, int64_t splits, bool bt, int64_t bn, int64_t bm) {
   CHECK_BF16(x);
   CHECK_BF16(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1, "gemm4w: 2-D, unit inner stride");
@@ -689,14 +690,15 @@ Tensor gemm4w(Tensor x, Tensor w, optional<Tensor> residual, int64_t splits, boo
     res = residual->data_ptr();
   }
   TORCH_CHECK(bn == 0 || bn == 128 || bn == 256 || (bn == 192 && !bt), "gemm4w: bn 0 / 128 / 256 / 192 (not bt)");
-  int bn_used = 0;
-  const int sp = gemm4w_plan(M, N, K, bt, (int)bn, (int)splits, &bn_used);
+  TORCH_CHECK(bm == 0 || bm == 128 || bm == 256, "gemm4w: bm 0 / 128 / 256");
+  int bn_used = 0, bm_used = 0;
+  const int sp = gemm4w_plan(M, N, K, bt, (int)bn, (int)splits, &bn_used, (int)bm, &bm_used);
   auto y = at::empty({M, N}, x.options());
   Tensor ws;
   int* cnt = nullptr;
   if (sp > 1) {
     ws = at::empty({sp, M, N}, x.options().dtype(at::kFloat));
-    const int64_t tiles = ((M + 255) / 256) * ((N + bn_used - 1) / bn_used);
+    const int64_t tiles = gemm4w_tiles(M, N, bm_used, bn_used);
     static const bool inlaunch = [] {
       // measured 1.1-1.2 ms/step SLOWER than the separate reduce launch (profiles/r3/README.md): the
       // last arriver's serial slab read + the agent fences sit on every split tile's critical path
@@ -706,7 +708,7 @@ Tensor gemm4w(Tensor x, Tensor w, optional<Tensor> residual, int64_t splits, boo
     if (inlaunch) cnt = split_tickets(x.device(), tiles);
   }
   launch_gemm4w(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), res, y.data_ptr(),
-                sp > 1 ? ws.data_ptr<float>() : nullptr, cnt, M, N, K, sp, bt, bn_used, stream());
+                sp > 1 ? ws.data_ptr<float>() : nullptr, cnt, M, N, K, sp, bt, bn_used, bm_used, stream());
   return y;
 }
 
@@ -722,11 +724,11 @@ std::vector<Tensor> gemm4w_swiglu(Tensor x, Tensor w) {
   TORCH_CHECK(w.size(0) == 2 * F && F % 16 == 0 && gemm4w_supported(M, 2 * F, K, x.stride(0), K, false) &&
                   reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
               "gemm4w_swiglu: unsupported shape / alignment");
-  int bn = 0;
-  gemm4w_plan(M, 2 * F, K, false, 0, 1, &bn);
+  int bn = 0, bm = 0;
+  gemm4w_plan(M, 2 * F, K, false, 0, 1, &bn, 0, &bm);
   auto gu = at::empty({M, 2 * F}, x.options());
   auto h = at::empty({M, F}, x.options());
-  launch_gemm4w_swiglu(x.data_ptr(), x.stride(0), w.data_ptr(), gu.data_ptr(), h.data_ptr(), M, F, K, bn, stream());
+  launch_gemm4w_swiglu(x.data_ptr(), x.stride(0), w.data_ptr(), gu.data_ptr(), h.data_ptr(), M, F, K, bn, bm, stream());
   return {gu, h};
 }
 
@@ -742,10 +744,10 @@ Tensor gemm4w_dswiglu(Tensor dy, Tensor w, Tensor gu) {
                   gemm4w_supported(M, F, Nw, dy.stride(0), F, true) &&
                   reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
               "gemm4w_dswiglu: unsupported shape / alignment");
-  int bn = 0;
-  gemm4w_plan(M, F, Nw, true, 0, 1, &bn);
+  int bn = 0, bm = 0;
+  gemm4w_plan(M, F, Nw, true, 0, 1, &bn, 0, &bm);
   auto dgu = at::empty({M, 2 * F}, dy.options());
-  launch_gemm4w_dswiglu(dy.data_ptr(), dy.stride(0), w.data_ptr(), gu.data_ptr(), dgu.data_ptr(), M, F, Nw, bn,
+  launch_gemm4w_dswiglu(dy.data_ptr(), dy.stride(0), w.data_ptr(), gu.data_ptr(), dgu.data_ptr(), M, F, Nw, bn, bm,
                         stream());
   return dgu;
 }
@@ -1425,7 +1427,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nf4", &gemm_nf4);
   m.def("gemm8", &gemm8);
   m.def("gemm4w", &gemm4w, py::arg("x"), py::arg("w"), py::arg("residual") = py::none(), py::arg("splits") = 0,
-        py::arg("bt") = false, py::arg("bn") = 0);
+        py::arg("bt") = false, py::arg("bn") = 0, py::arg("bm") = 0);
   m.def("gemm4w_swiglu", &gemm4w_swiglu);
   m.def("mlora_apply", &mlora_apply);
   m.def("gemm4w_dswiglu", &gemm4w_dswiglu);

@@ -44,8 +44,7 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
-constexpr int BM = 64 * 4, BK = 64, NT = 256;
-constexpr int IMG_A = 32768;   // 256 rows × 64 k bf16
+constexpr int BK = 64, NT = 256;
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint64_t bytes) {
   const uint64_t p = reinterpret_cast<uint64_t>(base);
@@ -107,42 +106,54 @@ struct Unroll<N, N> {
   __device__ __forceinline__ static void run(F&&) {}
 };
 
-// Per-BN schedule tables: MFMA order of a K-half (shells of max(i, j), then the rows i ≥ NB) and the
-// fragment-read order (a0 b0 a1 b1 …, then the remaining a's)
-template <int NB>
+// Per-tile schedule tables (NA a-fragments × NB b-fragments per wave and K-half): MFMA order of a
+// K-half (shells of max(i, j), then the remaining rows / columns) and the fragment-read order
+// (a0 b0 a1 b1 …, then the remaining a's or b's) — MFMA k waits only on reads issued well before it.
+template <int NA, int NB>
 struct Sched {
-  int i[8 * NB], j[8 * NB];
-  int rd_a[8 + NB], rd_i[8 + NB];   // read item r: a fragment? index
+  int i[NA * NB], j[NA * NB];
+  int rd_a[NA + NB], rd_i[NA + NB];   // read item r: a fragment? index
 };
-template <int NB>
-constexpr Sched<NB> make_sched() {
-  Sched<NB> o{};
+template <int NA, int NB>
+constexpr Sched<NA, NB> make_sched() {
+  Sched<NA, NB> o{};
+  constexpr int S = NA < NB ? NA : NB;
   int k = 0;
-  for (int s = 0; s < NB; ++s) {
+  for (int s = 0; s < S; ++s) {
     for (int j = 0; j <= s; ++j) { o.i[k] = s; o.j[k] = j; ++k; }
     for (int i = 0; i < s; ++i) { o.i[k] = i; o.j[k] = s; ++k; }
   }
-  for (int i = NB; i < 8; ++i)
+  for (int i = S; i < NA; ++i)
     for (int j = 0; j < NB; ++j) { o.i[k] = i; o.j[k] = j; ++k; }
+  for (int j = S; j < NB; ++j)
+    for (int i = 0; i < S; ++i) { o.i[k] = i; o.j[k] = j; ++k; }
   int r = 0;
-  for (int s = 0; s < NB; ++s) {
+  for (int s = 0; s < S; ++s) {
     o.rd_a[r] = 1; o.rd_i[r] = s; ++r;
     o.rd_a[r] = 0; o.rd_i[r] = s; ++r;
   }
-  for (int i = NB; i < 8; ++i) { o.rd_a[r] = 1; o.rd_i[r] = i; ++r; }
+  for (int i = S; i < NA; ++i) { o.rd_a[r] = 1; o.rd_i[r] = i; ++r; }
+  for (int j = S; j < NB; ++j) { o.rd_a[r] = 0; o.rd_i[r] = j; ++r; }
   return o;
 }
-constexpr Sched<8> kSched8 = make_sched<8>();
-constexpr Sched<4> kSched4 = make_sched<4>();
-constexpr Sched<6> kSched6 = make_sched<6>();
-template <int NB>
-__host__ __device__ constexpr const Sched<NB>& sched_of();
-template <>
-__host__ __device__ constexpr const Sched<8>& sched_of<8>() { return kSched8; }
-template <>
-__host__ __device__ constexpr const Sched<4>& sched_of<4>() { return kSched4; }
-template <>
-__host__ __device__ constexpr const Sched<6>& sched_of<6>() { return kSched6; }
+constexpr Sched<8, 8> kSched88 = make_sched<8, 8>();
+constexpr Sched<8, 4> kSched84 = make_sched<8, 4>();
+constexpr Sched<8, 6> kSched86 = make_sched<8, 6>();
+constexpr Sched<4, 8> kSched48 = make_sched<4, 8>();
+constexpr Sched<4, 4> kSched44 = make_sched<4, 4>();
+constexpr Sched<4, 6> kSched46 = make_sched<4, 6>();
+template <int NA, int NB>
+__host__ __device__ constexpr const Sched<NA, NB>& sched_of();
+#define G4W_SCHED(A_, B_) \
+  template <>             \
+  __host__ __device__ constexpr const Sched<A_, B_>& sched_of<A_, B_>() { return kSched##A_##B_; }
+G4W_SCHED(8, 8)
+G4W_SCHED(8, 4)
+G4W_SCHED(8, 6)
+G4W_SCHED(4, 8)
+G4W_SCHED(4, 4)
+G4W_SCHED(4, 6)
+#undef G4W_SCHED
 
 __device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g)); }
 
@@ -156,7 +167,7 @@ __device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g))
 //      the epilogue reads g, u from aux = gu [M, 2F] and writes dgu = [dh·u·silu'(g) | dh·silu(g)].
 //      N = F.
 // Both round the GEMM result to bf16 first, exactly where the unfused path stores it.
-template <int BN, bool BT, bool SPLIT, int EPI = 0>
+template <int BMT, int BN, bool BT, bool SPLIT, int EPI = 0>
 __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, int lda, const bf16* __restrict__ B,
                                                   int ldb, const bf16* __restrict__ residual, void* __restrict__ out,
                                                   int M, int N, int K, int splits, const bf16* __restrict__ aux,
@@ -165,29 +176,34 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   static_assert(EPI == 0 || !SPLIT, "fused epilogues run on whole-K tiles");
   static_assert(EPI != 1 || !BT, "SwiGLU forward epilogue: NT only");
   static_assert(EPI != 2 || BT, "SwiGLU backward epilogue: the transposed-B dX only");
+  static_assert(BMT == 256 || BMT == 128, "tile heights: 256, 128");
+  constexpr int NA = BMT / 32;                 // a fragments per wave per K-half
   constexpr int NB = BN / 32;                  // b fragments per wave per K-half
-  constexpr int STAGES = BN == 128 ? 3 : 2;
-  static_assert(BN == 128 || BN == 256 || (BN == 192 && !BT), "tile widths: 128, 256 (NT / BT), 192 (NT)");
+  constexpr int IMG_AT = BMT * BK * 2;
   constexpr int IMG_B = BN * BK * 2;
-  constexpr int STAGE = IMG_A + IMG_B;
-  constexpr int KT = 16 * NB;                  // MFMAs per K-tile per wave
+  constexpr int STAGE = IMG_AT + IMG_B;
+  constexpr int STAGES = 3 * STAGE <= 160 * 1024 ? 3 : 2;
+  static_assert(BN == 128 || BN == 256 || (BN == 192 && !BT), "tile widths: 128, 256 (NT / BT), 192 (NT)");
+  constexpr int KT = 2 * NA * NB;              // MFMAs per K-tile per wave
   constexpr int H = KT / 2;
-  constexpr int R = 8 + NB;                    // fragment-read items per K-half
+  constexpr int R = NA + NB;                   // fragment-read items per K-half
+  constexpr int DA = BMT / 32;                 // A DMAs per wave per K-tile
   constexpr int DB = BN / 32;                  // B DMAs per wave per K-tile
-  constexpr int D = 8 + DB;                    // all DMAs per wave per K-tile
-  constexpr int K1 = R + 9;                    // barrier 1 after this MFMA
+  constexpr int D = DA + DB;                   // all DMAs per wave per K-tile
+  constexpr bool BIG = NA == 8;
+  constexpr int K1 = R + (BIG ? 9 : 1);        // barrier 1 after this MFMA
   constexpr int K2 = KT - R - 1;               // barrier 2 after this MFMA
-  constexpr int DSP = (K2 - 10 - (K1 + 1)) / D;   // DMA spacing
+  constexpr int DSP = (K2 - (BIG ? 10 : 2) - (K1 + 1)) / D;   // DMA spacing
   static_assert(DSP >= 1, "schedule");
   __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE];
 
-  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  const int tiles_m = (M + BMT - 1) / BMT, tiles_n = (N + BN - 1) / BN;
   const int nwg = tiles_m * tiles_n * splits;
   const int id = xcd_remap(blockIdx.x, nwg);
   const int sp = id % splits;
   const int tid = id / splits;
   const int tm = tid % tiles_m, tn = tid / tiles_m;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = tm * BMT, n0 = tn * BN;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int wr = w >> 1, wc = w & 1;
@@ -206,8 +222,8 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   {
     const int r8 = lane >> 3, c = (lane & 7) ^ (r8 & 6);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {   // A: wave w, DMA i → rows 64w + 8i + r8
-      const int ra = min(m0 + w * 64 + i * 8 + r8, M - 1);
+    for (int i = 0; i < DA; ++i) {   // A: wave w, DMA i → rows (BMT/4)·w + 8i + r8
+      const int ra = min(m0 + w * (BMT / 4) + i * 8 + r8, M - 1);
       va[i] = ((uint32_t)ra * (uint32_t)lda + (uint32_t)(kt0 * BK + c * 8)) * 2u;
     }
     if constexpr (!BT) {
@@ -241,7 +257,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   int lo[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) lo[s] = ((lane >> 3) & 1) * 1024 + 16 * slot_of(lane & 7, 4 * s + (lane >> 4));
-  const int a_off = wr * 8 * 2048;
+  const int a_off = wr * NA * 2048;
   const int b_off = wc * NB * 2048;
   int boff_t[8];
   if constexpr (BT) {
@@ -252,7 +268,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
       boff_t[j] = (8 * g + q) * (2 * BN) + 32 * ((wc * NB + j) ^ hk) + 16 * (p >> 1) + 8 * (p & 1);
   }
 
-  f32x4 acc[8][8];   // [.][NB..7] unused when BN = 128
+  f32x4 acc[8][8];   // [NA..7][NB..7] unused for the smaller tiles
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
 
   // LDS-DMA as asm statements: hipcc then tracks no LDS-DMA and does not drain the whole queue
@@ -260,7 +276,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   // disjoint from the in-flight stages (measured: the dX kernel waited 33 % of its cycles there).
   // Every ordering of DMA'd data is by the explicit vmcnt + barrier pairs below.
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)lds);
-  const uint32_t wa = lds_base + (uint32_t)w * 8192u, wb = lds_base + IMG_A + (uint32_t)w * (IMG_B / 4);
+  const uint32_t wa = lds_base + (uint32_t)w * (IMG_AT / 4), wb = lds_base + IMG_AT + (uint32_t)w * (IMG_B / 4);
   auto dma_a = [&](uint32_t st, int t, int q) {
     dma_lds(rsa, wa + st + q * 1024, va[q], (uint32_t)t * (BK * 2));
   };
@@ -269,27 +285,27 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   };
   auto dma_tile = [&](uint32_t st, int t) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) dma_a(st, t, q);
+    for (int q = 0; q < DA; ++q) dma_a(st, t, q);
 #pragma unroll
     for (int q = 0; q < DB; ++q) dma_b(st, t, q);
   };
   // read item r of K-half s of the stage at st into (fa, fb)
   auto read_item = [&](bf16x8* fa, bf16x8* fb, const char* st, int s, int r) {
-    if (sched_of<NB>().rd_a[r]) {
-      fa[sched_of<NB>().rd_i[r]] = lds_frag(st + a_off + sched_of<NB>().rd_i[r] * 2048 + lo[s]);
+    if (sched_of<NA, NB>().rd_a[r]) {
+      fa[sched_of<NA, NB>().rd_i[r]] = lds_frag(st + a_off + sched_of<NA, NB>().rd_i[r] * 2048 + lo[s]);
     } else if constexpr (BT) {
-      const char* pb = st + IMG_A + s * (32 * 2 * BN) + boff_t[sched_of<NB>().rd_i[r]];
+      const char* pb = st + IMG_AT + s * (32 * 2 * BN) + boff_t[sched_of<NA, NB>().rd_i[r]];
       const bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)pb);
       const bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(pb + 4 * 2 * BN));
-      fb[sched_of<NB>().rd_i[r]] = bf16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+      fb[sched_of<NA, NB>().rd_i[r]] = bf16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
     } else {
-      fb[sched_of<NB>().rd_i[r]] = lds_frag(st + IMG_A + b_off + sched_of<NB>().rd_i[r] * 2048 + lo[s]);
+      fb[sched_of<NA, NB>().rd_i[r]] = lds_frag(st + IMG_AT + b_off + sched_of<NA, NB>().rd_i[r] * 2048 + lo[s]);
     }
   };
 
   if (nk <= 0) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < NA; ++i)
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   } else {
@@ -309,7 +325,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
       char* const ns = lds + (cur + STAGE == STAGES * STAGE ? 0 : cur + STAGE);
       Unroll<0, KT>::run([&](auto kc) {
         constexpr int k = decltype(kc)::value;
-        constexpr int i = sched_of<NB>().i[k % H], j = sched_of<NB>().j[k % H];
+        constexpr int i = sched_of<NA, NB>().i[k % H], j = sched_of<NA, NB>().j[k % H];
         if constexpr (k < H) {
           if constexpr (decltype(first)::value) mfma_zero(acc[i][j], fb0[j], fa0[i]);
           else mfma_acc(acc[i][j], fb0[j], fa0[i]);
@@ -324,8 +340,8 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
         }
         if constexpr (k > K1 && (k - K1 - 1) % DSP == 0 && (k - K1 - 1) / DSP < D) {
           constexpr int d = (k - K1 - 1) / DSP;
-          if constexpr (d < 8) dma_a(cur, tn_, d);
-          else dma_b(cur, tn_, d - 8);
+          if constexpr (d < DA) dma_a(cur, tn_, d);
+          else dma_b(cur, tn_, d - DA);
         }
         if constexpr (k == K2) {
           wait_vmcnt<(STAGES - 1) * D>();
@@ -344,8 +360,8 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   // ---- epilogue: lane holds C[m = col][n = 4·(lane>>4) + r … +3] of each 16×16 block
   if constexpr (EPI == 1) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = m0 + wr * 128 + i * 16 + (lane & 15);
+    for (int i = 0; i < NA; ++i) {
+      const int m = m0 + wr * (BMT / 2) + i * 16 + (lane & 15);
       if (m >= M) continue;
 #pragma unroll
       for (int j = 0; j < NB; j += 2) {
@@ -375,8 +391,8 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
     // splits over XCDs; the ticket is reset by the last arriver (zeroed once at allocation).
     float* wsf = ws;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = m0 + wr * 128 + i * 16 + (lane & 15);
+    for (int i = 0; i < NA; ++i) {
+      const int m = m0 + wr * (BMT / 2) + i * 16 + (lane & 15);
       if (m >= M) continue;
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
@@ -408,7 +424,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   // one per 16×16 block (a load behind a per-block bounds branch waits vmcnt(0) each time)
   const bool has_res = EPI == 0 && residual != nullptr;
   // rows per chunk: 4 (2 when a 256-wide tile also sums split-K slabs: register budget)
-  constexpr int RC = (SPLIT && NB >= 6) ? 2 : 4;
+  constexpr int RC = (SPLIT && NB >= 6) ? 2 : 4;   // (NA is 4 or 8: a multiple)
   auto rows = [&](auto hh_c, auto res_c) {
     constexpr int i0 = RC * decltype(hh_c)::value;
     constexpr bool RES = decltype(res_c)::value;
@@ -420,7 +436,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
       for (int j = 0; j < NB; ++j) tot[ii][j] = acc[i0 + ii][j];
 #pragma unroll
     for (int ii = 0; ii < RC; ++ii) {
-      const int m = min(m0 + wr * 128 + (i0 + ii) * 16 + (lane & 15), M - 1);
+      const int m = min(m0 + wr * (BMT / 2) + (i0 + ii) * 16 + (lane & 15), M - 1);
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         const int n = min(n0 + wc * (BN / 2) + j * 16 + 4 * (lane >> 4), N - 4);
@@ -439,7 +455,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
         f32x4 pv[RC][8];
 #pragma unroll
         for (int ii = 0; ii < RC; ++ii) {
-          const int m = min(m0 + wr * 128 + (i0 + ii) * 16 + (lane & 15), M - 1);
+          const int m = min(m0 + wr * (BMT / 2) + (i0 + ii) * 16 + (lane & 15), M - 1);
 #pragma unroll
           for (int j = 0; j < NB; ++j) {
             const int n = min(n0 + wc * (BN / 2) + j * 16 + 4 * (lane >> 4), N - 4);
@@ -454,7 +470,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
     }
 #pragma unroll
     for (int ii = 0; ii < RC; ++ii) {
-      const int m = m0 + wr * 128 + (i0 + ii) * 16 + (lane & 15);
+      const int m = m0 + wr * (BMT / 2) + (i0 + ii) * 16 + (lane & 15);
       if (m >= M) continue;
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
@@ -483,9 +499,9 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
     }
   };
   if (has_res) {
-    Unroll<0, 8 / RC>::run([&](auto hc) { rows(hc, std::true_type{}); });
+    Unroll<0, NA / RC>::run([&](auto hc) { rows(hc, std::true_type{}); });
   } else {
-    Unroll<0, 8 / RC>::run([&](auto hc) { rows(hc, std::false_type{}); });
+    Unroll<0, NA / RC>::run([&](auto hc) { rows(hc, std::false_type{}); });
   }
 }
 
@@ -511,7 +527,7 @@ __global__ __launch_bounds__(256) void splitk_sum_k(const float* __restrict__ ws
 }
 
 
-int tiles_of(int M, int N, int bn) { return ((M + BM - 1) / BM) * ((N + bn - 1) / bn); }
+int tiles_of(int M, int N, int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); }
 
 }  // namespace
 
@@ -522,43 +538,48 @@ bool gemm4w_supported(int M, int N, int K, int lda, int ldb, bool bt) {
          (bt ? (uint64_t)K * ldb * 2 < 0xFFFFFFFFull : (uint64_t)N * ldb * 2 < 0xFFFFFFFFull);
 }
 
-// Tile width and K-splits from one cost model: (rounds of 256 workgroups) × (K-tiles per workgroup)
-// × the measured in-step time of one K-tile at that width (256: 1.5 µs / 1.62 transposed-B, 192: 1.22,
-// 128: 0.92) + the
-// split-K reduce pass (its fp32 slabs: M·N·(8s + 2) bytes at ≈12 TB/s effective + a launch).  At
-// M = 2048 this picks: q|k|v fwd 192 (256 tiles); gate|up fwd / LM head 256; o fwd, every dX to
-// d_model and down dX (768 tiles = 3 full rounds) 128; down fwd 256 with 2 splits.
-// LIPA_GEMM4W_BN / LIPA_GEMM4W_SPLITS force either.
+// Tile (height × width) and K-splits from one cost model: (rounds of 256 workgroups) × (K-tiles per
+// workgroup) × the measured in-step time of one K-tile of that tile (256 × 256: 1.5 µs,
+// transposed-B 1.52, 256 × 192: 1.22, 256 × 128: 0.92; the 128-high tiles ≈ 0.56 × those) + the split-K
+// reduce launch (its fp32 slabs: M·N·(8s + 2) bytes at ≈12 TB/s effective + a launch).  At M = 2048
+// this picks: q|k|v fwd 256 × 192 (256 tiles); gate|up fwd / LM head 256 × 256; o fwd, the dX GEMMs to
+// d_model and down dX 128 × 256; down fwd and gate|up dX 256 × 256 with 2 splits.  At M = 1024 (the
+// sequential-GA micro-batches of the reference-faithful step) the 128-high tiles fill the chip without
+// split-K for q|k|v, o and their dX (profiles/r3/README.md: splitk_sum_k launches 650 → 146 per step).
+// LIPA_GEMM4W_BN / LIPA_GEMM4W_BM / LIPA_GEMM4W_SPLITS force a choice.
 struct G4wCfg {
-  int bn, splits;
+  int bm, bn, splits;
 };
-G4wCfg gemm4w_cfg(int M, int N, int K, bool bt, int bn_req, int sp_req) {
-  static const int forced_bn = [] {
-    const char* e = getenv("LIPA_GEMM4W_BN");
-    return e ? atoi(e) : 0;
-  }();
-  static const int forced_sp = [] {
-    const char* e = getenv("LIPA_GEMM4W_SPLITS");
-    return e ? atoi(e) : 0;
-  }();
+static int env_int(const char* name) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : 0;
+}
+G4wCfg gemm4w_cfg(int M, int N, int K, bool bt, int bn_req, int sp_req, int bm_req) {
+  static const int forced_bn = env_int("LIPA_GEMM4W_BN"), forced_sp = env_int("LIPA_GEMM4W_SPLITS"),
+                   forced_bm = env_int("LIPA_GEMM4W_BM");
   if (bn_req == 0) bn_req = forced_bn;
   if (sp_req <= 0) sp_req = forced_sp;
+  if (bm_req == 0) bm_req = forced_bm;
   const int nk = K / BK;
-  G4wCfg best{128, 1};
+  G4wCfg best{256, 128, 1};
   double best_t = 1e30;
-  for (int bn : {256, 192, 128}) {
-    if (bn == 192 && bt) continue;
-    if (bn_req && bn != bn_req) continue;
-    const int tiles = tiles_of(M, N, bn);
-    const double kt_us = bn == 256 ? (bt ? 1.62 : 1.5) : bn == 192 ? 1.22 : 0.92;
-    for (int s = 1; s <= 8; s *= 2) {
-      if (sp_req > 0 && s != sp_req) continue;
-      if (s > 1 && sp_req <= 0 && nk / s < 8) break;
-      double t = (double)((tiles * s + 255) / 256) * ((nk + s - 1) / s) * kt_us;
-      if (s > 1) t += (double)M * N * (8.0 * s + 2.0) / 12e6 + 2.0;
-      if (t < best_t - 1e-9) {
-        best_t = t;
-        best = G4wCfg{bn, s};
+  for (int bm : {256, 128}) {
+    if (bm_req && bm != bm_req) continue;
+    for (int bn : {256, 192, 128}) {
+      if (bn == 192 && bt) continue;
+      if (bn_req && bn != bn_req) continue;
+      const int tiles = tiles_of(M, N, bm, bn);
+      double kt_us = bn == 256 ? (bt ? 1.52 : 1.5) : bn == 192 ? 1.22 : 0.92;
+      if (bm == 128) kt_us *= 0.56;
+      for (int s = 1; s <= 8; s *= 2) {
+        if (sp_req > 0 && s != sp_req) continue;
+        if (s > 1 && sp_req <= 0 && nk / s < 8) break;
+        double t = (double)((tiles * s + 255) / 256) * ((nk + s - 1) / s) * kt_us;
+        if (s > 1) t += (double)M * N * (8.0 * s + 2.0) / 12e6 + 2.0;
+        if (t < best_t - 1e-9) {
+          best_t = t;
+          best = G4wCfg{bm, bn, s};
+        }
       }
     }
   }
@@ -566,37 +587,47 @@ G4wCfg gemm4w_cfg(int M, int N, int K, bool bt, int bn_req, int sp_req) {
   return best;
 }
 
-// bn / splits: 0 = chosen by gemm4w_cfg.  Returns the split count used (the caller's fp32 workspace
-// must hold splits·M·N floats when it is > 1).
-int gemm4w_plan(int M, int N, int K, bool bt, int bn, int splits, int* bn_out) {
-  const G4wCfg c = gemm4w_cfg(M, N, K, bt, bn, splits);
+// bn / splits / bm: 0 = chosen by gemm4w_cfg.  Returns the split count used (the caller's fp32
+// workspace must hold splits·M·N floats when it is > 1) and the tile through bn_out / bm_out.
+int gemm4w_plan(int M, int N, int K, bool bt, int bn, int splits, int* bn_out, int bm, int* bm_out) {
+  const G4wCfg c = gemm4w_cfg(M, N, K, bt, bn, splits, bm);
   if (bn_out) *bn_out = c.bn;
+  if (bm_out) *bm_out = c.bm;
   return c.splits;
 }
 
+int gemm4w_tiles(int M, int N, int bm, int bn) { return tiles_of(M, N, bm, bn); }
+
 // ws: splits·M·N fp32 slabs, cnt: one zero-initialised int per tile (both only when splits > 1);
-// cnt == nullptr: the slabs are summed by a separate splitk_sum_k launch instead of the last arriver
+// cnt == nullptr: the slabs are summed by a separate splitk_sum_k launch instead of the last arriver.
+// Callers pass the (bm, bn, splits) that gemm4w_plan returned.
 void launch_gemm4w(const void* A, int lda, const void* B, int ldb, const void* residual, void* out, float* ws,
-                   int* cnt, int M, int N, int K, int splits, bool bt, int bn, hipStream_t st) {
-  // callers pass the (bn, splits) that gemm4w_plan returned
-  const int tiles = tiles_of(M, N, bn);
+                   int* cnt, int M, int N, int K, int splits, bool bt, int bn, int bm, hipStream_t st) {
+  const int tiles = tiles_of(M, N, bm, bn);
   const bool split = splits > 1;
   const bf16* a = (const bf16*)A;
   const bf16* b = (const bf16*)B;
   const bf16* r = (const bf16*)residual;
   void* o = out;
   const int grid = tiles * (split ? splits : 1), sp = split ? splits : 1;
-#define G4W(BN_, BT_, SP_) \
-  gemm4w_k<BN_, BT_, SP_><<<grid, NT, 0, st>>>(a, lda, b, ldb, r, o, M, N, K, sp, nullptr, nullptr, 0, ws, cnt)
-  if (bn == 256) {
-    if (bt) { if (split) G4W(256, true, true); else G4W(256, true, false); }
-    else { if (split) G4W(256, false, true); else G4W(256, false, false); }
-  } else if (bn == 192) {
-    if (split) G4W(192, false, true); else G4W(192, false, false);
-  } else {
-    if (bt) { if (split) G4W(128, true, true); else G4W(128, true, false); }
-    else { if (split) G4W(128, false, true); else G4W(128, false, false); }
+#define G4W(BM_, BN_, BT_, SP_) \
+  gemm4w_k<BM_, BN_, BT_, SP_><<<grid, NT, 0, st>>>(a, lda, b, ldb, r, o, M, N, K, sp, nullptr, nullptr, 0, ws, cnt)
+#define G4W_BN(BM_)                                                                \
+  if (bn == 256) {                                                                 \
+    if (bt) { if (split) G4W(BM_, 256, true, true); else G4W(BM_, 256, true, false); }   \
+    else { if (split) G4W(BM_, 256, false, true); else G4W(BM_, 256, false, false); }    \
+  } else if (bn == 192) {                                                          \
+    if (split) G4W(BM_, 192, false, true); else G4W(BM_, 192, false, false);       \
+  } else {                                                                         \
+    if (bt) { if (split) G4W(BM_, 128, true, true); else G4W(BM_, 128, true, false); }   \
+    else { if (split) G4W(BM_, 128, false, true); else G4W(BM_, 128, false, false); }    \
   }
+  if (bm == 256) {
+    G4W_BN(256)
+  } else {
+    G4W_BN(128)
+  }
+#undef G4W_BN
 #undef G4W
   if (split && cnt == nullptr) {
     const size_t MN = (size_t)M * N;
@@ -608,32 +639,37 @@ void launch_gemm4w(const void* A, int lda, const void* B, int ldb, const void* r
 
 // gu [M, 2F] and h = silu(gate)·up [M, F] from x [M, K] and W_gu [2F, K] ([gate | up] rows), one launch
 void launch_gemm4w_swiglu(const void* X, int ldx, const void* W, void* gu, void* h, int M, int F, int K, int bn,
-                          hipStream_t st) {
+                          int bm, hipStream_t st) {
   const int N = 2 * F;
-  const int tiles = tiles_of(M, N, bn);
+  const int tiles = tiles_of(M, N, bm, bn);
   const bf16* a = (const bf16*)X;
   const bf16* b = (const bf16*)W;
-#define G4S(BN_) \
-  gemm4w_k<BN_, false, false, 1><<<tiles, NT, 0, st>>>(a, ldx, b, K, nullptr, gu, M, N, K, 1, nullptr, (bf16*)h, F, \
-                                                       nullptr, nullptr)
-  if (bn == 256) G4S(256);
-  else if (bn == 192) G4S(192);
-  else G4S(128);
+#define G4S(BM_, BN_)                                                                                          \
+  gemm4w_k<BM_, BN_, false, false, 1><<<tiles, NT, 0, st>>>(a, ldx, b, K, nullptr, gu, M, N, K, 1, nullptr,    \
+                                                            (bf16*)h, F, nullptr, nullptr)
+  if (bm == 256) {
+    if (bn == 256) G4S(256, 256); else if (bn == 192) G4S(256, 192); else G4S(256, 128);
+  } else {
+    if (bn == 256) G4S(128, 256); else if (bn == 192) G4S(128, 192); else G4S(128, 128);
+  }
 #undef G4S
   LIPA_CHECK_LAUNCH();
 }
 
 // dgu [M, 2F] = SwiGLU-backward(dh = dY·W_down, gu) with W_down [N_w, F] used as stored, one launch
 void launch_gemm4w_dswiglu(const void* DY, int lddy, const void* W, const void* gu, void* dgu, int M, int F, int Nw,
-                           int bn, hipStream_t st) {
-  const int tiles = tiles_of(M, F, bn);
+                           int bn, int bm, hipStream_t st) {
+  const int tiles = tiles_of(M, F, bm, bn);
   const bf16* a = (const bf16*)DY;
   const bf16* b = (const bf16*)W;
-  if (bn == 256)
-    gemm4w_k<256, true, false, 2><<<tiles, NT, 0, st>>>(a, lddy, b, F, nullptr, dgu, M, F, Nw, 1, (const bf16*)gu,
-                                                        nullptr, F, nullptr, nullptr);
-  else
-    gemm4w_k<128, true, false, 2><<<tiles, NT, 0, st>>>(a, lddy, b, F, nullptr, dgu, M, F, Nw, 1, (const bf16*)gu,
-                                                        nullptr, F, nullptr, nullptr);
+#define G4D(BM_, BN_)                                                                                        \
+  gemm4w_k<BM_, BN_, true, false, 2><<<tiles, NT, 0, st>>>(a, lddy, b, F, nullptr, dgu, M, F, Nw, 1,         \
+                                                           (const bf16*)gu, nullptr, F, nullptr, nullptr)
+  if (bm == 256) {
+    if (bn == 256) G4D(256, 256); else G4D(256, 128);
+  } else {
+    if (bn == 256) G4D(128, 256); else G4D(128, 128);
+  }
+#undef G4D
   LIPA_CHECK_LAUNCH();
 }

@@ -667,9 +667,10 @@ def test_gemm8_strided_input(native_ext):
                                                    (2048, 1024, 2048, 2, True, True), (257, 264, 640, 4, True, False),
                                                    (1000, 1536, 1024, 0, True, False)])
 @pytest.mark.parametrize("bn", [128, 192, 256])
-def test_gemm4w_matches_fp32(native_ext, M, N, K, splits, bt, resid, bn):
+@pytest.mark.parametrize("bm", [256, 128])
+def test_gemm4w_matches_fp32(native_ext, M, N, K, splits, bt, resid, bn, bm):
     """y = x·wᵀ (w [N, K]) or, bt, y = x·w (w [K, N], the dX form), + residual, split-K or not, every
-    tile width (192: forward only)"""
+    tile height and width (192: forward only)"""
     if bt and bn == 192:
         pytest.skip("the 192-wide tile is forward-only")
     torch.manual_seed(0)
@@ -677,7 +678,7 @@ def test_gemm4w_matches_fp32(native_ext, M, N, K, splits, bt, resid, bn):
     w = (torch.rand(K, N, device=DEV) * 2 - 1).to(torch.bfloat16) if bt else \
         (torch.rand(N, K, device=DEV) * 2 - 1).to(torch.bfloat16)
     res = torch.randn(M, N, device=DEV).to(torch.bfloat16) if resid else None
-    y = native_ext.gemm4w(x, w, res, splits, bt, bn)
+    y = native_ext.gemm4w(x, w, res, splits, bt, bn, bm)
     want = x.float() @ (w.float() if bt else w.float().t())
     if resid:
         want += res.float()
@@ -691,15 +692,17 @@ def test_gemm4w_asymmetric_operands(native_ext):
     torch.manual_seed(1)
     for bt in (False, True):
         for bn in ((128, 256) if bt else (128, 192, 256)):
-            M, N, K = 256, 512, 128
-            x = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
-            w = torch.randint(-3, 4, (K, N) if bt else (N, K), device=DEV).to(torch.bfloat16)
-            y = native_ext.gemm4w(x, w, None, 1, bt, bn).float()
-            want = x.float() @ (w.float() if bt else w.float().t())
-            assert torch.equal(y, want), f"bt={bt} bn={bn}: max |err| {(y - want).abs().max().item()}"
+            for bm in (256, 128):
+                M, N, K = 256, 512, 128
+                x = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
+                w = torch.randint(-3, 4, (K, N) if bt else (N, K), device=DEV).to(torch.bfloat16)
+                y = native_ext.gemm4w(x, w, None, 1, bt, bn, bm).float()
+                want = x.float() @ (w.float() if bt else w.float().t())
+                assert torch.equal(y, want), f"bt={bt} bn={bn} bm={bm}: max |err| {(y - want).abs().max().item()}"
 
 
-@pytest.mark.parametrize("M,Fd,K", [(256, 256, 128), (300, 1024, 512), (2048, 3072, 1024), (2048, 12288, 512)])
+@pytest.mark.parametrize("M,Fd,K", [(256, 256, 128), (300, 1024, 512), (2048, 3072, 1024), (2048, 12288, 512),
+                                    (1024, 12288, 512)])
 def test_gemm4w_swiglu_epilogues(native_ext, M, Fd, K):
     """gate|up GEMM with the SwiGLU forward epilogue (gu and h in one launch) and the down dX GEMM with
     the SwiGLU backward epilogue, vs fp32 (the unfused path rounds gu / dh to bf16 at the same points)"""
