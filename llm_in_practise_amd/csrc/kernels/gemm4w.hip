@@ -545,7 +545,7 @@ bool gemm4w_supported(int M, int N, int K, int lda, int ldb, bool bt) {
 // this picks: q|k|v fwd 256 × 192 (256 tiles); gate|up fwd / LM head 256 × 256; o fwd, the dX GEMMs to
 // d_model and down dX 128 × 256; down fwd and gate|up dX 256 × 256 with 2 splits.  At M = 1024 (the
 // sequential-GA micro-batches of the reference-faithful step) the 128-high tiles fill the chip without
-// split-K for q|k|v, o and their dX (profiles/r3/README.md: splitk_sum_k launches 650 → 146 per step).
+// split-K for q|k|v, o and their dX (profiles/r3/step_timeline_faithful_bm128.txt: splitk_sum_k launches 650 → 290 per step).
 // LIPA_GEMM4W_BN / LIPA_GEMM4W_BM / LIPA_GEMM4W_SPLITS force a choice.
 struct G4wCfg {
   int bm, bn, splits;
