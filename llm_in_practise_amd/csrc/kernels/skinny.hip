@@ -11,6 +11,8 @@
 //    16-column m-tiles, so every W byte feeds MT MFMAs (v_mfma_f32_16x16x32_bf16);
 //  * split-K partials go to an fp32 [S, M, N] buffer; a second kernel sums the S slices, adds the
 //    residual and writes bf16 (deterministic — no atomics).
+#include <cstdlib>
+
 #include "common.h"
 
 using namespace lipa;
@@ -92,7 +94,7 @@ __device__ __forceinline__ bf16x8 dequant8(uint32_t w, float sc, float bi) {
   return r;
 }
 
-template <int MT>
+template <int MT, bool PAD>
 __global__ __launch_bounds__(256) void gemm_w4_skinny_k(const bf16* __restrict__ X, int ldx,
                                                         const uint8_t* __restrict__ codes,
                                                         const float* __restrict__ scales,
@@ -162,7 +164,7 @@ __global__ __launch_bounds__(256) void gemm_w4_skinny_k(const bf16* __restrict__
             acc[1][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[s], xb[s][mt], acc[1][mt], 0, 0, 0);
           }
         __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+        if constexpr (PAD) asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
       }
   }
   float* pp = part + (size_t)sp * M * N;
@@ -244,8 +246,22 @@ void launch_gemm_w4_skinny(const void* X, int ldx, const uint8_t* codes, const f
   // MT >= 2 runs one workgroup per CU (a 96 KB dynamic-LDS reservation; the kernel uses no LDS):
   // measured on MI355X (ROCm 7.2), two co-resident workgroups of the MT >= 2 code returned
   // nondeterministically wrong fragments (scripts/experiments/dbg_w4.py); one per CU is exact.
-#define L(MT) gemm_w4_skinny_k<MT><<<grid, 256, (MT) >= 2 ? 98304 : 0, st>>>((const bf16*)X, ldx, codes, scales, biases, \
-                                                                          gs, part, M, N, K, kc)
+  // LIPA_W4_SKINNY_MODE (diagnosis): bit 0 drops the reservation, bit 1 drops the post-MFMA pad.
+  static const int mode = [] {
+    const char* e = getenv("LIPA_W4_SKINNY_MODE");
+    return e ? atoi(e) : 0;
+  }();
+  const bool reserve = !(mode & 1), pad = !(mode & 2);
+#define L(MT)                                                                                                     \
+  do {                                                                                                            \
+    const size_t lds = (MT) >= 2 && reserve ? 98304 : 0;                                                          \
+    if (pad)                                                                                                      \
+      gemm_w4_skinny_k<MT, true><<<grid, 256, lds, st>>>((const bf16*)X, ldx, codes, scales, biases, gs, part, M, \
+                                                         N, K, kc);                                               \
+    else                                                                                                          \
+      gemm_w4_skinny_k<MT, false><<<grid, 256, lds, st>>>((const bf16*)X, ldx, codes, scales, biases, gs, part,   \
+                                                          M, N, K, kc);                                           \
+  } while (0)
   if (M <= 16) L(1);
   else if (M <= 32) L(2);
   else L(4);

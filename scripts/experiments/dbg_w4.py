@@ -1,4 +1,9 @@
+import os
+import sys
+
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from llm_in_practise_amd.ops._native import native
 from llm_in_practise_amd.quant.int4 import quantize_rtn
 nat = native()
