@@ -113,7 +113,13 @@ def main():
                          "(gradient checkpointing on, sequential GA micro-steps) in the same process and report "
                          "them as the JSON's 'faithful' sub-record (0: skip; ddp strategy only)")
     ap.add_argument("--faithful-warmup", type=int, default=2)
+    ap.add_argument("--nf4-gemm", default="auto", choices=["auto", "w4", "expand"],
+                    help="NF4 base GEMM form (ops/linear.py _nf4_w4): auto = one bf16 expansion per step where the copy "
+                         "is reused (forward + dX), the in-kernel NF4 dequant-GEMM elsewhere; w4 = the NF4 dequant-GEMM "
+                         "everywhere (no bf16 copy of the base: the memory-lean QLoRA step); expand = always expand")
     args = ap.parse_args()
+    from llm_in_practise_amd.ops import linear as _lin
+    _lin._NF4_MODE = args.nf4_gemm
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `python bench.py --gpus N` without a launcher: start N ranks under torch.distributed.run
@@ -205,6 +211,8 @@ def main():
             sync()
             log(f"[bench] first step done, loss={loss.item():.4f}")
     sync()
+    if device.type == "cuda":     # peak HBM of the training steps (not of building / quantising the model)
+        torch.cuda.reset_peak_memory_stats(device)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -231,6 +239,8 @@ def main():
         for _ in range(args.faithful_warmup):
             step(fused=0)
         sync()
+        if device.type == "cuda":
+            torch.cuda.reset_peak_memory_stats(device)
         tf0 = time.perf_counter()
         for _ in range(args.faithful_steps):
             floss = step(fused=0)
@@ -238,11 +248,13 @@ def main():
         fel = D.all_reduce_max(time.perf_counter() - tf0)
         fms = 1000 * fel / args.faithful_steps
         ftps = args.micro_batch * args.seq_len * args.grad_accum * world * args.faithful_steps / fel
-        log(f"[bench] faithful (grad ckpt + sequential GA): loss={floss.item():.4f} {fms:.1f} ms/step  {ftps:,.0f} tok/s")
+        fmem = torch.cuda.max_memory_allocated(device) / 2 ** 30 if device.type == "cuda" else 0.0
+        log(f"[bench] faithful (grad ckpt + sequential GA): loss={floss.item():.4f} {fms:.1f} ms/step  {ftps:,.0f} tok/s"
+            f"  peak HBM {fmem:.1f} GiB")
         faithful = {"value": round(ftps, 1), "unit": "tokens/s", "ms_per_step": round(fms, 2),
                     "steps": args.faithful_steps, "warmup": args.faithful_warmup,
                     "gradient_checkpointing": True, "ga_execution": "sequential",
-                    "micro_batch": args.micro_batch, "grad_accum": args.grad_accum}
+                    "micro_batch": args.micro_batch, "grad_accum": args.grad_accum, "peak_hbm_gib": round(fmem, 1)}
     if D.is_main():
         rec = {
             "metric": f"tokens/sec (whole node) {MODEL_NAMES.get(args.model, args.model)} "
@@ -266,6 +278,7 @@ def main():
                 "micro_batch": args.micro_batch,
                 "grad_accum": args.grad_accum,
                 "quant": "nf4+double_quant" if args.mode == "qlora" else "none",
+                "nf4_gemm": args.nf4_gemm,
                 "lora": f"r{args.lora_r}/a{args.lora_alpha}/drop{args.lora_dropout}/{args.targets}",
                 "optimizer": args.optim if engine is None else f"zero3-{engine.optim_name}",
                 "gradient_checkpointing": bool(args.grad_ckpt),

@@ -53,15 +53,18 @@ void set_dequant_variant(int);
 void launch_nf4_dequant(const uint8_t*, const float*, const uint8_t*, const float*, const float*, const float*, void*,
                         size_t, hipStream_t);
 bool gemm8_supported(int, int, int, int, int);
-bool gemm4w_supported(int, int, int, int, int, bool);
-int gemm4w_plan(int, int, int, bool, int, int, int*, int, int*);
+bool gemm4w_supported(int, int, int, int, int, bool, bool);
+int gemm4w_plan(int, int, int, bool, int, int, int*, int, int*, bool);
 int gemm4w_tiles(int, int, int, int);
 void launch_mlora_apply(const void*, int, const void*, const void*, const int64_t*, const void*, int, void*, int, int, int,
                         int, int, int, hipStream_t);
-void launch_gemm4w_swiglu(const void*, int, const void*, void*, void*, int, int, int, int, int, hipStream_t);
-void launch_gemm4w_dswiglu(const void*, int, const void*, const void*, void*, int, int, int, int, int, hipStream_t);
-void launch_gemm4w(const void*, int, const void*, int, const void*, void*, float*, int*, int, int, int, int, bool, int,
-                   int, hipStream_t);
+void launch_gemm4w_swiglu(const void*, int, const void*, const float*, void*, void*, int, int, int, int, int,
+                          hipStream_t);
+void launch_gemm4w_dswiglu(const void*, int, const void*, const float*, const void*, void*, int, int, int, int, int,
+                           hipStream_t);
+void launch_gemm4w(const void*, int, const void*, int, const void*, void*, float*, const float*, int, int, int, int, bool,
+                   int, int, hipStream_t);
+void launch_pack_g4w(const uint8_t*, void*, int, int, hipStream_t);
 int gemm8_splits(int, int, int);
 void launch_gemm8(const void*, int, const void*, int, const void*, const void*, int, const void*, void*, float*, int, int,
                   int, int, hipStream_t);
@@ -659,97 +662,113 @@ Tensor gemm8(Tensor x, Tensor w, optional<Tensor> ext_a, optional<Tensor> ext_b,
              int64_t splits);
 
 
-// Split-K tickets of gemm4w (one int per output tile): zeroed once when allocated, reset by each
-// tile's last-arriving split; one buffer per (device, stream) so concurrent streams never share.
-static int* split_tickets(const at::Device& dev, int64_t tiles) {
-  static std::map<std::pair<int, hipStream_t>, Tensor> bufs;
-  auto key = std::make_pair((int)dev.index(), stream());
-  Tensor& t = bufs[key];
-  if (!t.defined() || t.numel() < tiles)
-    t = at::zeros({std::max<int64_t>(tiles, 4096)}, at::TensorOptions().device(dev).dtype(at::kInt));
-  return t.data_ptr<int>();
+// The B operand of the gemm4w entry points: a bf16 weight, or (wscale given) the g4w-packed NF4 codes of one
+// (uint8, R·C/2 bytes, NF4Weight.g4w_pack) with wscale = the decoded fp32 block absmax transposed [C/64, R].
+struct G4wB {
+  const void* ptr;
+  const float* scale;
+  int64_t ld;
+};
+static G4wB g4w_operand(const Tensor& w, const optional<Tensor>& wscale, int64_t rows, int64_t cols) {
+  if (wscale && wscale->defined()) {
+    TORCH_CHECK(w.scalar_type() == at::kByte && w.is_contiguous() && w.numel() * 2 == rows * cols,
+                "gemm4w: NF4 codes [rows·cols/2] uint8");
+    TORCH_CHECK(wscale->scalar_type() == at::kFloat && wscale->is_contiguous() && wscale->numel() * 64 == rows * cols,
+                "gemm4w: NF4 scales [cols/64, rows] fp32");
+    TORCH_CHECK(rows % 64 == 0 && cols % 64 == 0, "gemm4w: NF4 rows / cols multiples of 64");
+    return {w.data_ptr(), wscale->data_ptr<float>(), cols};
+  }
+  CHECK_BF16(w);
+  TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1 && w.size(0) == rows && w.size(1) == cols, "gemm4w: weight shape");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0, "gemm4w: 16-byte aligned weight");
+  return {w.data_ptr(), nullptr, w.stride(0)};
+}
+
+bool gemm4w_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, bool bt, bool w4) {
+  return M < (1ll << 31) && N < (1ll << 31) && K < (1ll << 31) && gemm4w_supported(M, N, K, lda, ldb, bt, w4);
 }
 
 // y = x·wᵀ (+ residual) through the one-wave-per-SIMD AGPR-accumulator MFMA GEMM (gemm4w.hip);
 // x [M, K] (row stride any multiple of 8), w [N, K] contiguous rows.  bt: y = x·w with w [K, N]
 // (the dX = dY·W of a frozen [N_w, K_w] weight, no transpose copy).  splits <= 0: auto split-K;
-// bn: tile width 128 / 256 / 192 (NT only), 0 = auto
-Tensor gemm4w(Tensor x, Tensor w, optional<Tensor> residual, int64_t splits, bool bt, int64_t bn, int64_t bm) {
+// bn: tile width 128 / 256 / 192 (NT only), 0 = auto.  wscale: w is an NF4 base (g4w_operand); n_w4
+// is then the GEMM N (the weight's rows for NT, its columns for bt).
+Tensor gemm4w(Tensor x, Tensor w, optional<Tensor> residual, int64_t splits, bool bt, int64_t bn, int64_t bm,
+              optional<Tensor> wscale, int64_t n_w4) {
   CHECK_BF16(x);
-  CHECK_BF16(w);
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1, "gemm4w: 2-D, unit inner stride");
-  const int64_t M = x.size(0), K = x.size(1), N = bt ? w.size(1) : w.size(0);
-  TORCH_CHECK((bt ? w.size(0) : w.size(1)) == K, "gemm4w: K mismatch");
-  TORCH_CHECK(gemm4w_supported(M, N, K, x.stride(0), w.stride(0), bt), "gemm4w: unsupported shape / strides");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
-              "gemm4w: 16-byte aligned operands");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "gemm4w: x 2-D, unit inner stride");
+  const bool w4 = wscale && wscale->defined();
+  const int64_t M = x.size(0), K = x.size(1);
+  const int64_t N = w4 ? n_w4 : (w.dim() == 2 ? (bt ? w.size(1) : w.size(0)) : 0);
+  const G4wB b = bt ? g4w_operand(w, wscale, K, N) : g4w_operand(w, wscale, N, K);
+  TORCH_CHECK(gemm4w_ok(M, N, K, x.stride(0), b.ld, bt, w4), "gemm4w: unsupported shape / strides");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "gemm4w: 16-byte aligned operands");
   const void* res = nullptr;
   if (residual && residual->defined()) {
     CHECK_BF16(*residual);
     TORCH_CHECK(residual->is_contiguous() && residual->size(0) == M && residual->size(1) == N, "gemm4w: residual [M, N]");
     res = residual->data_ptr();
   }
-  TORCH_CHECK(bn == 0 || bn == 128 || bn == 256 || (bn == 192 && !bt), "gemm4w: bn 0 / 128 / 256 / 192 (not bt)");
+  TORCH_CHECK(bn == 0 || bn == 128 || bn == 256 || (bn == 192 && !bt && !w4), "gemm4w: bn 0 / 128 / 256 / 192 (NT bf16)");
   TORCH_CHECK(bm == 0 || bm == 128 || bm == 256, "gemm4w: bm 0 / 128 / 256");
   int bn_used = 0, bm_used = 0;
-  const int sp = gemm4w_plan(M, N, K, bt, (int)bn, (int)splits, &bn_used, (int)bm, &bm_used);
+  const int sp = gemm4w_plan(M, N, K, bt, (int)bn, (int)splits, &bn_used, (int)bm, &bm_used, w4);
   auto y = at::empty({M, N}, x.options());
   Tensor ws;
-  int* cnt = nullptr;
-  if (sp > 1) {
-    ws = at::empty({sp, M, N}, x.options().dtype(at::kFloat));
-    const int64_t tiles = gemm4w_tiles(M, N, bm_used, bn_used);
-    static const bool inlaunch = [] {
-      // measured 1.1-1.2 ms/step SLOWER than the separate reduce launch (profiles/r3/README.md): the
-      // last arriver's serial slab read + the agent fences sit on every split tile's critical path
-      const char* e = getenv("LIPA_GEMM4W_INLAUNCH_REDUCE");
-      return e && atoi(e) != 0;
-    }();
-    if (inlaunch) cnt = split_tickets(x.device(), tiles);
-  }
-  launch_gemm4w(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), res, y.data_ptr(),
-                sp > 1 ? ws.data_ptr<float>() : nullptr, cnt, M, N, K, sp, bt, bn_used, bm_used, stream());
+  if (sp > 1) ws = at::empty({sp, M, N}, x.options().dtype(at::kFloat));
+  launch_gemm4w(x.data_ptr(), x.stride(0), b.ptr, b.ld, res, y.data_ptr(), sp > 1 ? ws.data_ptr<float>() : nullptr,
+                b.scale, M, N, K, sp, bt, bn_used, bm_used, stream());
   return y;
 }
 
 // Fused MLP GEMMs (gemm4w.hip EPI 1 / 2).  gemm4w_swiglu: x [M, K], w_gu [2F, K] ([gate | up] rows)
 // → (gu [M, 2F], h = silu(gate)·up [M, F]).  gemm4w_dswiglu: dy [M, N_w], w_down [N_w, F], gu [M, 2F]
-// → dgu [M, 2F] = SwiGLU-backward(dy·w_down).
-std::vector<Tensor> gemm4w_swiglu(Tensor x, Tensor w) {
+// → dgu [M, 2F] = SwiGLU-backward(dy·w_down).  wscale: the weight is an NF4 base (g4w_operand).
+std::vector<Tensor> gemm4w_swiglu(Tensor x, Tensor w, optional<Tensor> wscale, int64_t F_w4) {
   CHECK_BF16(x);
-  CHECK_BF16(w);
-  CHECK_CONTIG(w);
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && w.dim() == 2 && w.size(1) == x.size(1), "gemm4w_swiglu: shapes");
-  const int64_t M = x.size(0), K = x.size(1), F = w.size(0) / 2;
-  TORCH_CHECK(w.size(0) == 2 * F && F % 16 == 0 && gemm4w_supported(M, 2 * F, K, x.stride(0), K, false) &&
-                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "gemm4w_swiglu: x 2-D");
+  const bool w4 = wscale && wscale->defined();
+  const int64_t M = x.size(0), K = x.size(1), F = w4 ? F_w4 : w.size(0) / 2;
+  const G4wB b = g4w_operand(w, wscale, 2 * F, K);
+  TORCH_CHECK(F % 16 == 0 && gemm4w_ok(M, 2 * F, K, x.stride(0), K, false, w4) &&
+                  (w4 || w.is_contiguous()) && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
               "gemm4w_swiglu: unsupported shape / alignment");
   int bn = 0, bm = 0;
-  gemm4w_plan(M, 2 * F, K, false, 0, 1, &bn, 0, &bm);
+  gemm4w_plan(M, 2 * F, K, false, 0, 1, &bn, 0, &bm, w4);
   auto gu = at::empty({M, 2 * F}, x.options());
   auto h = at::empty({M, F}, x.options());
-  launch_gemm4w_swiglu(x.data_ptr(), x.stride(0), w.data_ptr(), gu.data_ptr(), h.data_ptr(), M, F, K, bn, bm, stream());
+  launch_gemm4w_swiglu(x.data_ptr(), x.stride(0), b.ptr, b.scale, gu.data_ptr(), h.data_ptr(), M, F, K, bn, bm,
+                       stream());
   return {gu, h};
 }
 
-Tensor gemm4w_dswiglu(Tensor dy, Tensor w, Tensor gu) {
+Tensor gemm4w_dswiglu(Tensor dy, Tensor w, Tensor gu, optional<Tensor> wscale) {
   CHECK_BF16(dy);
-  CHECK_BF16(w);
   CHECK_BF16(gu);
-  CHECK_CONTIG(w);
   CHECK_CONTIG(gu);
-  TORCH_CHECK(dy.dim() == 2 && dy.stride(1) == 1 && w.dim() == 2 && w.size(0) == dy.size(1), "gemm4w_dswiglu: shapes");
-  const int64_t M = dy.size(0), Nw = dy.size(1), F = w.size(1);
-  TORCH_CHECK(gu.size(0) == M && gu.size(1) == 2 * F && F % 16 == 0 &&
-                  gemm4w_supported(M, F, Nw, dy.stride(0), F, true) &&
-                  reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+  TORCH_CHECK(dy.dim() == 2 && dy.stride(1) == 1, "gemm4w_dswiglu: dy 2-D");
+  const bool w4 = wscale && wscale->defined();
+  const int64_t M = dy.size(0), Nw = dy.size(1), F = gu.size(1) / 2;
+  const G4wB b = g4w_operand(w, wscale, Nw, F);
+  TORCH_CHECK(gu.size(0) == M && gu.size(1) == 2 * F && F % 16 == 0 && gemm4w_ok(M, F, Nw, dy.stride(0), F, true, w4) &&
+                  (w4 || w.is_contiguous()) && reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0,
               "gemm4w_dswiglu: unsupported shape / alignment");
   int bn = 0, bm = 0;
-  gemm4w_plan(M, F, Nw, true, 0, 1, &bn, 0, &bm);
+  gemm4w_plan(M, F, Nw, true, 0, 1, &bn, 0, &bm, w4);
   auto dgu = at::empty({M, 2 * F}, dy.options());
-  launch_gemm4w_dswiglu(dy.data_ptr(), dy.stride(0), w.data_ptr(), gu.data_ptr(), dgu.data_ptr(), M, F, Nw, bn, bm,
+  launch_gemm4w_dswiglu(dy.data_ptr(), dy.stride(0), b.ptr, b.scale, gu.data_ptr(), dgu.data_ptr(), M, F, Nw, bn, bm,
                         stream());
   return dgu;
+}
+
+// bnb-layout NF4 codes [R, C/2] → the g4w tile layout gemm4w reads (gemm4w.hip pack_g4w_k)
+Tensor g4w_pack(Tensor codes, int64_t R, int64_t C) {
+  CHECK_CONTIG(codes);
+  TORCH_CHECK(codes.scalar_type() == at::kByte && codes.numel() * 2 == R * C && R % 64 == 0 && C % 64 == 0,
+              "g4w_pack: uint8 codes [R, C/2], R and C multiples of 64");
+  auto out = at::empty({R * C / 2}, codes.options());
+  launch_pack_g4w(codes.data_ptr<uint8_t>(), out.data_ptr(), (int)R, (int)C, stream());
+  return out;
 }
 
 // Multi-adapter LoRA (mlora.hip): y[:, c0:c0+N] += per-row s_a·(x·A_aᵀ)·B_aᵀ, a = ids[row] (0 = base).
@@ -1426,11 +1445,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nf4_absmax_t", &nf4_absmax_t);
   m.def("gemm_nf4", &gemm_nf4);
   m.def("gemm8", &gemm8);
+  m.def("gemm4w_ok", &gemm4w_ok);
+  m.def("g4w_pack", &g4w_pack);
   m.def("gemm4w", &gemm4w, py::arg("x"), py::arg("w"), py::arg("residual") = py::none(), py::arg("splits") = 0,
-        py::arg("bt") = false, py::arg("bn") = 0, py::arg("bm") = 0);
-  m.def("gemm4w_swiglu", &gemm4w_swiglu);
+        py::arg("bt") = false, py::arg("bn") = 0, py::arg("bm") = 0, py::arg("wscale") = py::none(),
+        py::arg("n_w4") = 0);
+  m.def("gemm4w_swiglu", &gemm4w_swiglu, py::arg("x"), py::arg("w"), py::arg("wscale") = py::none(),
+        py::arg("f_w4") = 0);
   m.def("mlora_apply", &mlora_apply);
-  m.def("gemm4w_dswiglu", &gemm4w_dswiglu);
+  m.def("gemm4w_dswiglu", &gemm4w_dswiglu, py::arg("dy"), py::arg("w"), py::arg("gu"), py::arg("wscale") = py::none());
   m.def("gemm_nf4_t", &gemm_nf4_t);
   m.def("gemm_bf16", &gemm_bf16);
   m.def("gemm_bf16_t", &gemm_bf16_t);

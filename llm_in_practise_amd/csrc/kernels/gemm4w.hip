@@ -3,35 +3,48 @@
 //   forward   y  = x·Wᵀ (+ residual)      A = x [M, K],  B = W  [N, K]   (NT)
 //   backward  dX = dY·W (+ C)             A = dY [M, K], B = W  [K, N]   (BT: W used as stored)
 //
-// Design (profiles/gemm4w_*.txt):
-//  * 256 threads = 4 waves as 2 (M) × 2 (N), one wave per SIMD; a wave owns a 128 × BN/2 output block
-//    of v_mfma_f32_16x16x32_bf16 accumulators (256 or 128 fp32 per lane) held in AGPRs.  The MFMAs
-//    are one-instruction asm statements with the accumulator a tied "+a" operand: with the builtin,
+// W is bf16, or (W4) the NF4 4-bit codes of a QLoRA base: the K9 "NF4 dequant-GEMM" — the codes are
+// expanded to bf16 inside the kernel, between the global load and the LDS B image, so no bf16 copy of
+// the frozen base ever exists in HBM (reference: BitsAndBytesConfig(load_in_4bit, nf4, double quant),
+// Fine-Tuning/qwen3-8b-qlora-dist.py:102-110).
+//
+// Design (profiles/gemm4w_*.txt, profiles/r3/, profiles/r4/):
+//  * 256 threads = 4 waves as 2 (M) × 2 (N), one wave per SIMD; a wave owns a BM/2 × BN/2 output block
+//    of v_mfma_f32_16x16x32_bf16 accumulators (up to 256 fp32 per lane) held in AGPRs.  The MFMAs
+//    are one-instruction asm statements with the accumulator a tied "+a" operand (with the builtin,
 //    hipcc split the accumulator phis between the two K-halves and shuffled ~48 v_accvgpr_mov/read/
-//    write per K-tile through the MFMA results.  Hazards the asm hides from hipcc: none in the loop
-//    (a fragment register is rewritten ≥ 16 MFMAs after its last reader; a single wave per SIMD, so
-//    no partner's MFMAs sit between); the epilogue's AGPR reads sit behind 16 wait states.
-//  * BN = 256 (grids of ≥ 256 tiles: gate|up forward, the LM head) or BN = 128 (the M = 2048 × 4096
-//    shapes — o / down forward and every dX to d_model: 256 tiles fill the chip without split-K).
-//  * global → LDS only by LDS-DMA (buffer_load … lds, 1 KB per wave-instruction, whole 128-B lines),
-//    STAGES K-tile stages (2 for BN = 256: 128 KB; 3 for BN = 128: 144 KB).  Per K-tile one
-//    compile-time-unrolled stream of 16·BN/32 MFMAs (first K-half on fA, second on fB):
+//    write per K-tile through the MFMA results).  A fragment register is rewritten ≥ 16 MFMAs after
+//    its last reader; one wave per SIMD, so no partner's MFMAs sit between; the epilogue's AGPR reads
+//    sit behind 16 wait states.
+//  * BN = 256 / 192 / 128 and BM = 256 / 128 chosen per shape by one cost model (gemm4w_cfg).
+//  * A (and bf16 B): global → LDS only by LDS-DMA (buffer_load … lds, 1 KB per wave-instruction,
+//    whole 128-B lines), STAGES K-tile stages (2 at 256 × 256: 128 KB; 3 where they fit 160 KB).
+//    Per K-tile one compile-time-unrolled stream of KT MFMAs (first K-half on fA, second on fB):
 //      - the first R MFMAs each carry one fragment read of this tile's second half (into fB);
-//      - barrier 1 (lgkmcnt(0)): nobody reads stage t % STAGES any more → its LDS-DMA refill with
-//        tile t + STAGES is spread over the middle MFMAs;
-//      - barrier 2 (vmcnt((STAGES − 1)·D)): tile t + 1 has landed;
+//      - barrier 1 (lgkmcnt(0)): nobody reads stage t % STAGES any more → its refill with tile
+//        t + STAGES is spread over the middle MFMAs;
+//      - barrier 2 (vmcnt): tile t + 1 has landed;
 //      - the last R MFMAs each carry one fragment read of tile t + 1's first half (into fA).
 //    The first half walks (i, j) in shells of max(i, j), so MFMA k waits only on reads issued ≥ 14
 //    MFMAs earlier.
-//  * NT images: 1 KB subtiles of 8 rows × 64 k, 16-B chunk c of row r at slot 8r + (c ^ (r & 6))
-//    (conflict-free ds_read_b128).  BT image: 64 k-rows × 2·BN bytes with the 32-B column pairs XOR-
-//    permuted by h(k) = (k & 3) | ((k >> 1) & 4), read as the B operand by two ds_read_b64_tr_b16 per
-//    fragment (a 32-lane half reads rows {0-3, 8-11} (+4) of a 16-row group: 8 distinct h → conflict-
-//    free).  Every swizzle is applied on the DMA SOURCE address (the LDS side is lane-linear).
+//  * W4 B operand (the NF4 base): per K-tile every lane expands ONE 64-element quant block (32 in the
+//    128-wide tiles).  Its 4-bit codes and fp32 absmax are LDS-DMA'd into a 2-slot ring one K-tile
+//    ahead (counted by the same explicit vmcnt waits as the A DMAs; each lane reads back its own
+//    bytes); the lane builds the block's scaled 16-entry table T[i] = bf16(code_i · absmax) —
+//    bit-identical to the bitsandbytes / nf4_dequant expansion — as lo-byte and hi-byte planes
+//    (4 + 4 dwords), expands its codes with v_perm_b32 byte lookups (3 VALU per element) and ds_writes
+//    the bf16 chunks into the SAME LDS B image the bf16 path DMAs.  At BM = 256 a lane expands 0.5
+//    elements per MFMA it issues: ≈1.8 VALU per 16x16x32 MFMA, cut into ≤2-VALU micro-ops placed one
+//    per MFMA.  The B bytes fetched drop 4× and the B LDS-DMAs disappear.  Codes are stored pre-tiled
+//    ("g4w" layout, NF4Weight.g4w_pack): [N/64][K/64][2][64 rows][16 B], nibble b of byte j = element
+//    j + 4b of an 8-element chunk.
+//  * NT images: 1 KB subtiles of 8 rows × 64 k, 16-B chunk c of row r at slot 8r + (c ^ f(r)), f(r) =
+//    r & 6 for the DMA'd images, r for the W4 B image (the expanding lanes write 8 rows × one chunk per
+//    ds_write group: conflict-free).  Both read conflict-free by ds_read_b128.  BT image: 64 k-rows ×
+//    2·BN bytes with the 32-B column pairs XOR-permuted by h(k) = (k & 3) | ((k >> 1) & 4), read as the B
+//    operand by two ds_read_b64_tr_b16 per fragment.  DMA'd swizzles are applied on the source address.
 //  * XCD-aware tile order: the m-tiles of one weight panel are consecutive ids and share an XCD's L2.
-//  * split-K (grids still smaller than the chip): fp32 slabs + one reduce launch (+ residual); the
-//    in-launch form (the tile's last-arriving split sums the slabs after an agent release / ticket /
-//    acquire) is kept behind LIPA_GEMM4W_INLAUNCH_REDUCE=1 — measured 1.1 ms/step slower.
+//  * split-K (grids still smaller than the chip): fp32 slabs + one reduce launch (+ residual).
 #include <type_traits>
 
 #include "common.h"
@@ -43,6 +56,7 @@ namespace {
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int BK = 64, NT = 256;
 
@@ -55,7 +69,10 @@ __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint64_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(b, 0, n, 0x00020000);
 }
 
-__device__ __forceinline__ int slot_of(int r8, int c) { return 8 * r8 + (c ^ (r8 & 6)); }
+// NT image slot of 16-B chunk c of row r8 (0..7) in a 1 KB subtile: DMA'd images (A, bf16 B) XOR by
+// r8 & 6, the lane-written W4 B image by r8
+template <bool FULL>
+__device__ __forceinline__ int slot_of(int r8, int c) { return 8 * r8 + (c ^ (FULL ? r8 : (r8 & 6))); }
 
 __device__ __forceinline__ bf16x8 lds_frag(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
@@ -157,6 +174,123 @@ G4W_SCHED(4, 6)
 
 __device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g)); }
 
+// ------------------------------------------------------------------ NF4 (W4) B-operand expansion
+// bitsandbytes NF4 code values
+constexpr float kNF4c[16] = {
+    -1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f,
+    -0.28444138169288635f, -0.18477343022823334f, -0.09105003625154495f, 0.0f,
+    0.07958029955625534f, 0.16093020141124725f, 0.24611230194568634f, 0.33791524171829224f,
+    0.44070982933044434f, 0.5626170039176941f, 0.7229568362236023f, 1.0f};
+
+__device__ __forceinline__ uint32_t vperm(uint32_t s0_hi, uint32_t s1_lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(s0_hi, s1_lo, sel);
+}
+// (m & a) | (~m & b), one v_bfi_b32
+__device__ __forceinline__ uint32_t vbfi(uint32_t m, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+// f32 product, never SLP-packed into v_pk_mul_f32 (packed f32 beside MFMAs is an anti-lever on CDNA4)
+__device__ __forceinline__ float vmul(float a, float b) {
+  float r;
+  asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {   // v_cvt_pk_bf16_f32 (RNE): a → low half
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
+}
+
+// one wave-instruction of dword LDS-DMA: 64 lanes × 4 B into LDS [dst, dst + 256 B)
+__device__ __forceinline__ void dma_lds4(const rsrc_t& rs, uint32_t dst, uint32_t voff, uint32_t soff) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dword %2, %3, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(dst), "v"(voff), "s"(rs), "s"(soff)
+      : "memory");
+}
+
+// code value × block absmax, exact constants folded (0 → 0, ±1 → ±s: bit-identical to the product)
+template <int I>
+__device__ __forceinline__ float mulc(float s) {
+  if constexpr (kNF4c[I] == 1.0f) return s;
+  else if constexpr (kNF4c[I] == -1.0f) return -s;
+  else if constexpr (kNF4c[I] == 0.0f) return 0.0f;
+  else return vmul(s, kNF4c[I]);
+}
+
+// A lane's block table as byte planes (l[q] byte i = low byte of T[4q + i], h[q] the high bytes) and
+// the expansion state of one 8-element chunk.  The expansion is cut into MICRO-OPS of at most two VALU
+// instructions each, spread one per MFMA over the K-tile: a 16x16x32 MFMA holds the SIMD's issue for
+// 8 of its 16 cycles, so two 4-cycle VALU fit beside it for free and a third does not
+// (MI355X_MICROARCH.md, per-instruction constants; measured: 4-VALU micro-ops every ~2 MFMAs cost
+// +31 % wave-cycles, profiles/r4/).
+struct W4St {
+  uint32_t l[4], h[4];
+  float m0, m1, m2, m3;
+  uint32_t p0, p1;
+  uint32_t sa, sb, t4, w4, w8, w12, ma, mb, x0, x1, x2, x3, lo, hi;
+  u32x4 o;
+};
+// table micro-op J (0..15): q = J / 4 builds planes l[q], h[q] from T[4q .. 4q+3]
+template <int J>
+__device__ __forceinline__ void w4_table(W4St& t, float s) {
+  constexpr int q = J / 4, r = J % 4;
+  if constexpr (r == 0) {
+    t.m0 = mulc<4 * q>(s);
+    t.m1 = mulc<4 * q + 1>(s);
+  } else if constexpr (r == 1) {
+    t.p0 = pk_bf16(t.m0, t.m1);
+    t.m2 = mulc<4 * q + 2>(s);
+  } else if constexpr (r == 2) {
+    t.m3 = mulc<4 * q + 3>(s);
+    t.p1 = pk_bf16(t.m2, t.m3);
+  } else {
+    t.l[q] = vperm(t.p1, t.p0, 0x06040200u);
+    t.h[q] = vperm(t.p1, t.p0, 0x07050301u);
+  }
+}
+// chunk micro-op P (0..11) on the 8 codes in w (nibble b of byte j = element j + 4b):
+//  0-1 selectors (low 3 bits of each code, one byte per element) and shifted copies of w;
+//  2-3 masks 0xFF where code >= 8 (v_perm selectors 8..11 replicate bit 15 / 31 of either source);
+//  4-7 elements 0-3: lo / hi plane lookups, select, interleave to bf16 pairs;  8-11 elements 4-7
+template <int P>
+__device__ __forceinline__ void w4_chunk(W4St& u, uint32_t w) {
+  if constexpr (P == 0) {
+    u.sa = w & 0x07070707u;
+    u.t4 = w >> 4;
+  } else if constexpr (P == 1) {
+    u.sb = u.t4 & 0x07070707u;
+    u.w4 = w << 4;
+  } else if constexpr (P == 2) {
+    u.w8 = w << 8;
+    u.w12 = w << 12;
+  } else if constexpr (P == 3) {
+    u.ma = vperm(u.w12, u.w4, 0x090B080Au);
+    u.mb = vperm(u.w8, w, 0x090B080Au);
+  } else if constexpr (P == 4 || P == 8) {
+    const uint32_t sel = P == 4 ? u.sa : u.sb;
+    u.x0 = vperm(u.l[1], u.l[0], sel);
+    u.x1 = vperm(u.l[3], u.l[2], sel);
+  } else if constexpr (P == 5 || P == 9) {
+    const uint32_t sel = P == 5 ? u.sa : u.sb;
+    u.x2 = vperm(u.h[1], u.h[0], sel);
+    u.x3 = vperm(u.h[3], u.h[2], sel);
+  } else if constexpr (P == 6 || P == 10) {
+    const uint32_t m = P == 6 ? u.ma : u.mb;
+    u.lo = vbfi(m, u.x1, u.x0);
+    u.hi = vbfi(m, u.x3, u.x2);
+  } else {
+    u.o[P == 7 ? 0 : 2] = vperm(u.hi, u.lo, 0x05010400u);
+    u.o[P == 7 ? 1 : 3] = vperm(u.hi, u.lo, 0x07030602u);
+  }
+}
+
 // EPI (fused MLP epilogues; SURVEY.md K5 "activation in the GEMM epilogue"):
 //   1  SwiGLU forward on the gate|up projection (NT, no split).  B = W_gu [2F, K] as stored ([gate | up]
 //      rows); the tile's B rows are gathered so that fragment pair (2c, 2c+1) of a wave is gate rows
@@ -167,35 +301,52 @@ __device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g))
 //      the epilogue reads g, u from aux = gu [M, 2F] and writes dgu = [dh·u·silu'(g) | dh·silu(g)].
 //      N = F.
 // Both round the GEMM result to bf16 first, exactly where the unfused path stores it.
-template <int BMT, int BN, bool BT, bool SPLIT, int EPI = 0>
-__global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, int lda, const bf16* __restrict__ B,
+// W4: Bv = g4w-packed NF4 codes of W ([N, K] when NT, [K, N] when BT, as W is stored), bscale =
+// decoded fp32 absmax transposed, [cols(W) / 64][rows(W)].
+template <int BMT, int BN, bool BT, bool SPLIT, int EPI, bool W4>
+__global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, int lda, const void* __restrict__ Bv,
                                                   int ldb, const bf16* __restrict__ residual, void* __restrict__ out,
                                                   int M, int N, int K, int splits, const bf16* __restrict__ aux,
                                                   bf16* __restrict__ aux_out, int F, float* __restrict__ ws,
-                                                  int* __restrict__ cnt) {
+                                                  const float* __restrict__ bscale) {
   static_assert(EPI == 0 || !SPLIT, "fused epilogues run on whole-K tiles");
   static_assert(EPI != 1 || !BT, "SwiGLU forward epilogue: NT only");
   static_assert(EPI != 2 || BT, "SwiGLU backward epilogue: the transposed-B dX only");
   static_assert(BMT == 256 || BMT == 128, "tile heights: 256, 128");
+  static_assert(!W4 || BN != 192, "W4: tile widths 128, 256");
   constexpr int NA = BMT / 32;                 // a fragments per wave per K-half
   constexpr int NB = BN / 32;                  // b fragments per wave per K-half
   constexpr int IMG_AT = BMT * BK * 2;
   constexpr int IMG_B = BN * BK * 2;
   constexpr int STAGE = IMG_AT + IMG_B;
-  constexpr int STAGES = 3 * STAGE <= 160 * 1024 ? 3 : 2;
+  constexpr int NLD = BN / 128;                // W4: 1 KB code DMAs per wave per K-tile
+  constexpr int CR_W = NLD * 1024 + 256;       // W4: a wave's codes + absmax of one K-tile (LDS ring)
+  constexpr int RING = W4 ? 2 * 4 * CR_W : 0;  // W4: two K-tiles of codes in flight
+  constexpr int STAGES = 3 * STAGE + RING <= 160 * 1024 ? 3 : 2;
   static_assert(BN == 128 || BN == 256 || (BN == 192 && !BT), "tile widths: 128, 256 (NT / BT), 192 (NT)");
   constexpr int KT = 2 * NA * NB;              // MFMAs per K-tile per wave
   constexpr int H = KT / 2;
   constexpr int R = NA + NB;                   // fragment-read items per K-half
   constexpr int DA = BMT / 32;                 // A DMAs per wave per K-tile
-  constexpr int DB = BN / 32;                  // B DMAs per wave per K-tile
+  constexpr int DB = W4 ? 0 : BN / 32;         // B DMAs per wave per K-tile
   constexpr int D = DA + DB;                   // all DMAs per wave per K-tile
+  constexpr int NCL = W4 ? NLD + 1 : 0;        // W4: LDS-DMAs per wave per K-tile for codes + absmax
+  constexpr int NCH = 4 * NLD;                 // W4: 8-element chunks a lane expands per K-tile
+  constexpr int KV = D + NCL;                  // vector-memory instructions per wave per K-tile
   constexpr bool BIG = NA == 8;
   constexpr int K1 = R + (BIG ? 9 : 1);        // barrier 1 after this MFMA
   constexpr int K2 = KT - R - 1;               // barrier 2 after this MFMA
   constexpr int DSP = (K2 - (BIG ? 10 : 2) - (K1 + 1)) / D;   // DMA spacing
   static_assert(DSP >= 1, "schedule");
-  __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE];
+  // W4 micro-op stream: 16 table ops, then 12 per chunk, spread evenly over MFMAs [M0S, KT - 1): the
+  // code DMAs of tile t + STAGES + 1 go on MFMAs 0 .. NCL-1, the wait + LDS reads of tile t + STAGES's
+  // codes on MFMA SW, the first micro-op 3 MFMAs later (the reads' latency)
+  constexpr int SW = NCL;
+  constexpr int M0S = SW + 3;
+  constexpr int NM = 16 + 12 * NCH;
+  constexpr int SPAN = KT - 1 - M0S;
+  static_assert(!W4 || M0S + (27 * SPAN) / NM > K1, "W4: the first chunk's ds_write must follow barrier 1");
+  __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE + RING];
 
   const int tiles_m = (M + BMT - 1) / BMT, tiles_n = (N + BN - 1) / BN;
   const int nwg = tiles_m * tiles_n * splits;
@@ -215,8 +366,9 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
 
   // ---- DMA sources (per-lane byte offsets; the K-tile step goes in the scalar offset)
   const rsrc_t rsa = make_rsrc(A, (uint64_t)((size_t)(M - 1) * lda + K) * 2);
-  const rsrc_t rsb = BT ? make_rsrc(B, (uint64_t)((size_t)(K - 1) * ldb + N) * 2)
-                        : make_rsrc(B, (uint64_t)((size_t)(N - 1) * ldb + K) * 2);
+  const rsrc_t rsb = W4 ? make_rsrc(Bv, (uint64_t)N * K / 2)
+                        : BT ? make_rsrc(Bv, (uint64_t)((size_t)(K - 1) * ldb + N) * 2)
+                             : make_rsrc(Bv, (uint64_t)((size_t)(N - 1) * ldb + K) * 2);
   uint32_t va[8], vb[8];   // (fixed sizes: a lambda capturing a template-sized local array drops the
                           // kernel's host-side instantiation — hipcc / clang, ROCm 7.2)
   {
@@ -226,7 +378,8 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
       const int ra = min(m0 + w * (BMT / 4) + i * 8 + r8, M - 1);
       va[i] = ((uint32_t)ra * (uint32_t)lda + (uint32_t)(kt0 * BK + c * 8)) * 2u;
     }
-    if constexpr (!BT) {
+    if constexpr (W4) {
+    } else if constexpr (!BT) {
 #pragma unroll
       for (int i = 0; i < DB; ++i) {   // B rows (BN/4)·w + 8i + r8
         int rb;
@@ -253,10 +406,58 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   }
   const uint32_t b_step = BT ? (uint32_t)BK * (uint32_t)ldb * 2u : (uint32_t)(BK * 2);
 
-  // ---- fragment read offsets
-  int lo[2];
+  // ---- W4: code / absmax DMA offsets and the LDS B-image chunk addresses of this lane's block
+  uint32_t w4c[2] = {0u, 0u}, w4s = 0u, w4cstep = 0u, w4sstep = 0u;
+  int w4o[8];
+  rsrc_t rss = rsb;
+  if constexpr (W4) {
+    const int hh = BN == 256 ? 0 : lane >> 5;   // BN = 128: the two lane halves take the block's k-halves
+    if constexpr (!BT) {   // lane = one W row (tile row rt) × the K-tile's 64 k: one quant block
+      const int rt = BN == 256 ? w * 64 + lane : w * 32 + (lane & 31);
+      int n;
+      if constexpr (EPI == 1) {
+        const int hr = min(tn * (BN / 2) + 16 * (rt >> 5) + (rt & 15), F - 1);
+        n = (rt & 16) ? F + hr : hr;
+      } else {
+        n = min(n0 + rt, N - 1);
+      }
+      const int KBw = K / 64;
 #pragma unroll
-  for (int s = 0; s < 2; ++s) lo[s] = ((lane >> 3) & 1) * 1024 + 16 * slot_of(lane & 7, 4 * s + (lane >> 4));
+      for (int j = 0; j < NLD; ++j)
+        w4c[j] = (uint32_t)((((n >> 6) * KBw + kt0) * 2 + (BN == 256 ? j : hh)) * 1024 + (n & 63) * 16);
+      w4cstep = 2048u;
+      w4s = (uint32_t)(kt0 * N + n) * 4u;
+      w4sstep = (uint32_t)N * 4u;
+      rss = make_rsrc(bscale, (uint64_t)N * (K / 64) * 4);
+      const int rl = rt - w * (BN / 4);   // row within the wave's BN/4 rows
+#pragma unroll
+      for (int u = 0; u < NCH; ++u)
+        w4o[u] = IMG_AT + w * (IMG_B / 4) + (rl >> 3) * 1024 + 16 * slot_of<true>(rl & 7, 4 * hh + u);
+    } else {   // lane = one W row (GEMM k-row kr of the tile) × 64 (or 32) W columns: one quant block
+      const int kr = 16 * w + (lane & 15);
+      const int cb = BN == 256 ? lane >> 4 : (lane >> 4) & 1;
+      const int KBw = N / 64;
+      const int kbw = min(n0 / 64 + cb, KBw - 1);
+#pragma unroll
+      for (int j = 0; j < NLD; ++j)
+        w4c[j] = (uint32_t)(((kt0 * KBw + kbw) * 2 + (BN == 256 ? j : hh)) * 1024 + kr * 16);
+      w4cstep = (uint32_t)KBw * 2048u;
+      w4s = (uint32_t)(kbw * K + kt0 * 64 + kr) * 4u;
+      w4sstep = 256u;
+      rss = make_rsrc(bscale, (uint64_t)K * (N / 64) * 4);
+      const int hk = (kr & 3) | ((kr >> 1) & 4);
+#pragma unroll
+      for (int u = 0; u < NCH; ++u) w4o[u] = IMG_AT + kr * (2 * BN) + 16 * ((8 * cb + 4 * hh + u) ^ (2 * hk));
+    }
+  }
+
+  // ---- fragment read offsets
+  int lo[2], lob[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    lo[s] = ((lane >> 3) & 1) * 1024 + 16 * slot_of<false>(lane & 7, 4 * s + (lane >> 4));
+    lob[s] = ((lane >> 3) & 1) * 1024 + 16 * slot_of<W4>(lane & 7, 4 * s + (lane >> 4));
+  }
   const int a_off = wr * NA * 2048;
   const int b_off = wc * NB * 2048;
   int boff_t[8];
@@ -299,8 +500,44 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
       const bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(pb + 4 * 2 * BN));
       fb[sched_of<NA, NB>().rd_i[r]] = bf16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
     } else {
-      fb[sched_of<NA, NB>().rd_i[r]] = lds_frag(st + IMG_AT + b_off + sched_of<NA, NB>().rd_i[r] * 2048 + lo[s]);
+      fb[sched_of<NA, NB>().rd_i[r]] = lds_frag(st + IMG_AT + b_off + sched_of<NA, NB>().rd_i[r] * 2048 + lob[s]);
     }
+  };
+
+  // W4: the codes + absmax of tile X are LDS-DMA'd (asm, counted by the explicit vmcnt waits like the A
+  // tiles) into ring slot X & 1 one K-tile before the tile that expands them reads them back — each lane
+  // its own 16-B pieces and dword, so the wave's own vmcnt orders them (no barrier)
+  const uint32_t ring = lds_base + STAGES * STAGE + (uint32_t)w * CR_W;
+  auto dma_code_item = [&](int slot, int t, int i) {
+    if (i < NLD) dma_lds(rsb, ring + slot * (4 * CR_W) + i * 1024, w4c[i], (uint32_t)t * w4cstep);
+    else dma_lds4(rss, ring + slot * (4 * CR_W) + NLD * 1024, w4s, (uint32_t)t * w4sstep);
+  };
+  auto dma_codes = [&](int slot, int t) {
+#pragma unroll
+    for (int i = 0; i < NCL; ++i) dma_code_item(slot, t, i);
+  };
+  u32x4 cq[2];
+  float csc = 0.f;
+  auto read_codes = [&](int slot) {
+    const char* rp = lds + STAGES * STAGE + slot * (4 * CR_W) + w * CR_W;
+#pragma unroll
+    for (int j = 0; j < NLD; ++j) cq[j] = *reinterpret_cast<const u32x4*>(rp + j * 1024 + lane * 16);
+    csc = *reinterpret_cast<const float*>(rp + NLD * 1024 + lane * 4);
+  };
+  W4St st4;
+  // micro-op J of the expansion of the codes in cq / csc into the stage at byte offset so
+  auto w4_mop = [&](auto j_c, uint32_t so) {
+    constexpr int J = decltype(j_c)::value;
+    if constexpr (J < 16) {
+      w4_table<J>(st4, csc);
+    } else {
+      constexpr int u = (J - 16) / 12, p = (J - 16) % 12;
+      w4_chunk<p>(st4, cq[u / 4][u % 4]);
+      if constexpr (p == 11) *reinterpret_cast<u32x4*>(lds + so + w4o[u]) = st4.o;
+    }
+  };
+  auto w4_all = [&](uint32_t so) {
+    Unroll<0, NM>::run([&](auto jc) { w4_mop(jc, so); });
   };
 
   if (nk <= 0) {
@@ -310,10 +547,29 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
       for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   } else {
     // prologue: tiles 0 .. STAGES-1 (clamped: past the last tile the DMAs re-stage tile nk-1 into
-    // stages nobody reads again), wait for tile 0, read its first half
+    // stages nobody reads again), wait for tile 0, read its first half.  W4: the B images of those
+    // tiles are expanded here first; then the vector-memory stream takes its steady-state order
+    // (the codes of tile STAGES ahead of the A DMAs of tile STAGES-1) so every counted wait below holds.
+    if constexpr (W4) {
 #pragma unroll
-    for (int s = 0; s < STAGES; ++s) dma_tile(s * STAGE, min(s, nk - 1));
-    wait_vmcnt<(STAGES - 1) * D>();
+      for (int s = 0; s < STAGES; ++s) {   // B images of tiles 0 .. STAGES-1, one at a time via ring slot 1
+        dma_codes(1, min(s, nk - 1));
+        wait_vmcnt<0>();
+        read_codes(1);
+        w4_all((uint32_t)(s * STAGE));
+      }
+#pragma unroll
+      for (int s = 0; s < STAGES; ++s) {
+        if (s == STAGES - 1) dma_codes(0, min(STAGES, nk - 1));
+        dma_tile(s * STAGE, min(s, nk - 1));
+      }
+      wait_vmcnt<(STAGES - 1) * DA + NCL>();
+      __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+    } else {
+#pragma unroll
+      for (int s = 0; s < STAGES; ++s) dma_tile(s * STAGE, min(s, nk - 1));
+      wait_vmcnt<(STAGES - 1) * D>();
+    }
     __builtin_amdgcn_s_barrier();
 #pragma unroll
     for (int r = 0; r < R; ++r) read_item(fa0, fb0, lds, 0, r);
@@ -321,7 +577,8 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
     int cur = 0;   // stage of tile t (byte offset)
     auto body = [&](auto first, int t) {
       const int tn_ = t + STAGES < nk ? t + STAGES : nk - 1;
-      char* const cs = lds + cur;
+      const int tc_ = t + STAGES + 1 < nk ? t + STAGES + 1 : nk - 1;
+      char* const cs_ = lds + cur;
       char* const ns = lds + (cur + STAGE == STAGES * STAGE ? 0 : cur + STAGE);
       Unroll<0, KT>::run([&](auto kc) {
         constexpr int k = decltype(kc)::value;
@@ -333,7 +590,20 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
           mfma_acc(acc[i][j], fb1[j], fa1[i]);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (k < R) read_item(fa1, fb1, cs, 1, k);
+        if constexpr (k < R) read_item(fa1, fb1, cs_, 1, k);
+        if constexpr (W4) {
+          if constexpr (k < NCL) dma_code_item((t + 1) & 1, tc_, k);
+          if constexpr (k == SW) {   // tile t + STAGES's codes (DMA'd one tile ago) have landed
+            wait_vmcnt<DA + NCL>();
+            read_codes(t & 1);
+          }
+          if constexpr (k >= M0S && k < M0S + SPAN) {
+            // micro-ops J with M0S + J·SPAN/NM == k
+            constexpr int jlo = ((k - M0S) * NM + SPAN - 1) / SPAN;
+            constexpr int jhi = ((k - M0S + 1) * NM + SPAN - 1) / SPAN;
+            Unroll<jlo, (jhi < NM ? jhi : NM)>::run([&](auto jc) { w4_mop(jc, (uint32_t)cur); });
+          }
+        }
         if constexpr (k == K1) {
           __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
           __builtin_amdgcn_s_barrier();
@@ -344,7 +614,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
           else dma_b(cur, tn_, d - DA);
         }
         if constexpr (k == K2) {
-          wait_vmcnt<(STAGES - 1) * D>();
+          wait_vmcnt<(STAGES - 1) * KV>();
           __builtin_amdgcn_s_barrier();
         }
         if constexpr (k > K2) read_item(fa0, fb0, ns, 0, k - K2 - 1);
@@ -382,14 +652,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
     }
     return;
   }
-  if constexpr (SPLIT) {
-    // Split-K, reduced in this launch by the LAST arriving split of the tile
-    // (cdna_hip_programming.md §5 "Projection GEMM" item 2): every split stores its fp32 slab, drains
-    // it (vmcnt(0) in every wave, barrier), and one lane releases at agent scope and takes a ticket;
-    // the split that draws splits-1 acquires at agent scope, adds the other slabs to its registers and
-    // runs the normal bf16 epilogue (residual included).  Correct for any placement of a tile's
-    // splits over XCDs; the ticket is reset by the last arriver (zeroed once at allocation).
-    float* wsf = ws;
+  if constexpr (SPLIT) {   // fp32 slab of this split; splitk_sum_k adds the slabs (+ residual)
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int m = m0 + wr * (BMT / 2) + i * 16 + (lane & 15);
@@ -397,43 +660,20 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         const int n = n0 + wc * (BN / 2) + j * 16 + 4 * (lane >> 4);
-        if (n < N) *reinterpret_cast<f32x4*>(wsf + ((size_t)sp * M + m) * N + n) = acc[i][j];
+        if (n < N) *reinterpret_cast<f32x4*>(ws + ((size_t)sp * M + m) * N + n) = acc[i][j];
       }
     }
-    if (cnt == nullptr) return;                // slabs only: splitk_sum_k reduces them
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* flag = reinterpret_cast<int*>(lds);   // the one LDS array (free: every DMA has landed)
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int old = __hip_atomic_fetch_add(cnt + tid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = old == splits - 1;
-      if (last) {
-        __hip_atomic_store(cnt + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      *flag = last;
-    }
-    __syncthreads();
-    if (*reinterpret_cast<volatile int*>(flag) == 0) return;
+    return;
   }
   // Epilogues that read global memory (residual; EPI 2's g / u) issue every load of four accumulator
   // rows before the first use, from clamped (always valid) addresses — one latency per four rows, not
   // one per 16×16 block (a load behind a per-block bounds branch waits vmcnt(0) each time)
   const bool has_res = EPI == 0 && residual != nullptr;
-  // rows per chunk: 4 (2 when a 256-wide tile also sums split-K slabs: register budget)
-  constexpr int RC = (SPLIT && NB >= 6) ? 2 : 4;   // (NA is 4 or 8: a multiple)
+  constexpr int RC = 4;   // rows per chunk (NA is 4 or 8: a multiple)
   auto rows = [&](auto hh_c, auto res_c) {
     constexpr int i0 = RC * decltype(hh_c)::value;
     constexpr bool RES = decltype(res_c)::value;
     bf16x4 la[RC][8], lb[RC][8];
-    f32x4 tot[RC][8];
-#pragma unroll
-    for (int ii = 0; ii < RC; ++ii)
-#pragma unroll
-      for (int j = 0; j < NB; ++j) tot[ii][j] = acc[i0 + ii][j];
 #pragma unroll
     for (int ii = 0; ii < RC; ++ii) {
       const int m = min(m0 + wr * (BMT / 2) + (i0 + ii) * 16 + (lane & 15), M - 1);
@@ -449,25 +689,6 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
         }
       }
     }
-    if constexpr (SPLIT) {   // the last arriver adds the other splits' slabs
-      for (int s2 = 0; s2 < splits; ++s2) {
-        if (s2 == sp) continue;
-        f32x4 pv[RC][8];
-#pragma unroll
-        for (int ii = 0; ii < RC; ++ii) {
-          const int m = min(m0 + wr * (BMT / 2) + (i0 + ii) * 16 + (lane & 15), M - 1);
-#pragma unroll
-          for (int j = 0; j < NB; ++j) {
-            const int n = min(n0 + wc * (BN / 2) + j * 16 + 4 * (lane >> 4), N - 4);
-            pv[ii][j] = *reinterpret_cast<const f32x4*>(ws + ((size_t)s2 * M + m) * N + n);
-          }
-        }
-#pragma unroll
-        for (int ii = 0; ii < RC; ++ii)
-#pragma unroll
-          for (int j = 0; j < NB; ++j) tot[ii][j] += pv[ii][j];
-      }
-    }
 #pragma unroll
     for (int ii = 0; ii < RC; ++ii) {
       const int m = m0 + wr * (BMT / 2) + (i0 + ii) * 16 + (lane & 15);
@@ -476,7 +697,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
       for (int j = 0; j < NB; ++j) {
         const int n = n0 + wc * (BN / 2) + j * 16 + 4 * (lane >> 4);
         if (n >= N) continue;
-        const f32x4 v = tot[ii][j];
+        const f32x4 v = acc[i0 + ii][j];
         if constexpr (EPI == 2) {
           bf16x4 dg, du;
 #pragma unroll
@@ -526,26 +747,50 @@ __global__ __launch_bounds__(256) void splitk_sum_k(const float* __restrict__ ws
   }
 }
 
+// bnb-layout NF4 codes [R][C/2] (element 2j in the high nibble of byte j) → the g4w layout
+// [R/64][C/64][2][64][16 B]: 16 B = elements 32h … 32h+31 of one row's block; in each dword (8 elements
+// 8c … 8c+7) byte j holds element j in its low nibble and element j + 4 in its high nibble
+__global__ __launch_bounds__(256) void pack_g4w_k(const uint8_t* __restrict__ src, uint32_t* __restrict__ dst, int R,
+                                                  int C) {
+  const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;   // one output dword
+  if (idx >= (size_t)R * C / 8) return;
+  const int d = idx & 3;
+  const int r = (idx >> 2) & 63;
+  const int h = (idx >> 8) & 1;
+  const size_t blk = idx >> 9;
+  const int CB = C / 64;
+  const int kb = blk % CB, g = blk / CB;
+  const int row = g * 64 + r, c0 = kb * 64 + 32 * h + 8 * d;
+  const uint8_t* s = src + (size_t)row * (C / 2) + c0 / 2;
+  uint32_t v = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const uint32_t nib = (e & 1) ? (s[e >> 1] & 15u) : (s[e >> 1] >> 4);
+    v |= nib << (8 * (e & 3) + 4 * (e >> 2));
+  }
+  dst[idx] = v;
+}
 
 int tiles_of(int M, int N, int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); }
 
 }  // namespace
 
-// bt: B given as [K, N] (row stride ldb) instead of [N, K]
-bool gemm4w_supported(int M, int N, int K, int lda, int ldb, bool bt) {
-  return M > 0 && K % BK == 0 && K >= BK && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
-         (uint64_t)M * lda * 2 < 0xFFFFFFFFull &&
-         (bt ? (uint64_t)K * ldb * 2 < 0xFFFFFFFFull : (uint64_t)N * ldb * 2 < 0xFFFFFFFFull);
+// bt: B given as [K, N] (row stride ldb) instead of [N, K]; w4: B = g4w-packed NF4 codes (the shape
+// of a bf16 W with ldb = its row length; rows and columns multiples of 64)
+bool gemm4w_supported(int M, int N, int K, int lda, int ldb, bool bt, bool w4) {
+  if (!(M > 0 && K % BK == 0 && K >= BK && N % 8 == 0 && lda % 8 == 0 && (uint64_t)M * lda * 2 < 0xFFFFFFFFull))
+    return false;
+  if (w4) return N % 64 == 0 && (uint64_t)N * K / 2 < 0xFFFFFFFFull;
+  return ldb % 8 == 0 && (bt ? (uint64_t)K * ldb * 2 < 0xFFFFFFFFull : (uint64_t)N * ldb * 2 < 0xFFFFFFFFull);
 }
 
 // Tile (height × width) and K-splits from one cost model: (rounds of 256 workgroups) × (K-tiles per
 // workgroup) × the measured in-step time of one K-tile of that tile (256 × 256: 1.5 µs,
-// transposed-B 1.52, 256 × 192: 1.22, 256 × 128: 0.92; the 128-high tiles ≈ 0.56 × those) + the split-K
+// transposed-B 1.52, 256 × 192: 1.22, 256 × 128: 0.92; the 128-high tiles ≈ 0.56 × those; W4 tiles
+// ×W4_COST, and 128-high W4 tiles — twice the expansion work per MFMA — ×W4_COST128) + the split-K
 // reduce launch (its fp32 slabs: M·N·(8s + 2) bytes at ≈12 TB/s effective + a launch).  At M = 2048
-// this picks: q|k|v fwd 256 × 192 (256 tiles); gate|up fwd / LM head 256 × 256; o fwd, the dX GEMMs to
-// d_model and down dX 128 × 256; down fwd and gate|up dX 256 × 256 with 2 splits.  At M = 1024 (the
-// sequential-GA micro-batches of the reference-faithful step) the 128-high tiles fill the chip without
-// split-K for q|k|v, o and their dX (profiles/r3/step_timeline_faithful_bm128.txt: splitk_sum_k launches 650 → 290 per step).
+// (bf16) this picks: q|k|v fwd 256 × 192 (256 tiles); gate|up fwd / LM head 256 × 256; o fwd, the dX
+// GEMMs to d_model and down dX 128 × 256; down fwd and gate|up dX 256 × 256 with 2 splits.
 // LIPA_GEMM4W_BN / LIPA_GEMM4W_BM / LIPA_GEMM4W_SPLITS force a choice.
 struct G4wCfg {
   int bm, bn, splits;
@@ -554,9 +799,14 @@ static int env_int(const char* name) {
   const char* e = getenv(name);
   return e ? atoi(e) : 0;
 }
-G4wCfg gemm4w_cfg(int M, int N, int K, bool bt, int bn_req, int sp_req, int bm_req) {
+static double env_dbl(const char* name, double d) {
+  const char* e = getenv(name);
+  return e ? atof(e) : d;
+}
+G4wCfg gemm4w_cfg(int M, int N, int K, bool bt, int bn_req, int sp_req, int bm_req, bool w4) {
   static const int forced_bn = env_int("LIPA_GEMM4W_BN"), forced_sp = env_int("LIPA_GEMM4W_SPLITS"),
                    forced_bm = env_int("LIPA_GEMM4W_BM");
+  static const double w4_cost = env_dbl("LIPA_W4_COST", 1.0), w4_cost128 = env_dbl("LIPA_W4_COST128", 1.35);
   if (bn_req == 0) bn_req = forced_bn;
   if (sp_req <= 0) sp_req = forced_sp;
   if (bm_req == 0) bm_req = forced_bm;
@@ -566,11 +816,12 @@ G4wCfg gemm4w_cfg(int M, int N, int K, bool bt, int bn_req, int sp_req, int bm_r
   for (int bm : {256, 128}) {
     if (bm_req && bm != bm_req) continue;
     for (int bn : {256, 192, 128}) {
-      if (bn == 192 && bt) continue;
+      if (bn == 192 && (bt || w4)) continue;
       if (bn_req && bn != bn_req) continue;
       const int tiles = tiles_of(M, N, bm, bn);
       double kt_us = bn == 256 ? (bt ? 1.52 : 1.5) : bn == 192 ? 1.22 : 0.92;
       if (bm == 128) kt_us *= 0.56;
+      if (w4) kt_us *= bm == 128 ? w4_cost128 : w4_cost;
       for (int s = 1; s <= 8; s *= 2) {
         if (sp_req > 0 && s != sp_req) continue;
         if (s > 1 && sp_req <= 0 && nk / s < 8) break;
@@ -589,8 +840,8 @@ G4wCfg gemm4w_cfg(int M, int N, int K, bool bt, int bn_req, int sp_req, int bm_r
 
 // bn / splits / bm: 0 = chosen by gemm4w_cfg.  Returns the split count used (the caller's fp32
 // workspace must hold splits·M·N floats when it is > 1) and the tile through bn_out / bm_out.
-int gemm4w_plan(int M, int N, int K, bool bt, int bn, int splits, int* bn_out, int bm, int* bm_out) {
-  const G4wCfg c = gemm4w_cfg(M, N, K, bt, bn, splits, bm);
+int gemm4w_plan(int M, int N, int K, bool bt, int bn, int splits, int* bn_out, int bm, int* bm_out, bool w4) {
+  const G4wCfg c = gemm4w_cfg(M, N, K, bt, bn, splits, bm, w4);
   if (bn_out) *bn_out = c.bn;
   if (bm_out) *bm_out = c.bm;
   return c.splits;
@@ -598,29 +849,31 @@ int gemm4w_plan(int M, int N, int K, bool bt, int bn, int splits, int* bn_out, i
 
 int gemm4w_tiles(int M, int N, int bm, int bn) { return tiles_of(M, N, bm, bn); }
 
-// ws: splits·M·N fp32 slabs, cnt: one zero-initialised int per tile (both only when splits > 1);
-// cnt == nullptr: the slabs are summed by a separate splitk_sum_k launch instead of the last arriver.
-// Callers pass the (bm, bn, splits) that gemm4w_plan returned.
+// ws: splits·M·N fp32 slabs (splits > 1).  Callers pass the (bm, bn, splits) that gemm4w_plan
+// returned.  bscale != nullptr: B is g4w-packed NF4 codes, bscale the transposed fp32 block absmax.
 void launch_gemm4w(const void* A, int lda, const void* B, int ldb, const void* residual, void* out, float* ws,
-                   int* cnt, int M, int N, int K, int splits, bool bt, int bn, int bm, hipStream_t st) {
+                   const float* bscale, int M, int N, int K, int splits, bool bt, int bn, int bm, hipStream_t st) {
   const int tiles = tiles_of(M, N, bm, bn);
   const bool split = splits > 1;
   const bf16* a = (const bf16*)A;
-  const bf16* b = (const bf16*)B;
   const bf16* r = (const bf16*)residual;
   void* o = out;
   const int grid = tiles * (split ? splits : 1), sp = split ? splits : 1;
-#define G4W(BM_, BN_, BT_, SP_) \
-  gemm4w_k<BM_, BN_, BT_, SP_><<<grid, NT, 0, st>>>(a, lda, b, ldb, r, o, M, N, K, sp, nullptr, nullptr, 0, ws, cnt)
-#define G4W_BN(BM_)                                                                \
-  if (bn == 256) {                                                                 \
-    if (bt) { if (split) G4W(BM_, 256, true, true); else G4W(BM_, 256, true, false); }   \
-    else { if (split) G4W(BM_, 256, false, true); else G4W(BM_, 256, false, false); }    \
-  } else if (bn == 192) {                                                          \
-    if (split) G4W(BM_, 192, false, true); else G4W(BM_, 192, false, false);       \
-  } else {                                                                         \
-    if (bt) { if (split) G4W(BM_, 128, true, true); else G4W(BM_, 128, true, false); }   \
-    else { if (split) G4W(BM_, 128, false, true); else G4W(BM_, 128, false, false); }    \
+#define G4W(BM_, BN_, BT_, SP_, W4_)                                                                            \
+  gemm4w_k<BM_, BN_, BT_, SP_, 0, W4_><<<grid, NT, 0, st>>>(a, lda, B, ldb, r, o, M, N, K, sp, nullptr, nullptr, \
+                                                             0, ws, bscale)
+#define G4W_SP(BM_, BN_, BT_, W4_) \
+  if (split) G4W(BM_, BN_, BT_, true, W4_); else G4W(BM_, BN_, BT_, false, W4_);
+#define G4W_BN(BM_)                                                                           \
+  if (bscale) {                                                                               \
+    if (bn == 256) { if (bt) { G4W_SP(BM_, 256, true, true) } else { G4W_SP(BM_, 256, false, true) } } \
+    else { if (bt) { G4W_SP(BM_, 128, true, true) } else { G4W_SP(BM_, 128, false, true) } }           \
+  } else if (bn == 256) {                                                                     \
+    if (bt) { G4W_SP(BM_, 256, true, false) } else { G4W_SP(BM_, 256, false, false) }         \
+  } else if (bn == 192) {                                                                     \
+    G4W_SP(BM_, 192, false, false)                                                            \
+  } else {                                                                                    \
+    if (bt) { G4W_SP(BM_, 128, true, false) } else { G4W_SP(BM_, 128, false, false) }         \
   }
   if (bm == 256) {
     G4W_BN(256)
@@ -628,8 +881,9 @@ void launch_gemm4w(const void* A, int lda, const void* B, int ldb, const void* r
     G4W_BN(128)
   }
 #undef G4W_BN
+#undef G4W_SP
 #undef G4W
-  if (split && cnt == nullptr) {
+  if (split) {
     const size_t MN = (size_t)M * N;
     const int blocks = (int)std::min<size_t>((MN / 8 + 255) / 256, 2048);
     splitk_sum_k<<<blocks, 256, 0, st>>>(ws, (const bf16*)residual, (bf16*)out, MN, splits);
@@ -638,38 +892,48 @@ void launch_gemm4w(const void* A, int lda, const void* B, int ldb, const void* r
 }
 
 // gu [M, 2F] and h = silu(gate)·up [M, F] from x [M, K] and W_gu [2F, K] ([gate | up] rows), one launch
-void launch_gemm4w_swiglu(const void* X, int ldx, const void* W, void* gu, void* h, int M, int F, int K, int bn,
-                          int bm, hipStream_t st) {
+void launch_gemm4w_swiglu(const void* X, int ldx, const void* W, const float* wscale, void* gu, void* h, int M, int F,
+                          int K, int bn, int bm, hipStream_t st) {
   const int N = 2 * F;
   const int tiles = tiles_of(M, N, bm, bn);
   const bf16* a = (const bf16*)X;
-  const bf16* b = (const bf16*)W;
-#define G4S(BM_, BN_)                                                                                          \
-  gemm4w_k<BM_, BN_, false, false, 1><<<tiles, NT, 0, st>>>(a, ldx, b, K, nullptr, gu, M, N, K, 1, nullptr,    \
-                                                            (bf16*)h, F, nullptr, nullptr)
-  if (bm == 256) {
-    if (bn == 256) G4S(256, 256); else if (bn == 192) G4S(256, 192); else G4S(256, 128);
+#define G4S(BM_, BN_, W4_)                                                                                        \
+  gemm4w_k<BM_, BN_, false, false, 1, W4_><<<tiles, NT, 0, st>>>(a, ldx, W, K, nullptr, gu, M, N, K, 1, nullptr, \
+                                                                  (bf16*)h, F, nullptr, wscale)
+  if (wscale) {
+    if (bm == 256) { if (bn == 256) G4S(256, 256, true); else G4S(256, 128, true); }
+    else { if (bn == 256) G4S(128, 256, true); else G4S(128, 128, true); }
+  } else if (bm == 256) {
+    if (bn == 256) G4S(256, 256, false); else if (bn == 192) G4S(256, 192, false); else G4S(256, 128, false);
   } else {
-    if (bn == 256) G4S(128, 256); else if (bn == 192) G4S(128, 192); else G4S(128, 128);
+    if (bn == 256) G4S(128, 256, false); else if (bn == 192) G4S(128, 192, false); else G4S(128, 128, false);
   }
 #undef G4S
   LIPA_CHECK_LAUNCH();
 }
 
 // dgu [M, 2F] = SwiGLU-backward(dh = dY·W_down, gu) with W_down [N_w, F] used as stored, one launch
-void launch_gemm4w_dswiglu(const void* DY, int lddy, const void* W, const void* gu, void* dgu, int M, int F, int Nw,
-                           int bn, int bm, hipStream_t st) {
+void launch_gemm4w_dswiglu(const void* DY, int lddy, const void* W, const float* wscale, const void* gu, void* dgu,
+                           int M, int F, int Nw, int bn, int bm, hipStream_t st) {
   const int tiles = tiles_of(M, F, bm, bn);
   const bf16* a = (const bf16*)DY;
-  const bf16* b = (const bf16*)W;
-#define G4D(BM_, BN_)                                                                                        \
-  gemm4w_k<BM_, BN_, true, false, 2><<<tiles, NT, 0, st>>>(a, lddy, b, F, nullptr, dgu, M, F, Nw, 1,         \
-                                                           (const bf16*)gu, nullptr, F, nullptr, nullptr)
-  if (bm == 256) {
-    if (bn == 256) G4D(256, 256); else G4D(256, 128);
+#define G4D(BM_, BN_, W4_)                                                                                        \
+  gemm4w_k<BM_, BN_, true, false, 2, W4_><<<tiles, NT, 0, st>>>(a, lddy, W, F, nullptr, dgu, M, F, Nw, 1,        \
+                                                                 (const bf16*)gu, nullptr, F, nullptr, wscale)
+  if (wscale) {
+    if (bm == 256) { if (bn == 256) G4D(256, 256, true); else G4D(256, 128, true); }
+    else { if (bn == 256) G4D(128, 256, true); else G4D(128, 128, true); }
+  } else if (bm == 256) {
+    if (bn == 256) G4D(256, 256, false); else G4D(256, 128, false);
   } else {
-    if (bn == 256) G4D(128, 256); else G4D(128, 128);
+    if (bn == 256) G4D(128, 256, false); else G4D(128, 128, false);
   }
 #undef G4D
+  LIPA_CHECK_LAUNCH();
+}
+
+void launch_pack_g4w(const uint8_t* codes, void* out, int R, int C, hipStream_t st) {
+  const size_t n = (size_t)R * C / 8;
+  pack_g4w_k<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(codes, (uint32_t*)out, R, C);
   LIPA_CHECK_LAUNCH();
 }

@@ -7,16 +7,18 @@ One op covers every projection of the stack:
 * ``base`` is a bf16 ``[N, K]`` tensor (LoRA / full fine-tune) or an :class:`NF4Weight`
   (QLoRA).  Several projections that share an input (q|k|v, gate|up) are row-concatenated
   into one base and one GEMM; each LoRA branch owns a column range ``[c0, c1)``.
-* What runs at training / prefill sizes (M ≥ 256), the default:
-  - an NF4 base is expanded to bf16 once per call (``nf4_dequant3_k``, HBM speed; inside
-    checkpointed layers once per optimizer step) and the copy is kept for the backward;
+* What runs at training / prefill sizes, the default:
   - the base GEMM is the hand-written one-wave-per-SIMD MFMA kernel ``gemm4w`` (forward x·Wᵀ with
     the residual in its epilogue; backward dY·W reading W as stored — the transposed-B form);
+  - an NF4 base (K9) takes one of two forms, chosen per call (``_nf4_w4``): the NF4 dequant-GEMM —
+    gemm4w reads the 4-bit codes (``NF4Weight.g4w_pack``) and expands each quant block to bf16
+    between the load and its LDS B image, no bf16 copy of the base anywhere — or one HBM-speed
+    expansion (``nf4_dequant3_k``) whose bf16 copy serves the forward AND the dX GEMM;
   - the LoRA branches run in ``lora.hip``: ``lora_proj2`` (both q/v adapters' s·D(x)·Aᵀ in one pass,
     keep bits stored), ``lora_apply`` (xa·Bᵀ added into the adapters' column blocks of the GEMM
     output), and in backward ``lora_proj_pair`` / ``lora_acc_pair`` / ``lora_dx2`` (the LoRA dX term
     enters the dX GEMM as its C matrix) / ``lora_dA_pair``.
-  ``LIPA_GEMM=lt`` swaps the base GEMMs for direct hipBLASLt calls; decode sizes (M ≤ 16) use the
+  ``LIPA_GEMM=lt`` swaps the bf16 base GEMMs for direct hipBLASLt calls; decode sizes (M ≤ 16) use the
   split-K weight-streaming kernels (``skinny.hip``, ``gemv_w4``).
 * The SwiGLU MLP block bypasses this op when it carries no adapters (``ops/mlp.py``).
 
@@ -26,6 +28,7 @@ Reference parity: PEFT ``LoraConfig(r, lora_alpha, lora_dropout, target_modules)
 from __future__ import annotations
 
 import dataclasses
+import os
 
 import torch
 import torch.nn.functional as F
@@ -35,74 +38,119 @@ from ._native import native, use_native
 
 EXT_ALIGN = 32   # the kernels consume the LoRA K-slice in MFMA K-steps of 32
 # LIPA_DENSE_GEMM=native: frozen bf16 bases through gemm_bf16w / gemm_bf16_t instead of hipBLASLt
-_NATIVE_DENSE = __import__("os").environ.get("LIPA_DENSE_GEMM", "") == "native"
-# NF4 bases at training / prefill sizes (M > 8; decode uses the NF4 GEMV):
-#  "dequant" (default) — nf4_dequant2_k expands the layer's 4-bit weight to bf16 once per step
-#    at HBM speed, the copy is kept for the backward dX GEMM and freed with the autograd graph
-#    (≈14 GB for Qwen3-8B: memory the 288 GB part has), and hipBLASLt runs fwd + dX at
-#    1.1-1.5 PFLOP/s: 76.7 vs 82.9 ms per Qwen3-8B QLoRA step (profiles/nf4_dequant_vs_fused_ab.txt);
-#  "fused" — the register-dequant MFMA GEMMs (gemm_w4v2, LoRA K-slice + residual epilogue):
-#    no bf16 copy at all, for memory-bound deployments.
-_NF4_MODE = __import__("os").environ.get("LIPA_NF4_GEMM", "dequant")
+_NATIVE_DENSE = os.environ.get("LIPA_DENSE_GEMM", "") == "native"
 # LoRA B term as an in-place column-block update after the base GEMM (LIPA_LORA_APPLY=0: K-slice form)
-_APPLY = __import__("os").environ.get("LIPA_LORA_APPLY", "1") != "0"
+_APPLY = os.environ.get("LIPA_LORA_APPLY", "1") != "0"
 # training-sized bf16 base GEMMs through direct hipBLASLt calls (csrc/kernels/blaslt.hip): the
 # residual as a separate C matrix (no copy into the output first) and a per-shape kernel choice
 # timed in the running step; LIPA_LT=0: torch.addmm / torch.mm / torch.bmm
-_LT = __import__("os").environ.get("LIPA_LT", "1") != "0"
+_LT = os.environ.get("LIPA_LT", "1") != "0"
 _LT_MIN_M = 256
 # training-sized frozen-base GEMMs (forward x·Wᵀ and backward dY·W) through the hand-written
 # one-wave-per-SIMD MFMA kernel (csrc/kernels/gemm4w.hip); LIPA_GEMM=lt: direct hipBLASLt
-_G4W = __import__("os").environ.get("LIPA_GEMM", "native") == "native"
+_G4W = os.environ.get("LIPA_GEMM", "native") == "native"
 
 
 def _g4w_ok(a: torch.Tensor, w: torch.Tensor, bt: bool) -> bool:
-    """Shapes / strides the gemm4w kernel takes: a [M, K] row-major (row stride % 8), w [N, K]
-    (or [K, N] when bt) contiguous, K % 64, N % 8, 16-B aligned, training-sized M."""
+    """Shapes / strides the gemm4w kernel takes for a bf16 weight: a [M, K] row-major (row stride % 8),
+    w [N, K] (or [K, N] when bt) with unit inner stride, training-sized M — the same predicate the
+    binding enforces (``gemm4w_supported``: K % 64, N % 8, every operand's byte extent < 4 GiB), so an
+    oversized operand falls back here instead of failing in the kernel's TORCH_CHECK."""
     if not (_G4W and a.is_cuda and a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and a.dim() == 2
-            and a.shape[0] >= _LT_MIN_M and a.stride(1) == 1 and a.stride(0) % 8 == 0 and w.is_contiguous()):
+            and w.dim() == 2 and a.shape[0] >= _LT_MIN_M and a.stride(1) == 1 and w.stride(1) == 1
+            and a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0):
         return False
     K = a.shape[1]
+    if (w.shape[0] if bt else w.shape[1]) != K:
+        return False
     N = w.shape[1] if bt else w.shape[0]
-    return ((w.shape[0] if bt else w.shape[1]) == K and K % 64 == 0 and N % 8 == 0 and a.data_ptr() % 16 == 0
-            and w.data_ptr() % 16 == 0)
-# q_proj + v_proj with dropout: the forward's lora_proj2 stores the keep bits (1 bit per element and
-# branch) and lora_acc2 reads them instead of re-hashing; LIPA_LORA_KEEP_BITS=0: regenerate
-_KEEP_BITS = __import__("os").environ.get("LIPA_LORA_KEEP_BITS", "1") != "0"
-# two-branch backward launches (lora_proj_pair / lora_acc_pair); LIPA_LORA_PAIR_BWD=0: per-branch
-_PAIR_BWD = __import__("os").environ.get("LIPA_LORA_PAIR_BWD", "1") != "0"
-# q+v dropout pair backward: the LoRA dx term as the dX GEMM's C matrix + a separate dA launch
-# (LIPA_LORA_DX_C=0: the fused read-modify-write lora_acc2 pass over dx)
-_DX_C = __import__("os").environ.get("LIPA_LORA_DX_C", "1") != "0"
+    return bool(native().gemm4w_ok(a.shape[0], N, K, a.stride(0), w.stride(0), bt, False))
+
+
+def _w4_ok(a: torch.Tensor, q: NF4Weight, bt: bool) -> bool:
+    """An NF4 base the gemm4w kernel reads as codes (K9): forward x·deq(W)ᵀ (bt=False, a [M, K_w]) or
+    dX = dY·deq(W) (bt=True, a [M, N_w]); blocksize 64, both dims multiples of 64, M > 8."""
+    if not (_G4W and a.is_cuda and a.dtype == torch.bfloat16 and a.dim() == 2 and a.shape[0] > 8
+            and a.stride(1) == 1 and a.data_ptr() % 16 == 0 and q.kernel_ok()):
+        return False
+    n, k = q.shape
+    if a.shape[1] != (n if bt else k):
+        return False
+    return bool(native().gemm4w_ok(a.shape[0], k if bt else n, a.shape[1], a.stride(0), 0, bt, True))
+
+
+def _w4_gemm(a: torch.Tensor, q: NF4Weight, bt: bool, c: torch.Tensor | None = None) -> torch.Tensor:
+    """gemm4w on NF4 codes: a·deq(W)ᵀ (+ c) or, bt, a·deq(W) (+ c)."""
+    codes, sc = q.g4w_pack()
+    n, k = q.shape
+    return native().gemm4w(a, codes, c, 0, bt, 0, 0, sc, k if bt else n)
+
+
+def _nf4_dequant_bf16(q: NF4Weight) -> torch.Tensor:
+    """One bf16 expansion of an NF4 base (HBM speed)."""
+    n, k = q.shape
+    return native().nf4_dequant_fast(q.codes, q.gemv_scales(), n, k)
+
+
+# Which NF4 form a call takes (LIPA_NF4_GEMM = w4 | expand | auto).  Measured per GEMM at the Qwen3-8B
+# shapes (profiles/r4/gemm4w_nf4_ab.txt): the in-kernel expansion costs 1.1-1.2x the bf16 gemm4w time
+# (the 3-VALU-per-element table lookup is only partly hidden beside 16x16x32 MFMAs), the same as an
+# expansion + bf16 GEMM when that copy serves ONE GEMM.  "auto" therefore expands where the copy is
+# reused — a training forward whose backward needs dX (the copy is kept for it: ≈14 GB transient for
+# Qwen3-8B), a checkpointed layer (one expansion per optimizer step, below) — and feeds the codes
+# straight in everywhere else (inference, no-grad prefill, frozen inputs): no transient bf16 weights.
+# "w4" everywhere is the memory-lean training mode (peak HBM ≈ the 4-bit model + activations).
+_NF4_MODE = os.environ.get("LIPA_NF4_GEMM", "auto")
+
+
+def _nf4_w4(reused: bool) -> bool:
+    if _NF4_MODE == "w4":
+        return True
+    if _NF4_MODE == "expand":
+        return False
+    return not (reused or _IN_CKPT[0])
 
 
 # NF4-aware activation checkpointing: inside a checkpointed layer (its forward AND its backward
 # recompute) the bf16 expansion of each frozen NF4 base is made once per optimizer step and reused —
 # the reference-faithful step (gradient checkpointing + sequential GA micro-steps) otherwise expands
-# every weight 2 × GA times per step instead of once.  The optimizer's step() advances the epoch
-# (optim/adamw.py, parallel/zero.py), dropping the step's copies.  LIPA_CKPT_NF4_CACHE=0: off.
-_CKPT_CACHE = __import__("os").environ.get("LIPA_CKPT_NF4_CACHE", "1") != "0"
+# every weight 2 × GA times per step.  The copies are held in ONE registry, bounded by
+# LIPA_CKPT_NF4_CACHE_GB (default 32; 0 = off: every call expands), and released eagerly when the
+# optimizer steps (``nf4_cache_advance``: optim/adamw.py, parallel/zero.py; an optimizer that never
+# calls it keeps at most the budget).  Memory: the budget is the cost — Qwen3-8B's bases expand to
+# 13.9 GB (peak HBM of the faithful bench step: README §3).
+_CKPT_BUDGET = float(os.environ.get("LIPA_CKPT_NF4_CACHE_GB", "32")) * 2 ** 30
 _IN_CKPT = [0]
-_EPOCH = [0]
+_CACHE: dict = {}        # id(NF4Weight) -> (weight, bf16 expansion)
+_CACHE_BYTES = [0]
 
 
 def nf4_cache_advance():
     """Called by the optimizers at every step: the expanded copies of the finished step are released."""
-    _EPOCH[0] += 1
+    _CACHE.clear()
+    _CACHE_BYTES[0] = 0
 
 
-def _nf4_dequant_bf16(q: NF4Weight) -> torch.Tensor:
-    if _CKPT_CACHE and _IN_CKPT[0]:
-        hit = getattr(q, "_lipa_bf16", None)
-        if hit is not None and hit[0] == _EPOCH[0]:
+def _nf4_expand(q: NF4Weight) -> torch.Tensor:
+    """The bf16 expansion for the "expand" form (cached inside checkpointed layers, see above)."""
+    if _IN_CKPT[0]:
+        hit = _CACHE.get(id(q))
+        if hit is not None and hit[0] is q:
             return hit[1]
-    n, k = q.shape
-    w = native().nf4_dequant_fast(q.codes, q.gemv_scales(), n, k)
-    if _CKPT_CACHE and _IN_CKPT[0]:
-        q._lipa_bf16 = (_EPOCH[0], w)
-    elif getattr(q, "_lipa_bf16", None) is not None:
-        q._lipa_bf16 = None
+    w = _nf4_dequant_bf16(q)
+    if _IN_CKPT[0] and _CACHE_BYTES[0] + w.numel() * 2 <= _CKPT_BUDGET:
+        _CACHE[id(q)] = (q, w)
+        _CACHE_BYTES[0] += w.numel() * 2
     return w
+
+
+# LoRA kernel forms (the A/B-measured winners of round 2, fixed; profiles/lora_acc_mfma_ab.txt):
+# q_proj + v_proj with dropout — the forward's lora_proj2 stores the keep bits (1 bit per element and
+# branch) for the backward instead of re-hashing; two-branch backward launches (lora_proj_pair /
+# lora_acc_pair); the LoRA dX term as the dX GEMM's C matrix + a separate dA launch
+_KEEP_BITS = True
+_PAIR_BWD = True
+_DX_C = True
 
 
 @dataclasses.dataclass
@@ -125,12 +173,7 @@ def _pad_cols(t: torch.Tensor, mult: int = EXT_ALIGN) -> torch.Tensor:
 
 def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
     if isinstance(base, NF4Weight):
-        if not base.kernel_ok():      # odd shapes: dequantise then library GEMM
-            y = x @ dequantize_nf4(base, x.dtype).t()
-            if ext_a is not None:
-                y = y + ext_a @ ext_b.t()
-            return y if residual is None else y + residual
-        if x.shape[0] <= 8:           # decode: weight-streaming GEMV, no MFMA tile
+        if x.shape[0] <= 8 and base.kernel_ok():   # decode: weight-streaming GEMV, no MFMA tile
             n, k = base.shape
             y = native().gemv_w4(x, base.codes, base.gemv_scales(), None, n, base.blocksize,
                                  residual if ext_a is None else None)
@@ -139,8 +182,11 @@ def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
                 if residual is not None:
                     y = y + residual
             return y
-        cf, _, at = base.kernel_pack()
-        return native().gemm_nf4(x, cf, at, base.shape[0], ext_a, ext_b, residual)
+        if _w4_ok(x, base, False):                  # the NF4 dequant-GEMM (gemm4w reads the codes)
+            y = _w4_gemm(x, base, False, None if residual is None else residual.contiguous())
+            return y if ext_a is None else y.addmm_(ext_a, ext_b.t())
+        w = _nf4_dequant_bf16(base) if (base.kernel_ok() and x.is_cuda) else dequantize_nf4(base, x.dtype)
+        return _base_gemm(x, w, ext_a, ext_b, residual)
     M, K = x.shape
     N = base.shape[0]
     if (M <= 16 and N <= 8192 and K <= 8192 and N % 16 == 0 and K % 64 == 0 and x.stride(0) % 8 == 0
@@ -170,7 +216,7 @@ def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
     return native().gemm_bf16(x, base, ext_a, ext_b, residual)
 
 
-_SPLIT_ENV = int(__import__("os").environ.get("LIPA_DX_SPLIT", "0"))   # 0: auto; 1, 2, 4, 8: forced
+_SPLIT_ENV = int(os.environ.get("LIPA_DX_SPLIT", "0"))   # 0: auto; 1, 2, 4, 8: forced
 
 
 def _dx_split(dy: torch.Tensor, w: torch.Tensor) -> int:
@@ -207,14 +253,21 @@ def _dense_dx(dy: torch.Tensor, w: torch.Tensor, tune: bool = True) -> torch.Ten
     return dy @ w
 
 
-def _base_gemm_t(dy, base, ext_a=None, ext_b=None):
-    """dX = dY·W (+ ext_a · ext_bᵀ, ext_b given as [K, R])."""
+def _base_gemm_t(dy, base, ext_a=None, ext_b=None, c=None):
+    """dX = dY·W (+ c) (+ ext_a · ext_bᵀ, ext_b given as [K, R])."""
     if isinstance(base, NF4Weight):
-        if not base.kernel_ok():
-            dx = dy @ dequantize_nf4(base, dy.dtype)
-            return dx if ext_a is None else dx + ext_a @ ext_b.t()
-        _, cb, at = base.kernel_pack()
-        return native().gemm_nf4_t(dy, cb, at, base.shape[1], ext_a, ext_b)
+        if _w4_ok(dy, base, True):
+            dx = _w4_gemm(dy, base, True, c)
+            return dx if ext_a is None else dx.addmm_(ext_a, ext_b.t())
+        base = _nf4_dequant_bf16(base) if (base.kernel_ok() and dy.is_cuda) else dequantize_nf4(base, dy.dtype)
+    if c is not None:
+        if _g4w_ok(dy, base, True) and not _NATIVE_DENSE:
+            dx = native().gemm4w(dy, base, c, 0, True)
+        elif _LT and dy.shape[0] >= _LT_MIN_M and dy.is_cuda and _dx_split(dy, base) == 1 and not _NATIVE_DENSE:
+            dx = native().lt_dx(dy.contiguous(), base.contiguous(), 1, True, c)
+        else:
+            dx = _dense_dx(dy, base) + c
+        return dx if ext_a is None else dx.addmm_(ext_a, ext_b.t())
     if not _NATIVE_DENSE:
         dx = _dense_dx(dy, base)
         return dx if ext_a is None else dx.addmm_(ext_a, ext_b.t())
@@ -259,7 +312,7 @@ def seed_dropout(seed: int):
     _KEY[0] = (int(seed) * 0x2545F4914F6CDD1D) & 0x7FFFFFFFFFFFFFFF
 
 
-_CKPT_REENTRANT = __import__("os").environ.get("LIPA_CKPT_REENTRANT", "1") == "1"
+_CKPT_REENTRANT = os.environ.get("LIPA_CKPT_REENTRANT", "1") == "1"
 
 
 def checkpoint(fn, *args):
@@ -341,7 +394,7 @@ def _zero_buffer(tag: str, rows: int, cols: int, like: torch.Tensor) -> torch.Te
 def _pair_ok(x, branches) -> bool:
     """Two rank-<=8 adapters on one fused projection (q_proj + v_proj): the two-branch kernels."""
     return (len(branches) == 2 and x.is_cuda and all(br.a.shape[0] <= 8 for br in branches)
-            and __import__("os").environ.get("LIPA_LORA_PAIR", "1") != "0")
+            and os.environ.get("LIPA_LORA_PAIR", "1") != "0")
 
 
 def _fast_lora_ok(x, branches) -> bool:
@@ -431,9 +484,10 @@ class _FusedLinearFn(torch.autograd.Function):
             if not fast:
                 ext_a = _pad_cols(torch.cat(cols, 1))
         wdq = None
-        if not dense and _NF4_MODE == "dequant" and x.shape[0] > 8 and base.kernel_ok():
-            wdq = _nf4_dequant_bf16(base)
+        if not dense and x.shape[0] > 8 and base.kernel_ok() and x.is_cuda and not _nf4_w4(ctx.needs_input_grad[0]):
+            wdq = _nf4_expand(base)     # the expand form: this copy also serves the dX GEMM
         y = _base_gemm(x, wdq if wdq is not None else (base if not dense else weight), ext_a, ext_b, residual)
+        ctx.wdq = wdq if ctx.needs_input_grad[0] else None
         ctx.bts = None
         if apply:
             bs = [bf16_view(b, x.dtype) for b in ab[1::2]]
@@ -443,7 +497,6 @@ class _FusedLinearFn(torch.autograd.Function):
             ctx.bts = bts or None
             if not need_xa:
                 xa_list = [None] * len(xa_list)
-        ctx.wdq = wdq if ctx.needs_input_grad[0] else None
         if bias is not None:
             y = y + bias
         ctx.meta = meta
@@ -538,17 +591,15 @@ class _FusedLinearFn(torch.autograd.Function):
             wb = ctx.wdq if ctx.wdq is not None else (base if not dense else weight)
             pair_ok = (ctx.pair and all(k is not None for k in ctx.keys) and not deterministic()
                        and ctx.needs_input_grad[5] and ctx.needs_input_grad[7])
-            g4w = _g4w_ok(dy, wb, True) if isinstance(wb, torch.Tensor) else False
-            if (pair_ok and _DX_C and ctx.masks is not None and not fold and isinstance(wb, torch.Tensor)
-                    and not _NATIVE_DENSE and dy.shape[0] >= _LT_MIN_M and (g4w or (_LT and _dx_split(dy, wb) == 1))):
+            if (pair_ok and _DX_C and ctx.masks is not None and not fold and dy.shape[0] >= _LT_MIN_M
+                    and not _NATIVE_DENSE):
                 # the LoRA input-gradient term written once (lora_dx2, from the stored keep bits) and
                 # added by the dX GEMM as its C matrix; dA from x in a separate launch — no
                 # read-modify-write pass over dx (lora_acc2)
                 a0, a1 = bf16_view(ab[0], dy.dtype), bf16_view(ab[2], dy.dtype)
                 p0, p1 = branches[0].dropout, branches[1].dropout
                 c = native().lora_dx2(g_list[0], g_list[1], a0, a1, ctx.masks, p0, p1)
-                dx = (native().gemm4w(dy, wb, c, 0, True) if g4w else
-                      native().lt_dx(dy.contiguous(), wb.contiguous(), 1, True, c))
+                dx = _base_gemm_t(dy, wb, None, None, c)
                 del c
                 (o0, ret0), (o1, ret1) = dest(0), dest(2)
                 native().lora_dA_pair(g_list[0], g_list[1], x, o0, o1, ctx.masks, p0, p1)

@@ -15,8 +15,8 @@ Per Qwen3-8B layer at T = 2048 that removes two memory-bound passes (≈ 25 + 38
 HBM traffic, and h is not saved for backward (the frozen down base needs no weight gradient).
 
 Used when nothing else sits between the GEMMs: no LoRA / multi-LoRA adapter on gate, up or down,
-frozen bases (NF4 — expanded to bf16 once per step and kept for the dX GEMMs, as in ops/linear.py —
-or bf16), training-sized token counts.  Otherwise the block runs as separate projections.
+frozen bases (NF4 — read by the kernels as 4-bit codes, expanded per quant block inside the GEMM — or
+bf16), training-sized token counts.  Otherwise the block runs as separate projections.
 Reference: ``Fine-Tuning/qwen3-8b-qlora-dist.py:96-125`` (Qwen3 MLP under QLoRA, adapters on q/v).
 """
 from __future__ import annotations
@@ -25,22 +25,20 @@ import torch
 
 from ..quant.nf4 import NF4Weight
 from ._native import native
-from .linear import _G4W, _LT_MIN_M, _nf4_dequant_bf16
+from .linear import _G4W, _LT_MIN_M, _nf4_expand, _nf4_w4
 
 
-def _expanded(base) -> torch.Tensor | None:
-    """bf16 [N, K] view of a frozen base (NF4 expanded once for this call), None if unusable."""
+def _operand(base, reused: bool):
+    """(weight, scale) as the gemm4w entry points take it: an NF4 base as its g4w-packed codes + the
+    transposed block absmax (the kernel expands them) or as one bf16 expansion (ops/linear.py
+    ``_nf4_w4`` decides), a bf16 base as itself with no scale."""
     if isinstance(base, NF4Weight):
-        if not base.kernel_ok():
-            return None
-        return _nf4_dequant_bf16(base)
-    if isinstance(base, torch.Tensor) and base.dtype == torch.bfloat16 and not base.requires_grad:
-        return base.contiguous()
-    return None
+        return base.g4w_pack() if _nf4_w4(reused) else (_nf4_expand(base), None)
+    return base.contiguous(), None
 
 
 def fusable(x: torch.Tensor, gu_base, down_base, F: int, K: int) -> bool:
-    if not (_G4W and x.is_cuda and x.dtype == torch.bfloat16 and F % 16 == 0 and K % 64 == 0 and F % 64 == 0):
+    if not (_G4W and x.is_cuda and x.dtype == torch.bfloat16 and F % 64 == 0 and K % 64 == 0):
         return False
     if x.numel() // x.shape[-1] < _LT_MIN_M:
         return False
@@ -58,13 +56,15 @@ class _SwiGLUMLPFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, bases):
         gu_base, down_base = bases
-        w_gu = _expanded(gu_base)
-        gu, h = native().gemm4w_swiglu(x, w_gu)
-        w_d = _expanded(down_base)
-        y = native().gemm4w(h, w_d, residual, 0, False)
+        K = x.shape[1]
         need = ctx.needs_input_grad[0]
+        w_gu, s_gu = _operand(gu_base, need)
+        F = gu_base.shape[0] // 2
+        gu, h = native().gemm4w_swiglu(x, w_gu, s_gu, F)
+        w_d, s_d = _operand(down_base, need)
+        y = native().gemm4w(h, w_d, residual, 0, False, 0, 0, s_d, K)
         ctx.save_for_backward(gu if need else None)
-        ctx.w = (w_gu, w_d) if need else None      # the expansions live until backward (ops/linear.py)
+        ctx.w = (w_gu, s_gu, w_d, s_d, K) if need else None
         ctx.has_residual = residual is not None
         return y
 
@@ -73,9 +73,9 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         (gu,) = ctx.saved_tensors
         dx = None
         if ctx.w is not None:
-            w_gu, w_d = ctx.w
-            dgu = native().gemm4w_dswiglu(dy.contiguous(), w_d, gu)
-            dx = native().gemm4w(dgu, w_gu, None, 0, True)
+            w_gu, s_gu, w_d, s_d, K = ctx.w
+            dgu = native().gemm4w_dswiglu(dy.contiguous(), w_d, gu, s_d)
+            dx = native().gemm4w(dgu, w_gu, None, 0, True, 0, 0, s_gu, K)
         ctx.w = None
         return dx, (dy if ctx.has_residual else None), None
 

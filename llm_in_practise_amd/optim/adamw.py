@@ -22,9 +22,8 @@ import torch
 
 from ..ops import reference as ref
 from ..ops._native import native, use_native
+from ..ops.linear import nf4_cache_advance
 
-
-from ..ops.linear import nf4_cache_advance  # noqa: E402
 
 
 class FlatParams:

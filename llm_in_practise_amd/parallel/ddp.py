@@ -202,16 +202,20 @@ class DistributedDataParallel(nn.Module):
         self._next = 0
         if self._stream is not None:
             torch.cuda.current_stream(self.grad_buffer.device).wait_stream(self._stream)
+        try:
+            for work, view in self._works:
+                work.wait()
+                view.div_(dist.get_world_size())
+        finally:
+            # the bucket state is reset even when a wait (or the poll below) raises: a caller that
+            # handles the error and goes on must get all-reduces launched again next step
+            self._works = []
+            for bk in self._buckets:
+                bk.launched = False
+                bk.remaining = len(bk.params)
+            self._ready = [False] * len(self._ready)
         if self.car is not None:
             self.car.poll()         # raises if a peer-memory reduction of the previous step timed out
-        for work, view in self._works:
-            work.wait()
-            view.div_(dist.get_world_size())
-        self._works = []
-        for bk in self._buckets:
-            bk.launched = False
-            bk.remaining = len(bk.params)
-        self._ready = [False] * len(self._ready)
 
     def reset_log(self):
         self.launch_log = []

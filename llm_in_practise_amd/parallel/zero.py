@@ -804,7 +804,11 @@ class ZeroEngine:
                     t.copy_(self._shard_of(full, block_units=True))
                 else:
                     full = self._unshard([o[k] for o in old], os_.get("layout"), os_["world"], ob)
-                    t.copy_(self._shard_of(full))
+                    # the 8-bit moments' padding must decode to 0: the index of the code nearest 0
+                    # (code 0 of the signed dynamic map is about -1.0, a phantom moment)
+                    fill = (int(torch.argmin(self.code_s.abs())) if k == "qm" else
+                            int(torch.argmin(self.code_u.abs())) if k == "qv" else 0)
+                    t.copy_(self._shard_of(full, fill=fill))
         self.opt_step = os_["opt_step"]
         if self.lr_scheduler is not None and os_.get("lr_scheduler"):
             self.lr_scheduler.load_state_dict(os_["lr_scheduler"])
@@ -830,22 +834,23 @@ class ZeroEngine:
             offs = [o + sn for o in offs]
         return torch.cat(parts)
 
-    def _shard_of(self, full: torch.Tensor, block_units: bool = False) -> torch.Tensor:
+    def _shard_of(self, full: torch.Tensor, block_units: bool = False, fill: int = 0) -> torch.Tensor:
         """This rank's shard of a full (unpadded) state vector in the current layout
-        (``block_units``: the vector counts 256-element blocks — the 8-bit state scales)."""
+        (``block_units``: the vector counts 256-element blocks — the 8-bit state scales; ``fill``: the
+        value of the padded tail)."""
         d = 256 if block_units else 1
         if self.stage == 3:
             out, o = [], 0
             for u in self.units:
                 n = (_pad_to(max(u.n, 1), 256) // 256) if block_units else u.n
-                v = torch.zeros(u.npad // d, dtype=full.dtype)
+                v = torch.full((u.npad // d,), fill, dtype=full.dtype)
                 v[:n] = full[o:o + n]
                 sn = u.shard_n // d
                 out.append(v[self.rank * sn:(self.rank + 1) * sn])
                 o += n
             return torch.cat(out)
         n = (_pad_to(max(self.n, 1), 256) // 256) if block_units else self.n
-        v = torch.zeros(self.npad // d, dtype=full.dtype)
+        v = torch.full((self.npad // d,), fill, dtype=full.dtype)
         v[:n] = full[:n]
         sn = self.shard_n // d
         r0 = self.shard_slice.start // self.shard_n if self.shard_n else 0

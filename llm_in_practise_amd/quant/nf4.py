@@ -135,6 +135,20 @@ class NF4Weight:
             self.packed = (cf, cb, at)
         return self.packed
 
+    def g4w_pack(self) -> tuple:
+        """(codes, scales_t) — the NF4 B operand of the hand-written gemm4w GEMM (csrc/kernels/gemm4w.hip):
+        the codes re-tiled to [N/64][K/64][2][64][16 B] (pack_g4w_k) and the decoded fp32 block absmax
+        transposed to [K/64, N].  Same bytes as the bnb layout, permuted; built once on first use."""
+        c = self.__dict__.get("_g4w")
+        if c is None:
+            from ..ops._native import native
+            n, k = self.shape
+            codes = native().g4w_pack(self.codes.contiguous(), n, k)
+            sc = self.gemv_scales().reshape(n, k // 64).t().contiguous()
+            c = (codes, sc)
+            self.__dict__["_g4w"] = c
+        return c
+
     def kernel_ok(self) -> bool:
         n, k = self.shape
         return self.blocksize == 64 and n % 64 == 0 and k % 64 == 0

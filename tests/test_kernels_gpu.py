@@ -725,6 +725,74 @@ def test_gemm4w_swiglu_epilogues(native_ext, M, Fd, K):
     assert rel_err(dgu[:, :Fd], gr.grad) < 1e-2 and rel_err(dgu[:, Fd:], ur.grad) < 1e-2
 
 
+# NF4 codes fed straight into gemm4w (K9 "NF4 dequant-GEMM"): the in-kernel expansion must give the
+# SAME bf16 weights as the bitsandbytes-style expansion, so with the same tile / split the outputs are
+# bit-identical to gemm4w on the expanded weight; both are also checked against fp32.
+@pytest.mark.parametrize("M,N,K,splits,bt,resid", [(256, 256, 64, 1, False, False), (512, 768, 512, 1, False, True),
+                                                   (300, 576, 192, 1, False, False), (2048, 1024, 1024, 4, False, True),
+                                                   (257, 320, 640, 2, False, True), (256, 256, 64, 1, True, False),
+                                                   (512, 768, 512, 1, True, True), (300, 576, 192, 1, True, False),
+                                                   (2048, 1024, 2048, 2, True, True), (257, 320, 640, 4, True, False),
+                                                   (1000, 1536, 1024, 0, True, False), (2048, 6144, 4096, 0, False, True)])
+@pytest.mark.parametrize("bn", [128, 256])
+@pytest.mark.parametrize("bm", [256, 128])
+@pytest.mark.parametrize("dq", [True, False])
+def test_gemm4w_nf4_matches_expanded(native_ext, M, N, K, splits, bt, resid, bn, bm, dq):
+    torch.manual_seed(0)
+    R, C = (K, N) if bt else (N, K)     # the stored weight [R, C]: NT reads it as [N, K], bt as [K, N]
+    q = quantize_nf4((0.05 * torch.randn(R, C, device=DEV)).to(torch.bfloat16), 64, double_quant=dq)
+    wd = native_ext.nf4_dequant_fast(q.codes, q.gemv_scales(), R, C)
+    assert torch.equal(wd, dequantize_nf4(q, torch.bfloat16))
+    codes, sc = q.g4w_pack()
+    x = (torch.rand(M, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16) if resid else None
+    y4 = native_ext.gemm4w(x, codes, res, splits, bt, bn, bm, sc, N)
+    y = native_ext.gemm4w(x, wd, res, splits, bt, bn, bm)
+    if splits > 0:   # same tile and split: the same MFMA sequence (auto may split W4 differently)
+        assert torch.equal(y4, y), f"max |diff| {(y4.float() - y.float()).abs().max().item()}"
+    want = x.float() @ (wd.float() if bt else wd.float().t())
+    if resid:
+        want += res.float()
+    assert rel_err(y4, want) < 1e-2
+
+
+def test_gemm4w_nf4_asymmetric(native_ext):
+    """integer-valued activations against a weight whose NF4 codes are all different per (row, column):
+    a misplaced nibble, chunk or row of the in-kernel expansion shows as a mismatch with the expansion"""
+    torch.manual_seed(2)
+    R, C = 256, 512
+    w = (torch.arange(R * C, device=DEV, dtype=torch.float32).view(R, C) * 0.37) % 2.0 - 1.0
+    q = quantize_nf4(w.to(torch.bfloat16), 64, double_quant=False)
+    wd = dequantize_nf4(q, torch.bfloat16)
+    codes, sc = q.g4w_pack()
+    for bt in (False, True):
+        N, K = (C, R) if bt else (R, C)
+        x = torch.eye(K, device=DEV, dtype=torch.bfloat16)[:256] if K >= 256 else torch.eye(K, device=DEV, dtype=torch.bfloat16)
+        for bn in (128, 256):
+            for bm in (256, 128):
+                y = native_ext.gemm4w(x, codes, None, 1, bt, bn, bm, sc, N).float()
+                want = (x.float() @ (wd.float() if bt else wd.float().t()))
+                assert torch.equal(y, want), f"bt={bt} bn={bn} bm={bm}: max |err| {(y - want).abs().max().item()}"
+
+
+@pytest.mark.parametrize("M,Fd,K", [(256, 256, 128), (300, 1024, 512), (2048, 3072, 1024), (1024, 12288, 512)])
+def test_gemm4w_nf4_swiglu_epilogues(native_ext, M, Fd, K):
+    """the fused SwiGLU gate|up forward and down-dX backward launches on NF4 codes == the same launches
+    on the expanded bf16 weights, bit for bit"""
+    torch.manual_seed(5)
+    x = (torch.rand(M, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    qg = quantize_nf4((0.05 * torch.randn(2 * Fd, K, device=DEV)).to(torch.bfloat16), 64, True)
+    qd = quantize_nf4((0.05 * torch.randn(K, Fd, device=DEV)).to(torch.bfloat16), 64, True)
+    wg, wd = dequantize_nf4(qg, torch.bfloat16), dequantize_nf4(qd, torch.bfloat16)
+    cg, sg = qg.g4w_pack()
+    cd, sd = qd.g4w_pack()
+    gu4, h4 = native_ext.gemm4w_swiglu(x, cg, sg, Fd)
+    gu, h = native_ext.gemm4w_swiglu(x, wg)
+    assert torch.equal(gu4, gu) and torch.equal(h4, h)
+    dy = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    assert torch.equal(native_ext.gemm4w_dswiglu(dy, cd, gu, sd), native_ext.gemm4w_dswiglu(dy, wd, gu))
+
+
 def test_lora_apply_column_blocks(native_ext):
     """lora_apply: y[:, c0_i:c0_i+n_i] += xa_i·B_iᵀ in place for several branches, other columns untouched."""
     torch.manual_seed(3)

@@ -344,6 +344,13 @@ def _w8(rank, world, port, stage, out, steps=4, ckpt=None, load=None):
     if load:
         eng.load_checkpoint(load)
         start = eng.global_steps
+        # the re-partitioned 8-bit moments' padding decodes to the zero code (no phantom moment)
+        real = eng._shard_of(torch.ones(sum(eng._layout()), dtype=torch.uint8)).bool().to(eng.qm.device)
+        if (~real).any():
+            z_s = eng.code_s[torch.argmin(eng.code_s.abs())]
+            z_u = eng.code_u[torch.argmin(eng.code_u.abs())]
+            assert torch.all(eng.code_s[eng.qm.long()][~real] == z_s)
+            assert torch.all(eng.code_u[eng.qv.long()][~real] == z_u)
     for s in range(start, start + steps):
         xs, ys = zip(*[_data(s, r) for r in range(4)])
         per = 8 // world            # the same global batch of 8 rows at every world size
