@@ -73,7 +73,7 @@ def build(args, device):
     pm = get_peft_model(model, lcfg)
     model.fuse_projections()
     if args.grad_ckpt:
-        model.gradient_checkpointing_enable()
+        model.gradient_checkpointing_enable({"use_reentrant": bool(args.ckpt_reentrant), "policy": args.ckpt_policy})
     pm.train()
     if device.type == "cuda":
         torch.cuda.synchronize()
@@ -113,6 +113,11 @@ def main():
                          "(gradient checkpointing on, sequential GA micro-steps) in the same process and report "
                          "them as the JSON's 'faithful' sub-record (0: skip; ddp strategy only)")
     ap.add_argument("--faithful-warmup", type=int, default=2)
+    ap.add_argument("--ckpt-reentrant", type=int, default=0,
+                    help="checkpoint form of the faithful sub-record (the reference passes use_reentrant=False)")
+    ap.add_argument("--ckpt-policy", default="selective", choices=["selective", "full"],
+                    help="recompute policy of the faithful sub-record: selective = GEMM outputs recorded in the "
+                         "first forward, norms / RoPE / attention recomputed; full = the whole layer (HF)")
     ap.add_argument("--nf4-gemm", default="auto", choices=["auto", "w4", "expand"],
                     help="NF4 base GEMM form (ops/linear.py _nf4_w4): auto = one bf16 expansion per step where the copy "
                          "is reused (forward + dX), the in-kernel NF4 dequant-GEMM elsewhere; w4 = the NF4 dequant-GEMM "
@@ -235,7 +240,7 @@ def main():
         # BASELINE.md's config exactly as the reference runs it (Fine-Tuning/qwen3-8b-qlora-dist.py:137-138,
         # 162-163): gradient_checkpointing=True and the GA micro-steps one after another (no_sync on all but
         # the last), same model / optimizer / data, timed the same way as the headline
-        model.gradient_checkpointing_enable()
+        model.gradient_checkpointing_enable({"use_reentrant": bool(args.ckpt_reentrant), "policy": args.ckpt_policy})
         for _ in range(args.faithful_warmup):
             step(fused=0)
         sync()
@@ -254,6 +259,8 @@ def main():
         faithful = {"value": round(ftps, 1), "unit": "tokens/s", "ms_per_step": round(fms, 2),
                     "steps": args.faithful_steps, "warmup": args.faithful_warmup,
                     "gradient_checkpointing": True, "ga_execution": "sequential",
+                    "gradient_checkpointing_kwargs": {"use_reentrant": bool(args.ckpt_reentrant)},
+                    "checkpoint_policy": args.ckpt_policy,
                     "micro_batch": args.micro_batch, "grad_accum": args.grad_accum, "peak_hbm_gib": round(fmem, 1)}
     if D.is_main():
         rec = {

@@ -726,12 +726,20 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   }
 }
 
+// out = Σ_s ws[s] (+ residual), 16 elements per thread with every load issued before the first add
+// (10 16-B loads in flight per lane at 2 splits: the slabs were just written and mostly hit the MALL).
+// SP: the split count (2 or 4), or 0 = any count up to 8 (runtime).  A tail of 8 (M·N % 16 == 8) runs
+// the 8-wide path.
+template <int SP>
 __global__ __launch_bounds__(256) void splitk_sum_k(const float* __restrict__ ws, const bf16* __restrict__ residual,
                                                     bf16* __restrict__ out, size_t MN, int splits) {
-  for (size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 8; i < MN; i += (size_t)gridDim.x * 256 * 8) {
+  const size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 16;
+  if (i >= MN) return;
+  const int ns = SP ? SP : splits;
+  if (i + 16 > MN) {   // the 8-element tail
     float v[8];
     load8(ws + i, v);
-    for (int s = 1; s < splits; ++s) {
+    for (int s = 1; s < ns; ++s) {
       float u[8];
       load8(ws + (size_t)s * MN + i, u);
 #pragma unroll
@@ -744,7 +752,39 @@ __global__ __launch_bounds__(256) void splitk_sum_k(const float* __restrict__ ws
       for (int j = 0; j < 8; ++j) v[j] += r[j];
     }
     store8(out + i, v);
+    return;
   }
+  constexpr int MAXS = SP ? SP : 8;
+  f32x4 v[MAXS][4];
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+    if (s >= ns) break;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[s][q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ws + (size_t)s * MN + i) + q);
+  }
+  bf16x8 r0, r1;
+  if (residual) {
+    r0 = *reinterpret_cast<const bf16x8*>(residual + i);
+    r1 = *reinterpret_cast<const bf16x8*>(residual + i + 8);
+  }
+  bf16x8 o0, o1;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x4 t = v[0][q];
+#pragma unroll
+    for (int s = 1; s < MAXS; ++s)
+      if (s < ns) t += v[s][q];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = 4 * q + e;
+      float x = t[e];
+      if (residual) x += (float)(j < 8 ? r0[j] : r1[j - 8]);
+      if (j < 8) o0[j] = (bf16)x;
+      else o1[j - 8] = (bf16)x;
+    }
+  }
+  *reinterpret_cast<bf16x8*>(out + i) = o0;
+  *reinterpret_cast<bf16x8*>(out + i + 8) = o1;
 }
 
 // bnb-layout NF4 codes [R][C/2] (element 2j in the high nibble of byte j) → the g4w layout
@@ -834,7 +874,7 @@ G4wCfg gemm4w_cfg(int M, int N, int K, bool bt, int bn_req, int sp_req, int bm_r
       }
     }
   }
-  if (sp_req > 0) best.splits = sp_req;
+  if (sp_req > 0) best.splits = std::min(sp_req, 8);
   return best;
 }
 
@@ -885,8 +925,11 @@ void launch_gemm4w(const void* A, int lda, const void* B, int ldb, const void* r
 #undef G4W
   if (split) {
     const size_t MN = (size_t)M * N;
-    const int blocks = (int)std::min<size_t>((MN / 8 + 255) / 256, 2048);
-    splitk_sum_k<<<blocks, 256, 0, st>>>(ws, (const bf16*)residual, (bf16*)out, MN, splits);
+    const unsigned blocks = (unsigned)(((MN + 15) / 16 + 255) / 256);
+    const bf16* res = (const bf16*)residual;
+    if (splits == 2) splitk_sum_k<2><<<blocks, 256, 0, st>>>(ws, res, (bf16*)out, MN, 2);
+    else if (splits == 4) splitk_sum_k<4><<<blocks, 256, 0, st>>>(ws, res, (bf16*)out, MN, 4);
+    else splitk_sum_k<0><<<blocks, 256, 0, st>>>(ws, res, (bf16*)out, MN, splits);
   }
   LIPA_CHECK_LAUNCH();
 }

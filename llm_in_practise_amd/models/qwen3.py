@@ -270,6 +270,7 @@ class Qwen3Model(nn.Module):
         self.register_buffer("inv_freq", inv, persistent=False)
         self.attn_factor = attn_factor
         self.gradient_checkpointing = False
+        self.ckpt_kwargs: dict = {}      # use_reentrant / policy (ops/linear.py checkpoint)
         self.pp = None          # parallel.pipeline_parallel stage link (inference PP), else None
 
     def rope(self, position_ids: torch.Tensor):
@@ -289,7 +290,7 @@ class Qwen3Model(nn.Module):
             x = self.pp.enter(x)        # stages > 0: the previous stage's hidden states
         for layer in self.layers:
             if self.gradient_checkpointing and self.training and cache is None:
-                x = lora_checkpoint(layer, x, cos, sin, B, S, None, 0, kv_lens)
+                x = lora_checkpoint(layer, x, cos, sin, B, S, None, 0, kv_lens, **self.ckpt_kwargs)
             else:
                 x = layer(x, cos, sin, B, S, cache, start, kv_lens)
         if self.pp is not None:
@@ -327,7 +328,15 @@ class Qwen3ForCausalLM(nn.Module):
         return m
 
     def gradient_checkpointing_enable(self, gradient_checkpointing_kwargs=None):
+        """HF's API (``Fine-Tuning/qwen3-8b-qlora-dist.py:162-163``): ``use_reentrant`` selects torch's
+        checkpoint form; ``policy`` ("selective" default / "full") is this framework's recompute policy
+        (ops/linear.py ``checkpoint``).  Unknown keys raise."""
+        kw = dict(gradient_checkpointing_kwargs or {})
+        bad = set(kw) - {"use_reentrant", "policy"}
+        if bad:
+            raise ValueError(f"gradient_checkpointing_kwargs: unsupported keys {sorted(bad)}")
         self.model.gradient_checkpointing = True
+        self.model.ckpt_kwargs = kw
 
     def gradient_checkpointing_disable(self):
         self.model.gradient_checkpointing = False

@@ -313,13 +313,17 @@ def seed_dropout(seed: int):
 
 
 _CKPT_REENTRANT = os.environ.get("LIPA_CKPT_REENTRANT", "1") == "1"
+_CKPT_POLICY = os.environ.get("LIPA_CKPT_POLICY", "selective")
 
 
-def checkpoint(fn, *args):
-    """Activation checkpointing that replays the SAME LoRA dropout masks.  Reentrant by default
-    (``LIPA_CKPT_REENTRANT=0``: the non-reentrant form): the reference-faithful QLoRA step
-    (checkpointing on, sequential GA) is partly host-bound and the non-reentrant form's saved-tensor
-    pack hooks cost it 10-15 ms per step (129-135 -> 120 ms, profiles/baseline_configs_r2_end.txt).
+def checkpoint(fn, *args, use_reentrant: bool | None = None, policy: str | None = None):
+    """Activation checkpointing of one layer that replays the SAME LoRA dropout masks.
+
+    ``use_reentrant`` selects torch's form (HF's ``gradient_checkpointing_kwargs={"use_reentrant": …}``,
+    ``Fine-Tuning/qwen3-8b-qlora-dist.py:162-163``; default: LIPA_CKPT_REENTRANT, on).  ``policy``:
+    ``"full"`` recomputes the whole layer in backward (HF's behaviour); ``"selective"`` (default,
+    LIPA_CKPT_POLICY) records the GEMM outputs in the first forward and replays them in the recompute —
+    only RMSNorm, q/k-norm + RoPE and attention run again (the stash above).
 
     The fused LoRA kernels draw their dropout mask from the host key stream above, not from
     torch's RNG, so torch's ``preserve_rng_state`` does not cover them: a plain
@@ -327,30 +331,43 @@ def checkpoint(fn, *args):
     a different mask than the forward applied.  Here the key-stream position at the first (forward)
     call is remembered and restored for the recompute, then the live stream is put back — the
     masks match exactly and the stream advances once per real forward.  Reference:
-    ``Fine-Tuning/qwen3-8b-lora.py:123`` (gradient checkpointing + ``lora_dropout``)."""
+    ``Fine-Tuning/qwen3-8b-lora.py:123`` (gradient checkpointing + ``lora_dropout``).  The reentrant
+    form's first forward builds no graph (no saved-tensor pack hooks: ~2k per step at Qwen3-8B, the
+    host-side cost of the checkpointed step, profiles/baseline_configs_r2_end.txt)."""
     import torch.utils.checkpoint as ckpt
+    reentrant = _CKPT_REENTRANT if use_reentrant is None else bool(use_reentrant)
+    policy = policy or _CKPT_POLICY
+    if policy not in ("full", "selective"):
+        raise ValueError(f"checkpoint policy {policy!r}: 'full' or 'selective'")
+    stash = _Stash() if policy == "selective" else None
     state: list = []
 
     def run(*a):
         _IN_CKPT[0] += 1
+        prev = list(_SAC)
         try:
             if not state:                      # the forward pass
                 state.append(_KEY[0])
+                if stash is not None:
+                    _SAC[:] = ["record", stash]
                 return fn(*a)
             live = _KEY[0]                     # the recompute inside backward
             _KEY[0] = state[0]
+            if stash is not None:
+                stash.pos = 0
+                _SAC[:] = ["replay", stash]
             try:
                 return fn(*a)
             finally:
                 _KEY[0] = live
         finally:
+            _SAC[:] = prev
             _IN_CKPT[0] -= 1
 
-    if _CKPT_REENTRANT:
-        # reentrant form: the first forward runs without building a graph (no saved-tensor pack hooks:
-        # ~2k per step at Qwen3-8B, the host-side cost of the checkpointed step); it needs an input
-        # that requires grad for the recompute to reach the LoRA parameters (layer 0's input is the
-        # frozen embedding) — the role of HF's enable_input_require_grads()
+    if reentrant:
+        # the first forward runs without building a graph; it needs an input that requires grad for the
+        # recompute to reach the LoRA parameters (layer 0's input is the frozen embedding) — the role of
+        # HF's enable_input_require_grads()
         args = tuple(a.detach().requires_grad_() if isinstance(a, torch.Tensor) and i == 0 and
                      a.is_floating_point() and not a.requires_grad else a for i, a in enumerate(args))
         return ckpt.checkpoint(run, *args, use_reentrant=True)
@@ -403,16 +420,60 @@ def _fast_lora_ok(x, branches) -> bool:
     return (K % 128 == 0 and all(br.a.shape[0] <= 16 and (br.c1 - br.c0) % 128 == 0 for br in branches))
 
 
+# Selective activation checkpointing (``checkpoint(..., policy="selective")``): the checkpointed
+# layer's first forward RECORDS the outputs of its GEMM ops (the frozen-base projections with their LoRA
+# side products, the fused SwiGLU MLP) in a per-call stash; the recompute inside backward REPLAYS them
+# instead of launching the GEMMs again, and recomputes only the cheap ops between them (RMSNorm, q/k-norm
+# + RoPE, attention).  The stash holds ≈ 78 MB per Qwen3-8B layer at 1024 tokens (y_qkv, y_o, gu, y_down
+# + the rank-r LoRA projections) until the backward consumes it.
+_SAC: list = [None, None]      # (mode "record" | "replay", stash list)
+
+
+def _sac_recording() -> bool:
+    return _SAC[0] == "record"
+
+
+def sac_put(item):
+    if _SAC[0] == "record":
+        _SAC[1].append(item)
+
+
+def sac_take():
+    """The next recorded op output when replaying, else None."""
+    if _SAC[0] != "replay":
+        return None
+    st = _SAC[1]
+    i = st.pos
+    st.pos += 1
+    item, st[i] = st[i], None
+    return item
+
+
+class _Stash(list):
+    pos = 0
+
+
 class _FusedLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, meta, *ab):
         base, branches, training = meta
         dense = not isinstance(base, NF4Weight)
+        replay = sac_take()
+        if replay is not None:   # selective checkpointing: this op's outputs from the layer's first forward
+            y, xa_list, keys, ctx.masks, ctx.bts, expanded = replay
+            for k in keys:       # the key stream advances exactly as in the recorded forward
+                if k is not None:
+                    next_dropout_key()
+            fast = bool(branches) and _fast_lora_ok(x, branches)
+            wdq = _nf4_expand(base) if expanded else None
+            return _FusedLinearFn._finish(ctx, x, residual, weight, meta, ab, y, xa_list, keys, fast, wdq)
         xa_list, keys = [], []
         ext_a = ext_b = None
         ctx.masks = None
         fast = bool(branches) and _fast_lora_ok(x, branches)
-        need_xa = any(ctx.needs_input_grad[5:])     # (grad mode is off inside forward: ask autograd)
+        # (grad mode is off inside forward: ask autograd; a recording first forward keeps the LoRA side
+        # products too — the replay's backward needs them)
+        need_xa = any(ctx.needs_input_grad[5:]) or _sac_recording()
         # "apply" form: the base GEMM runs alone, then lora_apply adds xa_i·B_iᵀ into ONLY the adapters'
         # column blocks of its output (no K-slice buffers, no per-call B copies, no rank-Σr addmm over
         # all N columns)
@@ -487,7 +548,6 @@ class _FusedLinearFn(torch.autograd.Function):
         if not dense and x.shape[0] > 8 and base.kernel_ok() and x.is_cuda and not _nf4_w4(ctx.needs_input_grad[0]):
             wdq = _nf4_expand(base)     # the expand form: this copy also serves the dX GEMM
         y = _base_gemm(x, wdq if wdq is not None else (base if not dense else weight), ext_a, ext_b, residual)
-        ctx.wdq = wdq if ctx.needs_input_grad[0] else None
         ctx.bts = None
         if apply:
             bs = [bf16_view(b, x.dtype) for b in ab[1::2]]
@@ -499,6 +559,13 @@ class _FusedLinearFn(torch.autograd.Function):
                 xa_list = [None] * len(xa_list)
         if bias is not None:
             y = y + bias
+        sac_put((y, list(xa_list), keys, ctx.masks, ctx.bts, wdq is not None))
+        return _FusedLinearFn._finish(ctx, x, residual, weight, meta, ab, y, xa_list, keys, fast, wdq)
+
+    @staticmethod
+    def _finish(ctx, x, residual, weight, meta, ab, y, xa_list, keys, fast, wdq):
+        branches = meta[1]
+        ctx.wdq = wdq if ctx.needs_input_grad[0] else None
         ctx.meta = meta
         ctx.keys = keys
         ctx.fast = fast

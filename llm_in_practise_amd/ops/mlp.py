@@ -25,7 +25,7 @@ import torch
 
 from ..quant.nf4 import NF4Weight
 from ._native import native
-from .linear import _G4W, _LT_MIN_M, _nf4_expand, _nf4_w4
+from .linear import _G4W, _LT_MIN_M, _nf4_expand, _nf4_w4, sac_put, sac_take
 
 
 def _operand(base, reused: bool):
@@ -59,10 +59,15 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         K = x.shape[1]
         need = ctx.needs_input_grad[0]
         w_gu, s_gu = _operand(gu_base, need)
-        F = gu_base.shape[0] // 2
-        gu, h = native().gemm4w_swiglu(x, w_gu, s_gu, F)
         w_d, s_d = _operand(down_base, need)
-        y = native().gemm4w(h, w_d, residual, 0, False, 0, 0, s_d, K)
+        replay = sac_take()       # selective checkpointing (ops/linear.py): the recorded (gu, y)
+        if replay is not None:
+            gu, y = replay
+        else:
+            F = gu_base.shape[0] // 2
+            gu, h = native().gemm4w_swiglu(x, w_gu, s_gu, F)
+            y = native().gemm4w(h, w_d, residual, 0, False, 0, 0, s_d, K)
+            sac_put((gu, y))
         ctx.save_for_backward(gu if need else None)
         ctx.w = (w_gu, s_gu, w_d, s_d, K) if need else None
         ctx.has_residual = residual is not None

@@ -76,9 +76,13 @@ def test_zero3_single_rank_gpu(tmp_path, native_ext):
 
 
 @pytest.mark.parametrize("targets", [["q_proj", "v_proj"], ["q_proj", "k_proj", "v_proj", "o_proj"]])
-def test_grad_ckpt_lora_dropout_same_gradients(native_ext, monkeypatch, targets):
+@pytest.mark.parametrize("kw", [{}, {"use_reentrant": False}, {"policy": "full"},
+                                {"use_reentrant": False, "policy": "full"}])
+def test_grad_ckpt_lora_dropout_same_gradients(native_ext, monkeypatch, targets, kw):
     """Gradient checkpointing must replay the exact LoRA dropout masks of the forward: LoRA
-    gradients with and without checkpointing agree at dropout 0.1 (Fine-Tuning/qwen3-8b-lora.py:123)."""
+    gradients with and without checkpointing agree at dropout 0.1 (Fine-Tuning/qwen3-8b-lora.py:123),
+    for both torch checkpoint forms (use_reentrant, qwen3-8b-qlora-dist.py:162-163) and both recompute
+    policies (selective: the GEMM outputs of the first forward replayed; full: the whole layer again)."""
     from llm_in_practise_amd.ops.linear import seed_dropout
     monkeypatch.setenv("LIPA_DETERMINISTIC", "1")
     grads = []
@@ -88,7 +92,7 @@ def test_grad_ckpt_lora_dropout_same_gradients(native_ext, monkeypatch, targets)
         pm = get_peft_model(m, LoraConfig(r=8, lora_alpha=16, lora_dropout=0.1, target_modules=targets))
         pm.fuse_projections()
         if ck:
-            pm.gradient_checkpointing_enable()
+            pm.gradient_checkpointing_enable(kw)
         pm.train()
         for n, p in pm.named_parameters():       # non-zero B so dA carries the mask too
             if p.requires_grad and "lora_B" in n:
