@@ -41,6 +41,7 @@ class ZeroConfig:
     stage3_max_live_parameters: int = int(1e9)
     stage3_max_reuse_distance: int = int(1e9)
     stage3_gather_16bit_weights_on_model_save: bool = False
+    stage3_partition_frozen_quant: bool = False     # extension: shard frozen NF4 bases too (zero.py)
     offload_optimizer: str = "none"          # "none" | "cpu"
     offload_param: str = "none"
     pin_memory: bool = False
@@ -105,6 +106,7 @@ def load_ds_config(cfg, world_size: int = 1, micro_batch: int | None = None, gra
         stage3_max_live_parameters=_num(z.get("stage3_max_live_parameters"), int(1e9)),
         stage3_max_reuse_distance=_num(z.get("stage3_max_reuse_distance"), int(1e9)),
         stage3_gather_16bit_weights_on_model_save=bool(z.get("stage3_gather_16bit_weights_on_model_save", False)),
+        stage3_partition_frozen_quant=bool(z.get("stage3_partition_frozen_quant", False)),
         offload_optimizer=(z.get("offload_optimizer") or {}).get("device", "none"),
         offload_param=(z.get("offload_param") or {}).get("device", "none"),
         pin_memory=bool((z.get("offload_optimizer") or {}).get("pin_memory", False)),

@@ -22,8 +22,11 @@ MI355X, ``gloo`` on CPU):
     - finished units' gradients are packed rank-major into persistent bucket buffers and
       reduce-scattered asynchronously (``overlap_comm``) in ``reduce_bucket_size`` buckets while
       the backward continues; ``step()`` joins them.
-  Frozen parameters (NF4 bases) stay replicated — only trainable parameters and their optimizer
-  state are partitioned (QLoRA + ZeRO-3, SURVEY §7.5 option 2).
+  Frozen NF4 bases stay replicated by default — only trainable parameters and their optimizer
+  state are partitioned (QLoRA + ZeRO-3, SURVEY §7.5.3 option 2).  With
+  ``zero_optimization.stage3_partition_frozen_quant: true`` (option 1) each unit's quantised bases
+  are partitioned too, by whole quant blocks, and all-gathered with its parameters (``_QuantFlat``):
+  per-rank base memory 1/W, at one extra byte all-gather of ≈0.53 B/weight per unit use.
 * no host synchronisation in ``step()`` (bf16 / fp32): the global-norm clip coefficient stays on
   the device and feeds the fused AdamW kernel.
 * checkpoints re-partition on load when the world size changed (per-unit / flat layouts are
@@ -105,6 +108,78 @@ def _in_backward() -> bool:
         return False
 
 
+_QALIGN = 512      # bytes: 16 NF4 quant blocks of codes, 512 block scales — shards hold whole blocks
+
+
+def _frozen_quant_tensors(module: nn.Module, claimed: set) -> tuple[list, list]:
+    """(tensors, owners) of the frozen quantised bases under ``module``: every Linear4bit's buffers
+    and every fused q|k|v / gate|up NF4 base (models/common.py FusedProjection, whose parts are views
+    of it).  ``owners`` are the NF4Weight objects whose derived caches must go when the bytes do."""
+    from ..peft.lora import Linear4bit
+    from ..quant.nf4 import NF4Weight
+    tensors, owners = [], []
+
+    def take(q: NF4Weight):
+        owners.append(q)
+        for t in q.tensors().values():
+            if id(t) not in claimed:
+                claimed.add(id(t))
+                tensors.append(t)
+
+    for m in module.modules():
+        if isinstance(m, Linear4bit) and m.codes.numel():
+            take(m.nf4)
+        for v in vars(m).values():
+            b = getattr(v, "base", None)
+            if isinstance(b, NF4Weight) and not isinstance(v, nn.Module):
+                take(b)
+    return tensors, owners
+
+
+class _QuantFlat:
+    """The frozen quantised bases of one stage-3 unit, partitioned by whole quant blocks (SURVEY.md
+    §7.5.3 option 1; ``zero_optimization.stage3_partition_frozen_quant``).
+
+    DeepSpeed stage 3 partitions every module parameter, the frozen 4-bit base included
+    (``Fine-Tuning/qwen3-14b-qlora-dist-deepspeed.py:164``, ``Fine-Tuning/ds_zero3_config.json:13-21``).
+    Here every storage behind the unit's NF4 tensors (codes, block scales, double-quant scales) is
+    laid into ONE uint8 buffer, each segment 512-B aligned, the buffer padded to W × 512 B, and every
+    tensor re-pointed (``Tensor.set_``) at its bytes — so the module's buffers, the fused base and the
+    parts' views all read the one buffer, and the unit's all-gather / ``resize_(0)`` serves them all.
+    Each rank keeps 1/W of the bytes (a whole number of quant blocks); the all-gather is a byte copy,
+    so the gathered weight is bit-identical to the unpartitioned one."""
+
+    def __init__(self, tensors, owners, world, rank, device):
+        self.tensors, self.owners = tensors, owners
+        self.world, self.rank = world, rank
+        segs, total = {}, 0
+        for t in tensors:
+            st = t.untyped_storage()
+            k = st.data_ptr()
+            if k not in segs:
+                segs[k] = (total, st)
+                total += _pad_to(max(st.nbytes(), 1), _QALIGN)
+        self.npad = _pad_to(max(total, 1), world * _QALIGN)
+        self.shard_n = self.npad // world
+        full = torch.zeros(self.npad, dtype=torch.uint8, device=device)
+        for o, st in segs.values():
+            full[o:o + st.nbytes()].copy_(torch.empty(0, dtype=torch.uint8, device=device).set_(st))
+        fst = full.untyped_storage()
+        with torch.no_grad():
+            for t in tensors:
+                o = segs[t.untyped_storage().data_ptr()][0]
+                t.set_(fst, o // t.element_size() + t.storage_offset(), t.size(), t.stride())
+        self.numel = 2 * total          # ≈ quantised weight elements (4-bit codes + their scales)
+        self.full = full
+        self.shard = full[rank * self.shard_n:(rank + 1) * self.shard_n].clone()
+
+    def drop_caches(self):
+        for q in self.owners:
+            q.__dict__.pop("_g4w", None)
+            q.__dict__.pop("_gemv_sc", None)
+            q.packed = None
+
+
 class _Unit:
     """A stage-3 partition unit: trainable params of one module, flattened and sharded."""
 
@@ -127,9 +202,20 @@ class _Unit:
         self.shard = full[rank * self.shard_n:(rank + 1) * self.shard_n].clone()
         self.full = full
         self.gathered = True
-        self.work = None                  # in-flight async all-gather (prefetch)
+        self.work = None                  # in-flight async all-gathers (prefetch)
+        self.quant: _QuantFlat | None = None
         self._point_params()
         self.grads_ready = 0
+
+    @property
+    def size(self) -> int:
+        """Elements the unit brings in when gathered (trainable + partitioned frozen quantised)."""
+        return self.n + (self.quant.numel if self.quant is not None else 0)
+
+    def _flats(self):
+        yield self.full, self.shard
+        if self.quant is not None:
+            yield self.quant.full, self.quant.shard
 
     def _point_params(self):
         o = 0
@@ -148,30 +234,38 @@ class _Unit:
             return False
         if self.work is not None:
             if not async_op:
-                self.work.wait()
+                for w in self.work:
+                    w.wait()
                 self.work = None
                 self.gathered = True
             return False
-        st = self.full.untyped_storage()
-        st.resize_(self.npad * self.full.element_size())
-        if self.world > 1:
-            w = dist.all_gather_into_tensor(self.full, self.shard, async_op=async_op)
-            if async_op:
-                self.work = w
-                return True
-        else:
-            self.full.copy_(self.shard)
+        works = []
+        for full, shard in self._flats():
+            full.untyped_storage().resize_(full.numel() * full.element_size())
+            if self.world > 1:
+                w = dist.all_gather_into_tensor(full, shard, async_op=async_op)
+                if async_op:
+                    works.append(w)
+            else:
+                full.copy_(shard)
+        if works:
+            self.work = works
+            return True
         self.gathered = True
         return True
 
     def release(self):
         if self.work is not None:
-            self.work.wait()
+            for w in self.work:
+                w.wait()
             self.work = None
             self.gathered = True
         if not self.gathered:
             return
-        self.full.untyped_storage().resize_(0)
+        for full, _ in self._flats():
+            full.untyped_storage().resize_(0)
+        if self.quant is not None:
+            self.quant.drop_caches()
         self.gathered = False
 
 
@@ -221,16 +315,16 @@ class ZeroEngine:
                 seen.add(id(p))
                 uniq.append(p)
         self.params = uniq
+        if is_dist():                     # before stage 3 may partition the frozen quantised buffers
+            with torch.no_grad():
+                for b in model.buffers():
+                    dist.broadcast(b, src=0)
         if self.stage == 3:
             self._init_stage3(units)
         else:
             self._init_flat()
         self._init_optimizer_state()
         self.lr_scheduler = self._build_scheduler(total_steps)
-        if is_dist():
-            with torch.no_grad():
-                for b in model.buffers():
-                    dist.broadcast(b, src=0)
 
     # ------------------------------------------------------------------ layout
     def _init_flat(self):
@@ -286,6 +380,14 @@ class ZeroEngine:
                     dist.broadcast(p.data, src=0)
         self.units = [_Unit(f"u{i}", u, groups[id(u)], W, r, self.params[0].dtype, self.device, index=i,
                             block=self.block) for i, u in enumerate(order)]
+        if self.cfg.zero.stage3_partition_frozen_quant:
+            claimed: set = set()
+            for u in self.units:
+                if u.module is self.module:       # the root unit: its own frozen tensors stay replicated
+                    continue
+                ts, owners = _frozen_quant_tensors(u.module, claimed)
+                if ts:
+                    u.quant = _QuantFlat(ts, owners, W, r, self.device)
         self.master = torch.cat([u.shard.float() for u in self.units])
         self.grad_shard = torch.zeros_like(self.master)
         self.unit_offsets, o = [], 0
@@ -294,7 +396,7 @@ class ZeroEngine:
             o += u.shard_n
         z = self.cfg.zero
         thr = z.stage3_param_persistence_threshold
-        self.persistent = {id(u): (u.n < thr or u.module is self.module) for u in self.units}
+        self.persistent = {id(u): (u.size < thr or u.module is self.module) for u in self.units}
         self.prefetch_bucket = int(z.stage3_prefetch_bucket_size)
         self.max_live = int(z.stage3_max_live_parameters)
         self.max_reuse = int(z.stage3_max_reuse_distance)
@@ -328,7 +430,7 @@ class ZeroEngine:
             self.event_log.append((what, u.index))
 
     def _live_params(self) -> int:
-        return sum(u.n for u in self.units if u.live)
+        return sum(u.size for u in self.units if u.live)
 
     def _prefetch(self, seq: list[int], pos: int):
         """Issue async all-gathers for the units after ``pos`` in ``seq`` (prefetch bucket /
@@ -340,14 +442,14 @@ class ZeroEngine:
             u = self.units[idx]
             if budget >= self.prefetch_bucket:
                 break
-            budget += u.n
+            budget += u.size
             if u.live:
                 continue
-            if live + u.n > self.max_live:
+            if live + u.size > self.max_live:
                 break
             if u.gather(async_op=True):
                 self._log("issue", u)
-            live += u.n
+            live += u.size
 
     def _reuse_distance(self, u) -> int:
         """Parameters touched between this unit's forward and its backward (fwd of the later
@@ -356,7 +458,7 @@ class ZeroEngine:
         if u.index not in seq:
             return 1 << 62
         after = seq[seq.index(u.index) + 1:]
-        return 2 * sum(self.units[i].n for i in after)
+        return 2 * sum(self.units[i].size for i in after)
 
     def _pre_fwd(self, u):
         def hook(mod, args):

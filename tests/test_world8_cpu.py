@@ -197,6 +197,142 @@ def test_custom_allreduce_host_model_world8():
         assert calls == {"oneshot": 2, "twoshot": 2, "fallback": 1}, calls
 
 
+# ----------------------------------------------------------------------------- DDP all-reduce policy at W=8
+def test_allreduce_path_policy():
+    from llm_in_practise_amd.parallel.ddp import ONE_SHOT_BYTES, allreduce_path
+    assert allreduce_path(4096, 1, True) == "none"
+    assert allreduce_path(4096, 8, True) == "peer-oneshot"
+    assert allreduce_path(ONE_SHOT_BYTES, 8, True) == "peer-oneshot"
+    assert allreduce_path(ONE_SHOT_BYTES + 16, 8, True) == "rccl"
+    assert allreduce_path(4096, 8, False) == "rccl"           # multi-node: RCCL
+    assert allreduce_path(4100, 8, True) == "rccl"            # not 16-B granular
+    assert allreduce_path(15 << 20, 8, True) == "rccl"        # the QLoRA headline's adapter-gradient sizes
+
+
+def _ddp_policy_worker(rank, world, port, out):
+    _init(rank, world, port)
+    torch.manual_seed(0)
+    big = Net(d=260, n=2)              # ~137k params: 2 buckets of ~68k floats (270 KB > 256 KiB) ...
+    small = Net(d=16, n=2)             # ... and one small model whose buckets are latency-bound
+    res = {}
+    for name, net, mb in (("big", big, 0.26), ("small", small, 0.004)):
+        opt = AdamW(net.parameters(), lr=1e-2, weight_decay=0.0)
+        ddp = DistributedDataParallel(net, flat=opt.flat, bucket_mb=mb, custom_allreduce="auto-host")
+        for s in range(2):
+            x, y = _data(s, rank)
+            ((ddp(x) - y) ** 2).mean().backward()
+            ddp.allreduce_grads()
+            opt.step()
+            opt.zero_grad()
+        res[name] = (None if ddp.car is None else dict(ddp.car.calls), {k: v.clone() for k, v in net.state_dict().items()})
+        ddp.close()
+    torch.save(res, out.format(rank))
+    torch.distributed.destroy_process_group()
+
+
+def test_ddp_allreduce_policy_world8(tmp_path):
+    """8 ranks: DDP's "auto" all-reduce sends only the ≤ 256 KiB buckets through the peer-memory one-shot
+    (here its /dev/shm host model) and builds no peer path at all when every bucket is larger (the
+    QLoRA headline); both train to the single-process oracle."""
+    out = str(tmp_path / "pol{}.pt")
+    mp.spawn(_ddp_policy_worker, args=(W8, _port(), out), nprocs=W8, join=True)
+    for name, net in (("big", Net(d=260, n=2)), ("small", Net(d=16, n=2))):
+        pass
+    got = [torch.load(out.format(r), weights_only=True) for r in range(W8)]
+    assert all(g["big"][0] is None for g in got)                     # no bucket small enough: RCCL only
+    for g in got:
+        calls = g["small"][0]
+        assert calls is not None and calls["oneshot"] > 0 and calls["twoshot"] == 0 and calls["fallback"] == 0
+    for name, d in (("big", 260), ("small", 16)):
+        torch.manual_seed(0)
+        if name == "small":
+            Net(d=260, n=2)                                            # same RNG consumption as the workers
+        net = Net(d=d, n=2)
+        opt = AdamW(net.parameters(), lr=1e-2, weight_decay=0.0)
+        for s in range(2):
+            x, y = _batch(s, W8)
+            ((net(x) - y) ** 2).mean().backward()
+            opt.step()
+            opt.zero_grad()
+        for r in range(W8):
+            for k, v in net.state_dict().items():
+                assert torch.allclose(got[r][name][1][k], v, atol=1e-5), (name, r, k)
+    assert not [f for f in os.listdir("/dev/shm") if f.startswith("lipa_car_")]
+
+
+# ----------------------------------------------------------------------------- ZeRO-3 frozen NF4 partition
+def _qlora_tiny():
+    from llm_in_practise_amd.models.qwen3 import Qwen3ForCausalLM, qwen3_config
+    from llm_in_practise_amd.peft.lora import LoraConfig, get_peft_model, quantize_model_nf4
+    cfg = qwen3_config("qwen3-tiny")
+    m = Qwen3ForCausalLM.from_config(cfg, dtype=torch.float32, seed=0)
+    quantize_model_nf4(m, compute_dtype=torch.float32)
+    pm = get_peft_model(m, LoraConfig(r=4, lora_alpha=8, lora_dropout=0.0, target_modules=["q_proj", "v_proj"]))
+    torch.manual_seed(1)
+    with torch.no_grad():
+        for n, p in pm.named_parameters():
+            if "lora_B" in n:
+                p.normal_(0, 0.05)
+    m.fuse_projections()
+    return pm, m, cfg
+
+
+def _nf4_part_worker(rank, world, port, part, out):
+    from llm_in_practise_amd.quant.nf4 import dequantize_nf4
+    _init(rank, world, port)
+    pm, m, cfg = _qlora_tiny()
+    gu0 = dequantize_nf4(m.model.layers[0].mlp._gu.base, torch.float32).clone()
+    down0 = m.model.layers[1].mlp.down_proj.weight.clone()        # Linear4bit: dequantised view
+    ds = {"train_micro_batch_size_per_gpu": 1, "gradient_accumulation_steps": 1,
+          "optimizer": {"type": "AdamW", "params": {"lr": 1e-2, "weight_decay": 0.0}},
+          "zero_optimization": {"stage": 3, "stage3_param_persistence_threshold": 0,
+                                "stage3_partition_frozen_quant": part}}
+    eng = ZeroEngine(pm, ds)
+    res = {}
+    for s in range(2):
+        g = torch.Generator().manual_seed(100 * s + rank)
+        ids = torch.randint(0, cfg.vocab_size, (1, 16), generator=g)
+        loss = eng(ids, labels=ids).loss
+        eng.backward(loss)
+        eng.step()
+        res[f"loss{s}"] = loss.detach()
+    quant = [u.quant for u in eng.units if u.quant is not None]
+    if part:
+        assert len(quant) == cfg.num_hidden_layers
+        for q in quant:       # released: this rank holds only its 1/W of the unit's quantised bytes
+            assert q.full.untyped_storage().nbytes() == 0
+            assert all(t.untyped_storage().nbytes() == 0 for t in q.tensors)
+            assert q.shard.numel() * world == q.npad and q.shard.numel() % 512 == 0
+        res["shard_bytes"] = torch.tensor(sum(q.shard.numel() for q in quant))
+    else:
+        assert not quant
+    with eng.gathered_params():   # bit-identical bases after gather (fused view and Linear4bit buffers)
+        assert torch.equal(dequantize_nf4(m.model.layers[0].mlp._gu.base, torch.float32), gu0)
+        assert torch.equal(m.model.layers[1].mlp.down_proj.weight, down0)
+    sd = eng.consolidated_state_dict()
+    res.update({k: v for k, v in sd.items() if "lora_" in k or k.endswith("codes")})
+    torch.save(res, out.format(rank))
+    torch.distributed.destroy_process_group()
+
+
+def test_zero3_partitions_frozen_nf4_world8(tmp_path):
+    """SURVEY §7.5.3 option 1 (qwen3-14b-qlora-dist-deepspeed.py:164 under ds_zero3_config.json): the
+    frozen NF4 bases are sharded by whole quant blocks over 8 ranks and all-gathered per layer unit;
+    the training trajectory equals the replicated-base run exactly."""
+    outs = {}
+    for part in (False, True):
+        out = str(tmp_path / f"p{int(part)}_{{}}.pt")
+        mp.spawn(_nf4_part_worker, args=(W8, _port(), part, out), nprocs=W8, join=True)
+        outs[part] = [torch.load(out.format(r), weights_only=True) for r in range(W8)]
+    for r in range(W8):
+        a, b = outs[False][r], outs[True][r]
+        for k in a:
+            assert torch.equal(a[k], b[k]), (r, k)
+    assert any("lora_B" in k for k in outs[True][0])
+    full = sum(v.numel() for k, v in outs[True][0].items() if k.endswith("codes"))
+    assert outs[True][0]["shard_bytes"].item() < full / W8 * 1.2     # 1/8 of codes + scales + padding
+
+
 # ----------------------------------------------------------------------------- bench.py --gpus 8
 def test_bench_self_launches_eight_ranks():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
