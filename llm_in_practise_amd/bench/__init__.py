@@ -5,5 +5,5 @@
   tokens/s, per-GPU tokens/s and weak-scaling efficiency against N = 1
   (BASELINE.md "report padded and non-pad tokens/s for 1, 2, 4 and 8 GPUs as a scaling curve").
 * ``scripts/bench_serve.py`` — serving (TTFT / ITL / throughput at the reference's concurrency
-  levels), ``scripts/bench_gemm8.py`` / ``bench_attn.py`` / ``bench_decode.py`` — kernel A/Bs.
+  levels), ``scripts/bench_gemm4w.py`` / ``bench_w4.py`` / ``bench_attn.py`` / ``bench_decode.py`` — kernel A/Bs.
 """

@@ -11,7 +11,7 @@ Here, on random-init weights of the named architecture (no checkpoints are reach
 2. time decode steps (hipGraph replay, ctx ``--ctx``) and a packed prefill on the bf16 model;
 3. AWQ-quantise the merged model (activation-aware scale search on calibration tokens, then
    group-128 asymmetric int4) — or RTN with ``--method rtn``;
-4. measure the same steps on the W4A16 model (``gemv_w4`` at M ≤ 8, ``gemm_int4`` MFMA above),
+4. measure the same steps on the W4A16 model (``gemv_w4`` at M ≤ 2, ``w4mm`` to 32 rows, gemm4w W4=2 above),
    plus the quality of int4 against bf16: next-token KL, top-1 agreement and the self-PPL proxy
    of both (random weights: the absolute PPL is not comparable to the reference's 8.19 / 9.0 bar,
    so the int4 / bf16 ratio is what is reported — "parity unpinned");

@@ -1,5 +1,6 @@
 // PyTorch bindings for the gfx950 kernels.  Launchers take raw pointers + the current HIP
 // stream (so every op is capturable in a hipGraph and ordered with PyTorch's own work).
+#include "kernels/lora_epi.h"
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
@@ -33,11 +34,6 @@ void launch_adamw8bit(int, float*, const void*, uint8_t*, uint8_t*, float*, floa
                       size_t, float, float, float, float, float, float, float, const float*, const float*,
                       hipStream_t);
 void launch_unscale(int, void*, size_t, const float*, float*, hipStream_t);
-void launch_gemm_w4(int, const void*, int, const uint32_t*, const float*, const void*, const void*, int, const void*,
-                    void*, int, int, int, hipStream_t);
-void launch_pack_nf4(const uint8_t*, uint32_t*, int, int, int, hipStream_t);
-void launch_absmax_t(const float*, const uint8_t*, const float*, const float*, const float*, float*, int, int,
-                     hipStream_t);
 void launch_nf4_quantize(const void*, uint8_t*, float*, size_t, hipStream_t);
 void launch_nf4_dequant2(const uint8_t*, const float*, void*, size_t, hipStream_t);
 int skinny_splits(int, int);
@@ -46,13 +42,13 @@ bool lt_gemm(bool, bool, long, long, long, const void*, long, const void*, long,
 void lt_reset();
 void launch_sum_slices(const void*, void*, int, size_t, size_t, hipStream_t);
 void launch_gemm_skinny(const void*, int, const void*, const void*, void*, float*, int, int, int, int, hipStream_t);
-int w4_skinny_splits(int, int);
-void launch_gemm_w4_skinny(const void*, int, const uint8_t*, const float*, const float*, int, const void*, void*, float*,
-                           int, int, int, int, hipStream_t);
+bool w4mm_supported(int, int, int, int);
+int w4mm_nkb(int, int, int);
+void launch_w4mm(const void*, int, const uint8_t*, const float*, int, const void*, void*, float*, int, int, int, int,
+                 hipStream_t);
 void set_dequant_variant(int);
 void launch_nf4_dequant(const uint8_t*, const float*, const uint8_t*, const float*, const float*, const float*, void*,
                         size_t, hipStream_t);
-bool gemm8_supported(int, int, int, int, int);
 bool gemm4w_supported(int, int, int, int, int, bool, bool);
 int gemm4w_plan(int, int, int, bool, int, int, int*, int, int*, bool);
 int gemm4w_tiles(int, int, int, int);
@@ -62,12 +58,13 @@ void launch_gemm4w_swiglu(const void*, int, const void*, const float*, void*, vo
                           hipStream_t);
 void launch_gemm4w_dswiglu(const void*, int, const void*, const float*, const void*, void*, int, int, int, int, int,
                            hipStream_t);
-void launch_gemm4w(const void*, int, const void*, int, const void*, void*, float*, const float*, int, int, int, int, bool,
-                   int, int, hipStream_t);
+void launch_gemm4w(const void*, int, const void*, int, const void*, void*, float*, const float*, const float*, int, int,
+                   int, int, bool, int, int, hipStream_t);
 void launch_pack_g4w(const uint8_t*, void*, int, int, hipStream_t);
-int gemm8_splits(int, int, int);
-void launch_gemm8(const void*, int, const void*, int, const void*, const void*, int, const void*, void*, float*, int, int,
-                  int, int, hipStream_t);
+void launch_gemm4w_lora(const void*, int, const void*, int, const float*, const void*, void*, const LoraEpi&, int, int,
+                        int, int, int, hipStream_t);
+void launch_gemm4w_loradx(const void*, int, const void*, int, const float*, const void*, void*, const LoraDx&, int, int,
+                          int, int, int, hipStream_t);
 void launch_attn_fwd(const void*, const void*, const void*, int, int, int, const int*, const int*, void*, float*, int,
                      int, int, int, int, int, int, int, float, float, uint64_t, hipStream_t);
 void launch_attn_bwd(const void*, const void*, const void*, const void*, const void*, const float*, const int*, int,
@@ -75,8 +72,6 @@ void launch_attn_bwd(const void*, const void*, const void*, const void*, const v
                      float*, hipStream_t);
 int attn_dkv_nsplit(int, int, int, int);
 
-void launch_gemm_int4_any(const void*, int, const uint32_t*, const float*, const float*, const void*, const void*, int,
-                      const void*, void*, int, int, int, hipStream_t);
 void launch_gemv_w4(int, const void*, int, const uint8_t*, const float*, const float*, int, const void*, void*, int, int,
                     int, hipStream_t);
 void launch_lora_proj(const void*, int, const void*, int, int, float*, int, void*, int, int, uint64_t, float, float,
@@ -501,34 +496,37 @@ Tensor gemm_skinny(Tensor x, Tensor w, optional<Tensor> residual) {
   return out;
 }
 
-// W4A16 decode GEMM: x [M<=64, K] bf16, codes u8 [N, K/2] (high nibble = even k), scales / biases fp32 [N, K/gs]
-Tensor gemm_w4_skinny(Tensor x, Tensor codes, Tensor scales, Tensor biases, int64_t N, int64_t gs,
-                      optional<Tensor> residual) {
-  CHECK_CUDA(x); CHECK_BF16(x); CHECK_CONTIG(codes); CHECK_CONTIG(scales); CHECK_CONTIG(biases);
+// W4A16 MFMA GEMM (csrc/kernels/w4mm.hip): x [M<=64, K] bf16, codes u8 [N, K/2] (high nibble = even k),
+// sc2 fp32 [N, K/gs, 2] = (scale, bias − 128·scale)
+bool w4mm_ok(int64_t M, int64_t N, int64_t K, int64_t gs) { return w4mm_supported((int)M, (int)N, (int)K, (int)gs); }
+
+Tensor w4mm(Tensor x, Tensor codes, Tensor sc2, int64_t N, int64_t gs, optional<Tensor> residual, int64_t nkb) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_CONTIG(codes); CHECK_CONTIG(sc2);
   const int64_t M = x.size(0), K = x.size(1);
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && M >= 1 && M <= 64,
-              "gemm_w4_skinny: x [M<=64, K] row-major, 16-B aligned rows");
-  TORCH_CHECK(codes.scalar_type() == at::kByte && codes.size(0) == N && codes.size(1) * 2 == K,
-              "gemm_w4_skinny: codes [N, K/2] uint8");
-  TORCH_CHECK(K % 256 == 0 && gs % 128 == 0 && K % gs == 0 && N % 16 == 0, "gemm_w4_skinny: K%256, gs%128, N%16");
-  TORCH_CHECK(scales.scalar_type() == at::kFloat && biases.scalar_type() == at::kFloat &&
-                  scales.numel() == N * (K / gs) && biases.numel() == N * (K / gs),
-              "gemm_w4_skinny: fp32 scales / biases [N, K/gs]");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(codes.data_ptr()) % 16 == 0,
-              "gemm_w4_skinny: 16-B aligned operands");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "w4mm: x row-major, 16-B aligned rows");
+  TORCH_CHECK(w4mm_supported((int)M, (int)N, (int)K, (int)gs), "w4mm: M<=64, N%128, K%128, gs%128");
+  TORCH_CHECK(codes.scalar_type() == at::kByte && codes.numel() == N * K / 2, "w4mm: codes [N, K/2] uint8");
+  TORCH_CHECK(sc2.scalar_type() == at::kFloat && sc2.numel() == N * (K / gs) * 2, "w4mm: sc2 fp32 [N, K/gs, 2]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(codes.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(sc2.data_ptr()) % 8 == 0,
+              "w4mm: aligned operands");
+  TORCH_CHECK((size_t)N * K / 2 < (1ull << 31) * 2, "w4mm: codes too large");
   const void* rp = nullptr;
   if (residual.has_value() && residual->defined()) {
     CHECK_BF16((*residual));
     CHECK_CONTIG((*residual));
-    TORCH_CHECK(residual->size(0) == M && residual->size(1) == N, "gemm_w4_skinny: residual shape");
+    TORCH_CHECK(residual->size(0) == M && residual->size(1) == N, "w4mm: residual shape");
     rp = residual->data_ptr();
   }
-  const int S = w4_skinny_splits(N, K);
-  Tensor part = at::empty({S, M, N}, x.options().dtype(at::kFloat));
+  const int nb = nkb > 0 ? (int)nkb : w4mm_nkb((int)M, (int)N, (int)K);
+  TORCH_CHECK(nb == 1 || nb == 2 || nb == 4 || nb == 8, "w4mm: nkb in 1/2/4/8");
+  TORCH_CHECK((K / 128) % nb == 0, "w4mm: K/128 divisible by nkb");
+  const int KS = (int)(K / (128 * nb));
   Tensor out = at::empty({M, N}, x.options());
-  launch_gemm_w4_skinny(x.data_ptr(), x.stride(0), codes.data_ptr<uint8_t>(), scales.data_ptr<float>(),
-                        biases.data_ptr<float>(), (int)gs, rp, out.data_ptr(), part.data_ptr<float>(), M, N, K, S,
-                        stream());
+  Tensor part;
+  if (KS > 1) part = at::empty({KS, M, N}, x.options().dtype(at::kFloat));
+  launch_w4mm(x.data_ptr(), (int)x.stride(0), codes.data_ptr<uint8_t>(), sc2.data_ptr<float>(), (int)gs, rp,
+              out.data_ptr(), KS > 1 ? part.data_ptr<float>() : nullptr, (int)M, (int)N, (int)K, nb, stream());
   return out;
 }
 
@@ -555,25 +553,6 @@ Tensor nf4_dequant(Tensor codes, optional<Tensor> absmax, optional<Tensor> qabs,
   return w;
 }
 
-std::vector<Tensor> nf4_pack(Tensor codes, int64_t N, int64_t K) {
-  CHECK_CONTIG(codes);
-  TORCH_CHECK(N % 64 == 0 && K % 64 == 0, "nf4_pack: N, K multiples of 64");
-  auto f = at::empty({N * K / 8}, codes.options().dtype(at::kInt));
-  auto b = at::empty({N * K / 8}, codes.options().dtype(at::kInt));
-  launch_pack_nf4(codes.data_ptr<uint8_t>(), (uint32_t*)f.data_ptr(), N, K, 0, stream());
-  launch_pack_nf4(codes.data_ptr<uint8_t>(), (uint32_t*)b.data_ptr(), N, K, 1, stream());
-  return {f, b};
-}
-
-Tensor nf4_absmax_t(optional<Tensor> absmax, optional<Tensor> qabs, optional<Tensor> absmax2, optional<Tensor> offset,
-                    optional<Tensor> dcode, int64_t N, int64_t K) {
-  const auto& ref = absmax ? *absmax : *qabs;
-  auto out = at::empty({K / 64, N}, ref.options().dtype(at::kFloat));
-  launch_absmax_t(optr_t<float>(absmax), optr_t<uint8_t>(qabs), optr_t<float>(absmax2), optr_t<float>(offset),
-                  optr_t<float>(dcode), out.data_ptr<float>(), N, K, stream());
-  return out;
-}
-
 void check_ext(const optional<Tensor>& ea, const optional<Tensor>& eb, int M, int C, int& R_ext) {
   R_ext = 0;
   if (ea && ea->defined()) {
@@ -586,42 +565,6 @@ void check_ext(const optional<Tensor>& ea, const optional<Tensor>& eb, int M, in
     TORCH_CHECK(R_ext % 32 == 0 && ea->size(0) == M && eb->size(0) == C && eb->size(1) == R_ext,
                 "LoRA K-slice shapes: ext_a [M, R], ext_b [C, R], R % 32 == 0");
   }
-}
-
-// Y[M, N] = X[M, K] · deq(W)ᵀ + ext_a·ext_bᵀ + residual
-Tensor gemm_nf4(Tensor x, Tensor codes_f, Tensor absmax_t, int64_t N, optional<Tensor> ext_a, optional<Tensor> ext_b,
-                optional<Tensor> residual) {
-  CHECK_BF16(x);
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "gemm_nf4: x row-major, 16-B aligned rows");
-  const int M = x.size(0), K = x.size(1);
-  TORCH_CHECK(N % 32 == 0 && K % 64 == 0, "gemm_nf4: N % 32, K % 64");
-  TORCH_CHECK(codes_f.numel() == N * K / 8 && absmax_t.numel() == N * K / 64, "gemm_nf4: packed weight size");
-  int R_ext;
-  check_ext(ext_a, ext_b, M, N, R_ext);
-  if (residual) TORCH_CHECK(residual->is_contiguous() && residual->size(0) == M && residual->size(1) == N, "residual");
-  auto y = at::empty({M, N}, x.options());
-  launch_gemm_w4(0, x.data_ptr(), x.stride(0), (const uint32_t*)codes_f.data_ptr(), absmax_t.data_ptr<float>(),
-                 optr(ext_a), optr(ext_b), R_ext, optr(residual), y.data_ptr(), M, N, K, stream());
-  return y;
-}
-
-// W4A16 affine int4 (K15): Y = X·(q·s + b)ᵀ (+ ext_a·ext_bᵀ) (+ residual); scale_t/bias_t [K/64, N]
-Tensor gemm_int4(Tensor x, Tensor codes_f, Tensor scale_t, Tensor bias_t, int64_t N, optional<Tensor> ext_a,
-                 optional<Tensor> ext_b, optional<Tensor> residual) {
-  CHECK_BF16(x);
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "gemm_int4: x row-major, 16-B aligned rows");
-  const int M = x.size(0), K = x.size(1);
-  TORCH_CHECK(N % 32 == 0 && K % 64 == 0, "gemm_int4: N % 32, K % 64");
-  TORCH_CHECK(codes_f.numel() == N * K / 8 && scale_t.numel() == N * K / 64 && bias_t.numel() == N * K / 64,
-              "gemm_int4: packed weight size");
-  int R_ext;
-  check_ext(ext_a, ext_b, M, N, R_ext);
-  if (residual) TORCH_CHECK(residual->is_contiguous() && residual->size(0) == M && residual->size(1) == N, "residual");
-  auto y = at::empty({M, N}, x.options());
-  launch_gemm_int4_any(x.data_ptr(), x.stride(0), (const uint32_t*)codes_f.data_ptr(), scale_t.data_ptr<float>(),
-                   bias_t.data_ptr<float>(), optr(ext_a), optr(ext_b), R_ext, optr(residual), y.data_ptr(), M, N, K,
-                   stream());
-  return y;
 }
 
 // decode GEMV (M <= 8): codes [N, K/2] bytes (high nibble = even k), scales [N, K/blk] fp32,
@@ -641,25 +584,6 @@ Tensor gemv_w4(Tensor x, Tensor codes, Tensor scales, optional<Tensor> bias, int
                  aff ? bias->data_ptr<float>() : nullptr, blk, optr(residual), y.data_ptr(), M, N, K, stream());
   return y;
 }
-
-// dX[M, K] = dY[M, N] · deq(W) + ext_a·ext_bᵀ  (ext_b is [K, R])
-Tensor gemm_nf4_t(Tensor dy, Tensor codes_b, Tensor absmax_t, int64_t K, optional<Tensor> ext_a,
-                  optional<Tensor> ext_b) {
-  CHECK_BF16(dy);
-  TORCH_CHECK(dy.dim() == 2 && dy.stride(1) == 1 && dy.stride(0) % 8 == 0, "gemm_nf4_t: dy row-major");
-  const int M = dy.size(0), N = dy.size(1);
-  TORCH_CHECK(N % 64 == 0 && K % 32 == 0, "gemm_nf4_t: N % 64, K % 32");
-  TORCH_CHECK(codes_b.numel() == N * K / 8, "gemm_nf4_t: packed weight size");
-  int R_ext;
-  check_ext(ext_a, ext_b, M, K, R_ext);
-  auto dx = at::empty({M, K}, dy.options());
-  launch_gemm_w4(1, dy.data_ptr(), dy.stride(0), (const uint32_t*)codes_b.data_ptr(), absmax_t.data_ptr<float>(),
-                 optr(ext_a), optr(ext_b), R_ext, nullptr, dx.data_ptr(), M, K, N, stream());
-  return dx;
-}
-
-Tensor gemm8(Tensor x, Tensor w, optional<Tensor> ext_a, optional<Tensor> ext_b, optional<Tensor> residual,
-             int64_t splits);
 
 
 // The B operand of the gemm4w entry points: a bf16 weight, or (wscale given) the g4w-packed NF4 codes of one
@@ -694,7 +618,7 @@ bool gemm4w_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, bool b
 // bn: tile width 128 / 256 / 192 (NT only), 0 = auto.  wscale: w is an NF4 base (g4w_operand); n_w4
 // is then the GEMM N (the weight's rows for NT, its columns for bt).
 Tensor gemm4w(Tensor x, Tensor w, optional<Tensor> residual, int64_t splits, bool bt, int64_t bn, int64_t bm,
-              optional<Tensor> wscale, int64_t n_w4) {
+              optional<Tensor> wscale, int64_t n_w4, optional<Tensor> wzero) {
   CHECK_BF16(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "gemm4w: x 2-D, unit inner stride");
   const bool w4 = wscale && wscale->defined();
@@ -716,8 +640,14 @@ Tensor gemm4w(Tensor x, Tensor w, optional<Tensor> residual, int64_t splits, boo
   auto y = at::empty({M, N}, x.options());
   Tensor ws;
   if (sp > 1) ws = at::empty({sp, M, N}, x.options().dtype(at::kFloat));
+  const float* zp = nullptr;
+  if (wzero && wzero->defined()) {   // affine int4 (W4A16): wscale / wzero = per-64-block fp32 s, z, [K/64, N]
+    TORCH_CHECK(w4 && !bt && wzero->scalar_type() == at::kFloat && wzero->is_contiguous() &&
+                    wzero->numel() == wscale->numel(), "gemm4w: wzero fp32 [K/64, N] with wscale, forward only");
+    zp = wzero->data_ptr<float>();
+  }
   launch_gemm4w(x.data_ptr(), x.stride(0), b.ptr, b.ld, res, y.data_ptr(), sp > 1 ? ws.data_ptr<float>() : nullptr,
-                b.scale, M, N, K, sp, bt, bn_used, bm_used, stream());
+                b.scale, zp, M, N, K, sp, bt, bn_used, bm_used, stream());
   return y;
 }
 
@@ -761,6 +691,113 @@ Tensor gemm4w_dswiglu(Tensor dy, Tensor w, Tensor gu, optional<Tensor> wscale) {
   return dgu;
 }
 
+// y = x·Wᵀ (+ residual) + Σ_b xa[:, kofs_b : kofs_b + r_b]·B_bᵀ into columns [c0_b, c0_b + n_b): the LoRA
+// branches of a fused projection as extra MFMA K-steps of the base GEMM (gemm4w.hip LORA epilogue).
+// xa bf16 [M, 32·nks] (zero outside the branches' slots), B_b bf16 [n_b, r_b] (r_b, kofs_b multiples of
+// 8, up to 4 branches); bts[b] (optional) receives B_bᵀ [r_b, n_b].  w / wscale / n_w4 as gemm4w.
+Tensor gemm4w_lora(Tensor x, Tensor w, optional<Tensor> wscale, int64_t n_w4, optional<Tensor> residual, Tensor xa,
+                   std::vector<Tensor> bs, std::vector<int64_t> c0s, std::vector<int64_t> kofs,
+                   std::vector<optional<Tensor>> bts) {
+  CHECK_BF16(x);
+  CHECK_BF16(xa);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "gemm4w_lora: x 2-D");
+  const bool w4 = wscale && wscale->defined();
+  const int64_t M = x.size(0), K = x.size(1);
+  const int64_t N = w4 ? n_w4 : w.size(0);
+  const G4wB b = g4w_operand(w, wscale, N, K);
+  TORCH_CHECK(gemm4w_ok(M, N, K, x.stride(0), b.ld, false, w4) && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "gemm4w_lora: unsupported shape / strides");
+  const int nbr = (int)bs.size();
+  TORCH_CHECK(nbr >= 1 && nbr <= 4 && (int)c0s.size() == nbr && (int)kofs.size() == nbr && (int)bts.size() == nbr,
+              "gemm4w_lora: 1..4 branches");
+  TORCH_CHECK(xa.dim() == 2 && xa.size(0) == M && xa.stride(1) == 1 && xa.size(1) % 32 == 0 && xa.size(1) <= 128 &&
+                  xa.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(xa.data_ptr()) % 16 == 0,
+              "gemm4w_lora: xa bf16 [M, 32·nks], 16-B aligned rows");
+  LoraEpi lx{};
+  lx.xa = xa.data_ptr();
+  lx.ldxa = (int)xa.stride(0);
+  lx.nks = (int)(xa.size(1) / 32);
+  lx.nbr = nbr;
+  for (int i = 0; i < nbr; ++i) {
+    const Tensor& bb = bs[i];
+    CHECK_BF16(bb);
+    CHECK_CONTIG(bb);
+    const int64_t n = bb.size(0), r = bb.size(1);
+    TORCH_CHECK(r % 8 == 0 && kofs[i] % 8 == 0 && kofs[i] + r <= xa.size(1) && c0s[i] >= 0 && c0s[i] + n <= N &&
+                    reinterpret_cast<uintptr_t>(bb.data_ptr()) % 16 == 0,
+                "gemm4w_lora: branch ", i, ": r, kofs multiples of 8 inside xa, columns inside N");
+    lx.b[i] = bb.data_ptr();
+    lx.c0[i] = (int)c0s[i];
+    lx.n[i] = (int)n;
+    lx.r[i] = (int)r;
+    lx.kofs[i] = (int)kofs[i];
+    if (bts[i] && bts[i]->defined()) {
+      TORCH_CHECK(bts[i]->scalar_type() == at::kBFloat16 && bts[i]->is_contiguous() && bts[i]->size(0) == r &&
+                      bts[i]->size(1) == n, "gemm4w_lora: bt [r, n] bf16");
+      lx.bt[i] = bts[i]->data_ptr();
+    }
+  }
+  const void* res = nullptr;
+  if (residual && residual->defined()) {
+    CHECK_BF16(*residual);
+    TORCH_CHECK(residual->is_contiguous() && residual->size(0) == M && residual->size(1) == N, "gemm4w_lora: residual");
+    res = residual->data_ptr();
+  }
+  int bn = 0, bm = 0;
+  gemm4w_plan(M, N, K, false, 0, 1, &bn, 0, &bm, w4);
+  auto y = at::empty({M, N}, x.options());
+  launch_gemm4w_lora(x.data_ptr(), x.stride(0), b.ptr, b.ld, b.scale, res, y.data_ptr(), lx, M, N, K, bn, bm, stream());
+  return y;
+}
+
+// dX = dY·W + Σ_b D_b(ds_b · g_b·A_b) for up to two dropout adapters of the projection (the LoRA input
+// gradient added in the gemm4w dX epilogue: no lora_dx2 matrix, no C read).  g_b fp32 [M, r_b] (row stride
+// >= r_b), A_b bf16 [r_b, N] (r_b <= 32), masks uint8 [2, M, N/8] keep bits (None: no dropout), ds_b = 1/(1-p_b).
+Tensor gemm4w_loradx(Tensor dy, Tensor w, optional<Tensor> wscale, int64_t n_w4, std::vector<Tensor> gs,
+                     std::vector<Tensor> as, optional<Tensor> masks, std::vector<double> ps) {
+  CHECK_BF16(dy);
+  TORCH_CHECK(dy.dim() == 2 && dy.stride(1) == 1, "gemm4w_loradx: dy 2-D");
+  const bool w4 = wscale && wscale->defined();
+  const int64_t M = dy.size(0), K = dy.size(1);
+  const int64_t N = w4 ? n_w4 : w.size(1);
+  const G4wB b = g4w_operand(w, wscale, K, N);
+  TORCH_CHECK(gemm4w_ok(M, N, K, dy.stride(0), b.ld, true, w4) && reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0,
+              "gemm4w_loradx: unsupported shape / strides");
+  const int nbr = (int)gs.size();
+  TORCH_CHECK(nbr >= 1 && nbr <= 2 && (int)as.size() == nbr && (int)ps.size() == nbr, "gemm4w_loradx: 1..2 branches");
+  TORCH_CHECK(N % 128 == 0, "gemm4w_loradx: N % 128 (16-B keep-bit runs)");
+  LoraDx ld{};
+  ld.nbr = nbr;
+  for (int i = 0; i < nbr; ++i) {
+    const Tensor& g = gs[i];
+    const Tensor& a = as[i];
+    TORCH_CHECK(g.scalar_type() == at::kFloat && g.dim() == 2 && g.size(0) == M && g.stride(1) == 1 &&
+                    g.size(1) <= 32 && g.size(1) % 8 == 0 && (i == 0 || g.stride(0) == gs[0].stride(0)) &&
+                    reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0 && g.stride(0) % 4 == 0,
+                "gemm4w_loradx: g fp32 [M, r], r a multiple of 8 up to 32, 16-B aligned rows");
+    CHECK_BF16(a);
+    CHECK_CONTIG(a);
+    TORCH_CHECK(a.size(0) == g.size(1) && a.size(1) == N && reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0,
+                "gemm4w_loradx: A [r, N]");
+    ld.g[i] = g.data_ptr<float>();
+    ld.ldg = (int)g.stride(0);
+    ld.a[i] = a.data_ptr();
+    ld.r[i] = (int)a.size(0);
+    ld.ds[i] = (float)(1.0 / (1.0 - ps[i]));
+  }
+  if (masks && masks->defined()) {
+    TORCH_CHECK(masks->scalar_type() == at::kByte && masks->is_contiguous() && masks->numel() == 2 * M * (N / 8),
+                "gemm4w_loradx: keep bits uint8 [2, M, N/8]");
+    for (int i = 0; i < nbr; ++i) ld.keep[i] = masks->data_ptr<uint8_t>() + (size_t)i * M * (N / 8);
+  }
+  int bn = 0, bm = 0;
+  gemm4w_plan(M, N, K, true, 0, 1, &bn, 0, &bm, w4);
+  auto dx = at::empty({M, N}, dy.options());
+  launch_gemm4w_loradx(dy.data_ptr(), dy.stride(0), b.ptr, b.ld, b.scale, nullptr, dx.data_ptr(), ld, M, N, K, bn, bm,
+                       stream());
+  return dx;
+}
+
 // bnb-layout NF4 codes [R, C/2] → the g4w tile layout gemm4w reads (gemm4w.hip pack_g4w_k)
 Tensor g4w_pack(Tensor codes, int64_t R, int64_t C) {
   CHECK_CONTIG(codes);
@@ -786,73 +823,6 @@ void mlora_apply(Tensor x, Tensor A, Tensor B, Tensor ids, Tensor seg, Tensor y,
   TORCH_CHECK(seg.scalar_type() == at::kInt && seg.dim() == 2 && seg.size(1) == 3, "mlora_apply: seg [n, 3] int32");
   launch_mlora_apply(x.data_ptr(), x.stride(0), A.data_ptr(), B.data_ptr(), ids.data_ptr<int64_t>(), seg.data_ptr(),
                      (int)seg.size(0), y.data_ptr(), y.stride(0), (int)c0, (int)T, (int)K, (int)N, (int)R, stream());
-}
-
-// y = x·wᵀ (+ LoRA K-slice) (+ residual) for a frozen bf16 base: the hand-written 8-phase MFMA GEMM
-// (gemm8.hip) whenever the shape / strides allow it, library GEMM otherwise.
-Tensor gemm_bf16(Tensor x, Tensor w, optional<Tensor> ext_a, optional<Tensor> ext_b, optional<Tensor> residual) {
-  CHECK_BF16(x);
-  CHECK_BF16(w);
-  CHECK_CONTIG(w);
-  const int M = x.size(0), K = x.size(1), N = w.size(0);
-  const bool ext_ok = !(ext_a && ext_a->defined()) || (ext_a->is_contiguous() && ext_b->is_contiguous() &&
-                                                       ext_a->size(1) % 32 == 0);
-  const bool res_ok = !(residual && residual->defined()) || residual->is_contiguous();
-  if (x.stride(1) != 1 || !gemm8_supported(M, N, K, x.stride(0), w.stride(0)) || !ext_ok || !res_ok ||
-      reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 != 0) {
-    auto y = at::matmul(x, w.t());
-    if (ext_a && ext_a->defined()) y.addmm_(*ext_a, ext_b->t());
-    if (residual && residual->defined()) y.add_(*residual);
-    return y;
-  }
-  return gemm8(x, w, ext_a, ext_b, residual, 0);
-}
-
-Tensor gemm_bf16_t(Tensor dy, Tensor w, optional<Tensor> ext_a, optional<Tensor> ext_b) {
-  auto dx = at::matmul(dy, w);
-  if (ext_a && ext_a->defined()) dx.addmm_(*ext_a, ext_b->t());
-  return dx;
-}
-
-// ------------------------------------------------------------------ 8-phase MFMA GEMM
-// y = x·wᵀ (+ ext_a·ext_bᵀ) (+ residual);  x [M, K] (row stride any multiple of 8), w [N, K]
-Tensor gemm8(Tensor x, Tensor w, optional<Tensor> ext_a, optional<Tensor> ext_b, optional<Tensor> residual,
-             int64_t splits) {
-  CHECK_BF16(x);
-  CHECK_BF16(w);
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1, "gemm8: 2-D, unit inner stride");
-  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K, "gemm8: K mismatch");
-  TORCH_CHECK(gemm8_supported(M, N, K, x.stride(0), w.stride(0)), "gemm8: unsupported shape / strides");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
-              "gemm8: 16-byte aligned operands");
-  const void* ea = nullptr;
-  const void* eb = nullptr;
-  int R = 0;
-  if (ext_a && ext_a->defined()) {
-    TORCH_CHECK(ext_b && ext_b->defined(), "gemm8: ext_b");
-    CHECK_BF16(*ext_a);
-    CHECK_BF16(*ext_b);
-    TORCH_CHECK(ext_a->is_contiguous() && ext_b->is_contiguous(), "gemm8: contiguous LoRA slices");
-    R = ext_a->size(1);
-    TORCH_CHECK(R % 32 == 0 && ext_a->size(0) == M && ext_b->size(0) == N && ext_b->size(1) == R,
-                "gemm8: LoRA K-slice shapes [M, R] / [N, R], R % 32 == 0");
-    ea = ext_a->data_ptr();
-    eb = ext_b->data_ptr();
-  }
-  const void* res = nullptr;
-  if (residual && residual->defined()) {
-    CHECK_BF16(*residual);
-    TORCH_CHECK(residual->is_contiguous() && residual->size(0) == M && residual->size(1) == N, "gemm8: residual [M, N]");
-    res = residual->data_ptr();
-  }
-  const int sp = splits > 0 ? (int)splits : gemm8_splits(M, N, K);
-  auto y = at::empty({M, N}, x.options());
-  Tensor ws;
-  if (sp > 1) ws = at::empty({sp, M, N}, x.options().dtype(at::kFloat));
-  launch_gemm8(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), ea, eb, R, res, y.data_ptr(),
-               sp > 1 ? ws.data_ptr<float>() : nullptr, M, N, K, sp, stream());
-  return y;
 }
 
 // ------------------------------------------------------------------ attention
@@ -1426,7 +1396,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lora_dA_pair", &lora_dA_pair);
   m.def("lora_dx2", &lora_dx2);
   m.def("lora_apply", &lora_apply);
-  m.def("gemm_int4", &gemm_int4);
   m.def("gemv_w4", &gemv_w4);
   m.def("sample", &sample);
   m.def("adamw", &adamw);
@@ -1439,24 +1408,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lt_linear", &lt_linear);
   m.def("lt_dx", &lt_dx);
   m.def("lt_reset", &lt_reset);
-  m.def("gemm_w4_skinny", &gemm_w4_skinny);
+  m.def("w4mm", &w4mm, py::arg("x"), py::arg("codes"), py::arg("sc2"), py::arg("N"), py::arg("gs"),
+        py::arg("residual") = py::none(), py::arg("nkb") = 0);
+  m.def("w4mm_ok", &w4mm_ok);
   m.def("set_dequant_variant", &set_dequant_variant);
-  m.def("nf4_pack", &nf4_pack);
-  m.def("nf4_absmax_t", &nf4_absmax_t);
-  m.def("gemm_nf4", &gemm_nf4);
-  m.def("gemm8", &gemm8);
   m.def("gemm4w_ok", &gemm4w_ok);
   m.def("g4w_pack", &g4w_pack);
+  m.def("gemm4w_lora", &gemm4w_lora);
+  m.def("gemm4w_loradx", &gemm4w_loradx);
   m.def("gemm4w", &gemm4w, py::arg("x"), py::arg("w"), py::arg("residual") = py::none(), py::arg("splits") = 0,
         py::arg("bt") = false, py::arg("bn") = 0, py::arg("bm") = 0, py::arg("wscale") = py::none(),
-        py::arg("n_w4") = 0);
+        py::arg("n_w4") = 0, py::arg("wzero") = py::none());
   m.def("gemm4w_swiglu", &gemm4w_swiglu, py::arg("x"), py::arg("w"), py::arg("wscale") = py::none(),
         py::arg("f_w4") = 0);
   m.def("mlora_apply", &mlora_apply);
   m.def("gemm4w_dswiglu", &gemm4w_dswiglu, py::arg("dy"), py::arg("w"), py::arg("gu"), py::arg("wscale") = py::none());
-  m.def("gemm_nf4_t", &gemm_nf4_t);
-  m.def("gemm_bf16", &gemm_bf16);
-  m.def("gemm_bf16_t", &gemm_bf16_t);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_fwd_ext", &attn_fwd_ext);
   m.def("attn_bwd", &attn_bwd);

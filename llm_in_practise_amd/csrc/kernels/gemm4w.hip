@@ -48,6 +48,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "lora_epi.h"
 
 using namespace lipa;
 
@@ -107,6 +108,18 @@ __device__ __forceinline__ void dma_lds(const rsrc_t& rs, uint32_t dst, uint32_t
       : "s"(dst), "v"(voff), "s"(rs), "s"(soff)
       : "memory");
 }
+
+// 16-B global load as an asm statement (hipcc does not count it: the explicit vmcnt waits that follow
+// cover it) and the empty asm that pins a register behind such a wait
+__device__ __forceinline__ u32x4 gload16_u(const void* p) {
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ bf16x8 gload16(const void* p) { return __builtin_bit_cast(bf16x8, gload16_u(p)); }
+__device__ __forceinline__ void pin(bf16x8& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pinf(f32x4& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pinu(u32x4& v) { asm volatile("" : "+v"(v)); }
 
 // compile-time unrolled loop: f(std::integral_constant<int, k>) for k in [K, N)
 template <int K, int N>
@@ -237,18 +250,25 @@ struct W4St {
   uint32_t sa, sb, t4, w4, w8, w12, ma, mb, x0, x1, x2, x3, lo, hi;
   u32x4 o;
 };
+// entry I of a block's table: NF4 (MODE 1) code_I · absmax; affine int4 (MODE 2, W4A16 GPTQ / AWQ)
+// (I − z)·s — exactly Int4Weight.dequantize's fp32 expression (I − z is exact)
+template <int I, int MODE>
+__device__ __forceinline__ float tab_entry(float s, float zf) {
+  if constexpr (MODE == 2) return vmul(s, (float)I - zf);
+  else return mulc<I>(s);
+}
 // table micro-op J (0..15): q = J / 4 builds planes l[q], h[q] from T[4q .. 4q+3]
-template <int J>
-__device__ __forceinline__ void w4_table(W4St& t, float s) {
+template <int J, int MODE>
+__device__ __forceinline__ void w4_table(W4St& t, float s, float zf) {
   constexpr int q = J / 4, r = J % 4;
   if constexpr (r == 0) {
-    t.m0 = mulc<4 * q>(s);
-    t.m1 = mulc<4 * q + 1>(s);
+    t.m0 = tab_entry<4 * q, MODE>(s, zf);
+    t.m1 = tab_entry<4 * q + 1, MODE>(s, zf);
   } else if constexpr (r == 1) {
     t.p0 = pk_bf16(t.m0, t.m1);
-    t.m2 = mulc<4 * q + 2>(s);
+    t.m2 = tab_entry<4 * q + 2, MODE>(s, zf);
   } else if constexpr (r == 2) {
-    t.m3 = mulc<4 * q + 3>(s);
+    t.m3 = tab_entry<4 * q + 3, MODE>(s, zf);
     t.p1 = pk_bf16(t.m2, t.m3);
   } else {
     t.l[q] = vperm(t.p1, t.p0, 0x06040200u);
@@ -303,13 +323,24 @@ __device__ __forceinline__ void w4_chunk(W4St& u, uint32_t w) {
 // Both round the GEMM result to bf16 first, exactly where the unfused path stores it.
 // W4: Bv = g4w-packed NF4 codes of W ([N, K] when NT, [K, N] when BT, as W is stored), bscale =
 // decoded fp32 absmax transposed, [cols(W) / 64][rows(W)].
-template <int BMT, int BN, bool BT, bool SPLIT, int EPI, bool W4>
+// LoRA branches fused into the forward GEMM (LORA = true): y += xa·Bᵀ over the adapters'
+// column ranges, as nks extra 32-deep MFMA K-steps on the tile's accumulators — before the bf16
+// rounding, so the adapter term is exact to fp32 like the base product.  xa [M, 32·nks] bf16 holds
+// s_b·D_b(x)·A_bᵀ of every branch b in its k-slot [kofs_b, kofs_b + r_b) (multiples of 8, zero elsewhere:
+// lora_proj / lora_proj2 outputs); B_b [n_b, r_b] bf16 covers GEMM columns [c0_b, c0_b + n_b).  The
+// fragments come straight from global memory (16 B per lane; the tile's xa rows and B rows are
+// L2-resident).  The workgroups of tile row 0 also write B_bᵀ [r_b, n_b] for the backward's dy·B
+// projection when bt_b is given.
+template <int BMT, int BN, bool BT, bool SPLIT, int EPI, int W4, bool LORA = false>
 __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, int lda, const void* __restrict__ Bv,
                                                   int ldb, const bf16* __restrict__ residual, void* __restrict__ out,
                                                   int M, int N, int K, int splits, const bf16* __restrict__ aux,
                                                   bf16* __restrict__ aux_out, int F, float* __restrict__ ws,
-                                                  const float* __restrict__ bscale) {
+                                                  const float* __restrict__ bscale, const float* __restrict__ bzero,
+                                                  const LoraEpi lx, const LoraDx ldx) {
+  static_assert(W4 != 2 || (!BT && EPI == 0 && !LORA), "affine int4 (W4A16): the plain forward");
   static_assert(EPI == 0 || !SPLIT, "fused epilogues run on whole-K tiles");
+  static_assert(!LORA || (EPI == 0 && !SPLIT), "LoRA epilogues: plain forward / dX, whole-K tiles");
   static_assert(EPI != 1 || !BT, "SwiGLU forward epilogue: NT only");
   static_assert(EPI != 2 || BT, "SwiGLU backward epilogue: the transposed-B dX only");
   static_assert(BMT == 256 || BMT == 128, "tile heights: 256, 128");
@@ -320,7 +351,8 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   constexpr int IMG_B = BN * BK * 2;
   constexpr int STAGE = IMG_AT + IMG_B;
   constexpr int NLD = BN / 128;                // W4: 1 KB code DMAs per wave per K-tile
-  constexpr int CR_W = NLD * 1024 + 256;       // W4: a wave's codes + absmax of one K-tile (LDS ring)
+  constexpr int NSC = W4 == 2 ? 2 : 1;         // W4: per-block fp32 words per lane (absmax | scale, zero)
+  constexpr int CR_W = NLD * 1024 + 256 * NSC; // W4: a wave's codes + tables of one K-tile (LDS ring)
   constexpr int RING = W4 ? 2 * 4 * CR_W : 0;  // W4: two K-tiles of codes in flight
   constexpr int STAGES = 3 * STAGE + RING <= 160 * 1024 ? 3 : 2;
   static_assert(BN == 128 || BN == 256 || (BN == 192 && !BT), "tile widths: 128, 256 (NT / BT), 192 (NT)");
@@ -330,7 +362,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   constexpr int DA = BMT / 32;                 // A DMAs per wave per K-tile
   constexpr int DB = W4 ? 0 : BN / 32;         // B DMAs per wave per K-tile
   constexpr int D = DA + DB;                   // all DMAs per wave per K-tile
-  constexpr int NCL = W4 ? NLD + 1 : 0;        // W4: LDS-DMAs per wave per K-tile for codes + absmax
+  constexpr int NCL = W4 ? NLD + NSC : 0;      // W4: LDS-DMAs per wave per K-tile for codes + tables
   constexpr int NCH = 4 * NLD;                 // W4: 8-element chunks a lane expands per K-tile
   constexpr int KV = D + NCL;                  // vector-memory instructions per wave per K-tile
   constexpr bool BIG = NA == 8;
@@ -409,7 +441,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   // ---- W4: code / absmax DMA offsets and the LDS B-image chunk addresses of this lane's block
   uint32_t w4c[2] = {0u, 0u}, w4s = 0u, w4cstep = 0u, w4sstep = 0u;
   int w4o[8];
-  rsrc_t rss = rsb;
+  rsrc_t rss = rsb, rsz = rsb;
   if constexpr (W4) {
     const int hh = BN == 256 ? 0 : lane >> 5;   // BN = 128: the two lane halves take the block's k-halves
     if constexpr (!BT) {   // lane = one W row (tile row rt) × the K-tile's 64 k: one quant block
@@ -429,6 +461,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
       w4s = (uint32_t)(kt0 * N + n) * 4u;
       w4sstep = (uint32_t)N * 4u;
       rss = make_rsrc(bscale, (uint64_t)N * (K / 64) * 4);
+      if constexpr (W4 == 2) rsz = make_rsrc(bzero, (uint64_t)N * (K / 64) * 4);
       const int rl = rt - w * (BN / 4);   // row within the wave's BN/4 rows
 #pragma unroll
       for (int u = 0; u < NCH; ++u)
@@ -456,7 +489,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     lo[s] = ((lane >> 3) & 1) * 1024 + 16 * slot_of<false>(lane & 7, 4 * s + (lane >> 4));
-    lob[s] = ((lane >> 3) & 1) * 1024 + 16 * slot_of<W4>(lane & 7, 4 * s + (lane >> 4));
+    lob[s] = ((lane >> 3) & 1) * 1024 + 16 * slot_of<(W4 != 0)>(lane & 7, 4 * s + (lane >> 4));
   }
   const int a_off = wr * NA * 2048;
   const int b_off = wc * NB * 2048;
@@ -510,26 +543,28 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   const uint32_t ring = lds_base + STAGES * STAGE + (uint32_t)w * CR_W;
   auto dma_code_item = [&](int slot, int t, int i) {
     if (i < NLD) dma_lds(rsb, ring + slot * (4 * CR_W) + i * 1024, w4c[i], (uint32_t)t * w4cstep);
-    else dma_lds4(rss, ring + slot * (4 * CR_W) + NLD * 1024, w4s, (uint32_t)t * w4sstep);
+    else if (i == NLD) dma_lds4(rss, ring + slot * (4 * CR_W) + NLD * 1024, w4s, (uint32_t)t * w4sstep);
+    else dma_lds4(rsz, ring + slot * (4 * CR_W) + NLD * 1024 + 256, w4s, (uint32_t)t * w4sstep);
   };
   auto dma_codes = [&](int slot, int t) {
 #pragma unroll
     for (int i = 0; i < NCL; ++i) dma_code_item(slot, t, i);
   };
   u32x4 cq[2];
-  float csc = 0.f;
+  float csc = 0.f, czf = 0.f;
   auto read_codes = [&](int slot) {
     const char* rp = lds + STAGES * STAGE + slot * (4 * CR_W) + w * CR_W;
 #pragma unroll
     for (int j = 0; j < NLD; ++j) cq[j] = *reinterpret_cast<const u32x4*>(rp + j * 1024 + lane * 16);
     csc = *reinterpret_cast<const float*>(rp + NLD * 1024 + lane * 4);
+    if constexpr (W4 == 2) czf = *reinterpret_cast<const float*>(rp + NLD * 1024 + 256 + lane * 4);
   };
   W4St st4;
   // micro-op J of the expansion of the codes in cq / csc into the stage at byte offset so
   auto w4_mop = [&](auto j_c, uint32_t so) {
     constexpr int J = decltype(j_c)::value;
     if constexpr (J < 16) {
-      w4_table<J>(st4, csc);
+      w4_table<J, W4>(st4, csc, czf);
     } else {
       constexpr int u = (J - 16) / 12, p = (J - 16) % 12;
       w4_chunk<p>(st4, cq[u / 4][u % 4]);
@@ -546,6 +581,87 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   } else {
+    // ---- LoRA terms, computed in the prologue so that their operand loads overlap the first DMA wait (at
+    // the end of the tile they ran serialized — every tile of a round finishes at once: +10-13 µs per call)
+    //  NT: K-step 0 of the adapters' extra K (xa·Bᵀ) initialises the accumulators;
+    //  BT: the masked input-gradient term Σ_b D_b(ds_b·g_b·A_b) initialises them.
+    // Operands come by asm global loads issued before every DMA (so the tile-0 vmcnt wait covers them)
+    // and pinned behind that wait by an empty asm; hipcc does not track them.
+    bf16x8 lxe[8], lbe[8], lbe2[8], lxe2[8];
+    // BT: raw asm-load destinations (g rows, keep bits) — written by the loads only and first read after the
+    // tile-0 wait: any copy made before it (a select, a vector rebuild) would copy registers still in flight
+    u32x4 lkeep[2][8], lga[2][8], lgb[2][8];
+    if constexpr (LORA && !BT) {
+      const int q = lane >> 4;   // 8-deep k-block of K-step 0
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int m = min(m0 + wr * (BMT / 2) + i * 16 + (lane & 15), M - 1);
+        lxe[i] = gload16((const bf16*)lx.xa + (size_t)m * lx.ldxa + 8 * q);
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int n = n0 + wc * (BN / 2) + j * 16 + (lane & 15);
+        const bf16* src = (const bf16*)lx.xa;   // any valid address; masked below
+        int hit = -1;
+        for (int b = 0; b < lx.nbr; ++b) {
+          const int kk = 8 * q - lx.kofs[b];
+          if (n >= lx.c0[b] && n < lx.c0[b] + lx.n[b] && kk >= 0 && kk < lx.r[b]) {
+            src = (const bf16*)lx.b[b] + (size_t)(n - lx.c0[b]) * lx.r[b] + kk;
+            hit = b;
+          }
+        }
+        lbe[j] = gload16(src);
+        lkeep[0][j][0] = (uint32_t)hit;
+      }
+    }
+    if constexpr (LORA && BT) {
+      constexpr int CPR = BN / 8;
+      // A_b columns [n0, n0 + BN) as the k-rows 0..31 of a BT image per branch (LDS offset b·64·BN; rows >= r_b
+      // zero), read back by the main loop's transposed reads; the LDS is free before the prologue DMAs
+      for (int b = 0; b < ldx.nbr; ++b) {
+        const bf16* Ab = (const bf16*)ldx.a[b];
+        for (int idx = threadIdx.x; idx < 32 * CPR; idx += NT) {
+          const int kr = idx / CPR, cc = idx % CPR;
+          const int hk = (kr & 3) | ((kr >> 1) & 4);
+          const int col = n0 + 8 * cc;
+          bf16x8 v = {};
+          if (kr < ldx.r[b] && col < N) v = *reinterpret_cast<const bf16x8*>(Ab + (size_t)kr * N + col);
+          *reinterpret_cast<bf16x8*>(lds + b * (64 * BN) + kr * (2 * BN) + 16 * (cc ^ (2 * hk))) = v;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(lds + boff_t[j]));
+        const bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(lds + boff_t[j] + 4 * 2 * BN));
+        lbe[j] = bf16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+        if (ldx.nbr > 1) {
+          const bf16x4 y0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(lds + 64 * BN + boff_t[j]));
+          const bf16x4 y1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(lds + 64 * BN + boff_t[j] + 4 * 2 * BN));
+          lbe2[j] = bf16x8{y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
+        }
+      }
+      // g_b rows (fp32, 8 per lane: ranks 8·(lane/16) ..) and the keep bits of the lane's 16-byte run of
+      // k (covers its NB 16-column blocks: 4 bits per block)
+      const int kq = 8 * (lane >> 4);
+      const int kb0 = ((n0 + wc * (BN / 2)) >> 3) & ~15;   // 16-B aligned keep-byte run (N % 128 == 0)
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int m = min(m0 + wr * (BMT / 2) + i * 16 + (lane & 15), M - 1);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          if (b >= ldx.nbr) break;
+          const float* gp = ldx.g[b] + (size_t)m * ldx.ldg + (kq < ldx.r[b] ? kq : 0);
+          lga[b][i] = gload16_u(gp);
+          lgb[b][i] = gload16_u(gp + 4);
+          // keep bits: 16 B = the lane's row over [n0 + wc·BN/2, + 128) (BN/2 ≤ 128 columns)
+          lkeep[b][i] = gload16_u(ldx.keep[b] + (size_t)m * (N >> 3) + min(kb0, (N >> 3) - 16));
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+      __syncthreads();   // every wave has read the staged A images: the DMAs may overwrite them
+    }
+
     // prologue: tiles 0 .. STAGES-1 (clamped: past the last tile the DMAs re-stage tile nk-1 into
     // stages nobody reads again), wait for tile 0, read its first half.  W4: the B images of those
     // tiles are expanded here first; then the vector-memory stream takes its steady-state order
@@ -571,6 +687,76 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
       wait_vmcnt<(STAGES - 1) * D>();
     }
     __builtin_amdgcn_s_barrier();
+    if constexpr (LORA && !BT) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) pin(lxe[i]);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        pin(lbe[j]);
+        const int hit = (int)lkeep[0][j][0];
+        if (hit < 0) lbe[j] = bf16x8{};
+        else if (tm == 0 && lx.bt[hit] != nullptr) {   // Bᵀ [r_b, n_b] for the backward, once per column
+          const int n = n0 + wc * (BN / 2) + j * 16 + (lane & 15);
+          const int kk = 8 * (lane >> 4) - lx.kofs[hit];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ((bf16*)lx.bt[hit])[(size_t)(kk + e) * lx.n[hit] + (n - lx.c0[hit])] = lbe[j][e];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NA; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) mfma_zero(acc[i][j], lbe[j], lxe[i]);
+    }
+    if constexpr (LORA && BT) {
+      const int kq = 8 * (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          if (b >= ldx.nbr) break;
+          pinu(lga[b][i]);
+          pinu(lgb[b][i]);
+          pinu(lkeep[b][i]);
+          bf16x8 a;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float v = __builtin_bit_cast(float, e < 4 ? lga[b][i][e] : lgb[b][i][e - 4]);
+            a[e] = kq + e < ldx.r[b] ? (bf16)v : (bf16)0.f;
+          }
+          (b ? lxe2[i] : lxe[i]) = a;
+        }
+      }
+      const int sub = ((lane >> 4) & 1) * 4;   // the lane's 4 columns inside each 8-column keep byte
+      const int kb0 = ((n0 + wc * (BN / 2)) >> 3) & ~15;
+      const int rel = ((n0 + wc * (BN / 2)) >> 3) - min(kb0, (N >> 3) - 16);
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          f32x4 v = acc[i][j];
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            if (b >= ldx.nbr) break;
+            const f32x4 t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b ? lbe2[j] : lbe[j], b ? lxe2[i] : lxe[i],
+                                                                   f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            const u32x4 kw = b ? lkeep[1][i] : lkeep[0][i];
+            const int byte = min(rel + 2 * j + (lane >> 5), 15);   // (16 j + 4 (lane>>4)) / 8 into the run
+            const uint32_t bits = (kw[byte >> 2] >> (8 * (byte & 3) + sub)) & 15u;
+            const float ds = ldx.ds[b];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += ((bits >> e) & 1u) ? t[e] * ds : 0.f;
+          }
+          acc[i][j] = v;
+          asm volatile("" : "+a"(acc[i][j]));   // into the AGPRs here, not right before the first MFMA
+        }
+      }
+      // the inline-asm MFMAs read acc as SrcC; the compiler's hazard checks do not see into them, so the
+      // v_accvgpr_write → MFMA SrcC distance is padded by hand (without it the last-written lane of a
+      // tile read a stale value: non-finite dX entries in every 4th column)
+      asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) read_item(fa0, fb0, lds, 0, r);
 
@@ -622,9 +808,45 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
       });
       cur = cur + STAGE == STAGES * STAGE ? 0 : cur + STAGE;
     };
-    body(std::integral_constant<bool, true>{}, 0);
+    body(std::integral_constant<bool, !LORA>{}, 0);
     for (int t = 1; t < nk; ++t) body(std::integral_constant<bool, false>{}, t);
     asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  }
+
+  if constexpr (LORA && !BT) {   // K-steps 1 .. nks-1 of the adapters (step 0 ran in the prologue)
+    const int kb = lane >> 4;
+    if (lx.nks > 1) {
+    for (int s = 1; s < lx.nks; ++s) {
+      bf16x8 xe[8], be[8];
+      const int q = 4 * s + kb;   // this lane's 8-deep k-block of the extra K
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int m = min(m0 + wr * (BMT / 2) + i * 16 + (lane & 15), M - 1);
+        xe[i] = *reinterpret_cast<const bf16x8*>((const bf16*)lx.xa + (size_t)m * lx.ldxa + 8 * q);
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int n = n0 + wc * (BN / 2) + j * 16 + (lane & 15);
+        bf16x8 v = {};
+        for (int b = 0; b < lx.nbr; ++b) {
+          const int kk = 8 * q - lx.kofs[b];
+          if (n >= lx.c0[b] && n < lx.c0[b] + lx.n[b] && kk >= 0 && kk < lx.r[b]) {
+            v = *reinterpret_cast<const bf16x8*>((const bf16*)lx.b[b] + (size_t)(n - lx.c0[b]) * lx.r[b] + kk);
+            if (tm == 0 && lx.bt[b] != nullptr) {   // Bᵀ [r_b, n_b] for the backward, once per column
+#pragma unroll
+              for (int e = 0; e < 8; ++e) ((bf16*)lx.bt[b])[(size_t)(kk + e) * lx.n[b] + (n - lx.c0[b])] = v[e];
+            }
+          }
+        }
+        be[j] = v;
+      }
+#pragma unroll
+      for (int i = 0; i < NA; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) mfma_acc(acc[i][j], be[j], xe[i]);
+    }
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 2" ::: "memory");   // MFMA results → AGPR reads below
+    }
   }
 
   // ---- epilogue: lane holds C[m = col][n = 4·(lane>>4) + r … +3] of each 16×16 block
@@ -727,7 +949,8 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
 }
 
 // out = Σ_s ws[s] (+ residual), 16 elements per thread with every load issued before the first add
-// (10 16-B loads in flight per lane at 2 splits: the slabs were just written and mostly hit the MALL).
+// (10 16-B loads in flight per lane at 2 splits; default cache policy: the slabs were just written and
+// mostly hit the MALL — non-temporal loads measured 20.8 vs 15 µs per call).
 // SP: the split count (2 or 4), or 0 = any count up to 8 (runtime).  A tail of 8 (M·N % 16 == 8) runs
 // the 8-wide path.
 template <int SP>
@@ -760,7 +983,7 @@ __global__ __launch_bounds__(256) void splitk_sum_k(const float* __restrict__ ws
   for (int s = 0; s < MAXS; ++s) {
     if (s >= ns) break;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) v[s][q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ws + (size_t)s * MN + i) + q);
+    for (int q = 0; q < 4; ++q) v[s][q] = reinterpret_cast<const f32x4*>(ws + (size_t)s * MN + i)[q];
   }
   bf16x8 r0, r1;
   if (residual) {
@@ -892,7 +1115,8 @@ int gemm4w_tiles(int M, int N, int bm, int bn) { return tiles_of(M, N, bm, bn); 
 // ws: splits·M·N fp32 slabs (splits > 1).  Callers pass the (bm, bn, splits) that gemm4w_plan
 // returned.  bscale != nullptr: B is g4w-packed NF4 codes, bscale the transposed fp32 block absmax.
 void launch_gemm4w(const void* A, int lda, const void* B, int ldb, const void* residual, void* out, float* ws,
-                   const float* bscale, int M, int N, int K, int splits, bool bt, int bn, int bm, hipStream_t st) {
+                   const float* bscale, const float* bzero, int M, int N, int K, int splits, bool bt, int bn, int bm,
+                   hipStream_t st) {
   const int tiles = tiles_of(M, N, bm, bn);
   const bool split = splits > 1;
   const bf16* a = (const bf16*)A;
@@ -901,19 +1125,21 @@ void launch_gemm4w(const void* A, int lda, const void* B, int ldb, const void* r
   const int grid = tiles * (split ? splits : 1), sp = split ? splits : 1;
 #define G4W(BM_, BN_, BT_, SP_, W4_)                                                                            \
   gemm4w_k<BM_, BN_, BT_, SP_, 0, W4_><<<grid, NT, 0, st>>>(a, lda, B, ldb, r, o, M, N, K, sp, nullptr, nullptr, \
-                                                             0, ws, bscale)
+                                                             0, ws, bscale, bzero, LoraEpi{}, LoraDx{})
 #define G4W_SP(BM_, BN_, BT_, W4_) \
   if (split) G4W(BM_, BN_, BT_, true, W4_); else G4W(BM_, BN_, BT_, false, W4_);
 #define G4W_BN(BM_)                                                                           \
-  if (bscale) {                                                                               \
-    if (bn == 256) { if (bt) { G4W_SP(BM_, 256, true, true) } else { G4W_SP(BM_, 256, false, true) } } \
-    else { if (bt) { G4W_SP(BM_, 128, true, true) } else { G4W_SP(BM_, 128, false, true) } }           \
+  if (bzero) {                                                                                \
+    if (bn == 256) { G4W_SP(BM_, 256, false, 2) } else { G4W_SP(BM_, 128, false, 2) }         \
+  } else if (bscale) {                                                                        \
+    if (bn == 256) { if (bt) { G4W_SP(BM_, 256, true, 1) } else { G4W_SP(BM_, 256, false, 1) } } \
+    else { if (bt) { G4W_SP(BM_, 128, true, 1) } else { G4W_SP(BM_, 128, false, 1) } }           \
   } else if (bn == 256) {                                                                     \
-    if (bt) { G4W_SP(BM_, 256, true, false) } else { G4W_SP(BM_, 256, false, false) }         \
+    if (bt) { G4W_SP(BM_, 256, true, 0) } else { G4W_SP(BM_, 256, false, 0) }                 \
   } else if (bn == 192) {                                                                     \
-    G4W_SP(BM_, 192, false, false)                                                            \
+    G4W_SP(BM_, 192, false, 0)                                                                \
   } else {                                                                                    \
-    if (bt) { G4W_SP(BM_, 128, true, false) } else { G4W_SP(BM_, 128, false, false) }         \
+    if (bt) { G4W_SP(BM_, 128, true, 0) } else { G4W_SP(BM_, 128, false, 0) }                 \
   }
   if (bm == 256) {
     G4W_BN(256)
@@ -934,6 +1160,50 @@ void launch_gemm4w(const void* A, int lda, const void* B, int ldb, const void* r
   LIPA_CHECK_LAUNCH();
 }
 
+// y = x·Wᵀ + Σ_b xa_b·B_bᵀ (LoRA branches in the epilogue) (+ residual), whole-K tiles (bm, bn from
+// gemm4w_plan with splits = 1)
+void launch_gemm4w_lora(const void* A, int lda, const void* B, int ldb, const float* bscale, const void* residual,
+                        void* out, const LoraEpi& lx, int M, int N, int K, int bn, int bm, hipStream_t st) {
+  const int tiles = tiles_of(M, N, bm, bn);
+  const bf16* a = (const bf16*)A;
+  const bf16* r = (const bf16*)residual;
+#define G4L(BM_, BN_, W4_)                                                                                       \
+  gemm4w_k<BM_, BN_, false, false, 0, W4_, true><<<tiles, NT, 0, st>>>(a, lda, B, ldb, r, out, M, N, K, 1,       \
+                                                                       nullptr, nullptr, 0, nullptr, bscale, nullptr, lx, LoraDx{})
+  if (bscale) {
+    if (bm == 256) { if (bn == 256) G4L(256, 256, 1); else G4L(256, 128, 1); }
+    else { if (bn == 256) G4L(128, 256, 1); else G4L(128, 128, 1); }
+  } else if (bm == 256) {
+    if (bn == 256) G4L(256, 256, 0); else if (bn == 192) G4L(256, 192, 0); else G4L(256, 128, 0);
+  } else {
+    if (bn == 256) G4L(128, 256, 0); else if (bn == 192) G4L(128, 192, 0); else G4L(128, 128, 0);
+  }
+#undef G4L
+  LIPA_CHECK_LAUNCH();
+}
+
+// dX = dY·W + the adapters' masked input-gradient term (LoraDx), whole-K transposed-B tiles
+void launch_gemm4w_loradx(const void* A, int lda, const void* B, int ldb, const float* bscale, const void* residual,
+                          void* out, const LoraDx& ld, int M, int N, int K, int bn, int bm, hipStream_t st) {
+  const int tiles = tiles_of(M, N, bm, bn);
+  const bf16* a = (const bf16*)A;
+  const bf16* r = (const bf16*)residual;
+#define G4X(BM_, BN_, W4_)                                                                                     \
+  gemm4w_k<BM_, BN_, true, false, 0, W4_, true><<<tiles, NT, 0, st>>>(a, lda, B, ldb, r, out, M, N, K, 1,       \
+                                                                      nullptr, nullptr, 0, nullptr, bscale,     \
+                                                                      nullptr, LoraEpi{}, ld)
+  if (bscale) {
+    if (bm == 256) { if (bn == 256) G4X(256, 256, 1); else G4X(256, 128, 1); }
+    else { if (bn == 256) G4X(128, 256, 1); else G4X(128, 128, 1); }
+  } else if (bm == 256) {
+    if (bn == 256) G4X(256, 256, 0); else G4X(256, 128, 0);
+  } else {
+    if (bn == 256) G4X(128, 256, 0); else G4X(128, 128, 0);
+  }
+#undef G4X
+  LIPA_CHECK_LAUNCH();
+}
+
 // gu [M, 2F] and h = silu(gate)·up [M, F] from x [M, K] and W_gu [2F, K] ([gate | up] rows), one launch
 void launch_gemm4w_swiglu(const void* X, int ldx, const void* W, const float* wscale, void* gu, void* h, int M, int F,
                           int K, int bn, int bm, hipStream_t st) {
@@ -942,14 +1212,14 @@ void launch_gemm4w_swiglu(const void* X, int ldx, const void* W, const float* ws
   const bf16* a = (const bf16*)X;
 #define G4S(BM_, BN_, W4_)                                                                                        \
   gemm4w_k<BM_, BN_, false, false, 1, W4_><<<tiles, NT, 0, st>>>(a, ldx, W, K, nullptr, gu, M, N, K, 1, nullptr, \
-                                                                  (bf16*)h, F, nullptr, wscale)
+                                                                  (bf16*)h, F, nullptr, wscale, nullptr, LoraEpi{}, LoraDx{})
   if (wscale) {
-    if (bm == 256) { if (bn == 256) G4S(256, 256, true); else G4S(256, 128, true); }
-    else { if (bn == 256) G4S(128, 256, true); else G4S(128, 128, true); }
+    if (bm == 256) { if (bn == 256) G4S(256, 256, 1); else G4S(256, 128, 1); }
+    else { if (bn == 256) G4S(128, 256, 1); else G4S(128, 128, 1); }
   } else if (bm == 256) {
-    if (bn == 256) G4S(256, 256, false); else if (bn == 192) G4S(256, 192, false); else G4S(256, 128, false);
+    if (bn == 256) G4S(256, 256, 0); else if (bn == 192) G4S(256, 192, 0); else G4S(256, 128, 0);
   } else {
-    if (bn == 256) G4S(128, 256, false); else if (bn == 192) G4S(128, 192, false); else G4S(128, 128, false);
+    if (bn == 256) G4S(128, 256, 0); else if (bn == 192) G4S(128, 192, 0); else G4S(128, 128, 0);
   }
 #undef G4S
   LIPA_CHECK_LAUNCH();
@@ -962,14 +1232,14 @@ void launch_gemm4w_dswiglu(const void* DY, int lddy, const void* W, const float*
   const bf16* a = (const bf16*)DY;
 #define G4D(BM_, BN_, W4_)                                                                                        \
   gemm4w_k<BM_, BN_, true, false, 2, W4_><<<tiles, NT, 0, st>>>(a, lddy, W, F, nullptr, dgu, M, F, Nw, 1,        \
-                                                                 (const bf16*)gu, nullptr, F, nullptr, wscale)
+                                                                 (const bf16*)gu, nullptr, F, nullptr, wscale, nullptr, LoraEpi{}, LoraDx{})
   if (wscale) {
-    if (bm == 256) { if (bn == 256) G4D(256, 256, true); else G4D(256, 128, true); }
-    else { if (bn == 256) G4D(128, 256, true); else G4D(128, 128, true); }
+    if (bm == 256) { if (bn == 256) G4D(256, 256, 1); else G4D(256, 128, 1); }
+    else { if (bn == 256) G4D(128, 256, 1); else G4D(128, 128, 1); }
   } else if (bm == 256) {
-    if (bn == 256) G4D(256, 256, false); else G4D(256, 128, false);
+    if (bn == 256) G4D(256, 256, 0); else G4D(256, 128, 0);
   } else {
-    if (bn == 256) G4D(128, 256, false); else G4D(128, 128, false);
+    if (bn == 256) G4D(128, 256, 0); else G4D(128, 128, 0);
   }
 #undef G4D
   LIPA_CHECK_LAUNCH();

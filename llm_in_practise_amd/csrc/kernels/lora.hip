@@ -925,8 +925,7 @@ void launch_lora_proj(const void* X, int ldx, const void* W, int r, int K, float
   const uint32_t thr = p > 0.f ? (uint32_t)(p * 65536.0f + 0.5f) : 0u;
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
   // 16-row workgroups leave half of the 256 CUs idle below M = 4096: use 8 (zero-padded MFMA rows)
-  static const int rw_env = [] { const char* e = getenv("LIPA_LORA_PROJ_RW"); return e ? atoi(e) : 0; }();
-  const int rw = rw_env ? rw_env : (M < 4096 ? 8 : 16);
+  const int rw = M < 4096 ? 8 : 16;
   const int grid = (M + rw - 1) / rw;
   if (K % (16 * 32) == 0 && rw == 8)
     lora_proj_k<16, 8><<<grid, 1024, 0, st>>>((const bf16*)X, ldx, (const bf16*)W, r, K, outf, ldof, (bf16*)outb, ldob,
@@ -945,8 +944,6 @@ void launch_lora_proj(const void* X, int ldx, const void* W, int r, int K, float
 // with DX: DX[m,k] += D(Σ_j G[m,j]·W[j,k]).
 // Chunk height: 64 rows, or 32 when that leaves fewer than 256 workgroups (narrow K).
 static int lora_acc_rows(int M, int K) {
-  static const int forced = [] { const char* e = getenv("LIPA_LORA_ROWS"); return e ? atoi(e) : 0; }();
-  if (forced == 32 || forced == 64 || forced == 128 || forced == 256) return forced;
   return ((K / 8 + 63) / 64) * ((M + 63) / 64) >= 256 ? 64 : 32;
 }
 int lora_acc_chunks(int M, int K) { const int rows = lora_acc_rows(M, K); return (M + rows - 1) / rows; }
@@ -956,20 +953,15 @@ void launch_lora_acc(const float* G, int ldg, int r, const void* X, int ldx, voi
                      hipStream_t st) {
   const uint32_t thr = p > 0.f ? (uint32_t)(p * 65536.0f + 0.5f) : 0u;
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  static const bool valu_only = getenv("LIPA_LORA_ACC_VALU") != nullptr;
-  if (!part && r <= 16 && K % 128 == 0 && ldx % 8 == 0 && ldg % 4 == 0 && ((uintptr_t)G & 15) == 0 && !valu_only) {
-    // matrix-core path (deterministic mode keeps the VALU kernel's fixed-order partials)
-    static const int sub_env = [] { const char* e = getenv("LIPA_LORA_SUB"); return e ? atoi(e) : 0; }();
-    const int sub = sub_env == 2 ? 2 : 1;   // 32 rows per wave: 2 waves/SIMD beat longer waves (-10-25 %)
+  if (!part && r <= 16 && K % 128 == 0 && ldx % 8 == 0 && ldg % 4 == 0 && ((uintptr_t)G & 15) == 0) {
+    // matrix-core path (deterministic mode keeps the VALU kernel's fixed-order partials); 32 rows per
+    // wave: 2 waves/SIMD beat longer waves (-10-25 %, profiles/lora_acc_mfma_ab.txt)
+    constexpr int sub = 1;
     dim3 g2(K / 128, (M + 128 * sub - 1) / (128 * sub));
 #define C(R_, D_, S_)                                                                                        \
   lora_acc_mfma_k<R_, D_, S_><<<g2, 256, 0, st>>>(G, ldg, r, (const bf16*)X, ldx, (bf16*)DX, lddx,            \
                                                   (const bf16*)W, K, out, sj, sk, M, key, thr, ds, mask_ld)
-#define D2(R_, D_) \
-  if (sub == 2)    \
-    C(R_, D_, 2);  \
-  else             \
-    C(R_, D_, 1)
+#define D2(R_, D_) C(R_, D_, 1)
     if (r <= 8) {
       if (DX) { D2(8, true); } else { D2(8, false); }
     } else {
@@ -1007,8 +999,7 @@ void launch_lora_acc(const float* G, int ldg, int r, const void* X, int ldx, voi
 
 // split-K lora_proj2s_k: NS (K per wave / 32) giving >= 256 workgroups, 0 = not applicable (old kernel)
 int lora_proj2_ns(int M, int K) {
-  static const int impl = [] { const char* e = getenv("LIPA_PROJ2_IMPL"); return e ? atoi(e) : 1; }();
-  if (impl == 0 || M <= 0) return 0;
+  if (M <= 0) return 0;
   const int nrb = (M + 63) / 64;
   for (int ns = 4; ns >= 1; ns /= 2)
     if (K % (128 * ns) == 0 && (nrb * (K / (128 * ns)) >= 256 || ns == 1)) return ns;
@@ -1137,18 +1128,10 @@ void launch_lora_dA_pair(const float* G0, const float* G1, int ldg, int r, const
 void launch_lora_dx2(const float* G0, const float* G1, int ldg, const void* A0, const void* A1, int r0, int r1,
                      const uint8_t* kb0, const uint8_t* kb1, float ds0, float ds1, void* out, int M, int K,
                      hipStream_t st) {
-  static const int rpt = [] { const char* e = getenv("LIPA_LORA_DX_RPT"); return e ? atoi(e) : 16; }();
-  if (rpt == 16 && r0 <= 8 && r1 <= 8) {
+  if (r0 <= 8 && r1 <= 8) {
     dim3 g16((K / 8 + 255) / 256, (M + 15) / 16);
     lora_dx2_r16_k<<<g16, 256, 0, st>>>(G0, G1, ldg, (const bf16*)A0, (const bf16*)A1, r0, r1, kb0, kb1, ds0, ds1,
                                        (bf16*)out, M, K);
-    LIPA_CHECK_LAUNCH();
-    return;
-  }
-  if (rpt == 8) {
-    dim3 g8((K / 8 + 63) / 64, (M + 31) / 32);
-    lora_dx2_k<8><<<g8, 256, 0, st>>>(G0, G1, ldg, (const bf16*)A0, (const bf16*)A1, r0, r1, kb0, kb1, ds0, ds1,
-                                      (bf16*)out, M, K);
     LIPA_CHECK_LAUNCH();
     return;
   }

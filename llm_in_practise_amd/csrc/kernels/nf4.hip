@@ -1,90 +1,19 @@
-// Weight-only GEMMs on gfx950 MFMA: the NF4 dequant-GEMM used by QLoRA
-// (forward Y = X·deq(W)ᵀ and backward dX = dY·deq(W)) and the bf16 frozen-base GEMM, both
-// with the LoRA low-rank product fused as an extra K-slice and the residual add fused into
-// the epilogue.
-//
-// Design (MI355X-first, not a CUDA tiling):
-//  * Output tile 128 (or 256) tokens × 128 weight-columns per 256-thread workgroup; the 4
-//    waves split the 128 columns (32 each) and every wave covers ALL tile rows, so each
-//    weight element is dequantised exactly once per workgroup (no dequant redundancy).
-//  * Weights never touch LDS: NF4 codes are stored in a fragment-native layout (one 16-B
-//    load per lane per 64-deep K-step gives the lane its four MFMA A-fragments), are
-//    dequantised in registers (16-entry code table in LDS, ×absmax, v_cvt_pk_bf16_f32) and
-//    fed to v_mfma_f32_16x16x32_bf16 directly.  The backward uses a second fragment-native
-//    packing of the SAME codes (nibbles grouped along the output-row axis) so dX needs no
-//    transpose: both layouts are permutations of the bitsandbytes codes.
-//  * Activations (X / dY) are the MFMA B operand: staged HBM→LDS with global_load_lds
-//    (16 B per lane, LDS-DMA, no VGPR round trip) into a double-buffered tile whose 16-B
-//    chunks are XOR-swizzled through the per-lane SOURCE address (chunk ^= (row>>1)&7), which
-//    makes every ds_read_b128 fragment read bank-conflict free.
-//  * Operand roles are swapped (W is the A operand) so each lane's accumulator holds 4
-//    consecutive output columns of one token row → 8-byte epilogue stores / residual loads.
-//  * XCD-aware bijective block remap: the workgroups that share one weight column-tile run
-//    on one XCD, so its L2 serves the codes to all of them.
+// NF4 (bitsandbytes layout) quantisation and bf16 expansion on gfx950: the
+// QLoRA load-time quantiser (bf16 → 4-bit codes + fp32 block absmax, 64-element blocks) and the
+// HBM-speed expansion kernels behind the "expand" NF4 form (ops/linear.py ``_nf4_expand``: one bf16
+// copy that the forward and the dX GEMM share).  The dequant-GEMM itself — NF4 codes fed straight
+// into the MFMA GEMM — is csrc/kernels/gemm4w.hip (W4 = 1).
 #include "common.h"
 
 using namespace lipa;
 
 namespace {
 
-constexpr int BN = 128;     // weight columns per workgroup
-constexpr int BK = 64;      // reduction depth per K-step (= NF4 block size)
-constexpr int NTHR = 256;
-
 __constant__ float kNF4[16] = {
     -1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f,
     -0.28444138169288635f, -0.18477343022823334f, -0.09105003625154495f, 0.0f,
     0.07958029955625534f, 0.16093020141124725f, 0.24611230194568634f, 0.33791524171829224f,
     0.44070982933044434f, 0.5626170039176941f, 0.7229568362236023f, 1.0f};
-
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
-
-// ------------------------------------------------------------------ packing / (de)quantisation
-// bnb-layout codes [N][K/2] (high nibble = even k) → fragment-native packed dwords
-__global__ __launch_bounds__(256) void pack_nf4_k(const uint8_t* __restrict__ src, uint32_t* __restrict__ dst, int N,
-                                                  int K, int bwd) {
-  const size_t total = (size_t)N * K / 8;
-  const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= total) return;
-  const int C = bwd ? K : N, R = bwd ? N : K;
-  const int d = idx & 3;
-  const int lane = (idx >> 2) & 63;
-  const size_t rest = idx >> 8;
-  const int nk = R / 64;
-  const int tk = rest % nk;
-  const int T = rest / nk;
-  const int st = d >> 1, s = d & 1;
-  const int c = 32 * T + 16 * st + (lane & 15);
-  const int rb = 64 * tk + 32 * s + 8 * (lane >> 4);
-  uint32_t v = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int r = rb + j;
-    const int n = bwd ? r : c, k = bwd ? c : r;
-    const uint8_t byte = src[(size_t)n * (K / 2) + (k >> 1)];
-    const uint32_t nib = (k & 1) ? (byte & 15) : (byte >> 4);
-    v |= nib << (4 * j);
-  }
-  dst[idx] = v;
-}
-
-// per-block absmax (row-major [N][K/64], fp32 or double-quant) → absmax_t [K/64][N] fp32
-__global__ __launch_bounds__(256) void absmax_t_k(const float* __restrict__ absmax, const uint8_t* __restrict__ qabs,
-                                                  const float* __restrict__ absmax2, const float* __restrict__ offset,
-                                                  const float* __restrict__ dcode, float* __restrict__ out, int N,
-                                                  int KB) {
-  const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (size_t)N * KB) return;
-  const int n = idx / KB, kb = idx % KB;
-  float v;
-  if (absmax) v = absmax[idx];
-  else {
-    const size_t g = idx / 256;
-    v = dcode[qabs[idx]] * absmax2[g] + offset[g];
-  }
-  out[(size_t)kb * N + n] = v;
-}
 
 // w [N][K] bf16 → codes [N][K/2] (bnb layout), absmax [N*K/64]; one lane per 8 elements
 __global__ __launch_bounds__(256) void nf4_quantize_k(const bf16* __restrict__ w, uint8_t* __restrict__ codes,
@@ -204,41 +133,6 @@ __global__ __launch_bounds__(256) void nf4_dequant_k(const uint8_t* __restrict__
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
-bool gemm_w4v2_supported(int M, int C, int R, int lda);
-void launch_gemm_w4v2(int bwd, const void* A, int lda, const uint32_t* codes, const float* absmax_t,
-                      const void* ext_a, const void* ext_b, int R_ext, const void* residual, void* out, int M, int C,
-                      int R, hipStream_t st);
-
-// NF4 register-dequant MFMA GEMM (gemm2.hip; the gen-1 kernel of round 1 and the gen-3 256-entry
-// pair-table variant, slower end-to-end — profiles/gemm_gen3_ab.txt — are retired)
-bool gemm_w4_supported(int M, int C, int R, int lda) { return gemm_w4v2_supported(M, C, R, lda); }
-void launch_gemm_w4(int bwd, const void* A, int lda, const uint32_t* codes, const float* absmax_t, const void* ext_a,
-                    const void* ext_b, int R_ext, const void* residual, void* out, int M, int C, int R,
-                    hipStream_t st) {
-  launch_gemm_w4v2(bwd, A, lda, codes, absmax_t, ext_a, ext_b, R_ext, residual, out, M, C, R, st);
-}
-
-void launch_gemm_int4(const void* A, int lda, const uint32_t* codes, const float* scale_t, const float* bias_t,
-                      const void* ext_a, const void* ext_b, int R_ext, const void* residual, void* out, int M, int N,
-                      int K, hipStream_t st);
-void launch_gemm_int4_any(const void* A, int lda, const uint32_t* codes, const float* scale_t, const float* bias_t,
-                          const void* ext_a, const void* ext_b, int R_ext, const void* residual, void* out, int M, int N,
-                          int K, hipStream_t st) {
-  launch_gemm_int4(A, lda, codes, scale_t, bias_t, ext_a, ext_b, R_ext, residual, out, M, N, K, st);
-}
-
-void launch_pack_nf4(const uint8_t* src, uint32_t* dst, int N, int K, int bwd, hipStream_t st) {
-  const size_t total = (size_t)N * K / 8;
-  pack_nf4_k<<<(total + 255) / 256, 256, 0, st>>>(src, dst, N, K, bwd);
-  LIPA_CHECK_LAUNCH();
-}
-
-void launch_absmax_t(const float* absmax, const uint8_t* qabs, const float* absmax2, const float* offset,
-                     const float* dcode, float* out, int N, int K, hipStream_t st) {
-  const size_t total = (size_t)N * (K / 64);
-  absmax_t_k<<<(total + 255) / 256, 256, 0, st>>>(absmax, qabs, absmax2, offset, dcode, out, N, K / 64);
-  LIPA_CHECK_LAUNCH();
-}
 
 void launch_nf4_quantize(const void* w, uint8_t* codes, float* absmax, size_t nelem, hipStream_t st) {
   const size_t vecs = nelem / 8;

@@ -386,16 +386,12 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_split_k(const bf16* __restric
   }
 }
 
-// waves per row (LIPA_NORM_WPR = 2 | 4; 4 needs N >= 2048); the template's CH is N / (512·WPR)
-static int norm_wpr(int ch) {
-  static const int v = [] { const char* e = getenv("LIPA_NORM_WPR"); return e ? atoi(e) : 2; }();
-  return v == 4 && ch >= 2 ? 4 : 2;
-}
+// waves per row: 2 (4 measured no faster at the Qwen3 widths); the template's CH is N / (512·WPR)
+static int norm_wpr(int) { return 2; }
 
-// split-row form for bf16 rows of N = 1024·{1, 2, 4, 8}; LIPA_NORM_SPLIT=0 keeps one wave per row
+// split-row form for bf16 rows of N = 1024·{1, 2, 4, 8}
 static int norm_split_ch(int dtype, int N) {
-  static const bool off = [] { const char* e = getenv("LIPA_NORM_SPLIT"); return e && atoi(e) == 0; }();
-  if (off || dtype != 1 || N % 1024) return 0;
+  if (dtype != 1 || N % 1024) return 0;
   const int ch = N / 1024;
   return (ch == 1 || ch == 2 || ch == 4 || ch == 8) ? ch : 0;
 }

@@ -1,0 +1,215 @@
+// W4A16 GEMM for decode batches and short prefills (the AWQ / GPTQ / RTN int4 serving
+// artifact of Quantization/LoRA-AWQ and Deployment/litellm-proxy/docker-compose-router-lb.yaml:85):
+//     y[M, N] = x[M, K] · deq(W)ᵀ (+ residual),   M <= 64,   deq(W)[n, k] = q·s[n, g] + b[n, g]
+// with W as 4-bit codes (uint8 [N, K/2], high nibble = even k) and one fp32 (scale, bias = −zero·scale)
+// per (row, 128·j-deep group).
+//
+// At these M the cost is streaming W once (N·K/2 bytes), so the design is about bytes in flight and
+// a cheap dequant, with the matrix cores doing the arithmetic:
+//  * grid = (N/128 column spans) × (KS K-slices); a 256-thread workgroup owns 128 columns × 128·NKB
+//    of K, each wave 32 columns (two 16-column MFMA tiles); every code (16 B per lane per tile and
+//    128-deep block) and scale of the wave's whole slice is loaded up front — 4-16 KB per wave in
+//    flight, the whole matrix in flight across the chip;
+//  * dequant in 7 VALU per 8 weights and no conversion: a nibble q becomes the bf16 bit pattern
+//    0x4300|q = 128+q by a byte permute (v_perm with a 0x43 byte plane), so the MFMA accumulates
+//    G = Σ x·(128+q) per group; a second MFMA against a ones operand gives X = Σ x, and the group
+//    folds as y += s·G + (b − 128·s)·X — scale and zero point never touch the weights;
+//  * the permute yields the lane's 8 weights in k order (1,3,5,7,0,2,4,6); x is staged once per
+//    workgroup into LDS (M × 128·NKB, 16-B padded rows: conflict-free ds_read_b128) in the same
+//    order, so every A/B k-slot pair matches (the MFMA sum is order-free);
+//  * v_mfma_f32_16x16x32_bf16 with x as A (rows = tokens, 16 per tile, RT tiles) and the codes as B;
+//    the lane's B column is its load column, so its output column needs just its own (s, c) pair;
+//  * KS > 1: fp32 partials [KS, M, N] + one reduce launch (the residual folds there); KS = 1 writes
+//    bf16 directly.  XCD-aware block order: the column spans of one K-slice (same x slice) share an
+//    L2.
+#include "common.h"
+
+using namespace lipa;
+
+namespace {
+
+constexpr int W4_CT = 2;                      // 16-column MFMA tiles per wave
+constexpr int W4_COLS = 4 * 16 * W4_CT;       // columns per workgroup
+
+__device__ __forceinline__ uint32_t vperm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// one code dword (k = 0..7; byte i = q[2i] << 4 | q[2i+1]) → four bf16 pairs of 128+q in k order
+// (1,3) (5,7) (0,2) (4,6)
+__device__ __forceinline__ bf16x8 i4_bf16(uint32_t w) {
+  constexpr uint32_t C = 0x43434343u;
+  const uint32_t lo = w & 0x0F0F0F0Fu, hi = (w >> 4) & 0x0F0F0F0Fu;
+  u32x4 o;
+  o[0] = vperm(C, lo, 0x04010400u);
+  o[1] = vperm(C, lo, 0x04030402u);
+  o[2] = vperm(C, hi, 0x04010400u);
+  o[3] = vperm(C, hi, 0x04030402u);
+  return __builtin_bit_cast(bf16x8, o);
+}
+
+// 8 bf16 of x in k order → the same (1,3,5,7,0,2,4,6) order
+__device__ __forceinline__ u32x4 x_perm(u32x4 d) {
+  u32x4 o;
+  o[0] = vperm(d[1], d[0], 0x07060302u);
+  o[1] = vperm(d[3], d[2], 0x07060302u);
+  o[2] = vperm(d[1], d[0], 0x05040100u);
+  o[3] = vperm(d[3], d[2], 0x05040100u);
+  return o;
+}
+
+template <int RT, int NKB>
+__global__ __launch_bounds__(256) void w4mm_k(const bf16* __restrict__ X, int ldx, const uint8_t* __restrict__ codes,
+                                              const float2* __restrict__ sc, int gs, const bf16* __restrict__ residual,
+                                              bf16* __restrict__ out, float* __restrict__ part, int M, int N, int K,
+                                              int ncs) {
+  constexpr int KR = 128 * NKB;           // K per workgroup
+  constexpr int LDXS = KR + 8;            // LDS row stride (bf16): 16-B pad
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  bf16* xs = reinterpret_cast<bf16*>(lds_raw);
+  const int KS = gridDim.x / ncs;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int cs = id % ncs, ks = id / ncs;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, li = lane & 15, q = lane >> 4;
+  const int k0 = ks * KR;
+  const int G = K / gs;
+
+  // 1) the wave's codes and (scale, c) pairs for the whole K slice, all in flight at once
+  u32x4 cq[NKB][W4_CT];
+  float2 s2[NKB][W4_CT];
+  int ncol[W4_CT];
+#pragma unroll
+  for (int ct = 0; ct < W4_CT; ++ct) ncol[ct] = min(cs * W4_COLS + 32 * w + 16 * ct + li, N - 1);
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+    for (int ct = 0; ct < W4_CT; ++ct) {
+      const int kk = k0 + 128 * kb;
+      cq[kb][ct] = *reinterpret_cast<const u32x4*>(codes + (size_t)ncol[ct] * (K / 2) + (kk + 32 * q) / 2);
+      s2[kb][ct] = sc[(size_t)ncol[ct] * G + kk / gs];
+    }
+
+  // 2) x slice → LDS, permuted to the dequant's k order; rows >= M are zero
+  constexpr int CH = KR / 8;              // 16-B chunks per row
+  for (int c = tid; c < RT * 16 * CH; c += 256) {
+    const int r = c / CH, kc = c - r * CH;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (r < M) v = x_perm(*reinterpret_cast<const u32x4*>(X + (size_t)r * ldx + k0 + 8 * kc));
+    *reinterpret_cast<u32x4*>(xs + r * LDXS + 8 * kc) = v;
+  }
+  __syncthreads();
+
+  f32x4 acc[W4_CT][RT];
+#pragma unroll
+  for (int ct = 0; ct < W4_CT; ++ct)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[ct][rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    bf16x8 bq[W4_CT][4];
+#pragma unroll
+    for (int ct = 0; ct < W4_CT; ++ct)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bq[ct][j] = i4_bf16(cq[kb][ct][j]);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      bf16x8 xa[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        xa[j] = *reinterpret_cast<const bf16x8*>(xs + (16 * rt + li) * LDXS + 128 * kb + 32 * q + 8 * j);
+      f32x4 ax = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[0], ones, zero, 0, 0, 0);
+#pragma unroll
+      for (int j = 1; j < 4; ++j) ax = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[j], ones, ax, 0, 0, 0);
+#pragma unroll
+      for (int ct = 0; ct < W4_CT; ++ct) {
+        f32x4 g = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[0], bq[ct][0], zero, 0, 0, 0);
+#pragma unroll
+        for (int j = 1; j < 4; ++j) g = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[j], bq[ct][j], g, 0, 0, 0);
+        const float s = s2[kb][ct].x, cc = s2[kb][ct].y;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[ct][rt][i] = fmaf(s, g[i], fmaf(cc, ax[i], acc[ct][rt][i]));
+      }
+    }
+  }
+
+  // 3) lane holds y[m = 16·rt + 4q + i][n = its load column]
+#pragma unroll
+  for (int ct = 0; ct < W4_CT; ++ct) {
+    const int n = cs * W4_COLS + 32 * w + 16 * ct + li;
+    if (n >= N) continue;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = 16 * rt + 4 * q + i;
+        if (m >= M) continue;
+        if (KS == 1) {
+          float v = acc[ct][rt][i];
+          if (residual) v += (float)residual[(size_t)m * N + n];
+          out[(size_t)m * N + n] = (bf16)v;
+        } else {
+          part[((size_t)ks * M + m) * N + n] = acc[ct][rt][i];
+        }
+      }
+  }
+}
+
+// out[m, n] = Σ_s part[s, m, n] (+ residual) → bf16; 4 outputs per thread
+__global__ __launch_bounds__(256) void w4mm_reduce_k(const float* __restrict__ part, const bf16* __restrict__ res,
+                                                     bf16* __restrict__ out, int S, size_t MN) {
+  const size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= MN) return;
+  f32x4 v = *reinterpret_cast<const f32x4*>(part + i);
+  for (int s = 1; s < S; ++s) v += *reinterpret_cast<const f32x4*>(part + (size_t)s * MN + i);
+  if (res) {
+    const bf16x4 r = *reinterpret_cast<const bf16x4*>(res + i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] += (float)r[j];
+  }
+  bf16x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
+  *reinterpret_cast<bf16x4*>(out + i) = o;
+}
+
+}  // namespace
+
+bool w4mm_supported(int M, int N, int K, int gs) {
+  return M >= 1 && M <= 64 && N % W4_COLS == 0 && K % 128 == 0 && gs % 128 == 0 && K % gs == 0;
+}
+
+// 128-deep blocks per workgroup (measured per shape at M = 1..64, profiles/r4/w4a16_w4mm.txt): 4, or 8 for
+// M <= 16 when that still leaves >= 192 workgroups (fewer, longer weight streams win there; at M > 16
+// the 8-block slice holds too many codes + accumulators); 2 / 1 when K allows nothing larger
+int w4mm_nkb(int M, int N, int K) {
+  const int ncs = N / W4_COLS, kb = K / 128;
+  if (M <= 16 && kb % 8 == 0 && ncs * (kb / 8) >= 192) return 8;
+  for (int nkb = 4; nkb >= 2; nkb /= 2)
+    if (kb % nkb == 0) return nkb;
+  return 1;
+}
+
+void launch_w4mm(const void* X, int ldx, const uint8_t* codes, const float* sc2, int gs, const void* res, void* out,
+                 float* part, int M, int N, int K, int nkb, hipStream_t st) {
+  const int ncs = N / W4_COLS, KS = K / (128 * nkb);
+  const int RT = M <= 16 ? 1 : M <= 32 ? 2 : 4;
+  const size_t lds = (size_t)RT * 16 * (128 * nkb + 8) * 2;
+#define L(RT_, NKB_)                                                                                            \
+  w4mm_k<RT_, NKB_><<<ncs * KS, 256, lds, st>>>((const bf16*)X, ldx, codes, (const float2*)sc2, gs,             \
+                                                (const bf16*)res, (bf16*)out, part, M, N, K, ncs)
+#define LN(RT_)                                                                                                 \
+  do {                                                                                                          \
+    if (nkb == 8) L(RT_, 8); else if (nkb == 4) L(RT_, 4); else if (nkb == 2) L(RT_, 2); else L(RT_, 1);       \
+  } while (0)
+  if (RT == 1) LN(1); else if (RT == 2) LN(2); else LN(4);
+#undef LN
+#undef L
+  if (KS > 1) {
+    const size_t MN = (size_t)M * N;
+    w4mm_reduce_k<<<(MN / 4 + 255) / 256, 256, 0, st>>>(part, (const bf16*)res, (bf16*)out, KS, MN);
+  }
+  LIPA_CHECK_LAUNCH();
+}

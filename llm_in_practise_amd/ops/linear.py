@@ -37,8 +37,6 @@ from ..quant.nf4 import NF4Weight, dequantize_nf4
 from ._native import native, use_native
 
 EXT_ALIGN = 32   # the kernels consume the LoRA K-slice in MFMA K-steps of 32
-# LIPA_DENSE_GEMM=native: frozen bf16 bases through gemm_bf16w / gemm_bf16_t instead of hipBLASLt
-_NATIVE_DENSE = os.environ.get("LIPA_DENSE_GEMM", "") == "native"
 # LoRA B term as an in-place column-block update after the base GEMM (LIPA_LORA_APPLY=0: K-slice form)
 _APPLY = os.environ.get("LIPA_LORA_APPLY", "1") != "0"
 # training-sized bf16 base GEMMs through direct hipBLASLt calls (csrc/kernels/blaslt.hip): the
@@ -190,33 +188,24 @@ def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
     M, K = x.shape
     N = base.shape[0]
     if (M <= 16 and N <= 8192 and K <= 8192 and N % 16 == 0 and K % 64 == 0 and x.stride(0) % 8 == 0
-            and x.stride(1) == 1 and base.is_contiguous() and not _NATIVE_DENSE):
+            and x.stride(1) == 1 and base.is_contiguous()):
         # decode-sized q|k|v / o projections: the split-K weight-streaming MFMA kernel
         # (csrc/kernels/skinny.hip) beats hipBLASLt's latency-bound 23 µs by 25-45 % and fuses
         # the residual; the wide gate|up / long-K down stay on hipBLASLt (≥ 5 TB/s there)
         y = native().gemm_skinny(x, base, residual)
         return y if ext_a is None else y.addmm_(ext_a, ext_b.t())
-    if _g4w_ok(x, base, False) and not _NATIVE_DENSE:
+    if _g4w_ok(x, base, False):
         y = native().gemm4w(x, base, None if residual is None else residual.contiguous(), 0, False)
         return y if ext_a is None else y.addmm_(ext_a, ext_b.t())
-    if _LT and M >= _LT_MIN_M and x.is_cuda and x.dtype == torch.bfloat16 and x.stride(1) == 1 \
-            and not _NATIVE_DENSE:
+    if _LT and M >= _LT_MIN_M and x.is_cuda and x.dtype == torch.bfloat16 and x.stride(1) == 1:
         y = native().lt_linear(x, base.contiguous(), None if residual is None else residual.contiguous(), True)
         return y if ext_a is None else y.addmm_(ext_a, ext_b.t())
-    if not _NATIVE_DENSE:
-        # a bf16 base is a plain library GEMM: hipBLASLt's tuned kernels run it at 1.1-1.5
-        # PFLOP/s at the Qwen3 shapes (profiles/gemm_nf4_v1_v2_hipblaslt_ab.txt) and its split-K
-        # skinny kernels stream decode weights at 2.6-6 TB/s (profiles/decode_skinny_gemm.txt),
-        # ahead of the register-fed gemm_bf16w kernel; residual = addmm's beta term, the LoRA
-        # K-slice one rank-Σr update
-        y = torch.addmm(residual, x, base.t()) if residual is not None else x @ base.t()
-        if ext_a is not None:
-            y.addmm_(ext_a, ext_b.t())
-        return y
-    return native().gemm_bf16(x, base, ext_a, ext_b, residual)
-
-
-_SPLIT_ENV = int(os.environ.get("LIPA_DX_SPLIT", "0"))   # 0: auto; 1, 2, 4, 8: forced
+    # everything else is a plain library GEMM (hipBLASLt via torch): residual = addmm's beta term, the
+    # LoRA K-slice one rank-Σr update
+    y = torch.addmm(residual, x, base.t()) if residual is not None else x @ base.t()
+    if ext_a is not None:
+        y.addmm_(ext_a, ext_b.t())
+    return y
 
 
 def _dx_split(dy: torch.Tensor, w: torch.Tensor) -> int:
@@ -230,8 +219,6 @@ def _dx_split(dy: torch.Tensor, w: torch.Tensor) -> int:
     s = 2
     while tiles * s < 256 and s < 8:
         s *= 2
-    if _SPLIT_ENV in (1, 2, 4, 8):
-        s = _SPLIT_ENV
     return s if N % s == 0 else 1
 
 
@@ -261,17 +248,15 @@ def _base_gemm_t(dy, base, ext_a=None, ext_b=None, c=None):
             return dx if ext_a is None else dx.addmm_(ext_a, ext_b.t())
         base = _nf4_dequant_bf16(base) if (base.kernel_ok() and dy.is_cuda) else dequantize_nf4(base, dy.dtype)
     if c is not None:
-        if _g4w_ok(dy, base, True) and not _NATIVE_DENSE:
+        if _g4w_ok(dy, base, True):
             dx = native().gemm4w(dy, base, c, 0, True)
-        elif _LT and dy.shape[0] >= _LT_MIN_M and dy.is_cuda and _dx_split(dy, base) == 1 and not _NATIVE_DENSE:
+        elif _LT and dy.shape[0] >= _LT_MIN_M and dy.is_cuda and _dx_split(dy, base) == 1:
             dx = native().lt_dx(dy.contiguous(), base.contiguous(), 1, True, c)
         else:
             dx = _dense_dx(dy, base) + c
         return dx if ext_a is None else dx.addmm_(ext_a, ext_b.t())
-    if not _NATIVE_DENSE:
-        dx = _dense_dx(dy, base)
-        return dx if ext_a is None else dx.addmm_(ext_a, ext_b.t())
-    return native().gemm_bf16_t(dy, base, ext_a, ext_b)
+    dx = _dense_dx(dy, base)
+    return dx if ext_a is None else dx.addmm_(ext_a, ext_b.t())
 
 
 _KEY = [0x5DEECE66D << 20]
@@ -408,6 +393,22 @@ def _zero_buffer(tag: str, rows: int, cols: int, like: torch.Tensor) -> torch.Te
     return t
 
 
+_LORA_EPI = os.environ.get("LIPA_LORA_EPI", "1") != "0"
+
+
+def _lora_epi_ok(x, base, wdq, weight, branches) -> bool:
+    """The branches fit the gemm4w LoRA epilogue: ranks multiples of 8 (≤ 128 in all), training-sized M, the
+    base GEMM itself on gemm4w (a bf16 weight / expansion, or NF4 codes)."""
+    if not (_LORA_EPI and x.shape[0] >= _LT_MIN_M and all(br.a.shape[0] % 8 == 0 for br in branches)
+            and sum(br.a.shape[0] for br in branches) <= 128):
+        return False
+    if wdq is not None:
+        return _g4w_ok(x, wdq, False)
+    if isinstance(base, NF4Weight):
+        return _w4_ok(x, base, False)
+    return weight is not None and not weight.requires_grad and _g4w_ok(x, weight, False)
+
+
 def _pair_ok(x, branches) -> bool:
     """Two rank-<=8 adapters on one fused projection (q_proj + v_proj): the two-branch kernels."""
     return (len(branches) == 2 and x.is_cuda and all(br.a.shape[0] <= 8 for br in branches)
@@ -478,6 +479,19 @@ class _FusedLinearFn(torch.autograd.Function):
         # column blocks of its output (no K-slice buffers, no per-call B copies, no rank-Σr addmm over
         # all N columns)
         apply = fast and x.is_cuda and len(branches) <= 4 and _APPLY
+        wdq = None
+        if not dense and x.shape[0] > 8 and base.kernel_ok() and x.is_cuda and not _nf4_w4(ctx.needs_input_grad[0]):
+            wdq = _nf4_expand(base)     # the expand form: this copy also serves the dX GEMM
+        # the adapters' B term as extra MFMA K-steps of the base GEMM (gemm4w LoRA epilogue): xa in bf16
+        # slots of a 32·k-wide buffer, no lora_apply pass over y
+        epi = apply and _lora_epi_ok(x, base, wdq, weight, branches)
+        xa32 = None
+        if epi:
+            kofs, k = [], 0
+            for br in branches:
+                kofs.append(k)
+                k += br.a.shape[0]
+            xa32 = _zero_buffer(f"lora_xa32_{(k + 31) // 32}", x.shape[0], (k + 31) // 32 * 32, x)
         if apply:
             pair = _pair_ok(x, branches)
             if pair:
@@ -487,16 +501,18 @@ class _FusedLinearFn(torch.autograd.Function):
                 # training with dropout on both: keep the masks' bits (2 bits / element of x) for lora_acc2
                 masks = (torch.empty(2, x.shape[0], x.shape[1] // 8, dtype=torch.uint8, device=x.device)
                          if need_xa and all(k is not None for k in keys) and _KEEP_BITS else None)
-                xa2 = native().lora_proj2(x, a0, a1, None, True, ps[0], keys[0] or 0, branches[0].scaling,
-                                          ps[1], keys[1] or 0, branches[1].scaling, masks)
+                xa2 = native().lora_proj2(x, a0, a1, None if xa32 is None else xa32[:, :a0.shape[0] + a1.shape[0]], True,
+                                          ps[0], keys[0] or 0, branches[0].scaling, ps[1], keys[1] or 0,
+                                          branches[1].scaling, masks)
                 ctx.masks = masks
                 r0 = a0.shape[0]
                 xa_list = [xa2[:, :r0], xa2[:, r0:]]
             else:
-                for br, a in zip(branches, ab[0::2]):
+                for bi, (br, a) in enumerate(zip(branches, ab[0::2])):
                     p = br.dropout if training else 0.0
                     key = next_dropout_key() if p > 0 else None
-                    xa_list.append(native().lora_proj(x, 0, x.shape[1], bf16_view(a, x.dtype), None, True, p,
+                    ob = None if xa32 is None else xa32[:, kofs[bi]:kofs[bi] + a.shape[0]]
+                    xa_list.append(native().lora_proj(x, 0, x.shape[1], bf16_view(a, x.dtype), ob, True, p,
                                                       key or 0, br.scaling))
                     keys.append(key)
         elif branches:
@@ -544,12 +560,25 @@ class _FusedLinearFn(torch.autograd.Function):
                 r0 += r
             if not fast:
                 ext_a = _pad_cols(torch.cat(cols, 1))
-        wdq = None
-        if not dense and x.shape[0] > 8 and base.kernel_ok() and x.is_cuda and not _nf4_w4(ctx.needs_input_grad[0]):
-            wdq = _nf4_expand(base)     # the expand form: this copy also serves the dX GEMM
-        y = _base_gemm(x, wdq if wdq is not None else (base if not dense else weight), ext_a, ext_b, residual)
         ctx.bts = None
-        if apply:
+        if epi:
+            bs = [bf16_view(b, x.dtype) for b in ab[1::2]]
+            bts = [torch.empty(b.shape[1], b.shape[0], dtype=x.dtype, device=x.device) for b in bs] if need_xa else []
+            w_op = wdq if wdq is not None else (weight if dense else None)
+            res = None if residual is None else residual.contiguous()
+            if w_op is not None:
+                y = native().gemm4w_lora(x, w_op, None, 0, res, xa32, bs, [br.c0 for br in branches], kofs,
+                                         bts or [None] * len(bs))
+            else:
+                codes, sc = base.g4w_pack()
+                y = native().gemm4w_lora(x, codes, sc, base.shape[0], res, xa32, bs, [br.c0 for br in branches], kofs,
+                                         bts or [None] * len(bs))
+            ctx.bts = bts or None
+            if not need_xa:
+                xa_list = [None] * len(xa_list)
+        else:
+            y = _base_gemm(x, wdq if wdq is not None else (base if not dense else weight), ext_a, ext_b, residual)
+        if apply and not epi:
             bs = [bf16_view(b, x.dtype) for b in ab[1::2]]
             # training: the same pass writes Bᵀ [r, n] for the backward's dy·B projection (no transpose kernel)
             bts = [torch.empty(b.shape[1], b.shape[0], dtype=x.dtype, device=x.device) for b in bs] if need_xa else []
@@ -659,15 +688,24 @@ class _FusedLinearFn(torch.autograd.Function):
             pair_ok = (ctx.pair and all(k is not None for k in ctx.keys) and not deterministic()
                        and ctx.needs_input_grad[5] and ctx.needs_input_grad[7])
             if (pair_ok and _DX_C and ctx.masks is not None and not fold and dy.shape[0] >= _LT_MIN_M
-                    and not _NATIVE_DENSE):
+                   ):
                 # the LoRA input-gradient term written once (lora_dx2, from the stored keep bits) and
                 # added by the dX GEMM as its C matrix; dA from x in a separate launch — no
                 # read-modify-write pass over dx (lora_acc2)
                 a0, a1 = bf16_view(ab[0], dy.dtype), bf16_view(ab[2], dy.dtype)
                 p0, p1 = branches[0].dropout, branches[1].dropout
-                c = native().lora_dx2(g_list[0], g_list[1], a0, a1, ctx.masks, p0, p1)
-                dx = _base_gemm_t(dy, wb, None, None, c)
-                del c
+                fused_ok = (_LORA_EPI and wb.shape[1] % 128 == 0 and all(g.shape[1] % 8 == 0 and g.shape[1] <= 32
+                                                                           for g in g_list))
+                if fused_ok and isinstance(wb, torch.Tensor) and _g4w_ok(dy, wb, True):
+                    # the masked LoRA input gradient inside the dX GEMM's epilogue (no lora_dx2 matrix)
+                    dx = native().gemm4w_loradx(dy, wb, None, 0, g_list, [a0, a1], ctx.masks, [p0, p1])
+                elif fused_ok and isinstance(wb, NF4Weight) and _w4_ok(dy, wb, True):
+                    codes, sc = wb.g4w_pack()
+                    dx = native().gemm4w_loradx(dy, codes, sc, wb.shape[1], g_list, [a0, a1], ctx.masks, [p0, p1])
+                else:
+                    c = native().lora_dx2(g_list[0], g_list[1], a0, a1, ctx.masks, p0, p1)
+                    dx = _base_gemm_t(dy, wb, None, None, c)
+                    del c
                 (o0, ret0), (o1, ret1) = dest(0), dest(2)
                 native().lora_dA_pair(g_list[0], g_list[1], x, o0, o1, ctx.masks, p0, p1)
                 ctx.masks = None

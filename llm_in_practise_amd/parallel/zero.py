@@ -177,7 +177,6 @@ class _QuantFlat:
         for q in self.owners:
             q.__dict__.pop("_g4w", None)
             q.__dict__.pop("_gemv_sc", None)
-            q.packed = None
 
 
 class _Unit:

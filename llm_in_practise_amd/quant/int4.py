@@ -5,10 +5,10 @@ Storage (one canonical layout for every producer — RTN, GPTQ, AWQ — and ever
 same fragment-native repacker feeds the MFMA kernel), unsigned q ∈ [0, 15]; ``scales`` fp32
 [N, K/g]; ``zeros`` uint8 [N, K/g] (8 for symmetric).  Dequant: ``w = (q − z)·s``.
 
-Kernels (``csrc/kernels/gemm2.hip`` MODE 2, ``gemv.hip``): the weight is ``q·s + b`` with
-``b = −z·s`` precomputed per (group, column), i.e. one FMA per weight after the 16-entry table
-lookup — the same cost as NF4.  Prefill / batched GEMMs use the MFMA kernel, decode (M ≤ 8)
-the weight-streaming GEMV.
+Kernels (dispatch in :func:`int4_linear`): ``gemv.hip`` (M ≤ 2, weight-streaming GEMV, ``q·s + b``
+with ``b = −z·s`` per group), ``w4mm.hip`` (M ≤ 32: the MFMA sums x·(128+q) from byte-permuted
+codes, the group's scale and zero fold after it), ``gemm4w.hip`` W4 = 2 (larger M: the codes expanded
+through a per-block (q − z)·s table into the bf16 B image of the hand-written GEMM).
 
 On-disk formats (converters below; exact bit layouts documented per function — no reference
 checkpoint ships with the reference repo, so byte-level parity is *unpinned* and covered by
@@ -37,7 +37,6 @@ class Int4Weight:
     shape: tuple
     group_size: int = 128
     sym: bool = False
-    packed: tuple | None = None  # (codes_f, scale_t, bias_t) kernel cache
     _gemv: tuple | None = None
 
     @property
@@ -59,8 +58,11 @@ class Int4Weight:
         return w.view(n, k).to(dtype)
 
     def to(self, device):
-        return dataclasses.replace(self, codes=self.codes.to(device), scales=self.scales.to(device),
-                                   zeros=self.zeros.to(device), packed=None, _gemv=None)
+        out = dataclasses.replace(self, codes=self.codes.to(device), scales=self.scales.to(device),
+                                  zeros=self.zeros.to(device), _gemv=None)
+        out.__dict__.pop("_g4w", None)
+        out.__dict__.pop("_w4mm", None)
+        return out
 
     def bias_table(self) -> torch.Tensor:
         return -(self.zeros.float() * self.scales.float())
@@ -69,22 +71,35 @@ class Int4Weight:
         n, k = self.shape
         return n % 32 == 0 and k % 64 == 0 and self.group_size % 64 == 0
 
-    def kernel_pack(self):
-        """(codes_f, scale_t, bias_t) for ``gemm_int4``: fragment-native codes (the NF4 forward
-        packing) and fp32 [K/64, N] tables with each group's value repeated per 64-deep K-step."""
-        if self.packed is None:
+    def g4w_pack(self) -> tuple:
+        """(codes, scale_t, zero_t) — the affine-int4 B operand of the hand-written gemm4w GEMM (the NF4
+        dequant-GEMM's kernel with a (q − z)·s table): the codes re-tiled like NF4 (same nibble
+        convention) and fp32 [K/64, N] scale / zero tables, each group's value repeated per 64-block."""
+        c = self.__dict__.get("_g4w")
+        if c is None:
             from ..ops._native import native
             n, k = self.shape
-            cf, _ = native().nf4_pack(self.codes.contiguous(), n, k)
             rep = self.group_size // 64
+            codes = native().g4w_pack(self.codes.contiguous(), n, k)
             st = self.scales.float().repeat_interleave(rep, dim=1).t().contiguous()
-            bt = self.bias_table().repeat_interleave(rep, dim=1).t().contiguous()
-            self.packed = (cf, st, bt)
-        return self.packed
+            zt = self.zeros.float().repeat_interleave(rep, dim=1).t().contiguous()
+            c = (codes, st, zt)
+            self.__dict__["_g4w"] = c
+        return c
 
-    def skinny_ok(self) -> bool:
+    def g4w_ok(self) -> bool:
         n, k = self.shape
-        return n % 16 == 0 and k % 256 == 0 and self.group_size % 128 == 0
+        return n % 64 == 0 and k % 64 == 0 and self.group_size % 64 == 0
+
+    def w4mm_table(self) -> torch.Tensor:
+        """fp32 [N, K/g, 2] = (scale, bias − 128·scale) for the w4mm kernel (csrc/kernels/w4mm.hip: the
+        MFMA sums x·(128+q), the group folds as s·G + (b − 128·s)·Σx); cached."""
+        t = self.__dict__.get("_w4mm")
+        if t is None:
+            s = self.scales.float()
+            t = torch.stack([s, self.bias_table() - 128.0 * s], -1).contiguous()
+            self.__dict__["_w4mm"] = t
+        return t
 
     def gemv_tables(self):
         if self._gemv is None:
@@ -216,31 +231,31 @@ def from_awq(d: dict, group_size: int) -> Int4Weight:
 
 
 # ============================================================================ module + op
-import os as _os
+# W4A16 kernel per row count (measured on the Qwen3-8B projection shapes, profiles/r4/w4a16_w4mm.txt):
+#   M <= 2    gemv_w4 (csrc/kernels/gemv.hip): weight-streaming GEMV, no matrix-core padding;
+#   3 .. 32   w4mm (csrc/kernels/w4mm.hip): byte-permute dequant, MFMA, per-group scale folded after it;
+#   > 32      gemm4w with the affine table expanded in-kernel (csrc/kernels/gemm4w.hip, W4 = 2);
+# anything the kernels do not take: one bf16 dequantisation + torch matmul.
+_W4MM_MAX = 32
 
-# decode-batch W4A16 kernel for 3..64 rows (profiles/w4a16_decode_gemm.txt); M <= 2 stays on the
-# GEMV, larger M on the MFMA tile kernel
-_W4_SKINNY_MAX = min(64, int(_os.environ.get("LIPA_W4_SKINNY_MAX", "64")))
 
 def int4_linear(x: torch.Tensor, w: Int4Weight, bias: torch.Tensor | None = None,
                 residual: torch.Tensor | None = None) -> torch.Tensor:
     from ..ops._native import native, use_native
     shape = x.shape
     x2 = x.reshape(-1, shape[-1])
-    n = w.shape[0]
+    n, k = w.shape
     r2 = residual.reshape(-1, n).contiguous() if residual is not None else None
     M = x2.shape[0]
-    if use_native(x2) and x2.dtype == torch.bfloat16 and 3 <= M <= _W4_SKINNY_MAX and w.skinny_ok():
-        s, b = w.gemv_tables()       # decode batches: split-K weight streaming, dequant in registers
-        y = native().gemm_w4_skinny(x2.contiguous(), w.codes, s, b, n, w.group_size, r2)
-    elif use_native(x2) and x2.dtype == torch.bfloat16 and w.kernel_ok():
-        x2 = x2.contiguous()
-        if x2.shape[0] <= 8:
-            s, b = w.gemv_tables()
-            y = native().gemv_w4(x2, w.codes, s, b, n, w.group_size, r2)
-        else:
-            cf, st, bt = w.kernel_pack()
-            y = native().gemm_int4(x2, cf, st, bt, n, None, None, r2)
+    nat = use_native(x2) and x2.dtype == torch.bfloat16 and x2.stride(-1) == 1
+    if nat and M <= 2 and w.kernel_ok():
+        s, b = w.gemv_tables()
+        y = native().gemv_w4(x2.contiguous(), w.codes, s, b, n, w.group_size, r2)
+    elif nat and M <= _W4MM_MAX and native().w4mm_ok(M, n, k, w.group_size):
+        y = native().w4mm(x2.contiguous(), w.codes, w.w4mm_table(), n, w.group_size, r2)
+    elif nat and w.g4w_ok():
+        codes, st, zt = w.g4w_pack()
+        y = native().gemm4w(x2.contiguous(), codes, r2, 0, False, 0, 0, st, n, zt)
     else:
         y = x2 @ w.dequantize(x2.dtype).t()
         if r2 is not None:

@@ -92,9 +92,6 @@ class NF4Weight:
     shape: tuple[int, int]
     blocksize: int = 64
     dtype: torch.dtype = torch.bfloat16   # compute / dequant dtype
-    # kernel-side layouts (built lazily on the GPU): fragment-native fwd / bwd code packings
-    # and transposed fp32 absmax [K/64, N] — see csrc/kernels/gemm.hip
-    packed: tuple | None = dataclasses.field(default=None, repr=False, compare=False)
 
     @property
     def double_quant(self) -> bool:
@@ -120,20 +117,9 @@ class NF4Weight:
         return d
 
     def to(self, device) -> "NF4Weight":
-        m = {f.name: getattr(self, f.name) for f in dataclasses.fields(self) if f.name != "packed"}
+        m = {f.name: getattr(self, f.name) for f in dataclasses.fields(self)}
         m = {k: (v.to(device) if isinstance(v, torch.Tensor) else v) for k, v in m.items()}
         return NF4Weight(**m)
-
-    def kernel_pack(self) -> tuple:
-        """(codes_fwd, codes_bwd, absmax_t) for the gfx950 NF4 GEMMs (GPU only, cached)."""
-        if self.packed is None:
-            from ..ops._native import native
-            n, k = self.shape
-            cf, cb = native().nf4_pack(self.codes, n, k)
-            at = native().nf4_absmax_t(self.absmax, self.qabsmax, self.absmax2, self.offset,
-                                       dynamic_code(str(self.codes.device)) if self.qabsmax is not None else None, n, k)
-            self.packed = (cf, cb, at)
-        return self.packed
 
     def g4w_pack(self) -> tuple:
         """(codes, scales_t) — the NF4 B operand of the hand-written gemm4w GEMM (csrc/kernels/gemm4w.hip):

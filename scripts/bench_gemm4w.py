@@ -1,4 +1,4 @@
-"""A/B: one-wave-per-SIMD AGPR GEMM (gemm4w) vs hipBLASLt (torch.matmul) vs gemm8 at the Qwen3-8B
+"""A/B: one-wave-per-SIMD AGPR GEMM (gemm4w) vs hipBLASLt (torch.matmul) at the Qwen3-8B
 QLoRA step shapes.  Interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24),
 uniform [-1, 1) operands; numerics vs an fp32 reference."""
 import os
@@ -45,7 +45,6 @@ def main():
         res = {}
         for rnd in range(3):
             res.setdefault("hipblaslt", []).append(timeit(lambda: x @ w.t()))
-            res.setdefault("gemm8", []).append(timeit(lambda: ext.gemm8(x, w, None, None, None, 0)))
             for sp in splits:
                 res.setdefault(f"gemm4w_s{sp}", []).append(timeit(lambda: ext.gemm4w(x, w, None, sp)))
         for k, v in res.items():

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Decode-shaped (small-M) GEMM micro-benchmark at the Qwen3-8B projection shapes:
-our bf16 weight GEMM, the NF4 GEMV / GEMM, vs hipBLASLt (torch.matmul).  Reports µs and
+the split-K bf16 skinny GEMM and the NF4 GEMV vs hipBLASLt (torch.matmul).  Reports µs and
 effective weight-stream bandwidth (GB/s) — at M <= 64 these GEMMs are HBM-bound.
 
     python scripts/bench_skinny.py --m 1 8 16 32 64
@@ -46,14 +46,11 @@ def main():
         for M in a.m:
             x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
             r = {"shape": name, "M": M, "N": N, "K": K}
-            fns = {"ours_bf16": lambda: C.gemm_bf16(x, w, None, None, None),
-                   "hipblaslt_bf16": lambda: x @ w.t()}
+            fns = {"hipblaslt_bf16": lambda: x @ w.t()}
             if hasattr(C, "gemm_skinny"):
                 fns["skinny_bf16"] = lambda: C.gemm_skinny(x, w, None)
             if q is not None:
-                cf, _, at = q.kernel_pack()
                 sc = q.gemv_scales()
-                fns["nf4_gemm"] = lambda: C.gemm_nf4(x, cf, at, N, None, None, None)
                 if M <= 8:
                     fns["nf4_gemv"] = lambda: C.gemv_w4(x, q.codes, sc, None, N, 64, None)
             for k, fn in fns.items():

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""W4A16 decode-batch GEMM microbenchmark (Qwen3-8B projection shapes): bf16 hipBLASLt vs the
-int4 kernels — gemv_w4 (M <= 8), gemm_int4 (MFMA tile kernel), gemm_w4_skinny (split-K weight
-streaming).  Prints one JSON line per (shape, M)."""
+"""W4A16 decode-batch GEMM microbenchmark (Qwen3-8B projection shapes): bf16 (hipBLASLt, gemm4w) vs the
+int4 kernels — gemv_w4 (M <= 8), w4mm (M <= 64, byte-permute dequant + MFMA, per-K-slice-count columns),
+gemm4w W4=2 (affine table expanded in-kernel).  Prints one JSON line per (shape, M)."""
 import json
 import os
 import sys
@@ -39,21 +39,28 @@ def main():
         wb = w.to(torch.bfloat16)
         q = quantize_rtn(w, 128)
         sc, bi = q.gemv_tables()
-        cf, st, bt = q.kernel_pack()
+        sc2 = q.w4mm_table()
+        gc, gst, gzt = q.g4w_pack()
         ref_w = q.dequantize()
         for M in Ms:
             x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
             ref = x.float() @ ref_w.t()
             row = {"shape": name, "M": M, "N": N, "K": K}
             row["bf16_us"] = round(timeit(lambda: x @ wb.t()), 2)
+            if M >= 16:
+                row["bf16_g4w_us"] = round(timeit(lambda: nat.gemm4w(x, wb, None, 0, False)), 2)
+            if nat.w4mm_ok(M, N, K, 128):
+                row["w4mm_us"] = round(timeit(lambda: nat.w4mm(x, q.codes, sc2, N, 128, None, 0)), 2)
+                y = nat.w4mm(x, q.codes, sc2, N, 128, None, 0)
+                row["w4mm_relerr"] = float(((y.float() - ref).norm() / ref.norm()).item())
+                row["w4mm_GBs"] = round(N * K / 2 / (row["w4mm_us"] * 1e-6) / 1e9, 1)
+                for nkb in (1, 2, 4, 8):
+                    if (K // 128) % nkb == 0:
+                        row[f"w4mm_nkb{nkb}_us"] = round(timeit(lambda: nat.w4mm(x, q.codes, sc2, N, 128, None, nkb)), 2)
+            if M > 8:
+                row["g4w_int4_us"] = round(timeit(lambda: nat.gemm4w(x, gc, None, 0, False, 0, 0, gst, N, gzt)), 2)
             if M <= 8:
                 row["gemv_w4_us"] = round(timeit(lambda: nat.gemv_w4(x, q.codes, sc, bi, N, 128, None)), 2)
-            row["gemm_int4_us"] = round(timeit(lambda: nat.gemm_int4(x, cf, st, bt, N, None, None, None)), 2)
-            if M <= 64:
-                row["w4_skinny_us"] = round(timeit(lambda: nat.gemm_w4_skinny(x, q.codes, sc, bi, N, 128, None)), 2)
-                y = nat.gemm_w4_skinny(x, q.codes, sc, bi, N, 128, None)
-                row["w4_skinny_relerr"] = float(((y.float() - ref).norm() / ref.norm()).item())
-                row["w4_skinny_GBs"] = round(N * K / 2 / (row["w4_skinny_us"] * 1e-6) / 1e9, 1)
             print(json.dumps(row), flush=True)
 
 

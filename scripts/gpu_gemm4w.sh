@@ -1,5 +1,5 @@
 #!/bin/bash
-# gemm4w vs hipBLASLt / gemm8 at the step shapes.  usage: scripts/gpu_gemm4w.sh <tag>
+# gemm4w vs hipBLASLt at the step shapes.  usage: scripts/gpu_gemm4w.sh <tag>
 set -u
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0 PYTHONPATH=.

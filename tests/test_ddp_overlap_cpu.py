@@ -38,7 +38,7 @@ def _worker(rank, world, port, out, ga, car=False):
     net = Net()
     opt = AdamW(net.parameters(), lr=1e-2, weight_decay=0.0)
     ddp = DistributedDataParallel(net, flat=opt.flat, bucket_mb=0.004,   # ~1k floats: several buckets
-                                  custom_allreduce="auto" if car else None)
+                                  custom_allreduce="auto-host" if car else None)
     logs = []
     for s in range(3):
         for m in range(ga):

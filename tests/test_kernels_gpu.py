@@ -292,54 +292,6 @@ def _lora_ref(x, w, ext_a=None, ext_b=None, res=None):
     return y
 
 
-@pytest.mark.parametrize("M,N,K", [(1024, 6144, 4096), (1000, 512, 1024), (64, 128, 256), (2048, 24576, 512)])
-@pytest.mark.parametrize("dq", [True, False])
-def test_gemm_nf4_fwd_bwd(native_ext, M, N, K, dq):
-    w = torch.randn(N, K, device=DEV).to(torch.bfloat16)
-    q = quantize_nf4(w, 64, double_quant=dq)
-    wd = dequantize_nf4(q, torch.float32)
-    cf, cb, at = q.kernel_pack()
-    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
-    R = 32
-    ea = (0.1 * torch.randn(M, R, device=DEV)).to(torch.bfloat16)
-    eb = (0.1 * torch.randn(N, R, device=DEV)).to(torch.bfloat16)
-    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
-    y = native_ext.gemm_nf4(x, cf, at, N, ea, eb, res)
-    assert rel_err(y, _lora_ref(x, wd, ea, eb, res)) < 1e-2
-    y0 = native_ext.gemm_nf4(x, cf, at, N, None, None, None)
-    assert rel_err(y0, _lora_ref(x, wd)) < 1e-2
-    dy = torch.randn(M, N, device=DEV).to(torch.bfloat16)
-    eb2 = (0.1 * torch.randn(K, R, device=DEV)).to(torch.bfloat16)
-    dx = native_ext.gemm_nf4_t(dy, cb, at, K, ea, eb2)
-    assert rel_err(dx, dy.float() @ wd + ea.float() @ eb2.float().t()) < 1e-2
-
-
-def test_gemm_nf4_asymmetric_layout(native_ext):
-    """A = I style check with an asymmetric weight catches a transposed epilogue."""
-    N, K = 128, 128
-    w = torch.arange(N * K, device=DEV, dtype=torch.float32).view(N, K) % 13 - 6
-    q = quantize_nf4(w.to(torch.bfloat16), 64, double_quant=False)
-    wd = dequantize_nf4(q, torch.float32)
-    cf, cb, at = q.kernel_pack()
-    x = torch.eye(K, device=DEV, dtype=torch.bfloat16)
-    y = native_ext.gemm_nf4(x, cf, at, N, None, None, None)
-    assert torch.allclose(y.float(), wd.t().to(torch.bfloat16).float(), atol=1e-2)
-    dx = native_ext.gemm_nf4_t(torch.eye(N, device=DEV, dtype=torch.bfloat16), cb, at, K, None, None)
-    assert torch.allclose(dx.float(), wd.to(torch.bfloat16).float(), atol=1e-2)
-
-
-@pytest.mark.parametrize("M,N,K", [(1024, 4096, 4096), (77, 256, 128), (77, 264, 96)])
-def test_gemm_bf16_lora(native_ext, M, N, K):
-    """gemm_bf16 = gemm8 (8-phase MFMA) where the shape allows it, library GEMM otherwise"""
-    w = (0.05 * torch.randn(N, K, device=DEV)).to(torch.bfloat16)
-    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
-    ea = torch.randn(M, 32, device=DEV).to(torch.bfloat16)
-    eb = (0.1 * torch.randn(N, 32, device=DEV)).to(torch.bfloat16)
-    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
-    y = native_ext.gemm_bf16(x, w, ea, eb, res)
-    assert rel_err(y, _lora_ref(x, w, ea, eb, res)) < 1e-2
-
-
 # ----------------------------------------------------------------------------- attention
 ATTN_CASES = [(2, 512, 32, 8, 128, True), (1, 256, 4, 4, 64, True), (2, 128, 8, 2, 128, False),
               (1, 192, 4, 2, 64, True),
@@ -631,34 +583,6 @@ def test_lora_two_branch_kernels(native_ext, M, K, p0, p1):
     assert rel_err(dxc, dyw.float() @ w.float() + c.float()) < 1e-2
 
 
-# ----------------------------------------------------------------------------- 8-phase GEMM
-@pytest.mark.parametrize("M,N,K,splits,lora,resid", [(256, 256, 64, 1, False, False), (512, 768, 512, 1, True, True),
-                                                     (300, 520, 192, 1, True, False), (2048, 1024, 1024, 4, True, True),
-                                                     (257, 264, 640, 2, False, True), (64, 4096, 4096, 0, False, False)])
-def test_gemm8_matches_fp32(native_ext, M, N, K, splits, lora, resid):
-    torch.manual_seed(0)
-    x = (torch.rand(M, K, device=DEV) * 2 - 1).to(torch.bfloat16)
-    w = (torch.rand(N, K, device=DEV) * 2 - 1).to(torch.bfloat16)
-    ea = (torch.randn(M, 32, device=DEV)).to(torch.bfloat16) if lora else None
-    eb = (0.1 * torch.randn(N, 32, device=DEV)).to(torch.bfloat16) if lora else None
-    res = torch.randn(M, N, device=DEV).to(torch.bfloat16) if resid else None
-    y = native_ext.gemm8(x, w, ea, eb, res, splits)
-    want = x.float() @ w.float().t()
-    if lora:
-        want += ea.float() @ eb.float().t()
-    if resid:
-        want += res.float()
-    assert rel_err(y, want) < 1e-2
-
-
-def test_gemm8_strided_input(native_ext):
-    """x may be a column slice of a wider activation (row stride != K)"""
-    big = torch.randn(512, 1024 + 64, device=DEV).to(torch.bfloat16)
-    x = big[:, 64:]
-    w = torch.randn(256, 1024, device=DEV).to(torch.bfloat16)
-    assert rel_err(native_ext.gemm8(x, w, None, None, None, 1), x.float() @ w.float().t()) < 1e-2
-
-
 # ----------------------------------------------------------------------------- one-wave-per-SIMD GEMM
 @pytest.mark.parametrize("M,N,K,splits,bt,resid", [(256, 256, 64, 1, False, False), (512, 768, 512, 1, False, True),
                                                    (300, 520, 192, 1, False, False), (2048, 1024, 1024, 4, False, True),
@@ -791,6 +715,130 @@ def test_gemm4w_nf4_swiglu_epilogues(native_ext, M, Fd, K):
     assert torch.equal(gu4, gu) and torch.equal(h4, h)
     dy = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     assert torch.equal(native_ext.gemm4w_dswiglu(dy, cd, gu, sd), native_ext.gemm4w_dswiglu(dy, wd, gu))
+
+
+@pytest.mark.parametrize("M,N,K,branches,w4,resid", [
+    (2048, 6144, 4096, [(0, 4096, 8), (5120, 1024, 8)], False, False),     # q | k | v, adapters on q and v
+    (1024, 6144, 4096, [(0, 4096, 8), (5120, 1024, 8)], True, False),
+    (512, 6144, 1024, [(0, 4096, 16), (4096, 1024, 16), (5120, 1024, 16)], False, False),   # q, k, v r16: 2 K-steps
+    (300, 1024, 512, [(0, 1024, 16)], False, True),                         # o_proj r16 with the residual
+    (256, 768, 256, [(64, 256, 8), (512, 128, 24)], True, True)])
+def test_gemm4w_lora_epilogue(native_ext, M, N, K, branches, w4, resid):
+    """y = x·Wᵀ (+ residual) + Σ_b xa_b·B_bᵀ over each adapter's column block, the adapter term as extra
+    MFMA K-steps of the base GEMM (bf16 or NF4 codes), and Bᵀ written for the backward, vs fp32"""
+    torch.manual_seed(7)
+    x = (torch.rand(M, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    w = (0.05 * torch.randn(N, K, device=DEV)).to(torch.bfloat16)
+    ktot = sum(r for _, _, r in branches)
+    xa = torch.zeros(M, (ktot + 31) // 32 * 32, device=DEV, dtype=torch.bfloat16)
+    bs, c0s, kofs, bts, k = [], [], [], [], 0
+    want_extra = torch.zeros(M, N, device=DEV)
+    for c0, n, r in branches:
+        xa[:, k:k + r] = (0.5 * torch.randn(M, r, device=DEV)).to(torch.bfloat16)
+        b = (0.05 * torch.randn(n, r, device=DEV)).to(torch.bfloat16)
+        bs.append(b); c0s.append(c0); kofs.append(k)
+        bts.append(torch.empty(r, n, device=DEV, dtype=torch.bfloat16))
+        want_extra[:, c0:c0 + n] += xa[:, k:k + r].float() @ b.float().t()
+        k += r
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16) if resid else None
+    if w4:
+        q = quantize_nf4(w, 64, True)
+        wd = dequantize_nf4(q, torch.bfloat16)
+        codes, sc = q.g4w_pack()
+        y = native_ext.gemm4w_lora(x, codes, sc, N, res, xa, bs, c0s, kofs, bts)
+    else:
+        wd = w
+        y = native_ext.gemm4w_lora(x, w, None, 0, res, xa, bs, c0s, kofs, bts)
+    want = x.float() @ wd.float().t() + want_extra
+    if resid:
+        want += res.float()
+    assert rel_err(y, want) < 1e-2
+    # the adapter columns: the LoRA term is really there (error vs the base-only product is large)
+    c0, n, _ = branches[0]
+    base_only = x.float() @ wd.float().t() + (res.float() if resid else 0)
+    assert rel_err(y[:, c0:c0 + n], base_only[:, c0:c0 + n]) > 10 * rel_err(y[:, c0:c0 + n], want[:, c0:c0 + n])
+    for b, bt in zip(bs, bts):
+        assert torch.equal(bt, b.t())
+
+
+@pytest.mark.parametrize("M,Nk,K,r,w4", [(2048, 4096, 6144, 8, False), (1024, 4096, 6144, 8, True),
+                                       (300, 640, 1024, 16, False), (256, 768, 512, 32, True),
+                                       (512, 1152, 256, 8, False)])
+def test_gemm4w_loradx_epilogue(native_ext, M, Nk, K, r, w4):
+    """dX = dY·W + Σ_b D_b(g_b·A_b)/(1 - p_b) with each adapter's keep bits, the LoRA term added in the
+    gemm4w dX epilogue, vs fp32 (and vs the lora_dx2 + C-matrix path)"""
+    torch.manual_seed(11)
+    dy = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (0.05 * torch.randn(K, Nk, device=DEV)).to(torch.bfloat16)      # the stored weight [N_w = K, K_w = Nk]
+    gs = [torch.randn(M, r, device=DEV) for _ in range(2)]
+    As = [(0.05 * torch.randn(r, Nk, device=DEV)).to(torch.bfloat16) for _ in range(2)]
+    masks = torch.randint(0, 256, (2, M, Nk // 8), device=DEV, dtype=torch.uint8)
+    ps = [0.1, 0.05]
+    if w4:
+        q = quantize_nf4(w, 64, True)
+        wd = dequantize_nf4(q, torch.bfloat16)
+        codes, sc = q.g4w_pack()
+        dx = native_ext.gemm4w_loradx(dy, codes, sc, Nk, gs, As, masks, ps)
+    else:
+        wd = w
+        dx = native_ext.gemm4w_loradx(dy, w, None, 0, gs, As, masks, ps)
+    bits = torch.arange(8, device=DEV, dtype=torch.uint8)
+    want = dy.float() @ wd.float()
+    for b in range(2):
+        keep = ((masks[b].unsqueeze(-1) >> bits) & 1).reshape(M, Nk).float()
+        want += keep * (gs[b].to(torch.bfloat16).float() @ As[b].float()) / (1 - ps[b])
+    assert rel_err(dx, want) < 1e-2
+    if r <= 8 and not w4:
+        c = native_ext.lora_dx2(gs[0], gs[1], As[0], As[1], masks, ps[0], ps[1])
+        ref2 = native_ext.gemm4w(dy, w, c, 0, True)
+        assert rel_err(dx, ref2) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K,g,sym,splits", [(64, 6144, 4096, 128, False, 0), (256, 4096, 4096, 128, True, 1),
+                                              (300, 1024, 512, 64, False, 2), (2048, 4096, 12288, 128, False, 0)])
+def test_gemm4w_int4_affine(native_ext, M, N, K, g, sym, splits):
+    """W4A16 (GPTQ / AWQ affine int4, w = (q − z)·s per group) through gemm4w: the codes expanded per
+    64-block in-kernel give exactly Int4Weight.dequantize's bf16 weights — bit-identical to gemm4w on the
+    expanded weight at the same tile / split — and match fp32"""
+    from llm_in_practise_amd.quant.int4 import quantize_rtn
+    torch.manual_seed(3)
+    w = (0.05 * torch.randn(N, K, device=DEV)).to(torch.bfloat16)
+    q = quantize_rtn(w, g, sym)
+    wd = q.dequantize(torch.bfloat16)
+    codes, st, zt = q.g4w_pack()
+    x = (torch.rand(M, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    for bn, bm in ((128, 256), (256, 128), (0, 0)):
+        y4 = native_ext.gemm4w(x, codes, None, splits, False, bn, bm, st, N, zt)
+        if splits > 0 and bn:
+            assert torch.equal(y4, native_ext.gemm4w(x, wd, None, splits, False, bn, bm))
+        assert rel_err(y4, x.float() @ wd.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("N,K,g,sym", [(256, 256, 128, False), (384, 1024, 128, True), (1024, 4096, 256, False),
+                                       (4096, 12288, 128, False)])
+@pytest.mark.parametrize("M", [1, 2, 5, 16, 17, 40, 64])
+def test_w4mm_matches_fp32(native_ext, M, N, K, g, sym):
+    """w4mm (decode / short-prefill W4A16 MFMA GEMM: codes → bf16(128+q) by byte permutes, per-group
+    scale / zero folded after the MFMA) against fp32 x·deq(W)ᵀ, every K-slice count, with and without
+    the residual."""
+    from llm_in_practise_amd.quant.int4 import quantize_rtn
+    torch.manual_seed(5)
+    w = 0.05 * torch.randn(N, K, device=DEV)
+    q = quantize_rtn(w, g, sym)
+    wd = q.dequantize(torch.float32)
+    x = (torch.rand(M, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    sc2 = q.w4mm_table()
+    want = x.float() @ wd.t()
+    assert native_ext.w4mm_ok(M, N, K, g)
+    for nkb in (0, 1, 2, 8):
+        if (K // 128) % nkb if nkb else False:
+            continue
+        y = native_ext.w4mm(x, q.codes, sc2, N, g, None, nkb)
+        assert rel_err(y, want) < 1e-2, nkb
+        yr = native_ext.w4mm(x, q.codes, sc2, N, g, res, nkb)
+        assert rel_err(yr, want + res.float()) < 1e-2, nkb
+    assert not native_ext.w4mm_ok(65, N, K, g) and not native_ext.w4mm_ok(M, N + 64, K, g)
 
 
 def test_lora_apply_column_blocks(native_ext):

@@ -1,4 +1,4 @@
-"""W4A16 int4 MFMA GEMM, 4-bit decode GEMV (NF4 + int4), GPTQ/AWQ on the GPU."""
+"""W4A16 int4 GEMMs (w4mm, gemm4w W4=2), 4-bit decode GEMV (NF4 + int4), GPTQ/AWQ on the GPU."""
 import pytest
 import torch
 
@@ -11,19 +11,6 @@ DEV = "cuda"
 
 def rel(a, b):
     return ((a.float() - b.float()).norm() / b.float().norm().clamp(min=1e-6)).item()
-
-
-@pytest.mark.parametrize("M,N,K", [(1000, 512, 1024), (2048, 4096, 4096), (64, 128, 256)])
-@pytest.mark.parametrize("sym", [False, True])
-def test_gemm_int4(native_ext, M, N, K, sym):
-    torch.manual_seed(0)
-    w = quantize_rtn(torch.randn(N, K, device=DEV), 128, sym)
-    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
-    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
-    cf, st, bt = w.kernel_pack()
-    y = native_ext.gemm_int4(x, cf, st, bt, N, None, None, res)
-    ref = x.float() @ w.dequantize().t() + res.float()
-    assert rel(y, ref) < 1e-2
 
 
 @pytest.mark.parametrize("M", [1, 3, 8])
@@ -41,26 +28,17 @@ def test_gemv_nf4_and_int4(native_ext, M, N, K):
     assert rel(y4, x.float() @ w4.dequantize().t() + res.float()) < 1e-2
 
 
-@pytest.mark.parametrize("M", [1, 2, 8, 17, 32, 40, 64])
-@pytest.mark.parametrize("N,K,gs", [(4096, 4096, 128), (6144, 4096, 128), (4096, 12288, 128), (48, 512, 256)])
-def test_gemm_w4_skinny(native_ext, M, N, K, gs):
-    """Decode-batch W4A16 (skinny.hip): split-K weight streaming, in-register dequant, vs fp32."""
-    torch.manual_seed(2)
-    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
-    w4 = quantize_rtn(torch.randn(N, K, device=DEV), gs, False)
-    s, b = w4.gemv_tables()
-    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
-    y = native_ext.gemm_w4_skinny(x, w4.codes, s, b, N, gs, res)
-    assert rel(y, x.float() @ w4.dequantize().t() + res.float()) < 1e-2
-    y0 = native_ext.gemm_w4_skinny(x, w4.codes, s, b, N, gs, None)
-    assert rel(y0, x.float() @ w4.dequantize().t()) < 1e-2
-
-
-def test_int4_linear_dispatch(native_ext):
-    w = quantize_rtn(torch.randn(256, 512, device=DEV), 128)
-    for M in (1, 8, 64, 300):
-        x = torch.randn(M, 512, device=DEV).to(torch.bfloat16)
-        assert rel(int4_linear(x, w), x.float() @ w.dequantize().t()) < 1e-2
+@pytest.mark.parametrize("N,K,gs,sym", [(256, 512, 128, False), (384, 1024, 128, True), (96, 256, 64, False)])
+def test_int4_linear_dispatch(native_ext, N, K, gs, sym):
+    """Every row count through int4_linear's kernel choice — gemv_w4 (M <= 2), w4mm (3..32), gemm4w W4=2
+    (larger), the dequant fallback for shapes no kernel takes (N = 96) — against fp32, with residual."""
+    torch.manual_seed(4)
+    w = quantize_rtn(torch.randn(N, K, device=DEV), gs, sym)
+    for M in (1, 2, 3, 8, 32, 33, 64, 300):
+        x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+        res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+        assert rel(int4_linear(x, w), x.float() @ w.dequantize().t()) < 1e-2, M
+        assert rel(int4_linear(x, w, residual=res), x.float() @ w.dequantize().t() + res.float()) < 1e-2, M
 
 
 def test_awq_gptq_on_gpu_and_quantized_generation(native_ext):
