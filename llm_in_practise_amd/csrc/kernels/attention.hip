@@ -127,7 +127,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const bf16* __restrict__ Q,
                                                   bf16* __restrict__ O, float* __restrict__ lse, int Sq, int Skv,
                                                   int kv_rows, int hq, int hkv, int causal, float scale_log2,
                                                   DropParams dp) {
-  constexpr int LDR = D + 8;        // padded LDS row (elements)
+  // padded LDS row (elements): a 288-B row stride (D = 128; D + 16 for every D) makes both fragment reads
+  // bank-conflict free — ds_read_b128 of rows 16t + li at column 32s + 8g, and ds_read_b64_tr_b16 of rows
+  // 4g + li/4 (+16) at column 16dt + 4(li%4) (the D + 8 stride was 2-way on both: 41 % of the LDS cycles
+  // of the backward were conflict cycles, profiles/r4/pmc_step_kernels.txt)
+  constexpr int LDR = D + 16;
   constexpr int CH = D / 8;         // 16-B chunks per row
   constexpr int TILE = 64 * LDR;    // elements per K or V tile
   constexpr int NS = D / 32;        // k-steps over head dim
@@ -336,7 +340,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(const bf16* __restrict__
                                                      int ldq, int ldk, int ldv, bf16* __restrict__ dQ, int S, int hq,
                                                      int hkv, int causal, float scale, float scale_log2,
                                                      DropParams drp) {
-  constexpr int LDR = D + 8, CH = D / 8, TILE = 64 * LDR, NS = D / 32, ND = D / 16;
+  constexpr int LDR = D + 16, CH = D / 8, TILE = 64 * LDR, NS = D / 32, ND = D / 16;   // D + 16: conflict-free (see attn_fwd_k)
   constexpr int LOADS = 64 * CH / 256;
   __shared__ __attribute__((aligned(16))) bf16 smem[4 * TILE];  // K0 V0 K1 V1
 
@@ -488,7 +492,7 @@ __global__ __launch_bounds__(256 * HALVES) void attn_bwd_dkv_k(const bf16* __res
                                                       bf16* __restrict__ dK, bf16* __restrict__ dV, int S, int hq,
                                                       int hkv, int causal, float scale, float scale_log2,
                                                       DropParams drp, float* __restrict__ ws, int nsplit) {
-  constexpr int LDR = D + 8, CH = D / 8, TILE = 64 * LDR, NS = D / 32, ND = D / 16;
+  constexpr int LDR = D + 16, CH = D / 8, TILE = 64 * LDR, NS = D / 32, ND = D / 16;   // D + 16: conflict-free (see attn_fwd_k)
   constexpr int LOADS = 64 * CH / 256;
   __shared__ __attribute__((aligned(16))) bf16 smem_all[HALVES * 4 * TILE];  // per half: Q0 dO0 Q1 dO1
   __shared__ __attribute__((aligned(16))) float stat_all[HALVES][2][2][64];  // [half][buf][lse|delta][q]

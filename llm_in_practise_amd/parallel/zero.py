@@ -174,9 +174,10 @@ class _QuantFlat:
         self.shard = full[rank * self.shard_n:(rank + 1) * self.shard_n].clone()
 
     def drop_caches(self):
+        # the g4w-packed copy of the codes goes with them; the decoded fp32 block scales (1/16 of the bf16
+        # size) stay cached — rebuilding them at every gather cost more than their bytes (BASELINE #4)
         for q in self.owners:
             q.__dict__.pop("_g4w", None)
-            q.__dict__.pop("_gemv_sc", None)
 
 
 class _Unit:
@@ -379,7 +380,7 @@ class ZeroEngine:
                     dist.broadcast(p.data, src=0)
         self.units = [_Unit(f"u{i}", u, groups[id(u)], W, r, self.params[0].dtype, self.device, index=i,
                             block=self.block) for i, u in enumerate(order)]
-        if self.cfg.zero.stage3_partition_frozen_quant:
+        if self.cfg.zero.stage3_partition_frozen_quant and W > 1:   # (world 1: nothing to shard)
             claimed: set = set()
             for u in self.units:
                 if u.module is self.module:       # the root unit: its own frozen tensors stay replicated
