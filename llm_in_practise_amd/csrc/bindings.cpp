@@ -94,6 +94,9 @@ void launch_lora_proj_pair(const void*, const void*, int, const void*, const voi
                            float, int, hipStream_t);
 void launch_lora_acc_pair(const float*, const float*, int, int, const void*, const void*, int, int, int, float*, float*,
                           int, hipStream_t);
+void launch_lora_acc_quad(const float* const[4], const int[4], const void* const[4], const int[4], const int[4],
+                          float* const[4], const int64_t[4], const int64_t[4], const float[4], const uint8_t* const[4],
+                          int, int, hipStream_t);
 void launch_lora_dA_pair(const float*, const float*, int, int, const void*, int, int, float*, float*, int64_t, int64_t,
                          int64_t, int64_t, const uint8_t*, const uint8_t*, float, float, int, hipStream_t);
 void launch_lora_dx2(const float*, const float*, int, const void*, const void*, int, int, const uint8_t*,
@@ -1133,6 +1136,45 @@ void lora_dA_pair(Tensor g0, Tensor g1, Tensor x, Tensor out0, Tensor out1, Tens
                       p0 > 0 ? (float)(1.0 / (1.0 - p0)) : 1.f, p1 > 0 ? (float)(1.0 / (1.0 - p1)) : 1.f, M, stream());
 }
 
+// dB_q, dB_v (as lora_acc_pair) and dA_q, dA_v (as lora_dA_pair) in one launch
+void lora_acc_quad(Tensor xa, Tensor xb, Tensor dy, int64_t c0a, Tensor outa, int64_t c0b, Tensor outb, Tensor g0,
+                   Tensor g1, Tensor x, Tensor out0, Tensor out1, Tensor masks, double p0, double p1) {
+  for (const Tensor* g : {&xa, &xb, &g0, &g1})
+    TORCH_CHECK(g->scalar_type() == at::kFloat && g->dim() == 2 && g->stride(1) == 1 && g->size(1) <= 8 &&
+                    g->stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(g->data_ptr()) % 16 == 0,
+                "lora_acc_quad: xa / g fp32 [M, r<=8], 16-B aligned rows");
+  const int r = xa.size(1);
+  TORCH_CHECK(xb.size(1) == r && g0.size(1) == r && g1.size(1) == r, "lora_acc_quad: one rank");
+  CHECK_BF16(dy);
+  CHECK_BF16(x);
+  TORCH_CHECK(dy.stride(1) == 1 && dy.stride(0) % 8 == 0 && c0a % 8 == 0 && c0b % 8 == 0, "lora_acc_quad: dy layout");
+  const int M = dy.size(0), K = x.size(1);
+  TORCH_CHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && K % 128 == 0 && x.size(0) == M, "lora_acc_quad: x layout");
+  for (const Tensor* o : {&outa, &outb})
+    TORCH_CHECK(o->scalar_type() == at::kFloat && o->is_contiguous() && o->dim() == 2 && o->size(1) == r &&
+                    o->size(0) % 128 == 0, "lora_acc_quad: dB fp32 [n_i % 128, r] contiguous");
+  for (const Tensor* o : {&out0, &out1})
+    TORCH_CHECK(o->scalar_type() == at::kFloat && o->dim() == 2 && o->size(0) == r && o->size(1) == K,
+                "lora_acc_quad: dA fp32 [r, K]");
+  TORCH_CHECK(xa.size(0) == M && xb.size(0) == M && g0.size(0) == M && g1.size(0) == M &&
+                  c0a + outa.size(0) <= dy.size(1) && c0b + outb.size(0) <= dy.size(1), "lora_acc_quad: shapes");
+  const uint8_t* kbits = keep_bits_ptr(masks, M, K, "lora_acc_quad");
+  TORCH_CHECK(kbits, "lora_acc_quad: keep bits required");
+  const size_t plane = (size_t)M * (K / 8);
+  const char* base = (const char*)dy.data_ptr();
+  const float* G[4] = {xa.data_ptr<float>(), xb.data_ptr<float>(), g0.data_ptr<float>(), g1.data_ptr<float>()};
+  const int ldg[4] = {(int)xa.stride(0), (int)xb.stride(0), (int)g0.stride(0), (int)g1.stride(0)};
+  const void* X[4] = {base + c0a * 2, base + c0b * 2, x.data_ptr(), x.data_ptr()};
+  const int ldx[4] = {(int)dy.stride(0), (int)dy.stride(0), (int)x.stride(0), (int)x.stride(0)};
+  const int Ks[4] = {(int)outa.size(0), (int)outb.size(0), K, K};
+  float* out[4] = {outa.data_ptr<float>(), outb.data_ptr<float>(), out0.data_ptr<float>(), out1.data_ptr<float>()};
+  const int64_t sj[4] = {1, 1, out0.stride(0), out1.stride(0)};
+  const int64_t sk[4] = {r, r, out0.stride(1), out1.stride(1)};
+  const float ds[4] = {1.f, 1.f, p0 > 0 ? (float)(1.0 / (1.0 - p0)) : 1.f, p1 > 0 ? (float)(1.0 / (1.0 - p1)) : 1.f};
+  const uint8_t* kb[4] = {nullptr, nullptr, p0 > 0 ? kbits : nullptr, p1 > 0 ? kbits + plane : nullptr};
+  launch_lora_acc_quad(G, ldg, X, ldx, Ks, out, sj, sk, ds, kb, r, M, stream());
+}
+
 //   dx_lora [M, K] bf16 = Σ_i D_i(G_i·A_i)·ds_i  — the dX GEMM's C matrix
 Tensor lora_dx2(Tensor g0, Tensor g1, Tensor a0, Tensor a1, Tensor masks, double p0, double p1) {
   TORCH_CHECK(g0.scalar_type() == at::kFloat && g1.scalar_type() == at::kFloat && g0.stride(0) == g1.stride(0) &&
@@ -1394,6 +1436,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lora_proj_pair", &lora_proj_pair);
   m.def("lora_acc_pair", &lora_acc_pair);
   m.def("lora_dA_pair", &lora_dA_pair);
+  m.def("lora_acc_quad", &lora_acc_quad);
   m.def("lora_dx2", &lora_dx2);
   m.def("lora_apply", &lora_apply);
   m.def("gemv_w4", &gemv_w4);

@@ -77,7 +77,7 @@ __device__ __forceinline__ void xcd_grid3(int& i0, int& i1, int& i2) {
 // Causal grids (i0 = query block, work grows with it): the same XCD grouping, but inside each run of
 // n0·G consecutive logical blocks (G (head, batch) pairs — one XCD's share at the training shapes)
 // the block index varies SLOWEST, so every XCD dispatches all its heavy blocks before any light one
-// (longest-first: the light blocks then fill the slots the heavy ones leave).  LIPA_ATTN_LPT=0: the
+// (longest-first: the light blocks then fill the slots the heavy ones leave).  lpt = 0: the
 // plain xcd_grid3 order.
 __device__ __forceinline__ void xcd_grid3_lpt(int& i0, int& i1, int& i2, int lpt) {
   if (!lpt) {
@@ -108,11 +108,9 @@ __device__ __forceinline__ void xcd_grid3_lpt(int& i0, int& i1, int& i2, int lpt
   i2 = pr / n1;
 }
 
-static int attn_lpt() {
-  // 0: plain XCD-grouped order; 1: longest-first (+ snake when the grid is resident); 2: longest-first only
-  static const int v = [] { const char* e = getenv("LIPA_ATTN_LPT"); return e ? atoi(e) : 1; }();
-  return v;
-}
+// 1: longest-first (+ snake when the grid is resident) — measured best against the plain XCD-grouped
+// order (0) and longest-first only (2), profiles/r4/attention_knobs_ab.txt
+static int attn_lpt() { return 1; }
 
 // ============================================================================ forward
 // Sq queries per batch row attend to Skv keys (K/V rows of batch b start at b·kv_rows: a KV cache
@@ -727,11 +725,10 @@ __global__ __launch_bounds__(256) void attn_dkv_fin_k(const float* __restrict__ 
 // S >= 1024: blocks whose query-tile count exceeds half the blocks.  Measured (same box, interleaved,
 // scripts/experiments/gpu_dkv_split_ab.sh): [1, 2048, 32, 8, 128] bwd 283 -> 260 us; at the bench
 // shape [4, 512, ...] the 4-tile units' fixed cost and the fp32 partial round trip lose (92 -> 102 us),
-// hence the S threshold.  LIPA_ATTN_DKV_SPLIT=0 disables, =2 also splits S < 1024.
+// hence the S threshold (still the best after the LDS re-pad: profiles/r4/attention_knobs_ab.txt, S = 2048 bwd 236 vs 262 us unsplit).
 int attn_dkv_nsplit(int B, int S, int hkv, int causal) {
-  static const int env = [] { const char* e = getenv("LIPA_ATTN_DKV_SPLIT"); return e ? atoi(e) : 1; }();
   const int nb = (S + 63) / 64;
-  if (!env || !causal || nb < (env == 2 ? 4 : 16) || (long)B * hkv * nb > 512) return 0;
+  if (!causal || nb < 16 || (long)B * hkv * nb > 512) return 0;
   return nb - (nb + 1) / 2;   // kb with nb - kb > ceil(nb / 2)
 }
 
@@ -752,12 +749,8 @@ static DropParams make_drop(float p, uint64_t seed) {
     default: { constexpr int DD = 128; __VA_ARGS__; } break;  \
   }
 
-// register prefetch depth per kernel (measured, profiles/attention_fwd_bwd.txt): fwd 1 (2 waves per
-// SIMD at 244 VGPRs; depth 2 spills), dQ 2 (236 VGPRs), dK/dV 1; LIPA_ATTN_PF=1|2 forces all
-static int attn_pf(int dflt) {
-  static const int pf = [] { const char* e = getenv("LIPA_ATTN_PF"); return e ? atoi(e) : 0; }();
-  return pf == 1 || pf == 2 ? pf : dflt;
-}
+// register prefetch depth per kernel (measured, profiles/attention_fwd_bwd.txt, re-checked after the LDS
+// re-pad in profiles/r4/attention_knobs_ab.txt): fwd 1 (depth 2 spills), dQ 2, dK/dV 1
 
 void launch_attn_fwd(const void* q, const void* k, const void* v, int ldq, int ldk, int ldv, const int* kv_lens,
                      const int* q_offs, void* o, float* lse, int B, int Sq, int Skv, int kv_rows, int hq, int hkv,
@@ -765,20 +758,15 @@ void launch_attn_fwd(const void* q, const void* k, const void* v, int ldq, int l
   const DropParams dp = make_drop(p_drop, seed);
   // 128-query workgroups (32 queries per wave, QT = 2) reuse each K/V tile for twice the queries;
   // 64-query ones (QT = 1) give the causal grid more, smaller blocks to balance — measured slower at
-  // S = 512 / 8192 and equal at 2048 (profiles/attention_fwd_bwd.txt).  LIPA_ATTN_QT=1|2 forces one.
-  static const int qt_env = [] { const char* e = getenv("LIPA_ATTN_QT"); return e ? atoi(e) : 0; }();
-  const int qt = qt_env == 1 || qt_env == 2 ? qt_env : 2;
+  // S = 512 / 8192 and equal at 2048 (profiles/attention_fwd_bwd.txt, profiles/r4/attention_knobs_ab.txt).
+  const int qt = 2;
   dim3 grid((Sq + 64 * qt - 1) / (64 * qt), hq, B), blk(256);
   const float sl2 = scale * LOG2E;
 #define FWD(PFV, QTV)                                                                                      \
   LIPA_ATTN_D(D, attn_fwd_k<DD, PFV, QTV><<<grid, blk, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,  \
                                                            ldq, ldk, ldv, kv_lens, q_offs, (bf16*)o, lse, Sq, Skv, \
                                                            kv_rows, hq, hkv, causal ? 1 | (attn_lpt() << 1) : 0, sl2, dp))
-  if (qt == 1) {
-    FWD(1, 1);
-  } else {
-    FWD(1, 2);
-  }
+  FWD(1, 2);
 #undef FWD
   LIPA_CHECK_LAUNCH();
 }
@@ -807,14 +795,7 @@ void launch_attn_bwd(const void* dout, const void* q, const void* k, const void*
                                              (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dq, S, hq, \
                                              hkv, causal ? 1 | (attn_lpt() << 1) : 0, scale, sl2, dp);            \
   DKV(DD, PFKV);
-  const int pfq = attn_pf(2), pfkv = attn_pf(1);
-  if (pfq == 2 && pfkv == 1) {
-    LIPA_ATTN_D(D, RUN(DD, 2, 1));
-  } else if (pfq == 1) {
-    LIPA_ATTN_D(D, RUN(DD, 1, 1));
-  } else {
-    LIPA_ATTN_D(D, RUN(DD, 2, 2));
-  }
+  LIPA_ATTN_D(D, RUN(DD, 2, 1));   // prefetch depth dQ 2, dK/dV 1
 #undef RUN
 #undef DKV
   if (nsplit > 0) {

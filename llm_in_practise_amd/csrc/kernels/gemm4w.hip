@@ -1054,25 +1054,14 @@ bool gemm4w_supported(int M, int N, int K, int lda, int ldb, bool bt, bool w4) {
 // reduce launch (its fp32 slabs: M·N·(8s + 2) bytes at ≈12 TB/s effective + a launch).  At M = 2048
 // (bf16) this picks: q|k|v fwd 256 × 192 (256 tiles); gate|up fwd / LM head 256 × 256; o fwd, the dX
 // GEMMs to d_model and down dX 128 × 256; down fwd and gate|up dX 256 × 256 with 2 splits.
-// LIPA_GEMM4W_BN / LIPA_GEMM4W_BM / LIPA_GEMM4W_SPLITS force a choice.
+// Callers may force bn / bm / splits through the binding arguments (the A/B scripts do).
 struct G4wCfg {
   int bm, bn, splits;
 };
-static int env_int(const char* name) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : 0;
-}
-static double env_dbl(const char* name, double d) {
-  const char* e = getenv(name);
-  return e ? atof(e) : d;
-}
 G4wCfg gemm4w_cfg(int M, int N, int K, bool bt, int bn_req, int sp_req, int bm_req, bool w4) {
-  static const int forced_bn = env_int("LIPA_GEMM4W_BN"), forced_sp = env_int("LIPA_GEMM4W_SPLITS"),
-                   forced_bm = env_int("LIPA_GEMM4W_BM");
-  static const double w4_cost = env_dbl("LIPA_W4_COST", 1.0), w4_cost128 = env_dbl("LIPA_W4_COST128", 1.35);
-  if (bn_req == 0) bn_req = forced_bn;
-  if (sp_req <= 0) sp_req = forced_sp;
-  if (bm_req == 0) bm_req = forced_bm;
+  // W4 (NF4 codes expanded in-kernel): the measured cost of a K-tile relative to bf16 per tile height
+  // (profiles/r4/gemm4w_nf4_ab.txt)
+  constexpr double w4_cost = 1.0, w4_cost128 = 1.35;
   const int nk = K / BK;
   G4wCfg best{256, 128, 1};
   double best_t = 1e30;

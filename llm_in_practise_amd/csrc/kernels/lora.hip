@@ -364,6 +364,28 @@ __global__ __launch_bounds__(256) void lora_acc_pair_k(AccPair a, int ldg, int r
                                     a.sk[b], M, 0, a.kb[b] ? 1u : 0u, a.ds[b], 0, bx, blockIdx.y, a.kb[b]);
 }
 
+// The q+v backward's four weight-gradient products in ONE launch (job = blockIdx.x range): dB_q, dB_v
+// (dy column blocks × the forward's xa) and dA_q, dA_v (x with the stored keep bits × g) — the same
+// MFMA body as lora_acc_pair_k, each job with its own operands and strides; one launch, one tail
+// (two back-to-back launches of ≈10 µs each left half of each launch's last wave of workgroups idle).
+struct AccQuad {
+  const float* G[4];
+  const bf16* X[4];
+  float* out[4];
+  int K[4], nb[4], ldg[4], ldx[4];   // nb: first blockIdx.x of the job
+  int64_t sj[4], sk[4];
+  float ds[4];
+  const uint8_t* kb[4];
+};
+template <int SUB>
+__global__ __launch_bounds__(256) void lora_acc_quad_k(AccQuad a, int r, int M) {
+  const int bx0 = blockIdx.x;
+  const int j = bx0 >= a.nb[3] ? 3 : bx0 >= a.nb[2] ? 2 : bx0 >= a.nb[1] ? 1 : 0;
+  lora_acc_mfma_body<8, false, SUB>(a.G[j], a.ldg[j], r, a.X[j], a.ldx[j], nullptr, 0, nullptr, a.K[j], a.out[j],
+                                    a.sj[j], a.sk[j], M, 0, a.kb[j] ? 1u : 0u, a.ds[j], 0, bx0 - a.nb[j], blockIdx.y,
+                                    a.kb[j]);
+}
+
 // dx_lora[m, k] = Σ_i D_i[m, k]·ds_i·Σ_j G_i[m, j]·A_i[j, k] for the two branches (bf16 [M, K]): the LoRA
 // input-gradient term, written once and handed to the dX GEMM as its C matrix (no read-modify-write
 // pass over dx).  A thread owns 8 consecutive k of 8 rows; A's 8 k-columns are loaded once per thread.
@@ -1122,6 +1144,32 @@ void launch_lora_dA_pair(const float* G0, const float* G1, int ldg, int r, const
             {ds0, ds1}, {kb0, kb1}};
   dim3 g(2 * (K / 128), (M + 127) / 128);
   lora_acc_pair_k<1><<<g, 256, 0, st>>>(a, ldg, r, ldx, M);
+  LIPA_CHECK_LAUNCH();
+}
+
+// jobs 0, 1: dB of the two branches (G = xa, X = dy column block, out [n, r] row-major);
+// jobs 2, 3: dA (G = g, X = x, out [r, K] with strides, keep bits / rescale per branch)
+void launch_lora_acc_quad(const float* const G[4], const int ldg[4], const void* const X[4], const int ldx[4],
+                          const int K[4], float* const out[4], const int64_t sj[4], const int64_t sk[4],
+                          const float ds[4], const uint8_t* const kb[4], int r, int M, hipStream_t st) {
+  AccQuad a{};
+  int nb = 0;
+  for (int j = 0; j < 4; ++j) {
+    a.G[j] = G[j];
+    a.X[j] = (const bf16*)X[j];
+    a.out[j] = out[j];
+    a.K[j] = K[j];
+    a.ldg[j] = ldg[j];
+    a.ldx[j] = ldx[j];
+    a.sj[j] = sj[j];
+    a.sk[j] = sk[j];
+    a.ds[j] = ds[j];
+    a.kb[j] = kb[j];
+    a.nb[j] = nb;
+    nb += K[j] / 128;
+  }
+  dim3 g(nb, (M + 127) / 128);
+  lora_acc_quad_k<1><<<g, 256, 0, st>>>(a, r, M);
   LIPA_CHECK_LAUNCH();
 }
 

@@ -618,6 +618,7 @@ class _FusedLinearFn(torch.autograd.Function):
         fast = ctx.fast
         grads_ab = [None] * (2 * nb)
         g_list = []
+        done_quad = None      # ((dA_0, ret), (dA_1, ret)) when lora_acc_quad already produced both dA
 
         def dest(i):   # the optimizer-owned fp32 grad view (accumulate in place) or a fresh buffer
             prm = ctx.ab_refs[i]
@@ -637,7 +638,18 @@ class _FusedLinearFn(torch.autograd.Function):
                     and xs[1] is not None and xs[0].stride(0) == xs[1].stride(0) and xs[0].shape[1] <= 8
                     and all((br.c1 - br.c0) % 128 == 0 for br in branches)):
                 (o0, ret0), (o1, ret1) = dest(1), dest(3)
-                native().lora_acc_pair(xs[0], xs[1], dy, branches[0].c0, o0, branches[1].c0, o1)
+                # with the dropout pair's dA due too (the keep-bit path below), both dB and both dA in ONE launch
+                quad = (ctx.pair and all(k is not None for k in ctx.keys) and ctx.masks is not None
+                        and ctx.needs_input_grad[0] and ctx.needs_input_grad[5] and ctx.needs_input_grad[7]
+                        and dy.shape[0] >= _LT_MIN_M and x.shape[1] % 128 == 0
+                        and g_list[0].shape[1] == xs[0].shape[1])
+                if quad:
+                    (a0o, aret0), (a1o, aret1) = dest(0), dest(2)
+                    native().lora_acc_quad(xs[0], xs[1], dy, branches[0].c0, o0, branches[1].c0, o1, g_list[0],
+                                           g_list[1], x, a0o, a1o, ctx.masks, branches[0].dropout, branches[1].dropout)
+                    done_quad = ((a0o, aret0), (a1o, aret1))
+                else:
+                    native().lora_acc_pair(xs[0], xs[1], dy, branches[0].c0, o0, branches[1].c0, o1)
                 for i, (o, ret) in ((0, (o0, ret0)), (1, (o1, ret1))):
                     if ret:
                         grads_ab[2 * i + 1] = o.to(ab[2 * i + 1].dtype)
@@ -706,8 +718,11 @@ class _FusedLinearFn(torch.autograd.Function):
                     c = native().lora_dx2(g_list[0], g_list[1], a0, a1, ctx.masks, p0, p1)
                     dx = _base_gemm_t(dy, wb, None, None, c)
                     del c
-                (o0, ret0), (o1, ret1) = dest(0), dest(2)
-                native().lora_dA_pair(g_list[0], g_list[1], x, o0, o1, ctx.masks, p0, p1)
+                if done_quad is not None:
+                    (o0, ret0), (o1, ret1) = done_quad
+                else:
+                    (o0, ret0), (o1, ret1) = dest(0), dest(2)
+                    native().lora_dA_pair(g_list[0], g_list[1], x, o0, o1, ctx.masks, p0, p1)
                 ctx.masks = None
                 for i, (o, ret) in ((0, (o0, ret0)), (1, (o1, ret1))):
                     if ret:
@@ -717,6 +732,7 @@ class _FusedLinearFn(torch.autograd.Function):
                 pair_ok = False
                 done_dA = True
             else:
+                assert done_quad is None, "lora_acc_quad ran but the keep-bit dX path did not"
                 ext_a, ext_b = fold_ext()
                 dx = _base_gemm_t(dy, wb, ext_a, ext_b)
                 done_dA = False
