@@ -12,8 +12,8 @@
 //    flight, the whole matrix in flight across the chip;
 //  * dequant in 7 VALU per 8 weights and no conversion: a nibble q becomes the bf16 bit pattern
 //    0x4300|q = 128+q by a byte permute (v_perm with a 0x43 byte plane), so the MFMA accumulates
-//    G = Σ x·(128+q) per group; a second MFMA against a ones operand gives X = Σ x, and the group
-//    folds as y += s·G + (b − 128·s)·X — scale and zero point never touch the weights;
+//    G = Σ x·(128+q) per group; X = Σ x per (row, group) is reduced once while x is staged, and the
+//    group folds as y += s·G + (b − 128·s)·X — scale and zero point never touch the weights;
 //  * the permute yields the lane's 8 weights in k order (1,3,5,7,0,2,4,6); x is staged once per
 //    workgroup into LDS (M × 128·NKB, 16-B padded rows: conflict-free ds_read_b128) in the same
 //    order, so every A/B k-slot pair matches (the MFMA sum is order-free);
@@ -89,13 +89,25 @@ __global__ __launch_bounds__(256) void w4mm_k(const bf16* __restrict__ X, int ld
       s2[kb][ct] = sc[(size_t)ncol[ct] * G + kk / gs];
     }
 
-  // 2) x slice → LDS, permuted to the dequant's k order; rows >= M are zero
-  constexpr int CH = KR / 8;              // 16-B chunks per row
-  for (int c = tid; c < RT * 16 * CH; c += 256) {
+  // 2) x slice → LDS, permuted to the dequant's k order; rows >= M are zero.  The 16 lanes that hold one
+  //    128-deep group of a row also reduce its sum Σx (xsum[kb][row], fp32) for the group fold
+  constexpr int CH = KR / 8;              // 16-B chunks per row (a multiple of 16)
+  constexpr int RWS = RT * 16;
+  float* xsum = reinterpret_cast<float*>(lds_raw + (size_t)RWS * LDXS * 2);
+  for (int c = tid; c < RWS * CH; c += 256) {
     const int r = c / CH, kc = c - r * CH;
     u32x4 v = {0u, 0u, 0u, 0u};
-    if (r < M) v = x_perm(*reinterpret_cast<const u32x4*>(X + (size_t)r * ldx + k0 + 8 * kc));
-    *reinterpret_cast<u32x4*>(xs + r * LDXS + 8 * kc) = v;
+    if (r < M) v = *reinterpret_cast<const u32x4*>(X + (size_t)r * ldx + k0 + 8 * kc);
+    const bf16x8 xb = __builtin_bit_cast(bf16x8, v);
+    float t = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t += (float)xb[e];
+    t += __shfl_xor(t, 1, 64);
+    t += __shfl_xor(t, 2, 64);
+    t += __shfl_xor(t, 4, 64);
+    t += __shfl_xor(t, 8, 64);
+    if ((kc & 15) == 0) xsum[(kc >> 4) * RWS + r] = t;
+    *reinterpret_cast<u32x4*>(xs + r * LDXS + 8 * kc) = x_perm(v);
   }
   __syncthreads();
 
@@ -104,7 +116,6 @@ __global__ __launch_bounds__(256) void w4mm_k(const bf16* __restrict__ X, int ld
   for (int ct = 0; ct < W4_CT; ++ct)
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) acc[ct][rt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
@@ -120,9 +131,7 @@ __global__ __launch_bounds__(256) void w4mm_k(const bf16* __restrict__ X, int ld
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         xa[j] = *reinterpret_cast<const bf16x8*>(xs + (16 * rt + li) * LDXS + 128 * kb + 32 * q + 8 * j);
-      f32x4 ax = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[0], ones, zero, 0, 0, 0);
-#pragma unroll
-      for (int j = 1; j < 4; ++j) ax = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[j], ones, ax, 0, 0, 0);
+      const f32x4 ax = *reinterpret_cast<const f32x4*>(xsum + kb * RWS + 16 * rt + 4 * q);   // Σx of rows 4q..4q+3
 #pragma unroll
       for (int ct = 0; ct < W4_CT; ++ct) {
         f32x4 g = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[0], bq[ct][0], zero, 0, 0, 0);
@@ -196,7 +205,7 @@ void launch_w4mm(const void* X, int ldx, const uint8_t* codes, const float* sc2,
                  float* part, int M, int N, int K, int nkb, hipStream_t st) {
   const int ncs = N / W4_COLS, KS = K / (128 * nkb);
   const int RT = M <= 16 ? 1 : M <= 32 ? 2 : 4;
-  const size_t lds = (size_t)RT * 16 * (128 * nkb + 8) * 2;
+  const size_t lds = (size_t)RT * 16 * (128 * nkb + 8) * 2 + (size_t)nkb * RT * 16 * 4;
 #define L(RT_, NKB_)                                                                                            \
   w4mm_k<RT_, NKB_><<<ncs * KS, 256, lds, st>>>((const bf16*)X, ldx, codes, (const float2*)sc2, gs,             \
                                                 (const bf16*)res, (bf16*)out, part, M, N, K, ncs)

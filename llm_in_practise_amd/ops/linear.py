@@ -639,7 +639,7 @@ class _FusedLinearFn(torch.autograd.Function):
                     and all((br.c1 - br.c0) % 128 == 0 for br in branches)):
                 (o0, ret0), (o1, ret1) = dest(1), dest(3)
                 # with the dropout pair's dA due too (the keep-bit path below), both dB and both dA in ONE launch
-                quad = (ctx.pair and all(k is not None for k in ctx.keys) and ctx.masks is not None
+                quad = (_DX_C and ctx.pair and all(k is not None for k in ctx.keys) and ctx.masks is not None
                         and ctx.needs_input_grad[0] and ctx.needs_input_grad[5] and ctx.needs_input_grad[7]
                         and dy.shape[0] >= _LT_MIN_M and x.shape[1] % 128 == 0
                         and g_list[0].shape[1] == xs[0].shape[1])
