@@ -166,22 +166,32 @@ __global__ __launch_bounds__(256) void w4mm_k(const bf16* __restrict__ X, int ld
   }
 }
 
-// out[m, n] = Σ_s part[s, m, n] (+ residual) → bf16; 4 outputs per thread
+// out[m, n] = Σ_s part[s, m, n] (+ residual) → bf16; 2 outputs per thread and every slice's load issued
+// before the adds (the grid is small at decode sizes — M·N/512 workgroups — so each thread's slice loads
+// must overlap, not run as KS dependent round trips)
+template <int SU>
 __global__ __launch_bounds__(256) void w4mm_reduce_k(const float* __restrict__ part, const bf16* __restrict__ res,
                                                      bf16* __restrict__ out, int S, size_t MN) {
-  const size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 2;
   if (i >= MN) return;
-  f32x4 v = *reinterpret_cast<const f32x4*>(part + i);
-  for (int s = 1; s < S; ++s) v += *reinterpret_cast<const f32x4*>(part + (size_t)s * MN + i);
-  if (res) {
-    const bf16x4 r = *reinterpret_cast<const bf16x4*>(res + i);
+  float2 v = {0.f, 0.f};
+  for (int s0 = 0; s0 < S; s0 += SU) {
+    float2 t[SU];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] += (float)r[j];
+    for (int u = 0; u < SU; ++u)
+      t[u] = s0 + u < S ? *reinterpret_cast<const float2*>(part + (size_t)(s0 + u) * MN + i) : float2{0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      v.x += t[u].x;
+      v.y += t[u].y;
+    }
   }
-  bf16x4 o;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
-  *reinterpret_cast<bf16x4*>(out + i) = o;
+  if (res) {
+    v.x += (float)res[i];
+    v.y += (float)res[i + 1];
+  }
+  bf16x2 o = {(bf16)v.x, (bf16)v.y};
+  *reinterpret_cast<bf16x2*>(out + i) = o;
 }
 
 }  // namespace
@@ -190,15 +200,13 @@ bool w4mm_supported(int M, int N, int K, int gs) {
   return M >= 1 && M <= 64 && N % W4_COLS == 0 && K % 128 == 0 && gs % 128 == 0 && K % gs == 0;
 }
 
-// 128-deep blocks per workgroup (measured per shape at M = 1..64, profiles/r4/w4a16_w4mm.txt): 4, or 8 for
-// M <= 16 when that still leaves >= 192 workgroups (fewer, longer weight streams win there; at M > 16
-// the 8-block slice holds too many codes + accumulators); 2 / 1 when K allows nothing larger
+// 128-deep blocks per workgroup (measured per shape at M = 1..64 with the unrolled reduce,
+// profiles/r4/w4a16_w4mm_reduce.txt): 4, or 2 for M <= 8 when 4 would leave fewer than 512 workgroups
+// (q|k|v, o: more, shorter weight streams win there); 2 / 1 when K allows nothing larger
 int w4mm_nkb(int M, int N, int K) {
   const int ncs = N / W4_COLS, kb = K / 128;
-  if (M <= 16 && kb % 8 == 0 && ncs * (kb / 8) >= 192) return 8;
-  for (int nkb = 4; nkb >= 2; nkb /= 2)
-    if (kb % nkb == 0) return nkb;
-  return 1;
+  if (kb % 4 == 0 && !(M <= 8 && ncs * (kb / 4) < 512)) return 4;
+  return kb % 2 == 0 ? 2 : 1;
 }
 
 void launch_w4mm(const void* X, int ldx, const uint8_t* codes, const float* sc2, int gs, const void* res, void* out,
@@ -218,7 +226,7 @@ void launch_w4mm(const void* X, int ldx, const uint8_t* codes, const float* sc2,
 #undef L
   if (KS > 1) {
     const size_t MN = (size_t)M * N;
-    w4mm_reduce_k<<<(MN / 4 + 255) / 256, 256, 0, st>>>(part, (const bf16*)res, (bf16*)out, KS, MN);
+    w4mm_reduce_k<8><<<(MN / 2 + 255) / 256, 256, 0, st>>>(part, (const bf16*)res, (bf16*)out, KS, MN);
   }
   LIPA_CHECK_LAUNCH();
 }

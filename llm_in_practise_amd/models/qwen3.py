@@ -35,6 +35,7 @@ from ..ops.norm import RMSNorm, rms_norm, rms_norm_residual
 from ..ops.rope import apply_rope, qk_norm_rope
 from ..parallel.tensor_parallel import tp_all_reduce
 from ..peft.lora import LoraLayer, base_of
+from ..quant.int4 import Int4Linear
 from ..ops.embedding import Embedding
 from .common import CausalLMOutput, FusedProjection, KVCache, PackedPrefill, _leaf_linear, can_fuse, project
 
@@ -224,6 +225,8 @@ class Qwen3MLP(nn.Module):
         if any((isinstance(m, LoraLayer) and not m.merged) or getattr(_leaf_linear(m), "_mlora", None) is not None
                for m in mods):
             return None
+        if isinstance(_leaf_linear(self.down_proj), Int4Linear):
+            return None     # W4A16 runs as separate projections (base_of would dequantise the weight)
         down_base, down_bias = base_of(self.down_proj)
         if self._gu.bias is not None or down_bias is not None:
             return None
