@@ -52,28 +52,31 @@ __global__ __launch_bounds__(256) void mlora_apply_k(const bf16* __restrict__ x,
     if (lane == 0) xa[r] = acc * sg.scale;
   }
   __syncthreads();
-  // expand: thread j owns 8 consecutive columns of this chunk
-  const int n = blockIdx.y * CHUNK + threadIdx.x * 8;
-  if (n >= N) return;
-  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int r0 = 0; r0 < sg.r; r0 += 8) {   // ranks and offsets are multiples of 8 (host): 16-B loads
-    float xv[8];
+  // expand: the row's whole column range in CHUNK-wide passes (the rank-r projection above is computed
+  // once per row, not once per column chunk); thread j owns 8 consecutive columns of each pass
+  for (int nb = 0; nb < N; nb += CHUNK) {
+    const int n = nb + threadIdx.x * 8;
+    if (n >= N) break;
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r0 = 0; r0 < sg.r; r0 += 8) {   // ranks and offsets are multiples of 8 (host): 16-B loads
+      float xv[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) xv[i] = xa[r0 + i];
+      for (int i = 0; i < 8; ++i) xv[i] = xa[r0 + i];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float bv[8];
-      load8(Bm + (size_t)(n + e) * R + sg.off + r0, bv);
+      for (int e = 0; e < 8; ++e) {
+        float bv[8];
+        load8(Bm + (size_t)(n + e) * R + sg.off + r0, bv);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o[e] = fmaf(xv[i], bv[i], o[e]);
+        for (int i = 0; i < 8; ++i) o[e] = fmaf(xv[i], bv[i], o[e]);
+      }
     }
-  }
-  bf16* yr = y + (size_t)t * ldy + c0 + n;
-  float cur[8];
-  load8(yr, cur);
+    bf16* yr = y + (size_t)t * ldy + c0 + n;
+    float cur[8];
+    load8(yr, cur);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) cur[e] += o[e];
-  store8(yr, cur);
+    for (int e = 0; e < 8; ++e) cur[e] += o[e];
+    store8(yr, cur);
+  }
 }
 
 }  // namespace
@@ -81,7 +84,7 @@ __global__ __launch_bounds__(256) void mlora_apply_k(const bf16* __restrict__ x,
 void launch_mlora_apply(const void* x, int ldx, const void* A, const void* B, const int64_t* ids, const void* seg,
                         int n_seg, void* y, int ldy, int c0, int T, int K, int N, int R, hipStream_t st) {
   if (T <= 0) return;
-  const dim3 grid(T, (N + CHUNK - 1) / CHUNK);
+  const dim3 grid(T);
   mlora_apply_k<<<grid, 256, 0, st>>>((const bf16*)x, ldx, (const bf16*)A, (const bf16*)B, ids, (const Seg*)seg,
                                       n_seg, (bf16*)y, ldy, c0, K, N, R);
   LIPA_CHECK_LAUNCH();

@@ -601,7 +601,10 @@ class _FusedLinearFn(torch.autograd.Function):
         ctx.pair = bool(branches) and fast and _pair_ok(x, branches)
         ctx.ab_refs = ab          # the parameters themselves: fused kernels accumulate into their .grad
         ctx.has_residual = residual is not None
-        ctx.save_for_backward(x, weight, *ab, *[t for t in xa_list if t is not None])
+        # the LoRA parameters travel as ctx.ab_refs, not through save_for_backward: under non-reentrant
+        # checkpointing every saved tensor costs a Python pack / unpack hook (host time of the
+        # reference-faithful step), and parameters need no saving
+        ctx.save_for_backward(x, weight, *[t for t in xa_list if t is not None])
         ctx.nb = len(branches)
         return y
 
@@ -611,8 +614,8 @@ class _FusedLinearFn(torch.autograd.Function):
         saved = ctx.saved_tensors
         x, weight = saved[0], saved[1]
         nb = ctx.nb
-        ab = saved[2:2 + 2 * nb]
-        xa_list = saved[2 + 2 * nb:2 + 3 * nb]
+        ab = ctx.ab_refs
+        xa_list = saved[2:2 + nb]
         dense = not isinstance(base, NF4Weight)
         dy = dy.contiguous()
         fast = ctx.fast

@@ -14,13 +14,14 @@ class _RMSNormFn(torch.autograd.Function):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).contiguous()
         y, rstd = native().rmsnorm_fwd(x2, weight, eps)
-        ctx.save_for_backward(x2, weight, rstd)
+        ctx.save_for_backward(x2, rstd)
+        ctx.weight = weight         # a parameter: no saved-tensor hook (non-reentrant checkpointing)
         ctx.shape = shape
         return y.view(shape)
 
     @staticmethod
     def backward(ctx, dy):
-        x2, weight, rstd = ctx.saved_tensors
+        (x2, rstd), weight = ctx.saved_tensors, ctx.weight
         need_dw = weight is not None and ctx.needs_input_grad[1]
         dx, dw = native().rmsnorm_bwd(dy.reshape(x2.shape).contiguous(), x2, weight, rstd, need_dw, None)
         return dx.view(ctx.shape), (dw.to(weight.dtype) if need_dw else None), None
@@ -37,13 +38,14 @@ class _RMSNormResidualFn(torch.autograd.Function):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).contiguous()
         y, rstd = native().rmsnorm_fwd(x2, weight, eps)
-        ctx.save_for_backward(x2, weight, rstd)
+        ctx.save_for_backward(x2, rstd)
+        ctx.weight = weight
         ctx.shape = shape
         return y.view(shape), x.view_as(x)
 
     @staticmethod
     def backward(ctx, dy, dskip):
-        x2, weight, rstd = ctx.saved_tensors
+        (x2, rstd), weight = ctx.saved_tensors, ctx.weight
         need_dw = weight is not None and ctx.needs_input_grad[1]
         if dy is None:
             return dskip, None, None

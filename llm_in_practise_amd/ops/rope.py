@@ -20,13 +20,13 @@ def _ref_rope_tok(x, cos, sin, interleaved):
 class _RopeFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, cos, sin, interleaved):
-        ctx.save_for_backward(cos, sin)
+        ctx.cs = (cos, sin)          # per-step constants: no saved-tensor hooks
         ctx.interleaved = interleaved
         return native().rope(x.contiguous(), cos, sin, interleaved, False)
 
     @staticmethod
     def backward(ctx, dy):
-        cos, sin = ctx.saved_tensors
+        cos, sin = ctx.cs
         return native().rope(dy.contiguous(), cos, sin, ctx.interleaved, True), None, None, None
 
 
@@ -43,14 +43,16 @@ class _QKNormRopeFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, qw, kw, cos, sin, hq, hkv, d, eps):
         q, k, rq, rk = native().qk_norm_rope_fwd(qkv, qw, kw, cos, sin, hq, hkv, d, eps)
-        ctx.save_for_backward(qkv, qw, kw, cos, sin, rq, rk)
+        ctx.save_for_backward(qkv, rq, rk)
+        ctx.consts = (qw, kw, cos, sin)   # parameters / per-step tables: no saved-tensor hooks
         ctx.dims = (hq, hkv, d)
         v = qkv[:, (hq + hkv) * d:]
         return q, k, v
 
     @staticmethod
     def backward(ctx, dq, dk, dv):
-        qkv, qw, kw, cos, sin, rq, rk = ctx.saved_tensors
+        qkv, rq, rk = ctx.saved_tensors
+        qw, kw, cos, sin = ctx.consts
         hq, hkv, d = ctx.dims
         dqkv = native().qk_norm_rope_bwd(dq.contiguous(), dk.contiguous(),
                                          None if dv is None else dv.contiguous(), qkv, qw, kw, cos, sin, rq, rk, hq, hkv, d)

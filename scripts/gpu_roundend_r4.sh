@@ -1,0 +1,13 @@
+#!/bin/bash
+# round-end rehearsal: the whole GPU test tier, smoke(), then the default bench.py (as the driver runs them).
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+export HSA_ENABLE_IPC_MODE_LEGACY=0 PYTHONPATH=$R
+OUT=$R/gpurun_out/roundend_$1; mkdir -p $OUT
+cd $R
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/tests.txt 2>&1
+rc=$?; tail -4 $OUT/tests.txt; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.txt 2>&1
+rc=$?; tail -2 $OUT/smoke.txt; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
+rc=$?; tail -1 $OUT/bench.json; exit $rc
