@@ -99,6 +99,17 @@ void launch_lora_acc_quad(const float* const[4], const int[4], const void* const
                           int, int, hipStream_t);
 void launch_lora_dA_pair(const float*, const float*, int, int, const void*, int, int, float*, float*, int64_t, int64_t,
                          int64_t, int64_t, const uint8_t*, const uint8_t*, float, float, int, hipStream_t);
+void launch_lora_acc_jobs(int, const float* const*, const int*, const int*, const void* const*, const int*, const int*,
+                          float* const*, const int64_t*, const int64_t*, const float*, const uint8_t* const*, int,
+                          hipStream_t);
+void launch_lora_proj_m(const void*, int, int, int, int, const void* const*, const int*, const uint64_t*, const float*,
+                        const float*, uint8_t* const*, size_t, float* const*, const int*, void* const*, const int*, float*,
+                        hipStream_t);
+int lora_proj_m_ws_floats(int, int, int);
+void launch_lora_proj_cols(int, const void* const*, int, const void* const*, const int*, const int*, float* const*,
+                           const float*, int, hipStream_t);
+void launch_lora_dxc(int, const float* const*, const int*, const void* const*, const int*, const uint8_t* const*,
+                     const float*, void*, int, int, hipStream_t);
 void launch_lora_dx2(const float*, const float*, int, const void*, const void*, int, int, const uint8_t*,
                      const uint8_t*, float, float, void*, int, int, hipStream_t);
 void launch_lora_apply(void*, int, int, int, const float* const*, const int*, const void* const*, void* const*, const int*, const int*,
@@ -788,9 +799,11 @@ Tensor gemm4w_loradx(Tensor dy, Tensor w, optional<Tensor> wscale, int64_t n_w4,
     ld.r[i] = (int)a.size(0);
     ld.ds[i] = (float)(1.0 / (1.0 - ps[i]));
   }
-  if (masks && masks->defined()) {
-    TORCH_CHECK(masks->scalar_type() == at::kByte && masks->is_contiguous() && masks->numel() == 2 * M * (N / 8),
-                "gemm4w_loradx: keep bits uint8 [2, M, N/8]");
+  // the kernel's prologue always loads the keep bits (a branch without dropout passes an all-ones plane)
+  TORCH_CHECK(masks && masks->defined(), "gemm4w_loradx: keep bits required");
+  {
+    TORCH_CHECK(masks->scalar_type() == at::kByte && masks->is_contiguous() && masks->numel() >= nbr * M * (N / 8) &&
+                    masks->numel() % (M * (N / 8)) == 0, "gemm4w_loradx: keep bits uint8 [P >= nbr, M, N/8]");
     for (int i = 0; i < nbr; ++i) ld.keep[i] = masks->data_ptr<uint8_t>() + (size_t)i * M * (N / 8);
   }
   int bn = 0, bm = 0;
@@ -1175,6 +1188,177 @@ void lora_acc_quad(Tensor xa, Tensor xb, Tensor dy, int64_t c0a, Tensor outa, in
   launch_lora_acc_quad(G, ldg, X, ldx, Ks, out, sj, sk, ds, kb, r, M, stream());
 }
 
+// ---- 1-4 adapters of one projection (the general multi-adapter path; BASELINE #2's q, k, v and o) ----
+static uint8_t* keep_plane(const optional<Tensor>& m, int64_t plane, int64_t M, int64_t K, const char* who) {
+  if (!m || !m->defined() || plane < 0) return nullptr;
+  TORCH_CHECK(m->scalar_type() == at::kByte && m->is_contiguous() && m->dim() == 3 && m->size(1) == M &&
+                  m->size(2) == K / 8 && plane < m->size(0), who, ": keep bits uint8 [P, M, K/8] contiguous");
+  return m->data_ptr<uint8_t>() + (size_t)plane * M * (K / 8);
+}
+
+// xa_b = s_b·D_b(x)·A_bᵀ for every adapter in one pass over x: fp32 [M, r_b] returned (want_f32), bf16 into
+// outbs[b] (column-slice views) when given; masks [nbr, M, K/8] (optional) receives every branch's keep bits.
+std::vector<Tensor> lora_proj_m(Tensor x, std::vector<Tensor> as, std::vector<optional<Tensor>> outbs, bool want_f32,
+                                std::vector<double> ps, std::vector<int64_t> keys, std::vector<double> scales,
+                                optional<Tensor> masks) {
+  CHECK_BF16(x);
+  const int nbr = (int)as.size();
+  TORCH_CHECK(nbr >= 1 && nbr <= 4 && (int)outbs.size() == nbr && (int)ps.size() == nbr && (int)keys.size() == nbr &&
+                  (int)scales.size() == nbr, "lora_proj_m: 1..4 branches");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && K % 128 == 0 &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "lora_proj_m: x [M, K % 128], 16-B rows");
+  const void* W[4] = {};
+  int r[4] = {}, ldof[4] = {}, ldob[4] = {};
+  uint64_t key[4] = {};
+  float p[4] = {}, sc[4] = {};
+  uint8_t* mko[4] = {};
+  float* outf[4] = {};
+  void* outb[4] = {};
+  std::vector<Tensor> res;
+  for (int b = 0; b < nbr; ++b) {
+    const Tensor& a = as[b];
+    CHECK_BF16(a);
+    TORCH_CHECK(a.is_contiguous() && a.size(1) == K && a.size(0) <= 16 && reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0,
+                "lora_proj_m: A_b [r <= 16, K]");
+    W[b] = a.data_ptr();
+    r[b] = (int)a.size(0);
+    key[b] = (uint64_t)keys[b];
+    p[b] = (float)ps[b];
+    sc[b] = (float)scales[b];
+    mko[b] = keep_plane(masks, masks ? b : -1, M, K, "lora_proj_m");
+    if (want_f32) {
+      res.push_back(at::empty({M, r[b]}, x.options().dtype(at::kFloat)));
+      outf[b] = res.back().data_ptr<float>();
+      ldof[b] = r[b];
+    }
+    if (outbs[b] && outbs[b]->defined()) {
+      const Tensor& o = *outbs[b];
+      TORCH_CHECK(o.scalar_type() == at::kBFloat16 && o.stride(1) == 1 && o.size(0) == M && o.size(1) == r[b],
+                  "lora_proj_m: outb [M, r_b] bf16");
+      outb[b] = o.data_ptr();
+      ldob[b] = (int)o.stride(0);
+    }
+    TORCH_CHECK(outf[b] || outb[b], "lora_proj_m: no output for branch ", b);
+  }
+  if (masks && masks->defined()) TORCH_CHECK(masks->size(0) == nbr, "lora_proj_m: one keep-bit plane per branch");
+  Tensor ws = at::empty({lora_proj_m_ws_floats((int)M, (int)K, nbr)}, x.options().dtype(at::kFloat));
+  launch_lora_proj_m(x.data_ptr(), (int)x.stride(0), (int)K, (int)M, nbr, W, r, key, p, sc, mko, (size_t)x.stride(0),
+                     outf, ldof, outb, ldob, ws.data_ptr<float>(), stream());
+  return res;
+}
+
+// g_b = s_b·dy[:, c0_b : c0_b + n_b]·B_b for 1-4 adapters (B_b as Bᵀ [r_b, n_b] bf16, n_b % 512) -> fp32 [M, r_b]
+std::vector<Tensor> lora_proj_cols(Tensor dy, std::vector<int64_t> c0s, std::vector<Tensor> bts, std::vector<double> scales) {
+  CHECK_BF16(dy);
+  const int nbr = (int)bts.size();
+  TORCH_CHECK(nbr >= 1 && nbr <= 4 && (int)c0s.size() == nbr && (int)scales.size() == nbr, "lora_proj_cols: 1..4 branches");
+  TORCH_CHECK(dy.dim() == 2 && dy.stride(1) == 1 && dy.stride(0) % 8 == 0, "lora_proj_cols: dy layout");
+  const int M = dy.size(0);
+  const char* base = (const char*)dy.data_ptr();
+  const void* X[4] = {};
+  const void* W[4] = {};
+  int r[4] = {}, K[4] = {};
+  float* out[4] = {};
+  float sc[4] = {};
+  std::vector<Tensor> res;
+  for (int b = 0; b < nbr; ++b) {
+    const Tensor& bt = bts[b];
+    CHECK_BF16(bt);
+    TORCH_CHECK(bt.is_contiguous() && bt.size(0) <= 16 && bt.size(1) % 512 == 0 && c0s[b] % 8 == 0 &&
+                    c0s[b] + bt.size(1) <= dy.size(1), "lora_proj_cols: Bt_b [r <= 16, n_b % 512] within dy");
+    X[b] = base + c0s[b] * 2;
+    W[b] = bt.data_ptr();
+    r[b] = (int)bt.size(0);
+    K[b] = (int)bt.size(1);
+    res.push_back(at::empty({M, r[b]}, dy.options().dtype(at::kFloat)));
+    out[b] = res.back().data_ptr<float>();
+    sc[b] = (float)scales[b];
+  }
+  launch_lora_proj_cols(nbr, X, (int)dy.stride(0), W, r, K, out, sc, M, stream());
+  return res;
+}
+
+// up to 8 weight-gradient products in one launch: out_i += G_iᵀ·D_i(X_i[:, c0_i : c0_i + k_i]) (fp32 atomics);
+// out_t[i]: out_i is [k_i, r_i] (a dB) rather than [r_i, k_i] (a dA); planes[i] >= 0 selects keep bits of masks
+// (its K = k_i), ps[i] the matching dropout rate.
+void lora_acc_jobs(std::vector<Tensor> gs, std::vector<Tensor> xs, std::vector<int64_t> c0s, std::vector<int64_t> ks,
+                   std::vector<Tensor> outs, std::vector<bool> out_t, optional<Tensor> masks, std::vector<int64_t> planes,
+                   std::vector<double> ps) {
+  const int nj = (int)gs.size();
+  TORCH_CHECK(nj >= 1 && nj <= 8 && (int)xs.size() == nj && (int)c0s.size() == nj && (int)ks.size() == nj &&
+                  (int)outs.size() == nj && (int)out_t.size() == nj && (int)planes.size() == nj && (int)ps.size() == nj,
+              "lora_acc_jobs: 1..8 jobs");
+  const int M = gs[0].size(0);
+  const float* G[8] = {};
+  const void* X[8] = {};
+  float* out[8] = {};
+  int ldg[8] = {}, r[8] = {}, ldx[8] = {}, K[8] = {};
+  int64_t sj[8] = {}, sk[8] = {};
+  float ds[8] = {};
+  const uint8_t* kb[8] = {};
+  for (int i = 0; i < nj; ++i) {
+    const Tensor& g = gs[i];
+    const Tensor& x = xs[i];
+    const Tensor& o = outs[i];
+    TORCH_CHECK(g.scalar_type() == at::kFloat && g.dim() == 2 && g.stride(1) == 1 && g.size(0) == M && g.size(1) <= 16,
+                "lora_acc_jobs: G fp32 [M, r <= 16]");
+    CHECK_BF16(x);
+    TORCH_CHECK(x.dim() == 2 && x.size(0) == M && x.stride(1) == 1 && x.stride(0) % 8 == 0 && c0s[i] % 8 == 0 &&
+                    ks[i] % 128 == 0 && c0s[i] + ks[i] <= x.size(1), "lora_acc_jobs: X column block [M, k % 128]");
+    const int64_t rr = g.size(1);
+    TORCH_CHECK(o.scalar_type() == at::kFloat && o.dim() == 2 &&
+                    (out_t[i] ? (o.size(0) == ks[i] && o.size(1) == rr) : (o.size(0) == rr && o.size(1) == ks[i])),
+                "lora_acc_jobs: out fp32 [k, r] (out_t) or [r, k]");
+    G[i] = g.data_ptr<float>();
+    ldg[i] = (int)g.stride(0);
+    r[i] = (int)rr;
+    X[i] = (const char*)x.data_ptr() + c0s[i] * 2;
+    ldx[i] = (int)x.stride(0);
+    K[i] = (int)ks[i];
+    out[i] = o.data_ptr<float>();
+    sj[i] = out_t[i] ? o.stride(1) : o.stride(0);
+    sk[i] = out_t[i] ? o.stride(0) : o.stride(1);
+    kb[i] = ps[i] > 0 ? keep_plane(masks, planes[i], M, ks[i], "lora_acc_jobs") : nullptr;
+    TORCH_CHECK(ps[i] <= 0 || kb[i], "lora_acc_jobs: a dropout job needs its keep bits");
+    ds[i] = ps[i] > 0 ? (float)(1.0 / (1.0 - ps[i])) : 1.f;
+  }
+  launch_lora_acc_jobs(nj, G, ldg, r, X, ldx, K, out, sj, sk, ds, kb, M, stream());
+}
+
+// C = Σ_b keep_b·ds_b·(g_b·A_b) bf16 [M, K] for 1-4 adapters (masks [nbr, M, K/8] or None; ps_b = 0: no mask)
+Tensor lora_dxc(std::vector<Tensor> gs, std::vector<Tensor> as, optional<Tensor> masks, std::vector<double> ps) {
+  const int nbr = (int)gs.size();
+  TORCH_CHECK(nbr >= 1 && nbr <= 4 && (int)as.size() == nbr && (int)ps.size() == nbr, "lora_dxc: 1..4 branches");
+  const int64_t M = gs[0].size(0), K = as[0].size(1);
+  TORCH_CHECK(K % 64 == 0, "lora_dxc: K % 64");
+  const float* g[4] = {};
+  const void* a[4] = {};
+  int ldg[4] = {}, r[4] = {};
+  const uint8_t* kb[4] = {};
+  float ds[4] = {};
+  for (int b = 0; b < nbr; ++b) {
+    const Tensor& gg = gs[b];
+    const Tensor& aa = as[b];
+    TORCH_CHECK(gg.scalar_type() == at::kFloat && gg.dim() == 2 && gg.stride(1) == 1 && gg.size(0) == M &&
+                    gg.size(1) <= 16 && gg.size(1) % 4 == 0 && gg.stride(0) % 4 == 0 &&
+                    reinterpret_cast<uintptr_t>(gg.data_ptr()) % 16 == 0, "lora_dxc: g fp32 [M, r <= 16, r % 4], 16-B rows");
+    CHECK_BF16(aa);
+    TORCH_CHECK(aa.is_contiguous() && aa.size(0) == gg.size(1) && aa.size(1) == K &&
+                    reinterpret_cast<uintptr_t>(aa.data_ptr()) % 16 == 0, "lora_dxc: A_b [r_b, K]");
+    g[b] = gg.data_ptr<float>();
+    ldg[b] = (int)gg.stride(0);
+    a[b] = aa.data_ptr();
+    r[b] = (int)aa.size(0);
+    kb[b] = ps[b] > 0 ? keep_plane(masks, b, M, K, "lora_dxc") : nullptr;
+    TORCH_CHECK(ps[b] <= 0 || kb[b], "lora_dxc: a dropout branch needs its keep bits");
+    ds[b] = ps[b] > 0 ? (float)(1.0 / (1.0 - ps[b])) : 1.f;
+  }
+  Tensor out = at::empty({M, K}, as[0].options());
+  launch_lora_dxc(nbr, g, ldg, a, r, kb, ds, out.data_ptr(), (int)M, (int)K, stream());
+  return out;
+}
+
 //   dx_lora [M, K] bf16 = Σ_i D_i(G_i·A_i)·ds_i  — the dX GEMM's C matrix
 Tensor lora_dx2(Tensor g0, Tensor g1, Tensor a0, Tensor a1, Tensor masks, double p0, double p1) {
   TORCH_CHECK(g0.scalar_type() == at::kFloat && g1.scalar_type() == at::kFloat && g0.stride(0) == g1.stride(0) &&
@@ -1438,6 +1622,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lora_dA_pair", &lora_dA_pair);
   m.def("lora_acc_quad", &lora_acc_quad);
   m.def("lora_dx2", &lora_dx2);
+  m.def("lora_proj_m", &lora_proj_m);
+  m.def("lora_proj_cols", &lora_proj_cols);
+  m.def("lora_acc_jobs", &lora_acc_jobs);
+  m.def("lora_dxc", &lora_dxc);
   m.def("lora_apply", &lora_apply);
   m.def("gemv_w4", &gemv_w4);
   m.def("sample", &sample);

@@ -368,20 +368,30 @@ __global__ __launch_bounds__(256) void lora_acc_pair_k(AccPair a, int ldg, int r
 // (dy column blocks × the forward's xa) and dA_q, dA_v (x with the stored keep bits × g) — the same
 // MFMA body as lora_acc_pair_k, each job with its own operands and strides; one launch, one tail
 // (two back-to-back launches of ≈10 µs each left half of each launch's last wave of workgroups idle).
-struct AccQuad {
-  const float* G[4];
-  const bf16* X[4];
-  float* out[4];
-  int K[4], nb[4], ldg[4], ldx[4];   // nb: first blockIdx.x of the job
-  int64_t sj[4], sk[4];
-  float ds[4];
-  const uint8_t* kb[4];
+// The general form (AccJobs, up to 8 jobs, rank per job) serves the multi-adapter backward as well: all
+// dB and dA products of a projection's 1-4 adapters (BASELINE #2: q, k, v on q|k|v and o) in one launch.
+// (Grouping the dA jobs that share x so that one workgroup loads each x tile once for all members measured
+// slower at BASELINE #2's shapes: q|k|v 45 -> 62 µs — a third of the workgroups, and the re-reads of x hit
+// the MALL anyway; profiles/r4/lora_multi_adapter.txt.)
+constexpr int kAccJobs = 8;
+struct AccJobs {
+  const float* G[kAccJobs];
+  const bf16* X[kAccJobs];
+  float* out[kAccJobs];
+  int K[kAccJobs], nb[kAccJobs], ldg[kAccJobs], ldx[kAccJobs], r[kAccJobs];   // nb: first blockIdx.x of the job
+  int64_t sj[kAccJobs], sk[kAccJobs];
+  float ds[kAccJobs];
+  const uint8_t* kb[kAccJobs];
+  int njobs;
 };
 template <int SUB>
-__global__ __launch_bounds__(256) void lora_acc_quad_k(AccQuad a, int r, int M) {
+__global__ __launch_bounds__(256) void lora_acc_jobs_k(AccJobs a, int M) {
   const int bx0 = blockIdx.x;
-  const int j = bx0 >= a.nb[3] ? 3 : bx0 >= a.nb[2] ? 2 : bx0 >= a.nb[1] ? 1 : 0;
-  lora_acc_mfma_body<8, false, SUB>(a.G[j], a.ldg[j], r, a.X[j], a.ldx[j], nullptr, 0, nullptr, a.K[j], a.out[j],
+  int j = 0;
+#pragma unroll
+  for (int i = 1; i < kAccJobs; ++i)
+    if (i < a.njobs && bx0 >= a.nb[i]) j = i;
+  lora_acc_mfma_body<8, false, SUB>(a.G[j], a.ldg[j], a.r[j], a.X[j], a.ldx[j], nullptr, 0, nullptr, a.K[j], a.out[j],
                                     a.sj[j], a.sk[j], M, 0, a.kb[j] ? 1u : 0u, a.ds[j], 0, bx0 - a.nb[j], blockIdx.y,
                                     a.kb[j]);
 }
@@ -938,6 +948,238 @@ __global__ __launch_bounds__(256) void lora_apply_k(bf16* __restrict__ Y, int ld
   }
 }
 
+// ---- 1-4 adapters of one projection, any mix of dropout rates (BASELINE #2: q, k, v on q|k|v) ----------
+// The pair kernels above pack two rank-8 adapters into one 16-column MFMA tile; with rank-16 adapters each
+// branch is its own tile.  Forward: lora_projms_k reads x ONCE for all NBR branches (split-K like
+// lora_proj2s_k: 64 rows × 4·NS·32 of K per workgroup, all loads issued before the first MFMA), masks the
+// x fragment per branch with a bitwise AND and writes every branch's keep bits for the backward.
+struct ProjM {
+  const bf16* W[4];
+  int r[4];
+  uint64_t key[4];
+  uint32_t thr[4];
+  uint8_t* mko[4];   // keep-bit plane [M, K/8] per branch (null: not stored)
+};
+struct ProjMOut {
+  float* outf[4];
+  bf16* outb[4];
+  int ldof[4], ldob[4], r[4];
+  float sc[4];       // scale · 1/(1-p)
+  int nbr;
+};
+template <int NS, int NBR>
+__global__ __launch_bounds__(256) void lora_projms_k(const bf16* __restrict__ X, int ldx, int K, int M, ProjM p,
+                                                    size_t mask_ld, float* __restrict__ ws) {
+  constexpr int KW = NS * 32, KC = 4 * KW;
+  __shared__ f32x4 red[4][4][64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = lane >> 4, n = lane & 15;
+  const int kc = blockIdx.x, m0 = blockIdx.y * 64;
+  const int kl = kc * KC + w * KW + g * (NS * 8);
+  bf16x8 xv[4][NS], bv[NBR][NS];
+#pragma unroll
+  for (int br = 0; br < NBR; ++br) {
+    const bf16* wr = p.W[br] + (size_t)(n < p.r[br] ? n : 0) * K;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) bv[br][s] = *reinterpret_cast<const bf16x8*>(wr + kl + 8 * s);
+  }
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int row = min(m0 + 16 * b + n, M - 1);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) xv[b][s] = *reinterpret_cast<const bf16x8*>(X + (size_t)row * ldx + kl + 8 * s);
+  }
+  f32x4 acc[NBR][4];
+#pragma unroll
+  for (int br = 0; br < NBR; ++br) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      if (n >= p.r[br]) bv[br][s] = bf16x8{};
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[br][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint32_t thr = p.thr[br];
+    if (thr == 0 && !p.mko[br]) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[br][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xv[b][s], bv[br][s], acc[br][b], 0, 0, 0);
+      continue;
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int mg = m0 + 16 * b + n;
+      const int row = min(mg, M - 1);
+      uint32_t kp = 0;
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        kp |= (thr ? dropout_keep8(p.key[br], ((size_t)row * mask_ld + kl + 8 * s) >> 3, thr) : 0xFFu) << (8 * s);
+      if (p.mko[br] && mg < M) {   // NS keep bytes of the lane's row, one store
+        uint8_t* dst = p.mko[br] + (size_t)mg * (K >> 3) + (kl >> 3);
+        if constexpr (NS == 4) *reinterpret_cast<uint32_t*>(dst) = kp;
+        else if constexpr (NS == 2) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)kp;
+        else *dst = (uint8_t)kp;
+      }
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const uint32_t k8 = kp >> (8 * s);
+        const u32x4 xw = __builtin_bit_cast(u32x4, xv[b][s]);
+        u32x4 a;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          a[q] = xw[q] & (((0u - ((k8 >> (2 * q)) & 1u)) & 0xFFFFu) | ((0u - ((k8 >> (2 * q + 1)) & 1u)) << 16));
+        acc[br][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), bv[br][s], acc[br][b], 0, 0, 0);
+      }
+    }
+  }
+  // per branch: the 4 waves' K ranges meet in LDS, wave w sums row block w (D: col j = lane & 15, rows 4g + i)
+#pragma unroll
+  for (int br = 0; br < NBR; ++br) {
+    if (br) __syncthreads();
+#pragma unroll
+    for (int b = 0; b < 4; ++b) red[w][b][lane] = acc[br][b];
+    __syncthreads();
+    f32x4 t = red[0][w][lane];
+#pragma unroll
+    for (int v = 1; v < 4; ++v) t += red[v][w][lane];
+    if (n < p.r[br]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + 16 * w + 4 * g + i;
+        if (m < M) ws[((size_t)kc * M + m) * (16 * NBR) + 16 * br + n] = t[i];
+      }
+    }
+  }
+}
+
+// out_b[m, j] = sc_b · Σ_c ws[c][m][16 b + j] (fixed order), fp32 and / or bf16 per branch
+__global__ __launch_bounds__(256) void lora_projm_sum_k(const float* __restrict__ ws, int nkc, int M, ProjMOut o) {
+  const int w16 = 16 * o.nbr;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  const int m = idx / w16, c = idx % w16, b = c >> 4, j = c & 15;
+  if (m >= M || j >= o.r[b]) return;
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < nkc; c0 += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (c0 + u < nkc) v[u] += ws[((size_t)(c0 + u) * M + m) * w16 + c];
+  }
+  const float t = (((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]))) * o.sc[b];
+  if (o.outf[b]) o.outf[b][(size_t)m * o.ldof[b] + j] = t;
+  if (o.outb[b]) o.outb[b][(size_t)m * o.ldob[b] + j] = (bf16)t;
+}
+
+// backward projections g_b = s_b·dy[:, c0_b : c0_b + K_b]·B_b (Bᵀ [r_b, K_b]) of 1-4 adapters, blockIdx.y = branch
+struct ProjMulti {
+  const bf16* X[4];
+  const bf16* W[4];
+  float* out[4];
+  int K[4], r[4];
+  float scale[4];
+};
+template <int NW, int RW>
+__global__ __launch_bounds__(NW * 64) void lora_proj_multi_k(ProjMulti p, int ldx, int M) {
+  const int b = blockIdx.y;
+  lora_proj_body<NW, RW>(p.X[b], ldx, p.W[b], p.r[b], p.K[b], p.out[b], p.r[b], nullptr, 0, M, 0, 0u, 1.f, p.scale[b], 0,
+                         blockIdx.x);
+}
+
+// The adapters' input-gradient term as the dX GEMM's C matrix:
+//   C[m, k] = Σ_b keep_b[m, k]·ds_b·Σ_j g_b[m, j]·A_b[j, k]     (bf16 [M, K], 1-4 branches, r_b <= 16)
+// One MFMA per (branch, 16 k × 16 m tile): A operand = A_b columns (rows k, depth j, staged through LDS),
+// B operand = the g_b row of the lane's m (depth j = rank, 16 deep).  The MFMA rows of the two tiles of a pair are mapped
+// to k so that each lane's 2 × 4 accumulator rows are 8 CONSECUTIVE k of its m (tile h of pair P: row rr ↔
+// k = 32 P + 8 (rr / 4) + 4 h + rr % 4): the keep bits of the lane are one byte per pair, the store is 16 B.
+// A workgroup is 64 k × 4 waves × RB 16-row blocks; the A fragments are built once per workgroup and the
+// next row block's g rows / keep words are loaded before the current block is computed and stored.
+struct DxcArgs {
+  const float* g[4];
+  int ldg[4];
+  const bf16* a[4];
+  int r[4];
+  const uint8_t* keep[4];   // [M, K/8] or null (no dropout)
+  float ds[4];
+  int nbr;
+};
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+template <int RB>
+__global__ __launch_bounds__(256) void lora_dxc_k(DxcArgs d, bf16* __restrict__ out, int M, int K) {
+  __shared__ bf16 as[4][16][64 + 8];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int q = lane >> 4, c = lane & 15;
+  const int kb = blockIdx.x * 64;
+  const int nbr = d.nbr;
+  for (int idx = threadIdx.x; idx < 4 * 16 * 8; idx += 256) {   // A_b[:, kb : kb + 64] (rows >= r_b zero)
+    const int b = idx >> 7, j = (idx >> 3) & 15, cc = idx & 7;
+    bf16x8 v = {};
+    if (b < nbr && j < d.r[b]) v = *reinterpret_cast<const bf16x8*>(d.a[b] + (size_t)j * K + kb + 8 * cc);
+    *reinterpret_cast<bf16x8*>(&as[b][j][8 * cc]) = v;
+  }
+  const int mb = (blockIdx.y * 4 + w) * RB * 16;
+  // rank depth 16 = one v_mfma_f32_16x16x16_bf16: lane (q, c) holds ranks 4 q .. 4 q + 3
+  f32x4 gq[2][4];      // [row-block parity][branch]: g_b[m, 4 q .. 4 q + 3]
+  uint64_t kq[2][4];   // keep word of the lane's row over [kb, kb + 64)
+  auto load_rb = [&](int rb, int par) {
+    const int gm = min(mb + 16 * rb + c, M - 1);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      gq[par][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      kq[par][b] = ~0ull;
+      if (b < nbr) {
+        if (4 * q < d.r[b]) gq[par][b] = *reinterpret_cast<const f32x4*>(d.g[b] + (size_t)gm * d.ldg[b] + 4 * q);
+        if (d.keep[b]) kq[par][b] = *reinterpret_cast<const uint64_t*>(d.keep[b] + (size_t)gm * (K >> 3) + (kb >> 3));
+      }
+    }
+  };
+  load_rb(0, 0);
+  __syncthreads();
+  s16x4 af[4][4];   // [branch][tile 2P + h]: row rr = c ↔ k = kb + 32 P + 8 (c / 4) + 4 h + c % 4, depth j = 4 q + e
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int kl = 32 * (t >> 1) + 8 * (c >> 2) + 4 * (t & 1) + (c & 3);
+      bf16x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = b < nbr ? as[b][4 * q + e][kl] : (bf16)0.f;
+      af[b][t] = __builtin_bit_cast(s16x4, v);
+    }
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    const int par = rb & 1;
+    if (rb + 1 < RB) load_rb(rb + 1, par ^ 1);
+    const int m = mb + 16 * rb + c;
+    f32x4 v[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      if (b >= nbr) break;
+      const bf16x4 gb = {(bf16)gq[par][b][0], (bf16)gq[par][b][1], (bf16)gq[par][b][2], (bf16)gq[par][b][3]};
+      const float ds = d.ds[b];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const f32x4 p = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af[b][t], __builtin_bit_cast(s16x4, gb),
+                                                                  f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        // k = kb + 32 P + 8 q + 4 h + i: byte 4 P + q of the keep word, bit 4 h + i
+        const uint32_t bits = (uint32_t)(kq[par][b] >> (8 * (4 * (t >> 1) + q) + 4 * (t & 1))) & 15u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[t][i] += ((bits >> i) & 1u) ? p[i] * ds : 0.f;
+      }
+    }
+    if (m < M) {
+#pragma unroll
+      for (int P = 0; P < 2; ++P) {
+        bf16x8 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          o[i] = (bf16)v[2 * P][i];
+          o[i + 4] = (bf16)v[2 * P + 1][i];
+        }
+        *reinterpret_cast<bf16x8*>(out + (size_t)m * K + kb + 32 * P + 8 * q) = o;
+      }
+    }
+  }
+}
 
 }  // namespace
 
@@ -1149,18 +1391,21 @@ void launch_lora_dA_pair(const float* G0, const float* G1, int ldg, int r, const
 
 // jobs 0, 1: dB of the two branches (G = xa, X = dy column block, out [n, r] row-major);
 // jobs 2, 3: dA (G = g, X = x, out [r, K] with strides, keep bits / rescale per branch)
-void launch_lora_acc_quad(const float* const G[4], const int ldg[4], const void* const X[4], const int ldx[4],
-                          const int K[4], float* const out[4], const int64_t sj[4], const int64_t sk[4],
-                          const float ds[4], const uint8_t* const kb[4], int r, int M, hipStream_t st) {
-  AccQuad a{};
+// (any job count 1..8: the multi-adapter backward's dB / dA products go through the same launch)
+void launch_lora_acc_jobs(int njobs, const float* const* G, const int* ldg, const int* r, const void* const* X,
+                          const int* ldx, const int* K, float* const* out, const int64_t* sj, const int64_t* sk,
+                          const float* ds, const uint8_t* const* kb, int M, hipStream_t st) {
+  AccJobs a{};
+  a.njobs = njobs;
   int nb = 0;
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < njobs; ++j) {
     a.G[j] = G[j];
     a.X[j] = (const bf16*)X[j];
     a.out[j] = out[j];
     a.K[j] = K[j];
     a.ldg[j] = ldg[j];
     a.ldx[j] = ldx[j];
+    a.r[j] = r[j];
     a.sj[j] = sj[j];
     a.sk[j] = sk[j];
     a.ds[j] = ds[j];
@@ -1168,8 +1413,103 @@ void launch_lora_acc_quad(const float* const G[4], const int ldg[4], const void*
     a.nb[j] = nb;
     nb += K[j] / 128;
   }
-  dim3 g(nb, (M + 127) / 128);
-  lora_acc_quad_k<1><<<g, 256, 0, st>>>(a, r, M);
+  // rank 16 with >= 16 row blocks of 256: two 32-row steps per wave (half the fp32 atomics; BASELINE #2's
+  // q|k|v + o products 2.66 -> 2.31 ms/step, 4 steps 2.35 — profiles/r4/lora_multi_adapter.txt); rank 8
+  // keeps one (the headline's quad launch, round-2 A/B)
+  int rmax = 0;
+  for (int j = 0; j < njobs; ++j) rmax = r[j] > rmax ? r[j] : rmax;
+  const int su = rmax > 8 && (M + 255) / 256 >= 16 ? 2 : 1;
+  dim3 g(nb, (M + 128 * su - 1) / (128 * su));
+  if (su == 2) lora_acc_jobs_k<2><<<g, 256, 0, st>>>(a, M);
+  else lora_acc_jobs_k<1><<<g, 256, 0, st>>>(a, M);
+  LIPA_CHECK_LAUNCH();
+}
+
+void launch_lora_acc_quad(const float* const G[4], const int ldg[4], const void* const X[4], const int ldx[4],
+                          const int K[4], float* const out[4], const int64_t sj[4], const int64_t sk[4],
+                          const float ds[4], const uint8_t* const kb[4], int r, int M, hipStream_t st) {
+  const int rr[4] = {r, r, r, r};
+  launch_lora_acc_jobs(4, G, ldg, rr, X, ldx, K, out, sj, sk, ds, kb, M, st);
+}
+
+// N adapters sharing x: split-K projection (+ every branch's keep bits), then the fixed-order slab sum
+void launch_lora_proj_m(const void* X, int ldx, int K, int M, int nbr, const void* const* W, const int* r,
+                        const uint64_t* key, const float* p, const float* scale, uint8_t* const* mko, size_t mask_ld,
+                        float* const* outf, const int* ldof, void* const* outb, const int* ldob, float* ws,
+                        hipStream_t st) {
+  ProjM pm{};
+  ProjMOut po{};
+  po.nbr = nbr;
+  for (int b = 0; b < nbr; ++b) {
+    pm.W[b] = (const bf16*)W[b];
+    pm.r[b] = r[b];
+    pm.key[b] = key[b];
+    pm.thr[b] = p[b] > 0.f ? (uint32_t)(p[b] * 65536.0f + 0.5f) : 0u;
+    pm.mko[b] = mko[b];
+    po.r[b] = r[b];
+    po.sc[b] = scale[b] * (p[b] > 0.f ? 1.f / (1.f - p[b]) : 1.f);
+    po.outf[b] = outf[b];
+    po.ldof[b] = ldof[b];
+    po.outb[b] = (bf16*)outb[b];
+    po.ldob[b] = ldob[b];
+  }
+  const int ns = lora_proj2_ns(M, K);
+  dim3 grid(K / (128 * ns), (M + 63) / 64);
+#define P(NS_, NB_) lora_projms_k<NS_, NB_><<<grid, 256, 0, st>>>((const bf16*)X, ldx, K, M, pm, mask_ld, ws)
+#define PN(NS_) \
+  if (nbr == 1) P(NS_, 1); else if (nbr == 2) P(NS_, 2); else if (nbr == 3) P(NS_, 3); else P(NS_, 4)
+  if (ns == 4) { PN(4); } else if (ns == 2) { PN(2); } else { PN(1); }
+#undef PN
+#undef P
+  lora_projm_sum_k<<<(M * 16 * nbr + 255) / 256, 256, 0, st>>>(ws, grid.x, M, po);
+  LIPA_CHECK_LAUNCH();
+}
+int lora_proj_m_ws_floats(int M, int K, int nbr) {
+  const int ns = lora_proj2_ns(M, K);
+  return ns ? (K / (128 * ns)) * M * 16 * nbr : 0;
+}
+
+// the backward's g_b = s_b·dy[:, c0_b : c0_b + K_b]·B_b for 1-4 adapters of one projection (blockIdx.y = branch)
+void launch_lora_proj_cols(int nbr, const void* const* X, int ldx, const void* const* W, const int* r, const int* K,
+                           float* const* out, const float* scale, int M, hipStream_t st) {
+  ProjMulti pm{};
+  for (int b = 0; b < nbr; ++b) {
+    pm.X[b] = (const bf16*)X[b];
+    pm.W[b] = (const bf16*)W[b];
+    pm.r[b] = r[b];
+    pm.K[b] = K[b];
+    pm.out[b] = out[b];
+    pm.scale[b] = scale[b];
+  }
+  const int rw = M < 4096 ? 8 : 16;
+  dim3 grid((M + rw - 1) / rw, nbr);
+  if (rw == 8)
+    lora_proj_multi_k<16, 8><<<grid, 1024, 0, st>>>(pm, ldx, M);
+  else
+    lora_proj_multi_k<16, 16><<<grid, 1024, 0, st>>>(pm, ldx, M);
+  LIPA_CHECK_LAUNCH();
+}
+
+// C = Σ_b keep_b·ds_b·(g_b·A_b), bf16 [M, K] (the dX GEMM's C matrix) for 1-4 adapters
+void launch_lora_dxc(int nbr, const float* const* g, const int* ldg, const void* const* a, const int* r,
+                     const uint8_t* const* keep, const float* ds, void* out, int M, int K, hipStream_t st) {
+  DxcArgs d{};
+  d.nbr = nbr;
+  for (int b = 0; b < nbr; ++b) {
+    d.g[b] = g[b];
+    d.ldg[b] = ldg[b];
+    d.a[b] = (const bf16*)a[b];
+    d.r[b] = r[b];
+    d.keep[b] = keep[b];
+    d.ds[b] = ds[b];
+  }
+  if ((K / 64) * ((M + 255) / 256) >= 512) {
+    dim3 g4(K / 64, (M + 255) / 256);
+    lora_dxc_k<4><<<g4, 256, 0, st>>>(d, (bf16*)out, M, K);
+  } else {
+    dim3 g1(K / 64, (M + 63) / 64);
+    lora_dxc_k<1><<<g1, 256, 0, st>>>(d, (bf16*)out, M, K);
+  }
   LIPA_CHECK_LAUNCH();
 }
 

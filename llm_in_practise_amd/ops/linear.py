@@ -415,6 +415,20 @@ def _pair_ok(x, branches) -> bool:
             and os.environ.get("LIPA_LORA_PAIR", "1") != "0")
 
 
+_MULTI = os.environ.get("LIPA_LORA_MULTI", "1") != "0"
+
+
+def _multi_ok(x, branches) -> bool:
+    """1-4 adapters of rank 8 or 16 on one projection that are not the rank-8 q+v pair (BASELINE #2: q, k, v
+    on q|k|v, o alone): the multi-adapter kernels — one pass over x for every branch's s·D(x)·Aᵀ with the
+    keep bits stored (``lora_proj_m``), every g_b in one launch (``lora_proj_cols``), every dB and dA in
+    one launch (``lora_acc_jobs``), the masked dX term inside the dX GEMM (1-2 branches: gemm4w_loradx)
+    or as its C matrix (``lora_dxc``).  Training-sized M only; decode keeps the per-branch kernels."""
+    return (_MULTI and x.is_cuda and 1 <= len(branches) <= 4 and x.shape[0] >= _LT_MIN_M
+            and not _pair_ok(x, branches)
+            and all(br.a.shape[0] in (8, 16) and (br.c1 - br.c0) % 512 == 0 for br in branches))
+
+
 def _fast_lora_ok(x, branches) -> bool:
     """Shapes the fused LoRA branch kernels (csrc/kernels/lora.hip) take."""
     K = x.shape[1]
@@ -507,6 +521,17 @@ class _FusedLinearFn(torch.autograd.Function):
                 ctx.masks = masks
                 r0 = a0.shape[0]
                 xa_list = [xa2[:, :r0], xa2[:, r0:]]
+            elif _multi_ok(x, branches):
+                ps = [br.dropout if training else 0.0 for br in branches]
+                keys = [next_dropout_key() if p > 0 else None for p in ps]
+                # every branch's keep bits (an all-ones plane for a branch without dropout) for the backward
+                masks = (torch.empty(len(branches), x.shape[0], x.shape[1] // 8, dtype=torch.uint8, device=x.device)
+                         if need_xa and any(k is not None for k in keys) else None)
+                obs = [None if xa32 is None else xa32[:, kofs[i]:kofs[i] + br.a.shape[0]]
+                       for i, br in enumerate(branches)]
+                xa_list = list(native().lora_proj_m(x, [bf16_view(a, x.dtype) for a in ab[0::2]], obs, True, ps,
+                                                    [k or 0 for k in keys], [br.scaling for br in branches], masks))
+                ctx.masks = masks
             else:
                 for bi, (br, a) in enumerate(zip(branches, ab[0::2])):
                     p = br.dropout if training else 0.0
@@ -599,6 +624,9 @@ class _FusedLinearFn(torch.autograd.Function):
         ctx.keys = keys
         ctx.fast = fast
         ctx.pair = bool(branches) and fast and _pair_ok(x, branches)
+        # (the forward's condition for lora_proj_m: "apply" form and the multi-adapter shapes)
+        ctx.multi = (bool(branches) and fast and x.is_cuda and len(branches) <= 4 and _APPLY
+                     and _multi_ok(x, branches))
         ctx.ab_refs = ab          # the parameters themselves: fused kernels accumulate into their .grad
         ctx.has_residual = residual is not None
         # the LoRA parameters travel as ctx.ab_refs, not through save_for_backward: under non-reentrant
@@ -630,6 +658,9 @@ class _FusedLinearFn(torch.autograd.Function):
                 return gr, False
             return torch.zeros(prm.shape, dtype=torch.float32, device=dy.device), True
 
+        if (ctx.multi and not deterministic() and ctx.bts is not None and all(t is not None for t in xa_list)
+                and (ctx.masks is not None or all(k is None for k in ctx.keys))):
+            return _multi_backward(ctx, dy, x, weight, xa_list, base, branches, dense, dest)
         # q_proj + v_proj: both adapters' s·dy_i·B_i in one launch, both dB_i in another
         pair_g = (fast and nb == 2 and ctx.bts is not None and ctx.bts[0].shape[0] == ctx.bts[1].shape[0]
                   and all(bt.shape[1] % 512 == 0 for bt in ctx.bts) and _PAIR_BWD)
@@ -780,6 +811,63 @@ class _FusedLinearFn(torch.autograd.Function):
             dw = (dy.t() @ x).to(weight.dtype)
         dbias = dy.sum(0) if ctx.needs_input_grad[3] else None
         return (dx, dres, dw, dbias, None, *grads_ab)
+
+
+def _multi_backward(ctx, dy, x, weight, xa_list, base, branches, dense, dest):
+    """Backward of 1-4 adapters through the multi-adapter kernels (see ``_multi_ok``): 3 LoRA launches
+    (g, dB + dA, and the dX term when it cannot ride in the dX GEMM's prologue)."""
+    ab = ctx.ab_refs
+    nb = len(branches)
+    grads_ab = [None] * (2 * nb)
+    masks, ctx.masks = ctx.masks, None
+    ps = [br.dropout if k is not None else 0.0 for br, k in zip(branches, ctx.keys)]
+    g_list = native().lora_proj_cols(dy, [br.c0 for br in branches], ctx.bts, [br.scaling for br in branches])
+    ctx.bts = None
+    jobs, fin = [], []
+    for i, br in enumerate(branches):
+        if ctx.needs_input_grad[5 + 2 * i + 1]:      # dB_i [n_i, r] += dy_iᵀ·xa_i
+            o, ret = dest(2 * i + 1)
+            jobs.append((xa_list[i], dy, br.c0, br.c1 - br.c0, o, True, -1, 0.0))
+            fin.append((2 * i + 1, o, ret))
+    for i, br in enumerate(branches):
+        if ctx.needs_input_grad[5 + 2 * i]:          # dA_i [r, K] += g_iᵀ·D_i(x)
+            o, ret = dest(2 * i)
+            jobs.append((g_list[i], x, 0, x.shape[1], o, False, i, ps[i]))
+            fin.append((2 * i, o, ret))
+    if jobs:
+        cols = list(zip(*jobs))
+        native().lora_acc_jobs(list(cols[0]), list(cols[1]), list(cols[2]), list(cols[3]), list(cols[4]),
+                               list(cols[5]), masks, list(cols[6]), list(cols[7]))
+    for idx, o, ret in fin:
+        if ret:
+            grads_ab[idx] = o.to(ab[idx].dtype)
+        else:
+            _notify_grad_ready(ab[idx])
+    dx = None
+    if ctx.needs_input_grad[0]:
+        wb = ctx.wdq if ctx.wdq is not None else (base if not dense else weight)
+        a_list = [bf16_view(ab[2 * i], dy.dtype) for i in range(nb)]
+        if masks is None:    # no dropout: the adapters' g·A as an extra K-slice of the dX GEMM
+            ea = _pad_cols(torch.cat([g.to(dy.dtype) for g in g_list], 1))
+            eb = torch.cat(a_list, 0)
+            dx = _base_gemm_t(dy, wb, ea, F.pad(eb, (0, 0, 0, ea.shape[1] - eb.shape[0])).t().contiguous())
+        else:
+            fused = (_LORA_EPI and nb <= 2 and wb.shape[1] % 128 == 0
+                     and all(g.shape[1] == g_list[0].shape[1] for g in g_list))
+            if fused and isinstance(wb, torch.Tensor) and _g4w_ok(dy, wb, True):
+                dx = native().gemm4w_loradx(dy, wb, None, 0, g_list, a_list, masks, ps)
+            elif fused and isinstance(wb, NF4Weight) and _w4_ok(dy, wb, True):
+                codes, sc = wb.g4w_pack()
+                dx = native().gemm4w_loradx(dy, codes, sc, wb.shape[1], g_list, a_list, masks, ps)
+            else:
+                c = native().lora_dxc(g_list, a_list, masks, ps)
+                dx = _base_gemm_t(dy, wb, None, None, c)
+                del c
+    ctx.wdq = None
+    dres = dy if ctx.has_residual else None
+    dw = (dy.t() @ x).to(weight.dtype) if (dense and weight is not None and ctx.needs_input_grad[2]) else None
+    dbias = dy.sum(0) if ctx.needs_input_grad[3] else None
+    return (dx, dres, dw, dbias, None, *grads_ab)
 
 
 def _reference(x, base, bias, branches, residual, training):
