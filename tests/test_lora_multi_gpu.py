@@ -45,9 +45,10 @@ def test_lora_proj_m_matches_fp32(native_ext, M, K, ranks, ps):
         assert ((obs[b].float() - ref).norm() / ref.norm()) < 1e-2
 
 
-def test_lora_proj_cols_and_acc_jobs_match_fp32(native_ext):
+@pytest.mark.parametrize("M", [512, 4096])   # 4096 rows: the two-step (rank 16, >= 16 row blocks) form
+def test_lora_proj_cols_and_acc_jobs_match_fp32(native_ext, M):
     g = torch.Generator(device="cuda").manual_seed(1)
-    M, K = 512, 1024
+    K = 1024
     ncols = [1024, 512, 512]
     c0s = [0, 1024, 1536]
     dy = torch.randn(M, sum(ncols), device="cuda", generator=g).bfloat16()
