@@ -384,15 +384,25 @@ struct AccJobs {
   const uint8_t* kb[kAccJobs];
   int njobs;
 };
+// XCD-aware order: the hardware deals workgroups round-robin over the 8 XCDs (each with its own L2); the
+// logical order runs along k fastest, so the workgroups that read one row block's G rows and keep-bit lines
+// (partial 128-B lines per workgroup) sit on ONE XCD instead of pulling the same lines into all eight L2s.
+__device__ __forceinline__ void xcd_grid(int& bx, int& by) {
+  const int gx = gridDim.x, nwg = gx * gridDim.y;
+  const int lid = xcd_remap(blockIdx.y * gx + blockIdx.x, nwg);
+  bx = lid % gx;
+  by = lid / gx;
+}
 template <int SUB>
 __global__ __launch_bounds__(256) void lora_acc_jobs_k(AccJobs a, int M) {
-  const int bx0 = blockIdx.x;
+  int bx0, by;
+  xcd_grid(bx0, by);
   int j = 0;
 #pragma unroll
   for (int i = 1; i < kAccJobs; ++i)
     if (i < a.njobs && bx0 >= a.nb[i]) j = i;
   lora_acc_mfma_body<8, false, SUB>(a.G[j], a.ldg[j], a.r[j], a.X[j], a.ldx[j], nullptr, 0, nullptr, a.K[j], a.out[j],
-                                    a.sj[j], a.sk[j], M, 0, a.kb[j] ? 1u : 0u, a.ds[j], 0, bx0 - a.nb[j], blockIdx.y,
+                                    a.sj[j], a.sk[j], M, 0, a.kb[j] ? 1u : 0u, a.ds[j], 0, bx0 - a.nb[j], by,
                                     a.kb[j]);
 }
 
@@ -974,7 +984,9 @@ __global__ __launch_bounds__(256) void lora_projms_k(const bf16* __restrict__ X,
   __shared__ f32x4 red[4][4][64];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = lane >> 4, n = lane & 15;
-  const int kc = blockIdx.x, m0 = blockIdx.y * 64;
+  int kc, mbk;
+  xcd_grid(kc, mbk);   // neighbouring K chunks of a row block (their keep-bit bytes share lines) on one XCD
+  const int m0 = mbk * 64;
   const int kl = kc * KC + w * KW + g * (NS * 8);
   bf16x8 xv[4][NS], bv[NBR][NS];
 #pragma unroll
@@ -1106,7 +1118,9 @@ __global__ __launch_bounds__(256) void lora_dxc_k(DxcArgs d, bf16* __restrict__ 
   __shared__ bf16 as[4][16][64 + 8];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int q = lane >> 4, c = lane & 15;
-  const int kb = blockIdx.x * 64;
+  int bx, by;
+  xcd_grid(bx, by);   // the 64 column blocks of a row block (its g rows, keep lines) on one XCD
+  const int kb = bx * 64;
   const int nbr = d.nbr;
   for (int idx = threadIdx.x; idx < 4 * 16 * 8; idx += 256) {   // A_b[:, kb : kb + 64] (rows >= r_b zero)
     const int b = idx >> 7, j = (idx >> 3) & 15, cc = idx & 7;
@@ -1114,7 +1128,7 @@ __global__ __launch_bounds__(256) void lora_dxc_k(DxcArgs d, bf16* __restrict__ 
     if (b < nbr && j < d.r[b]) v = *reinterpret_cast<const bf16x8*>(d.a[b] + (size_t)j * K + kb + 8 * cc);
     *reinterpret_cast<bf16x8*>(&as[b][j][8 * cc]) = v;
   }
-  const int mb = (blockIdx.y * 4 + w) * RB * 16;
+  const int mb = (by * 4 + w) * RB * 16;
   // rank depth 16 = one v_mfma_f32_16x16x16_bf16: lane (q, c) holds ranks 4 q .. 4 q + 3
   f32x4 gq[2][4];      // [row-block parity][branch]: g_b[m, 4 q .. 4 q + 3]
   uint64_t kq[2][4];   // keep word of the lane's row over [kb, kb + 64)
