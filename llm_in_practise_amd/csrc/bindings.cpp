@@ -36,6 +36,7 @@ void launch_adamw8bit(int, float*, const void*, uint8_t*, uint8_t*, float*, floa
 void launch_unscale(int, void*, size_t, const float*, float*, hipStream_t);
 void launch_nf4_quantize(const void*, uint8_t*, float*, size_t, hipStream_t);
 void launch_nf4_dequant2(const uint8_t*, const float*, void*, size_t, hipStream_t);
+void launch_int4_dequant(const uint8_t*, const float*, const float*, void*, size_t, int, hipStream_t);
 int skinny_splits(int, int);
 bool lt_gemm(bool, bool, long, long, long, const void*, long, const void*, long, const void*, void*, long, int, long,
              long, long, void*, size_t, hipStream_t, bool);
@@ -545,6 +546,23 @@ Tensor w4mm(Tensor x, Tensor codes, Tensor sc2, int64_t N, int64_t gs, optional<
 }
 
 // codes [N, K/2] u8 (bnb layout), absmax fp32 [N*K/64] (decoded) → bf16 [N, K]
+// affine int4 codes [N, K/2] + fp32 scale / bias tables [N, K/g] -> bf16 [N, K] (quant/int4.py layout)
+Tensor int4_dequant(Tensor codes, Tensor sc, Tensor bi, int64_t N, int64_t K, int64_t group) {
+  CHECK_CUDA(codes);
+  CHECK_CONTIG(codes);
+  CHECK_CONTIG(sc);
+  CHECK_CONTIG(bi);
+  TORCH_CHECK(codes.scalar_type() == at::kByte && codes.numel() * 2 == N * K && K % group == 0 && group % 8 == 0,
+              "int4_dequant: codes uint8 [N, K/2], K % group, group % 8");
+  TORCH_CHECK(sc.scalar_type() == at::kFloat && bi.scalar_type() == at::kFloat && sc.numel() * group == N * K &&
+                  bi.numel() == sc.numel(), "int4_dequant: fp32 tables [N, K/g]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(codes.data_ptr()) % 4 == 0, "int4_dequant: 4-B aligned codes");
+  auto w = at::empty({N, K}, codes.options().dtype(at::kBFloat16));
+  launch_int4_dequant(codes.data_ptr<uint8_t>(), sc.data_ptr<float>(), bi.data_ptr<float>(), w.data_ptr(),
+                      (size_t)N * K, (int)group, stream());
+  return w;
+}
+
 Tensor nf4_dequant_fast(Tensor codes, Tensor absmax, int64_t N, int64_t K) {
   CHECK_CUDA(codes);
   CHECK_CONTIG(codes);
@@ -1623,6 +1641,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lora_acc_quad", &lora_acc_quad);
   m.def("lora_dx2", &lora_dx2);
   m.def("lora_proj_m", &lora_proj_m);
+  m.def("int4_dequant", &int4_dequant);
   m.def("lora_proj_cols", &lora_proj_cols);
   m.def("lora_acc_jobs", &lora_acc_jobs);
   m.def("lora_dxc", &lora_dxc);

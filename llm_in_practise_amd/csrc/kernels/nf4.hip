@@ -110,6 +110,39 @@ __global__ __launch_bounds__(256) void nf4_dequant3_k(const uint32_t* __restrict
 }
 
 
+// Affine int4 (GPTQ / AWQ, ``quant/int4.py``) → bf16 at HBM speed, the nf4_dequant3_k pattern: codes
+// [N, K/2] (per byte: element 2i = high nibble, 2i + 1 = low), w = q·s + b per group (b = −z·s), fp32
+// tables [N, K/g]; one lane per 8 elements, 4 items per lane strided by the block.  The W4A16 prefill
+// path (quant/int4.py: M >= 2048) expands each weight into a transient copy for the bf16 gemm4w.
+__global__ __launch_bounds__(256) void int4_dequant_k(const uint32_t* __restrict__ codes, const float* __restrict__ sc,
+                                                      const float* __restrict__ bi, bf16* __restrict__ w, size_t n8,
+                                                      int g8) {
+  const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x;
+  uint32_t c[4];
+  float s[4], b[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const size_t i = base + 256 * j;
+    const size_t t = i < n8 ? i / g8 : 0;
+    c[j] = i < n8 ? codes[i] : 0u;
+    s[j] = sc[t];
+    b[j] = bi[t];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const size_t i = base + 256 * j;
+    if (i >= n8) break;
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t byte = (c[j] >> (8 * e)) & 0xffu;
+      o[2 * e] = (bf16)fmaf((float)(byte >> 4), s[j], b[j]);
+      o[2 * e + 1] = (bf16)fmaf((float)(byte & 15u), s[j], b[j]);
+    }
+    *reinterpret_cast<bf16x8*>(w + i * 8) = o;
+  }
+}
+
 // bnb-layout codes → bf16 (reference / merge path)
 __global__ __launch_bounds__(256) void nf4_dequant_k(const uint8_t* __restrict__ codes, const float* __restrict__ absmax,
                                                      const uint8_t* __restrict__ qabs, const float* __restrict__ absmax2,
@@ -153,6 +186,13 @@ void launch_nf4_dequant2(const uint8_t* codes, const float* absmax, void* w, siz
   LIPA_CHECK_LAUNCH();
 }
 
+
+void launch_int4_dequant(const uint8_t* codes, const float* sc, const float* bi, void* w, size_t nelem, int group,
+                         hipStream_t st) {
+  const size_t n8 = nelem / 8;
+  int4_dequant_k<<<(n8 + 1023) / 1024, 256, 0, st>>>((const uint32_t*)codes, sc, bi, (bf16*)w, n8, group / 8);
+  LIPA_CHECK_LAUNCH();
+}
 
 void launch_nf4_dequant(const uint8_t* codes, const float* absmax, const uint8_t* qabs, const float* absmax2,
                         const float* offset, const float* dcode, void* w, size_t nelem, hipStream_t st) {

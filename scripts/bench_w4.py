@@ -59,6 +59,12 @@ def main():
                         row[f"w4mm_nkb{nkb}_us"] = round(timeit(lambda: nat.w4mm(x, q.codes, sc2, N, 128, None, nkb)), 2)
             if M > 8:
                 row["g4w_int4_us"] = round(timeit(lambda: nat.gemm4w(x, gc, None, 0, False, 0, 0, gst, N, gzt)), 2)
+            if M >= 128:   # the prefill form: one bf16 expansion + the bf16 gemm4w
+                row["expand_us"] = round(timeit(lambda: nat.int4_dequant(q.codes, sc, bi, N, K, 128)), 2)
+                row["expand_g4w_us"] = round(timeit(lambda: nat.gemm4w(x, nat.int4_dequant(q.codes, sc, bi, N, K, 128),
+                                                                    None, 0, False)), 2)
+                y = nat.gemm4w(x, nat.int4_dequant(q.codes, sc, bi, N, K, 128), None, 0, False)
+                row["expand_relerr"] = float(((y.float() - ref).norm() / ref.norm()).item())
             if M <= 8:
                 row["gemv_w4_us"] = round(timeit(lambda: nat.gemv_w4(x, q.codes, sc, bi, N, 128, None)), 2)
             print(json.dumps(row), flush=True)

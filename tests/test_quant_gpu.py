@@ -34,11 +34,23 @@ def test_int4_linear_dispatch(native_ext, N, K, gs, sym):
     (larger), the dequant fallback for shapes no kernel takes (N = 96) — against fp32, with residual."""
     torch.manual_seed(4)
     w = quantize_rtn(torch.randn(N, K, device=DEV), gs, sym)
-    for M in (1, 2, 3, 8, 32, 33, 64, 300):
+    for M in (1, 2, 3, 8, 32, 33, 64, 300, 2048):
         x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
         res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
         assert rel(int4_linear(x, w), x.float() @ w.dequantize().t()) < 1e-2, M
         assert rel(int4_linear(x, w, residual=res), x.float() @ w.dequantize().t() + res.float()) < 1e-2, M
+
+
+@pytest.mark.parametrize("N,K,gs,sym", [(256, 512, 128, False), (384, 1024, 64, True)])
+def test_int4_dequant_kernel_matches_fp32(native_ext, N, K, gs, sym):
+    """The HBM-speed int4 -> bf16 expansion (the W4A16 prefill form) against the fp32 dequantisation."""
+    torch.manual_seed(5)
+    w = quantize_rtn(torch.randn(N, K, device=DEV), gs, sym)
+    s, b = w.gemv_tables()
+    got = native_ext.int4_dequant(w.codes, s, b, N, K, gs)
+    ref = w.dequantize()
+    assert got.dtype == torch.bfloat16 and got.shape == (N, K)
+    assert (got.float() - ref).abs().max() <= 1e-2 * ref.abs().max()
 
 
 def test_awq_gptq_on_gpu_and_quantized_generation(native_ext):
