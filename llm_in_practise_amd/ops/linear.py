@@ -46,15 +46,31 @@ _LT = os.environ.get("LIPA_LT", "1") != "0"
 _LT_MIN_M = 256
 # training-sized frozen-base GEMMs (forward x·Wᵀ and backward dY·W) through the hand-written
 # one-wave-per-SIMD MFMA kernel (csrc/kernels/gemm4w.hip); LIPA_GEMM=lt: direct hipBLASLt
-_G4W = os.environ.get("LIPA_GEMM", "native") == "native"
+# Which frozen-base GEMMs run on the hand-written gemm4w (LIPA_GEMM):
+#   hybrid (default) — gemm4w where work rides inside it: the LoRA terms in its prologue (the adapters'
+#       projection forward and dX) and, inside checkpointed layers, the NF4 codes / fused SwiGLU MLP of the
+#       reference-faithful step; every plain bf16 GEMM of the tuned step (o, gate|up, down, their dX, the LM
+#       head) through hipBLASLt + the separate elementwise passes, which measured faster there: per layer
+#       1268 vs 1338 µs in isolation, headline 62.0 vs 62.8 ms/step on one box (profiles/r4/gemm_hybrid_ab.txt);
+#   native — gemm4w everywhere;   lt — hipBLASLt everywhere (no LoRA prologue).
+_GEMM_MODE = os.environ.get("LIPA_GEMM", "hybrid")
 
 
-def _g4w_ok(a: torch.Tensor, w: torch.Tensor, bt: bool) -> bool:
+def _g4w_on(lora: bool = False) -> bool:
+    if _GEMM_MODE == "native":
+        return True
+    if _GEMM_MODE == "hybrid":
+        return lora or _IN_CKPT[0] > 0
+    return False
+
+
+def _g4w_ok(a: torch.Tensor, w: torch.Tensor, bt: bool, lora: bool = False) -> bool:
     """Shapes / strides the gemm4w kernel takes for a bf16 weight: a [M, K] row-major (row stride % 8),
     w [N, K] (or [K, N] when bt) with unit inner stride, training-sized M — the same predicate the
     binding enforces (``gemm4w_supported``: K % 64, N % 8, every operand's byte extent < 4 GiB), so an
     oversized operand falls back here instead of failing in the kernel's TORCH_CHECK."""
-    if not (_G4W and a.is_cuda and a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and a.dim() == 2
+    if not (_g4w_on(lora) and a.is_cuda and a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and a.dim() == 2
             and w.dim() == 2 and a.shape[0] >= _LT_MIN_M and a.stride(1) == 1 and w.stride(1) == 1
             and a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0):
         return False
@@ -65,10 +81,10 @@ def _g4w_ok(a: torch.Tensor, w: torch.Tensor, bt: bool) -> bool:
     return bool(native().gemm4w_ok(a.shape[0], N, K, a.stride(0), w.stride(0), bt, False))
 
 
-def _w4_ok(a: torch.Tensor, q: NF4Weight, bt: bool) -> bool:
+def _w4_ok(a: torch.Tensor, q: NF4Weight, bt: bool, lora: bool = False) -> bool:
     """An NF4 base the gemm4w kernel reads as codes (K9): forward x·deq(W)ᵀ (bt=False, a [M, K_w]) or
     dX = dY·deq(W) (bt=True, a [M, N_w]); blocksize 64, both dims multiples of 64, M > 8."""
-    if not (_G4W and a.is_cuda and a.dtype == torch.bfloat16 and a.dim() == 2 and a.shape[0] > 8
+    if not (_g4w_on(lora) and a.is_cuda and a.dtype == torch.bfloat16 and a.dim() == 2 and a.shape[0] > 8
             and a.stride(1) == 1 and a.data_ptr() % 16 == 0 and q.kernel_ok()):
         return False
     n, k = q.shape
@@ -403,10 +419,10 @@ def _lora_epi_ok(x, base, wdq, weight, branches) -> bool:
             and sum(br.a.shape[0] for br in branches) <= 128):
         return False
     if wdq is not None:
-        return _g4w_ok(x, wdq, False)
+        return _g4w_ok(x, wdq, False, lora=True)
     if isinstance(base, NF4Weight):
-        return _w4_ok(x, base, False)
-    return weight is not None and not weight.requires_grad and _g4w_ok(x, weight, False)
+        return _w4_ok(x, base, False, lora=True)
+    return weight is not None and not weight.requires_grad and _g4w_ok(x, weight, False, lora=True)
 
 
 def _pair_ok(x, branches) -> bool:
@@ -629,6 +645,7 @@ class _FusedLinearFn(torch.autograd.Function):
                      and _multi_ok(x, branches))
         ctx.ab_refs = ab          # the parameters themselves: fused kernels accumulate into their .grad
         ctx.has_residual = residual is not None
+        ctx.ckpt = _IN_CKPT[0] > 0     # hybrid GEMM mode: a checkpointed layer's backward keeps gemm4w too
         # the LoRA parameters travel as ctx.ab_refs, not through save_for_backward: under non-reentrant
         # checkpointing every saved tensor costs a Python pack / unpack hook (host time of the
         # reference-faithful step), and parameters need no saving
@@ -638,6 +655,16 @@ class _FusedLinearFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        if ctx.ckpt and _GEMM_MODE == "hybrid":
+            _IN_CKPT[0] += 1
+            try:
+                return _FusedLinearFn._backward(ctx, dy)
+            finally:
+                _IN_CKPT[0] -= 1
+        return _FusedLinearFn._backward(ctx, dy)
+
+    @staticmethod
+    def _backward(ctx, dy):
         base, branches, training = ctx.meta
         saved = ctx.saved_tensors
         x, weight = saved[0], saved[1]
@@ -742,10 +769,10 @@ class _FusedLinearFn(torch.autograd.Function):
                 p0, p1 = branches[0].dropout, branches[1].dropout
                 fused_ok = (_LORA_EPI and wb.shape[1] % 128 == 0 and all(g.shape[1] % 8 == 0 and g.shape[1] <= 32
                                                                            for g in g_list))
-                if fused_ok and isinstance(wb, torch.Tensor) and _g4w_ok(dy, wb, True):
+                if fused_ok and isinstance(wb, torch.Tensor) and _g4w_ok(dy, wb, True, lora=True):
                     # the masked LoRA input gradient inside the dX GEMM's epilogue (no lora_dx2 matrix)
                     dx = native().gemm4w_loradx(dy, wb, None, 0, g_list, [a0, a1], ctx.masks, [p0, p1])
-                elif fused_ok and isinstance(wb, NF4Weight) and _w4_ok(dy, wb, True):
+                elif fused_ok and isinstance(wb, NF4Weight) and _w4_ok(dy, wb, True, lora=True):
                     codes, sc = wb.g4w_pack()
                     dx = native().gemm4w_loradx(dy, codes, sc, wb.shape[1], g_list, [a0, a1], ctx.masks, [p0, p1])
                 else:
@@ -854,9 +881,9 @@ def _multi_backward(ctx, dy, x, weight, xa_list, base, branches, dense, dest):
         else:
             fused = (_LORA_EPI and nb <= 2 and wb.shape[1] % 128 == 0
                      and all(g.shape[1] == g_list[0].shape[1] for g in g_list))
-            if fused and isinstance(wb, torch.Tensor) and _g4w_ok(dy, wb, True):
+            if fused and isinstance(wb, torch.Tensor) and _g4w_ok(dy, wb, True, lora=True):
                 dx = native().gemm4w_loradx(dy, wb, None, 0, g_list, a_list, masks, ps)
-            elif fused and isinstance(wb, NF4Weight) and _w4_ok(dy, wb, True):
+            elif fused and isinstance(wb, NF4Weight) and _w4_ok(dy, wb, True, lora=True):
                 codes, sc = wb.g4w_pack()
                 dx = native().gemm4w_loradx(dy, codes, sc, wb.shape[1], g_list, a_list, masks, ps)
             else:

@@ -25,7 +25,7 @@ import torch
 
 from ..quant.nf4 import NF4Weight
 from ._native import native
-from .linear import _G4W, _LT_MIN_M, _nf4_expand, _nf4_w4, sac_put, sac_take
+from .linear import _LT_MIN_M, _g4w_on, _nf4_expand, _nf4_w4, sac_put, sac_take
 
 
 def _operand(base, reused: bool):
@@ -38,7 +38,7 @@ def _operand(base, reused: bool):
 
 
 def fusable(x: torch.Tensor, gu_base, down_base, F: int, K: int) -> bool:
-    if not (_G4W and x.is_cuda and x.dtype == torch.bfloat16 and F % 64 == 0 and K % 64 == 0):
+    if not (_g4w_on() and x.is_cuda and x.dtype == torch.bfloat16 and F % 64 == 0 and K % 64 == 0):
         return False
     if x.numel() // x.shape[-1] < _LT_MIN_M:
         return False
