@@ -49,8 +49,8 @@ _LT_MIN_M = 256
 # Which frozen-base GEMMs run on the hand-written gemm4w (LIPA_GEMM):
 #   hybrid (default) — gemm4w where work rides inside it: the LoRA terms in its prologue (the adapters'
 #       projection forward and dX) and, inside checkpointed layers, the NF4 codes / fused SwiGLU MLP of the
-#       reference-faithful step; every plain bf16 GEMM of the tuned step (o, gate|up, down, their dX, the LM
-#       head) through hipBLASLt + the separate elementwise passes, which measured faster there: per layer
+#       reference-faithful step, and the LM head (ops/loss.py); every other plain bf16 GEMM of the tuned step
+#       (o, gate|up, down, their dX) through hipBLASLt + the separate elementwise passes, faster there: per layer
 #       1268 vs 1338 µs in isolation, headline 62.0 vs 62.8 ms/step on one box (profiles/r4/gemm_hybrid_ab.txt);
 #   native — gemm4w everywhere;   lt — hipBLASLt everywhere (no LoRA prologue).
 _GEMM_MODE = os.environ.get("LIPA_GEMM", "hybrid")

@@ -39,12 +39,15 @@ class _FusedLinearCEFn(torch.autograd.Function):
         loss = torch.zeros((), dtype=torch.float32, device=h.device)
         for s in range(0, T, chunk):
             hc = h[s:s + chunk]
-            g4w = _g4w_ok(hc, weight, False)
+            # the LM head keeps gemm4w under the hybrid GEMM default (lora=True: "gemm4w on"): tie with the
+            # library at the tuned step's 2048 rows, ~2 ms/step faster at the faithful micro-step's 1024
+            # (profiles/r4/gemm_hybrid_ab.txt)
+            g4w = _g4w_ok(hc, weight, False, lora=True)
             logits = native().gemm4w(hc, weight, None, 0, False) if g4w else hc @ weight.t()
             g0, g1 = s // rows_g, (s + hc.shape[0]) // rows_g
             row_loss = native().ce_fwd_bwd(logits, labels[s:s + chunk], ignore_index, inv[g0:g1])
             loss += (row_loss.view(g1 - g0, -1).sum(1) * inv[g0:g1]).sum()
-            if g4w and _g4w_ok(logits, weight, True):
+            if g4w and _g4w_ok(logits, weight, True, lora=True):
                 dhc = native().gemm4w(logits, weight, None, 0, True)
                 if hc.shape[0] == T:
                     dh = dhc
