@@ -31,6 +31,7 @@ from llm_in_practise_amd.optim.adamw import LRScheduler, build_optimizer  # noqa
 from llm_in_practise_amd.parallel import dist as D  # noqa: E402
 from llm_in_practise_amd.parallel.ddp import DistributedDataParallel  # noqa: E402
 from llm_in_practise_amd.peft.lora import LoraConfig, get_peft_model, quantize_model_nf4  # noqa: E402
+from llm_in_practise_amd.utils.gc_control import ManualGC  # noqa: E402
 
 BASELINE_TOKENS_PER_S = None   # the reference publishes no fine-tune throughput
 MODEL_NAMES = {"qwen3-8b": "Qwen3-8B", "qwen3-14b": "Qwen3-14B", "qwen3-4b": "Qwen3-4B",
@@ -218,9 +219,11 @@ def main():
     sync()
     if device.type == "cuda":     # peak HBM of the training steps (not of building / quantising the model)
         torch.cuda.reset_peak_memory_stats(device)
+    gcm = ManualGC().__enter__()    # automatic Python GC off, a full pass every LIPA_GC_INTERVAL steps (utils/gc_control.py)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
+        gcm.step()
     sync()
     elapsed = D.all_reduce_max(time.perf_counter() - t0)
     ms = 1000 * elapsed / max(1, args.steps)
@@ -249,6 +252,7 @@ def main():
         tf0 = time.perf_counter()
         for _ in range(args.faithful_steps):
             floss = step(fused=0)
+            gcm.step()
         sync()
         fel = D.all_reduce_max(time.perf_counter() - tf0)
         fms = 1000 * fel / args.faithful_steps
@@ -262,6 +266,7 @@ def main():
                     "gradient_checkpointing_kwargs": {"use_reentrant": bool(args.ckpt_reentrant)},
                     "checkpoint_policy": args.ckpt_policy,
                     "micro_batch": args.micro_batch, "grad_accum": args.grad_accum, "peak_hbm_gib": round(fmem, 1)}
+    gcm.__exit__(None, None, None)
     if D.is_main():
         rec = {
             "metric": f"tokens/sec (whole node) {MODEL_NAMES.get(args.model, args.model)} "

@@ -42,6 +42,7 @@ import torch.nn as nn
 from ..optim.adamw import LRScheduler, build_optimizer
 from ..parallel import dist as D
 from ..utils.faults import FaultInjector
+from ..utils.gc_control import ManualGC
 from ..utils.logging import get_logger
 from ..utils.metrics import MetricsWriter
 from ..utils.timer import StepTimer
@@ -543,6 +544,7 @@ class Trainer:
             self.log.info(f"***** Running training ***** examples={n} epochs={self.state.num_train_epochs} "
                           f"micro={bs} GA={ga} world={self.world} total_steps={total} fused_ga={fused} "
                           f"strategy={'zero' + str(self.engine.stage) if self.engine else 'ddp' if self.ddp else 'single'}")
+        gcm = ManualGC().__enter__()   # automatic Python GC off; a full pass every LIPA_GC_INTERVAL steps
         try:
             for epoch in range(start_epoch, self.state.num_train_epochs):
                 it = self.get_train_batches(epoch, skip=skip_batches if epoch == start_epoch else 0)
@@ -558,6 +560,7 @@ class Trainer:
                     loss = self._micro_step(group, fused and all(isinstance(b, dict) for b in group)
                                             and len({tuple(b["input_ids"].shape) for b in group}) == 1)
                     gn = self._optimizer_step()
+                    gcm.step()
                     self.state.global_step += 1
                     self.state.epoch = epoch + (self.state.global_step - epoch * steps_per_epoch) / steps_per_epoch
                     log_loss = log_loss + loss
@@ -586,6 +589,8 @@ class Trainer:
         except BaseException:
             self._interrupt_dir = a.output_dir.rstrip("/") + "_interrupted"
             raise
+        finally:
+            gcm.__exit__(None, None, None)
         if log_n:
             tr_loss_sum += float(log_loss)
             tr_loss_n += log_n
