@@ -1517,7 +1517,14 @@ void launch_lora_dxc(int nbr, const float* const* g, const int* ldg, const void*
     d.keep[b] = keep[b];
     d.ds[b] = ds[b];
   }
-  if ((K / 64) * ((M + 255) / 256) >= 512) {
+  static const int rbx = getenv("LIPA_TMP_DXC_RB") ? atoi(getenv("LIPA_TMP_DXC_RB")) : 4;   // A/B only
+  if (rbx == 2 && (K / 64) * ((M + 127) / 128) >= 512) {
+    dim3 g2(K / 64, (M + 127) / 128);
+    lora_dxc_k<2><<<g2, 256, 0, st>>>(d, (bf16*)out, M, K);
+  } else if (rbx == 8 && (K / 64) * ((M + 511) / 512) >= 256) {
+    dim3 g8(K / 64, (M + 511) / 512);
+    lora_dxc_k<8><<<g8, 256, 0, st>>>(d, (bf16*)out, M, K);
+  } else if (rbx != 1 && (K / 64) * ((M + 255) / 256) >= 512) {
     dim3 g4(K / 64, (M + 255) / 256);
     lora_dxc_k<4><<<g4, 256, 0, st>>>(d, (bf16*)out, M, K);
   } else {
