@@ -110,7 +110,7 @@ int lora_proj_m_ws_floats(int, int, int);
 void launch_lora_proj_cols(int, const void* const*, int, const void* const*, const int*, const int*, float* const*,
                            const float*, int, hipStream_t);
 void launch_lora_dxc(int, const float* const*, const int*, const void* const*, const int*, const uint8_t* const*,
-                     const float*, void*, int, int, hipStream_t);
+                     const float*, void*, int, int, int, hipStream_t);
 void launch_lora_dx2(const float*, const float*, int, const void*, const void*, int, int, const uint8_t*,
                      const uint8_t*, float, float, void*, int, int, hipStream_t);
 void launch_lora_apply(void*, int, int, int, const float* const*, const int*, const void* const*, void* const*, const int*, const int*,
@@ -1345,7 +1345,8 @@ void lora_acc_jobs(std::vector<Tensor> gs, std::vector<Tensor> xs, std::vector<i
 }
 
 // C = Σ_b keep_b·ds_b·(g_b·A_b) bf16 [M, K] for 1-4 adapters (masks [nbr, M, K/8] or None; ps_b = 0: no mask)
-Tensor lora_dxc(std::vector<Tensor> gs, std::vector<Tensor> as, optional<Tensor> masks, std::vector<double> ps) {
+Tensor lora_dxc(std::vector<Tensor> gs, std::vector<Tensor> as, optional<Tensor> masks, std::vector<double> ps,
+                int64_t rb) {
   const int nbr = (int)gs.size();
   TORCH_CHECK(nbr >= 1 && nbr <= 4 && (int)as.size() == nbr && (int)ps.size() == nbr, "lora_dxc: 1..4 branches");
   const int64_t M = gs[0].size(0), K = as[0].size(1);
@@ -1373,7 +1374,7 @@ Tensor lora_dxc(std::vector<Tensor> gs, std::vector<Tensor> as, optional<Tensor>
     ds[b] = ps[b] > 0 ? (float)(1.0 / (1.0 - ps[b])) : 1.f;
   }
   Tensor out = at::empty({M, K}, as[0].options());
-  launch_lora_dxc(nbr, g, ldg, a, r, kb, ds, out.data_ptr(), (int)M, (int)K, stream());
+  launch_lora_dxc(nbr, g, ldg, a, r, kb, ds, out.data_ptr(), (int)M, (int)K, (int)rb, stream());
   return out;
 }
 
@@ -1644,7 +1645,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("int4_dequant", &int4_dequant);
   m.def("lora_proj_cols", &lora_proj_cols);
   m.def("lora_acc_jobs", &lora_acc_jobs);
-  m.def("lora_dxc", &lora_dxc);
+  m.def("lora_dxc", &lora_dxc, py::arg("gs"), py::arg("as"), py::arg("masks"), py::arg("ps"), py::arg("rb") = 0);
   m.def("lora_apply", &lora_apply);
   m.def("gemv_w4", &gemv_w4);
   m.def("sample", &sample);

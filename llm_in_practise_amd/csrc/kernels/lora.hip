@@ -1505,8 +1505,9 @@ void launch_lora_proj_cols(int nbr, const void* const* X, int ldx, const void* c
 }
 
 // C = Σ_b keep_b·ds_b·(g_b·A_b), bf16 [M, K] (the dX GEMM's C matrix) for 1-4 adapters
+// rows per wave (16-row blocks): rb = 0 picks 4 when that still gives >= 512 workgroups, else 1
 void launch_lora_dxc(int nbr, const float* const* g, const int* ldg, const void* const* a, const int* r,
-                     const uint8_t* const* keep, const float* ds, void* out, int M, int K, hipStream_t st) {
+                     const uint8_t* const* keep, const float* ds, void* out, int M, int K, int rb, hipStream_t st) {
   DxcArgs d{};
   d.nbr = nbr;
   for (int b = 0; b < nbr; ++b) {
@@ -1517,7 +1518,7 @@ void launch_lora_dxc(int nbr, const float* const* g, const int* ldg, const void*
     d.keep[b] = keep[b];
     d.ds[b] = ds[b];
   }
-  static const int rbx = getenv("LIPA_TMP_DXC_RB") ? atoi(getenv("LIPA_TMP_DXC_RB")) : 4;   // A/B only
+  const int rbx = rb > 0 ? rb : 4;
   if (rbx == 2 && (K / 64) * ((M + 127) / 128) >= 512) {
     dim3 g2(K / 64, (M + 127) / 128);
     lora_dxc_k<2><<<g2, 256, 0, st>>>(d, (bf16*)out, M, K);

@@ -61,8 +61,8 @@ def acc1():
     ext.lora_acc_jobs([xa1[0], gl1[0]], [dyo, xo], [0, 0], [K, K], [dB1, dA1], [True, False], masks1, [-1, 0], [0.0, p])
 
 
-def dxc3():
-    return ext.lora_dxc(list(gl3), A3, masks3, [p] * 3)
+def dxc3(rb=0):
+    return ext.lora_dxc(list(gl3), A3, masks3, [p] * 3, rb)
 
 
 MB = 1 << 20
@@ -74,7 +74,8 @@ cases = [  # name, fn, compulsory bytes
     ("acc_jobs q|k|v (3 dB + 3 dA)", acc3, M * sum(cols) * 2 + 3 * M * K * 2 + 3 * M * K // 8),
     ("acc_jobs o (dB + dA)", acc1, 2 * M * K * 2 + M * K // 8),
     ("dxc q|k|v (C bf16 [M, K])", dxc3, M * K * 2 + 3 * M * K // 8 + 3 * M * r * 4),
-]
+] + [(f"dxc q|k|v rows/wave {16 * rb}", (lambda rb=rb: dxc3(rb)), M * K * 2 + 3 * M * K // 8 + 3 * M * r * 4)
+     for rb in (1, 2, 4, 8)]
 
 
 def timeit(fn, it=20):

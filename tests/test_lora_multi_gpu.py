@@ -90,14 +90,15 @@ def test_lora_dxc_matches_fp32(native_ext, M, K, nbr):
     As = [(torch.randn(16, K, device="cuda", generator=g) * 0.05).bfloat16() for _ in range(nbr)]
     ps = [0.05, 0.0, 0.2, 0.1][:nbr]
     masks = torch.randint(0, 256, (nbr, M, K // 8), dtype=torch.uint8, device="cuda", generator=g)
-    c = native_ext.lora_dxc(gs, As, masks, ps)
     ref = torch.zeros(M, K, device="cuda")
     for b in range(nbr):
         t = gs[b] @ As[b].float()
         if ps[b] > 0:
             t = t * _unpack(masks[b], K) / (1 - ps[b])
         ref += t
-    assert ((c.float() - ref).norm() / ref.norm()) < 1e-2
+    for rb in (0, 1, 2, 4, 8):      # rows per wave (each form falls back to 1 where it would under-fill)
+        c = native_ext.lora_dxc(gs, As, masks, ps, rb)
+        assert ((c.float() - ref).norm() / ref.norm()) < 1e-2, rb
 
 
 @pytest.mark.parametrize("nbr", [3, 1])
