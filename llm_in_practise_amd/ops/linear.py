@@ -439,7 +439,8 @@ def _multi_ok(x, branches) -> bool:
     on q|k|v, o alone): the multi-adapter kernels — one pass over x for every branch's s·D(x)·Aᵀ with the
     keep bits stored (``lora_proj_m``), every g_b in one launch (``lora_proj_cols``), every dB and dA in
     one launch (``lora_acc_jobs``), the masked dX term inside the dX GEMM (1-2 branches: gemm4w_loradx)
-    or as its C matrix (``lora_dxc``).  Training-sized M only; decode keeps the per-branch kernels."""
+    or as its C matrix (``lora_dxc``).  Training-sized M only; decode keeps the per-branch kernels.
+    Reference config: ``Fine-Tuning/qwen3-8b-lora.py:128-141`` (r 16 / alpha 32 / dropout 0.05 on q, k, v, o)."""
     return (_MULTI and x.is_cuda and 1 <= len(branches) <= 4 and x.shape[0] >= _LT_MIN_M
             and not _pair_ok(x, branches)
             and all(br.a.shape[0] in (8, 16) and (br.c1 - br.c0) % 512 == 0 for br in branches))
