@@ -84,7 +84,10 @@ def _g4w_ok(a: torch.Tensor, w: torch.Tensor, bt: bool, lora: bool = False) -> b
 def _w4_ok(a: torch.Tensor, q: NF4Weight, bt: bool, lora: bool = False) -> bool:
     """An NF4 base the gemm4w kernel reads as codes (K9): forward x·deq(W)ᵀ (bt=False, a [M, K_w]) or
     dX = dY·deq(W) (bt=True, a [M, N_w]); blocksize 64, both dims multiples of 64, M > 8."""
-    if not (_g4w_on(lora) and a.is_cuda and a.dtype == torch.bfloat16 and a.dim() == 2 and a.shape[0] > 8
+    # (LIPA_NF4_GEMM=w4, the memory-lean mode, keeps every NF4 GEMM on the codes whatever the GEMM mode: the
+    # library cannot read them, and expanding would undo the mode)
+    if not (_g4w_on(lora or _NF4_MODE == "w4") and a.is_cuda and a.dtype == torch.bfloat16 and a.dim() == 2
+            and a.shape[0] > 8
             and a.stride(1) == 1 and a.data_ptr() % 16 == 0 and q.kernel_ok()):
         return False
     n, k = q.shape
