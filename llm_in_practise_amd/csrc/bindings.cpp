@@ -786,7 +786,8 @@ Tensor gemm4w_lora(Tensor x, Tensor w, optional<Tensor> wscale, int64_t n_w4, op
 // gradient added in the gemm4w dX epilogue: no lora_dx2 matrix, no C read).  g_b fp32 [M, r_b] (row stride
 // >= r_b), A_b bf16 [r_b, N] (r_b <= 32), masks uint8 [2, M, N/8] keep bits (None: no dropout), ds_b = 1/(1-p_b).
 Tensor gemm4w_loradx(Tensor dy, Tensor w, optional<Tensor> wscale, int64_t n_w4, std::vector<Tensor> gs,
-                     std::vector<Tensor> as, optional<Tensor> masks, std::vector<double> ps) {
+                     std::vector<Tensor> as, optional<Tensor> masks, std::vector<double> ps, int64_t bn_req,
+                     int64_t bm_req) {
   CHECK_BF16(dy);
   TORCH_CHECK(dy.dim() == 2 && dy.stride(1) == 1, "gemm4w_loradx: dy 2-D");
   const bool w4 = wscale && wscale->defined();
@@ -825,7 +826,9 @@ Tensor gemm4w_loradx(Tensor dy, Tensor w, optional<Tensor> wscale, int64_t n_w4,
     for (int i = 0; i < nbr; ++i) ld.keep[i] = masks->data_ptr<uint8_t>() + (size_t)i * M * (N / 8);
   }
   int bn = 0, bm = 0;
-  gemm4w_plan(M, N, K, true, 0, 1, &bn, 0, &bm, w4);
+  TORCH_CHECK((bn_req == 0 || bn_req == 128 || bn_req == 256) && (bm_req == 0 || bm_req == 128 || bm_req == 256),
+              "gemm4w_loradx: bn / bm 0 (plan), 128 or 256");
+  gemm4w_plan(M, N, K, true, (int)bn_req, 1, &bn, (int)bm_req, &bm, w4);
   auto dx = at::empty({M, N}, dy.options());
   launch_gemm4w_loradx(dy.data_ptr(), dy.stride(0), b.ptr, b.ld, b.scale, nullptr, dx.data_ptr(), ld, M, N, K, bn, bm,
                        stream());
@@ -1666,7 +1669,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm4w_ok", &gemm4w_ok);
   m.def("g4w_pack", &g4w_pack);
   m.def("gemm4w_lora", &gemm4w_lora);
-  m.def("gemm4w_loradx", &gemm4w_loradx);
+  m.def("gemm4w_loradx", &gemm4w_loradx, py::arg("dy"), py::arg("w"), py::arg("wscale"), py::arg("n_w4"), py::arg("gs"),
+        py::arg("as"), py::arg("masks"), py::arg("ps"), py::arg("bn") = 0, py::arg("bm") = 0);
   m.def("gemm4w", &gemm4w, py::arg("x"), py::arg("w"), py::arg("residual") = py::none(), py::arg("splits") = 0,
         py::arg("bt") = false, py::arg("bn") = 0, py::arg("bm") = 0, py::arg("wscale") = py::none(),
         py::arg("n_w4") = 0, py::arg("wzero") = py::none());

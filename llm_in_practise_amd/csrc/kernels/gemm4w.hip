@@ -652,10 +652,20 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
         for (int b = 0; b < 2; ++b) {
           if (b >= ldx.nbr) break;
           const float* gp = ldx.g[b] + (size_t)m * ldx.ldg + (kq < ldx.r[b] ? kq : 0);
-          lga[b][i] = gload16_u(gp);
-          lgb[b][i] = gload16_u(gp + 4);
           // keep bits: 16 B = the lane's row over [n0 + wc·BN/2, + 128) (BN/2 ≤ 128 columns)
-          lkeep[b][i] = gload16_u(ldx.keep[b] + (size_t)m * (N >> 3) + min(kb0, (N >> 3) - 16));
+          const unsigned char* kp = ldx.keep[b] + (size_t)m * (N >> 3) + min(kb0, (N >> 3) - 16);
+          if constexpr (W4) {
+            // W4: the codes prologue below drains the vector-memory queue right away (nothing to overlap),
+            // and at the 256-row tile its register pressure made hipcc copy in-flight asm-load destinations
+            // (wrong dX at M = 2048): compiler-tracked loads here
+            lga[b][i] = *reinterpret_cast<const u32x4*>(gp);
+            lgb[b][i] = *reinterpret_cast<const u32x4*>(gp + 4);
+            lkeep[b][i] = *reinterpret_cast<const u32x4*>(kp);
+          } else {
+            lga[b][i] = gload16_u(gp);
+            lgb[b][i] = gload16_u(gp + 4);
+            lkeep[b][i] = gload16_u(kp);
+          }
         }
       }
       __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
