@@ -1,7 +1,8 @@
 """The kept opt-in variants stay numerically equivalent to the default path, so their A/B records
 (profiles/) compare like with like: the unfused SwiGLU MLP (LIPA_FUSED_MLP=0) and
 hipBLASLt in place of every hand-written gemm4w GEMM (LIPA_GEMM=lt) and gemm4w for every one (LIPA_GEMM=native;
-the default, hybrid, keeps it where the LoRA terms ride in the GEMM).  Each runs the bench step on a small Qwen3 in a
+the default, hybrid, keeps it where the LoRA terms ride in the GEMM), and the memory-lean NF4 mode that
+feeds every NF4 GEMM the 4-bit codes (LIPA_NF4_GEMM=w4).  Each runs the bench step on a small Qwen3 in a
 subprocess (the switches are read once per process).  The measured-slower scheduling variants of
 round 2 (side-stream LoRA projection, two-stream attention backward, background NF4 expansion,
 deferred attention max, multi-adapter dx-as-C) were deleted; their records stay in profiles/."""
@@ -31,7 +32,8 @@ def base_losses():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{"LIPA_FUSED_MLP": "0"}, {"LIPA_GEMM": "lt"}, {"LIPA_GEMM": "native"}],
+@pytest.mark.parametrize("env", [{"LIPA_FUSED_MLP": "0"}, {"LIPA_GEMM": "lt"}, {"LIPA_GEMM": "native"},
+                                 {"LIPA_NF4_GEMM": "w4"}],
                          ids=lambda e: ",".join(e))
 def test_opt_in_schedule_matches_default(base_losses, env):
     got = _losses(env)
