@@ -83,6 +83,67 @@ def build(args, device):
     return cfg, pm
 
 
+def zero3_subrecord(args, device, rank: int, world: int, sync) -> dict:
+    """BASELINE config #4 at world > 1: ``Fine-Tuning/qwen3-14b-qlora-dist-deepspeed.py:164`` + ``ds_zero3_config.json``
+    — the QLoRA model (--zero3-model, Qwen3-14B by default) on the ZeRO-3 engine, the client paged 8-bit AdamW on
+    each rank's partition, the same micro-batch / GA / sequence length as the headline, GA micro-batches fused
+    into one pass (identical gradient).  Timed like the headline (barrier + synchronize on both sides, max over
+    ranks) with the per-step collective record (all-gathers, reduce-scatters)."""
+    import gc
+    from llm_in_practise_amd.parallel.zero import ZeroEngine
+    gc.collect()
+    if device.type == "cuda":
+        torch.cuda.empty_cache()
+    sub = argparse.Namespace(**vars(args))
+    sub.model = args.zero3_model or ("qwen3-14b" if device.type == "cuda" else args.model)
+    cfg, model = build(sub, device)
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "configs", "ds_zero3_config.json")
+    with open(path) as f:
+        ds = json.load(f)
+    ds["gradient_accumulation_steps"] = 1
+    ds["train_micro_batch_size_per_gpu"] = args.micro_batch * args.grad_accum
+    ds["train_batch_size"] = args.micro_batch * args.grad_accum * world
+    warm = 1
+    engine = ZeroEngine(model, ds, lr=args.lr, weight_decay=0.0, hidden_size=cfg.hidden_size,
+                        total_steps=warm + args.zero3_steps, optim=args.optim)
+    gen = torch.Generator(device=device).manual_seed(2000 + rank)
+    data = torch.randint(0, cfg.vocab_size, (args.micro_batch * args.grad_accum, args.seq_len), device=device,
+                         generator=gen)
+
+    def step():
+        out = engine.module(data, labels=data, num_micro_batches=args.grad_accum)
+        engine.backward(out.loss)
+        loss = out.loss.detach()
+        del out
+        engine.step()
+        return loss
+
+    for _ in range(warm):
+        step()
+    sync()
+    if device.type == "cuda":
+        torch.cuda.reset_peak_memory_stats(device)
+    D.COMM.reset()
+    D.COMM.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(args.zero3_steps):
+        loss = step()
+        D.COMM.step()
+    sync()
+    el = D.all_reduce_max(time.perf_counter() - t0)
+    D.COMM.enabled = False
+    ms = 1000 * el / args.zero3_steps
+    tps = args.micro_batch * args.seq_len * args.grad_accum * world * args.zero3_steps / el
+    mem = torch.cuda.max_memory_allocated(device) / 2 ** 30 if device.type == "cuda" else 0.0
+    log(f"[bench] zero3 {sub.model}: loss={loss.item():.4f} {ms:.1f} ms/step {tps:,.0f} tok/s peak HBM {mem:.1f} GiB")
+    return {"model": MODEL_NAMES.get(sub.model, sub.model), "value": round(tps, 1), "unit": "tokens/s",
+            "ms_per_step": round(ms, 2), "steps": args.zero3_steps, "warmup": warm, "n_gpus": world,
+            "parallelism": f"zero3-dp{world}", "ds_config": "configs/ds_zero3_config.json",
+            "optimizer": f"zero3-{engine.optim_name}", "global_batch": args.micro_batch * args.grad_accum * world,
+            "ga_execution": "fused-pass", "peak_hbm_gib": round(mem, 1),
+            "dist_backend": torch.distributed.get_backend(), "comm": D.COMM.summary()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -116,16 +177,29 @@ def main():
     ap.add_argument("--faithful-warmup", type=int, default=2)
     ap.add_argument("--ckpt-reentrant", type=int, default=0,
                     help="checkpoint form of the faithful sub-record (the reference passes use_reentrant=False)")
-    ap.add_argument("--ckpt-policy", default="selective", choices=["selective", "full"],
-                    help="recompute policy of the faithful sub-record: selective = GEMM outputs recorded in the "
-                         "first forward, norms / RoPE / attention recomputed; full = the whole layer (HF)")
-    ap.add_argument("--nf4-gemm", default="auto", choices=["auto", "w4", "expand"],
+    ap.add_argument("--ckpt-policy", default="full", choices=["selective", "full"],
+                    help="recompute policy of --grad-ckpt (the faithful sub-record is always full): full = the whole layer "
+                         "recomputed in backward (HF gradient_checkpointing, the reference); selective = GEMM outputs "
+                         "recorded in the first forward, norms / RoPE / attention recomputed")
+    ap.add_argument("--nf4-gemm", default=None, choices=["auto", "w4", "expand"],
                     help="NF4 base GEMM form (ops/linear.py _nf4_w4): auto = one bf16 expansion per step where the copy "
                          "is reused (forward + dX), the in-kernel NF4 dequant-GEMM elsewhere; w4 = the NF4 dequant-GEMM "
-                         "everywhere (no bf16 copy of the base: the memory-lean QLoRA step); expand = always expand")
+                         "everywhere (no bf16 copy of the base: the memory-lean QLoRA step); expand = always expand "
+                         "(default: LIPA_NF4_GEMM, else auto)")
+    ap.add_argument("--zero3-steps", type=int, default=3,
+                    help="world > 1 (ddp strategy): after the headline, also time this many steps of BASELINE config #4 "
+                         "(--zero3-model QLoRA on the ZeRO-3 engine with configs/ds_zero3_config.json, same GA / optimizer) "
+                         "as the 'zero3' sub-record, with its per-step collective record (0: skip)")
+    ap.add_argument("--zero3-model", default=None,
+                    help="model of the zero3 sub-record (default: qwen3-14b on GPUs, the headline model on CPU)")
+    ap.add_argument("--selective-steps", type=int, default=3,
+                    help="after the faithful sub-record, time this many steps with the selective recompute policy "
+                         "(GEMM outputs of the first forward kept, not recomputed) as the 'selective_ckpt' sub-record")
     args = ap.parse_args()
     from llm_in_practise_amd.ops import linear as _lin
-    _lin._NF4_MODE = args.nf4_gemm
+    if args.nf4_gemm is not None:        # else the LIPA_NF4_GEMM environment choice stands
+        _lin._NF4_MODE = args.nf4_gemm
+    args.nf4_gemm = _lin._NF4_MODE
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `python bench.py --gpus N` without a launcher: start N ranks under torch.distributed.run
@@ -220,12 +294,17 @@ def main():
     if device.type == "cuda":     # peak HBM of the training steps (not of building / quantising the model)
         torch.cuda.reset_peak_memory_stats(device)
     gcm = ManualGC().__enter__()    # automatic Python GC off, a full pass every LIPA_GC_INTERVAL steps (utils/gc_control.py)
+    D.COMM.reset()
+    D.COMM.enabled = world > 1      # collectives of the timed steps: bytes, run time, exposed time (parallel/dist.py)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
         gcm.step()
+        D.COMM.step()
     sync()
     elapsed = D.all_reduce_max(time.perf_counter() - t0)
+    D.COMM.enabled = False
+    comm = D.COMM.summary() if world > 1 else None
     ms = 1000 * elapsed / max(1, args.steps)
     tokens = args.micro_batch * args.seq_len * args.grad_accum * world * args.steps
     tps = tokens / elapsed
@@ -238,34 +317,48 @@ def main():
     log(f"[bench] loss={loss.item():.4f} {ms:.1f} ms/step  {tps:,.0f} tok/s  "
         f"~{tps * fl_per_tok / world / 1e12:.0f} TFLOP/s/GPU (matmul)  peak HBM {mem:.1f} GiB")
 
-    faithful = None
-    if args.faithful_steps > 0 and engine is None and not (args.grad_ckpt and not args.ga_fusion):
-        # BASELINE.md's config exactly as the reference runs it (Fine-Tuning/qwen3-8b-qlora-dist.py:137-138,
-        # 162-163): gradient_checkpointing=True and the GA micro-steps one after another (no_sync on all but
-        # the last), same model / optimizer / data, timed the same way as the headline
-        model.gradient_checkpointing_enable({"use_reentrant": bool(args.ckpt_reentrant), "policy": args.ckpt_policy})
+    def timed_ckpt(policy: str, n_steps: int) -> dict:
+        """BASELINE.md's config as the reference runs it (Fine-Tuning/qwen3-8b-qlora-dist.py:137-138, 162-163):
+        gradient checkpointing on and the GA micro-steps one after another (no_sync on all but the last), same
+        model / optimizer / data, timed the same way as the headline.  policy "full" = HF's whole-layer
+        recompute (use_reentrant=False, as the reference passes); "selective" = this framework's cheaper recompute."""
+        model.gradient_checkpointing_enable({"use_reentrant": bool(args.ckpt_reentrant), "policy": policy})
         for _ in range(args.faithful_warmup):
             step(fused=0)
         sync()
         if device.type == "cuda":
             torch.cuda.reset_peak_memory_stats(device)
         tf0 = time.perf_counter()
-        for _ in range(args.faithful_steps):
+        for _ in range(n_steps):
             floss = step(fused=0)
             gcm.step()
         sync()
         fel = D.all_reduce_max(time.perf_counter() - tf0)
-        fms = 1000 * fel / args.faithful_steps
-        ftps = args.micro_batch * args.seq_len * args.grad_accum * world * args.faithful_steps / fel
+        fms = 1000 * fel / n_steps
+        ftps = args.micro_batch * args.seq_len * args.grad_accum * world * n_steps / fel
         fmem = torch.cuda.max_memory_allocated(device) / 2 ** 30 if device.type == "cuda" else 0.0
-        log(f"[bench] faithful (grad ckpt + sequential GA): loss={floss.item():.4f} {fms:.1f} ms/step  {ftps:,.0f} tok/s"
-            f"  peak HBM {fmem:.1f} GiB")
-        faithful = {"value": round(ftps, 1), "unit": "tokens/s", "ms_per_step": round(fms, 2),
-                    "steps": args.faithful_steps, "warmup": args.faithful_warmup,
-                    "gradient_checkpointing": True, "ga_execution": "sequential",
-                    "gradient_checkpointing_kwargs": {"use_reentrant": bool(args.ckpt_reentrant)},
-                    "checkpoint_policy": args.ckpt_policy,
-                    "micro_batch": args.micro_batch, "grad_accum": args.grad_accum, "peak_hbm_gib": round(fmem, 1)}
+        log(f"[bench] grad ckpt ({policy}) + sequential GA: loss={floss.item():.4f} {fms:.1f} ms/step  "
+            f"{ftps:,.0f} tok/s  peak HBM {fmem:.1f} GiB")
+        return {"value": round(ftps, 1), "unit": "tokens/s", "ms_per_step": round(fms, 2),
+                "steps": n_steps, "warmup": args.faithful_warmup,
+                "gradient_checkpointing": True, "ga_execution": "sequential",
+                "gradient_checkpointing_kwargs": {"use_reentrant": bool(args.ckpt_reentrant)},
+                "checkpoint_policy": policy,
+                "micro_batch": args.micro_batch, "grad_accum": args.grad_accum, "peak_hbm_gib": round(fmem, 1)}
+
+    faithful = selective = None
+    if engine is None and not (args.grad_ckpt and not args.ga_fusion):
+        if args.faithful_steps > 0:
+            faithful = timed_ckpt("full", args.faithful_steps)
+        if args.selective_steps > 0:
+            selective = timed_ckpt("selective", args.selective_steps)
+
+    zero3 = None
+    if world > 1 and engine is None and args.zero3_steps > 0:
+        del step
+        model = opt = sched = ddp = data = None
+        spent[0] = None
+        zero3 = zero3_subrecord(args, device, rank, world, sync)
     gcm.__exit__(None, None, None)
     if D.is_main():
         rec = {
@@ -305,8 +398,18 @@ def main():
                 "tokens_per_s_nonpad": round(tps * nonpad_frac, 1),
             },
         }
+        if comm is not None:
+            rec["comm"] = comm
+        else:
+            rec["comm"] = {"skipped": "single rank: no collectives"}
+        if zero3 is not None:
+            rec["zero3"] = zero3
+        elif world == 1:
+            rec["zero3"] = {"skipped": "single rank (the ZeRO-3 sub-record runs when world > 1)"}
         if faithful is not None:
             rec["faithful"] = faithful
+        if selective is not None:
+            rec["selective_ckpt"] = selective
         print(json.dumps(rec), flush=True)
     D.destroy()
 

@@ -647,7 +647,7 @@ bool gemm4w_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, bool b
 // y = x·wᵀ (+ residual) through the one-wave-per-SIMD AGPR-accumulator MFMA GEMM (gemm4w.hip);
 // x [M, K] (row stride any multiple of 8), w [N, K] contiguous rows.  bt: y = x·w with w [K, N]
 // (the dX = dY·W of a frozen [N_w, K_w] weight, no transpose copy).  splits <= 0: auto split-K;
-// bn: tile width 128 / 256 / 192 (NT only), 0 = auto.  wscale: w is an NF4 base (g4w_operand); n_w4
+// bn: tile width 128 / 256 / 192 (bf16; the transposed-B 192 tile is 256 rows high), 0 = auto.  wscale: w is an NF4 base (g4w_operand); n_w4
 // is then the GEMM N (the weight's rows for NT, its columns for bt).
 Tensor gemm4w(Tensor x, Tensor w, optional<Tensor> residual, int64_t splits, bool bt, int64_t bn, int64_t bm,
               optional<Tensor> wscale, int64_t n_w4, optional<Tensor> wzero) {
@@ -665,7 +665,8 @@ Tensor gemm4w(Tensor x, Tensor w, optional<Tensor> residual, int64_t splits, boo
     TORCH_CHECK(residual->is_contiguous() && residual->size(0) == M && residual->size(1) == N, "gemm4w: residual [M, N]");
     res = residual->data_ptr();
   }
-  TORCH_CHECK(bn == 0 || bn == 128 || bn == 256 || (bn == 192 && !bt && !w4), "gemm4w: bn 0 / 128 / 256 / 192 (NT bf16)");
+  TORCH_CHECK(bn == 0 || bn == 128 || bn == 256 || (bn == 192 && !w4 && !(bt && bm == 128)),
+              "gemm4w: bn 0 / 128 / 256 / 192 (bf16; transposed-B 192 with 256-row tiles)");
   TORCH_CHECK(bm == 0 || bm == 128 || bm == 256, "gemm4w: bm 0 / 128 / 256");
   int bn_used = 0, bm_used = 0;
   const int sp = gemm4w_plan(M, N, K, bt, (int)bn, (int)splits, &bn_used, (int)bm, &bm_used, w4);

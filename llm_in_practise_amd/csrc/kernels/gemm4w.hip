@@ -77,6 +77,17 @@ __device__ __forceinline__ int slot_of(int r8, int c) { return 8 * r8 + (c ^ (FU
 
 __device__ __forceinline__ bf16x8 lds_frag(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
+// BT image: 32-B column pair c of k-row k sits at pair c ^ bt_swz(k).  A ds_read_b64_tr_b16 lane group reads
+// 8 k-rows {0-3, 8-11} (+ a multiple of 4) × one 32-B pair each: at BN = 256 / 128 every row starts on bank 0
+// and the 8 rows take 8 distinct 32-B bank slots through a 3-bit swizzle; at BN = 192 (384-B rows, starting on
+// banks 0 / 32 alternately) a 2-bit swizzle inside each aligned group of 4 pairs (12 pairs = 3 groups: no
+// pair leaves its group) gives the 8 rows distinct slots — conflict-free either way.
+template <int BN>
+__device__ __forceinline__ int bt_swz(int k) {
+  if constexpr (BN == 192) return ((k >> 1) & 1) | ((k >> 2) & 2);
+  else return (k & 3) | ((k >> 1) & 4);
+}
+
 __device__ __forceinline__ void mfma_acc(f32x4& acc, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
@@ -355,7 +366,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   constexpr int CR_W = NLD * 1024 + 256 * NSC; // W4: a wave's codes + tables of one K-tile (LDS ring)
   constexpr int RING = W4 ? 2 * 4 * CR_W : 0;  // W4: two K-tiles of codes in flight
   constexpr int STAGES = 3 * STAGE + RING <= 160 * 1024 ? 3 : 2;
-  static_assert(BN == 128 || BN == 256 || (BN == 192 && !BT), "tile widths: 128, 256 (NT / BT), 192 (NT)");
+  static_assert(BN == 128 || BN == 256 || (BN == 192 && !(BT && LORA)), "tile widths: 128, 256, 192 (not the LoRA dX)");
   constexpr int KT = 2 * NA * NB;              // MFMAs per K-tile per wave
   constexpr int H = KT / 2;
   constexpr int R = NA + NB;                   // fragment-read items per K-half
@@ -425,13 +436,13 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
         vb[i] = ((uint32_t)rb * (uint32_t)ldb + (uint32_t)(kt0 * BK + c * 8)) * 2u;
       }
     } else {
-      constexpr int CPR = BN / 8;             // 16-B chunks per k-row (32 or 16)
-      constexpr int RPD = 64 / CPR;            // k-rows per DMA (2 or 4)
+      // the lane's 16 B of the lane-linear BT image (k-rows of 2·BN bytes; wave w fills rows 16w .. 16w + 15,
+      // DMA i the next 1 KB of them — at BN = 192 a piece spans 2 2/3 rows), fetched from the swizzled column
 #pragma unroll
-      for (int i = 0; i < DB; ++i) {   // k-rows (16)·w + RPD·i + lane / CPR
-        const int kr = 16 * w + RPD * i + lane / CPR;
-        const int hk = (kr & 3) | ((kr >> 1) & 4);
-        const int cc = (lane % CPR) ^ (2 * hk);
+      for (int i = 0; i < DB; ++i) {
+        const int b = w * (IMG_B / 4) + i * 1024 + lane * 16;
+        const int kr = b / (2 * BN), ch = (b % (2 * BN)) / 16;
+        const int cc = ch ^ (2 * bt_swz<BN>(kr));
         vb[i] = ((uint32_t)(kt0 * BK + kr) * (uint32_t)ldb + (uint32_t)(n0 + 8 * cc)) * 2u;
       }
     }
@@ -478,7 +489,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
       w4s = (uint32_t)(kbw * K + kt0 * 64 + kr) * 4u;
       w4sstep = 256u;
       rss = make_rsrc(bscale, (uint64_t)K * (N / 64) * 4);
-      const int hk = (kr & 3) | ((kr >> 1) & 4);
+      const int hk = bt_swz<BN>(kr);
 #pragma unroll
       for (int u = 0; u < NCH; ++u) w4o[u] = IMG_AT + kr * (2 * BN) + 16 * ((8 * cb + 4 * hh + u) ^ (2 * hk));
     }
@@ -496,7 +507,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   int boff_t[8];
   if constexpr (BT) {
     const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const int hk = q | ((g & 1) << 2);
+    const int hk = bt_swz<BN>(8 * g + q);   // = the swizzle of row + 4 and of the second K-half's rows
 #pragma unroll
     for (int j = 0; j < NB; ++j)
       boff_t[j] = (8 * g + q) * (2 * BN) + 32 * ((wc * NB + j) ^ hk) + 16 * (p >> 1) + 8 * (p & 1);
@@ -622,7 +633,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
         const bf16* Ab = (const bf16*)ldx.a[b];
         for (int idx = threadIdx.x; idx < 32 * CPR; idx += NT) {
           const int kr = idx / CPR, cc = idx % CPR;
-          const int hk = (kr & 3) | ((kr >> 1) & 4);
+          const int hk = bt_swz<BN>(kr);
           const int col = n0 + 8 * cc;
           bf16x8 v = {};
           if (kr < ldx.r[b] && col < N) v = *reinterpret_cast<const bf16x8*>(Ab + (size_t)kr * N + col);
@@ -1078,10 +1089,10 @@ G4wCfg gemm4w_cfg(int M, int N, int K, bool bt, int bn_req, int sp_req, int bm_r
   for (int bm : {256, 128}) {
     if (bm_req && bm != bm_req) continue;
     for (int bn : {256, 192, 128}) {
-      if (bn == 192 && (bt || w4)) continue;
+      if (bn == 192 && (w4 || (bt && bm != 256))) continue;   // (instantiated: NT any height, BT 256-high)
       if (bn_req && bn != bn_req) continue;
       const int tiles = tiles_of(M, N, bm, bn);
-      double kt_us = bn == 256 ? (bt ? 1.52 : 1.5) : bn == 192 ? 1.22 : 0.92;
+      double kt_us = bn == 256 ? (bt ? 1.52 : 1.5) : bn == 192 ? (bt ? 1.24 : 1.22) : 0.92;
       if (bm == 128) kt_us *= 0.56;
       if (w4) kt_us *= bm == 128 ? w4_cost128 : w4_cost;
       for (int s = 1; s <= 8; s *= 2) {
@@ -1136,7 +1147,7 @@ void launch_gemm4w(const void* A, int lda, const void* B, int ldb, const void* r
   } else if (bn == 256) {                                                                     \
     if (bt) { G4W_SP(BM_, 256, true, 0) } else { G4W_SP(BM_, 256, false, 0) }                 \
   } else if (bn == 192) {                                                                     \
-    G4W_SP(BM_, 192, false, 0)                                                                \
+    if (bt) { G4W_SP(256, 192, true, 0) } else { G4W_SP(BM_, 192, false, 0) }                  \
   } else {                                                                                    \
     if (bt) { G4W_SP(BM_, 128, true, 0) } else { G4W_SP(BM_, 128, false, 0) }                 \
   }
@@ -1236,7 +1247,7 @@ void launch_gemm4w_dswiglu(const void* DY, int lddy, const void* W, const float*
     if (bm == 256) { if (bn == 256) G4D(256, 256, 1); else G4D(256, 128, 1); }
     else { if (bn == 256) G4D(128, 256, 1); else G4D(128, 128, 1); }
   } else if (bm == 256) {
-    if (bn == 256) G4D(256, 256, 0); else G4D(256, 128, 0);
+    if (bn == 256) G4D(256, 256, 0); else if (bn == 192) G4D(256, 192, 0); else G4D(256, 128, 0);
   } else {
     if (bn == 256) G4D(128, 256, 0); else G4D(128, 128, 0);
   }

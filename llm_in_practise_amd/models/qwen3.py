@@ -332,8 +332,9 @@ class Qwen3ForCausalLM(nn.Module):
 
     def gradient_checkpointing_enable(self, gradient_checkpointing_kwargs=None):
         """HF's API (``Fine-Tuning/qwen3-8b-qlora-dist.py:162-163``): ``use_reentrant`` selects torch's
-        checkpoint form; ``policy`` ("selective" default / "full") is this framework's recompute policy
-        (ops/linear.py ``checkpoint``).  Unknown keys raise."""
+        checkpoint form; ``policy`` ("full" default = HF's whole-layer recompute / "selective" = keep the GEMM
+        outputs, ≈ 78 MB more per layer per 1024 tokens) is this framework's recompute policy (ops/linear.py
+        ``checkpoint``).  Unknown keys raise."""
         kw = dict(gradient_checkpointing_kwargs or {})
         bad = set(kw) - {"use_reentrant", "policy"}
         if bad:

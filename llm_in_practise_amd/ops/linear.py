@@ -317,7 +317,9 @@ def seed_dropout(seed: int):
 
 
 _CKPT_REENTRANT = os.environ.get("LIPA_CKPT_REENTRANT", "1") == "1"
-_CKPT_POLICY = os.environ.get("LIPA_CKPT_POLICY", "selective")
+# HF semantics by default (the whole layer recomputed); "selective" keeps every GEMM output of the
+# first forward (~78 MB per Qwen3-8B layer per 1024 tokens) and is opt-in
+_CKPT_POLICY = os.environ.get("LIPA_CKPT_POLICY", "full")
 
 
 def checkpoint(fn, *args, use_reentrant: bool | None = None, policy: str | None = None):
@@ -325,9 +327,10 @@ def checkpoint(fn, *args, use_reentrant: bool | None = None, policy: str | None 
 
     ``use_reentrant`` selects torch's form (HF's ``gradient_checkpointing_kwargs={"use_reentrant": …}``,
     ``Fine-Tuning/qwen3-8b-qlora-dist.py:162-163``; default: LIPA_CKPT_REENTRANT, on).  ``policy``:
-    ``"full"`` recomputes the whole layer in backward (HF's behaviour); ``"selective"`` (default,
-    LIPA_CKPT_POLICY) records the GEMM outputs in the first forward and replays them in the recompute —
-    only RMSNorm, q/k-norm + RoPE and attention run again (the stash above).
+    ``"full"`` (default, LIPA_CKPT_POLICY) recomputes the whole layer in backward (HF's behaviour);
+    ``"selective"`` records the GEMM outputs in the first forward and replays them in the recompute —
+    only RMSNorm, q/k-norm + RoPE and attention run again (the stash below): faster, but it holds
+    ≈ 78 MB per Qwen3-8B layer per 1024 tokens from the forward until the backward.
 
     The fused LoRA kernels draw their dropout mask from the host key stream above, not from
     torch's RNG, so torch's ``preserve_rng_state`` does not cover them: a plain

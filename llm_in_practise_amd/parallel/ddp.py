@@ -25,7 +25,8 @@ never fewer than ~4 per model so the first can start early); LoRA-sized gradient
 
 Small buckets can go over the intra-node peer-memory all-reduce instead of RCCL
 (``custom_allreduce=`` a :class:`~.custom_allreduce.CustomAllReduce`, or ``"auto"`` /
-``LIPA_CUSTOM_AR=1`` to build one): one- or two-shot by size, RCCL above its staging cap.
+``LIPA_CUSTOM_AR=1`` to build one; default off until an 8-GPU run records it): one- or two-shot by
+size, RCCL above its staging cap.
 
 On start the module's parameters and buffers are broadcast from rank 0
 (``sync_module_states``).
@@ -34,12 +35,13 @@ from __future__ import annotations
 
 import contextlib
 import os
+import time
 
 import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from .dist import all_reduce_mean_, is_dist
+from .dist import COMM, all_reduce_mean_, is_dist
 
 
 ONE_SHOT_BYTES = 256 << 10
@@ -91,7 +93,8 @@ class DistributedDataParallel(nn.Module):
         self._stream = torch.cuda.Stream(device=self.grad_buffer.device) if (self.overlap and self._cuda) else None
         self._works: list = []
         if custom_allreduce is None:
-            custom_allreduce = os.environ.get("LIPA_CUSTOM_AR", "auto")
+            # default off: the peer-memory path has no multi-GPU hardware record yet (parallel/custom_allreduce.py)
+            custom_allreduce = os.environ.get("LIPA_CUSTOM_AR", "0")
             custom_allreduce = {"0": None, "off": None, "1": "auto"}.get(custom_allreduce, custom_allreduce)
         if self.grad_buffer is not None:
             total = self.grad_buffer.numel()
@@ -102,6 +105,8 @@ class DistributedDataParallel(nn.Module):
         if self.overlap:
             self._build_buckets()
         host_ok = custom_allreduce == "auto-host"     # the /dev/shm model of the protocol (CPU rehearsal)
+        if custom_allreduce in ("auto", "auto-host") and not self.overlap:
+            custom_allreduce = None         # the non-overlapped path reduces whole buckets on RCCL only
         if custom_allreduce == "auto-host" or (custom_allreduce == "auto" and self._cuda):
             # the decided policy (allreduce_path): a peer-memory one-shot all-reduce only for buckets that
             # are latency-bound (<= 256 KiB on one node); everything larger goes to RCCL.  Built only when
@@ -168,13 +173,16 @@ class DistributedDataParallel(nn.Module):
         bk.launched = True
         self.launch_log.append((b, why))
         view = self.grad_buffer[bk.start:bk.end]
+        COMM.issue("all_reduce", view.numel() * view.element_size())
         if self._stream is not None:
             self._stream.wait_stream(torch.cuda.current_stream(view.device))
             with torch.cuda.stream(self._stream):
+                ev0 = COMM.events(self._stream)
                 if self.car is not None and self.car.should_use(view):
                     self.car.all_reduce_(view, average=True)
                 else:
                     all_reduce_mean_(view)
+                COMM.span_end("all_reduce", ev0, self._stream)
         elif self.car is not None and self.car.should_use(view):     # peer-memory path (host model on CPU)
             self.car.all_reduce_(view, average=True)
         else:       # gloo / CPU: an async collective on the process group's own thread
@@ -239,10 +247,15 @@ class DistributedDataParallel(nn.Module):
             self._launch(b, "flush")
         self._next = 0
         if self._stream is not None:
-            torch.cuda.current_stream(self.grad_buffer.device).wait_stream(self._stream)
+            cur = torch.cuda.current_stream(self.grad_buffer.device)
+            ev0 = COMM.events(cur)          # the backward's last kernel is queued ahead of this point
+            cur.wait_stream(self._stream)
+            COMM.wait_end("all_reduce", ev0, cur)
         try:
             for work, view in self._works:
+                t0 = time.perf_counter()
                 work.wait()
+                COMM.host_wait("all_reduce", time.perf_counter() - t0)
                 view.div_(dist.get_world_size())
         finally:
             # the bucket state is reset even when a wait (or the poll below) raises: a caller that

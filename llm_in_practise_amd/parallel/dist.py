@@ -94,3 +94,96 @@ def all_reduce_max(x: float) -> float:
 def destroy():
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
+
+
+class CommStats:
+    """Per-step accounting of the data-parallel collectives, for the bench record (``COMM`` below).
+
+    Per collective kind (``all_reduce`` / ``reduce_scatter`` / ``all_gather``):
+      * ``calls`` and ``bytes`` issued;
+      * ``busy_ms`` — time the collective itself ran, from CUDA events recorded on the stream that runs it
+        (DDP's side stream; only where the framework owns that stream);
+      * ``exposed_ms`` — time the compute stream stood waiting for collectives (CUDA events around the join
+        on the GPU, host wall time of ``work.wait()`` on gloo).
+    ``overlap_fraction`` = 1 − exposed / busy: the share of the communication hidden under the backward.
+    Off unless ``enabled``; event pairs are resolved once, in :meth:`summary` (after a synchronise)."""
+
+    KINDS = ("all_reduce", "reduce_scatter", "all_gather")
+
+    def __init__(self):
+        self.enabled = False
+        self.reset()
+
+    def reset(self):
+        import collections
+        self.calls = collections.Counter()
+        self.bytes = collections.Counter()
+        self._spans: list = []         # (kind, ev0, ev1): the collective's own run time
+        self._waits: list = []         # (kind, ev0, ev1): compute stream stalled on it
+        self._host_wait = collections.Counter()
+        self.steps = 0
+
+    def issue(self, kind: str, nbytes: int):
+        if self.enabled:
+            self.calls[kind] += 1
+            self.bytes[kind] += int(nbytes)
+
+    def events(self, stream=None):
+        """(begin, end) recorder pair on ``stream`` (current stream if None), or None when off / on CPU."""
+        if not (self.enabled and torch.cuda.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"):
+            return None
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        return ev0
+
+    def span_end(self, kind: str, ev0, stream=None):
+        if ev0 is not None:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record(stream)
+            self._spans.append((kind, ev0, ev1))
+
+    def wait_end(self, kind: str, ev0, stream=None):
+        if ev0 is not None:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record(stream)
+            self._waits.append((kind, ev0, ev1))
+
+    def host_wait(self, kind: str, seconds: float):
+        if self.enabled:
+            self._host_wait[kind] += seconds
+
+    def step(self):
+        if self.enabled:
+            self.steps += 1
+
+    def summary(self) -> dict:
+        """Per-step means over the recorded steps (call after the device is synchronised)."""
+        n = max(1, self.steps)
+        busy = {k: 0.0 for k in self.KINDS}
+        exposed = {k: 0.0 for k in self.KINDS}
+        timed_busy = {k: False for k in self.KINDS}
+        for kind, a, b in self._spans:
+            busy[kind] += a.elapsed_time(b)
+            timed_busy[kind] = True
+        for kind, a, b in self._waits:
+            exposed[kind] += a.elapsed_time(b)
+        for kind, s in self._host_wait.items():
+            exposed[kind] += 1000.0 * s
+        out = {"steps": self.steps}
+        tot_busy = tot_exp = 0.0
+        for k in self.KINDS:
+            if not self.calls[k]:
+                continue
+            rec = {"calls_per_step": round(self.calls[k] / n, 2), "mbytes_per_step": round(self.bytes[k] / n / 2 ** 20, 3),
+                   "busy_ms_per_step": round(busy[k] / n, 3) if timed_busy[k] else None,
+                   "exposed_ms_per_step": round(exposed[k] / n, 3)}
+            out[k] = rec
+            tot_exp += exposed[k] / n
+            if timed_busy[k]:
+                tot_busy += busy[k] / n
+        out["exposed_ms_per_step"] = round(tot_exp, 3)
+        out["overlap_fraction"] = (round(max(0.0, min(1.0, 1.0 - tot_exp / tot_busy)), 3) if tot_busy > 0 else None)
+        return out
+
+
+COMM = CommStats()

@@ -92,7 +92,8 @@ def load_ds_config(cfg, world_size: int = 1, micro_batch: int | None = None, gra
     h2 = hidden_size * hidden_size if hidden_size else None
     zc = ZeroConfig(
         stage=int(z.get("stage", 0)),
-        overlap_comm=bool(z.get("overlap_comm", False)),
+        # DeepSpeed's default: overlapped for stage 3, not for stages 1-2
+        overlap_comm=bool(z.get("overlap_comm", int(z.get("stage", 0)) == 3)),
         contiguous_gradients=bool(z.get("contiguous_gradients", True)),
         reduce_scatter=bool(z.get("reduce_scatter", True)),
         reduce_bucket_size=_num(z.get("reduce_bucket_size"), h2 or int(5e8)),

@@ -49,6 +49,7 @@ from __future__ import annotations
 import contextlib
 import math
 import os
+import time
 
 import torch
 import torch.distributed as dist
@@ -57,7 +58,7 @@ import torch.nn as nn
 from ..ops import reference as ref
 from ..ops._native import native, use_native
 from ..optim.adamw import LRScheduler
-from .dist import is_dist
+from .dist import COMM, is_dist
 from .ds_config import DSConfig, load_ds_config
 
 
@@ -180,6 +181,18 @@ class _QuantFlat:
             q.__dict__.pop("_g4w", None)
 
 
+def _join(works, kind: str):
+    """Join async collectives, timing the wait for the bench's comm record (parallel/dist.py COMM)."""
+    ev0 = COMM.events() if torch.cuda.is_available() else None
+    t0 = time.perf_counter()
+    for w in works:
+        w.wait()
+    if ev0 is not None:
+        COMM.wait_end(kind, ev0)
+    elif torch.distributed.get_backend() != "nccl":
+        COMM.host_wait(kind, time.perf_counter() - t0)
+
+
 class _Unit:
     """A stage-3 partition unit: trainable params of one module, flattened and sharded."""
 
@@ -234,8 +247,7 @@ class _Unit:
             return False
         if self.work is not None:
             if not async_op:
-                for w in self.work:
-                    w.wait()
+                _join(self.work, "all_gather")
                 self.work = None
                 self.gathered = True
             return False
@@ -243,6 +255,7 @@ class _Unit:
         for full, shard in self._flats():
             full.untyped_storage().resize_(full.numel() * full.element_size())
             if self.world > 1:
+                COMM.issue("all_gather", full.numel() * full.element_size())
                 w = dist.all_gather_into_tensor(full, shard, async_op=async_op)
                 if async_op:
                     works.append(w)
@@ -256,8 +269,7 @@ class _Unit:
 
     def release(self):
         if self.work is not None:
-            for w in self.work:
-                w.wait()
+            _join(self.work, "all_gather")
             self.work = None
             self.gathered = True
         if not self.gathered:
@@ -401,7 +413,13 @@ class ZeroEngine:
         self.max_live = int(z.stage3_max_live_parameters)
         self.max_reuse = int(z.stage3_max_reuse_distance)
         self.reduce_bucket = max(1, int(z.reduce_bucket_size))
-        self.overlap_comm = bool(z.overlap_comm) or True   # async collectives are always safe here
+        # ds_config "overlap_comm": True (the reference's ds_zero3_config.json) issues the gradient
+        # reduce-scatters asynchronously while the backward continues and prefetches all-gathers ahead of
+        # use; False runs every collective synchronously at its point of use (no prefetch, each reduce-scatter
+        # joined before the backward goes on) — DeepSpeed's non-overlapped schedule
+        self.overlap_comm = bool(z.overlap_comm)
+        if not self.overlap_comm:
+            self.prefetch_bucket = 0
         self.fwd_order: list[int] = [u.index for u in self.units if u.module is not self.module]
         self._recorded: list[int] = []
         self._recording = True
@@ -545,7 +563,7 @@ class ZeroEngine:
                 keep.append((work, out, units, i))
                 continue
             if work is not None:
-                work.wait()
+                _join([work], "reduce_scatter")
             col = 0
             for u in units:
                 o = self.unit_offsets[u.index]
@@ -589,7 +607,10 @@ class ZeroEngine:
         out = bo[:n]
         work = None
         if W > 1:
-            work = dist.reduce_scatter_tensor(out, src, op=dist.ReduceOp.SUM, async_op=True)
+            COMM.issue("reduce_scatter", src.numel() * src.element_size())
+            work = dist.reduce_scatter_tensor(out, src, op=dist.ReduceOp.SUM, async_op=self.overlap_comm)
+            if not self.overlap_comm:
+                work = None          # completed in-line (synchronous schedule); _retire folds it now
         else:
             out.copy_(src[:n])
         self._rs_pool[i] = (bi, bo, work)

@@ -8,7 +8,7 @@ mkdir -p $OUT
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d $OUT -o run -- \
-  python3 $R/bench.py --steps 3 --warmup 2 --faithful-steps 0 "$@" > $OUT/bench.log 2>&1
+  python3 $R/bench.py --steps 3 --warmup 2 --faithful-steps 0 --selective-steps 0 "$@" > $OUT/bench.log 2>&1
 rc=$?
 echo "rocprof rc=$rc"; tail -2 $OUT/bench.log
 f=$(find $OUT -name "*kernel_trace.csv" | head -1)

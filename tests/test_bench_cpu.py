@@ -54,6 +54,42 @@ def test_bench_json_contract_two_ranks(extra):
     assert abs(d["value"] - tokens / (d["ms_per_step"] * 2 / 1000)) / d["value"] < 0.02
     assert d["config"]["global_batch"] == 8
     assert d["config"]["parallelism"] == ("zero3-dp2" if "zero3" in extra else "dp2")
+    _check_comm(d["comm"], "all_gather" if "zero3" in extra else "all_reduce")
+    if "zero3" not in extra:       # the DDP headline carries BASELINE #4 (ZeRO-3) as a sub-record at world > 1
+        _check_zero3(d["zero3"], 2)
+
+
+def _check_comm(c, kind):
+    """the per-step collective record of a multi-rank bench line (parallel/dist.py CommStats)"""
+    assert c["steps"] >= 1 and kind in c, c
+    assert c[kind]["calls_per_step"] > 0 and c[kind]["mbytes_per_step"] > 0
+    assert c[kind]["exposed_ms_per_step"] >= 0 and "overlap_fraction" in c and "exposed_ms_per_step" in c
+
+
+def _check_zero3(z, world):
+    assert "error" not in z, z
+    for k in ("model", "value", "unit", "ms_per_step", "steps", "warmup", "n_gpus", "parallelism", "ds_config",
+              "optimizer", "global_batch", "dist_backend", "comm"):
+        assert k in z, k
+    assert z["n_gpus"] == world and z["parallelism"] == f"zero3-dp{world}" and z["value"] > 0
+    assert z["optimizer"] == "zero3-paged_adamw_8bit" and z["ds_config"].endswith("ds_zero3_config.json")
+    _check_comm(z["comm"], "reduce_scatter")
+    _check_comm(z["comm"], "all_gather")
+
+
+def test_bench_zero3_subrecord_four_ranks():
+    """world 4 (gloo): the headline DDP line carries the zero3 sub-record and both comm records"""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "4", "--steps", "1", "--warmup", "1", "--model", "qwen3-tiny", "--seq-len", "64",
+           "--faithful-steps", "0", "--selective-steps", "0", "--zero3-steps", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    _check_comm(d["comm"], "all_reduce")
+    _check_zero3(d["zero3"], 4)
 
 
 def test_scaling_harness_runs_each_world_size(tmp_path):
