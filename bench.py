@@ -296,6 +296,7 @@ def main():
     gcm = ManualGC().__enter__()    # automatic Python GC off, a full pass every LIPA_GC_INTERVAL steps (utils/gc_control.py)
     D.COMM.reset()
     D.COMM.enabled = world > 1      # collectives of the timed steps: bytes, run time, exposed time (parallel/dist.py)
+    _lin.GEMM_STATS.clear()         # GEMM launches by form over the timed steps (kernel provenance)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -305,6 +306,7 @@ def main():
     elapsed = D.all_reduce_max(time.perf_counter() - t0)
     D.COMM.enabled = False
     comm = D.COMM.summary() if world > 1 else None
+    gemm_forms = {k: round(v / max(1, args.steps), 2) for k, v in sorted(_lin.GEMM_STATS.items())}
     ms = 1000 * elapsed / max(1, args.steps)
     tokens = args.micro_batch * args.seq_len * args.grad_accum * world * args.steps
     tps = tokens / elapsed
@@ -384,6 +386,12 @@ def main():
                 "grad_accum": args.grad_accum,
                 "quant": "nf4+double_quant" if args.mode == "qlora" else "none",
                 "nf4_gemm": args.nf4_gemm,
+                # kernel provenance of the timed steps (ops/linear.py GEMM_STATS): GEMM launches per step by form —
+                # gemm4w = the hand-written HIP GEMM on a bf16 operand, gemm4w-nf4 = the same kernel reading NF4 codes,
+                # library = torch.matmul (shapes gemm4w does not take); nf4-expansion = bf16 copies of NF4 bases
+                "gemm_backend": "gemm4w" if device.type == "cuda" else "torch-cpu",
+                "gemm_launches_per_step": {k: v for k, v in gemm_forms.items() if k != "nf4-expansion"},
+                "nf4_expansions_per_step": gemm_forms.get("nf4-expansion", 0),
                 "lora": f"r{args.lora_r}/a{args.lora_alpha}/drop{args.lora_dropout}/{args.targets}",
                 "optimizer": args.optim if engine is None else f"zero3-{engine.optim_name}",
                 "gradient_checkpointing": bool(args.grad_ckpt),

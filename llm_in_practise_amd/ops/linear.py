@@ -7,26 +7,30 @@ One op covers every projection of the stack:
 * ``base`` is a bf16 ``[N, K]`` tensor (LoRA / full fine-tune) or an :class:`NF4Weight`
   (QLoRA).  Several projections that share an input (q|k|v, gate|up) are row-concatenated
   into one base and one GEMM; each LoRA branch owns a column range ``[c0, c1)``.
-* What runs at training / prefill sizes, the default:
-  - the base GEMM is the hand-written one-wave-per-SIMD MFMA kernel ``gemm4w`` (forward x·Wᵀ with
-    the residual in its epilogue; backward dY·W reading W as stored — the transposed-B form);
-  - an NF4 base (K9) takes one of two forms, chosen per call (``_nf4_w4``): the NF4 dequant-GEMM —
-    gemm4w reads the 4-bit codes (``NF4Weight.g4w_pack``) and expands each quant block to bf16
-    between the load and its LDS B image, no bf16 copy of the base anywhere — or one HBM-speed
-    expansion (``nf4_dequant3_k``) whose bf16 copy serves the forward AND the dX GEMM;
-  - the LoRA branches run in ``lora.hip``: ``lora_proj2`` (both q/v adapters' s·D(x)·Aᵀ in one pass,
-    keep bits stored), ``lora_apply`` (xa·Bᵀ added into the adapters' column blocks of the GEMM
-    output), and in backward ``lora_proj_pair`` / ``lora_acc_pair`` / ``lora_dx2`` (the LoRA dX term
-    enters the dX GEMM as its C matrix) / ``lora_dA_pair``.
-  ``LIPA_GEMM=lt`` swaps the bf16 base GEMMs for direct hipBLASLt calls; decode sizes (M ≤ 16) use the
-  split-K weight-streaming kernels (``skinny.hip``, ``gemv_w4``).
+* Every frozen-base GEMM at training / prefill sizes is the hand-written MFMA kernel ``gemm4w``
+  (csrc/kernels/gemm4w.hip) — there is no library GEMM on the path: forward x·Wᵀ with the residual in
+  its epilogue, backward dY·W reading W as stored (the transposed-B form), split-K by its own cost model.
+  - An NF4 base (K9) takes one of two forms, chosen per call (``_nf4_w4``): the NF4 dequant-GEMM —
+    gemm4w reads the 4-bit codes (``NF4Weight.g4w_pack``) and expands each quant block to bf16 between
+    the load and its LDS B image, no bf16 copy of the base anywhere — or one HBM-speed expansion
+    (``nf4_dequant3_k``) whose bf16 copy serves the forward AND the dX GEMM.
+  - The LoRA branches ride inside gemm4w where their shapes allow: the adapters' B term as extra MFMA
+    K-steps of the forward (``gemm4w_lora``), the dropout-masked input-gradient term in the dX GEMM's
+    prologue (``gemm4w_loradx``); the rank-r projections, dB and dA run in ``lora.hip`` (``lora_proj2`` /
+    ``lora_proj_m`` forward, ``lora_proj_pair`` / ``lora_acc_quad`` / ``lora_acc_jobs`` backward).
+    Other shapes fall back to ``lora_apply`` (B term added into the adapters' column blocks) and
+    ``lora_acc`` / ``lora_dx2``.
+  - Decode sizes (M ≤ 16) use the split-K weight-streaming kernels (``skinny.hip``, ``gemv_w4``).
+  - Shapes gemm4w does not take (K % 64 ≠ 0, tiny M, CPU tensors) run ``torch.matmul``.
 * The SwiGLU MLP block bypasses this op when it carries no adapters (``ops/mlp.py``).
+* ``GEMM_STATS`` counts every GEMM launch by form (the bench record's provenance).
 
 Reference parity: PEFT ``LoraConfig(r, lora_alpha, lora_dropout, target_modules)``
 (``Fine-Tuning/qwen3-8b-qlora.py:107-114``), scaling = alpha / r.
 """
 from __future__ import annotations
 
+import collections
 import dataclasses
 import os
 
@@ -37,41 +41,25 @@ from ..quant.nf4 import NF4Weight, dequantize_nf4
 from ._native import native, use_native
 
 EXT_ALIGN = 32   # the kernels consume the LoRA K-slice in MFMA K-steps of 32
-# LoRA B term as an in-place column-block update after the base GEMM (LIPA_LORA_APPLY=0: K-slice form)
-_APPLY = os.environ.get("LIPA_LORA_APPLY", "1") != "0"
-# training-sized bf16 base GEMMs through direct hipBLASLt calls (csrc/kernels/blaslt.hip): the
-# residual as a separate C matrix (no copy into the output first) and a per-shape kernel choice
-# timed in the running step; LIPA_LT=0: torch.addmm / torch.mm / torch.bmm
-_LT = os.environ.get("LIPA_LT", "1") != "0"
-_LT_MIN_M = 256
-# training-sized frozen-base GEMMs (forward x·Wᵀ and backward dY·W) through the hand-written
-# one-wave-per-SIMD MFMA kernel (csrc/kernels/gemm4w.hip); LIPA_GEMM=lt: direct hipBLASLt
-# Which frozen-base GEMMs run on the hand-written gemm4w (LIPA_GEMM):
-#   hybrid (default) — gemm4w where work rides inside it: the LoRA terms in its prologue (the adapters'
-#       projection forward and dX) and, inside checkpointed layers, the NF4 codes / fused SwiGLU MLP of the
-#       reference-faithful step, and the LM head (ops/loss.py); every other plain bf16 GEMM of the tuned step
-#       (o, gate|up, down, their dX) through hipBLASLt + the separate elementwise passes, faster there: per layer
-#       1268 vs 1338 µs in isolation, headline 62.0 vs 62.8 ms/step on one box (profiles/r4/gemm_hybrid_ab.txt);
-#   native — gemm4w everywhere;   lt — hipBLASLt everywhere (no LoRA prologue).
-_GEMM_MODE = os.environ.get("LIPA_GEMM", "hybrid")
+_MIN_M = 256     # training / prefill-sized GEMMs: gemm4w and the fused LoRA paths
+
+# GEMM launches by form since the last clear (bench.py provenance): "gemm4w" (bf16 B operand), "gemm4w-nf4"
+# (the NF4 codes read in-kernel), "nf4-expansion" (one bf16 copy of an NF4 base), "decode" (skinny / gemv
+# weight-streaming kernels), "library" (torch.matmul fallback for shapes gemm4w does not take)
+GEMM_STATS: collections.Counter = collections.Counter()
 
 
-def _g4w_on(lora: bool = False) -> bool:
-    if _GEMM_MODE == "native":
-        return True
-    if _GEMM_MODE == "hybrid":
-        return lora or _IN_CKPT[0] > 0
-    return False
+def _count(form: str, n: int = 1):
+    GEMM_STATS[form] += n
 
 
-def _g4w_ok(a: torch.Tensor, w: torch.Tensor, bt: bool, lora: bool = False) -> bool:
+def _g4w_ok(a: torch.Tensor, w: torch.Tensor, bt: bool) -> bool:
     """Shapes / strides the gemm4w kernel takes for a bf16 weight: a [M, K] row-major (row stride % 8),
     w [N, K] (or [K, N] when bt) with unit inner stride, training-sized M — the same predicate the
     binding enforces (``gemm4w_supported``: K % 64, N % 8, every operand's byte extent < 4 GiB), so an
     oversized operand falls back here instead of failing in the kernel's TORCH_CHECK."""
-    if not (_g4w_on(lora) and a.is_cuda and a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
-            and a.dim() == 2
-            and w.dim() == 2 and a.shape[0] >= _LT_MIN_M and a.stride(1) == 1 and w.stride(1) == 1
+    if not (a.is_cuda and a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and a.dim() == 2
+            and w.dim() == 2 and a.shape[0] >= _MIN_M and a.stride(1) == 1 and w.stride(1) == 1
             and a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0):
         return False
     K = a.shape[1]
@@ -81,13 +69,10 @@ def _g4w_ok(a: torch.Tensor, w: torch.Tensor, bt: bool, lora: bool = False) -> b
     return bool(native().gemm4w_ok(a.shape[0], N, K, a.stride(0), w.stride(0), bt, False))
 
 
-def _w4_ok(a: torch.Tensor, q: NF4Weight, bt: bool, lora: bool = False) -> bool:
+def _w4_ok(a: torch.Tensor, q: NF4Weight, bt: bool) -> bool:
     """An NF4 base the gemm4w kernel reads as codes (K9): forward x·deq(W)ᵀ (bt=False, a [M, K_w]) or
     dX = dY·deq(W) (bt=True, a [M, N_w]); blocksize 64, both dims multiples of 64, M > 8."""
-    # (LIPA_NF4_GEMM=w4, the memory-lean mode, keeps every NF4 GEMM on the codes whatever the GEMM mode: the
-    # library cannot read them, and expanding would undo the mode)
-    if not (_g4w_on(lora or _NF4_MODE == "w4") and a.is_cuda and a.dtype == torch.bfloat16 and a.dim() == 2
-            and a.shape[0] > 8
+    if not (a.is_cuda and a.dtype == torch.bfloat16 and a.dim() == 2 and a.shape[0] > 8
             and a.stride(1) == 1 and a.data_ptr() % 16 == 0 and q.kernel_ok()):
         return False
     n, k = q.shape
@@ -100,12 +85,14 @@ def _w4_gemm(a: torch.Tensor, q: NF4Weight, bt: bool, c: torch.Tensor | None = N
     """gemm4w on NF4 codes: a·deq(W)ᵀ (+ c) or, bt, a·deq(W) (+ c)."""
     codes, sc = q.g4w_pack()
     n, k = q.shape
+    _count("gemm4w-nf4")
     return native().gemm4w(a, codes, c, 0, bt, 0, 0, sc, k if bt else n)
 
 
 def _nf4_dequant_bf16(q: NF4Weight) -> torch.Tensor:
     """One bf16 expansion of an NF4 base (HBM speed)."""
     n, k = q.shape
+    _count("nf4-expansion")
     return native().nf4_dequant_fast(q.codes, q.gemv_scales(), n, k)
 
 
@@ -192,6 +179,7 @@ def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
     if isinstance(base, NF4Weight):
         if x.shape[0] <= 8 and base.kernel_ok():   # decode: weight-streaming GEMV, no MFMA tile
             n, k = base.shape
+            _count("decode")
             y = native().gemv_w4(x, base.codes, base.gemv_scales(), None, n, base.blocksize,
                                  residual if ext_a is None else None)
             if ext_a is not None:
@@ -206,57 +194,35 @@ def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
         return _base_gemm(x, w, ext_a, ext_b, residual)
     M, K = x.shape
     N = base.shape[0]
-    if (M <= 16 and N <= 8192 and K <= 8192 and N % 16 == 0 and K % 64 == 0 and x.stride(0) % 8 == 0
+    if (x.is_cuda and M <= 16 and N <= 8192 and K <= 8192 and N % 16 == 0 and K % 64 == 0 and x.stride(0) % 8 == 0
             and x.stride(1) == 1 and base.is_contiguous()):
         # decode-sized q|k|v / o projections: the split-K weight-streaming MFMA kernel
         # (csrc/kernels/skinny.hip) beats hipBLASLt's latency-bound 23 µs by 25-45 % and fuses
         # the residual; the wide gate|up / long-K down stay on hipBLASLt (≥ 5 TB/s there)
+        _count("decode")
         y = native().gemm_skinny(x, base, residual)
         return y if ext_a is None else y.addmm_(ext_a, ext_b.t())
     if _g4w_ok(x, base, False):
+        _count("gemm4w")
         y = native().gemm4w(x, base, None if residual is None else residual.contiguous(), 0, False)
         return y if ext_a is None else y.addmm_(ext_a, ext_b.t())
-    if _LT and M >= _LT_MIN_M and x.is_cuda and x.dtype == torch.bfloat16 and x.stride(1) == 1:
-        y = native().lt_linear(x, base.contiguous(), None if residual is None else residual.contiguous(), True)
-        return y if ext_a is None else y.addmm_(ext_a, ext_b.t())
-    # everything else is a plain library GEMM (hipBLASLt via torch): residual = addmm's beta term, the
-    # LoRA K-slice one rank-Σr update
+    # shapes gemm4w does not take (CPU, M < 256, K % 64): torch — residual = addmm's beta term, the LoRA
+    # K-slice one rank-Σr update
+    _count("library")
     y = torch.addmm(residual, x, base.t()) if residual is not None else x @ base.t()
     if ext_a is not None:
         y.addmm_(ext_a, ext_b.t())
     return y
 
 
-def _dx_split(dy: torch.Tensor, w: torch.Tensor) -> int:
-    M, N = dy.shape
-    K = w.shape[1]
-    tiles = (M // 256) * max(1, K // 256)
-    if not (N >= 4 * K and M >= 256 and tiles < 256):
-        return 1
-    # the fewest K-slices that give every CU an output tile (gate|up dX at M = 2048: 128 tiles -> 2;
-    # 2 slices beat 4 by 0.5 ms/step: same GEMM time, half the partial bytes to sum)
-    s = 2
-    while tiles * s < 256 and s < 8:
-        s *= 2
-    return s if N % s == 0 else 1
-
-
-def _dense_dx(dy: torch.Tensor, w: torch.Tensor, tune: bool = True) -> torch.Tensor:
-    """dX = dY·W for a bf16 [N, K] weight.  A long reduction into a small output (gate|up:
-    N = 24576 → K = 4096 at M = 2048 is 128 output tiles for 256 CUs) leaves half the chip idle
-    in hipBLASLt's non-split-K kernel (491 µs; its best in-step candidate 365 µs); K-slices as one
-    batched GEMM + an fp32 slice sum fill it (2 slices: 301 + 8 µs; profiles/hipblaslt_direct_ab.txt)."""
-    M, N = dy.shape
-    K = w.shape[1]
+def _dense_dx(dy: torch.Tensor, w: torch.Tensor, c: torch.Tensor | None = None) -> torch.Tensor:
+    """dX = dY·W (+ c) for a bf16 [N, K] weight: gemm4w's transposed-B form (W read as stored; split-K when
+    the output has fewer tiles than CUs, e.g. gate|up dX at M = 2048), else torch."""
     if _g4w_ok(dy, w, True):
-        return native().gemm4w(dy, w, None, 0, True)
-    split = _dx_split(dy, w)
-    if _LT and M >= _LT_MIN_M and dy.is_cuda and dy.dtype == torch.bfloat16 and K % 8 == 0:
-        return native().lt_dx(dy.contiguous(), w.contiguous(), split, tune, None)
-    if split > 1:
-        s = split
-        return torch.bmm(dy.view(M, s, N // s).transpose(0, 1), w.view(s, N // s, K)).sum(0)
-    return dy @ w
+        _count("gemm4w")
+        return native().gemm4w(dy, w, c, 0, True)
+    _count("library")
+    return dy @ w if c is None else torch.addmm(c, dy, w)
 
 
 def _base_gemm_t(dy, base, ext_a=None, ext_b=None, c=None):
@@ -266,15 +232,7 @@ def _base_gemm_t(dy, base, ext_a=None, ext_b=None, c=None):
             dx = _w4_gemm(dy, base, True, c)
             return dx if ext_a is None else dx.addmm_(ext_a, ext_b.t())
         base = _nf4_dequant_bf16(base) if (base.kernel_ok() and dy.is_cuda) else dequantize_nf4(base, dy.dtype)
-    if c is not None:
-        if _g4w_ok(dy, base, True):
-            dx = native().gemm4w(dy, base, c, 0, True)
-        elif _LT and dy.shape[0] >= _LT_MIN_M and dy.is_cuda and _dx_split(dy, base) == 1:
-            dx = native().lt_dx(dy.contiguous(), base.contiguous(), 1, True, c)
-        else:
-            dx = _dense_dx(dy, base) + c
-        return dx if ext_a is None else dx.addmm_(ext_a, ext_b.t())
-    dx = _dense_dx(dy, base)
+    dx = _dense_dx(dy, base, c)
     return dx if ext_a is None else dx.addmm_(ext_a, ext_b.t())
 
 
@@ -415,29 +373,28 @@ def _zero_buffer(tag: str, rows: int, cols: int, like: torch.Tensor) -> torch.Te
     return t
 
 
-_LORA_EPI = os.environ.get("LIPA_LORA_EPI", "1") != "0"
-
-
 def _lora_epi_ok(x, base, wdq, weight, branches) -> bool:
     """The branches fit the gemm4w LoRA epilogue: ranks multiples of 8 (≤ 128 in all), training-sized M, the
     base GEMM itself on gemm4w (a bf16 weight / expansion, or NF4 codes)."""
-    if not (_LORA_EPI and x.shape[0] >= _LT_MIN_M and all(br.a.shape[0] % 8 == 0 for br in branches)
+    if not (x.shape[0] >= _MIN_M and all(br.a.shape[0] % 8 == 0 for br in branches)
             and sum(br.a.shape[0] for br in branches) <= 128):
         return False
     if wdq is not None:
-        return _g4w_ok(x, wdq, False, lora=True)
+        return _g4w_ok(x, wdq, False)
     if isinstance(base, NF4Weight):
-        return _w4_ok(x, base, False, lora=True)
-    return weight is not None and not weight.requires_grad and _g4w_ok(x, weight, False, lora=True)
+        return _w4_ok(x, base, False)
+    return weight is not None and not weight.requires_grad and _g4w_ok(x, weight, False)
+
+
+# the two-branch (q_proj + v_proj) and multi-adapter kernel families; the GPU tests switch these off to
+# check them against the per-adapter kernels, which stay the general path for every other shape
+_PAIR = True
+_MULTI = True
 
 
 def _pair_ok(x, branches) -> bool:
     """Two rank-<=8 adapters on one fused projection (q_proj + v_proj): the two-branch kernels."""
-    return (len(branches) == 2 and x.is_cuda and all(br.a.shape[0] <= 8 for br in branches)
-            and os.environ.get("LIPA_LORA_PAIR", "1") != "0")
-
-
-_MULTI = os.environ.get("LIPA_LORA_MULTI", "1") != "0"
+    return _PAIR and len(branches) == 2 and x.is_cuda and all(br.a.shape[0] <= 8 for br in branches)
 
 
 def _multi_ok(x, branches) -> bool:
@@ -447,7 +404,7 @@ def _multi_ok(x, branches) -> bool:
     one launch (``lora_acc_jobs``), the masked dX term inside the dX GEMM (1-2 branches: gemm4w_loradx)
     or as its C matrix (``lora_dxc``).  Training-sized M only; decode keeps the per-branch kernels.
     Reference config: ``Fine-Tuning/qwen3-8b-lora.py:128-141`` (r 16 / alpha 32 / dropout 0.05 on q, k, v, o)."""
-    return (_MULTI and x.is_cuda and 1 <= len(branches) <= 4 and x.shape[0] >= _LT_MIN_M
+    return (_MULTI and x.is_cuda and 1 <= len(branches) <= 4 and x.shape[0] >= _MIN_M
             and not _pair_ok(x, branches)
             and all(br.a.shape[0] in (8, 16) and (br.c1 - br.c0) % 512 == 0 for br in branches))
 
@@ -512,10 +469,10 @@ class _FusedLinearFn(torch.autograd.Function):
         # (grad mode is off inside forward: ask autograd; a recording first forward keeps the LoRA side
         # products too — the replay's backward needs them)
         need_xa = any(ctx.needs_input_grad[5:]) or _sac_recording()
-        # "apply" form: the base GEMM runs alone, then lora_apply adds xa_i·B_iᵀ into ONLY the adapters'
-        # column blocks of its output (no K-slice buffers, no per-call B copies, no rank-Σr addmm over
-        # all N columns)
-        apply = fast and x.is_cuda and len(branches) <= 4 and _APPLY
+        # "apply" form: the adapters' B term inside gemm4w (epi) or added by lora_apply into ONLY their column
+        # blocks of the base GEMM's output (no K-slice buffers, no per-call B copies, no rank-Σr update over
+        # all N columns); the K-slice form below serves the CPU / odd-shaped rest
+        apply = fast and x.is_cuda and len(branches) <= 4
         wdq = None
         if not dense and x.shape[0] > 8 and base.kernel_ok() and x.is_cuda and not _nf4_w4(ctx.needs_input_grad[0]):
             wdq = _nf4_expand(base)     # the expand form: this copy also serves the dX GEMM
@@ -614,6 +571,7 @@ class _FusedLinearFn(torch.autograd.Function):
             bts = [torch.empty(b.shape[1], b.shape[0], dtype=x.dtype, device=x.device) for b in bs] if need_xa else []
             w_op = wdq if wdq is not None else (weight if dense else None)
             res = None if residual is None else residual.contiguous()
+            _count("gemm4w" if w_op is not None else "gemm4w-nf4")
             if w_op is not None:
                 y = native().gemm4w_lora(x, w_op, None, 0, res, xa32, bs, [br.c0 for br in branches], kofs,
                                          bts or [None] * len(bs))
@@ -648,11 +606,9 @@ class _FusedLinearFn(torch.autograd.Function):
         ctx.fast = fast
         ctx.pair = bool(branches) and fast and _pair_ok(x, branches)
         # (the forward's condition for lora_proj_m: "apply" form and the multi-adapter shapes)
-        ctx.multi = (bool(branches) and fast and x.is_cuda and len(branches) <= 4 and _APPLY
-                     and _multi_ok(x, branches))
+        ctx.multi = bool(branches) and fast and x.is_cuda and len(branches) <= 4 and _multi_ok(x, branches)
         ctx.ab_refs = ab          # the parameters themselves: fused kernels accumulate into their .grad
         ctx.has_residual = residual is not None
-        ctx.ckpt = _IN_CKPT[0] > 0     # hybrid GEMM mode: a checkpointed layer's backward keeps gemm4w too
         # the LoRA parameters travel as ctx.ab_refs, not through save_for_backward: under non-reentrant
         # checkpointing every saved tensor costs a Python pack / unpack hook (host time of the
         # reference-faithful step), and parameters need no saving
@@ -662,16 +618,6 @@ class _FusedLinearFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        if ctx.ckpt and _GEMM_MODE == "hybrid":
-            _IN_CKPT[0] += 1
-            try:
-                return _FusedLinearFn._backward(ctx, dy)
-            finally:
-                _IN_CKPT[0] -= 1
-        return _FusedLinearFn._backward(ctx, dy)
-
-    @staticmethod
-    def _backward(ctx, dy):
         base, branches, training = ctx.meta
         saved = ctx.saved_tensors
         x, weight = saved[0], saved[1]
@@ -709,7 +655,7 @@ class _FusedLinearFn(torch.autograd.Function):
                 # with the dropout pair's dA due too (the keep-bit path below), both dB and both dA in ONE launch
                 quad = (_DX_C and ctx.pair and all(k is not None for k in ctx.keys) and ctx.masks is not None
                         and ctx.needs_input_grad[0] and ctx.needs_input_grad[5] and ctx.needs_input_grad[7]
-                        and dy.shape[0] >= _LT_MIN_M and x.shape[1] % 128 == 0
+                        and dy.shape[0] >= _MIN_M and x.shape[1] % 128 == 0
                         and g_list[0].shape[1] == xs[0].shape[1])
                 if quad:
                     (a0o, aret0), (a1o, aret1) = dest(0), dest(2)
@@ -767,20 +713,20 @@ class _FusedLinearFn(torch.autograd.Function):
             wb = ctx.wdq if ctx.wdq is not None else (base if not dense else weight)
             pair_ok = (ctx.pair and all(k is not None for k in ctx.keys) and not deterministic()
                        and ctx.needs_input_grad[5] and ctx.needs_input_grad[7])
-            if (pair_ok and _DX_C and ctx.masks is not None and not fold and dy.shape[0] >= _LT_MIN_M
-                   ):
+            if pair_ok and _DX_C and ctx.masks is not None and not fold and dy.shape[0] >= _MIN_M:
                 # the LoRA input-gradient term written once (lora_dx2, from the stored keep bits) and
                 # added by the dX GEMM as its C matrix; dA from x in a separate launch — no
                 # read-modify-write pass over dx (lora_acc2)
                 a0, a1 = bf16_view(ab[0], dy.dtype), bf16_view(ab[2], dy.dtype)
                 p0, p1 = branches[0].dropout, branches[1].dropout
-                fused_ok = (_LORA_EPI and wb.shape[1] % 128 == 0 and all(g.shape[1] % 8 == 0 and g.shape[1] <= 32
-                                                                           for g in g_list))
-                if fused_ok and isinstance(wb, torch.Tensor) and _g4w_ok(dy, wb, True, lora=True):
+                fused_ok = wb.shape[1] % 128 == 0 and all(g.shape[1] % 8 == 0 and g.shape[1] <= 32 for g in g_list)
+                if fused_ok and isinstance(wb, torch.Tensor) and _g4w_ok(dy, wb, True):
                     # the masked LoRA input gradient inside the dX GEMM's epilogue (no lora_dx2 matrix)
+                    _count("gemm4w")
                     dx = native().gemm4w_loradx(dy, wb, None, 0, g_list, [a0, a1], ctx.masks, [p0, p1])
-                elif fused_ok and isinstance(wb, NF4Weight) and _w4_ok(dy, wb, True, lora=True):
+                elif fused_ok and isinstance(wb, NF4Weight) and _w4_ok(dy, wb, True):
                     codes, sc = wb.g4w_pack()
+                    _count("gemm4w-nf4")
                     dx = native().gemm4w_loradx(dy, codes, sc, wb.shape[1], g_list, [a0, a1], ctx.masks, [p0, p1])
                 else:
                     c = native().lora_dx2(g_list[0], g_list[1], a0, a1, ctx.masks, p0, p1)
@@ -886,12 +832,13 @@ def _multi_backward(ctx, dy, x, weight, xa_list, base, branches, dense, dest):
             eb = torch.cat(a_list, 0)
             dx = _base_gemm_t(dy, wb, ea, F.pad(eb, (0, 0, 0, ea.shape[1] - eb.shape[0])).t().contiguous())
         else:
-            fused = (_LORA_EPI and nb <= 2 and wb.shape[1] % 128 == 0
-                     and all(g.shape[1] == g_list[0].shape[1] for g in g_list))
-            if fused and isinstance(wb, torch.Tensor) and _g4w_ok(dy, wb, True, lora=True):
+            fused = nb <= 2 and wb.shape[1] % 128 == 0 and all(g.shape[1] == g_list[0].shape[1] for g in g_list)
+            if fused and isinstance(wb, torch.Tensor) and _g4w_ok(dy, wb, True):
+                _count("gemm4w")
                 dx = native().gemm4w_loradx(dy, wb, None, 0, g_list, a_list, masks, ps)
-            elif fused and isinstance(wb, NF4Weight) and _w4_ok(dy, wb, True, lora=True):
+            elif fused and isinstance(wb, NF4Weight) and _w4_ok(dy, wb, True):
                 codes, sc = wb.g4w_pack()
+                _count("gemm4w-nf4")
                 dx = native().gemm4w_loradx(dy, codes, sc, wb.shape[1], g_list, a_list, masks, ps)
             else:
                 c = native().lora_dxc(g_list, a_list, masks, ps)
@@ -936,5 +883,6 @@ def fused_linear(x: torch.Tensor, base, bias: torch.Tensor | None = None,
         y = _FusedLinearFn.apply(x2.contiguous(), None if res2 is None else res2.contiguous(),
                                  weight, bias, (base, tuple(branches), training), *ab)
     else:
+        _count("library")
         y = _reference(x2, base, bias, branches, res2, training)
     return y.view(*shape[:-1], y.shape[-1])

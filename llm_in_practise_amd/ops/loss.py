@@ -15,7 +15,7 @@ import torch.nn.functional as F
 
 from . import reference as ref
 from ._native import native, use_native
-from .linear import _g4w_ok
+from .linear import _count, _g4w_ok
 
 
 def cross_entropy(logits, labels, ignore_index: int = -100):
@@ -39,15 +39,15 @@ class _FusedLinearCEFn(torch.autograd.Function):
         loss = torch.zeros((), dtype=torch.float32, device=h.device)
         for s in range(0, T, chunk):
             hc = h[s:s + chunk]
-            # the LM head keeps gemm4w under the hybrid GEMM default (lora=True: "gemm4w on"): tie with the
-            # library at the tuned step's 2048 rows, ~2 ms/step faster at the faithful micro-step's 1024
-            # (profiles/r4/gemm_hybrid_ab.txt)
-            g4w = _g4w_ok(hc, weight, False, lora=True)
+            g4w = _g4w_ok(hc, weight, False)
+            _count("gemm4w" if g4w else "library")
             logits = native().gemm4w(hc, weight, None, 0, False) if g4w else hc @ weight.t()
             g0, g1 = s // rows_g, (s + hc.shape[0]) // rows_g
             row_loss = native().ce_fwd_bwd(logits, labels[s:s + chunk], ignore_index, inv[g0:g1])
             loss += (row_loss.view(g1 - g0, -1).sum(1) * inv[g0:g1]).sum()
-            if g4w and _g4w_ok(logits, weight, True, lora=True):
+            dx_g4w = g4w and _g4w_ok(logits, weight, True)
+            _count("gemm4w" if dx_g4w else "library")
+            if dx_g4w:
                 dhc = native().gemm4w(logits, weight, None, 0, True)
                 if hc.shape[0] == T:
                     dh = dhc
@@ -76,6 +76,7 @@ def fused_linear_cross_entropy(h: torch.Tensor, weight: torch.Tensor, labels: to
         need_w = weight.requires_grad
         return _FusedLinearCEFn.apply(h.contiguous(), weight, labels.contiguous(), ignore_index, chunk, need_w,
                                       groups)
+    _count("library")
     logits = h.float() @ weight.float().t()
     if groups == 1:
         return F.cross_entropy(logits, labels, ignore_index=ignore_index)

@@ -25,7 +25,7 @@ import torch
 
 from ..quant.nf4 import NF4Weight
 from ._native import native
-from .linear import _LT_MIN_M, _g4w_on, _nf4_expand, _nf4_w4, sac_put, sac_take
+from .linear import _MIN_M, _count, _nf4_expand, _nf4_w4, sac_put, sac_take
 
 
 def _operand(base, reused: bool):
@@ -37,10 +37,14 @@ def _operand(base, reused: bool):
     return base.contiguous(), None
 
 
+def _form(scale) -> str:
+    return "gemm4w" if scale is None else "gemm4w-nf4"
+
+
 def fusable(x: torch.Tensor, gu_base, down_base, F: int, K: int) -> bool:
-    if not (_g4w_on() and x.is_cuda and x.dtype == torch.bfloat16 and F % 64 == 0 and K % 64 == 0):
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and F % 64 == 0 and K % 64 == 0):
         return False
-    if x.numel() // x.shape[-1] < _LT_MIN_M:
+    if x.numel() // x.shape[-1] < _MIN_M:
         return False
     for b, shape in ((gu_base, (2 * F, K)), (down_base, (K, F))):
         if isinstance(b, NF4Weight):
@@ -65,6 +69,8 @@ class _SwiGLUMLPFn(torch.autograd.Function):
             gu, y = replay
         else:
             F = gu_base.shape[0] // 2
+            _count(_form(s_gu))
+            _count(_form(s_d))
             gu, h = native().gemm4w_swiglu(x, w_gu, s_gu, F)
             y = native().gemm4w(h, w_d, residual, 0, False, 0, 0, s_d, K)
             sac_put((gu, y))
@@ -79,6 +85,8 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         dx = None
         if ctx.w is not None:
             w_gu, s_gu, w_d, s_d, K = ctx.w
+            _count(_form(s_d))
+            _count(_form(s_gu))
             dgu = native().gemm4w_dswiglu(dy.contiguous(), w_d, gu, s_d)
             dx = native().gemm4w(dgu, w_gu, None, 0, True, 0, 0, s_gu, K)
         ctx.w = None

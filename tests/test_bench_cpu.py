@@ -54,6 +54,10 @@ def test_bench_json_contract_two_ranks(extra):
     assert abs(d["value"] - tokens / (d["ms_per_step"] * 2 / 1000)) / d["value"] < 0.02
     assert d["config"]["global_batch"] == 8
     assert d["config"]["parallelism"] == ("zero3-dp2" if "zero3" in extra else "dp2")
+    # kernel provenance: GEMM launches per step by form (CPU: every GEMM is the torch fallback)
+    c = d["config"]
+    assert c["gemm_backend"] == "torch-cpu" and c["gemm_launches_per_step"]["library"] > 0
+    assert "nf4_expansions_per_step" in c and c["gemm_launches_per_step"].get("gemm4w", 0) == 0
     _check_comm(d["comm"], "all_gather" if "zero3" in extra else "all_reduce")
     if "zero3" not in extra:       # the DDP headline carries BASELINE #4 (ZeRO-3) as a sub-record at world > 1
         _check_zero3(d["zero3"], 2)

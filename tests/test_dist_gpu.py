@@ -25,3 +25,27 @@ def test_bench_two_ranks_share_one_gpu(strategy):
     assert rec["value"] > 0 and rec["config"]["parallelism"].endswith("dp2")
     if strategy == "zero3":      # the client 8-bit AdamW runs on each rank's partition (E6)
         assert rec["config"]["optimizer"] == "zero3-paged_adamw_8bit"
+
+
+def _zero3_losses(extra):
+    env = dict(os.environ, LIPA_DIST_BACKEND="gloo", LIPA_SHARE_GPU="1", HSA_ENABLE_IPC_MODE_LEGACY="0",
+               PYTHONPATH=ROOT)
+    env.pop("LIPA_NF4_GEMM", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", "qwen3-small",
+                          "--steps", "2", "--warmup", "1", "--strategy", "zero3", "--nf4-gemm", "w4", *extra],
+                         env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["config"]["nf4_gemm"] == "w4"
+    return [float(x) for x in __import__("re").findall(r"loss=([0-9.]+)", out.stderr)]
+
+
+@pytest.mark.gpu
+def test_zero3_partitioned_nf4_bases_w4_match_replicated():
+    """ZeRO-3 with the frozen NF4 bases partitioned across ranks (stage3_partition_frozen_quant) in the
+    memory-lean w4 mode: the backward re-gathers the codes after release() and rebuilds the g4w pack —
+    the losses match the replicated-base run."""
+    rep = _zero3_losses([])
+    part = _zero3_losses(["--ds-config", os.path.join(ROOT, "configs", "ds_zero3_nf4_partition.json")])
+    assert len(rep) == len(part) == 2
+    assert all(abs(a - b) <= 1e-3 * abs(b) for a, b in zip(part, rep)), (part, rep)

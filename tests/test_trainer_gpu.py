@@ -86,9 +86,6 @@ def test_grad_ckpt_lora_dropout_same_gradients(native_ext, monkeypatch, targets,
     import llm_in_practise_amd.ops.linear as L
     from llm_in_practise_amd.ops.linear import seed_dropout
     monkeypatch.setenv("LIPA_DETERMINISTIC", "1")
-    # one GEMM form for both runs (the default hybrid mode takes gemm4w inside checkpointed layers and the
-    # library outside them: 1 % apart in bf16, which would hide a mask mismatch at this tolerance)
-    monkeypatch.setattr(L, "_GEMM_MODE", "native")
     grads = []
     for ck in (False, True):
         m = Qwen3ForCausalLM.from_config(qwen3_config("qwen3-small"), dtype=torch.bfloat16, device="cuda", seed=5)
@@ -118,8 +115,9 @@ def test_lora_pair_kernels_match_single_branch_path(native_ext, monkeypatch):
     torch.manual_seed(0)
     ids = torch.randint(0, 1000, (2, 64), device="cuda")
     res = {}
+    import llm_in_practise_amd.ops.linear as L
     for mode in ("0", "1"):
-        monkeypatch.setenv("LIPA_LORA_PAIR", mode)
+        monkeypatch.setattr(L, "_PAIR", mode == "1")
         pm = _qlora(seed=0)
         pm.train()
         seed_dropout(42)
