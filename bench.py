@@ -195,6 +195,9 @@ def main():
     ap.add_argument("--selective-steps", type=int, default=3,
                     help="after the faithful sub-record, time this many steps with the selective recompute policy "
                          "(GEMM outputs of the first forward kept, not recomputed) as the 'selective_ckpt' sub-record")
+    ap.add_argument("--host-steps", type=int, default=2,
+                    help="after the timed steps, issue this many steps onto an idle device and record the host "
+                         "launch time of one step (host_launch_ms; LIPA_HOST_PROFILE=<file> adds a cProfile of them)")
     args = ap.parse_args()
     from llm_in_practise_amd.ops import linear as _lin
     if args.nf4_gemm is not None:        # else the LIPA_NF4_GEMM environment choice stands
@@ -319,6 +322,33 @@ def main():
     log(f"[bench] loss={loss.item():.4f} {ms:.1f} ms/step  {tps:,.0f} tok/s  "
         f"~{tps * fl_per_tok / world / 1e12:.0f} TFLOP/s/GPU (matmul)  peak HBM {mem:.1f} GiB")
 
+    # host launch cost of one headline step (untimed, after the timed steps): the step is issued onto an idle
+    # device and timed until step() returns — how far the Python/launch side is from becoming the bottleneck
+    host_ms = None
+    if args.host_steps > 0:
+        prof = None
+        if os.environ.get("LIPA_HOST_PROFILE"):
+            import cProfile
+            prof = cProfile.Profile()
+        hs = []
+        for _ in range(args.host_steps):
+            sync()
+            h0 = time.perf_counter()
+            if prof is not None:
+                prof.enable()
+            step()
+            if prof is not None:
+                prof.disable()
+            hs.append(time.perf_counter() - h0)
+            gcm.step()
+        sync()
+        host_ms = round(1000 * min(hs), 2)
+        log(f"[bench] host launch time of one step: {host_ms:.1f} ms (device {ms:.1f} ms/step)")
+        if prof is not None and D.is_main():
+            import pstats
+            with open(os.environ["LIPA_HOST_PROFILE"], "w") as f:
+                pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(60)
+
     def timed_ckpt(policy: str, n_steps: int) -> dict:
         """BASELINE.md's config as the reference runs it (Fine-Tuning/qwen3-8b-qlora-dist.py:137-138, 162-163):
         gradient checkpointing on and the GA micro-steps one after another (no_sync on all but the last), same
@@ -372,6 +402,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 2),
+            "host_launch_ms": host_ms,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(tps / BASELINE_TOKENS_PER_S, 3) if BASELINE_TOKENS_PER_S else None),

@@ -320,6 +320,232 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(const bf16* __restrict__ Q,
   }
 }
 
+// ============================================================================ forward, D = 128
+// The 32x32x16 form.  Same contract as attn_fwd_k (128 queries per workgroup, 4 waves × 32, 64-key K/V
+// tiles register-staged one tile ahead), but:
+//  * Sᵀ = K·Qᵀ with v_mfma_f32_32x32x16_bf16: a lane owns ONE query (column lane&31) and 32 of the tile's 64
+//    keys; the row max is lane-local + one v_permlane32_swap with the other half (no ds_bpermute), the row
+//    sum stays a per-lane partial until the epilogue;
+//  * P feeds Oᵀ += Vᵀ·Pᵀ as the B operand with no lane movement: the k-slot order of each 16-key step is the
+//    accumulator's row order (keys +{0-3, 8-11} in the low half, +{4-7, 12-15} in the high half) and the
+//    transposed V reads (ds_read_b64_tr_b16) fetch exactly those rows;
+//  * K and V tiles are one XOR-swizzled image each (256-B rows, chunk ^ ((row&3)<<2 | (row>>2)&3)): the
+//    row-wise ds_read_b128 of K and the transposed reads of V are both conflict-free;
+//  * deferred rescale: the running max moves only when a tile's max exceeds it by more than 2^8 in the
+//    exponent (P ≤ 256 in bf16, l and O in fp32 see the same factor), so O is rarely rescaled;
+//  * a wave skips the MFMAs of tiles wholly above its causal diagonal;
+//  * the output rows are stored 16 B per lane after a permlane32 exchange of the accumulator halves.
+__device__ __forceinline__ int swz128(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+// byte offset of 16-B chunk `ch` of row `row` in a [64][128 × bf16] tile image
+__device__ __forceinline__ int toff(int row, int ch) { return 256 * row + 16 * (ch ^ swz128(row)); }
+
+// lanes 32-63 of `a` trade places with lanes 0-31 of `b` (v_permlane32_swap): afterwards the low half holds
+// (a_lo, a_hi→b) and the high half (b_lo→a, b_hi) — see the callers for the element bookkeeping
+__device__ __forceinline__ void swap32(float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+
+template <int PF, bool DROP>
+__global__ __launch_bounds__(256, 2) void attn_fwd128_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
+                                                     const bf16* __restrict__ V, int ldq, int ldk, int ldv,
+                                                     const int* __restrict__ kv_lens, const int* __restrict__ q_offs,
+                                                     bf16* __restrict__ O, float* __restrict__ lse, int Sq, int Skv,
+                                                     int kv_rows, int hq, int hkv, int causal, float scale_log2,
+                                                     DropParams dp) {
+  constexpr int D = 128, TB = 64 * 256;   // bytes per K or V tile image
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB];   // K0 V0 K1 V1
+  const int nqb = (Sq + 127) / 128;
+  int i0, h, b;
+  xcd_grid3_lpt(i0, h, b, causal >> 1);
+  const int qb = nqb - 1 - i0;   // heavy (late, causal) blocks first
+  const int hk = h / (hq / hkv);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r32 = lane & 31, hi = lane >> 5;
+  const int q0w = qb * 128 + 32 * w;   // this wave's first query
+  const int qa = q0w + r32;            // this lane's query
+  const int qoff = q_offs ? q_offs[b] : 0;
+  const int kvlen = min(kv_lens ? kv_lens[b] : Skv, Skv);
+  const size_t tok0 = (size_t)b * Sq, ktok0 = (size_t)b * kv_rows;
+
+  // Q as the B operand of Sᵀ = K·Qᵀ: lane (q, hi) holds Q[q][16ds + 8hi + j]
+  bf16x8 qf[8];
+  {
+    const int qc = qa < Sq ? qa : Sq - 1;
+    const bf16* qp = Q + (tok0 + qc) * ldq + h * D + 8 * hi;
+#pragma unroll
+    for (int ds = 0; ds < 8; ++ds) qf[ds] = *reinterpret_cast<const bf16x8*>(qp + 16 * ds);
+  }
+  int kend = causal ? min(Skv, qoff + qb * 128 + 128) : Skv;
+  kend = min(kend, kvlen);
+  const int nt = (kend + 63) / 64;
+  const int wend = causal ? min(kend, qoff + q0w + 32) : kend;   // keys any query of this wave may see
+  const int ntw = wend > 0 ? (wend + 63) / 64 : 0;
+  const int klim = min(causal ? qoff + qa : Skv - 1, kvlen - 1);  // last key this query may see
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  bf16x8 kr[PF][4], vr[PF][4];
+  const int row0 = tid >> 4, ch0 = tid & 15;   // this thread's tile rows row0 + 16p, chunk ch0
+  auto load_tile = [&](int set, int t) {
+    if (t * 64 + 64 <= Skv) {   // whole tile in range: one base address, row steps as offsets
+      const bf16* kp = K + (ktok0 + t * 64 + row0) * ldk + hk * D + ch0 * 8;
+      const bf16* vp = V + (ktok0 + t * 64 + row0) * ldv + hk * D + ch0 * 8;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        kr[set][p] = *reinterpret_cast<const bf16x8*>(kp + (size_t)(16 * p) * ldk);
+        vr[set][p] = *reinterpret_cast<const bf16x8*>(vp + (size_t)(16 * p) * ldv);
+      }
+      return;
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const size_t key = ktok0 + min(t * 64 + row0 + 16 * p, Skv - 1);
+      kr[set][p] = *reinterpret_cast<const bf16x8*>(K + key * ldk + hk * D + ch0 * 8);
+      vr[set][p] = *reinterpret_cast<const bf16x8*>(V + key * ldv + hk * D + ch0 * 8);
+    }
+  };
+  auto store_tile = [&](int set, int buf) {
+    char* Kl = smem + buf * 2 * TB;
+    char* Vl = Kl + TB;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      *reinterpret_cast<bf16x8*>(Kl + toff(row0 + 16 * p, ch0)) = kr[set][p];
+      *reinterpret_cast<bf16x8*>(Vl + toff(row0 + 16 * p, ch0)) = vr[set][p];
+    }
+  };
+  // transposed-read geometry (T10): lane 4q'+p' of 16-lane group g addresses row q' of a 4-row block,
+  // chunk 2(g&1) + (p'>>1) of the 32-column d block, half p'&1 of it
+  const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+
+  if (nt > 0) load_tile(0, 0);
+  if (PF == 2 && nt > 1) load_tile(PF - 1, 1);
+  for (int t2 = 0; t2 < nt; t2 += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = t2 + u;
+      if (t >= nt) break;
+      const int set = PF == 2 ? u : 0;
+      store_tile(set, u);
+      __syncthreads();
+      if (t + PF < nt) load_tile(set, t + PF);
+      if (t >= ntw) continue;   // wave-uniform: every key of the tile is above this wave's diagonal
+      const char* Kl = smem + u * 2 * TB;
+      const char* Vl = Kl + TB;
+      const int k0 = t * 64;
+      // ---- Sᵀ[key][q]: keys k0 + 32kh + (r&3) + 8(r>>2) + 4hi of accumulator element r
+      f32x16 sc[2];
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc[kh][r] = 0.f;
+#pragma unroll
+        for (int ds = 0; ds < 8; ++ds) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kl + toff(32 * kh + r32, 2 * ds + hi));
+          sc[kh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], sc[kh], 0, 0, 0);
+        }
+      }
+      const bool need_mask = (causal && k0 + 63 > qoff + q0w) || (k0 + 64 > kvlen);
+      if (need_mask) {
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * hi;
+            sc[kh][r] = key <= klim ? sc[kh][r] : -INFINITY;
+          }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kh][r]);
+      {
+        float a = mx, c = mx;
+        swap32(a, c);           // a = the low half's max, c = the high half's, in every lane
+        mx = fmaxf(a, c);
+      }
+      const float mn = fmaxf(m_run, mx);
+      const bool resc = (mn - m_run) * scale_log2 > 8.f;   // false while every key so far is masked (NaN)
+      if (__any(resc)) {
+        const float alpha = resc ? fexp2((m_run - mn) * scale_log2) : 1.f;
+        m_run = resc ? mn : m_run;
+        l_run *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) acc[dt] *= alpha;
+      }
+      const float mc = m_run == -INFINITY ? 0.f : m_run * scale_log2;
+      float rs = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fexp2(fmaf(sc[kh][r], scale_log2, -mc));
+          sc[kh][r] = p;
+          rs += p;
+        }
+      l_run += rs;   // this half's keys only; the halves are summed in the epilogue
+      if (DROP) {
+        const uint32_t bh = (uint32_t)(b * hq + h);
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * hi;
+            sc[kh][r] = drop_hash(dp.s0, dp.s1, bh, qa, key) >= dp.thresh ? sc[kh][r] * dp.rinv : 0.f;
+          }
+      }
+      // ---- Oᵀ[d][q] += Vᵀ[d][key]·Pᵀ[key][q], 16 keys per step: P elements 8u..8u+7 are the step's k-slots
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int u2 = 0; u2 < 2; ++u2) {
+          bf16x8 pb;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pb[j] = (bf16)sc[kh][8 * u2 + j];
+          const int ra = 32 * kh + 16 * u2 + 4 * (g >> 1) + qq;
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) {
+            const int ch = 4 * dt + 2 * (g & 1) + (pp >> 1);
+            const bf16x8 vf = cat8(tr_read((const bf16*)(Vl + toff(ra, ch) + 8 * (pp & 1))),
+                                   tr_read((const bf16*)(Vl + toff(ra + 8, ch) + 8 * (pp & 1))));
+            acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb, acc[dt], 0, 0, 0);
+          }
+        }
+    }
+  }
+  // ---- epilogue: l over both halves; O rows 16 B per lane after exchanging accumulator quarters
+  float la = l_run, lb = l_run;
+  swap32(la, lb);
+  const float lt = la + lb;
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  bf16* orow = O + (tok0 + (qa < Sq ? qa : 0)) * (size_t)(hq * D) + h * D + 8 * hi;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      // elements 8hf + j: d = 32dt + 16hf + 4hi + j (j < 4) and + 8 (j >= 4); after the swap lane-half hi
+      // holds d = 32dt + 16hf + 8hi + 0..7
+      float a[4], c[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[j] = acc[dt][8 * hf + j] * inv;
+        c[j] = acc[dt][8 * hf + 4 + j] * inv;
+        swap32(a[j], c[j]);
+      }
+      if (qa < Sq)
+        *reinterpret_cast<bf16x8*>(orow + 32 * dt + 16 * hf) =
+            bf16x8{(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)c[0], (bf16)c[1], (bf16)c[2], (bf16)c[3]};
+    }
+  if (hi == 0 && qa < Sq)
+    lse[((size_t)b * hq + h) * Sq + qa] = lt > 0.f ? (m_run * scale_log2 + log2f(lt)) * 0.6931471805599453f : INFINITY;
+}
+
 // ============================================================================ backward
 // Two atomic-free kernels (FA2 split).  Both recompute P from the saved log-sum-exp.
 //  * attn_bwd_dq_k : workgroup = 64 queries of one q-head (4 waves × 16, one query per lane, so
@@ -479,6 +705,160 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(const bf16* __restrict__
   }
 }
 
+
+// dQ for D = 128 in the 32x32x16 form of attn_fwd128_k: 128 queries per workgroup (4 waves × 32), a lane owns
+// one query (lse and delta are lane constants).  Per 64-key tile and 32-key half: Sᵀ = K·Qᵀ and dPᵀ = V·dOᵀ
+// (row reads of the swizzled K / V images), dS = P∘(dP − delta) in registers, dQᵀ += Kᵀ·dSᵀ with Kᵀ from the
+// transposed reads of the same K image and dS as the B operand in accumulator-row slot order (no lane
+// movement).  Writes delta for the dK/dV kernel, as attn_bwd_dq_k.
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq128_k(const bf16* __restrict__ dO, const bf16* __restrict__ O,
+                                                        const bf16* __restrict__ Q, const bf16* __restrict__ K,
+                                                        const bf16* __restrict__ V, const float* __restrict__ lse,
+                                                        float* __restrict__ delta, const int* __restrict__ kv_lens,
+                                                        int ldq, int ldk, int ldv, bf16* __restrict__ dQ, int S,
+                                                        int hq, int hkv, int causal, float scale, float scale_log2,
+                                                        DropParams drp) {
+  constexpr int D = 128, TB = 64 * 256;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB];   // K0 V0 K1 V1
+  const int nqb = (S + 127) / 128;
+  int i0, h, b;
+  xcd_grid3_lpt(i0, h, b, causal >> 1);
+  const int qb = nqb - 1 - i0;
+  const int hk = h / (hq / hkv);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r32 = lane & 31, hi = lane >> 5;
+  const int q0w = qb * 128 + 32 * w, qa = q0w + r32, qc = qa < S ? qa : S - 1;
+  const int kvlen = min(kv_lens ? kv_lens[b] : S, S);
+  const size_t tok0 = (size_t)b * S, ldo = (size_t)hq * D;
+  const size_t bh = ((size_t)b * hq + h) * S;
+
+  bf16x8 qf[8], dof[8];
+  float dsum = 0.f;
+  {
+    const bf16* qp = Q + (tok0 + qc) * ldq + h * D + 8 * hi;
+    const size_t off = (tok0 + qc) * ldo + h * D + 8 * hi;
+#pragma unroll
+    for (int ds = 0; ds < 8; ++ds) {
+      qf[ds] = *reinterpret_cast<const bf16x8*>(qp + 16 * ds);
+      dof[ds] = *reinterpret_cast<const bf16x8*>(dO + off + 16 * ds);
+      const bf16x8 of = *reinterpret_cast<const bf16x8*>(O + off + 16 * ds);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dsum += (float)dof[ds][j] * (float)of[j];
+    }
+  }
+  {
+    float a = dsum, c = dsum;
+    swap32(a, c);
+    dsum = a + c;
+  }
+  if (hi == 0 && qa < S) delta[bh + qa] = dsum;
+  const float lse2 = lse[bh + qc] * LOG2E;
+  const int klim = min(causal ? qa : S - 1, kvlen - 1);   // last key this query may see
+  int kend = causal ? min(S, qb * 128 + 128) : S;
+  kend = min(kend, kvlen);
+  const int nt = (kend + 63) / 64;
+  const int wend = causal ? min(kend, q0w + 32) : kend;
+  const int ntw = wend > 0 ? (wend + 63) / 64 : 0;
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
+
+  bf16x8 kr[4], vr[4];
+  const int row0 = tid >> 4, ch0 = tid & 15;   // this thread's tile rows row0 + 16p, chunk ch0
+  auto load_tile = [&](int t) {   // (a separate whole-tile fast path spills here: 256 VGPRs)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const size_t key = tok0 + min(t * 64 + row0 + 16 * p, S - 1);
+      kr[p] = *reinterpret_cast<const bf16x8*>(K + key * ldk + hk * D + ch0 * 8);
+      vr[p] = *reinterpret_cast<const bf16x8*>(V + key * ldv + hk * D + ch0 * 8);
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* Kl = smem + buf * 2 * TB;
+    char* Vl = Kl + TB;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      *reinterpret_cast<bf16x8*>(Kl + toff(row0 + 16 * p, ch0)) = kr[p];
+      *reinterpret_cast<bf16x8*>(Vl + toff(row0 + 16 * p, ch0)) = vr[p];
+    }
+  };
+  const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+
+  if (nt > 0) load_tile(0);
+  for (int t2 = 0; t2 < nt; t2 += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = t2 + u;
+      if (t >= nt) break;
+      store_tile(u);
+      __syncthreads();
+      if (t + 1 < nt) load_tile(t + 1);
+      if (t >= ntw) continue;
+      const char* Kl = smem + u * 2 * TB;
+      const char* Vl = Kl + TB;
+      const int k0 = t * 64;
+      const bool need_mask = (causal && k0 + 63 > q0w) || (k0 + 64 > kvlen);
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        f32x16 s, dp;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
+#pragma unroll
+        for (int ds = 0; ds < 8; ++ds) {
+          const int o = toff(32 * kh + r32, 2 * ds + hi);
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kl + o);
+          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(Vl + o);
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, dof[ds], dp, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * hi;
+          float p = fexp2(fmaf(s[r], scale_log2, -lse2));
+          if (need_mask) p = key <= klim ? p : 0.f;
+          float d = dp[r];
+          if (DROP) d = drop_hash(drp.s0, drp.s1, (uint32_t)(b * hq + h), qa, key) >= drp.thresh ? d * drp.rinv : 0.f;
+          s[r] = p * (d - dsum);
+        }
+        // dQᵀ[d][q] += Kᵀ[d][key]·dSᵀ[key][q]
+#pragma unroll
+        for (int u2 = 0; u2 < 2; ++u2) {
+          bf16x8 pb;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pb[j] = (bf16)s[8 * u2 + j];
+          const int ra = 32 * kh + 16 * u2 + 4 * (g >> 1) + qq;
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) {
+            const int ch = 4 * dt + 2 * (g & 1) + (pp >> 1);
+            const bf16x8 kt = cat8(tr_read((const bf16*)(Kl + toff(ra, ch) + 8 * (pp & 1))),
+                                   tr_read((const bf16*)(Kl + toff(ra + 8, ch) + 8 * (pp & 1))));
+            acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt, pb, acc[dt], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+  // ---- dQ = scale · acc, 16 B per lane after the permlane32 exchange (as attn_fwd128_k's epilogue)
+  bf16* qrow = dQ + (tok0 + (qa < S ? qa : 0)) * ldo + h * D + 8 * hi;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      float a[4], c[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[j] = acc[dt][8 * hf + j] * scale;
+        c[j] = acc[dt][8 * hf + 4 + j] * scale;
+        swap32(a[j], c[j]);
+      }
+      if (qa < S)
+        *reinterpret_cast<bf16x8*>(qrow + 32 * dt + 16 * hf) =
+            bf16x8{(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)c[0], (bf16)c[1], (bf16)c[2], (bf16)c[3]};
+    }
+}
 
 // HALVES = 2: a 512-thread workgroup, the two 4-wave halves sweep different q-heads of the GQA
 // group over the SAME 64 keys (2 waves per SIMD instead of 1) and meet in LDS at the end.
@@ -741,12 +1121,12 @@ static DropParams make_drop(float p, uint64_t seed) {
   return d;
 }
 
-#define LIPA_ATTN_D(D, ...)                 \
+// the head dims below 128 (128 has its own 32x32x16 forward / dQ kernels)
+#define LIPA_ATTN_D3(D, ...)                \
   switch (D) {                              \
     case 32: { constexpr int DD = 32; __VA_ARGS__; } break;   \
     case 64: { constexpr int DD = 64; __VA_ARGS__; } break;   \
-    case 96: { constexpr int DD = 96; __VA_ARGS__; } break;   \
-    default: { constexpr int DD = 128; __VA_ARGS__; } break;  \
+    default: { constexpr int DD = 96; __VA_ARGS__; } break;   \
   }
 
 // register prefetch depth per kernel (measured, profiles/attention_fwd_bwd.txt, re-checked after the LDS
@@ -762,11 +1142,21 @@ void launch_attn_fwd(const void* q, const void* k, const void* v, int ldq, int l
   const int qt = 2;
   dim3 grid((Sq + 64 * qt - 1) / (64 * qt), hq, B), blk(256);
   const float sl2 = scale * LOG2E;
+  if (D == 128) {   // the 32x32x16 form (attn_fwd128_k); other head dims: attn_fwd_k
+#define F128(DR)                                                                                              \
+  attn_fwd128_k<1, DR><<<grid, blk, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, ldq, ldk, ldv, kv_lens, \
+                                             q_offs, (bf16*)o, lse, Sq, Skv, kv_rows, hq, hkv,                    \
+                                             causal ? 1 | (attn_lpt() << 1) : 0, sl2, dp)
+    if (dp.thresh) F128(true); else F128(false);
+#undef F128
+    LIPA_CHECK_LAUNCH();
+    return;
+  }
 #define FWD(PFV, QTV)                                                                                      \
-  LIPA_ATTN_D(D, attn_fwd_k<DD, PFV, QTV><<<grid, blk, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,  \
-                                                           ldq, ldk, ldv, kv_lens, q_offs, (bf16*)o, lse, Sq, Skv, \
-                                                           kv_rows, hq, hkv, causal ? 1 | (attn_lpt() << 1) : 0, sl2, dp))
-  FWD(1, 2);
+  attn_fwd_k<DD, PFV, QTV><<<grid, blk, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v,                 \
+                                                ldq, ldk, ldv, kv_lens, q_offs, (bf16*)o, lse, Sq, Skv,          \
+                                                kv_rows, hq, hkv, causal ? 1 | (attn_lpt() << 1) : 0, sl2, dp)
+  LIPA_ATTN_D3(D, FWD(1, 2));
 #undef FWD
   LIPA_CHECK_LAUNCH();
 }
@@ -795,7 +1185,18 @@ void launch_attn_bwd(const void* dout, const void* q, const void* k, const void*
                                              (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dq, S, hq, \
                                              hkv, causal ? 1 | (attn_lpt() << 1) : 0, scale, sl2, dp);            \
   DKV(DD, PFKV);
-  LIPA_ATTN_D(D, RUN(DD, 2, 1));   // prefetch depth dQ 2, dK/dV 1
+  if (D == 128) {   // dQ in the 32x32x16 form (attn_bwd_dq128_k), dK/dV in the 8-wave 16x16x32 form
+    dim3 gq2((S + 127) / 128, hq, B);
+#define DQ2(DR)                                                                                                  \
+  attn_bwd_dq128_k<DR><<<gq2, blk, 0, st>>>((const bf16*)dout, (const bf16*)o, (const bf16*)q, (const bf16*)k,   \
+                                            (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dq, S, hq, \
+                                            hkv, causal ? 1 | (attn_lpt() << 1) : 0, scale, sl2, dp)
+    if (dp.thresh) DQ2(true); else DQ2(false);
+#undef DQ2
+    DKV(128, 1);
+  } else {
+    LIPA_ATTN_D3(D, RUN(DD, 2, 1));   // prefetch depth dQ 2, dK/dV 1
+  }
 #undef RUN
 #undef DKV
   if (nsplit > 0) {

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--hq", type=int, default=32)
     ap.add_argument("--hkv", type=int, default=8)
     ap.add_argument("--d", type=int, default=128)
+    ap.add_argument("--no-sdpa", action="store_true", help="skip the torch SDPA comparison")
+    ap.add_argument("--iters", type=int, default=50)
     a = ap.parse_args()
     B, S, hq, hkv, d = a.B, a.S, a.hq, a.hkv, a.d
     ext = native()
@@ -44,9 +46,13 @@ def main():
     scale = 1 / math.sqrt(d)
     o, lse = ext.attn_fwd(q, k, v, None, B, S, hq, hkv, d, True, scale)
     do = torch.randn_like(o)
-    t_f = timeit(lambda: ext.attn_fwd(q, k, v, None, B, S, hq, hkv, d, True, scale))
-    t_b = timeit(lambda: ext.attn_bwd(do, q, k, v, o, lse, None, B, S, hq, hkv, d, True, scale, 0.0, 0))
+    t_f = timeit(lambda: ext.attn_fwd(q, k, v, None, B, S, hq, hkv, d, True, scale), a.iters)
+    t_b = timeit(lambda: ext.attn_bwd(do, q, k, v, o, lse, None, B, S, hq, hkv, d, True, scale, 0.0, 0), a.iters)
     fl = 4 * B * hq * S * S * d / 2  # causal fwd
+    if a.no_sdpa:
+        print(json.dumps({"shape": [B, S, hq, hkv, d], "ours_fwd_us": round(t_f, 1), "ours_bwd_us": round(t_b, 1),
+                          "ours_fwd_TFs": round(fl / t_f / 1e6, 1), "ours_bwd_TFs": round(2.5 * fl / t_b / 1e6, 1)}))
+        return
     qs = q.view(B, S, hq, d).transpose(1, 2)
     ks = k.reshape(B, S, hkv, d).transpose(1, 2).repeat_interleave(hq // hkv, 1).contiguous()
     vs = v.reshape(B, S, hkv, d).transpose(1, 2).repeat_interleave(hq // hkv, 1).contiguous()

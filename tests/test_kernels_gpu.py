@@ -335,24 +335,46 @@ def test_flash_attention_fwd_bwd(native_ext, B, S, hq, hkv, d, causal):
     assert rel_err(dv.view(B, S, hkv, d), gv) < 2e-2
 
 
-@pytest.mark.parametrize("S", [128, 87])
-def test_flash_attention_padding(native_ext, S):
+@pytest.mark.parametrize("S,d", [(128, 64), (87, 64), (200, 128)])
+def test_flash_attention_padding(native_ext, S, d):
     """right-padded keys (kv_lens) in the forward AND backward, incl. a ragged tail tile"""
-    B, h, d = 2, 4, 64
+    B, h = 2, 4
     q = torch.randn(B * S, h * d, device=DEV).to(torch.bfloat16)
     k = torch.randn(B * S, h * d, device=DEV).to(torch.bfloat16)
     v = torch.randn(B * S, h * d, device=DEV).to(torch.bfloat16)
     lens = torch.tensor([S - 28, S], device=DEV, dtype=torch.int32)
-    o, lse = native_ext.attn_fwd(q, k, v, lens, B, S, h, h, d, True, 0.125)
+    sc = 1 / math.sqrt(d)
+    o, lse = native_ext.attn_fwd(q, k, v, lens, B, S, h, h, d, True, sc)
     mask = torch.arange(S, device=DEV)[None] < lens[:, None]
     do = torch.randn_like(o)
-    orf, gq, gk, gv = _attn_ref_grads(q, k, v, do, B, S, h, h, d, True, 0.125, mask=mask)
+    orf, gq, gk, gv = _attn_ref_grads(q, k, v, do, B, S, h, h, d, True, sc, mask=mask)
     assert rel_err(o.view(B, S, h, d)[mask], orf[mask]) < 1e-2
-    dq, dk, dv = native_ext.attn_bwd(do, q, k, v, o, lse, lens, B, S, h, h, d, True, 0.125, 0.0, 0)
+    dq, dk, dv = native_ext.attn_bwd(do, q, k, v, o, lse, lens, B, S, h, h, d, True, sc, 0.0, 0)
     assert rel_err(dq.view(B, S, h, d)[mask], gq[mask]) < 2e-2
     assert rel_err(dk.view(B, S, h, d)[mask], gk[mask]) < 2e-2
     assert rel_err(dv.view(B, S, h, d)[mask], gv[mask]) < 2e-2
     assert dk.view(B, S, h, d)[~mask].abs().max() == 0
+
+
+@pytest.mark.parametrize("gain", [1.0, 6.0])
+def test_flash_attention_lse_and_rescale(native_ext, gain):
+    """the forward's log-sum-exp against the fp32 reference, with scores large enough (gain 6) that the
+    running max moves by more than the deferred-rescale threshold inside a row"""
+    B, S, hq, hkv, d = 2, 384, 8, 2, 128
+    q = (torch.randn(B * S, hq * d, device=DEV) * gain).to(torch.bfloat16)
+    k = torch.randn(B * S, hkv * d, device=DEV).to(torch.bfloat16)
+    v = torch.randn(B * S, hkv * d, device=DEV).to(torch.bfloat16)
+    scale = 1 / math.sqrt(d)
+    o, lse = native_ext.attn_fwd(q, k, v, None, B, S, hq, hkv, d, True, scale)
+    qh = q.float().view(B, S, hq, d).transpose(1, 2)
+    kh = k.float().view(B, S, hkv, d).transpose(1, 2).repeat_interleave(hq // hkv, 1)
+    vh = v.float().view(B, S, hkv, d).transpose(1, 2).repeat_interleave(hq // hkv, 1)
+    sc = (qh @ kh.transpose(-1, -2) * scale).masked_fill(torch.ones(S, S, dtype=torch.bool, device=DEV).triu(1),
+                                                        float("-inf"))
+    want_lse = torch.logsumexp(sc, -1)                                  # [B, H, S]
+    want_o = (torch.softmax(sc, -1) @ vh).transpose(1, 2)
+    assert (lse.view(B, hq, S) - want_lse).abs().max().item() < 2e-2 * max(1.0, gain)
+    assert rel_err(o.view(B, S, hq, d), want_o) < 1e-2
 
 
 def _drop_keep(seed, B, H, S, p):
