@@ -44,6 +44,10 @@ void lt_reset();
 void launch_sum_slices(const void*, void*, int, size_t, size_t, hipStream_t);
 void launch_gemm_skinny(const void*, int, const void*, const void*, void*, float*, int, int, int, int, hipStream_t);
 bool w4mm_supported(int, int, int, int);
+bool w4g_supported(int, int, int, int);
+int w4g_splits(int, int, int);
+void launch_w4g(const void*, int, const uint8_t*, const float*, int, const void*, void*, float*, int, int, int, int,
+                hipStream_t);
 int w4mm_nkb(int, int, int);
 void launch_w4mm(const void*, int, const uint8_t*, const float*, int, const void*, void*, float*, int, int, int, int,
                  hipStream_t);
@@ -545,6 +549,36 @@ Tensor w4mm(Tensor x, Tensor codes, Tensor sc2, int64_t N, int64_t gs, optional<
   return out;
 }
 
+// The decode-batch tiling of the same W4A16 GEMM (w4mm.hip w4g_k): 1 <= M <= 64, same operands as w4mm.
+bool w4g_ok(int64_t M, int64_t N, int64_t K, int64_t gs) { return w4g_supported((int)M, (int)N, (int)K, (int)gs); }
+
+Tensor w4g(Tensor x, Tensor codes, Tensor sc2, int64_t N, int64_t gs, optional<Tensor> residual, int64_t ks) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_CONTIG(codes); CHECK_CONTIG(sc2);
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "w4g: x row-major, 16-B aligned rows");
+  TORCH_CHECK(w4g_supported((int)M, (int)N, (int)K, (int)gs), "w4g: M<=64, N%128, K%128, gs%128");
+  TORCH_CHECK(codes.scalar_type() == at::kByte && codes.numel() == N * K / 2, "w4g: codes [N, K/2] uint8");
+  TORCH_CHECK(sc2.scalar_type() == at::kFloat && sc2.numel() == N * (K / gs) * 2, "w4g: sc2 fp32 [N, K/gs, 2]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(codes.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(sc2.data_ptr()) % 8 == 0,
+              "w4g: aligned operands");
+  const void* rp = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    CHECK_BF16((*residual));
+    CHECK_CONTIG((*residual));
+    TORCH_CHECK(residual->size(0) == M && residual->size(1) == N, "w4g: residual shape");
+    rp = residual->data_ptr();
+  }
+  const int s = ks > 0 ? (int)ks : w4g_splits((int)M, (int)N, (int)K);
+  TORCH_CHECK((K / 128) % s == 0, "w4g: K/128 divisible by the K-slice count");
+  Tensor out = at::empty({M, N}, x.options());
+  Tensor part;
+  if (s > 1) part = at::empty({s, M, N}, x.options().dtype(at::kFloat));
+  launch_w4g(x.data_ptr(), (int)x.stride(0), codes.data_ptr<uint8_t>(), sc2.data_ptr<float>(), (int)gs, rp,
+             out.data_ptr(), s > 1 ? part.data_ptr<float>() : nullptr, (int)M, (int)N, (int)K, s, stream());
+  return out;
+}
+
 // codes [N, K/2] u8 (bnb layout), absmax fp32 [N*K/64] (decoded) → bf16 [N, K]
 // affine int4 codes [N, K/2] + fp32 scale / bias tables [N, K/g] -> bf16 [N, K] (quant/int4.py layout)
 Tensor int4_dequant(Tensor codes, Tensor sc, Tensor bi, int64_t N, int64_t K, int64_t group) {
@@ -642,6 +676,13 @@ static G4wB g4w_operand(const Tensor& w, const optional<Tensor>& wscale, int64_t
 
 bool gemm4w_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, bool bt, bool w4) {
   return M < (1ll << 31) && N < (1ll << 31) && K < (1ll << 31) && gemm4w_supported(M, N, K, lda, ldb, bt, w4);
+}
+
+// the cost model's choice for a plain gemm4w call (host-only: no device needed): (splits, bn, bm)
+std::vector<int64_t> gemm4w_plan_info(int64_t M, int64_t N, int64_t K, bool bt, bool w4) {
+  int bn = 0, bm = 0;
+  const int sp = gemm4w_plan((int)M, (int)N, (int)K, bt, 0, 0, &bn, 0, &bm, w4);
+  return {sp, bn, bm};
 }
 
 // y = x·wᵀ (+ residual) through the one-wave-per-SIMD AGPR-accumulator MFMA GEMM (gemm4w.hip);
@@ -1666,8 +1707,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("w4mm", &w4mm, py::arg("x"), py::arg("codes"), py::arg("sc2"), py::arg("N"), py::arg("gs"),
         py::arg("residual") = py::none(), py::arg("nkb") = 0);
   m.def("w4mm_ok", &w4mm_ok);
+  m.def("w4g", &w4g, py::arg("x"), py::arg("codes"), py::arg("sc2"), py::arg("N"), py::arg("gs"),
+        py::arg("residual") = py::none(), py::arg("ks") = 0);
+  m.def("w4g_ok", &w4g_ok);
+  m.def("w4g_splits", &w4g_splits);
   m.def("set_dequant_variant", &set_dequant_variant);
   m.def("gemm4w_ok", &gemm4w_ok);
+  m.def("gemm4w_plan_info", &gemm4w_plan_info);
   m.def("g4w_pack", &g4w_pack);
   m.def("gemm4w_lora", &gemm4w_lora);
   m.def("gemm4w_loradx", &gemm4w_loradx, py::arg("dy"), py::arg("w"), py::arg("wscale"), py::arg("n_w4"), py::arg("gs"),

@@ -194,7 +194,169 @@ __global__ __launch_bounds__(256) void w4mm_reduce_k(const float* __restrict__ p
   *reinterpret_cast<bf16x2*>(out + i) = o;
 }
 
+// ============================================================================ w4g: 32 < M <= 64
+// The same dequant and group fold, tiled for decode batches: a workgroup owns BM = 16·RT rows × BN = 64·CT
+// columns (4 waves × 16·CT, each wave every row) over a K slice of nkb 128-deep blocks.  x is streamed per
+// block through a double-buffered LDS tile (permuted to the dequant's k order), x, the codes and (scale, c)
+// pairs PD blocks ahead in a register ring — so x crosses L2→LDS once per column span (not once per K-slice × span
+// as in w4mm), each code dword feeds RT MFMAs, and PD·CT·16 B per lane of codes stay in flight.  Σx per (row,
+// block) for the zero-point fold is one more MFMA chain against a ones operand (no cross-lane reduction).
+// Split-K (KS > 1) writes fp32 partials for w4mm_reduce_k.  Measured (profiles/r5/w4g_decode.txt): ahead of
+// w4mm and gemm4w W4=2 on the Qwen3-8B projections at M = 33..64; at M = 128 / 256 gemm4w W4=2 wins (the
+// per-block fold and x restaging scale with the rows), and prefetching 3 blocks instead of 2 loses.
+template <int RT, int CT, int PD>
+__global__ __launch_bounds__(256, 2) void w4g_k(const bf16* __restrict__ X, int ldx, const uint8_t* __restrict__ codes,
+                                                const float2* __restrict__ sc, int gs, const bf16* __restrict__ residual,
+                                                bf16* __restrict__ out, float* __restrict__ part, int M, int N, int K,
+                                                int ncs, int nrb, int nkb) {
+  constexpr int BM = 16 * RT, LDXS = 128 + 8;   // 272-B rows: the 16 rows of a ds_read_b128 group hit distinct banks
+  constexpr int NR = PD + 1;                    // code ring depth
+  __shared__ __attribute__((aligned(16))) bf16 xs[2][BM * LDXS];
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int cs = id % ncs, rb = (id / ncs) % nrb, ks = id / (ncs * nrb);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, li = lane & 15, q = lane >> 4;
+  const int m0 = rb * BM, kb0 = ks * nkb;
+  const int G = K / gs;
+  const uint8_t* cp[CT];
+  const float2* sp[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int n = cs * (64 * CT) + 16 * CT * w + 16 * ct + li;
+    cp[ct] = codes + (size_t)n * (K / 2) + 16 * q;
+    sp[ct] = sc + (size_t)n * G;
+  }
+
+  u32x4 cq[NR][CT];
+  float2 s2[NR][CT];
+  auto load_codes = [&](int set, int kb) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      cq[set][ct] = *reinterpret_cast<const u32x4*>(cp[ct] + (size_t)kb * 64);
+      s2[set][ct] = sp[ct][kb * 128 / gs];
+    }
+  };
+  // x block: BM rows × 16 chunks of 16 B, RT chunks per thread, in the same ring as the codes
+  u32x4 xr[NR][RT];
+  auto load_x = [&](int set, int kb) {
+#pragma unroll
+    for (int p = 0; p < RT; ++p) {
+      const int r = 16 * p + (tid >> 4), kc = tid & 15;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (m0 + r < M) v = *reinterpret_cast<const u32x4*>(X + (size_t)(m0 + r) * ldx + kb * 128 + 8 * kc);
+      xr[set][p] = v;
+    }
+  };
+  auto store_x = [&](int set, int buf) {
+#pragma unroll
+    for (int p = 0; p < RT; ++p) {
+      const int r = 16 * p + (tid >> 4), kc = tid & 15;
+      *reinterpret_cast<u32x4*>(xs[buf] + r * LDXS + 8 * kc) = x_perm(xr[set][p]);
+    }
+  };
+
+  f32x4 acc[CT][RT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[ct][rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.f;
+
+  // blocks 0..PD-1 in flight; block 0's x staged
+#pragma unroll
+  for (int d = 0; d < PD; ++d)
+    if (d < nkb) {
+      load_codes(d, kb0 + d);
+      load_x(d, kb0 + d);
+    }
+  store_x(0, 0);
+  __syncthreads();
+  for (int i0 = 0; i0 < nkb; i0 += NR) {
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {   // static ring slot u = block i % NR
+      const int i = i0 + u;
+      if (i >= nkb) break;
+      if (i + PD < nkb) {
+        load_codes((u + PD) % NR, kb0 + i + PD);
+        load_x((u + PD) % NR, kb0 + i + PD);
+      }
+      const int buf = i & 1;
+      bf16x8 bq[CT][4];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bq[ct][j] = i4_bf16(cq[u][ct][j]);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        bf16x8 xa[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          xa[j] = *reinterpret_cast<const bf16x8*>(xs[buf] + (16 * rt + li) * LDXS + 32 * q + 8 * j);
+        f32x4 ax = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[0], ones, zero, 0, 0, 0);   // Σx, rows 4q..4q+3
+#pragma unroll
+        for (int j = 1; j < 4; ++j) ax = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[j], ones, ax, 0, 0, 0);
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          f32x4 g = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[0], bq[ct][0], zero, 0, 0, 0);
+#pragma unroll
+          for (int j = 1; j < 4; ++j) g = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[j], bq[ct][j], g, 0, 0, 0);
+          const float sv = s2[u][ct].x, c = s2[u][ct].y;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[ct][rt][e] = fmaf(sv, g[e], fmaf(c, ax[e], acc[ct][rt][e]));
+        }
+      }
+      if (i + 1 < nkb) store_x((u + 1) % NR, buf ^ 1);   // block i+1 (loaded PD-1 blocks ago) into the buffer block i-1 used
+      __syncthreads();
+    }
+  }
+  // lane holds y[m = m0 + 16·rt + 4q + e][n]
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + 16 * rt + 4 * q + e, n = cs * (64 * CT) + 16 * CT * w + 16 * ct + li;
+        if (m >= M) continue;
+        if (!part) {
+          float v = acc[ct][rt][e];
+          if (residual) v += (float)residual[(size_t)m * N + n];
+          out[(size_t)m * N + n] = (bf16)v;
+        } else {
+          part[((size_t)ks * M + m) * N + n] = acc[ct][rt][e];
+        }
+      }
+}
+
 }  // namespace
+
+bool w4g_supported(int M, int N, int K, int gs) {
+  return M >= 1 && M <= 64 && N % 128 == 0 && K % 128 == 0 && gs % 128 == 0 && K % gs == 0;
+}
+
+// K slices: the fewest (halving the 128-deep blocks per workgroup, at least 2 left) that put >= 256 workgroups
+// on the 256 CUs (BN = 128: 32 columns per wave; 64 per wave halves the x re-reads of wide N but spills)
+int w4g_splits(int M, int N, int K) {
+  const int ncs = N / 128, kb = K / 128;
+  int ks = 1;
+  while (ncs * ks < 256 && kb % (2 * ks) == 0 && kb / (2 * ks) >= 2) ks *= 2;
+  return ks;
+}
+
+void launch_w4g(const void* X, int ldx, const uint8_t* codes, const float* sc2, int gs, const void* res, void* out,
+                float* part, int M, int N, int K, int ks, hipStream_t st) {
+  const int ncs = N / 128, nkb = K / 128 / ks, grid = ncs * ks;
+  w4g_k<4, 2, 2><<<grid, 256, 0, st>>>((const bf16*)X, ldx, codes, (const float2*)sc2, gs,
+                                       ks > 1 ? nullptr : (const bf16*)res, (bf16*)out, ks > 1 ? part : nullptr, M, N,
+                                       K, ncs, 1, nkb);
+  if (ks > 1) {
+    const size_t MN = (size_t)M * N;
+    w4mm_reduce_k<8><<<(MN / 2 + 255) / 256, 256, 0, st>>>(part, (const bf16*)res, (bf16*)out, ks, MN);
+  }
+  LIPA_CHECK_LAUNCH();
+}
 
 bool w4mm_supported(int M, int N, int K, int gs) {
   return M >= 1 && M <= 64 && N % W4_COLS == 0 && K % 128 == 0 && gs % 128 == 0 && K % gs == 0;

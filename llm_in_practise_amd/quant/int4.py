@@ -231,15 +231,19 @@ def from_awq(d: dict, group_size: int) -> Int4Weight:
 
 
 # ============================================================================ module + op
-# W4A16 kernel per row count (measured on the Qwen3-8B projection shapes, profiles/r4/w4a16_w4mm.txt):
-#   M <= 2    gemv_w4 (csrc/kernels/gemv.hip): weight-streaming GEMV, no matrix-core padding;
-#   3 .. 32   w4mm (csrc/kernels/w4mm.hip): byte-permute dequant, MFMA, per-group scale folded after it;
-#   > 32      gemm4w with the affine table expanded in-kernel (csrc/kernels/gemm4w.hip, W4 = 2);
-#   >= 1024   prefill: one HBM-speed bf16 expansion (int4_dequant_k, 6.6 TB/s) into a transient copy + the
-#             bf16 library GEMM — at these row counts the in-kernel table costs more than the expansion
-#             (per layer at M = 2048: 708 -> 639 µs; profiles/r4/w4a16_prefill.txt);
+# W4A16 kernel per row count (measured on the Qwen3-8B projection shapes, profiles/r4/w4a16_w4mm.txt,
+# profiles/r5/w4g_decode.txt):
+#   M <= 2      gemv_w4 (csrc/kernels/gemv.hip): weight-streaming GEMV, no matrix-core padding;
+#   3 .. 32     w4mm (csrc/kernels/w4mm.hip): byte-permute dequant, MFMA, per-group scale folded after it;
+#   33 .. 64    w4g (w4mm.hip w4g_k): the same dequant / fold tiled for decode batches — x streamed per
+#               128-deep block through LDS once per column span, codes two blocks ahead in registers;
+#   65 .. 1023  gemm4w with the affine table expanded in-kernel (csrc/kernels/gemm4w_kernel.h, W4 = 2);
+#   >= 1024     prefill: one HBM-speed bf16 expansion (int4_dequant_k, 6.6 TB/s) into a transient copy + the
+#               gemm4w bf16 GEMM (ops/linear.py _base_gemm) — at these row counts the in-kernel table costs more
+#               than the expansion (per layer at M = 2048: 708 -> 639 µs; profiles/r4/w4a16_prefill.txt);
 # anything the kernels do not take: one bf16 dequantisation + torch matmul.
 _W4MM_MAX = 32
+_W4G_MAX = 64
 _EXPAND_MIN = 1024
 
 
@@ -257,10 +261,13 @@ def int4_linear(x: torch.Tensor, w: Int4Weight, bias: torch.Tensor | None = None
         y = native().gemv_w4(x2.contiguous(), w.codes, s, b, n, w.group_size, r2)
     elif nat and M <= _W4MM_MAX and native().w4mm_ok(M, n, k, w.group_size):
         y = native().w4mm(x2.contiguous(), w.codes, w.w4mm_table(), n, w.group_size, r2)
+    elif nat and M <= _W4G_MAX and native().w4g_ok(M, n, k, w.group_size):
+        y = native().w4g(x2.contiguous(), w.codes, w.w4mm_table(), n, w.group_size, r2)
     elif nat and M >= _EXPAND_MIN and k % w.group_size == 0 and w.group_size % 8 == 0:
+        from ..ops.linear import _base_gemm
         s, b = w.gemv_tables()
         wb = native().int4_dequant(w.codes, s, b, n, k, w.group_size)
-        y = torch.addmm(r2, x2, wb.t()) if r2 is not None else x2 @ wb.t()
+        y = _base_gemm(x2, wb, residual=r2)
         del wb
     elif nat and w.g4w_ok():
         codes, st, zt = w.g4w_pack()

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """W4A16 decode-batch GEMM microbenchmark (Qwen3-8B projection shapes): bf16 (hipBLASLt, gemm4w) vs the
 int4 kernels — gemv_w4 (M <= 8), w4mm (M <= 64, byte-permute dequant + MFMA, per-K-slice-count columns),
-gemm4w W4=2 (affine table expanded in-kernel).  Prints one JSON line per (shape, M)."""
+w4g (M <= 256, the same dequant tiled for decode batches, per-K-slice-count columns), gemm4w W4=2 (affine table expanded in-kernel).  Prints one JSON line per (shape, M)."""
 import json
 import os
 import sys
@@ -57,6 +57,14 @@ def main():
                 for nkb in (1, 2, 4, 8):
                     if (K // 128) % nkb == 0:
                         row[f"w4mm_nkb{nkb}_us"] = round(timeit(lambda: nat.w4mm(x, q.codes, sc2, N, 128, None, nkb)), 2)
+            if nat.w4g_ok(M, N, K, 128):
+                row["w4g_us"] = round(timeit(lambda: nat.w4g(x, q.codes, sc2, N, 128, None, 0)), 2)
+                y = nat.w4g(x, q.codes, sc2, N, 128, None, 0)
+                row["w4g_relerr"] = float(((y.float() - ref).norm() / ref.norm()).item())
+                row["w4g_ks"] = nat.w4g_splits(M, N, K)
+                for ks in (1, 2, 4, 8):
+                    if (K // 128) % ks == 0 and ks != row["w4g_ks"]:
+                        row[f"w4g_ks{ks}_us"] = round(timeit(lambda: nat.w4g(x, q.codes, sc2, N, 128, None, ks)), 2)
             if M > 8:
                 row["g4w_int4_us"] = round(timeit(lambda: nat.gemm4w(x, gc, None, 0, False, 0, 0, gst, N, gzt)), 2)
             if M >= 128:   # the prefill form: one bf16 expansion + the bf16 gemm4w

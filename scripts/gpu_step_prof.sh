@@ -12,6 +12,6 @@ timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d $OUT -o run --
 rc=$?
 echo "rocprof rc=$rc"; tail -2 $OUT/bench.log
 f=$(find $OUT -name "*kernel_trace.csv" | head -1)
-[ -n "$f" ] && python3 $R/scripts/step_timeline.py "$f" --marker "${MARKER:-adamw8bit}" > $OUT/timeline.txt && head -60 $OUT/timeline.txt
+[ -n "$f" ] && python3 $R/scripts/step_timeline.py "$f" --marker "${MARKER:-adamw8bit}" --skip "${SKIP:-1}" > $OUT/timeline.txt && head -60 $OUT/timeline.txt
 rm -f "$f"
 exit $rc

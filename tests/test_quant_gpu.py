@@ -30,15 +30,34 @@ def test_gemv_nf4_and_int4(native_ext, M, N, K):
 
 @pytest.mark.parametrize("N,K,gs,sym", [(256, 512, 128, False), (384, 1024, 128, True), (96, 256, 64, False)])
 def test_int4_linear_dispatch(native_ext, N, K, gs, sym):
-    """Every row count through int4_linear's kernel choice — gemv_w4 (M <= 2), w4mm (3..32), gemm4w W4=2
-    (larger), the dequant fallback for shapes no kernel takes (N = 96) — against fp32, with residual."""
+    """Every row count through int4_linear's kernel choice — gemv_w4 (M <= 2), w4mm (3..32), w4g (33..64),
+    gemm4w W4=2 (65..1023), the expansion + gemm4w prefill (>= 1024), the dequant fallback for shapes no kernel
+    takes (N = 96) — against fp32, with residual."""
     torch.manual_seed(4)
     w = quantize_rtn(torch.randn(N, K, device=DEV), gs, sym)
-    for M in (1, 2, 3, 8, 32, 33, 64, 300, 2048):
+    for M in (1, 2, 3, 8, 32, 33, 64, 100, 256, 300, 2048):
         x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
         res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
         assert rel(int4_linear(x, w), x.float() @ w.dequantize().t()) < 1e-2, M
         assert rel(int4_linear(x, w, residual=res), x.float() @ w.dequantize().t() + res.float()) < 1e-2, M
+
+
+@pytest.mark.parametrize("M", [33, 48, 64])
+@pytest.mark.parametrize("N,K,gs", [(6144, 4096, 128), (4096, 12288, 128), (512, 1024, 256)])
+def test_w4g_decode_batches(native_ext, M, N, K, gs):
+    """The decode-batch W4A16 GEMM (w4g) at the Qwen3-8B q|k|v / down shapes and a 256-deep group: every
+    K-slice count it may pick (1 = bf16 out + residual in-kernel, > 1 = fp32 partials + reduce) against fp32."""
+    torch.manual_seed(6)
+    w = quantize_rtn(torch.randn(N, K, device=DEV), gs, False)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    want = x.float() @ w.dequantize().t() + res.float()
+    auto = native_ext.w4g_splits(M, N, K)
+    for ks in sorted({1, 2, auto}):
+        if (K // 128) % ks:
+            continue
+        y = native_ext.w4g(x, w.codes, w.w4mm_table(), N, gs, res, ks)
+        assert y.shape == (M, N) and rel(y, want) < 1e-2, (ks, rel(y, want))
 
 
 @pytest.mark.parametrize("N,K,gs,sym", [(256, 512, 128, False), (384, 1024, 64, True)])

@@ -145,13 +145,15 @@ def test_trainer_zero3_saves_gathered_adapter(tmp_path):
     assert os.path.isdir(tmp_path / "checkpoint-2" / "global_step2")
 
 
-def test_dx_split_policy():
-    """K-slices for the dX GEMM: only long reductions into an output that leaves CUs idle, and the
-    fewest slices that give every CU a 256x256 tile (gate|up dX at M = 2048 -> 2)."""
-    from llm_in_practise_amd.ops.linear import _dx_split
-    t = lambda m, n, k: (torch.empty(m, n), torch.empty(n, k))  # noqa: E731  (dy [M, N], W [N, K])
-    assert _dx_split(*t(2048, 24576, 4096)) == 2      # gate|up: 128 tiles
-    assert _dx_split(*t(2048, 6144, 4096)) == 1       # qkv: reduction not 4x the output width
-    assert _dx_split(*t(2048, 4096, 12288)) == 1      # down: 384 tiles
-    assert _dx_split(*t(1024, 24576, 4096)) == 4      # 64 tiles -> 4 slices
-    assert _dx_split(*t(128, 24576, 4096)) == 1       # small M: no split
+def test_gemm4w_plan_policy():
+    """gemm4w's host cost model (gemm4w.hip gemm4w_cfg; no device needed): tile shape and split-K per role of
+    the Qwen3-8B step at M = 2048 — split only long reductions into an output that leaves CUs idle (gate|up dX,
+    down fwd: 128 256x256 tiles -> 2 slices), the transposed-B 256x192 tile where it makes whole rounds."""
+    from llm_in_practise_amd.ops._native import native
+    plan = lambda m, n, k, bt: tuple(native().gemm4w_plan_info(m, n, k, bt, False))  # noqa: E731  (splits, bn, bm)
+    assert plan(2048, 4096, 24576, True) == (2, 256, 256)     # gate|up dX
+    assert plan(2048, 4096, 12288, False) == (2, 256, 256)    # down fwd
+    assert plan(2048, 4096, 6144, True)[0] == 1               # q|k|v dX: reduction not long enough to split
+    assert plan(2048, 6144, 4096, False) == (1, 192, 256)     # q|k|v fwd: 8 x 32 = 256 tiles
+    assert plan(2048, 12288, 4096, True) == (1, 192, 256)     # down dX: 512 tiles = 2 whole rounds
+    assert plan(1024, 4096, 24576, True)[0] == 4              # 64 tiles -> 4 slices
