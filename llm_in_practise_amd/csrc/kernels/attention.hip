@@ -1106,9 +1106,12 @@ __global__ __launch_bounds__(256) void attn_dkv_fin_k(const float* __restrict__ 
 // scripts/experiments/gpu_dkv_split_ab.sh): [1, 2048, 32, 8, 128] bwd 283 -> 260 us; at the bench
 // shape [4, 512, ...] the 4-tile units' fixed cost and the fp32 partial round trip lose (92 -> 102 us),
 // hence the S threshold (still the best after the LDS re-pad: profiles/r4/attention_knobs_ab.txt, S = 2048 bwd 236 vs 262 us unsplit).
+// Also split when the unsplit grid would fill at most half the CUs (one 512-thread workgroup per CU): the
+// sequential-GA micro-batch [2, 512, 8 kv-heads] is 128 workgroups (profiles/r5/attention_dkv_split_b2.txt).
 int attn_dkv_nsplit(int B, int S, int hkv, int causal) {
   const int nb = (S + 63) / 64;
-  if (!causal || nb < 16 || (long)B * hkv * nb > 512) return 0;
+  const long grid = (long)B * hkv * nb;
+  if (!causal || nb < 2 || grid > 512 || (nb < 16 && grid > 128)) return 0;
   return nb - (nb + 1) / 2;   // kb with nb - kb > ceil(nb / 2)
 }
 

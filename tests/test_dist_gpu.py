@@ -17,14 +17,19 @@ def test_bench_two_ranks_share_one_gpu(strategy):
     env = dict(os.environ, LIPA_DIST_BACKEND="gloo", LIPA_SHARE_GPU="1", HSA_ENABLE_IPC_MODE_LEGACY="0",
                PYTHONPATH=ROOT)
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", "qwen3-small",
-                          "--steps", "2", "--warmup", "1", "--strategy", strategy],
+                          "--steps", "2", "--warmup", "1", "--strategy", strategy, "--faithful-steps", "1",
+                          "--selective-steps", "1", "--zero3-model", "qwen3-small", "--zero3-steps", "1"],
                          env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-3000:]
     rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["n_gpus"] == 2 and rec["config"]["dist_world_size"] == 2 and rec["config"]["dist_backend"] == "gloo"
     assert rec["value"] > 0 and rec["config"]["parallelism"].endswith("dp2")
+    assert rec["comm"]["exposed_ms_per_step"] >= 0 and 0.0 <= rec["comm"]["overlap_fraction"] <= 1.0
     if strategy == "zero3":      # the client 8-bit AdamW runs on each rank's partition (E6)
         assert rec["config"]["optimizer"] == "zero3-paged_adamw_8bit"
+    else:                        # world > 1 DDP: config #4's sub-record (ZeRO-3 engine) with its collectives
+        z = rec["zero3"]
+        assert z["value"] > 0 and z["ms_per_step"] > 0 and "all_gather" in json.dumps(z["comm"]), z
 
 
 def _zero3_losses(extra):
