@@ -369,9 +369,17 @@ def main():
         fms = 1000 * fel / n_steps
         ftps = args.micro_batch * args.seq_len * args.grad_accum * world * n_steps / fel
         fmem = torch.cuda.max_memory_allocated(device) / 2 ** 30 if device.type == "cuda" else 0.0
+        fhost = None
+        if args.host_steps > 0:     # host issue time of one such step onto an idle device (untimed, after)
+            sync()
+            h0 = time.perf_counter()
+            step(fused=0)
+            fhost = round(1000 * (time.perf_counter() - h0), 2)
+            gcm.step()
+            sync()
         log(f"[bench] grad ckpt ({policy}) + sequential GA: loss={floss.item():.4f} {fms:.1f} ms/step  "
-            f"{ftps:,.0f} tok/s  peak HBM {fmem:.1f} GiB")
-        return {"value": round(ftps, 1), "unit": "tokens/s", "ms_per_step": round(fms, 2),
+            f"{ftps:,.0f} tok/s  peak HBM {fmem:.1f} GiB  host {fhost} ms/step")
+        return {"value": round(ftps, 1), "unit": "tokens/s", "ms_per_step": round(fms, 2), "host_launch_ms": fhost,
                 "steps": n_steps, "warmup": args.faithful_warmup,
                 "gradient_checkpointing": True, "ga_execution": "sequential",
                 "gradient_checkpointing_kwargs": {"use_reentrant": bool(args.ckpt_reentrant)},

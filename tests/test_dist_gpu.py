@@ -24,7 +24,9 @@ def test_bench_two_ranks_share_one_gpu(strategy):
     rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["n_gpus"] == 2 and rec["config"]["dist_world_size"] == 2 and rec["config"]["dist_backend"] == "gloo"
     assert rec["value"] > 0 and rec["config"]["parallelism"].endswith("dp2")
-    assert rec["comm"]["exposed_ms_per_step"] >= 0 and 0.0 <= rec["comm"]["overlap_fraction"] <= 1.0
+    # gloo on one device: the wait is host time, no comm-stream events, so no overlap fraction (RCCL runs time both)
+    ov = rec["comm"]["overlap_fraction"]
+    assert rec["comm"]["exposed_ms_per_step"] >= 0 and (ov is None or 0.0 <= ov <= 1.0)
     if strategy == "zero3":      # the client 8-bit AdamW runs on each rank's partition (E6)
         assert rec["config"]["optimizer"] == "zero3-paged_adamw_8bit"
     else:                        # world > 1 DDP: config #4's sub-record (ZeRO-3 engine) with its collectives
