@@ -82,8 +82,8 @@ class FlatParams:
     def sync_grads(self):
         """Copy grads that autograd allocated separately (low-precision params) into the flat
         buffer.  fp32 params accumulate straight into their views."""
-        # pointer compare only: slicing a view of the flat buffer per parameter cost ~3 us each
-        # (0.2-0.4 ms of host time per step with 144 LoRA tensors, visible as GPU idle)
+        # pointer compare only: slicing a view of the flat buffer per parameter cost ~3 us each (an fp32
+        # param's grad is separate only after something set it to None, e.g. zero_grad(set_to_none=True))
         for p, o, ptr in zip(self.params, self.offsets, self.grad_ptrs):
             g = p.grad
             if g is None or g.data_ptr() == ptr:
@@ -140,8 +140,13 @@ class _FlatOptimizer:
         return self.flat.grad
 
     def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
-        """Global L2 norm of the flat grads + clip coefficient, on the device."""
+        """Global L2 norm of the flat grads + clip coefficient, on the device.  The host-side step preparation
+        (separately allocated grads folded into the flat buffer — which the norm must include — and the NF4
+        expansion cache released) runs here, before the norm launches, so step() is one launch per group
+        right behind them."""
         self.max_grad_norm = max_norm
+        nf4_cache_advance()
+        self.flat.sync_grads()
         g = self.flat.grad
         if use_native(g):
             native().grad_norm(g, float(max_norm), self.norm_out, False)

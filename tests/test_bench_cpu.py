@@ -58,6 +58,8 @@ def test_bench_json_contract_two_ranks(extra):
     c = d["config"]
     assert c["gemm_backend"] == "torch-cpu" and c["gemm_launches_per_step"]["library"] > 0
     assert "nf4_expansions_per_step" in c and c["gemm_launches_per_step"].get("gemm4w", 0) == 0
+    # host issue time of one step onto an idle device (a measure of launch-boundness; CPU: the whole step)
+    assert d["host_launch_ms"] is None or d["host_launch_ms"] > 0
     _check_comm(d["comm"], "all_gather" if "zero3" in extra else "all_reduce")
     if "zero3" not in extra:       # the DDP headline carries BASELINE #4 (ZeRO-3) as a sub-record at world > 1
         _check_zero3(d["zero3"], 2)
