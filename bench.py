@@ -195,6 +195,9 @@ def main():
     ap.add_argument("--selective-steps", type=int, default=3,
                     help="after the faithful sub-record, time this many steps with the selective recompute policy "
                          "(GEMM outputs of the first forward kept, not recomputed) as the 'selective_ckpt' sub-record")
+    ap.add_argument("--selective-reentrant", type=int, default=1,
+                    help="the selective_ckpt sub-record's checkpoint form (1: reentrant, this framework's choice; the "
+                         "faithful record follows --ckpt-reentrant, the reference's use_reentrant=False)")
     ap.add_argument("--host-steps", type=int, default=2,
                     help="after the timed steps, issue this many steps onto an idle device and record the host "
                          "launch time of one step (host_launch_ms; LIPA_HOST_PROFILE=<file> adds a cProfile of them)")
@@ -349,12 +352,14 @@ def main():
             with open(os.environ["LIPA_HOST_PROFILE"], "w") as f:
                 pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(60)
 
-    def timed_ckpt(policy: str, n_steps: int) -> dict:
+    def timed_ckpt(policy: str, n_steps: int, reentrant: bool) -> dict:
         """BASELINE.md's config as the reference runs it (Fine-Tuning/qwen3-8b-qlora-dist.py:137-138, 162-163):
         gradient checkpointing on and the GA micro-steps one after another (no_sync on all but the last), same
         model / optimizer / data, timed the same way as the headline.  policy "full" = HF's whole-layer
-        recompute (use_reentrant=False, as the reference passes); "selective" = this framework's cheaper recompute."""
-        model.gradient_checkpointing_enable({"use_reentrant": bool(args.ckpt_reentrant), "policy": policy})
+        recompute (use_reentrant=False, as the reference passes); "selective" = this framework's cheaper recompute,
+        in the reentrant form by default (no saved-tensor pack / unpack hooks: ~20 ms less host time per step,
+        which the selective step — 73 ms of GPU work — would otherwise wait on)."""
+        model.gradient_checkpointing_enable({"use_reentrant": reentrant, "policy": policy})
         for _ in range(args.faithful_warmup):
             step(fused=0)
         sync()
@@ -371,27 +376,43 @@ def main():
         fmem = torch.cuda.max_memory_allocated(device) / 2 ** 30 if device.type == "cuda" else 0.0
         fhost = None
         if args.host_steps > 0:     # host issue time of one such step onto an idle device (untimed, after)
+            prof = None
+            if os.environ.get("LIPA_HOST_PROFILE_CKPT") == policy:   # cProfile it, backward on this thread
+                import cProfile
+                prof = cProfile.Profile()
+                torch.autograd.set_multithreading_enabled(False)
             sync()
             h0 = time.perf_counter()
+            if prof is not None:
+                prof.enable()
             step(fused=0)
+            if prof is not None:
+                prof.disable()
             fhost = round(1000 * (time.perf_counter() - h0), 2)
             gcm.step()
             sync()
+            if prof is not None:
+                torch.autograd.set_multithreading_enabled(True)
+                if D.is_main():
+                    import pstats
+                    with open(os.environ.get("LIPA_HOST_PROFILE", "host_profile_ckpt.txt"), "w") as f:
+                        pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(50)
+                        pstats.Stats(prof, stream=f).sort_stats("cumulative").print_stats(40)
         log(f"[bench] grad ckpt ({policy}) + sequential GA: loss={floss.item():.4f} {fms:.1f} ms/step  "
             f"{ftps:,.0f} tok/s  peak HBM {fmem:.1f} GiB  host {fhost} ms/step")
         return {"value": round(ftps, 1), "unit": "tokens/s", "ms_per_step": round(fms, 2), "host_launch_ms": fhost,
                 "steps": n_steps, "warmup": args.faithful_warmup,
                 "gradient_checkpointing": True, "ga_execution": "sequential",
-                "gradient_checkpointing_kwargs": {"use_reentrant": bool(args.ckpt_reentrant)},
+                "gradient_checkpointing_kwargs": {"use_reentrant": reentrant},
                 "checkpoint_policy": policy,
                 "micro_batch": args.micro_batch, "grad_accum": args.grad_accum, "peak_hbm_gib": round(fmem, 1)}
 
     faithful = selective = None
     if engine is None and not (args.grad_ckpt and not args.ga_fusion):
         if args.faithful_steps > 0:
-            faithful = timed_ckpt("full", args.faithful_steps)
+            faithful = timed_ckpt("full", args.faithful_steps, bool(args.ckpt_reentrant))
         if args.selective_steps > 0:
-            selective = timed_ckpt("selective", args.selective_steps)
+            selective = timed_ckpt("selective", args.selective_steps, bool(args.selective_reentrant))
 
     zero3 = None
     if world > 1 and engine is None and args.zero3_steps > 0:
