@@ -19,6 +19,8 @@
 
 #include "common.h"
 
+#include <cstdlib>
+
 using namespace lipa;
 
 namespace {
@@ -111,6 +113,16 @@ __device__ __forceinline__ void xcd_grid3_lpt(int& i0, int& i1, int& i2, int lpt
 // 1: longest-first (+ snake when the grid is resident) — measured best against the plain XCD-grouped
 // order (0) and longest-first only (2), profiles/r4/attention_knobs_ab.txt
 static int attn_lpt() { return 1; }
+
+// D = 128 dK/dV kernel: 1 = the 32x32x16 form (attn_bwd_dkv128_k), 0 = the 16x16x32 8-wave form
+// (LIPA_ATTN_DKV128=0, for A/B runs)
+static int attn_dkv128() {
+  static const int v = [] {
+    const char* e = std::getenv("LIPA_ATTN_DKV128");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
 
 // ============================================================================ forward
 // Sq queries per batch row attend to Skv keys (K/V rows of batch b start at b·kv_rows: a KV cache
@@ -860,6 +872,246 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq128_k(const bf16* __restric
     }
 }
 
+// dK / dV for D = 128 in the 32x32x16 form, two waves per SIMD: a 512-thread workgroup = 64 keys of one KV
+// head; wave w = (key half kw2 = w&1: 32 keys on the lanes, query half qh = (w>>1)&1: 32 of the tile's 64
+// queries, head half hw = w>>2: the GQA group's q-heads split even / odd).  The K / V images of the block sit
+// in LDS for the whole sweep (B operands of S = Q·Kᵀ and dP = dO·Vᵀ by row reads), each head half streams
+// its Q / dO tiles through one register-staged LDS buffer (loads of tile it+1 in flight during tile it);
+// dVᵀ += dOᵀ·P and dKᵀ += Qᵀ·dS take dOᵀ / Qᵀ from transposed reads of the same swizzled images and P / dS
+// as B operands in accumulator-row slot order.  The four waves of a key half meet in LDS at the end.
+// Split key blocks (nsplit) write fp32 partials as attn_bwd_dkv_k.  ~97 KB LDS, ≤ 256 VGPRs.
+template <bool DROP>
+__global__ __launch_bounds__(512, 1) void attn_bwd_dkv128_k(const bf16* __restrict__ dO, const bf16* __restrict__ Q,
+                                                         const bf16* __restrict__ K, const bf16* __restrict__ V,
+                                                         const float* __restrict__ lse,
+                                                         const float* __restrict__ delta,
+                                                         const int* __restrict__ kv_lens, int ldq, int ldk, int ldv,
+                                                         bf16* __restrict__ dK, bf16* __restrict__ dV, int S, int hq,
+                                                         int hkv, int causal, float scale, float scale_log2,
+                                                         DropParams drp, float* __restrict__ ws, int nsplit) {
+  constexpr int D = 128, TB = 64 * 256;
+  __shared__ __attribute__((aligned(16))) char smem[6 * TB];       // K | V | [head half][Q | dO]
+  __shared__ __attribute__((aligned(16))) float stat[2][2][64];    // [head half][lse | delta][q]
+  int ui, hk, b;
+  xcd_grid3(ui, hk, b);
+  int kbi, part;
+  if (ui < 2 * nsplit) {
+    kbi = ui >> 1;
+    part = ui & 1;
+  } else {
+    kbi = ui - nsplit;
+    part = -1;
+  }
+  const int rep = hq / hkv;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r32 = lane & 31, hi = lane >> 5;
+  const int kw2 = w & 1, qh = (w >> 1) & 1, hw = w >> 2, th = tid & 255;
+  const int kb0 = kbi * 64;
+  const int kw = kb0 + 32 * kw2 + r32;   // this lane's key
+  const int kvlen = min(kv_lens ? kv_lens[b] : S, S);
+  const size_t tok0 = (size_t)b * S, ldo = (size_t)hq * D, ldkv = (size_t)hkv * D;
+  char* const Kl = smem;
+  char* const Vl = smem + TB;
+  char* const Ql = smem + (2 + 2 * hw) * TB;
+  char* const dOl = Ql + TB;
+
+  // K / V images of the 64 keys (512 threads × 2 chunks each per tensor)
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int id = p * 512 + tid, row = id >> 4, ch = id & 15;
+    const size_t key = tok0 + min(kb0 + row, S - 1);
+    *reinterpret_cast<bf16x8*>(Kl + toff(row, ch)) = *reinterpret_cast<const bf16x8*>(K + key * ldk + hk * D + ch * 8);
+    *reinterpret_cast<bf16x8*>(Vl + toff(row, ch)) = *reinterpret_cast<const bf16x8*>(V + key * ldv + hk * D + ch * 8);
+  }
+  f32x16 dk[4], dv[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dk[dt][r] = dv[dt][r] = 0.f;
+
+  int qt0 = causal ? kbi : 0;
+  const int qmin = kw < kvlen ? (causal ? kw : 0) : 1 << 30;   // first query that sees this key
+  int nqt = (S + 63) / 64 - qt0;
+  if (part >= 0) {
+    const int h1 = (nqt + 1) / 2;
+    if (part == 0) {
+      nqt = h1;
+    } else {
+      qt0 += h1;
+      nqt -= h1;
+    }
+  }
+  const int nh = (rep + 1) / 2;
+  const int n_it = kb0 < kvlen ? nh * nqt : 0;
+
+  // staging: the head half's 256 threads load its Q / dO tile (4 chunks each per tensor) + 128 stats
+  bf16x8 qr[4], dr[4];
+  float st = 0.f;
+  const int row0 = th >> 4, ch0 = th & 15;   // rows row0 + 16p
+  auto load_it = [&](int it) {
+    const int j = hw + 2 * (it / nqt);
+    if (j >= rep) return;
+    const int h = hk * rep + j;
+    const int qa0 = (qt0 + it % nqt) * 64;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const size_t tq = tok0 + min(qa0 + row0 + 16 * p, S - 1);
+      qr[p] = *reinterpret_cast<const bf16x8*>(Q + tq * ldq + h * D + ch0 * 8);
+      dr[p] = *reinterpret_cast<const bf16x8*>(dO + tq * ldo + h * D + ch0 * 8);
+    }
+    if (th < 128) {
+      const int qs = qa0 + (th & 63);
+      const size_t bh = ((size_t)b * hq + h) * S + min(qs, S - 1);
+      st = th < 64 ? (qs < S ? lse[bh] * LOG2E : INFINITY) : delta[bh];   // rows past S: P = 0
+    }
+  };
+  auto store_it = [&]() {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      *reinterpret_cast<bf16x8*>(Ql + toff(row0 + 16 * p, ch0)) = qr[p];
+      *reinterpret_cast<bf16x8*>(dOl + toff(row0 + 16 * p, ch0)) = dr[p];
+    }
+    if (th < 128) stat[hw][th >> 6][th & 63] = st;
+  };
+  const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+
+  if (n_it > 0) load_it(0);
+  for (int it = 0; it < n_it; ++it) {
+    __syncthreads();          // the previous tile's reads are done (and, at it = 0, the K / V images are written)
+    store_it();
+    __syncthreads();
+    if (it + 1 < n_it) load_it(it + 1);
+    const int j = hw + 2 * (it / nqt);
+    if (j >= rep) continue;   // odd group size: the odd half has no head this round
+    const int qa0 = (qt0 + it % nqt) * 64;
+    if (causal && qa0 + 32 * qh + 31 < kb0 + 32 * kw2) continue;   // every query of this half precedes our keys
+    f32x16 s, dp;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
+#pragma unroll
+    for (int ds = 0; ds < 8; ++ds) {
+      const int oq = toff(32 * qh + r32, 2 * ds + hi), ok = toff(32 * kw2 + r32, 2 * ds + hi);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(Ql + oq),
+                                                 *reinterpret_cast<const bf16x8*>(Kl + ok), s, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(dOl + oq),
+                                                  *reinterpret_cast<const bf16x8*>(Vl + ok), dp, 0, 0, 0);
+    }
+    // element r is row q = qa0 + 32qh + 4hi + c(r), c(r) = (r&3) + 8(r>>2); causal: valid iff c(r) >= qmin − base
+    const bool need_mask = (causal && qa0 + 32 * qh < kb0 + 32 * kw2 + 32) || (kb0 + 64 > kvlen);
+    const int lo = qmin - (qa0 + 32 * qh + 4 * hi);
+    const float* Ls = stat[hw][0];
+    const float* Dls = stat[hw][1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x4 L = *reinterpret_cast<const f32x4*>(Ls + 32 * qh + 8 * i + 4 * hi);
+      const f32x4 Dl = *reinterpret_cast<const f32x4*>(Dls + 32 * qh + 8 * i + 4 * hi);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = 4 * i + e;
+        float p = fexp2(fmaf(s[r], scale_log2, -L[e]));
+        if (need_mask) p = (8 * i + e >= lo) ? p : 0.f;
+        if (DROP) {
+          const int q = qa0 + 32 * qh + 8 * i + 4 * hi + e;
+          const bool keep = drop_hash(drp.s0, drp.s1, (uint32_t)(b * hq + hk * rep + j), q, kw) >= drp.thresh;
+          dp[r] = p * ((keep ? dp[r] * drp.rinv : 0.f) - Dl[e]);
+          s[r] = keep ? p * drp.rinv : 0.f;
+        } else {
+          dp[r] = p * (dp[r] - Dl[e]);
+          s[r] = p;
+        }
+      }
+    }
+    // dVᵀ[d][key] += dOᵀ[d][q]·P[q][key] ; dKᵀ += Qᵀ·dS
+#pragma unroll
+    for (int u2 = 0; u2 < 2; ++u2) {
+      bf16x8 pb, db;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        pb[e] = (bf16)s[8 * u2 + e];
+        db[e] = (bf16)dp[8 * u2 + e];
+      }
+      const int ra = 32 * qh + 16 * u2 + 4 * (g >> 1) + qq;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int ch = 4 * dt + 2 * (g & 1) + (pp >> 1);
+        const int o0 = toff(ra, ch) + 8 * (pp & 1), o1 = toff(ra + 8, ch) + 8 * (pp & 1);
+        const bf16x8 ot = cat8(tr_read((const bf16*)(dOl + o0)), tr_read((const bf16*)(dOl + o1)));
+        const bf16x8 qt = cat8(tr_read((const bf16*)(Ql + o0)), tr_read((const bf16*)(Ql + o1)));
+        dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ot, pb, dv[dt], 0, 0, 0);
+        dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qt, db, dk[dt], 0, 0, 0);
+      }
+    }
+  }
+  // ---- the four waves of a key half (head half × query half) sum through LDS: query half 1 → 0, then head
+  // half 1 → 0, dK and dV in separate passes (a wave's 16 f32x4 per tensor = 16 KB per slot, 4 slots ≤ 96 KB)
+  f32x4* red = reinterpret_cast<f32x4*>(smem);
+  auto pass = [&](f32x16 (&a)[4], bool src, bool dst, int slot) {
+    __syncthreads();
+    if (src) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          red[((slot * 4 + dt) * 4 + i) * 64 + lane] = f32x4{a[dt][4 * i], a[dt][4 * i + 1], a[dt][4 * i + 2], a[dt][4 * i + 3]};
+    }
+    __syncthreads();
+    if (dst) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f32x4 c = red[((slot * 4 + dt) * 4 + i) * 64 + lane];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a[dt][4 * i + e] += c[e];
+        }
+    }
+  };
+  pass(dk, qh == 1, qh == 0, hw * 2 + kw2);
+  pass(dv, qh == 1, qh == 0, hw * 2 + kw2);
+  pass(dk, qh == 0 && hw == 1, qh == 0 && hw == 0, kw2);
+  pass(dv, qh == 0 && hw == 1, qh == 0 && hw == 0, kw2);
+  if (qh != 0 || hw != 0) return;
+  // ---- d = 32dt + (r&3) + 8(r>>2) + 4hi of element r
+  if (part >= 0) {   // split block: raw fp32 partials, planes [part][dK | dV][T][hkv·D]
+    if (kw >= S) return;
+    const size_t plane = (size_t)gridDim.z * S * ldkv;
+    float* wk = ws + (size_t)(2 * part) * plane + (tok0 + kw) * ldkv + hk * D + 4 * hi;
+    float* wv = wk + plane;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        *reinterpret_cast<f32x4*>(wk + 32 * dt + 8 * i) =
+            f32x4{dk[dt][4 * i], dk[dt][4 * i + 1], dk[dt][4 * i + 2], dk[dt][4 * i + 3]};
+        *reinterpret_cast<f32x4*>(wv + 32 * dt + 8 * i) =
+            f32x4{dv[dt][4 * i], dv[dt][4 * i + 1], dv[dt][4 * i + 2], dv[dt][4 * i + 3]};
+      }
+    return;
+  }
+  bf16* krow = dK + (tok0 + (kw < S ? kw : 0)) * ldkv + hk * D + 8 * hi;
+  bf16* vrow = dV + (tok0 + (kw < S ? kw : 0)) * ldkv + hk * D + 8 * hi;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      float a[4], c[4], x[4], y[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e] = dk[dt][8 * hf + e] * scale;
+        c[e] = dk[dt][8 * hf + 4 + e] * scale;
+        swap32(a[e], c[e]);
+        x[e] = dv[dt][8 * hf + e];
+        y[e] = dv[dt][8 * hf + 4 + e];
+        swap32(x[e], y[e]);
+      }
+      if (kw < S) {
+        *reinterpret_cast<bf16x8*>(krow + 32 * dt + 16 * hf) =
+            bf16x8{(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)c[0], (bf16)c[1], (bf16)c[2], (bf16)c[3]};
+        *reinterpret_cast<bf16x8*>(vrow + 32 * dt + 16 * hf) =
+            bf16x8{(bf16)x[0], (bf16)x[1], (bf16)x[2], (bf16)x[3], (bf16)y[0], (bf16)y[1], (bf16)y[2], (bf16)y[3]};
+      }
+    }
+}
+
 // HALVES = 2: a 512-thread workgroup, the two 4-wave halves sweep different q-heads of the GQA
 // group over the SAME 64 keys (2 waves per SIMD instead of 1) and meet in LDS at the end.
 template <int D, int HALVES, int PF>
@@ -1109,9 +1361,15 @@ __global__ __launch_bounds__(256) void attn_dkv_fin_k(const float* __restrict__ 
 // Also split when the unsplit grid would fill at most half the CUs (one 512-thread workgroup per CU): the
 // sequential-GA micro-batch [2, 512, 8 kv-heads] is 128 workgroups (profiles/r5/attention_dkv_split_b2.txt).
 int attn_dkv_nsplit(int B, int S, int hkv, int causal) {
+  static const int force = [] {   // LIPA_ATTN_DKV_SPLIT=0 / 1: never / always split (A/B runs)
+    const char* e = std::getenv("LIPA_ATTN_DKV_SPLIT");
+    return e ? std::atoi(e) : -1;
+  }();
   const int nb = (S + 63) / 64;
   const long grid = (long)B * hkv * nb;
-  if (!causal || nb < 2 || grid > 512 || (nb < 16 && grid > 128)) return 0;
+  if (!causal || nb < 2 || force == 0) return 0;
+  if (force == 1) return nb - (nb + 1) / 2;
+  if (grid > 512 || (nb < 16 && grid > 128)) return 0;
   return nb - (nb + 1) / 2;   // kb with nb - kb > ceil(nb / 2)
 }
 
@@ -1196,7 +1454,16 @@ void launch_attn_bwd(const void* dout, const void* q, const void* k, const void*
                                             hkv, causal ? 1 | (attn_lpt() << 1) : 0, scale, sl2, dp)
     if (dp.thresh) DQ2(true); else DQ2(false);
 #undef DQ2
-    DKV(128, 1);
+    if (attn_dkv128()) {
+#define DKV3(DR)                                                                                                 \
+  attn_bwd_dkv128_k<DR><<<gkv, 512, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k, (const bf16*)v,   \
+                                             lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, (bf16*)dv, S, hq, hkv, \
+                                             causal, scale, sl2, dp, ws, nsplit)
+      if (dp.thresh) DKV3(true); else DKV3(false);
+#undef DKV3
+    } else {
+      DKV(128, 1);
+    }
   } else {
     LIPA_ATTN_D3(D, RUN(DD, 2, 1));   // prefetch depth dQ 2, dK/dV 1
   }
