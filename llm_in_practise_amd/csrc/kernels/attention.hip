@@ -434,6 +434,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd128_k(const bf16* __restrict__
   // transposed-read geometry (T10): lane 4q'+p' of 16-lane group g addresses row q' of a 4-row block,
   // chunk 2(g&1) + (p'>>1) of the 32-column d block, half p'&1 of it
   const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  // XOR-addressed operand bases (see attn_bwd_dkv128_k): K row r32 (+32 kh rows = 8 KB), Vᵀ rows ra0 / ra0 + 8
+  // (+16 u2 rows = 4 KB, transposed chunk 4dt + c0 = base ^ 64dt)
+  int ak = toff(r32, hi);
+  const int ra0 = 4 * (g >> 1) + qq, c0 = 2 * (g & 1) + (pp >> 1);
+  int at0 = toff(ra0, c0) + 8 * (pp & 1), at1 = toff(ra0 + 8, c0) + 8 * (pp & 1);
 
   if (nt > 0) load_tile(0, 0);
   if (PF == 2 && nt > 1) load_tile(PF - 1, 1);
@@ -450,6 +455,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd128_k(const bf16* __restrict__
       const char* Kl = smem + u * 2 * TB;
       const char* Vl = Kl + TB;
       const int k0 = t * 64;
+      asm volatile("" : "+v"(ak), "+v"(at0), "+v"(at1));   // keep the XORs in the loop
       // ---- Sᵀ[key][q]: keys k0 + 32kh + (r&3) + 8(r>>2) + 4hi of accumulator element r
       f32x16 sc[2];
 #pragma unroll
@@ -458,7 +464,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd128_k(const bf16* __restrict__
         for (int r = 0; r < 16; ++r) sc[kh][r] = 0.f;
 #pragma unroll
         for (int ds = 0; ds < 8; ++ds) {
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kl + toff(32 * kh + r32, 2 * ds + hi));
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kl + 8192 * kh + (ak ^ (32 * ds)));
           sc[kh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], sc[kh], 0, 0, 0);
         }
       }
@@ -520,12 +526,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd128_k(const bf16* __restrict__
           bf16x8 pb;
 #pragma unroll
           for (int j = 0; j < 8; ++j) pb[j] = (bf16)sc[kh][8 * u2 + j];
-          const int ra = 32 * kh + 16 * u2 + 4 * (g >> 1) + qq;
 #pragma unroll
           for (int dt = 0; dt < 4; ++dt) {
-            const int ch = 4 * dt + 2 * (g & 1) + (pp >> 1);
-            const bf16x8 vf = cat8(tr_read((const bf16*)(Vl + toff(ra, ch) + 8 * (pp & 1))),
-                                   tr_read((const bf16*)(Vl + toff(ra + 8, ch) + 8 * (pp & 1))));
+            const char* p0 = Vl + 8192 * kh + 4096 * u2 + (at0 ^ (64 * dt));
+            const char* p1 = Vl + 8192 * kh + 4096 * u2 + (at1 ^ (64 * dt));
+            const bf16x8 vf = cat8(tr_read((const bf16*)p0), tr_read((const bf16*)p1));
             acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb, acc[dt], 0, 0, 0);
           }
         }
@@ -798,6 +803,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq128_k(const bf16* __restric
     }
   };
   const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  // operand rows as XOR-addressed bases (see attn_bwd_dkv128_k): K row r32 (+32 kh rows = 8 KB), Kᵀ rows
+  // ra0 / ra0 + 8 (+16 u2 rows = 4 KB, transposed chunk 4dt + c0 = base ^ 64dt)
+  int ak = toff(r32, hi);
+  const int ra0 = 4 * (g >> 1) + qq, c0 = 2 * (g & 1) + (pp >> 1);
+  int at0 = toff(ra0, c0) + 8 * (pp & 1), at1 = toff(ra0 + 8, c0) + 8 * (pp & 1);
 
   if (nt > 0) load_tile(0);
   for (int t2 = 0; t2 < nt; t2 += 2) {
@@ -810,9 +820,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq128_k(const bf16* __restric
       if (t + 1 < nt) load_tile(t + 1);
       if (t >= ntw) continue;
       const char* Kl = smem + u * 2 * TB;
-      const char* Vl = Kl + TB;
       const int k0 = t * 64;
       const bool need_mask = (causal && k0 + 63 > q0w) || (k0 + 64 > kvlen);
+      asm volatile("" : "+v"(ak), "+v"(at0), "+v"(at1));   // keep the XORs in the loop
 #pragma unroll
       for (int kh = 0; kh < 2; ++kh) {
         f32x16 s, dp;
@@ -820,9 +830,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq128_k(const bf16* __restric
         for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
 #pragma unroll
         for (int ds = 0; ds < 8; ++ds) {
-          const int o = toff(32 * kh + r32, 2 * ds + hi);
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kl + o);
-          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(Vl + o);
+          const char* pk = Kl + 8192 * kh + (ak ^ (32 * ds));
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(pk);
+          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(pk + TB);
           s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], s, 0, 0, 0);
           dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, dof[ds], dp, 0, 0, 0);
         }
@@ -841,12 +851,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq128_k(const bf16* __restric
           bf16x8 pb;
 #pragma unroll
           for (int j = 0; j < 8; ++j) pb[j] = (bf16)s[8 * u2 + j];
-          const int ra = 32 * kh + 16 * u2 + 4 * (g >> 1) + qq;
 #pragma unroll
           for (int dt = 0; dt < 4; ++dt) {
-            const int ch = 4 * dt + 2 * (g & 1) + (pp >> 1);
-            const bf16x8 kt = cat8(tr_read((const bf16*)(Kl + toff(ra, ch) + 8 * (pp & 1))),
-                                   tr_read((const bf16*)(Kl + toff(ra + 8, ch) + 8 * (pp & 1))));
+            const char* p0 = Kl + 8192 * kh + 4096 * u2 + (at0 ^ (64 * dt));
+            const char* p1 = Kl + 8192 * kh + 4096 * u2 + (at1 ^ (64 * dt));
+            const bf16x8 kt = cat8(tr_read((const bf16*)p0), tr_read((const bf16*)p1));
             acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt, pb, acc[dt], 0, 0, 0);
           }
         }
@@ -952,11 +961,22 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkv128_k(const bf16* __restri
     if (j >= rep) return;
     const int h = hk * rep + j;
     const int qa0 = (qt0 + it % nqt) * 64;
+    if (qa0 + 64 <= S) {   // whole tile in range: one base address per tensor, rows as scalar strides
+      const size_t tq = tok0 + qa0 + row0;
+      const bf16* qp = Q + tq * ldq + h * D + ch0 * 8;
+      const bf16* op = dO + tq * ldo + h * D + ch0 * 8;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const size_t tq = tok0 + min(qa0 + row0 + 16 * p, S - 1);
-      qr[p] = *reinterpret_cast<const bf16x8*>(Q + tq * ldq + h * D + ch0 * 8);
-      dr[p] = *reinterpret_cast<const bf16x8*>(dO + tq * ldo + h * D + ch0 * 8);
+      for (int p = 0; p < 4; ++p) {
+        qr[p] = *reinterpret_cast<const bf16x8*>(qp + (size_t)(16 * p) * ldq);
+        dr[p] = *reinterpret_cast<const bf16x8*>(op + (size_t)(16 * p) * ldo);
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const size_t tq = tok0 + min(qa0 + row0 + 16 * p, S - 1);
+        qr[p] = *reinterpret_cast<const bf16x8*>(Q + tq * ldq + h * D + ch0 * 8);
+        dr[p] = *reinterpret_cast<const bf16x8*>(dO + tq * ldo + h * D + ch0 * 8);
+      }
     }
     if (th < 128) {
       const int qs = qa0 + (th & 63);
@@ -973,6 +993,14 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkv128_k(const bf16* __restri
     if (th < 128) stat[hw][th >> 6][th & 63] = st;
   };
   const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  // LDS byte offsets of this lane's operand rows.  The swizzle permutes only bits 4-7 of a row's byte offset
+  // (images start at multiples of 16 KB), so chunk 2ds + hi of row r is toff(r, hi) ^ 32ds and the transposed
+  // chunk 4dt + c of row ra is toff(ra, c) ^ 64dt: four base registers instead of one address per read
+  int aq = (2 + 2 * hw) * TB + toff(32 * qh + r32, hi);   // Q row (dO: + TB)
+  int ak = toff(32 * kw2 + r32, hi);                     // K row (V: + TB)
+  const int ra0 = 32 * qh + 4 * (g >> 1) + qq, c0 = 2 * (g & 1) + (pp >> 1);
+  int at0 = (2 + 2 * hw) * TB + toff(ra0, c0) + 8 * (pp & 1);       // rows ra0 (+16 u2), Qᵀ (dOᵀ: + TB)
+  int at1 = (2 + 2 * hw) * TB + toff(ra0 + 8, c0) + 8 * (pp & 1);   // rows ra0 + 8 (+16 u2)
 
   if (n_it > 0) load_it(0);
   for (int it = 0; it < n_it; ++it) {
@@ -984,16 +1012,18 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkv128_k(const bf16* __restri
     if (j >= rep) continue;   // odd group size: the odd half has no head this round
     const int qa0 = (qt0 + it % nqt) * 64;
     if (causal && qa0 + 32 * qh + 31 < kb0 + 32 * kw2) continue;   // every query of this half precedes our keys
+    asm volatile("" : "+v"(aq), "+v"(ak), "+v"(at0), "+v"(at1));   // keep the XORs in the loop (not 24 hoisted registers)
     f32x16 s, dp;
 #pragma unroll
     for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
 #pragma unroll
     for (int ds = 0; ds < 8; ++ds) {
-      const int oq = toff(32 * qh + r32, 2 * ds + hi), ok = toff(32 * kw2 + r32, 2 * ds + hi);
-      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(Ql + oq),
-                                                 *reinterpret_cast<const bf16x8*>(Kl + ok), s, 0, 0, 0);
-      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(dOl + oq),
-                                                  *reinterpret_cast<const bf16x8*>(Vl + ok), dp, 0, 0, 0);
+      const char* pq = smem + (aq ^ (32 * ds));
+      const char* pk = smem + (ak ^ (32 * ds));
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(pq),
+                                                 *reinterpret_cast<const bf16x8*>(pk), s, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(pq + TB),
+                                                  *reinterpret_cast<const bf16x8*>(pk + TB), dp, 0, 0, 0);
     }
     // element r is row q = qa0 + 32qh + 4hi + c(r), c(r) = (r&3) + 8(r>>2); causal: valid iff c(r) >= qmin − base
     const bool need_mask = (causal && qa0 + 32 * qh < kb0 + 32 * kw2 + 32) || (kb0 + 64 > kvlen);
@@ -1029,13 +1059,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkv128_k(const bf16* __restri
         pb[e] = (bf16)s[8 * u2 + e];
         db[e] = (bf16)dp[8 * u2 + e];
       }
-      const int ra = 32 * qh + 16 * u2 + 4 * (g >> 1) + qq;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const int ch = 4 * dt + 2 * (g & 1) + (pp >> 1);
-        const int o0 = toff(ra, ch) + 8 * (pp & 1), o1 = toff(ra + 8, ch) + 8 * (pp & 1);
-        const bf16x8 ot = cat8(tr_read((const bf16*)(dOl + o0)), tr_read((const bf16*)(dOl + o1)));
-        const bf16x8 qt = cat8(tr_read((const bf16*)(Ql + o0)), tr_read((const bf16*)(Ql + o1)));
+        const char* p0 = smem + (at0 ^ (64 * dt)) + 4096 * u2;
+        const char* p1 = smem + (at1 ^ (64 * dt)) + 4096 * u2;
+        const bf16x8 ot = cat8(tr_read((const bf16*)(p0 + TB)), tr_read((const bf16*)(p1 + TB)));
+        const bf16x8 qt = cat8(tr_read((const bf16*)p0), tr_read((const bf16*)p1));
         dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ot, pb, dv[dt], 0, 0, 0);
         dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qt, db, dk[dt], 0, 0, 0);
       }
