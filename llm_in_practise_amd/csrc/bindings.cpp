@@ -76,6 +76,7 @@ void launch_attn_bwd(const void*, const void*, const void*, const void*, const v
                      int, int, void*, void*, void*, float*, int, int, int, int, int, int, float, float, uint64_t,
                      float*, hipStream_t);
 int attn_dkv_nsplit(int, int, int, int);
+void attn_set_trace(void*);
 
 void launch_gemv_w4(int, const void*, int, const uint8_t*, const float*, const float*, int, const void*, void*, int, int,
                     int, hipStream_t);
@@ -1728,6 +1729,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_fwd_ext", &attn_fwd_ext);
   m.def("attn_bwd", &attn_bwd);
+  // debug: phase timestamps of the D = 128 dK/dV kernel go into `buf` (u8/i64 tensor) while set; None clears
+  m.def("attn_set_trace", [](optional<Tensor> buf) { attn_set_trace(buf && buf->defined() ? buf->data_ptr() : nullptr); });
   m.def("car_alloc", &car_alloc_py);
   m.def("car_free", &car_free_py);
   m.def("car_handle", &car_handle_py);

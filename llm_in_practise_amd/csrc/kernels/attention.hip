@@ -881,15 +881,47 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq128_k(const bf16* __restric
     }
 }
 
+// LDS-DMA and raw-buffer helpers for attn_bwd_dkv128_k.  A raw buffer descriptor (stride 0) range-checks the
+// per-lane offset against num_records: rows past the end read as zero and never touch memory.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+__device__ __forceinline__ rsrc_t attn_rsrc(const void* base, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0,
+                                           (int)(bytes > 0x7fffffffull ? 0x7fffffffull : bytes), 0x00020000);
+}
+// one wave-instruction of LDS-DMA: lane l's 16 B from rs + voff land at LDS m0v + 16·l (M0 saved / restored)
+__device__ __forceinline__ void attn_dma16(const rsrc_t& rs, uint32_t m0v, uint32_t voff) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(m0v), "v"(voff), "s"(rs)
+      : "memory");
+}
+// 16-B raw-buffer load as an asm statement: hipcc does not count it, the explicit vmcnt wait below does
+template <int OFF>
+__device__ __forceinline__ f32x4 attn_bld4(const rsrc_t& rs, uint32_t voff) {
+  f32x4 r;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3" : "=v"(r) : "v"(voff), "s"(rs), "n"(OFF) : "memory");
+  return r;
+}
+
 // dK / dV for D = 128 in the 32x32x16 form, two waves per SIMD: a 512-thread workgroup = 64 keys of one KV
 // head; wave w = (key half kw2 = w&1: 32 keys on the lanes, query half qh = (w>>1)&1: 32 of the tile's 64
 // queries, head half hw = w>>2: the GQA group's q-heads split even / odd).  The K / V images of the block sit
-// in LDS for the whole sweep (B operands of S = Q·Kᵀ and dP = dO·Vᵀ by row reads), each head half streams
-// its Q / dO tiles through one register-staged LDS buffer (loads of tile it+1 in flight during tile it);
+// in LDS for the whole sweep (B operands of S = Q·Kᵀ and dP = dO·Vᵀ by row reads); each head half streams its
+// Q / dO tiles by LDS-DMA into two buffers (tile it+1 lands while tile it is computed: one barrier per tile, no
+// staging registers), the swizzle applied on the global side (lane l of a 1 KB DMA fetches the chunk that the
+// image keeps at slot l).  lse / delta come straight from global (raw-buffer loads, zero past S).
 // dVᵀ += dOᵀ·P and dKᵀ += Qᵀ·dS take dOᵀ / Qᵀ from transposed reads of the same swizzled images and P / dS
 // as B operands in accumulator-row slot order.  The four waves of a key half meet in LDS at the end.
-// Split key blocks (nsplit) write fp32 partials as attn_bwd_dkv_k.  ~97 KB LDS, ≤ 256 VGPRs.
-template <bool DROP>
+// Split key blocks (nsplit) write fp32 partials as attn_bwd_dkv_k.  160 KB LDS, ≤ 256 VGPRs.
+// Requires ldq % 128 == 0 (row strides in whole 256-B units: see attn_dkv128_ok).
+template <bool DROP, bool TRACE = false>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dkv128_k(const bf16* __restrict__ dO, const bf16* __restrict__ Q,
                                                          const bf16* __restrict__ K, const bf16* __restrict__ V,
                                                          const float* __restrict__ lse,
@@ -899,8 +931,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkv128_k(const bf16* __restri
                                                          int hkv, int causal, float scale, float scale_log2,
                                                          DropParams drp, float* __restrict__ ws, int nsplit) {
   constexpr int D = 128, TB = 64 * 256;
-  __shared__ __attribute__((aligned(16))) char smem[6 * TB];       // K | V | [head half][Q | dO]
-  __shared__ __attribute__((aligned(16))) float stat[2][2][64];    // [head half][lse | delta][q]
+  __shared__ __attribute__((aligned(1024))) char smem[10 * TB];   // K | V | [head half][buffer][Q | dO]
   int ui, hk, b;
   xcd_grid3(ui, hk, b);
   int kbi, part;
@@ -912,24 +943,23 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkv128_k(const bf16* __restri
     part = -1;
   }
   const int rep = hq / hkv;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r32 = lane & 31, hi = lane >> 5;
-  const int kw2 = w & 1, qh = (w >> 1) & 1, hw = w >> 2, th = tid & 255;
+  const int tid = threadIdx.x, lane = tid & 63, r32 = lane & 31, hi = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform roles
+  const int kw2 = w & 1, qh = (w >> 1) & 1, hw = w >> 2, w4 = w & 3;
   const int kb0 = kbi * 64;
   const int kw = kb0 + 32 * kw2 + r32;   // this lane's key
   const int kvlen = min(kv_lens ? kv_lens[b] : S, S);
   const size_t tok0 = (size_t)b * S, ldo = (size_t)hq * D, ldkv = (size_t)hkv * D;
-  char* const Kl = smem;
-  char* const Vl = smem + TB;
-  char* const Ql = smem + (2 + 2 * hw) * TB;
-  char* const dOl = Ql + TB;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)smem);
 
   // K / V images of the 64 keys (512 threads × 2 chunks each per tensor)
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     const int id = p * 512 + tid, row = id >> 4, ch = id & 15;
     const size_t key = tok0 + min(kb0 + row, S - 1);
-    *reinterpret_cast<bf16x8*>(Kl + toff(row, ch)) = *reinterpret_cast<const bf16x8*>(K + key * ldk + hk * D + ch * 8);
-    *reinterpret_cast<bf16x8*>(Vl + toff(row, ch)) = *reinterpret_cast<const bf16x8*>(V + key * ldv + hk * D + ch * 8);
+    *reinterpret_cast<bf16x8*>(smem + toff(row, ch)) = *reinterpret_cast<const bf16x8*>(K + key * ldk + hk * D + ch * 8);
+    *reinterpret_cast<bf16x8*>(smem + TB + toff(row, ch)) =
+        *reinterpret_cast<const bf16x8*>(V + key * ldv + hk * D + ch * 8);
   }
   f32x16 dk[4], dv[4];
 #pragma unroll
@@ -952,104 +982,126 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkv128_k(const bf16* __restri
   const int nh = (rep + 1) / 2;
   const int n_it = kb0 < kvlen ? nh * nqt : 0;
 
-  // staging: the head half's 256 threads load its Q / dO tile (4 chunks each per tensor) + 128 stats
-  bf16x8 qr[4], dr[4];
-  float st = 0.f;
-  const int row0 = th >> 4, ch0 = th & 15;   // rows row0 + 16p
-  auto load_it = [&](int it) {
-    const int j = hw + 2 * (it / nqt);
-    if (j >= rep) return;
-    const int h = hk * rep + j;
-    const int qa0 = (qt0 + it % nqt) * 64;
-    if (qa0 + 64 <= S) {   // whole tile in range: one base address per tensor, rows as scalar strides
-      const size_t tq = tok0 + qa0 + row0;
-      const bf16* qp = Q + tq * ldq + h * D + ch0 * 8;
-      const bf16* op = dO + tq * ldo + h * D + ch0 * 8;
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        qr[p] = *reinterpret_cast<const bf16x8*>(qp + (size_t)(16 * p) * ldq);
-        dr[p] = *reinterpret_cast<const bf16x8*>(op + (size_t)(16 * p) * ldo);
-      }
-    } else {
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const size_t tq = tok0 + min(qa0 + row0 + 16 * p, S - 1);
-        qr[p] = *reinterpret_cast<const bf16x8*>(Q + tq * ldq + h * D + ch0 * 8);
-        dr[p] = *reinterpret_cast<const bf16x8*>(dO + tq * ldo + h * D + ch0 * 8);
-      }
-    }
-    if (th < 128) {
-      const int qs = qa0 + (th & 63);
-      const size_t bh = ((size_t)b * hq + h) * S + min(qs, S - 1);
-      st = th < 64 ? (qs < S ? lse[bh] * LOG2E : INFINITY) : delta[bh];   // rows past S: P = 0
-    }
-  };
-  auto store_it = [&]() {
+  // DMA geometry: wave w4 of a head half moves image rows 16w4 .. 16w4 + 15 of Q and of dO (4 × 1 KB each);
+  // in 1 KB chunk p lane l fills row 16w4 + 4p + (l>>4), slot l&15, i.e. logical chunk (l&15) ^ swz(row) =
+  // (l&15) ^ ((l>>4)<<2) ^ p.  Row strides are multiples of 256 B, so the chunk XOR never carries into them.
+  const uint32_t ldq2 = (uint32_t)ldq * 2, ldo2 = (uint32_t)ldo * 2;
+  const uint32_t xs = 16u * (uint32_t)((lane & 15) ^ ((lane >> 4) << 2));
+  const uint32_t vq = (16u * w4 + (lane >> 4)) * ldq2 + xs, vo = (16u * w4 + (lane >> 4)) * ldo2 + xs;
+  auto dma_it = [&](int it2) {
+    const int j2 = hw + 2 * (it2 / nqt);
+    if (j2 >= rep) return;
+    const int h2 = hk * rep + j2;
+    const int qb = (qt0 + it2 % nqt) * 64;
+    const rsrc_t rq = attn_rsrc(Q + (tok0 + qb) * ldq + h2 * D, (size_t)(S - qb) * ldq2);
+    const rsrc_t ro = attn_rsrc(dO + (tok0 + qb) * ldo + h2 * D, (size_t)(S - qb) * ldo2);
+    const uint32_t dst = lds0 + (uint32_t)(2 * TB * (1 + 2 * hw + (it2 & 1)) + 4096 * w4);
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      *reinterpret_cast<bf16x8*>(Ql + toff(row0 + 16 * p, ch0)) = qr[p];
-      *reinterpret_cast<bf16x8*>(dOl + toff(row0 + 16 * p, ch0)) = dr[p];
+      attn_dma16(rq, dst + 1024 * p, (vq + 4u * p * ldq2) ^ (16u * p));
+      attn_dma16(ro, dst + TB + 1024 * p, (vo + 4u * p * ldo2) ^ (16u * p));
     }
-    if (th < 128) stat[hw][th >> 6][th & 63] = st;
   };
   const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
   // LDS byte offsets of this lane's operand rows.  The swizzle permutes only bits 4-7 of a row's byte offset
   // (images start at multiples of 16 KB), so chunk 2ds + hi of row r is toff(r, hi) ^ 32ds and the transposed
   // chunk 4dt + c of row ra is toff(ra, c) ^ 64dt: four base registers instead of one address per read
-  int aq = (2 + 2 * hw) * TB + toff(32 * qh + r32, hi);   // Q row (dO: + TB)
+  const int img = 2 * TB * (1 + 2 * hw);                 // this head half's buffer 0 (buffer 1: + 2 TB)
+  int aq = img + toff(32 * qh + r32, hi);                // Q row (dO: + TB)
   int ak = toff(32 * kw2 + r32, hi);                     // K row (V: + TB)
   const int ra0 = 32 * qh + 4 * (g >> 1) + qq, c0 = 2 * (g & 1) + (pp >> 1);
-  int at0 = (2 + 2 * hw) * TB + toff(ra0, c0) + 8 * (pp & 1);       // rows ra0 (+16 u2), Qᵀ (dOᵀ: + TB)
-  int at1 = (2 + 2 * hw) * TB + toff(ra0 + 8, c0) + 8 * (pp & 1);   // rows ra0 + 8 (+16 u2)
+  int at0 = img + toff(ra0, c0) + 8 * (pp & 1);          // rows ra0 (+16 u2), Qᵀ (dOᵀ: + TB)
+  int at1 = img + toff(ra0 + 8, c0) + 8 * (pp & 1);      // rows ra0 + 8 (+16 u2)
+  const uint32_t vst = (uint32_t)(32 * qh + 4 * hi) * 4;   // this lane's first lse / delta byte in the tile
 
-  if (n_it > 0) load_it(0);
+  // TRACE (LIPA_ATTN_TRACE, attn_set_trace): lane 0 of every wave stamps s_memtime at the loop's phase
+  // boundaries into ws: per wave [hw_id, xcc_id, unit, n_it, t_start, t_end, rt_start, rt_end, 4 × 64 iterations]
+  unsigned long long* trc = nullptr;
+  if (TRACE) {
+    const int wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    trc = reinterpret_cast<unsigned long long*>(ws) + ((size_t)wg * 8 + w) * 264;
+    if (lane == 0) {
+      trc[0] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      trc[1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+      trc[2] = (unsigned long long)(kbi * 2 + (part + 1)) | ((unsigned long long)(hk + hkv * b) << 32);
+      trc[3] = n_it;
+      trc[4] = __builtin_readcyclecounter();
+      trc[6] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  auto mark = [&](int it, int e) {
+    if (TRACE && lane == 0 && it < 64) trc[8 + 4 * it + e] = __builtin_readcyclecounter();
+  };
+  if (n_it > 0) dma_it(0);
   for (int it = 0; it < n_it; ++it) {
-    __syncthreads();          // the previous tile's reads are done (and, at it = 0, the K / V images are written)
-    store_it();
-    __syncthreads();
-    if (it + 1 < n_it) load_it(it + 1);
+    mark(it, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of tile it have landed
+    __syncthreads();   // ... everyone's; and every read of tile it-1's buffer (the next DMA target) is done
+    mark(it, 1);
     const int j = hw + 2 * (it / nqt);
-    if (j >= rep) continue;   // odd group size: the odd half has no head this round
     const int qa0 = (qt0 + it % nqt) * 64;
-    if (causal && qa0 + 32 * qh + 31 < kb0 + 32 * kw2) continue;   // every query of this half precedes our keys
+    const bool act = j < rep && !(causal && qa0 + 32 * qh + 31 < kb0 + 32 * kw2);
+    f32x4 L[4], Dl[4];
+    if (act) {   // this tile's lse / delta rows, in flight under the S / dP MFMAs
+      const size_t bh = ((size_t)b * hq + hk * rep + j) * S + qa0;
+      const rsrc_t rl = attn_rsrc(lse + bh, (size_t)(S - qa0) * 4);
+      const rsrc_t rd = attn_rsrc(delta + bh, (size_t)(S - qa0) * 4);
+      L[0] = attn_bld4<0>(rl, vst);
+      L[1] = attn_bld4<32>(rl, vst);
+      L[2] = attn_bld4<64>(rl, vst);
+      L[3] = attn_bld4<96>(rl, vst);
+      Dl[0] = attn_bld4<0>(rd, vst);
+      Dl[1] = attn_bld4<32>(rd, vst);
+      Dl[2] = attn_bld4<64>(rd, vst);
+      Dl[3] = attn_bld4<96>(rd, vst);
+    }
+    const bool more = it + 1 < n_it && hw + 2 * ((it + 1) / nqt) < rep;
+    if (it + 1 < n_it) dma_it(it + 1);
+    if (!act) continue;   // odd group size (no head for this half) or every query of this half precedes our keys
+    const int bo = (it & 1) * 2 * TB;
     asm volatile("" : "+v"(aq), "+v"(ak), "+v"(at0), "+v"(at1));   // keep the XORs in the loop (not 24 hoisted registers)
     f32x16 s, dp;
 #pragma unroll
     for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
 #pragma unroll
     for (int ds = 0; ds < 8; ++ds) {
-      const char* pq = smem + (aq ^ (32 * ds));
+      const char* pq = smem + bo + (aq ^ (32 * ds));
       const char* pk = smem + (ak ^ (32 * ds));
       s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(pq),
                                                  *reinterpret_cast<const bf16x8*>(pk), s, 0, 0, 0);
       dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(pq + TB),
                                                   *reinterpret_cast<const bf16x8*>(pk + TB), dp, 0, 0, 0);
     }
-    // element r is row q = qa0 + 32qh + 4hi + c(r), c(r) = (r&3) + 8(r>>2); causal: valid iff c(r) >= qmin − base
-    const bool need_mask = (causal && qa0 + 32 * qh < kb0 + 32 * kw2 + 32) || (kb0 + 64 > kvlen);
-    const int lo = qmin - (qa0 + 32 * qh + 4 * hi);
-    const float* Ls = stat[hw][0];
-    const float* Dls = stat[hw][1];
+    // the stats loads were issued before the 8 DMAs of tile it+1 (if any): wait for them only
+    if (more)
+      asm volatile("s_waitcnt vmcnt(8)" : "+v"(L[0]), "+v"(L[1]), "+v"(L[2]), "+v"(L[3]), "+v"(Dl[0]), "+v"(Dl[1]),
+                   "+v"(Dl[2]), "+v"(Dl[3])::"memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(L[0]), "+v"(L[1]), "+v"(L[2]), "+v"(L[3]), "+v"(Dl[0]), "+v"(Dl[1]),
+                   "+v"(Dl[2]), "+v"(Dl[3])::"memory");
+    // element r is row q = qa0 + 32qh + 4hi + c(r), c(r) = (r&3) + 8(r>>2); valid iff lo <= c(r) < hs (causal /
+    // kv length: q >= qmin; rows past S: q < S)
+    const bool need_mask = (causal && qa0 + 32 * qh < kb0 + 32 * kw2 + 32) || (kb0 + 64 > kvlen) || (qa0 + 64 > S);
+    const int lo = qmin - (qa0 + 32 * qh + 4 * hi), hs = S - (qa0 + 32 * qh + 4 * hi);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const f32x4 L = *reinterpret_cast<const f32x4*>(Ls + 32 * qh + 8 * i + 4 * hi);
-      const f32x4 Dl = *reinterpret_cast<const f32x4*>(Dls + 32 * qh + 8 * i + 4 * hi);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int r = 4 * i + e;
-        float p = fexp2(fmaf(s[r], scale_log2, -L[e]));
-        if (need_mask) p = (8 * i + e >= lo) ? p : 0.f;
+        float p = fexp2(fmaf(s[r], scale_log2, L[i][e] * -LOG2E));
+        if (need_mask) p = (8 * i + e >= lo && 8 * i + e < hs) ? p : 0.f;
         if (DROP) {
           const int q = qa0 + 32 * qh + 8 * i + 4 * hi + e;
           const bool keep = drop_hash(drp.s0, drp.s1, (uint32_t)(b * hq + hk * rep + j), q, kw) >= drp.thresh;
-          dp[r] = p * ((keep ? dp[r] * drp.rinv : 0.f) - Dl[e]);
+          dp[r] = p * ((keep ? dp[r] * drp.rinv : 0.f) - Dl[i][e]);
           s[r] = keep ? p * drp.rinv : 0.f;
         } else {
-          dp[r] = p * (dp[r] - Dl[e]);
+          dp[r] = p * (dp[r] - Dl[i][e]);
           s[r] = p;
         }
       }
     }
+    mark(it, 2);
     // dVᵀ[d][key] += dOᵀ[d][q]·P[q][key] ; dKᵀ += Qᵀ·dS
 #pragma unroll
     for (int u2 = 0; u2 < 2; ++u2) {
@@ -1061,14 +1113,18 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkv128_k(const bf16* __restri
       }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const char* p0 = smem + (at0 ^ (64 * dt)) + 4096 * u2;
-        const char* p1 = smem + (at1 ^ (64 * dt)) + 4096 * u2;
+        const char* p0 = smem + bo + (at0 ^ (64 * dt)) + 4096 * u2;
+        const char* p1 = smem + bo + (at1 ^ (64 * dt)) + 4096 * u2;
         const bf16x8 ot = cat8(tr_read((const bf16*)(p0 + TB)), tr_read((const bf16*)(p1 + TB)));
         const bf16x8 qt = cat8(tr_read((const bf16*)p0), tr_read((const bf16*)p1));
         dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ot, pb, dv[dt], 0, 0, 0);
         dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qt, db, dk[dt], 0, 0, 0);
       }
     }
+  }
+  if (TRACE && lane == 0) {
+    trc[5] = __builtin_readcyclecounter();
+    trc[7] = __builtin_amdgcn_s_memrealtime();
   }
   // ---- the four waves of a key half (head half × query half) sum through LDS: query half 1 → 0, then head
   // half 1 → 0, dK and dV in separate passes (a wave's 16 f32x4 per tensor = 16 KB per slot, 4 slots ≤ 96 KB)
@@ -1389,6 +1445,11 @@ __global__ __launch_bounds__(256) void attn_dkv_fin_k(const float* __restrict__ 
 // hence the S threshold (still the best after the LDS re-pad: profiles/r4/attention_knobs_ab.txt, S = 2048 bwd 236 vs 262 us unsplit).
 // Also split when the unsplit grid would fill at most half the CUs (one 512-thread workgroup per CU): the
 // sequential-GA micro-batch [2, 512, 8 kv-heads] is 128 workgroups (profiles/r5/attention_dkv_split_b2.txt).
+// per-wave phase timestamps of the D = 128 dK/dV kernel (debug; see attn_bwd_dkv128_k TRACE): while set, the
+// dK/dV launches write [grid · 8 waves · 264] u64 into this buffer instead of splitting key blocks
+static float* g_attn_trace = nullptr;
+void attn_set_trace(void* p) { g_attn_trace = (float*)p; }
+
 int attn_dkv_nsplit(int B, int S, int hkv, int causal) {
   static const int force = [] {   // LIPA_ATTN_DKV_SPLIT=0 / 1: never / always split (A/B runs)
     const char* e = std::getenv("LIPA_ATTN_DKV_SPLIT");
@@ -1458,7 +1519,8 @@ void launch_attn_bwd(const void* dout, const void* q, const void* k, const void*
   const float sl2 = scale * LOG2E;
   const DropParams dp = make_drop(p_drop, seed);
   const int nb = (S + 63) / 64;
-  const int nsplit = ws ? attn_dkv_nsplit(B, S, hkv, causal) : 0;
+  const bool trace = g_attn_trace && D == 128 && attn_dkv128() && ldq % 128 == 0;
+  const int nsplit = ws && !trace ? attn_dkv_nsplit(B, S, hkv, causal) : 0;
   dim3 gq(nb, hq, B), gkv(nb + nsplit, hkv, B), blk(256);
 #define DKV(DD, PFKV)                                                                                             \
   if ((hq / hkv) % 2 == 0)                                                                                       \
@@ -1483,12 +1545,17 @@ void launch_attn_bwd(const void* dout, const void* q, const void* k, const void*
                                             hkv, causal ? 1 | (attn_lpt() << 1) : 0, scale, sl2, dp)
     if (dp.thresh) DQ2(true); else DQ2(false);
 #undef DQ2
-    if (attn_dkv128()) {
+    if (attn_dkv128() && ldq % 128 == 0) {   // the DMA row geometry needs 256-B-multiple Q row strides
 #define DKV3(DR)                                                                                                 \
   attn_bwd_dkv128_k<DR><<<gkv, 512, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k, (const bf16*)v,   \
                                              lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, (bf16*)dv, S, hq, hkv, \
                                              causal, scale, sl2, dp, ws, nsplit)
-      if (dp.thresh) DKV3(true); else DKV3(false);
+      if (trace)
+        attn_bwd_dkv128_k<false, true><<<gkv, 512, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k,
+                                                            (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv,
+                                                            (bf16*)dk, (bf16*)dv, S, hq, hkv, causal, scale, sl2, dp,
+                                                            g_attn_trace, 0);
+      else if (dp.thresh) DKV3(true); else DKV3(false);
 #undef DKV3
     } else {
       DKV(128, 1);
