@@ -9,8 +9,8 @@ export PYTHONPATH=$R
 cd /tmp && export TMPDIR=/tmp
 for shape in "4 512" "2 512" "1 2048"; do
   set -- $shape
-  for cfg in "1 -1" "1 1" "0 -1" "0 1"; do
-    read v sp <<< "$cfg"
+  for cfg in ${CFGS:-"1,-1" "1,1" "0,-1" "0,1"}; do   # kernel,split (LIPA_ATTN_DKV128, LIPA_ATTN_DKV_SPLIT)
+    IFS=, read v sp <<< "$cfg"
     tag=B$1_S$2_v${v}_s${sp}
     LIPA_ATTN_DKV128=$v LIPA_ATTN_DKV_SPLIT=$sp timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$tag -o kt -- \
       python3 $R/scripts/bench_attn.py --B $1 --S $2 --no-sdpa --iters 20 > $OUT/$tag.log 2>&1 || exit 1
