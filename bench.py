@@ -304,10 +304,15 @@ def main():
     D.COMM.enabled = world > 1      # collectives of the timed steps: bytes, run time, exposed time (parallel/dist.py)
     _lin.GEMM_STATS.clear()         # GEMM launches by form over the timed steps (kernel provenance)
     t0 = time.perf_counter()
+    dbg = os.environ.get("LIPA_BENCH_DEBUG_LOSS") == "1"     # per-step loss / grad norm (syncs: debug only)
     for _ in range(args.steps):
         loss = step()
         gcm.step()
         D.COMM.step()
+        if dbg:
+            gn = getattr(engine, "last_grad_norm", None) if engine is not None else None
+            print(f"[rank {rank}] step loss={loss.item():.6f} grad_norm={None if gn is None else float(gn):}",
+                  file=sys.stderr, flush=True)
     sync()
     elapsed = D.all_reduce_max(time.perf_counter() - t0)
     D.COMM.enabled = False

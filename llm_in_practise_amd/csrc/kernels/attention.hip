@@ -902,13 +902,6 @@ __device__ __forceinline__ void attn_dma16(const rsrc_t& rs, uint32_t m0v, uint3
       : "s"(m0v), "v"(voff), "s"(rs)
       : "memory");
 }
-// 16-B raw-buffer load as an asm statement: hipcc does not count it, the explicit vmcnt wait below does
-template <int OFF>
-__device__ __forceinline__ f32x4 attn_bld4(const rsrc_t& rs, uint32_t voff) {
-  f32x4 r;
-  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3" : "=v"(r) : "v"(voff), "s"(rs), "n"(OFF) : "memory");
-  return r;
-}
 
 // dK / dV for D = 128 in the 32x32x16 form, two waves per SIMD: a 512-thread workgroup = 64 keys of one KV
 // head; wave w = (key half kw2 = w&1: 32 keys on the lanes, query half qh = (w>>1)&1: 32 of the tile's 64
@@ -916,7 +909,7 @@ __device__ __forceinline__ f32x4 attn_bld4(const rsrc_t& rs, uint32_t voff) {
 // in LDS for the whole sweep (B operands of S = Q·Kᵀ and dP = dO·Vᵀ by row reads); each head half streams its
 // Q / dO tiles by LDS-DMA into two buffers (tile it+1 lands while tile it is computed: one barrier per tile, no
 // staging registers), the swizzle applied on the global side (lane l of a 1 KB DMA fetches the chunk that the
-// image keeps at slot l).  lse / delta come straight from global (raw-buffer loads, zero past S).
+// image keeps at slot l).  lse / delta come straight from global (raw-buffer loads, zero past S, one tile ahead).
 // dVᵀ += dOᵀ·P and dKᵀ += Qᵀ·dS take dOᵀ / Qᵀ from transposed reads of the same swizzled images and P / dS
 // as B operands in accumulator-row slot order.  The four waves of a key half meet in LDS at the end.
 // Split key blocks (nsplit) write fp32 partials as attn_bwd_dkv_k.  160 KB LDS, ≤ 256 VGPRs.
@@ -1032,32 +1025,43 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkv128_k(const bf16* __restri
   auto mark = [&](int it, int e) {
     if (TRACE && lane == 0 && it < 64) trc[8 + 4 * it + e] = __builtin_readcyclecounter();
   };
-  if (n_it > 0) dma_it(0);
+  // lse / delta of a tile: compiler-visible raw-buffer loads (zero past S), issued at the end of the previous
+  // iteration and covered by the loop-top vmcnt(0) — no counted wait that would assume in-order completion
+  // beside the LDS-DMAs (a vmcnt(8) "stats only" wait raced under contention: scripts/experiments/
+  // attn_bwd_repeat.py, two processes)
+  f32x4 L[4], Dl[4];
+  auto act_of = [&](int it2) {
+    const int j2 = hw + 2 * (it2 / nqt);
+    const int qb = (qt0 + it2 % nqt) * 64;
+    return j2 < rep && !(causal && qb + 32 * qh + 31 < kb0 + 32 * kw2);
+  };
+  auto stats_it = [&](int it2) {
+    if (!act_of(it2)) return;
+    const int j2 = hw + 2 * (it2 / nqt);
+    const int qb = (qt0 + it2 % nqt) * 64;
+    const size_t bh = ((size_t)b * hq + hk * rep + j2) * S + qb;
+    const rsrc_t rl = attn_rsrc(lse + bh, (size_t)(S - qb) * 4);
+    const rsrc_t rd = attn_rsrc(delta + bh, (size_t)(S - qb) * 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      L[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rl, vst + 32 * i, 0, 0));
+      Dl[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rd, vst + 32 * i, 0, 0));
+    }
+  };
+  if (n_it > 0) {
+    dma_it(0);
+    stats_it(0);
+  }
   for (int it = 0; it < n_it; ++it) {
     mark(it, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of tile it have landed
+    __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0): this wave's DMAs and lse / delta loads of tile it have landed
     __syncthreads();   // ... everyone's; and every read of tile it-1's buffer (the next DMA target) is done
     mark(it, 1);
     const int j = hw + 2 * (it / nqt);
     const int qa0 = (qt0 + it % nqt) * 64;
-    const bool act = j < rep && !(causal && qa0 + 32 * qh + 31 < kb0 + 32 * kw2);
-    f32x4 L[4], Dl[4];
-    if (act) {   // this tile's lse / delta rows, in flight under the S / dP MFMAs
-      const size_t bh = ((size_t)b * hq + hk * rep + j) * S + qa0;
-      const rsrc_t rl = attn_rsrc(lse + bh, (size_t)(S - qa0) * 4);
-      const rsrc_t rd = attn_rsrc(delta + bh, (size_t)(S - qa0) * 4);
-      L[0] = attn_bld4<0>(rl, vst);
-      L[1] = attn_bld4<32>(rl, vst);
-      L[2] = attn_bld4<64>(rl, vst);
-      L[3] = attn_bld4<96>(rl, vst);
-      Dl[0] = attn_bld4<0>(rd, vst);
-      Dl[1] = attn_bld4<32>(rd, vst);
-      Dl[2] = attn_bld4<64>(rd, vst);
-      Dl[3] = attn_bld4<96>(rd, vst);
-    }
-    const bool more = it + 1 < n_it && hw + 2 * ((it + 1) / nqt) < rep;
+    const bool act = act_of(it);
     if (it + 1 < n_it) dma_it(it + 1);
-    if (!act) continue;   // odd group size (no head for this half) or every query of this half precedes our keys
+    if (act) {
     const int bo = (it & 1) * 2 * TB;
     asm volatile("" : "+v"(aq), "+v"(ak), "+v"(at0), "+v"(at1));   // keep the XORs in the loop (not 24 hoisted registers)
     f32x16 s, dp;
@@ -1072,13 +1076,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkv128_k(const bf16* __restri
       dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(pq + TB),
                                                   *reinterpret_cast<const bf16x8*>(pk + TB), dp, 0, 0, 0);
     }
-    // the stats loads were issued before the 8 DMAs of tile it+1 (if any): wait for them only
-    if (more)
-      asm volatile("s_waitcnt vmcnt(8)" : "+v"(L[0]), "+v"(L[1]), "+v"(L[2]), "+v"(L[3]), "+v"(Dl[0]), "+v"(Dl[1]),
-                   "+v"(Dl[2]), "+v"(Dl[3])::"memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(L[0]), "+v"(L[1]), "+v"(L[2]), "+v"(L[3]), "+v"(Dl[0]), "+v"(Dl[1]),
-                   "+v"(Dl[2]), "+v"(Dl[3])::"memory");
     // element r is row q = qa0 + 32qh + 4hi + c(r), c(r) = (r&3) + 8(r>>2); valid iff lo <= c(r) < hs (causal /
     // kv length: q >= qmin; rows past S: q < S)
     const bool need_mask = (causal && qa0 + 32 * qh < kb0 + 32 * kw2 + 32) || (kb0 + 64 > kvlen) || (qa0 + 64 > S);
@@ -1121,6 +1118,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkv128_k(const bf16* __restri
         dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qt, db, dk[dt], 0, 0, 0);
       }
     }
+    }   // act
+    if (it + 1 < n_it) stats_it(it + 1);
   }
   if (TRACE && lane == 0) {
     trc[5] = __builtin_readcyclecounter();

@@ -66,6 +66,14 @@ def _world():
     return dist.get_world_size() if is_dist() else 1
 
 
+_CHECK = os.environ.get("LIPA_ZERO_CHECK") == "1"     # debug: verify gathered copies / unit grads (host syncs)
+
+
+def _check(what: str, ok: bool):
+    if not ok:
+        print(f"[zero-check rank {_rank()}] FAILED: {what}", flush=True)
+
+
 def _rank():
     return dist.get_rank() if is_dist() else 0
 
@@ -250,6 +258,7 @@ class _Unit:
                 _join(self.work, "all_gather")
                 self.work = None
                 self.gathered = True
+                self._verify("joined prefetch")
             return False
         works = []
         for full, shard in self._flats():
@@ -265,7 +274,17 @@ class _Unit:
             self.work = works
             return True
         self.gathered = True
+        self._verify("sync gather")
         return True
+
+    def _verify(self, how: str):
+        if not _CHECK:
+            return
+        for i, (full, shard) in enumerate(self._flats()):
+            mine = full.view(self.world, -1)[self.rank]
+            _check(f"{self.name} flat {i} ({how}): own slice != shard", bool(torch.equal(mine, shard)))
+            if full.is_floating_point():
+                _check(f"{self.name} flat {i} ({how}): non-finite", bool(torch.isfinite(full).all()))
 
     def release(self):
         if self.work is not None:
@@ -545,6 +564,9 @@ class ZeroEngine:
                 flat[o:o + k].copy_(p.grad.reshape(-1))
                 p.grad = None
             o += k
+        if _CHECK:
+            _check(f"{u.name} grads non-finite / huge (max {float(flat.abs().max()):.3g})",
+                   bool(torch.isfinite(flat).all()) and float(flat.abs().max()) < 1e3)
         view[:, col:col + u.shard_n].copy_(flat.view(W, u.shard_n))
         self._pending_units.append(u)
         self._pending_n += u.shard_n
@@ -734,6 +756,9 @@ class ZeroEngine:
                     u.grads_ready = 0
                     self._queue_reduce(u)
             self._join_reduces()
+            if _CHECK:
+                _check(f"grad shard non-finite / huge (max {float(self.grad_shard.abs().max()):.3g})",
+                       bool(torch.isfinite(self.grad_shard).all()) and float(self.grad_shard.abs().max()) < 1e3)
             if self._recording and self._recorded:      # execution order seen by the first step
                 self.fwd_order = list(self._recorded)
                 self._recording = False
