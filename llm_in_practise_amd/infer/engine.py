@@ -33,6 +33,7 @@ import torch
 
 from ..models.common import KVCache, PackedPrefill
 from ..ops.decode import sample
+from ..ops.linear import head_logits
 from ..train.data import render_chatml
 
 
@@ -697,7 +698,7 @@ class ServingEngine:
             return
         s.prefilled = -1
         self.stats["prompt_tokens_total"] += L
-        logits = h[-1:] @ self.lm.lm_head.weight.t()
+        logits = head_logits(h[-1:], self.lm.lm_head.weight)
         dev_toks, toks = self._sample(logits, [slot])
         self.next_tok[slot] = dev_toks[0]
         if self.prefix is not None:
@@ -715,7 +716,7 @@ class ServingEngine:
             h = lm.model(ids, None, view, None)
         finally:
             self._rows_done()
-        logits = h[-1:] @ lm.lm_head.weight.t()
+        logits = head_logits(h[-1:], lm.lm_head.weight)
         L = len(r.prompt_ids)
         self.cache.pos[slot] = L
         self.slots[slot] = _Slot(r)
@@ -737,7 +738,7 @@ class ServingEngine:
             h = lm.model(ids, pp.positions, pp, None)
         finally:
             self._rows_done()
-        logits = h[pp.last] @ lm.lm_head.weight.t()
+        logits = head_logits(h[pp.last], lm.lm_head.weight)
         rows = torch.tensor([s for s, _ in new], device=self.device)
         self.cache.pos[rows] = torch.tensor(lens, dtype=torch.long, device=self.device)
         now = time.time()
@@ -840,7 +841,7 @@ class ServingEngine:
             logits = self.graphs.step(None, n)
         else:
             h = lm.model(self.next_tok[:n, None], None, self.cache.head_rows(n), None)   # per-row positions
-            logits = h @ lm.lm_head.weight.t()
+            logits = head_logits(h, lm.lm_head.weight)
         free = [i for i in range(n) if self.slots[i] is None]
         if free:                                                              # idle rows stay at position 0
             self.cache.pos[torch.tensor(free, device=self.device)] = 0

@@ -18,6 +18,7 @@ from __future__ import annotations
 import torch
 
 from ..models.common import KVCache
+from ..ops.linear import head_logits
 
 
 def _buckets(max_batch: int) -> list[int]:
@@ -49,7 +50,7 @@ class DecodeGraphs:
 
     def _forward(self, n: int) -> torch.Tensor:
         h = self.lm.model(self.tokens[:n, None], None, self.cache.head_rows(n), None)
-        return h @ self.lm.lm_head.weight.t()
+        return head_logits(h, self.lm.lm_head.weight)
 
     @torch.no_grad()
     def _capture_all(self):

@@ -175,6 +175,17 @@ def _pad_cols(t: torch.Tensor, mult: int = EXT_ALIGN) -> torch.Tensor:
     return F.pad(t, (0, rp - r)).contiguous()
 
 
+def head_logits(h: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """LM-head logits of serving rows through the same dispatch as the projections: decode-sized row counts take
+    the split-K weight-streaming kernel, whose per-row result does not depend on how many rows share the call
+    (the library GEMM's algorithm — and rounding — changes with M), so a request's greedy tokens do not depend on
+    the batch it was decoded in (continuous batching, hipGraph buckets, the pipelined engine)."""
+    x = h.reshape(-1, h.shape[-1])
+    if not x.is_contiguous():
+        x = x.contiguous()
+    return _base_gemm(x, weight).view(*h.shape[:-1], weight.shape[0])
+
+
 def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
     if isinstance(base, NF4Weight):
         if x.shape[0] <= 8 and base.kernel_ok():   # decode: weight-streaming GEMV, no MFMA tile
