@@ -114,6 +114,15 @@ __device__ __forceinline__ void xcd_grid3_lpt(int& i0, int& i1, int& i2, int lpt
 // order (0) and longest-first only (2), profiles/r4/attention_knobs_ab.txt
 static int attn_lpt() { return 1; }
 
+// D = 128 forward / dQ: K / V tiles by LDS-DMA (1, default) or register-staged (LIPA_ATTN_FWD_DMA=0, A/B runs)
+static int attn_fwd_dma() {
+  static const int v = [] {
+    const char* e = std::getenv("LIPA_ATTN_FWD_DMA");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+
 // D = 128 dK/dV kernel: 1 = the 32x32x16 form (attn_bwd_dkv128_k), 0 = the 16x16x32 8-wave form
 // (LIPA_ATTN_DKV128=0, for A/B runs)
 static int attn_dkv128() {
@@ -359,6 +368,28 @@ __device__ __forceinline__ void swap32(float& a, float& b) {
   b = __uint_as_float(r[1]);
 }
 
+// LDS-DMA and raw-buffer helpers (attn_fwd128_k<0>, attn_bwd_dkv128_k).  A raw buffer descriptor (stride 0) range-checks the
+// per-lane offset against num_records: rows past the end read as zero and never touch memory.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+__device__ __forceinline__ rsrc_t attn_rsrc(const void* base, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0,
+                                           (int)(bytes > 0x7fffffffull ? 0x7fffffffull : bytes), 0x00020000);
+}
+// one wave-instruction of LDS-DMA: lane l's 16 B from rs + voff land at LDS m0v + 16·l (M0 saved / restored)
+__device__ __forceinline__ void attn_dma16(const rsrc_t& rs, uint32_t m0v, uint32_t voff) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(m0v), "v"(voff), "s"(rs)
+      : "memory");
+}
+
 template <int PF, bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_fwd128_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ V, int ldq, int ldk, int ldv,
@@ -402,7 +433,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd128_k(const bf16* __restrict__
     for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
 
-  bf16x8 kr[PF][4], vr[PF][4];
+  bf16x8 kr[PF > 0 ? PF : 1][4], vr[PF > 0 ? PF : 1][4];   // (PF = 0: LDS-DMA, no staging)
   const int row0 = tid >> 4, ch0 = tid & 15;   // this thread's tile rows row0 + 16p, chunk ch0
   auto load_tile = [&](int set, int t) {
     if (t * 64 + 64 <= Skv) {   // whole tile in range: one base address, row steps as offsets
@@ -440,17 +471,44 @@ __global__ __launch_bounds__(256, 2) void attn_fwd128_k(const bf16* __restrict__
   const int ra0 = 4 * (g >> 1) + qq, c0 = 2 * (g & 1) + (pp >> 1);
   int at0 = toff(ra0, c0) + 8 * (pp & 1), at1 = toff(ra0 + 8, c0) + 8 * (pp & 1);
 
-  if (nt > 0) load_tile(0, 0);
-  if (PF == 2 && nt > 1) load_tile(PF - 1, 1);
+  // PF = 0: K / V tiles by LDS-DMA (as attn_bwd_dkv128_k: wave w moves image rows 16w .. 16w + 15, the swizzle
+  // applied on the global side, zero past Skv), one barrier per tile, no staging VGPRs or LDS stores
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)smem);
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const uint32_t ldk2 = (uint32_t)ldk * 2, ldv2 = (uint32_t)ldv * 2;
+  const uint32_t xs = 16u * (uint32_t)((lane & 15) ^ ((lane >> 4) << 2));
+  const uint32_t vk = (16u * wu + (lane >> 4)) * ldk2 + xs, vv = (16u * wu + (lane >> 4)) * ldv2 + xs;
+  auto dma_tile = [&](int t) {
+    const rsrc_t rk = attn_rsrc(K + (ktok0 + t * 64) * ldk + hk * D, (size_t)max(Skv - t * 64, 0) * ldk2);
+    const rsrc_t rv = attn_rsrc(V + (ktok0 + t * 64) * ldv + hk * D, (size_t)max(Skv - t * 64, 0) * ldv2);
+    const uint32_t dst = lds0 + (uint32_t)(2 * TB * (t & 1) + 4096 * wu);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      attn_dma16(rk, dst + 1024 * p, (vk + 4u * p * ldk2) ^ (16u * p));
+      attn_dma16(rv, dst + TB + 1024 * p, (vv + 4u * p * ldv2) ^ (16u * p));
+    }
+  };
+  if constexpr (PF == 0) {
+    if (nt > 0) dma_tile(0);
+  } else {
+    if (nt > 0) load_tile(0, 0);
+    if (PF == 2 && nt > 1) load_tile(PF - 1, 1);
+  }
   for (int t2 = 0; t2 < nt; t2 += 2) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int t = t2 + u;
       if (t >= nt) break;
-      const int set = PF == 2 ? u : 0;
-      store_tile(set, u);
-      __syncthreads();
-      if (t + PF < nt) load_tile(set, t + PF);
+      if constexpr (PF == 0) {
+        __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0): this wave's DMAs of tile t have landed
+        __syncthreads();                     // ... everyone's; every read of the other buffer is done
+        if (t + 1 < nt) dma_tile(t + 1);
+      } else {
+        const int set = PF == 2 ? u : 0;
+        store_tile(set, u);
+        __syncthreads();
+        if (t + PF < nt) load_tile(set, t + PF);
+      }
       if (t >= ntw) continue;   // wave-uniform: every key of the tile is above this wave's diagonal
       const char* Kl = smem + u * 2 * TB;
       const char* Vl = Kl + TB;
@@ -728,7 +786,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(const bf16* __restrict__
 // (row reads of the swizzled K / V images), dS = P∘(dP − delta) in registers, dQᵀ += Kᵀ·dSᵀ with Kᵀ from the
 // transposed reads of the same K image and dS as the B operand in accumulator-row slot order (no lane
 // movement).  Writes delta for the dK/dV kernel, as attn_bwd_dq_k.
-template <bool DROP>
+template <bool DROP, bool DMA = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq128_k(const bf16* __restrict__ dO, const bf16* __restrict__ O,
                                                         const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                         const bf16* __restrict__ V, const float* __restrict__ lse,
@@ -809,15 +867,40 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq128_k(const bf16* __restric
   const int ra0 = 4 * (g >> 1) + qq, c0 = 2 * (g & 1) + (pp >> 1);
   int at0 = toff(ra0, c0) + 8 * (pp & 1), at1 = toff(ra0 + 8, c0) + 8 * (pp & 1);
 
-  if (nt > 0) load_tile(0);
+  // DMA: K / V tiles by LDS-DMA as attn_fwd128_k<0> (no staging VGPRs / LDS stores, one barrier per tile)
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)smem);
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const uint32_t ldk2 = (uint32_t)ldk * 2, ldv2 = (uint32_t)ldv * 2;
+  const uint32_t xs = 16u * (uint32_t)((lane & 15) ^ ((lane >> 4) << 2));
+  const uint32_t vk = (16u * wu + (lane >> 4)) * ldk2 + xs, vv = (16u * wu + (lane >> 4)) * ldv2 + xs;
+  auto dma_tile = [&](int t) {
+    const rsrc_t rk = attn_rsrc(K + (tok0 + t * 64) * ldk + hk * D, (size_t)max(S - t * 64, 0) * ldk2);
+    const rsrc_t rv = attn_rsrc(V + (tok0 + t * 64) * ldv + hk * D, (size_t)max(S - t * 64, 0) * ldv2);
+    const uint32_t dst = lds0 + (uint32_t)(2 * TB * (t & 1) + 4096 * wu);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      attn_dma16(rk, dst + 1024 * p, (vk + 4u * p * ldk2) ^ (16u * p));
+      attn_dma16(rv, dst + TB + 1024 * p, (vv + 4u * p * ldv2) ^ (16u * p));
+    }
+  };
+  if (nt > 0) {
+    if constexpr (DMA) dma_tile(0);
+    else load_tile(0);
+  }
   for (int t2 = 0; t2 < nt; t2 += 2) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int t = t2 + u;
       if (t >= nt) break;
-      store_tile(u);
-      __syncthreads();
-      if (t + 1 < nt) load_tile(t + 1);
+      if constexpr (DMA) {
+        __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0): this wave's DMAs of tile t have landed
+        __syncthreads();
+        if (t + 1 < nt) dma_tile(t + 1);
+      } else {
+        store_tile(u);
+        __syncthreads();
+        if (t + 1 < nt) load_tile(t + 1);
+      }
       if (t >= ntw) continue;
       const char* Kl = smem + u * 2 * TB;
       const int k0 = t * 64;
@@ -879,28 +962,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq128_k(const bf16* __restric
         *reinterpret_cast<bf16x8*>(qrow + 32 * dt + 16 * hf) =
             bf16x8{(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)c[0], (bf16)c[1], (bf16)c[2], (bf16)c[3]};
     }
-}
-
-// LDS-DMA and raw-buffer helpers for attn_bwd_dkv128_k.  A raw buffer descriptor (stride 0) range-checks the
-// per-lane offset against num_records: rows past the end read as zero and never touch memory.
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-__device__ __forceinline__ rsrc_t attn_rsrc(const void* base, size_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0,
-                                           (int)(bytes > 0x7fffffffull ? 0x7fffffffull : bytes), 0x00020000);
-}
-// one wave-instruction of LDS-DMA: lane l's 16 B from rs + voff land at LDS m0v + 16·l (M0 saved / restored)
-__device__ __forceinline__ void attn_dma16(const rsrc_t& rs, uint32_t m0v, uint32_t voff) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "s"(m0v), "v"(voff), "s"(rs)
-      : "memory");
 }
 
 // dK / dV for D = 128 in the 32x32x16 form, two waves per SIMD: a 512-thread workgroup = 64 keys of one KV
@@ -1497,7 +1558,14 @@ void launch_attn_fwd(const void* q, const void* k, const void* v, int ldq, int l
   attn_fwd128_k<1, DR><<<grid, blk, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, ldq, ldk, ldv, kv_lens, \
                                              q_offs, (bf16*)o, lse, Sq, Skv, kv_rows, hq, hkv,                    \
                                              causal ? 1 | (attn_lpt() << 1) : 0, sl2, dp)
-    if (dp.thresh) F128(true); else F128(false);
+    if (attn_fwd_dma() && ldk % 128 == 0 && ldv % 128 == 0) {   // K / V by LDS-DMA (row strides in 256-B units)
+#define F128D(DR)                                                                                              \
+  attn_fwd128_k<0, DR><<<grid, blk, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, ldq, ldk, ldv, kv_lens, \
+                                             q_offs, (bf16*)o, lse, Sq, Skv, kv_rows, hq, hkv,                    \
+                                             causal ? 1 | (attn_lpt() << 1) : 0, sl2, dp)
+      if (dp.thresh) F128D(true); else F128D(false);
+#undef F128D
+    } else if (dp.thresh) F128(true); else F128(false);
 #undef F128
     LIPA_CHECK_LAUNCH();
     return;
@@ -1542,7 +1610,15 @@ void launch_attn_bwd(const void* dout, const void* q, const void* k, const void*
   attn_bwd_dq128_k<DR><<<gq2, blk, 0, st>>>((const bf16*)dout, (const bf16*)o, (const bf16*)q, (const bf16*)k,   \
                                             (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dq, S, hq, \
                                             hkv, causal ? 1 | (attn_lpt() << 1) : 0, scale, sl2, dp)
-    if (dp.thresh) DQ2(true); else DQ2(false);
+    if (attn_fwd_dma() && ldk % 128 == 0 && ldv % 128 == 0) {
+#define DQ2D(DR)                                                                                                 \
+  attn_bwd_dq128_k<DR, true><<<gq2, blk, 0, st>>>((const bf16*)dout, (const bf16*)o, (const bf16*)q,              \
+                                                  (const bf16*)k, (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, \
+                                                  (bf16*)dq, S, hq, hkv, causal ? 1 | (attn_lpt() << 1) : 0, scale,   \
+                                                  sl2, dp)
+      if (dp.thresh) DQ2D(true); else DQ2D(false);
+#undef DQ2D
+    } else if (dp.thresh) DQ2(true); else DQ2(false);
 #undef DQ2
     if (attn_dkv128() && ldq % 128 == 0) {   // the DMA row geometry needs 256-B-multiple Q row strides
 #define DKV3(DR)                                                                                                 \
