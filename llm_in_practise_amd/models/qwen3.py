@@ -276,6 +276,7 @@ class Qwen3Model(nn.Module):
         self.gradient_checkpointing = False
         self.ckpt_kwargs: dict = {}      # use_reentrant / policy (ops/linear.py checkpoint)
         self.pp = None          # parallel.pipeline_parallel stage link (inference PP), else None
+        self._rope_cache: dict = {}   # (B, S, inv_freq, factor) -> (cos, sin) for positions 0 .. S-1
 
     def rope(self, position_ids: torch.Tensor):
         ang = position_ids.reshape(-1).float()[:, None] * self.inv_freq[None, :]
@@ -285,10 +286,22 @@ class Qwen3Model(nn.Module):
         B, S = input_ids.shape
         start = cache.len if cache is not None else 0
         decoding = cache is not None and cache.pos is not None and S == 1
-        if position_ids is None:
-            position_ids = cache.pos[:, None] if decoding else \
-                torch.arange(start, start + S, device=input_ids.device).expand(B, S)
-        cos, sin = self.rope(position_ids)
+        if position_ids is None and not decoding and start == 0:
+            # positions 0 .. S-1 (every training step, every fresh prefill): the cos / sin tables depend only on
+            # (B, S) — computed once instead of ~7 small launches + their host time at the head of every step
+            key = (B, S, self.inv_freq.data_ptr(), self.attn_factor)
+            cs = self._rope_cache.get(key)
+            if cs is None:
+                if len(self._rope_cache) >= 8:
+                    self._rope_cache.clear()
+                cs = self.rope(torch.arange(S, device=input_ids.device).expand(B, S))
+                self._rope_cache[key] = cs
+            cos, sin = cs
+        else:
+            if position_ids is None:
+                position_ids = cache.pos[:, None] if decoding else \
+                    torch.arange(start, start + S, device=input_ids.device).expand(B, S)
+            cos, sin = self.rope(position_ids)
         x = self.embed_tokens(input_ids).reshape(B * S, -1)
         if self.pp is not None:
             x = self.pp.enter(x)        # stages > 0: the previous stage's hidden states

@@ -147,6 +147,7 @@ class _FlatOptimizer:
         self.max_grad_norm = max_norm
         nf4_cache_advance()
         self.flat.sync_grads()
+        self._prepared = True    # step() right behind: no second pass over the parameters
         g = self.flat.grad
         if use_native(g):
             native().grad_norm(g, float(max_norm), self.norm_out, False)
@@ -188,8 +189,10 @@ class AdamW(_FlatOptimizer):
 
     @torch.no_grad()
     def step(self, closure=None):
-        nf4_cache_advance()
-        self.flat.sync_grads()
+        if not getattr(self, "_prepared", False):   # (clip_grad_norm_ already did it)
+            nf4_cache_advance()
+            self.flat.sync_grads()
+        self._prepared = False
         self.step_count += 1
         b1, b2 = self.betas
         g = self.flat.grad
@@ -236,8 +239,10 @@ class AdamW8bit(_FlatOptimizer):
 
     @torch.no_grad()
     def step(self, closure=None):
-        nf4_cache_advance()
-        self.flat.sync_grads()
+        if not getattr(self, "_prepared", False):   # (clip_grad_norm_ already did it)
+            nf4_cache_advance()
+            self.flat.sync_grads()
+        self._prepared = False
         self.step_count += 1
         b1, b2 = self.betas
         g = self.flat.grad
