@@ -79,3 +79,19 @@ def test_generate_simple_minigpt_greedy_window():
     assert out.shape == (1, 25)
     nxt = m(out[:, 20 - 16 + 0:20])[:, -1].argmax(-1)
     assert nxt.item() == out[0, 20].item()
+
+
+def test_rope_table_cache_matches_explicit_positions():
+    """Qwen3Model caches the cos / sin tables of positions 0 .. S-1 per (B, S): the default-position forward
+    equals the forward with explicit position ids, call after call and across shapes"""
+    import torch
+    from llm_in_practise_amd.models.qwen3 import Qwen3ForCausalLM, qwen3_config
+    lm = Qwen3ForCausalLM.from_config(qwen3_config("qwen2-tiny"), dtype=torch.float32, seed=0).eval()
+    with torch.no_grad():
+        for B, S in ((2, 7), (1, 16), (2, 7)):
+            ids = torch.randint(0, 512, (B, S))
+            pos = torch.arange(S).expand(B, S)
+            a = lm.model(ids)
+            b = lm.model(ids, pos)
+            assert torch.equal(a, b)
+    assert len(lm.model._rope_cache) == 2
