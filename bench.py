@@ -20,6 +20,7 @@ import contextlib
 import json
 import os
 import sys
+import threading
 import time
 
 import torch
@@ -32,6 +33,7 @@ from llm_in_practise_amd.parallel import dist as D  # noqa: E402
 from llm_in_practise_amd.parallel.ddp import DistributedDataParallel  # noqa: E402
 from llm_in_practise_amd.peft.lora import LoraConfig, get_peft_model, quantize_model_nf4  # noqa: E402
 from llm_in_practise_amd.utils.gc_control import ManualGC  # noqa: E402
+from llm_in_practise_amd.utils.watchdog import Watchdog  # noqa: E402
 
 BASELINE_TOKENS_PER_S = None   # the reference publishes no fine-tune throughput
 MODEL_NAMES = {"qwen3-8b": "Qwen3-8B", "qwen3-14b": "Qwen3-14B", "qwen3-4b": "Qwen3-4B",
@@ -62,6 +64,15 @@ def _self_launch(n: int) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def _fault_injector(record: str, rank: int):
+    """``LIPA_BENCH_FAULT=<record>=<rank>:<step>:<kind>[;...]`` (kinds: utils/faults.py) — a fault injected into one
+    sub-record of the bench (faithful / selective / zero3) to test that the headline record survives it."""
+    from llm_in_practise_amd.utils.faults import FaultInjector
+    spec = ",".join(item.split("=", 1)[1] for item in os.environ.get("LIPA_BENCH_FAULT", "").split(";")
+                    if item.startswith(record + "="))
+    return FaultInjector(spec, rank=rank)
+
+
 def build(args, device):
     cfg = qwen3_config(args.model)
     t0 = time.time()
@@ -83,7 +94,7 @@ def build(args, device):
     return cfg, pm
 
 
-def zero3_subrecord(args, device, rank: int, world: int, sync) -> dict:
+def zero3_subrecord(args, device, rank: int, world: int, sync, beat=lambda: None) -> dict:
     """BASELINE config #4 at world > 1: ``Fine-Tuning/qwen3-14b-qlora-dist-deepspeed.py:164`` + ``ds_zero3_config.json``
     — the QLoRA model (--zero3-model, Qwen3-14B by default) on the ZeRO-3 engine, the client paged 8-bit AdamW on
     each rank's partition, the same micro-batch / GA / sequence length as the headline, GA micro-batches fused
@@ -118,17 +129,21 @@ def zero3_subrecord(args, device, rank: int, world: int, sync) -> dict:
         engine.step()
         return loss
 
+    inj = _fault_injector("zero3", rank)
     for _ in range(warm):
         step()
+        beat()
     sync()
     if device.type == "cuda":
         torch.cuda.reset_peak_memory_stats(device)
     D.COMM.reset()
     D.COMM.enabled = True
     t0 = time.perf_counter()
-    for _ in range(args.zero3_steps):
+    for i in range(args.zero3_steps):
+        inj.check(i)
         loss = step()
         D.COMM.step()
+        beat()
     sync()
     el = D.all_reduce_max(time.perf_counter() - t0)
     D.COMM.enabled = False
@@ -201,6 +216,14 @@ def main():
     ap.add_argument("--host-steps", type=int, default=2,
                     help="after the timed steps, issue this many steps onto an idle device and record the host "
                          "launch time of one step (host_launch_ms; LIPA_HOST_PROFILE=<file> adds a cProfile of them)")
+    ap.add_argument("--stall-timeout-s", type=float, default=900.0,
+                    help="watchdog (utils/watchdog.py): no progress (model built, one step finished) for this long "
+                         "during the headline -> diagnostic with every thread's stack, exit 3 (a collective stall must "
+                         "not wait out the process group's 30-minute timeout)")
+    ap.add_argument("--subrecord-budget-s", type=float, default=None,
+                    help="time budget of each sub-record (host / faithful / selective / zero3); past it the headline "
+                         "line is printed with '<record>': {'error': ...} and the process exits 0 "
+                         "(default: 240 s, 420 s for the zero3 sub-record, which builds its own model)")
     args = ap.parse_args()
     from llm_in_practise_amd.ops import linear as _lin
     if args.nf4_gemm is not None:        # else the LIPA_NF4_GEMM environment choice stands
@@ -214,8 +237,11 @@ def main():
     rank, local_rank, world = D.init_distributed()
     if world != args.gpus:
         raise SystemExit(f"[bench] --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    wd = Watchdog(rank)
+    wd.arm(args.stall_timeout_s, "headline: build + warmup", exit_code=3)
     device = torch.device("cuda", D.local_device_index(local_rank)) if torch.cuda.is_available() else torch.device("cpu")
     cfg, model = build(args, device)
+    wd.beat()
     total_steps = args.warmup + args.steps
     engine = None
     if args.strategy == "zero3":
@@ -293,6 +319,7 @@ def main():
 
     for i in range(args.warmup):
         loss = step()
+        wd.beat()
         if i == 0:
             sync()
             log(f"[bench] first step done, loss={loss.item():.4f}")
@@ -305,16 +332,19 @@ def main():
     _lin.GEMM_STATS.clear()         # GEMM launches by form over the timed steps (kernel provenance)
     t0 = time.perf_counter()
     dbg = os.environ.get("LIPA_BENCH_DEBUG_LOSS") == "1"     # per-step loss / grad norm (syncs: debug only)
+    wd.arm(args.stall_timeout_s, "headline: timed steps", exit_code=3)
     for _ in range(args.steps):
         loss = step()
         gcm.step()
         D.COMM.step()
+        wd.beat()
         if dbg:
             gn = getattr(engine, "last_grad_norm", None) if engine is not None else None
             print(f"[rank {rank}] step loss={loss.item():.6f} grad_norm={None if gn is None else float(gn):}",
                   file=sys.stderr, flush=True)
     sync()
     elapsed = D.all_reduce_max(time.perf_counter() - t0)
+    wd.disarm()
     D.COMM.enabled = False
     comm = D.COMM.summary() if world > 1 else None
     gemm_forms = {k: round(v / max(1, args.steps), 2) for k, v in sorted(_lin.GEMM_STATS.items())}
@@ -330,10 +360,101 @@ def main():
     log(f"[bench] loss={loss.item():.4f} {ms:.1f} ms/step  {tps:,.0f} tok/s  "
         f"~{tps * fl_per_tok / world / 1e12:.0f} TFLOP/s/GPU (matmul)  peak HBM {mem:.1f} GiB")
 
+    # ---- the headline record, complete before any sub-record runs (every rank holds it; rank 0 prints it)
+    rec = {
+        "metric": f"tokens/sec (whole node) {MODEL_NAMES.get(args.model, args.model)} "
+                  f"{'QLoRA' if args.mode == 'qlora' else 'LoRA'} fine-tune at 1/2/4/8 MI355X",
+        "value": round(tps, 1),
+        "unit": "tokens/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 2),
+        "host_launch_ms": None,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (round(tps / BASELINE_TOKENS_PER_S, 3) if BASELINE_TOKENS_PER_S else None),
+        "dtype": "bf16" if device.type == "cuda" else "fp32",
+        "data": "synthetic",
+        "config": {
+            "model": MODEL_NAMES.get(args.model, args.model),
+            "global_batch": args.micro_batch * args.grad_accum * world,
+            "seq_len": args.seq_len,
+            "parallelism": f"dp{world}" if engine is None else f"zero3-dp{world}",
+            "micro_batch": args.micro_batch,
+            "grad_accum": args.grad_accum,
+            "quant": "nf4+double_quant" if args.mode == "qlora" else "none",
+            "nf4_gemm": args.nf4_gemm,
+            # kernel provenance of the timed steps (ops/linear.py GEMM_STATS): GEMM launches per step by form —
+            # gemm4w = the hand-written HIP GEMM on a bf16 operand, gemm4w-nf4 = the same kernel reading NF4 codes,
+            # library = torch.matmul (shapes gemm4w does not take); nf4-expansion = bf16 copies of NF4 bases
+            "gemm_backend": "gemm4w" if device.type == "cuda" else "torch-cpu",
+            "gemm_launches_per_step": {k: v for k, v in gemm_forms.items() if k != "nf4-expansion"},
+            "nf4_expansions_per_step": gemm_forms.get("nf4-expansion", 0),
+            "lora": f"r{args.lora_r}/a{args.lora_alpha}/drop{args.lora_dropout}/{args.targets}",
+            "optimizer": args.optim if engine is None else f"zero3-{engine.optim_name}",
+            "gradient_checkpointing": bool(args.grad_ckpt),
+            "ga_execution": "fused-pass" if args.ga_fusion else "sequential",
+            "weights": "random-init",
+            "peak_hbm_gib": round(mem, 1),
+            "dist_backend": (torch.distributed.get_backend() if D.is_dist() else "none"),
+            "dist_world_size": D.world_size(),
+            # padded = micro x 512 x GA x world / step; non-pad counts only label != -100 positions
+            # (synthetic ids carry no padding, so the two agree here)
+            "tokens_per_s_padded": round(tps, 1),
+            "tokens_per_s_nonpad": round(tps * nonpad_frac, 1),
+        },
+        "comm": dict(comm, **D.comm_environment()) if comm is not None else {"skipped": "single rank: no collectives"},
+    }
+    if world == 1:
+        rec["zero3"] = {"skipped": "single rank (the ZeRO-3 sub-record runs when world > 1)"}
+
+    emitted = [False]
+    emit_lock = threading.Lock()
+
+    def emit():
+        with emit_lock:
+            if not emitted[0]:
+                emitted[0] = True
+                if D.is_main():
+                    print(json.dumps(rec), flush=True)
+
+    # ---- sub-records, each fault-isolated: an exception becomes '<key>': {'error': ...}; a stall (no progress for
+    # the budget) prints the headline line with that error from the watchdog and exits 0.  After a failure at
+    # world > 1 this rank issues no further collective (its peers may still be inside one): the remaining
+    # sub-records are skipped and the process ends without the final barrier.
+    poisoned = [False]
+    budget_default = args.subrecord_budget_s or 240.0
+
+    def sub(key, fn, budget_s=None):
+        budget_s = budget_s or budget_default
+        if poisoned[0]:
+            rec[key] = {"skipped": "an earlier sub-record failed on this rank"}
+            return None
+
+        def expire():
+            rec[key] = {"error": f"watchdog: no progress for {budget_s:.0f} s (collective stall, dead peer or hang)"}
+            emit()
+        wd.arm(budget_s, f"sub-record {key}", on_expire=expire, exit_code=0)
+        try:
+            out = fn(wd.beat)
+        except Exception as e:   # noqa: BLE001 - every failure of a sub-record is recorded, none ends the run
+            import traceback
+            traceback.print_exc()
+            rec[key] = {"error": f"{type(e).__name__}: {e}"[:600]}
+            poisoned[0] = world > 1
+            if device.type == "cuda":
+                torch.cuda.empty_cache()
+            return None
+        finally:
+            wd.disarm()
+        if out is not None:
+            rec[key] = out
+        return out
+
     # host launch cost of one headline step (untimed, after the timed steps): the step is issued onto an idle
     # device and timed until step() returns — how far the Python/launch side is from becoming the bottleneck
-    host_ms = None
-    if args.host_steps > 0:
+    def host_record(beat):
         prof = None
         if os.environ.get("LIPA_HOST_PROFILE"):
             import cProfile
@@ -349,6 +470,7 @@ def main():
                 prof.disable()
             hs.append(time.perf_counter() - h0)
             gcm.step()
+            beat()
         sync()
         host_ms = round(1000 * min(hs), 2)
         log(f"[bench] host launch time of one step: {host_ms:.1f} ms (device {ms:.1f} ms/step)")
@@ -356,24 +478,30 @@ def main():
             import pstats
             with open(os.environ["LIPA_HOST_PROFILE"], "w") as f:
                 pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(60)
+        rec["host_launch_ms"] = host_ms
+        return None
 
-    def timed_ckpt(policy: str, n_steps: int, reentrant: bool) -> dict:
+    def timed_ckpt(policy: str, n_steps: int, reentrant: bool, beat) -> dict:
         """BASELINE.md's config as the reference runs it (Fine-Tuning/qwen3-8b-qlora-dist.py:137-138, 162-163):
         gradient checkpointing on and the GA micro-steps one after another (no_sync on all but the last), same
         model / optimizer / data, timed the same way as the headline.  policy "full" = HF's whole-layer
         recompute (use_reentrant=False, as the reference passes); "selective" = this framework's cheaper recompute,
         in the reentrant form by default (no saved-tensor pack / unpack hooks: ~20 ms less host time per step,
         which the selective step — 73 ms of GPU work — would otherwise wait on)."""
+        inj = _fault_injector("faithful" if policy == "full" else "selective", rank)
         model.gradient_checkpointing_enable({"use_reentrant": reentrant, "policy": policy})
         for _ in range(args.faithful_warmup):
             step(fused=0)
+            beat()
         sync()
         if device.type == "cuda":
             torch.cuda.reset_peak_memory_stats(device)
         tf0 = time.perf_counter()
-        for _ in range(n_steps):
+        for i in range(n_steps):
+            inj.check(i)
             floss = step(fused=0)
             gcm.step()
+            beat()
         sync()
         fel = D.all_reduce_max(time.perf_counter() - tf0)
         fms = 1000 * fel / n_steps
@@ -412,79 +540,33 @@ def main():
                 "checkpoint_policy": policy,
                 "micro_batch": args.micro_batch, "grad_accum": args.grad_accum, "peak_hbm_gib": round(fmem, 1)}
 
-    faithful = selective = None
+    if args.host_steps > 0:
+        sub("host_launch_ms", host_record)
     if engine is None and not (args.grad_ckpt and not args.ga_fusion):
         if args.faithful_steps > 0:
-            faithful = timed_ckpt("full", args.faithful_steps, bool(args.ckpt_reentrant))
+            sub("faithful", lambda beat: timed_ckpt("full", args.faithful_steps, bool(args.ckpt_reentrant), beat))
         if args.selective_steps > 0:
-            selective = timed_ckpt("selective", args.selective_steps, bool(args.selective_reentrant))
+            sub("selective_ckpt",
+                lambda beat: timed_ckpt("selective", args.selective_steps, bool(args.selective_reentrant), beat))
 
-    zero3 = None
-    if world > 1 and engine is None and args.zero3_steps > 0:
-        del step
+    if world > 1 and engine is None and args.zero3_steps > 0 and poisoned[0]:
+        rec["zero3"] = {"skipped": "an earlier sub-record failed on this rank"}
+    elif world > 1 and engine is None and args.zero3_steps > 0:
+        del step, timed_ckpt, host_record
         model = opt = sched = ddp = data = None
         spent[0] = None
-        zero3 = zero3_subrecord(args, device, rank, world, sync)
+        sub("zero3", lambda beat: zero3_subrecord(args, device, rank, world, sync, beat),
+            args.subrecord_budget_s or 420.0)
     gcm.__exit__(None, None, None)
-    if D.is_main():
-        rec = {
-            "metric": f"tokens/sec (whole node) {MODEL_NAMES.get(args.model, args.model)} "
-                      f"{'QLoRA' if args.mode == 'qlora' else 'LoRA'} fine-tune at 1/2/4/8 MI355X",
-            "value": round(tps, 1),
-            "unit": "tokens/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms, 2),
-            "host_launch_ms": host_ms,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": (round(tps / BASELINE_TOKENS_PER_S, 3) if BASELINE_TOKENS_PER_S else None),
-            "dtype": "bf16" if device.type == "cuda" else "fp32",
-            "data": "synthetic",
-            "config": {
-                "model": MODEL_NAMES.get(args.model, args.model),
-                "global_batch": args.micro_batch * args.grad_accum * world,
-                "seq_len": args.seq_len,
-                "parallelism": f"dp{world}" if engine is None else f"zero3-dp{world}",
-                "micro_batch": args.micro_batch,
-                "grad_accum": args.grad_accum,
-                "quant": "nf4+double_quant" if args.mode == "qlora" else "none",
-                "nf4_gemm": args.nf4_gemm,
-                # kernel provenance of the timed steps (ops/linear.py GEMM_STATS): GEMM launches per step by form —
-                # gemm4w = the hand-written HIP GEMM on a bf16 operand, gemm4w-nf4 = the same kernel reading NF4 codes,
-                # library = torch.matmul (shapes gemm4w does not take); nf4-expansion = bf16 copies of NF4 bases
-                "gemm_backend": "gemm4w" if device.type == "cuda" else "torch-cpu",
-                "gemm_launches_per_step": {k: v for k, v in gemm_forms.items() if k != "nf4-expansion"},
-                "nf4_expansions_per_step": gemm_forms.get("nf4-expansion", 0),
-                "lora": f"r{args.lora_r}/a{args.lora_alpha}/drop{args.lora_dropout}/{args.targets}",
-                "optimizer": args.optim if engine is None else f"zero3-{engine.optim_name}",
-                "gradient_checkpointing": bool(args.grad_ckpt),
-                "ga_execution": "fused-pass" if args.ga_fusion else "sequential",
-                "weights": "random-init",
-                "peak_hbm_gib": round(mem, 1),
-                "dist_backend": (torch.distributed.get_backend() if D.is_dist() else "none"),
-                "dist_world_size": D.world_size(),
-                # padded = micro x 512 x GA x world / step; non-pad counts only label != -100 positions
-                # (synthetic ids carry no padding, so the two agree here)
-                "tokens_per_s_padded": round(tps, 1),
-                "tokens_per_s_nonpad": round(tps * nonpad_frac, 1),
-            },
-        }
-        if comm is not None:
-            rec["comm"] = comm
-        else:
-            rec["comm"] = {"skipped": "single rank: no collectives"}
-        if zero3 is not None:
-            rec["zero3"] = zero3
-        elif world == 1:
-            rec["zero3"] = {"skipped": "single rank (the ZeRO-3 sub-record runs when world > 1)"}
-        if faithful is not None:
-            rec["faithful"] = faithful
-        if selective is not None:
-            rec["selective_ckpt"] = selective
-        print(json.dumps(rec), flush=True)
+    emit()
+    if poisoned[0]:
+        # a peer may still be inside a collective of the failed sub-record: no barrier / destroy from here
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+    wd.arm(120.0, "shutdown", exit_code=0)
     D.destroy()
+    wd.disarm()
 
 
 if __name__ == "__main__":

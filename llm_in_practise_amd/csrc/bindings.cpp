@@ -871,7 +871,9 @@ Tensor gemm4w_loradx(Tensor dy, Tensor w, optional<Tensor> wscale, int64_t n_w4,
   int bn = 0, bm = 0;
   TORCH_CHECK((bn_req == 0 || bn_req == 128 || bn_req == 256) && (bm_req == 0 || bm_req == 128 || bm_req == 256),
               "gemm4w_loradx: bn / bm 0 (plan), 128 or 256");
-  gemm4w_plan(M, N, K, true, (int)bn_req, 1, &bn, (int)bm_req, &bm, w4);
+  // the LoRA dX kernel is instantiated for 128- and 256-wide tiles only: the plan must not return 192
+  gemm4w_plan(M, N, K, true, bn_req ? (int)bn_req : -1, 1, &bn, (int)bm_req, &bm, w4);
+  TORCH_CHECK(bn == 128 || bn == 256, "gemm4w_loradx: planned tile width ", bn, " has no kernel");
   auto dx = at::empty({M, N}, dy.options());
   launch_gemm4w_loradx(dy.data_ptr(), dy.stride(0), b.ptr, b.ld, b.scale, nullptr, dx.data_ptr(), ld, M, N, K, bn, bm,
                        stream());

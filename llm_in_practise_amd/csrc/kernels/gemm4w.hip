@@ -112,7 +112,8 @@ bool gemm4w_supported(int M, int N, int K, int lda, int ldb, bool bt, bool w4) {
 // reduce launch (its fp32 slabs: M·N·(8s + 2) bytes at ≈12 TB/s effective + a launch).  At M = 2048
 // (bf16) this picks: q|k|v fwd 256 × 192 (256 tiles); gate|up fwd / LM head 256 × 256; o fwd, the dX
 // GEMMs to d_model and down dX 128 × 256; down fwd and gate|up dX 256 × 256 with 2 splits.
-// Callers may force bn / bm / splits through the binding arguments (the A/B scripts do).
+// Callers may force bn / bm / splits through the binding arguments (the A/B scripts do); bn_req = -1 excludes
+// the 192 tile (the LoRA dX kernel has no 192-wide instance).
 struct G4wCfg {
   int bm, bn, splits;
 };
@@ -127,7 +128,8 @@ G4wCfg gemm4w_cfg(int M, int N, int K, bool bt, int bn_req, int sp_req, int bm_r
     if (bm_req && bm != bm_req) continue;
     for (int bn : {256, 192, 128}) {
       if (bn == 192 && (w4 || (bt && bm != 256))) continue;   // (instantiated: NT any height, BT 256-high)
-      if (bn_req && bn != bn_req) continue;
+      if (bn_req > 0 && bn != bn_req) continue;
+      if (bn_req < 0 && bn == 192) continue;                    // -1: any width the caller instantiates but 192
       const int tiles = tiles_of(M, N, bm, bn);
       double kt_us = bn == 256 ? (bt ? 1.52 : 1.5) : bn == 192 ? (bt ? 1.24 : 1.22) : 0.92;
       if (bm == 128) kt_us *= 0.56;

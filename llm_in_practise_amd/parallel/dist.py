@@ -48,6 +48,21 @@ def init_distributed(backend: str | None = None, timeout_s: int = 1800) -> tuple
     return env.rank, env.local_rank, env.world_size
 
 
+def comm_environment() -> dict:
+    """What a multi-rank record needs to be reproduced: the collective library's version (RCCL on ROCm) and the
+    NCCL_* / RCCL_* / TORCH_NCCL_* environment the run saw."""
+    out: dict = {}
+    try:
+        if torch.cuda.is_available() and is_dist() and dist.get_backend() == "nccl":
+            v = torch.cuda.nccl.version()
+            out["rccl_version" if torch.version.hip else "nccl_version"] = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+    except Exception as e:   # pragma: no cover - the version query is informational
+        out["rccl_version"] = f"unavailable ({type(e).__name__})"
+    out["comm_env"] = {k: v for k, v in sorted(os.environ.items())
+                       if k.startswith(("NCCL_", "RCCL_", "TORCH_NCCL_")) or k == "HSA_ENABLE_IPC_MODE_LEGACY"}
+    return out
+
+
 def is_dist() -> bool:
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 

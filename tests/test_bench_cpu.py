@@ -127,3 +127,47 @@ def test_awq_infer_bench_tiny(tmp_path):
     assert d["int4"]["kl_vs_bf16"] < 0.05 and d["int4"]["top1_agree_vs_bf16"] > 0.5
     assert d["int4"]["serve"]["output_tok_per_s"] > 0
     assert [x["batch"] for x in d["int4"]["decode"]] == [1, 4]
+
+
+def _bench_with_fault(world, fault, extra=(), hang_s=None, timeout=600):
+    env = dict(os.environ, OMP_NUM_THREADS="1", LIPA_BENCH_FAULT=fault)
+    if hang_s is not None:
+        env["FAULT_HANG_S"] = str(hang_s)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(world), "--steps", "1", "--warmup", "1", "--model", "qwen3-tiny", "--seq-len", "64",
+           "--host-steps", "1", "--zero3-steps", "2", *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["value"] > 0 and d["ms_per_step"] > 0 and d["n_gpus"] == world   # the headline survived
+    _check_comm(d["comm"], "all_reduce")
+    return d, r.stderr
+
+
+@pytest.mark.parametrize("world,fault", [(2, "zero3=1:0:raise"), (4, "zero3=*:1:raise"), (4, "zero3=2:0:raise")])
+def test_bench_headline_survives_zero3_failure(world, fault):
+    """a failure inside the ZeRO-3 sub-record (one rank or all) is recorded as zero3.error; the headline line is
+    printed and the job exits 0 (bench.py sub())"""
+    d, _ = _bench_with_fault(world, fault, ["--faithful-steps", "0", "--selective-steps", "0"])
+    assert "error" in d["zero3"], d["zero3"]
+
+
+def test_bench_headline_survives_zero3_hang():
+    """a rank that hangs inside the ZeRO-3 sub-record: every rank's watchdog ends the sub-record after its budget,
+    rank 0 prints the headline with the watchdog's error"""
+    d, err = _bench_with_fault(2, "zero3=1:0:hang", ["--faithful-steps", "0", "--selective-steps", "0",
+                                                     "--subrecord-budget-s", "15"], hang_s=300)
+    assert d["zero3"]["error"].startswith("watchdog"), d["zero3"]
+    assert "[watchdog] rank 0" in err
+
+
+def test_bench_faithful_failure_skips_later_subrecords():
+    """a failure in the faithful sub-record at world 2: recorded; the later sub-records are skipped on that rank
+    (its peers may still be inside a collective) and the headline is printed"""
+    d, _ = _bench_with_fault(2, "faithful=*:0:raise", ["--faithful-steps", "2", "--selective-steps", "1"])
+    assert "error" in d["faithful"]
+    assert "skipped" in d["selective_ckpt"] and "skipped" in d["zero3"]
+    assert d["host_launch_ms"] is not None and d["host_launch_ms"] > 0

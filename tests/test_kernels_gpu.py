@@ -807,7 +807,8 @@ def test_gemm4w_lora_epilogue(native_ext, M, N, K, branches, w4, resid):
 @pytest.mark.parametrize("M,Nk,K,r,w4", [(2048, 4096, 6144, 8, False), (1024, 4096, 6144, 8, True),
                                        (2048, 4096, 6144, 8, True),     # the 256-row W4 tile (was wrong: asm-load copies)
                                        (300, 640, 1024, 16, False), (256, 768, 512, 32, True),
-                                       (512, 1152, 256, 8, False)])
+                                       (512, 1152, 256, 8, False),
+                                       (2048, 5120, 7168, 8, False)])   # Qwen3-14B q|k|v dX: the plan would pick 192
 def test_gemm4w_loradx_epilogue(native_ext, M, Nk, K, r, w4):
     """dX = dY·W + Σ_b D_b(g_b·A_b)/(1 - p_b) with each adapter's keep bits, the LoRA term added in the
     gemm4w dX epilogue, vs fp32 (and vs the lora_dx2 + C-matrix path)"""
