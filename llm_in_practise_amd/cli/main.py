@@ -422,6 +422,71 @@ def cmd_eval_quant(a):
     print(json.dumps({"self_ppl": ppl, "pass": ppl < PASS_THRESHOLD, "threshold": PASS_THRESHOLD}))
 
 
+_VLLM_QUANT = {"awq": ("awq", "compressed-tensors"), "awq_marlin": ("awq", "compressed-tensors"),
+               "gptq": ("gptq", "compressed-tensors"), "gptq_marlin": ("gptq", "compressed-tensors"),
+               "compressed-tensors": ("compressed-tensors", "awq", "gptq")}
+
+
+def _vllm_compat(a):
+    """Map vLLM's ``vllm serve`` flags onto ``lipa serve`` so the reference's manifests apply unchanged
+    (``LLM_on_Kubernetes/Inference_Platfrom/01-Base/vLLM/vllm-deployment.yaml:97-114``, the litellm-proxy compose
+    files, ``07-L1-Cache/LMCache/vllm-statefulset-lmcache.yaml``):
+
+    * positional ``MODEL`` (the vllm-openai image's first arg) = ``--model``;
+    * ``--max-num-seqs`` = ``--max-batch``; ``--gpu-memory-utilization`` sizes the KV pool (``kv_slots_for_budget``);
+    * ``--dtype auto|bfloat16`` run bf16 (the kernels' compute dtype); ``half``/``float16`` are served in bf16
+      with a notice (no fp16 kernel path on this stack);
+    * ``--quantization awq|gptq|compressed-tensors`` check the checkpoint's ``quantization_config`` (the int4
+      W4A16 path loads it either way); ``bitsandbytes`` = in-flight NF4 (``--quant nf4``);
+    * ``--kv-transfer-config`` with an LMCache connector = the prefix cache with the host tier
+      (``LMCACHE_MAX_LOCAL_CPU_SIZE`` GB) and, from ``LMCACHE_REMOTE_URL`` (lm://host:port), the shared
+      ``lipa kv-server`` at http://host:port; ``LMCACHE_CHUNK_SIZE`` = the prefix block;
+    * ``--enforce-eager`` = no decode hipGraphs; ``--trust-remote-code``, ``--disable-log-requests``,
+      ``--disable-usage-stats`` are accepted (nothing to switch).
+    Returns ``a`` (mutated)."""
+    import sys
+    if getattr(a, "model_tag", None):
+        if a.model and a.model != a.model_tag:
+            raise SystemExit(f"model given twice: positional {a.model_tag!r} and --model {a.model!r}")
+        a.model = a.model_tag
+    if not getattr(a, "model", None):
+        raise SystemExit("lipa serve: a model is required (--model DIR or positional DIR)")
+    dt = getattr(a, "dtype", "auto")
+    if dt in ("half", "float16"):
+        print(f"[lipa serve] --dtype {dt}: this stack computes in bfloat16 (MFMA bf16 kernels); serving bf16",
+              file=sys.stderr)
+    elif dt == "float32":
+        raise SystemExit("--dtype float32: not supported (bf16 kernels)")
+    vq = getattr(a, "vllm_quant", None)
+    if vq == "bitsandbytes":
+        a.quant = "nf4"
+    elif vq is not None:
+        cfgp = os.path.join(a.model, "config.json")
+        qc = None
+        if os.path.exists(cfgp):
+            with open(cfgp) as f:
+                qc = (json.load(f).get("quantization_config") or {}).get("quant_method")
+        if qc is None:
+            raise SystemExit(f"--quantization {vq}: {cfgp} declares no quantization_config")
+        if qc not in _VLLM_QUANT[vq]:
+            raise SystemExit(f"--quantization {vq}: the checkpoint is quantized with {qc!r}")
+    kvt = getattr(a, "kv_transfer_config", None)
+    if kvt:
+        spec = json.loads(kvt)
+        if str(spec.get("kv_connector", "")).startswith("LMCache"):
+            a.prefix_caching = True
+            if os.environ.get("LMCACHE_LOCAL_CPU", "True").lower() in ("1", "true") and not a.host_blocks:
+                gb = float(os.environ.get("LMCACHE_MAX_LOCAL_CPU_SIZE", "5"))
+                a.prefix_block = int(os.environ.get("LMCACHE_CHUNK_SIZE", a.prefix_block))
+                a.host_blocks = -int(gb * 2 ** 30)     # bytes: converted to blocks once the model is known
+            url = os.environ.get("LMCACHE_REMOTE_URL")
+            if url and not a.kv_remote_url:
+                a.kv_remote_url = "http://" + url.split("://", 1)[-1] if url.startswith("lm://") else url
+        else:
+            raise SystemExit(f"--kv-transfer-config: connector {spec.get('kv_connector')!r} not supported")
+    return a
+
+
 def _serving_engine_from_args(a, tp=None, tpg=None, ppg=None):
     """Build the ServingEngine ``lipa serve`` describes (runs in the engine process by default)."""
     from ..infer.engine import ServingEngine
@@ -429,14 +494,27 @@ def _serving_engine_from_args(a, tp=None, tpg=None, ppg=None):
     g = lambda k, d=None: getattr(a, k, d)      # noqa: E731  (namespaces built by other commands)
     m = _load_for_inference(a.model, g("adapter"), quant=g("quant"), tp_group=tpg, pp_group=ppg)
     tok = load_tokenizer(g("tokenizer") or a.model)
+    if g("chat_template"):                        # vLLM --chat-template: a jinja file (or the template itself)
+        path = g("chat_template")
+        text = open(path).read() if os.path.exists(path) else path
+        if hasattr(tok, "chat_template"):
+            tok.chat_template = text
     loras = dict(spec.split("=", 1) for spec in g("lora_modules")) if g("lora_modules") else None
+    host_blocks = g("host_blocks", 0)
+    block = g("prefix_block", 64)
+    if host_blocks < 0:                           # a byte budget (LMCache LMCACHE_MAX_LOCAL_CPU_SIZE): in blocks
+        cfg = m.config
+        per = 2 * cfg.num_hidden_layers * block * cfg.num_key_value_heads * cfg.head_dim * 2
+        host_blocks = max(1, -host_blocks // per)
     return ServingEngine(m, tok, model_name=g("served_model_name") or os.path.basename(a.model.rstrip("/")),
                          max_batch=g("max_batch", 32), system_prompt=g("system"), tp_group=tp,
                          max_model_len=g("max_model_len"),
                          prefix_cache_blocks=g("prefix_blocks", 1024) if g("prefix_caching") else 0,
+                         prefix_block=block,
                          chunked_prefill=g("max_batched_tokens", 2048) if g("chunked_prefill") else 0,
-                         lora_modules=loras, host_cache_blocks=g("host_blocks", 0),
-                         kv_remote_url=g("kv_remote_url"))
+                         lora_modules=loras, host_cache_blocks=host_blocks,
+                         kv_remote_url=g("kv_remote_url"), gpu_memory_utilization=g("gpu_memory_utilization"),
+                         use_graphs=False if g("enforce_eager") else None)
 
 
 def cmd_serve(a):
@@ -444,6 +522,7 @@ def cmd_serve(a):
     process only formats and streams — ``infer/mp_engine.py``); TP/PP groups and
     ``--no-engine-process`` keep the engine in-process."""
     from ..infer.server import serve
+    _vllm_compat(a)
     if getattr(a, "lora_modules", None) and not a.enable_lora:
         raise SystemExit("--lora-modules needs --enable-lora (vLLM semantics)")
     moderation = None
@@ -462,7 +541,8 @@ def cmd_serve(a):
         if tp is not None and eng.tp_rank != 0:
             eng.follower_loop()              # TP / PP followers replay rank 0's iterations
             return
-    serve(eng, a.host, a.port, api_key=a.api_key, moderation=moderation)
+    serve(eng, a.host, a.port, api_key=a.api_key, moderation=moderation,
+          log_level=getattr(a, "uvicorn_log_level", "info"))
 
 
 def cmd_serve_deploy(a):
@@ -760,8 +840,20 @@ def _lm_args(p):
     p.add_argument("--local_rank", type=int, default=None)
 
 
+class _Parser(argparse.ArgumentParser):
+    """vLLM's parser accepts ``--flag_name`` for ``--flag-name``; ``lipa serve`` does too (the reference's
+    compose files pass ``--trust_remote_code``).  Other subcommands keep their own underscore flags."""
+
+    def parse_known_args(self, args=None, namespace=None):
+        args = list(sys.argv[1:] if args is None else args)
+        if args and args[0] == "serve":
+            args = [("--" + a[2:].split("=", 1)[0].replace("_", "-") + ("=" + a.split("=", 1)[1] if "=" in a else ""))
+                    if a.startswith("--") else a for a in args]
+        return super().parse_known_args(args, namespace)
+
+
 def build_parser() -> argparse.ArgumentParser:
-    ap = argparse.ArgumentParser(prog="lipa", description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap = _Parser(prog="lipa", description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     sub = ap.add_subparsers(dest="cmd", required=True)
 
     p = sub.add_parser("minigpt-train")
@@ -776,6 +868,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--n_layers", type=int, default=2)
     p.add_argument("--causal", action="store_true", help="fix the reference's missing causal mask")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--load-format", dest="load_format", default="auto", choices=["auto", "safetensors", "pt"],
+                   help="vLLM flag: checkpoint files are read by their extension (safetensors first)")
     p.add_argument("--device", default="cpu")
     p.add_argument("--out", default="mg_edu_gpt.pth")
     p.set_defaults(fn=cmd_minigpt_train)
@@ -874,14 +968,34 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--max_new", type=int, default=256)
     p.set_defaults(fn=cmd_eval_quant)
 
-    p = sub.add_parser("serve")
-    p.add_argument("--model", required=True)
+    p = sub.add_parser("serve", help="OpenAI-compatible server; also takes vLLM's `vllm serve` flags (_vllm_compat)")
+    p.add_argument("model_tag", nargs="?", default=None, metavar="MODEL", help="model dir (vLLM positional form)")
+    p.add_argument("--model", default=None)
     p.add_argument("--adapter")
     p.add_argument("--tokenizer")
     p.add_argument("--quant", choices=["nf4"])
+    p.add_argument("--quantization", dest="vllm_quant", default=None,
+                   choices=["awq", "awq_marlin", "gptq", "gptq_marlin", "compressed-tensors", "bitsandbytes"],
+                   help="vLLM flag: int4 checkpoints load by their quantization_config; bitsandbytes = NF4")
+    p.add_argument("--dtype", default="auto", choices=["auto", "bfloat16", "bf16", "half", "float16", "float32"])
+    p.add_argument("--gpu-memory-utilization", dest="gpu_memory_utilization", type=float, default=None,
+                   help="vLLM flag: fraction of device memory for weights + KV; sizes the KV slot pool")
     p.add_argument("--host", default="0.0.0.0")
     p.add_argument("--port", type=int, default=8000)
-    p.add_argument("--max-batch", dest="max_batch", type=int, default=32)
+    p.add_argument("--max-batch", "--max-num-seqs", dest="max_batch", type=int, default=32,
+                   help="concurrent sequences (vLLM --max-num-seqs)")
+    p.add_argument("--uvicorn-log-level", dest="uvicorn_log_level", default="info",
+                   choices=["critical", "error", "warning", "info", "debug", "trace"])
+    p.add_argument("--chat-template", dest="chat_template", default=None, help="jinja chat template file")
+    p.add_argument("--kv-transfer-config", dest="kv_transfer_config", default=None,
+                   help="vLLM KV connector JSON; LMCache connectors map onto the prefix cache tiers")
+    p.add_argument("--prefix-block", dest="prefix_block", type=int, default=64, help="prefix-cache chunk tokens")
+    p.add_argument("--enforce-eager", dest="enforce_eager", action="store_true", help="no decode hipGraphs")
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--load-format", dest="load_format", default="auto", choices=["auto", "safetensors", "pt"],
+                   help="vLLM flag: checkpoint files are read by their extension (safetensors first)")
+    for flag in ("--trust-remote-code", "--disable-log-requests", "--disable-usage-stats"):
+        p.add_argument(flag, action="store_true", help="accepted for vLLM compatibility (no effect)")
     p.add_argument("--served-model-name", dest="served_model_name")
     p.add_argument("--api-key", dest="api_key")
     p.add_argument("--guard-url", dest="guard_url")
@@ -1020,6 +1134,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("demo", choices=["mlp", "optimizers", "rnn", "cnn", "seq2seq"])
     p.add_argument("--epochs", type=int, default=30)
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--load-format", dest="load_format", default="auto", choices=["auto", "safetensors", "pt"],
+                   help="vLLM flag: checkpoint files are read by their extension (safetensors first)")
     p.set_defaults(fn=cmd_dl_basics)
     p = sub.add_parser("env")
     p.set_defaults(fn=cmd_env)

@@ -327,13 +327,31 @@ def _unwrap_lm(model):
     raise TypeError("ServingEngine needs a causal LM with .model and .lm_head")
 
 
+def kv_slots_for_budget(total_bytes: int, used_bytes: int, fraction: float, slot_bytes: int,
+                        reserve_bytes: int = 0) -> int:
+    """vLLM ``--gpu-memory-utilization`` semantics: the engine may occupy ``fraction`` of the device's memory;
+    what the resident weights (``used_bytes``) and the prefill activation reserve leave of it holds the KV
+    cache — here whole sequence slots of ``max_model_len`` tokens (the contiguous cache below).  Raises, like
+    vLLM, when not even one slot fits."""
+    if not 0.0 < fraction <= 1.0:
+        raise ValueError(f"gpu_memory_utilization {fraction}: must be in (0, 1]")
+    budget = fraction * total_bytes - used_bytes - reserve_bytes
+    if budget < slot_bytes:
+        raise ValueError(f"no memory for the KV cache at gpu_memory_utilization={fraction}: "
+                         f"{budget / 2 ** 30:.2f} GiB left after weights and activations, one "
+                         f"{slot_bytes / 2 ** 30:.2f} GiB sequence slot needed (raise the fraction or lower "
+                         f"--max-model-len)")
+    return int(budget // slot_bytes)
+
+
 class ServingEngine:
     def __init__(self, model, tokenizer, model_name: str = "lipa-model", max_batch: int = 16,
                  system_prompt: str | None = None, chat_template: str = "auto", space_before_end: bool = False,
                  max_model_len: int | None = None, max_prefill_batch: int | None = None, prefill_token_budget: int = 16384,
                  use_graphs: bool | None = None, tp_group=None, prefix_cache_blocks: int = 0,
                  prefix_block: int = 64, chunked_prefill: int = 0, lora_modules: dict[str, str] | None = None,
-                 host_cache_blocks: int = 0, kv_remote_url: str | None = None):
+                 host_cache_blocks: int = 0, kv_remote_url: str | None = None,
+                 gpu_memory_utilization: float | None = None):
         """``tp_group``: the model was sharded by ``parallel.tensor_parallel`` over this group.
         The engine then runs SPMD — group rank 0 owns the request queue and broadcasts each
         iteration's admissions; the other ranks call :meth:`follower_loop` and replay exactly the
@@ -386,6 +404,16 @@ class ServingEngine:
         self.h_latency = _Histogram([0.05, 0.1, 0.25, 0.5, 1, 2, 5, 10, 30, 60])
         self.h_ttft = _Histogram([0.01, 0.025, 0.05, 0.1, 0.2, 0.5, 1, 2, 5])
         self.queue_time_ewma: float | None = None
+        if gpu_memory_utilization is not None and self.device.type == "cuda":
+            # the KV pool sized from the memory fraction (vLLM --gpu-memory-utilization), capped by max_batch
+            elt = torch.finfo(self.lm.lm_head.weight.dtype).bits // 8
+            slot = 2 * cfg.num_hidden_layers * self.max_len * cfg.num_key_value_heads * cfg.head_dim * elt
+            reserve = (2 << 30) + prefill_token_budget * (16 * cfg.hidden_size + 6 * getattr(cfg, "intermediate_size", 0))
+            fit = kv_slots_for_budget(torch.cuda.get_device_properties(self.device).total_memory,
+                                      torch.cuda.memory_allocated(self.device), gpu_memory_utilization, slot, reserve)
+            max_batch = max(1, min(max_batch, fit))
+            self.max_batch = max_batch
+            self.max_prefill_batch = min(self.max_prefill_batch, max_batch)
         self.cache = KVCache(cfg.num_hidden_layers, max_batch, self.max_len, cfg.num_key_value_heads, cfg.head_dim,
                              self.lm.lm_head.weight.dtype, self.device)
         self.cache.pos = torch.zeros(max_batch, dtype=torch.long, device=self.device)

@@ -260,6 +260,6 @@ hist.push({role:'assistant',content:text});}
 </script></body></html>"""
 
 
-def serve(engine: ServingEngine, host: str = "0.0.0.0", port: int = 8000, **kw):
+def serve(engine: ServingEngine, host: str = "0.0.0.0", port: int = 8000, log_level: str = "info", **kw):
     import uvicorn
-    uvicorn.run(create_app(engine, **kw), host=host, port=port, log_level="info")
+    uvicorn.run(create_app(engine, **kw), host=host, port=port, log_level=log_level)

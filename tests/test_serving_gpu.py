@@ -224,3 +224,24 @@ def test_multi_lora_decode_graphs_apply_per_row_adapters(tmp_path, lm):
         assert (replay - eager).abs().max().item() < 1e-3 * eager.abs().max().item() + 1e-3, ids
     # and the rows really carry different adapters
     assert (eager[0] - eager[1]).abs().max() > 0
+
+
+def test_gpu_memory_utilization_sizes_kv_pool(lm):
+    """vLLM --gpu-memory-utilization: the slot pool is what the fraction leaves after the weights; a fraction too
+    small for one slot raises"""
+    total = torch.cuda.get_device_properties(0).total_memory
+    cfg = lm.config
+    slot = 2 * cfg.num_hidden_layers * 2048 * cfg.num_key_value_heads * cfg.head_dim * 2
+    used = torch.cuda.memory_allocated(0)
+    want = 3
+    frac = (used + (2 << 30) + 16384 * (16 * cfg.hidden_size + 6 * cfg.intermediate_size) + (want + 0.5) * slot) / total
+    eng = ServingEngine(lm, _tok(), max_batch=64, max_model_len=2048, use_graphs=False, gpu_memory_utilization=frac)
+    try:
+        assert eng.max_batch == want and eng.cache.k[0].shape[0] == want
+        out = eng.complete("hello", SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True), timeout=120)
+        assert out["completion_tokens"] == 4
+    finally:
+        eng.shutdown()
+    with pytest.raises(ValueError):
+        ServingEngine(lm, _tok(), max_batch=4, max_model_len=2048, use_graphs=False,
+                      gpu_memory_utilization=used / total)
