@@ -121,17 +121,9 @@ __device__ __forceinline__ void dma_lds(const rsrc_t& rs, uint32_t dst, uint32_t
       : "memory");
 }
 
-// 16-B global load as an asm statement (hipcc does not count it: the explicit vmcnt waits that follow
-// cover it) and the empty asm that pins a register behind such a wait
-__device__ __forceinline__ u32x4 gload16_u(const void* p) {
-  u32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-__device__ __forceinline__ bf16x8 gload16(const void* p) { return __builtin_bit_cast(bf16x8, gload16_u(p)); }
-__device__ __forceinline__ void pin(bf16x8& v) { asm volatile("" : "+v"(v)); }
-__device__ __forceinline__ void pinf(f32x4& v) { asm volatile("" : "+v"(v)); }
-__device__ __forceinline__ void pinu(u32x4& v) { asm volatile("" : "+v"(v)); }
+// s_waitcnt immediate for vmcnt(0) alone (the full drain that register loads issued near LDS-DMAs need: a counted
+// vmcnt(N > 0) is never their guard — scripts/vmcnt_audit.py, tests/test_vmcnt_audit_cpu.py)
+constexpr int WAIT_VM0 = 0 | (7 << 4) | (15 << 8) | (0 << 14);
 
 // compile-time unrolled loop: f(std::integral_constant<int, k>) for k in [K, N)
 template <int K, int N>
@@ -629,22 +621,22 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   } else {
-    // ---- LoRA terms, computed in the prologue so that their operand loads overlap the first DMA wait (at
-    // the end of the tile they ran serialized — every tile of a round finishes at once: +10-13 µs per call)
+    // ---- LoRA terms, computed in the prologue (at the end of the tile they ran serialized — every tile of a
+    // round finishes at once: +10-13 µs per call)
     //  NT: K-step 0 of the adapters' extra K (xa·Bᵀ) initialises the accumulators;
     //  BT: the masked input-gradient term Σ_b D_b(ds_b·g_b·A_b) initialises them.
-    // Operands come by asm global loads issued before every DMA (so the tile-0 vmcnt wait covers them)
-    // and pinned behind that wait by an empty asm; hipcc does not track them.
+    // Operands come by compiler-visible global loads, drained by vmcnt(0) BEFORE the first LDS-DMA is issued:
+    // no counted wait ever guards a register load beside the DMAs (the round-5 dK/dV race:
+    // profiles/r5/zero3_dkv_race.txt; pinned by tests/test_vmcnt_audit_cpu.py).  The loads hit L2 (xa / g were
+    // written by the launch before), so the drain costs one L2 latency per workgroup.
     bf16x8 lxe[8], lbe[8], lbe2[8], lxe2[8];
-    // BT: raw asm-load destinations (g rows, keep bits) — written by the loads only and first read after the
-    // tile-0 wait: any copy made before it (a select, a vector rebuild) would copy registers still in flight
     u32x4 lkeep[2][8], lga[2][8], lgb[2][8];
     if constexpr (LORA && !BT) {
       const int q = lane >> 4;   // 8-deep k-block of K-step 0
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         const int m = min(m0 + wr * (BMT / 2) + i * 16 + (lane & 15), M - 1);
-        lxe[i] = gload16((const bf16*)lx.xa + (size_t)m * lx.ldxa + 8 * q);
+        lxe[i] = *reinterpret_cast<const bf16x8*>((const bf16*)lx.xa + (size_t)m * lx.ldxa + 8 * q);
       }
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
@@ -658,9 +650,10 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
             hit = b;
           }
         }
-        lbe[j] = gload16(src);
+        lbe[j] = *reinterpret_cast<const bf16x8*>(src);
         lkeep[0][j][0] = (uint32_t)hit;
       }
+      __builtin_amdgcn_s_waitcnt(WAIT_VM0);
     }
     if constexpr (LORA && BT) {
       constexpr int CPR = BN / 8;
@@ -702,20 +695,12 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
           const float* gp = ldx.g[b] + (size_t)m * ldx.ldg + (kq < ldx.r[b] ? kq : 0);
           // keep bits: 16 B = the lane's row over [n0 + wc·BN/2, + 128) (BN/2 ≤ 128 columns)
           const unsigned char* kp = ldx.keep[b] + (size_t)m * (N >> 3) + min(kb0, (N >> 3) - 16);
-          if constexpr (W4) {
-            // W4: the codes prologue below drains the vector-memory queue right away (nothing to overlap),
-            // and at the 256-row tile its register pressure made hipcc copy in-flight asm-load destinations
-            // (wrong dX at M = 2048): compiler-tracked loads here
-            lga[b][i] = *reinterpret_cast<const u32x4*>(gp);
-            lgb[b][i] = *reinterpret_cast<const u32x4*>(gp + 4);
-            lkeep[b][i] = *reinterpret_cast<const u32x4*>(kp);
-          } else {
-            lga[b][i] = gload16_u(gp);
-            lgb[b][i] = gload16_u(gp + 4);
-            lkeep[b][i] = gload16_u(kp);
-          }
+          lga[b][i] = *reinterpret_cast<const u32x4*>(gp);
+          lgb[b][i] = *reinterpret_cast<const u32x4*>(gp + 4);
+          lkeep[b][i] = *reinterpret_cast<const u32x4*>(kp);
         }
       }
+      __builtin_amdgcn_s_waitcnt(WAIT_VM0);
       __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
       __syncthreads();   // every wave has read the staged A images: the DMAs may overwrite them
     }
@@ -747,10 +732,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
     __builtin_amdgcn_s_barrier();
     if constexpr (LORA && !BT) {
 #pragma unroll
-      for (int i = 0; i < NA; ++i) pin(lxe[i]);
-#pragma unroll
       for (int j = 0; j < NB; ++j) {
-        pin(lbe[j]);
         const int hit = (int)lkeep[0][j][0];
         if (hit < 0) lbe[j] = bf16x8{};
         else if (tm == 0 && lx.bt[hit] != nullptr) {   // Bᵀ [r_b, n_b] for the backward, once per column
@@ -774,9 +756,6 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
           if (b >= ldx.nbr) break;
-          pinu(lga[b][i]);
-          pinu(lgb[b][i]);
-          pinu(lkeep[b][i]);
           bf16x8 a;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {

@@ -356,23 +356,18 @@ def test_flash_attention_padding(native_ext, S, d):
     assert dk.view(B, S, h, d)[~mask].abs().max() == 0
 
 
-def test_flash_attention_bwd_bit_stable_under_contention(native_ext):
-    """the backward kernels use no atomics: dQ / dK / dV are bit-identical call after call, also while a second
-    process keeps the GPU busy (a counted vmcnt wait in the dK/dV kernel once assumed in-order completion
-    beside its LDS-DMAs and raced under exactly this contention: profiles/r5/zero3_dkv_race.txt)"""
+def test_flash_attention_bwd_bit_stable(native_ext):
+    """the backward kernels use no atomics: dQ / dK / dV are bit-identical call after call.  (The round-5 race of a
+    counted vmcnt wait beside LDS-DMAs is pinned structurally on the CPU: tests/test_vmcnt_audit_cpu.py.)"""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, os.path.join(root, "scripts", "experiments", "attn_bwd_repeat.py"), "--fused",
-           "--iters", "300"]
-    env = dict(os.environ, PYTHONPATH=root)
-    procs = [subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
-             for _ in range(2)]
-    outs = [p.communicate(timeout=100)[0] for p in procs]
-    for p, out in zip(procs, outs):
-        assert p.returncode == 0, out[-2000:]
-        assert "differing calls dq 0 dk 0 dv 0" in out, out[-2000:]
+           "--iters", "50"]
+    r = subprocess.run(cmd, env=dict(os.environ, PYTHONPATH=root), capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-2000:]
+    assert "differing calls dq 0 dk 0 dv 0" in r.stdout, r.stdout[-2000:]
 
 
 @pytest.mark.parametrize("gain", [1.0, 6.0])
