@@ -197,7 +197,7 @@ def main():
                          "recomputed in backward (HF gradient_checkpointing, the reference); selective = GEMM outputs "
                          "recorded in the first forward, norms / RoPE / attention recomputed")
     ap.add_argument("--nf4-gemm", default=None, choices=["auto", "w4", "expand"],
-                    help="NF4 base GEMM form (ops/linear.py _nf4_w4): auto = one bf16 expansion per step where the copy "
+                    help="NF4 base GEMM form (ops/gemm.py _nf4_w4): auto = one bf16 expansion per step where the copy "
                          "is reused (forward + dX), the in-kernel NF4 dequant-GEMM elsewhere; w4 = the NF4 dequant-GEMM "
                          "everywhere (no bf16 copy of the base: the memory-lean QLoRA step); expand = always expand "
                          "(default: LIPA_NF4_GEMM, else auto)")
@@ -225,7 +225,7 @@ def main():
                          "line is printed with '<record>': {'error': ...} and the process exits 0 "
                          "(default: 240 s, 420 s for the zero3 sub-record, which builds its own model)")
     args = ap.parse_args()
-    from llm_in_practise_amd.ops import linear as _lin
+    from llm_in_practise_amd.ops import gemm as _lin
     if args.nf4_gemm is not None:        # else the LIPA_NF4_GEMM environment choice stands
         _lin._NF4_MODE = args.nf4_gemm
     args.nf4_gemm = _lin._NF4_MODE
@@ -385,7 +385,7 @@ def main():
             "grad_accum": args.grad_accum,
             "quant": "nf4+double_quant" if args.mode == "qlora" else "none",
             "nf4_gemm": args.nf4_gemm,
-            # kernel provenance of the timed steps (ops/linear.py GEMM_STATS): GEMM launches per step by form —
+            # kernel provenance of the timed steps (ops/gemm.py GEMM_STATS): GEMM launches per step by form —
             # gemm4w = the hand-written HIP GEMM on a bf16 operand, gemm4w-nf4 = the same kernel reading NF4 codes,
             # library = torch.matmul (shapes gemm4w does not take); nf4-expansion = bf16 copies of NF4 bases
             "gemm_backend": "gemm4w" if device.type == "cuda" else "torch-cpu",

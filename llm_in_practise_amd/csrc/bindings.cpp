@@ -921,6 +921,8 @@ static void attn_check(const Tensor& t, int64_t rows, int64_t heads, int64_t d, 
   TORCH_CHECK(t.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "attn: ", name,
               " rows must be 16-byte aligned");
   TORCH_CHECK(t.size(0) >= rows && t.size(1) >= heads * d, "attn: ", name, " too small for the launch shape");
+  TORCH_CHECK(d != 128 || t.stride(0) % 128 == 0, "attn: ", name,
+              " row stride must be a multiple of 128 elements at head_dim 128 (LDS-DMA rows)");
 }
 
 // General forward: Sq queries per batch row (absolute positions q_offs[b] + i) over Skv keys stored

@@ -1,25 +1,22 @@
 // Flash attention forward / backward for gfx950: causal, GQA by head
-// broadcast (K/V never repeated), right-padding via per-batch kv length, bf16 I/O, fp32
-// online softmax.  Token-major layout: q [T, Hq*D], k/v [T, Hkv*D] with arbitrary row
-// stride (k/v may be strided views into the fused qkv projection).
+// broadcast (K/V never repeated), right-padding via per-batch kv length, query offsets (chunked /
+// prefix-cache prefill), attention dropout, bf16 I/O, fp32 online softmax.  Token-major layout:
+// q [T, Hq*D], k/v [T, Hkv*D] with arbitrary row stride (k/v may be strided views into the fused
+// qkv projection output).  One kernel per (head dim class, pass):
 //
-// Forward: 256-thread workgroup = 4 waves × 32 queries of one (batch, head).  Scores are
-// computed SWAPPED, Sᵀ = K·Qᵀ with v_mfma_f32_16x16x32_bf16 (K tile from LDS, Q fragments
-// held in registers), so each lane owns ONE query: the row max / row sum are lane-local
-// plus two shuffles, and the probabilities are already the B operand of Oᵀ = Vᵀ·Pᵀ in a
-// permuted key order (no LDS round trip for P).  V's matching operand comes from the
-// gfx950 transposed LDS read ds_read_b64_tr_b16.  K/V tiles (64 keys) are register-staged
-// one tile ahead into double-buffered LDS (one barrier per tile).
-//
-// Backward: workgroup = 4 waves × 16 keys (a 64-key block) of one (batch, q-head); K and V
-// fragments stay in registers for the whole sweep, dKᵀ/dVᵀ accumulate in registers over all
-// query tiles (no atomics), P is recomputed from the saved log-sum-exp, dQ is accumulated
-// with fp32 atomics (the dQ sum spans key blocks).  GQA partial dK/dV per q-head are summed
-// in a finalize pass (deterministic).
+//  * D = 128 (every Qwen / Llama shape): v_mfma_f32_32x32x16_bf16 kernels whose K / V (forward, dQ)
+//    and Q / dO (dK/dV) tiles arrive by LDS-DMA (buffer_load … lds, the swizzle applied on the global
+//    side) into double-buffered XOR-addressed LDS images, one barrier per tile:
+//      attn_fwd128_k     Sᵀ = K·Qᵀ (each lane owns one query: lane-local softmax), Oᵀ += Vᵀ·Pᵀ;
+//      attn_bwd_dq128_k  dQ, and delta = rowsum(dO∘O) for the dK/dV kernel;
+//      attn_bwd_dkv128_k 8 waves, K / V images resident, dKᵀ / dVᵀ accumulated in registers over
+//                        the query sweep (no atomics); key blocks split over two workgroups when the
+//                        causal grid is too small for the chip (attn_dkv_nsplit + attn_dkv_fin_k).
+//    Row strides must be multiples of 128 elements (256-B DMA rows; the binding checks).
+//  * D = 32 / 64 / 96: the 16x16x32 kernels attn_fwd_k / attn_bwd_dq_k / attn_bwd_dkv_k (register-staged
+//    tiles; GQA partial dK/dV per q-head summed in a deterministic finalize pass).
 
 #include "common.h"
-
-#include <cstdlib>
 
 using namespace lipa;
 
@@ -114,24 +111,6 @@ __device__ __forceinline__ void xcd_grid3_lpt(int& i0, int& i1, int& i2, int lpt
 // order (0) and longest-first only (2), profiles/r4/attention_knobs_ab.txt
 static int attn_lpt() { return 1; }
 
-// D = 128 forward / dQ: K / V tiles by LDS-DMA (1, default) or register-staged (LIPA_ATTN_FWD_DMA=0, A/B runs)
-static int attn_fwd_dma() {
-  static const int v = [] {
-    const char* e = std::getenv("LIPA_ATTN_FWD_DMA");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v;
-}
-
-// D = 128 dK/dV kernel: 1 = the 32x32x16 form (attn_bwd_dkv128_k), 0 = the 16x16x32 8-wave form
-// (LIPA_ATTN_DKV128=0, for A/B runs)
-static int attn_dkv128() {
-  static const int v = [] {
-    const char* e = std::getenv("LIPA_ATTN_DKV128");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v;
-}
 
 // ============================================================================ forward
 // Sq queries per batch row attend to Skv keys (K/V rows of batch b start at b·kv_rows: a KV cache
@@ -390,7 +369,7 @@ __device__ __forceinline__ void attn_dma16(const rsrc_t& rs, uint32_t m0v, uint3
       : "memory");
 }
 
-template <int PF, bool DROP>
+template <bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_fwd128_k(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                      const bf16* __restrict__ V, int ldq, int ldk, int ldv,
                                                      const int* __restrict__ kv_lens, const int* __restrict__ q_offs,
@@ -433,35 +412,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd128_k(const bf16* __restrict__
     for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
 
-  bf16x8 kr[PF > 0 ? PF : 1][4], vr[PF > 0 ? PF : 1][4];   // (PF = 0: LDS-DMA, no staging)
-  const int row0 = tid >> 4, ch0 = tid & 15;   // this thread's tile rows row0 + 16p, chunk ch0
-  auto load_tile = [&](int set, int t) {
-    if (t * 64 + 64 <= Skv) {   // whole tile in range: one base address, row steps as offsets
-      const bf16* kp = K + (ktok0 + t * 64 + row0) * ldk + hk * D + ch0 * 8;
-      const bf16* vp = V + (ktok0 + t * 64 + row0) * ldv + hk * D + ch0 * 8;
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        kr[set][p] = *reinterpret_cast<const bf16x8*>(kp + (size_t)(16 * p) * ldk);
-        vr[set][p] = *reinterpret_cast<const bf16x8*>(vp + (size_t)(16 * p) * ldv);
-      }
-      return;
-    }
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const size_t key = ktok0 + min(t * 64 + row0 + 16 * p, Skv - 1);
-      kr[set][p] = *reinterpret_cast<const bf16x8*>(K + key * ldk + hk * D + ch0 * 8);
-      vr[set][p] = *reinterpret_cast<const bf16x8*>(V + key * ldv + hk * D + ch0 * 8);
-    }
-  };
-  auto store_tile = [&](int set, int buf) {
-    char* Kl = smem + buf * 2 * TB;
-    char* Vl = Kl + TB;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      *reinterpret_cast<bf16x8*>(Kl + toff(row0 + 16 * p, ch0)) = kr[set][p];
-      *reinterpret_cast<bf16x8*>(Vl + toff(row0 + 16 * p, ch0)) = vr[set][p];
-    }
-  };
   // transposed-read geometry (T10): lane 4q'+p' of 16-lane group g addresses row q' of a 4-row block,
   // chunk 2(g&1) + (p'>>1) of the 32-column d block, half p'&1 of it
   const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
@@ -471,8 +421,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd128_k(const bf16* __restrict__
   const int ra0 = 4 * (g >> 1) + qq, c0 = 2 * (g & 1) + (pp >> 1);
   int at0 = toff(ra0, c0) + 8 * (pp & 1), at1 = toff(ra0 + 8, c0) + 8 * (pp & 1);
 
-  // PF = 0: K / V tiles by LDS-DMA (as attn_bwd_dkv128_k: wave w moves image rows 16w .. 16w + 15, the swizzle
-  // applied on the global side, zero past Skv), one barrier per tile, no staging VGPRs or LDS stores
+  // K / V tiles by LDS-DMA (as attn_bwd_dkv128_k: wave w moves image rows 16w .. 16w + 15, the swizzle applied on
+  // the global side, zero past Skv), one barrier per tile, no staging VGPRs or LDS stores (row strides ldk / ldv
+  // multiples of 128 elements: the binding checks)
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)smem);
   const int wu = __builtin_amdgcn_readfirstlane(w);
   const uint32_t ldk2 = (uint32_t)ldk * 2, ldv2 = (uint32_t)ldv * 2;
@@ -488,27 +439,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd128_k(const bf16* __restrict__
       attn_dma16(rv, dst + TB + 1024 * p, (vv + 4u * p * ldv2) ^ (16u * p));
     }
   };
-  if constexpr (PF == 0) {
-    if (nt > 0) dma_tile(0);
-  } else {
-    if (nt > 0) load_tile(0, 0);
-    if (PF == 2 && nt > 1) load_tile(PF - 1, 1);
-  }
+  if (nt > 0) dma_tile(0);
   for (int t2 = 0; t2 < nt; t2 += 2) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int t = t2 + u;
       if (t >= nt) break;
-      if constexpr (PF == 0) {
-        __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0): this wave's DMAs of tile t have landed
-        __syncthreads();                     // ... everyone's; every read of the other buffer is done
-        if (t + 1 < nt) dma_tile(t + 1);
-      } else {
-        const int set = PF == 2 ? u : 0;
-        store_tile(set, u);
-        __syncthreads();
-        if (t + PF < nt) load_tile(set, t + PF);
-      }
+      __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0): this wave's DMAs of tile t have landed
+      __syncthreads();                     // ... everyone's; every read of the other buffer is done
+      if (t + 1 < nt) dma_tile(t + 1);
       if (t >= ntw) continue;   // wave-uniform: every key of the tile is above this wave's diagonal
       const char* Kl = smem + u * 2 * TB;
       const char* Vl = Kl + TB;
@@ -786,7 +725,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(const bf16* __restrict__
 // (row reads of the swizzled K / V images), dS = P∘(dP − delta) in registers, dQᵀ += Kᵀ·dSᵀ with Kᵀ from the
 // transposed reads of the same K image and dS as the B operand in accumulator-row slot order (no lane
 // movement).  Writes delta for the dK/dV kernel, as attn_bwd_dq_k.
-template <bool DROP, bool DMA = false>
+template <bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq128_k(const bf16* __restrict__ dO, const bf16* __restrict__ O,
                                                         const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                         const bf16* __restrict__ V, const float* __restrict__ lse,
@@ -841,25 +780,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq128_k(const bf16* __restric
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
 
-  bf16x8 kr[4], vr[4];
-  const int row0 = tid >> 4, ch0 = tid & 15;   // this thread's tile rows row0 + 16p, chunk ch0
-  auto load_tile = [&](int t) {   // (a separate whole-tile fast path spills here: 256 VGPRs)
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const size_t key = tok0 + min(t * 64 + row0 + 16 * p, S - 1);
-      kr[p] = *reinterpret_cast<const bf16x8*>(K + key * ldk + hk * D + ch0 * 8);
-      vr[p] = *reinterpret_cast<const bf16x8*>(V + key * ldv + hk * D + ch0 * 8);
-    }
-  };
-  auto store_tile = [&](int buf) {
-    char* Kl = smem + buf * 2 * TB;
-    char* Vl = Kl + TB;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      *reinterpret_cast<bf16x8*>(Kl + toff(row0 + 16 * p, ch0)) = kr[p];
-      *reinterpret_cast<bf16x8*>(Vl + toff(row0 + 16 * p, ch0)) = vr[p];
-    }
-  };
   const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
   // operand rows as XOR-addressed bases (see attn_bwd_dkv128_k): K row r32 (+32 kh rows = 8 KB), Kᵀ rows
   // ra0 / ra0 + 8 (+16 u2 rows = 4 KB, transposed chunk 4dt + c0 = base ^ 64dt)
@@ -867,7 +787,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq128_k(const bf16* __restric
   const int ra0 = 4 * (g >> 1) + qq, c0 = 2 * (g & 1) + (pp >> 1);
   int at0 = toff(ra0, c0) + 8 * (pp & 1), at1 = toff(ra0 + 8, c0) + 8 * (pp & 1);
 
-  // DMA: K / V tiles by LDS-DMA as attn_fwd128_k<0> (no staging VGPRs / LDS stores, one barrier per tile)
+  // K / V tiles by LDS-DMA as attn_fwd128_k (no staging VGPRs / LDS stores, one barrier per tile)
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_ptr_t)smem);
   const int wu = __builtin_amdgcn_readfirstlane(w);
   const uint32_t ldk2 = (uint32_t)ldk * 2, ldv2 = (uint32_t)ldv * 2;
@@ -883,24 +803,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq128_k(const bf16* __restric
       attn_dma16(rv, dst + TB + 1024 * p, (vv + 4u * p * ldv2) ^ (16u * p));
     }
   };
-  if (nt > 0) {
-    if constexpr (DMA) dma_tile(0);
-    else load_tile(0);
-  }
+  if (nt > 0) dma_tile(0);
   for (int t2 = 0; t2 < nt; t2 += 2) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int t = t2 + u;
       if (t >= nt) break;
-      if constexpr (DMA) {
-        __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0): this wave's DMAs of tile t have landed
-        __syncthreads();
-        if (t + 1 < nt) dma_tile(t + 1);
-      } else {
-        store_tile(u);
-        __syncthreads();
-        if (t + 1 < nt) load_tile(t + 1);
-      }
+      __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0): this wave's DMAs of tile t have landed
+      __syncthreads();
+      if (t + 1 < nt) dma_tile(t + 1);
       if (t >= ntw) continue;
       const char* Kl = smem + u * 2 * TB;
       const int k0 = t * 64;
@@ -1511,14 +1422,9 @@ static float* g_attn_trace = nullptr;
 void attn_set_trace(void* p) { g_attn_trace = (float*)p; }
 
 int attn_dkv_nsplit(int B, int S, int hkv, int causal) {
-  static const int force = [] {   // LIPA_ATTN_DKV_SPLIT=0 / 1: never / always split (A/B runs)
-    const char* e = std::getenv("LIPA_ATTN_DKV_SPLIT");
-    return e ? std::atoi(e) : -1;
-  }();
   const int nb = (S + 63) / 64;
   const long grid = (long)B * hkv * nb;
-  if (!causal || nb < 2 || force == 0) return 0;
-  if (force == 1) return nb - (nb + 1) / 2;
+  if (!causal || nb < 2) return 0;
   if (grid > 512 || (nb < 16 && grid > 128)) return 0;
   return nb - (nb + 1) / 2;   // kb with nb - kb > ceil(nb / 2)
 }
@@ -1553,19 +1459,12 @@ void launch_attn_fwd(const void* q, const void* k, const void* v, int ldq, int l
   const int qt = 2;
   dim3 grid((Sq + 64 * qt - 1) / (64 * qt), hq, B), blk(256);
   const float sl2 = scale * LOG2E;
-  if (D == 128) {   // the 32x32x16 form (attn_fwd128_k); other head dims: attn_fwd_k
+  if (D == 128) {   // the 32x32x16 form with LDS-DMA K / V tiles (attn_fwd128_k); other head dims: attn_fwd_k
 #define F128(DR)                                                                                              \
-  attn_fwd128_k<1, DR><<<grid, blk, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, ldq, ldk, ldv, kv_lens, \
-                                             q_offs, (bf16*)o, lse, Sq, Skv, kv_rows, hq, hkv,                    \
-                                             causal ? 1 | (attn_lpt() << 1) : 0, sl2, dp)
-    if (attn_fwd_dma() && ldk % 128 == 0 && ldv % 128 == 0) {   // K / V by LDS-DMA (row strides in 256-B units)
-#define F128D(DR)                                                                                              \
-  attn_fwd128_k<0, DR><<<grid, blk, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, ldq, ldk, ldv, kv_lens, \
-                                             q_offs, (bf16*)o, lse, Sq, Skv, kv_rows, hq, hkv,                    \
-                                             causal ? 1 | (attn_lpt() << 1) : 0, sl2, dp)
-      if (dp.thresh) F128D(true); else F128D(false);
-#undef F128D
-    } else if (dp.thresh) F128(true); else F128(false);
+  attn_fwd128_k<DR><<<grid, blk, 0, st>>>((const bf16*)q, (const bf16*)k, (const bf16*)v, ldq, ldk, ldv, kv_lens, \
+                                          q_offs, (bf16*)o, lse, Sq, Skv, kv_rows, hq, hkv,                    \
+                                          causal ? 1 | (attn_lpt() << 1) : 0, sl2, dp)
+    if (dp.thresh) F128(true); else F128(false);
 #undef F128
     LIPA_CHECK_LAUNCH();
     return;
@@ -1586,7 +1485,7 @@ void launch_attn_bwd(const void* dout, const void* q, const void* k, const void*
   const float sl2 = scale * LOG2E;
   const DropParams dp = make_drop(p_drop, seed);
   const int nb = (S + 63) / 64;
-  const bool trace = g_attn_trace && D == 128 && attn_dkv128() && ldq % 128 == 0;
+  const bool trace = g_attn_trace && D == 128;
   const int nsplit = ws && !trace ? attn_dkv_nsplit(B, S, hkv, causal) : 0;
   dim3 gq(nb, hq, B), gkv(nb + nsplit, hkv, B), blk(256);
 #define DKV(DD, PFKV)                                                                                             \
@@ -1604,37 +1503,25 @@ void launch_attn_bwd(const void* dout, const void* q, const void* k, const void*
                                              (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dq, S, hq, \
                                              hkv, causal ? 1 | (attn_lpt() << 1) : 0, scale, sl2, dp);            \
   DKV(DD, PFKV);
-  if (D == 128) {   // dQ in the 32x32x16 form (attn_bwd_dq128_k), dK/dV in the 8-wave 16x16x32 form
+  if (D == 128) {   // the 32x32x16 forms: dQ (attn_bwd_dq128_k) and dK/dV (attn_bwd_dkv128_k), LDS-DMA operand tiles
     dim3 gq2((S + 127) / 128, hq, B);
 #define DQ2(DR)                                                                                                  \
   attn_bwd_dq128_k<DR><<<gq2, blk, 0, st>>>((const bf16*)dout, (const bf16*)o, (const bf16*)q, (const bf16*)k,   \
                                             (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dq, S, hq, \
                                             hkv, causal ? 1 | (attn_lpt() << 1) : 0, scale, sl2, dp)
-    if (attn_fwd_dma() && ldk % 128 == 0 && ldv % 128 == 0) {
-#define DQ2D(DR)                                                                                                 \
-  attn_bwd_dq128_k<DR, true><<<gq2, blk, 0, st>>>((const bf16*)dout, (const bf16*)o, (const bf16*)q,              \
-                                                  (const bf16*)k, (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv, \
-                                                  (bf16*)dq, S, hq, hkv, causal ? 1 | (attn_lpt() << 1) : 0, scale,   \
-                                                  sl2, dp)
-      if (dp.thresh) DQ2D(true); else DQ2D(false);
-#undef DQ2D
-    } else if (dp.thresh) DQ2(true); else DQ2(false);
+    if (dp.thresh) DQ2(true); else DQ2(false);
 #undef DQ2
-    if (attn_dkv128() && ldq % 128 == 0) {   // the DMA row geometry needs 256-B-multiple Q row strides
 #define DKV3(DR)                                                                                                 \
   attn_bwd_dkv128_k<DR><<<gkv, 512, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k, (const bf16*)v,   \
                                              lse, delta, kv_lens, ldq, ldk, ldv, (bf16*)dk, (bf16*)dv, S, hq, hkv, \
                                              causal, scale, sl2, dp, ws, nsplit)
-      if (trace)
-        attn_bwd_dkv128_k<false, true><<<gkv, 512, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k,
-                                                            (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv,
-                                                            (bf16*)dk, (bf16*)dv, S, hq, hkv, causal, scale, sl2, dp,
-                                                            g_attn_trace, 0);
-      else if (dp.thresh) DKV3(true); else DKV3(false);
+    if (trace)
+      attn_bwd_dkv128_k<false, true><<<gkv, 512, 0, st>>>((const bf16*)dout, (const bf16*)q, (const bf16*)k,
+                                                          (const bf16*)v, lse, delta, kv_lens, ldq, ldk, ldv,
+                                                          (bf16*)dk, (bf16*)dv, S, hq, hkv, causal, scale, sl2, dp,
+                                                          g_attn_trace, 0);
+    else if (dp.thresh) DKV3(true); else DKV3(false);
 #undef DKV3
-    } else {
-      DKV(128, 1);
-    }
   } else {
     LIPA_ATTN_D3(D, RUN(DD, 2, 1));   // prefetch depth dQ 2, dK/dV 1
   }

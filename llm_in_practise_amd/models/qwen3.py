@@ -289,7 +289,9 @@ class Qwen3Model(nn.Module):
         if position_ids is None and not decoding and start == 0:
             # positions 0 .. S-1 (every training step, every fresh prefill): the cos / sin tables depend only on
             # (B, S) — computed once instead of ~7 small launches + their host time at the head of every step
-            key = (B, S, self.inv_freq.data_ptr(), self.attn_factor)
+            # (inv_freq's version: an in-place rescale re-keys; inference-mode tables never serve autograd)
+            key = (B, S, self.inv_freq.data_ptr(), self.inv_freq._version, str(input_ids.device), self.attn_factor,
+                   torch.is_inference_mode_enabled())
             cs = self._rope_cache.get(key)
             if cs is None:
                 if len(self._rope_cache) >= 8:

@@ -55,8 +55,10 @@ class _FlashAttnFn(torch.autograd.Function):
         return dq, dk, dv, None, None, None, None, None, None, None, None, None, None
 
 
-def _aligned(t: torch.Tensor) -> bool:
-    return t.stride(-1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0
+def _aligned(t: torch.Tensor, d: int = 0) -> bool:
+    """Operand layout the kernels take: unit inner stride, 16-B aligned rows; at head_dim 128 (the LDS-DMA
+    kernels) row strides in whole 256-B units."""
+    return (t.stride(-1) == 1 and t.stride(0) % (128 if d == 128 else 8) == 0 and t.data_ptr() % 16 == 0)
 
 
 def native_ok(q, d: int) -> bool:
@@ -69,7 +71,7 @@ def flash_attention(q, k, v, batch: int, seqlen: int, hq: int, hkv: int, d: int,
                     seed: int | None = None) -> torch.Tensor:
     scale = scale if scale is not None else 1.0 / math.sqrt(d)
     if native_ok(q, d):
-        if not (_aligned(q) and _aligned(k) and _aligned(v)):
+        if not (_aligned(q, d) and _aligned(k, d) and _aligned(v, d)):
             q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
         seed = _next_seed() if (dropout_p > 0 and seed is None) else (seed or 0)
         return _FlashAttnFn.apply(q, k, v, batch, seqlen, hq, hkv, d, causal, scale, kv_lens, float(dropout_p), seed)
@@ -97,8 +99,10 @@ def flash_attention_prefix(q, k_cache, v_cache, batch: int, sq: int, skv: int, h
     if native_ok(q, d):
         kc = k_cache.reshape(batch * kv_rows, -1)
         vc = v_cache.reshape(batch * kv_rows, -1)
-        if not _aligned(q):
+        if not _aligned(q, d):
             q = q.contiguous()
+        if not (_aligned(kc, d) and _aligned(vc, d)):
+            kc, vc = kc.contiguous(), vc.contiguous()
         o, _ = native().attn_fwd_ext(q, kc, vc, kv_lens, q_offs, batch, sq, skv, kv_rows, hq, hkv, d, True, scale,
                                      0.0, 0)
         return o

@@ -1,0 +1,123 @@
+"""Activation checkpointing that replays the same LoRA dropout masks, NF4-aware, with a selective policy
+(the reference's ``gradient_checkpointing_enable(gradient_checkpointing_kwargs=...)``,
+``Fine-Tuning/qwen3-8b-qlora-dist.py:162-163``), and the host-side dropout key stream the fused LoRA kernels
+draw their masks from (``next_dropout_key`` / ``seed_dropout``).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from .gemm import _IN_CKPT
+
+_KEY = [0x5DEECE66D << 20]
+
+def next_dropout_key() -> int:
+    """Counter-based dropout stream: every call gets a fresh 63-bit key (deterministic given
+    the seed set by :func:`seed_dropout`)."""
+    _KEY[0] = (_KEY[0] + 0x9E3779B97F4A7C15) & 0x7FFFFFFFFFFFFFFF
+    return _KEY[0]
+
+
+def seed_dropout(seed: int):
+    _KEY[0] = (int(seed) * 0x2545F4914F6CDD1D) & 0x7FFFFFFFFFFFFFFF
+
+
+_CKPT_REENTRANT = os.environ.get("LIPA_CKPT_REENTRANT", "1") == "1"
+# HF semantics by default (the whole layer recomputed); "selective" keeps every GEMM output of the
+# first forward (~78 MB per Qwen3-8B layer per 1024 tokens) and is opt-in
+_CKPT_POLICY = os.environ.get("LIPA_CKPT_POLICY", "full")
+
+
+def checkpoint(fn, *args, use_reentrant: bool | None = None, policy: str | None = None):
+    """Activation checkpointing of one layer that replays the SAME LoRA dropout masks.
+
+    ``use_reentrant`` selects torch's form (HF's ``gradient_checkpointing_kwargs={"use_reentrant": …}``,
+    ``Fine-Tuning/qwen3-8b-qlora-dist.py:162-163``; default: LIPA_CKPT_REENTRANT, on).  ``policy``:
+    ``"full"`` (default, LIPA_CKPT_POLICY) recomputes the whole layer in backward (HF's behaviour);
+    ``"selective"`` records the GEMM outputs in the first forward and replays them in the recompute —
+    only RMSNorm, q/k-norm + RoPE and attention run again (the stash below): faster, but it holds
+    ≈ 78 MB per Qwen3-8B layer per 1024 tokens from the forward until the backward.
+
+    The fused LoRA kernels draw their dropout mask from the host key stream above, not from
+    torch's RNG, so torch's ``preserve_rng_state`` does not cover them: a plain
+    ``torch.utils.checkpoint`` recompute would draw fresh keys and the backward would differentiate
+    a different mask than the forward applied.  Here the key-stream position at the first (forward)
+    call is remembered and restored for the recompute, then the live stream is put back — the
+    masks match exactly and the stream advances once per real forward.  Reference:
+    ``Fine-Tuning/qwen3-8b-lora.py:123`` (gradient checkpointing + ``lora_dropout``).  The reentrant
+    form's first forward builds no graph (no saved-tensor pack hooks: ~2k per step at Qwen3-8B, the
+    host-side cost of the checkpointed step, profiles/baseline_configs_r2_end.txt)."""
+    import torch.utils.checkpoint as ckpt
+    reentrant = _CKPT_REENTRANT if use_reentrant is None else bool(use_reentrant)
+    policy = policy or _CKPT_POLICY
+    if policy not in ("full", "selective"):
+        raise ValueError(f"checkpoint policy {policy!r}: 'full' or 'selective'")
+    stash = _Stash() if policy == "selective" else None
+    state: list = []
+
+    def run(*a):
+        _IN_CKPT[0] += 1
+        prev = list(_SAC)
+        try:
+            if not state:                      # the forward pass
+                state.append(_KEY[0])
+                if stash is not None:
+                    _SAC[:] = ["record", stash]
+                return fn(*a)
+            live = _KEY[0]                     # the recompute inside backward
+            _KEY[0] = state[0]
+            if stash is not None:
+                stash.pos = 0
+                _SAC[:] = ["replay", stash]
+            try:
+                return fn(*a)
+            finally:
+                _KEY[0] = live
+        finally:
+            _SAC[:] = prev
+            _IN_CKPT[0] -= 1
+
+    if reentrant:
+        # the first forward runs without building a graph; it needs an input that requires grad for the
+        # recompute to reach the LoRA parameters (layer 0's input is the frozen embedding) — the role of
+        # HF's enable_input_require_grads()
+        args = tuple(a.detach().requires_grad_() if isinstance(a, torch.Tensor) and i == 0 and
+                     a.is_floating_point() and not a.requires_grad else a for i, a in enumerate(args))
+        return ckpt.checkpoint(run, *args, use_reentrant=True)
+    return ckpt.checkpoint(run, *args, use_reentrant=False)
+
+
+
+# Selective activation checkpointing (``checkpoint(..., policy="selective")``): the checkpointed
+# layer's first forward RECORDS the outputs of its GEMM ops (the frozen-base projections with their LoRA
+# side products, the fused SwiGLU MLP) in a per-call stash; the recompute inside backward REPLAYS them
+# instead of launching the GEMMs again, and recomputes only the cheap ops between them (RMSNorm, q/k-norm
+# + RoPE, attention).  The stash holds ≈ 78 MB per Qwen3-8B layer at 1024 tokens (y_qkv, y_o, gu, y_down
+# + the rank-r LoRA projections) until the backward consumes it.
+_SAC: list = [None, None]      # (mode "record" | "replay", stash list)
+
+
+def _sac_recording() -> bool:
+    return _SAC[0] == "record"
+
+
+def sac_put(item):
+    if _SAC[0] == "record":
+        _SAC[1].append(item)
+
+
+def sac_take():
+    """The next recorded op output when replaying, else None."""
+    if _SAC[0] != "replay":
+        return None
+    st = _SAC[1]
+    i = st.pos
+    st.pos += 1
+    item, st[i] = st[i], None
+    return item
+
+
+class _Stash(list):
+    pos = 0

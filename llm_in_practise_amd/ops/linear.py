@@ -1,36 +1,29 @@
-"""Frozen-base linear with LoRA branches (K8) over NF4 or bf16 bases (K9).
-
-One op covers every projection of the stack:
+"""Frozen-base linear with LoRA branches over NF4 or bf16 bases (K9): the op every
+projection of the stack runs through.
 
     y[:, c0:c1] (+)= x · deq(W)ᵀ  +  Σ_i s_i · (drop_i(x) · A_iᵀ) · B_iᵀ   (+ residual)
 
-* ``base`` is a bf16 ``[N, K]`` tensor (LoRA / full fine-tune) or an :class:`NF4Weight`
-  (QLoRA).  Several projections that share an input (q|k|v, gate|up) are row-concatenated
-  into one base and one GEMM; each LoRA branch owns a column range ``[c0, c1)``.
-* Every frozen-base GEMM at training / prefill sizes is the hand-written MFMA kernel ``gemm4w``
-  (csrc/kernels/gemm4w.hip) — there is no library GEMM on the path: forward x·Wᵀ with the residual in
-  its epilogue, backward dY·W reading W as stored (the transposed-B form), split-K by its own cost model.
-  - An NF4 base (K9) takes one of two forms, chosen per call (``_nf4_w4``): the NF4 dequant-GEMM —
-    gemm4w reads the 4-bit codes (``NF4Weight.g4w_pack``) and expands each quant block to bf16 between
-    the load and its LDS B image, no bf16 copy of the base anywhere — or one HBM-speed expansion
-    (``nf4_dequant3_k``) whose bf16 copy serves the forward AND the dX GEMM.
-  - The LoRA branches ride inside gemm4w where their shapes allow: the adapters' B term as extra MFMA
-    K-steps of the forward (``gemm4w_lora``), the dropout-masked input-gradient term in the dX GEMM's
-    prologue (``gemm4w_loradx``); the rank-r projections, dB and dA run in ``lora.hip`` (``lora_proj2`` /
-    ``lora_proj_m`` forward, ``lora_proj_pair`` / ``lora_acc_quad`` / ``lora_acc_jobs`` backward).
-    Other shapes fall back to ``lora_apply`` (B term added into the adapters' column blocks) and
-    ``lora_acc`` / ``lora_dx2``.
-  - Decode sizes (M ≤ 16) use the split-K weight-streaming kernels (``skinny.hip``, ``gemv_w4``).
-  - Shapes gemm4w does not take (K % 64 ≠ 0, tiny M, CPU tensors) run ``torch.matmul``.
-* The SwiGLU MLP block bypasses this op when it carries no adapters (``ops/mlp.py``).
-* ``GEMM_STATS`` counts every GEMM launch by form (the bench record's provenance).
+* ``base`` is a bf16 ``[N, K]`` tensor (LoRA / full fine-tune) or an :class:`NF4Weight` (QLoRA).  Projections
+  that share an input (q|k|v, gate|up) are row-concatenated into one base and one GEMM; each LoRA branch owns a
+  column range ``[c0, c1)``.  The base GEMMs themselves are dispatched by ``ops/gemm.py`` (gemm4w, the NF4
+  dequant-GEMM or one expansion per step, decode kernels).
+* LoRA kernel forms (csrc/kernels/lora.hip, gemm4w_lora.hip), one per adapter layout:
+  - pair — q_proj + v_proj of rank <= 8 (the QLoRA configs): ``lora_proj2`` (both s·D(x)·Aᵀ in one pass over x,
+    keep bits stored), backward ``lora_proj_pair`` + ``lora_acc_quad`` (both dB and dA in one launch);
+  - multi — 1-4 adapters of rank 8 / 16 (BASELINE #2: q, k, v, o): ``lora_proj_m``, ``lora_proj_cols``,
+    ``lora_acc_jobs``;
+  - per-branch — any other rank <= 16 / 128-aligned shape: ``lora_proj`` / ``lora_acc`` per adapter;
+  - general — anything else (rank > 16, odd widths, > 4 adapters): torch matmuls as an extra K-slice of the base
+    GEMM.
+  At training sizes the adapters' B term rides inside the forward GEMM as extra MFMA K-steps (``gemm4w_lora``)
+  and the masked input-gradient term inside the dX GEMM's prologue (``gemm4w_loradx``); at decode / small M the
+  B term is added into the adapters' column blocks (``lora_apply``).
 
 Reference parity: PEFT ``LoraConfig(r, lora_alpha, lora_dropout, target_modules)``
 (``Fine-Tuning/qwen3-8b-qlora.py:107-114``), scaling = alpha / r.
 """
 from __future__ import annotations
 
-import collections
 import dataclasses
 import os
 
@@ -39,122 +32,11 @@ import torch.nn.functional as F
 
 from ..quant.nf4 import NF4Weight, dequantize_nf4
 from ._native import native, use_native
+from .checkpoint import _KEY, _sac_recording, checkpoint, next_dropout_key, sac_put, sac_take, seed_dropout  # noqa: F401
+from .gemm import (GEMM_STATS, _MIN_M, _base_gemm, _base_gemm_t, _count, _g4w_ok, _nf4_expand,  # noqa: F401
+                   _nf4_w4, _w4_ok, head_logits, nf4_cache_advance)
 
-EXT_ALIGN = 32   # the kernels consume the LoRA K-slice in MFMA K-steps of 32
-_MIN_M = 256     # training / prefill-sized GEMMs: gemm4w and the fused LoRA paths
-
-# GEMM launches by form since the last clear (bench.py provenance): "gemm4w" (bf16 B operand), "gemm4w-nf4"
-# (the NF4 codes read in-kernel), "nf4-expansion" (one bf16 copy of an NF4 base), "decode" (skinny / gemv
-# weight-streaming kernels), "library" (torch.matmul fallback for shapes gemm4w does not take)
-GEMM_STATS: collections.Counter = collections.Counter()
-
-
-def _count(form: str, n: int = 1):
-    GEMM_STATS[form] += n
-
-
-def _g4w_ok(a: torch.Tensor, w: torch.Tensor, bt: bool) -> bool:
-    """Shapes / strides the gemm4w kernel takes for a bf16 weight: a [M, K] row-major (row stride % 8),
-    w [N, K] (or [K, N] when bt) with unit inner stride, training-sized M — the same predicate the
-    binding enforces (``gemm4w_supported``: K % 64, N % 8, every operand's byte extent < 4 GiB), so an
-    oversized operand falls back here instead of failing in the kernel's TORCH_CHECK."""
-    if not (a.is_cuda and a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and a.dim() == 2
-            and w.dim() == 2 and a.shape[0] >= _MIN_M and a.stride(1) == 1 and w.stride(1) == 1
-            and a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0):
-        return False
-    K = a.shape[1]
-    if (w.shape[0] if bt else w.shape[1]) != K:
-        return False
-    N = w.shape[1] if bt else w.shape[0]
-    return bool(native().gemm4w_ok(a.shape[0], N, K, a.stride(0), w.stride(0), bt, False))
-
-
-def _w4_ok(a: torch.Tensor, q: NF4Weight, bt: bool) -> bool:
-    """An NF4 base the gemm4w kernel reads as codes (K9): forward x·deq(W)ᵀ (bt=False, a [M, K_w]) or
-    dX = dY·deq(W) (bt=True, a [M, N_w]); blocksize 64, both dims multiples of 64, M > 8."""
-    if not (a.is_cuda and a.dtype == torch.bfloat16 and a.dim() == 2 and a.shape[0] > 8
-            and a.stride(1) == 1 and a.data_ptr() % 16 == 0 and q.kernel_ok()):
-        return False
-    n, k = q.shape
-    if a.shape[1] != (n if bt else k):
-        return False
-    return bool(native().gemm4w_ok(a.shape[0], k if bt else n, a.shape[1], a.stride(0), 0, bt, True))
-
-
-def _w4_gemm(a: torch.Tensor, q: NF4Weight, bt: bool, c: torch.Tensor | None = None) -> torch.Tensor:
-    """gemm4w on NF4 codes: a·deq(W)ᵀ (+ c) or, bt, a·deq(W) (+ c)."""
-    codes, sc = q.g4w_pack()
-    n, k = q.shape
-    _count("gemm4w-nf4")
-    return native().gemm4w(a, codes, c, 0, bt, 0, 0, sc, k if bt else n)
-
-
-def _nf4_dequant_bf16(q: NF4Weight) -> torch.Tensor:
-    """One bf16 expansion of an NF4 base (HBM speed)."""
-    n, k = q.shape
-    _count("nf4-expansion")
-    return native().nf4_dequant_fast(q.codes, q.gemv_scales(), n, k)
-
-
-# Which NF4 form a call takes (LIPA_NF4_GEMM = w4 | expand | auto).  Measured per GEMM at the Qwen3-8B
-# shapes (profiles/r4/gemm4w_nf4_ab.txt): the in-kernel expansion costs 1.1-1.2x the bf16 gemm4w time
-# (the 3-VALU-per-element table lookup is only partly hidden beside 16x16x32 MFMAs), the same as an
-# expansion + bf16 GEMM when that copy serves ONE GEMM.  "auto" therefore expands where the copy is
-# reused — a training forward whose backward needs dX (the copy is kept for it: ≈14 GB transient for
-# Qwen3-8B), a checkpointed layer (one expansion per optimizer step, below) — and feeds the codes
-# straight in everywhere else (inference, no-grad prefill, frozen inputs): no transient bf16 weights.
-# "w4" everywhere is the memory-lean training mode (peak HBM ≈ the 4-bit model + activations).
-_NF4_MODE = os.environ.get("LIPA_NF4_GEMM", "auto")
-
-
-def _nf4_w4(reused: bool) -> bool:
-    if _NF4_MODE == "w4":
-        return True
-    if _NF4_MODE == "expand":
-        return False
-    return not (reused or _IN_CKPT[0])
-
-
-# NF4-aware activation checkpointing: inside a checkpointed layer (its forward AND its backward
-# recompute) the bf16 expansion of each frozen NF4 base is made once per optimizer step and reused —
-# the reference-faithful step (gradient checkpointing + sequential GA micro-steps) otherwise expands
-# every weight 2 × GA times per step.  The copies are held in ONE registry, bounded by
-# LIPA_CKPT_NF4_CACHE_GB (default 32; 0 = off: every call expands), and released eagerly when the
-# optimizer steps (``nf4_cache_advance``: optim/adamw.py, parallel/zero.py; an optimizer that never
-# calls it keeps at most the budget).  Memory: the budget is the cost — Qwen3-8B's bases expand to
-# 13.9 GB (peak HBM of the faithful bench step: README §3).
-_CKPT_BUDGET = float(os.environ.get("LIPA_CKPT_NF4_CACHE_GB", "32")) * 2 ** 30
-_IN_CKPT = [0]
-_CACHE: dict = {}        # id(NF4Weight) -> (weight, bf16 expansion)
-_CACHE_BYTES = [0]
-
-
-def nf4_cache_advance():
-    """Called by the optimizers at every step: the expanded copies of the finished step are released."""
-    _CACHE.clear()
-    _CACHE_BYTES[0] = 0
-
-
-def _nf4_expand(q: NF4Weight) -> torch.Tensor:
-    """The bf16 expansion for the "expand" form (cached inside checkpointed layers, see above)."""
-    if _IN_CKPT[0]:
-        hit = _CACHE.get(id(q))
-        if hit is not None and hit[0] is q:
-            return hit[1]
-    w = _nf4_dequant_bf16(q)
-    if _IN_CKPT[0] and _CACHE_BYTES[0] + w.numel() * 2 <= _CKPT_BUDGET:
-        _CACHE[id(q)] = (q, w)
-        _CACHE_BYTES[0] += w.numel() * 2
-    return w
-
-
-# LoRA kernel forms (the A/B-measured winners of round 2, fixed; profiles/lora_acc_mfma_ab.txt):
-# q_proj + v_proj with dropout — the forward's lora_proj2 stores the keep bits (1 bit per element and
-# branch) for the backward instead of re-hashing; two-branch backward launches (lora_proj_pair /
-# lora_acc_pair); the LoRA dX term as the dX GEMM's C matrix + a separate dA launch
-_KEEP_BITS = True
-_PAIR_BWD = True
-_DX_C = True
+EXT_ALIGN = 32   # the general form's K-slice: MFMA K-steps of 32
 
 
 @dataclasses.dataclass
@@ -174,80 +56,6 @@ def _pad_cols(t: torch.Tensor, mult: int = EXT_ALIGN) -> torch.Tensor:
         return t.contiguous()
     return F.pad(t, (0, rp - r)).contiguous()
 
-
-def head_logits(h: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
-    """LM-head logits of serving rows through the same dispatch as the projections: decode-sized row counts take
-    the split-K weight-streaming kernel, whose per-row result does not depend on how many rows share the call
-    (the library GEMM's algorithm — and rounding — changes with M), so a request's greedy tokens do not depend on
-    the batch it was decoded in (continuous batching, hipGraph buckets, the pipelined engine)."""
-    x = h.reshape(-1, h.shape[-1])
-    if not x.is_contiguous():
-        x = x.contiguous()
-    return _base_gemm(x, weight).view(*h.shape[:-1], weight.shape[0])
-
-
-def _base_gemm(x, base, ext_a=None, ext_b=None, residual=None):
-    if isinstance(base, NF4Weight):
-        if x.shape[0] <= 8 and base.kernel_ok():   # decode: weight-streaming GEMV, no MFMA tile
-            n, k = base.shape
-            _count("decode")
-            y = native().gemv_w4(x, base.codes, base.gemv_scales(), None, n, base.blocksize,
-                                 residual if ext_a is None else None)
-            if ext_a is not None:
-                y = y + ext_a @ ext_b.t()
-                if residual is not None:
-                    y = y + residual
-            return y
-        if _w4_ok(x, base, False):                  # the NF4 dequant-GEMM (gemm4w reads the codes)
-            y = _w4_gemm(x, base, False, None if residual is None else residual.contiguous())
-            return y if ext_a is None else y.addmm_(ext_a, ext_b.t())
-        w = _nf4_dequant_bf16(base) if (base.kernel_ok() and x.is_cuda) else dequantize_nf4(base, x.dtype)
-        return _base_gemm(x, w, ext_a, ext_b, residual)
-    M, K = x.shape
-    N = base.shape[0]
-    if (x.is_cuda and M <= 16 and N <= 8192 and K <= 8192 and N % 16 == 0 and K % 64 == 0 and x.stride(0) % 8 == 0
-            and x.stride(1) == 1 and base.is_contiguous()):
-        # decode-sized q|k|v / o projections: the split-K weight-streaming MFMA kernel
-        # (csrc/kernels/skinny.hip) beats hipBLASLt's latency-bound 23 µs by 25-45 % and fuses
-        # the residual; the wide gate|up / long-K down stay on hipBLASLt (≥ 5 TB/s there)
-        _count("decode")
-        y = native().gemm_skinny(x, base, residual)
-        return y if ext_a is None else y.addmm_(ext_a, ext_b.t())
-    if _g4w_ok(x, base, False):
-        _count("gemm4w")
-        y = native().gemm4w(x, base, None if residual is None else residual.contiguous(), 0, False)
-        return y if ext_a is None else y.addmm_(ext_a, ext_b.t())
-    # shapes gemm4w does not take (CPU, M < 256, K % 64): torch — residual = addmm's beta term, the LoRA
-    # K-slice one rank-Σr update
-    _count("library")
-    y = torch.addmm(residual, x, base.t()) if residual is not None else x @ base.t()
-    if ext_a is not None:
-        y.addmm_(ext_a, ext_b.t())
-    return y
-
-
-def _dense_dx(dy: torch.Tensor, w: torch.Tensor, c: torch.Tensor | None = None) -> torch.Tensor:
-    """dX = dY·W (+ c) for a bf16 [N, K] weight: gemm4w's transposed-B form (W read as stored; split-K when
-    the output has fewer tiles than CUs, e.g. gate|up dX at M = 2048), else torch."""
-    if _g4w_ok(dy, w, True):
-        _count("gemm4w")
-        return native().gemm4w(dy, w, c, 0, True)
-    _count("library")
-    return dy @ w if c is None else torch.addmm(c, dy, w)
-
-
-def _base_gemm_t(dy, base, ext_a=None, ext_b=None, c=None):
-    """dX = dY·W (+ c) (+ ext_a · ext_bᵀ, ext_b given as [K, R])."""
-    if isinstance(base, NF4Weight):
-        if _w4_ok(dy, base, True):
-            dx = _w4_gemm(dy, base, True, c)
-            return dx if ext_a is None else dx.addmm_(ext_a, ext_b.t())
-        base = _nf4_dequant_bf16(base) if (base.kernel_ok() and dy.is_cuda) else dequantize_nf4(base, dy.dtype)
-    dx = _dense_dx(dy, base, c)
-    return dx if ext_a is None else dx.addmm_(ext_a, ext_b.t())
-
-
-_KEY = [0x5DEECE66D << 20]
 
 # "gradient final" listeners (parallel/ddp.py bucket overlap): called with the parameter whose
 # flat-buffer gradient a fused backward kernel has just accumulated in place (those gradients
@@ -274,82 +82,6 @@ def _notify_grad_ready(p):
         _GRAD_READY[:] = [r for r in _GRAD_READY if r() is not None]
 
 
-def next_dropout_key() -> int:
-    """Counter-based dropout stream: every call gets a fresh 63-bit key (deterministic given
-    the seed set by :func:`seed_dropout`)."""
-    _KEY[0] = (_KEY[0] + 0x9E3779B97F4A7C15) & 0x7FFFFFFFFFFFFFFF
-    return _KEY[0]
-
-
-def seed_dropout(seed: int):
-    _KEY[0] = (int(seed) * 0x2545F4914F6CDD1D) & 0x7FFFFFFFFFFFFFFF
-
-
-_CKPT_REENTRANT = os.environ.get("LIPA_CKPT_REENTRANT", "1") == "1"
-# HF semantics by default (the whole layer recomputed); "selective" keeps every GEMM output of the
-# first forward (~78 MB per Qwen3-8B layer per 1024 tokens) and is opt-in
-_CKPT_POLICY = os.environ.get("LIPA_CKPT_POLICY", "full")
-
-
-def checkpoint(fn, *args, use_reentrant: bool | None = None, policy: str | None = None):
-    """Activation checkpointing of one layer that replays the SAME LoRA dropout masks.
-
-    ``use_reentrant`` selects torch's form (HF's ``gradient_checkpointing_kwargs={"use_reentrant": …}``,
-    ``Fine-Tuning/qwen3-8b-qlora-dist.py:162-163``; default: LIPA_CKPT_REENTRANT, on).  ``policy``:
-    ``"full"`` (default, LIPA_CKPT_POLICY) recomputes the whole layer in backward (HF's behaviour);
-    ``"selective"`` records the GEMM outputs in the first forward and replays them in the recompute —
-    only RMSNorm, q/k-norm + RoPE and attention run again (the stash below): faster, but it holds
-    ≈ 78 MB per Qwen3-8B layer per 1024 tokens from the forward until the backward.
-
-    The fused LoRA kernels draw their dropout mask from the host key stream above, not from
-    torch's RNG, so torch's ``preserve_rng_state`` does not cover them: a plain
-    ``torch.utils.checkpoint`` recompute would draw fresh keys and the backward would differentiate
-    a different mask than the forward applied.  Here the key-stream position at the first (forward)
-    call is remembered and restored for the recompute, then the live stream is put back — the
-    masks match exactly and the stream advances once per real forward.  Reference:
-    ``Fine-Tuning/qwen3-8b-lora.py:123`` (gradient checkpointing + ``lora_dropout``).  The reentrant
-    form's first forward builds no graph (no saved-tensor pack hooks: ~2k per step at Qwen3-8B, the
-    host-side cost of the checkpointed step, profiles/baseline_configs_r2_end.txt)."""
-    import torch.utils.checkpoint as ckpt
-    reentrant = _CKPT_REENTRANT if use_reentrant is None else bool(use_reentrant)
-    policy = policy or _CKPT_POLICY
-    if policy not in ("full", "selective"):
-        raise ValueError(f"checkpoint policy {policy!r}: 'full' or 'selective'")
-    stash = _Stash() if policy == "selective" else None
-    state: list = []
-
-    def run(*a):
-        _IN_CKPT[0] += 1
-        prev = list(_SAC)
-        try:
-            if not state:                      # the forward pass
-                state.append(_KEY[0])
-                if stash is not None:
-                    _SAC[:] = ["record", stash]
-                return fn(*a)
-            live = _KEY[0]                     # the recompute inside backward
-            _KEY[0] = state[0]
-            if stash is not None:
-                stash.pos = 0
-                _SAC[:] = ["replay", stash]
-            try:
-                return fn(*a)
-            finally:
-                _KEY[0] = live
-        finally:
-            _SAC[:] = prev
-            _IN_CKPT[0] -= 1
-
-    if reentrant:
-        # the first forward runs without building a graph; it needs an input that requires grad for the
-        # recompute to reach the LoRA parameters (layer 0's input is the frozen embedding) — the role of
-        # HF's enable_input_require_grads()
-        args = tuple(a.detach().requires_grad_() if isinstance(a, torch.Tensor) and i == 0 and
-                     a.is_floating_point() and not a.requires_grad else a for i, a in enumerate(args))
-        return ckpt.checkpoint(run, *args, use_reentrant=True)
-    return ckpt.checkpoint(run, *args, use_reentrant=False)
-
-
 def bf16_view(p: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
     """The optimizer-maintained low-precision shadow of a fp32 trainable parameter
     (written by the fused AdamW kernel every step), else a cast."""
@@ -363,7 +95,6 @@ def deterministic() -> bool:
     """Bit-reproducible LoRA gradients (``LIPA_DETERMINISTIC=1`` or
     ``torch.use_deterministic_algorithms(True)``): fixed-order partial sums instead of fp32
     atomics in the fused LoRA backward (≈0.5 % slower)."""
-    import os
     return os.environ.get("LIPA_DETERMINISTIC", "0") == "1" or torch.are_deterministic_algorithms_enabled()
 
 
@@ -421,42 +152,11 @@ def _multi_ok(x, branches) -> bool:
 
 
 def _fast_lora_ok(x, branches) -> bool:
-    """Shapes the fused LoRA branch kernels (csrc/kernels/lora.hip) take."""
+    """Shapes the fused LoRA branch kernels (csrc/kernels/lora.hip) take: up to 4 adapters of rank <= 16 on
+    128-aligned column ranges of a 128-aligned input (else the general torch form)."""
     K = x.shape[1]
-    return (K % 128 == 0 and all(br.a.shape[0] <= 16 and (br.c1 - br.c0) % 128 == 0 for br in branches))
-
-
-# Selective activation checkpointing (``checkpoint(..., policy="selective")``): the checkpointed
-# layer's first forward RECORDS the outputs of its GEMM ops (the frozen-base projections with their LoRA
-# side products, the fused SwiGLU MLP) in a per-call stash; the recompute inside backward REPLAYS them
-# instead of launching the GEMMs again, and recomputes only the cheap ops between them (RMSNorm, q/k-norm
-# + RoPE, attention).  The stash holds ≈ 78 MB per Qwen3-8B layer at 1024 tokens (y_qkv, y_o, gu, y_down
-# + the rank-r LoRA projections) until the backward consumes it.
-_SAC: list = [None, None]      # (mode "record" | "replay", stash list)
-
-
-def _sac_recording() -> bool:
-    return _SAC[0] == "record"
-
-
-def sac_put(item):
-    if _SAC[0] == "record":
-        _SAC[1].append(item)
-
-
-def sac_take():
-    """The next recorded op output when replaying, else None."""
-    if _SAC[0] != "replay":
-        return None
-    st = _SAC[1]
-    i = st.pos
-    st.pos += 1
-    item, st[i] = st[i], None
-    return item
-
-
-class _Stash(list):
-    pos = 0
+    return (K % 128 == 0 and len(branches) <= 4
+            and all(br.a.shape[0] <= 16 and (br.c1 - br.c0) % 128 == 0 for br in branches))
 
 
 class _FusedLinearFn(torch.autograd.Function):
@@ -480,10 +180,9 @@ class _FusedLinearFn(torch.autograd.Function):
         # (grad mode is off inside forward: ask autograd; a recording first forward keeps the LoRA side
         # products too — the replay's backward needs them)
         need_xa = any(ctx.needs_input_grad[5:]) or _sac_recording()
-        # "apply" form: the adapters' B term inside gemm4w (epi) or added by lora_apply into ONLY their column
-        # blocks of the base GEMM's output (no K-slice buffers, no per-call B copies, no rank-Σr update over
-        # all N columns); the K-slice form below serves the CPU / odd-shaped rest
-        apply = fast and x.is_cuda and len(branches) <= 4
+        # the fused kernels: the adapters' B term inside gemm4w (epi) or added by lora_apply into ONLY their
+        # column blocks of the base GEMM's output; the general form below serves the odd-shaped rest
+        apply = fast
         wdq = None
         if not dense and x.shape[0] > 8 and base.kernel_ok() and x.is_cuda and not _nf4_w4(ctx.needs_input_grad[0]):
             wdq = _nf4_expand(base)     # the expand form: this copy also serves the dX GEMM
@@ -503,9 +202,9 @@ class _FusedLinearFn(torch.autograd.Function):
                 ps = [br.dropout if training else 0.0 for br in branches]
                 keys = [next_dropout_key() if p > 0 else None for p in ps]
                 a0, a1 = bf16_view(ab[0], x.dtype), bf16_view(ab[2], x.dtype)
-                # training with dropout on both: keep the masks' bits (2 bits / element of x) for lora_acc2
+                # training with dropout on both: keep the masks' bits (2 bits / element of x) for the backward (lora_acc_quad, gemm4w_loradx)
                 masks = (torch.empty(2, x.shape[0], x.shape[1] // 8, dtype=torch.uint8, device=x.device)
-                         if need_xa and all(k is not None for k in keys) and _KEEP_BITS else None)
+                         if need_xa and all(k is not None for k in keys) else None)
                 xa2 = native().lora_proj2(x, a0, a1, None if xa32 is None else xa32[:, :a0.shape[0] + a1.shape[0]], True,
                                           ps[0], keys[0] or 0, branches[0].scaling, ps[1], keys[1] or 0,
                                           branches[1].scaling, masks)
@@ -532,50 +231,26 @@ class _FusedLinearFn(torch.autograd.Function):
                                                       key or 0, br.scaling))
                     keys.append(key)
         elif branches:
+            # the general form: each adapter's s·D(x)·Aᵀ by torch, all of them one extra K-slice of the base GEMM
             N = base.shape[0]
             rtot = sum(br.a.shape[0] for br in branches)
             rp = (rtot + EXT_ALIGN - 1) // EXT_ALIGN * EXT_ALIGN
             layout = tuple((br.c0, br.c1, br.a.shape[0]) for br in branches)
-            if x.is_cuda and not torch.cuda.is_current_stream_capturing():
-                ext_b = _zero_buffer(f"lora_b{layout}", N, rp, x)
-                ext_a = _zero_buffer(f"lora_xa{rtot}", x.shape[0], rp, x) if fast else None
-            else:
-                ext_b = x.new_zeros(N, rp)
-                ext_a = x.new_zeros(x.shape[0], rp) if fast else None
+            ext_b = (_zero_buffer(f"lora_b{layout}", N, rp, x) if not torch.cuda.is_current_stream_capturing()
+                     else x.new_zeros(N, rp))
             cols, r0 = [], 0
-            pair = fast and _pair_ok(x, branches)
-            if pair:   # q_proj + v_proj: ONE pass over x for both adapters (lora_proj2)
-                ps = [br.dropout if training else 0.0 for br in branches]
-                pair_keys = [next_dropout_key() if p > 0 else None for p in ps]
-                a0, a1 = bf16_view(ab[0], x.dtype), bf16_view(ab[2], x.dtype)
-                rr = a0.shape[0] + a1.shape[0]
-                xa2 = native().lora_proj2(x, a0, a1, ext_a[:, :rr], need_xa, ps[0], pair_keys[0] or 0,
-                                          branches[0].scaling, ps[1], pair_keys[1] or 0, branches[1].scaling, None)
-            for bi, (br, (a, b)) in enumerate(zip(branches, zip(ab[0::2], ab[1::2]))):
+            for br, a, b in zip(branches, ab[0::2], ab[1::2]):
                 r = a.shape[0]
                 p = br.dropout if training else 0.0
-                if pair:
-                    key = pair_keys[bi]
-                    xa = xa2[:, r0:r0 + r] if need_xa else None
-                    ext_b[br.c0:br.c1, r0:r0 + r] = bf16_view(b, x.dtype)
-                    xa_list.append(xa)
-                    keys.append(key)
-                    r0 += r
-                    continue
                 key = next_dropout_key() if p > 0 else None
-                if fast:   # one MFMA pass: s·D(x)·Aᵀ into the ext slice (bf16) + fp32 copy for dB
-                    xa = native().lora_proj(x, 0, x.shape[1], bf16_view(a, x.dtype), ext_a[:, r0:r0 + r],
-                                            need_xa, p, key or 0, br.scaling)
-                else:
-                    xd = native().dropout_fwd(x, p, key) if key is not None else x
-                    xa = xd @ bf16_view(a, x.dtype).t()                # [T, r]
-                    cols.append(xa * br.scaling)
+                xd = native().dropout_fwd(x, p, key) if key is not None else x
+                xa = xd @ bf16_view(a, x.dtype).t()                # [T, r]
+                cols.append(xa * br.scaling)
                 ext_b[br.c0:br.c1, r0:r0 + r] = bf16_view(b, x.dtype)
                 xa_list.append(xa)
                 keys.append(key)
                 r0 += r
-            if not fast:
-                ext_a = _pad_cols(torch.cat(cols, 1))
+            ext_a = _pad_cols(torch.cat(cols, 1))
         ctx.bts = None
         if epi:
             bs = [bf16_view(b, x.dtype) for b in ab[1::2]]
@@ -654,7 +329,7 @@ class _FusedLinearFn(torch.autograd.Function):
             return _multi_backward(ctx, dy, x, weight, xa_list, base, branches, dense, dest)
         # q_proj + v_proj: both adapters' s·dy_i·B_i in one launch, both dB_i in another
         pair_g = (fast and nb == 2 and ctx.bts is not None and ctx.bts[0].shape[0] == ctx.bts[1].shape[0]
-                  and all(bt.shape[1] % 512 == 0 for bt in ctx.bts) and _PAIR_BWD)
+                  and all(bt.shape[1] % 512 == 0 for bt in ctx.bts))
         if pair_g:
             g_list = list(native().lora_proj_pair(dy, branches[0].c0, ctx.bts[0], branches[0].scaling,
                                                   branches[1].c0, ctx.bts[1], branches[1].scaling))
@@ -664,7 +339,7 @@ class _FusedLinearFn(torch.autograd.Function):
                     and all((br.c1 - br.c0) % 128 == 0 for br in branches)):
                 (o0, ret0), (o1, ret1) = dest(1), dest(3)
                 # with the dropout pair's dA due too (the keep-bit path below), both dB and both dA in ONE launch
-                quad = (_DX_C and ctx.pair and all(k is not None for k in ctx.keys) and ctx.masks is not None
+                quad = (ctx.pair and all(k is not None for k in ctx.keys) and ctx.masks is not None
                         and ctx.needs_input_grad[0] and ctx.needs_input_grad[5] and ctx.needs_input_grad[7]
                         and dy.shape[0] >= _MIN_M and x.shape[1] % 128 == 0
                         and g_list[0].shape[1] == xs[0].shape[1])
@@ -724,10 +399,10 @@ class _FusedLinearFn(torch.autograd.Function):
             wb = ctx.wdq if ctx.wdq is not None else (base if not dense else weight)
             pair_ok = (ctx.pair and all(k is not None for k in ctx.keys) and not deterministic()
                        and ctx.needs_input_grad[5] and ctx.needs_input_grad[7])
-            if pair_ok and _DX_C and ctx.masks is not None and not fold and dy.shape[0] >= _MIN_M:
-                # the LoRA input-gradient term written once (lora_dx2, from the stored keep bits) and
-                # added by the dX GEMM as its C matrix; dA from x in a separate launch — no
-                # read-modify-write pass over dx (lora_acc2)
+            if pair_ok and ctx.masks is not None and not fold and dy.shape[0] >= _MIN_M:
+                # the masked LoRA input-gradient term from the stored keep bits, inside the dX GEMM (or, for shapes
+                # gemm4w_loradx does not take, written once by lora_dx2 and added as the GEMM's C matrix); dA by
+                # lora_acc_quad above or one lora_dA_pair launch — no read-modify-write pass over dx
                 a0, a1 = bf16_view(ab[0], dy.dtype), bf16_view(ab[2], dy.dtype)
                 p0, p1 = branches[0].dropout, branches[1].dropout
                 fused_ok = wb.shape[1] % 128 == 0 and all(g.shape[1] % 8 == 0 and g.shape[1] <= 32 for g in g_list)
@@ -754,7 +429,6 @@ class _FusedLinearFn(torch.autograd.Function):
                         grads_ab[2 * i] = o.to(ab[2 * i].dtype)
                     else:
                         _notify_grad_ready(ctx.ab_refs[2 * i])
-                pair_ok = False
                 done_dA = True
             else:
                 assert done_quad is None, "lora_acc_quad ran but the keep-bit dX path did not"
@@ -762,26 +436,12 @@ class _FusedLinearFn(torch.autograd.Function):
                 dx = _base_gemm_t(dy, wb, ext_a, ext_b)
                 done_dA = False
         else:
-            pair_ok = done_dA = False
+            done_dA = False
         ctx.wdq = None
         ctx.bts = None
-        if done_dA:
-            branches_acc = ()
-        elif (ctx.pair and dx is not None and all(k is not None for k in ctx.keys) and not deterministic()
-                and ctx.needs_input_grad[5] and ctx.needs_input_grad[7]):
-            # both adapters' dA and their dx terms in ONE pass over x and dx (lora_acc2)
-            (o0, ret0), (o1, ret1) = dest(0), dest(2)
-            native().lora_acc2(g_list[0], g_list[1], x, dx, bf16_view(ab[0], dy.dtype), bf16_view(ab[2], dy.dtype),
-                               o0, o1, branches[0].dropout, ctx.keys[0], branches[1].dropout, ctx.keys[1], ctx.masks)
-            ctx.masks = None
-            for i, (o, ret) in ((0, (o0, ret0)), (1, (o1, ret1))):
-                if ret:
-                    grads_ab[2 * i] = o.to(ab[2 * i].dtype)
-                else:
-                    _notify_grad_ready(ctx.ab_refs[2 * i])
-            branches_acc = ()
-        else:
-            branches_acc = branches
+        ctx.masks = None
+        # dA (and, for dropout adapters outside the fused dX paths, their input-gradient term) per adapter
+        branches_acc = () if done_dA else branches
         for i, br in enumerate(branches_acc):
             key = ctx.keys[i]
             if fast:   # dA += gᵀ·D(x) and (dropout branches) dx += D(g·A), one pass over x / dx

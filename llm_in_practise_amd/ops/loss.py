@@ -15,7 +15,7 @@ import torch.nn.functional as F
 
 from . import reference as ref
 from ._native import native, use_native
-from .linear import _count, _g4w_ok
+from .gemm import _count, _g4w_ok
 
 
 def cross_entropy(logits, labels, ignore_index: int = -100):

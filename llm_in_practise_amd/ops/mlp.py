@@ -25,7 +25,8 @@ import torch
 
 from ..quant.nf4 import NF4Weight
 from ._native import native
-from .linear import _MIN_M, _count, _nf4_expand, _nf4_w4, sac_put, sac_take
+from .checkpoint import sac_put, sac_take
+from .gemm import _MIN_M, _count, _nf4_expand, _nf4_w4
 
 
 def _operand(base, reused: bool):

@@ -134,6 +134,9 @@ class _FlatOptimizer:
     # torch.optim-like surface ----------------------------------------------------
     def zero_grad(self, set_to_none: bool = False):
         self.flat.zero_grad()
+        # a clip_grad_norm_ that no step() followed (a logged-only norm, a skipped step) must not let the next
+        # step() skip its own sync_grads / NF4-cache release
+        self._prepared = False
 
     @property
     def grad_buffer(self) -> torch.Tensor:

@@ -508,9 +508,9 @@ def test_qwen3_native_matches_reference(mode, arch, monkeypatch):
         pm.train()
         return pm
 
-    if mode == "qlora-dequant":      # NF4 bases: HIP dequant once per step + hipBLASLt fwd / dX
-        from llm_in_practise_amd.ops import linear
-        monkeypatch.setattr(linear, "_NF4_MODE", "dequant")
+    if mode == "qlora-dequant":      # NF4 bases: one HIP expansion per step + gemm4w fwd / dX on the bf16 copy
+        from llm_in_practise_amd.ops import gemm
+        monkeypatch.setattr(gemm, "_NF4_MODE", "expand")
     ids = torch.randint(0, cfg.vocab_size, (2, 128), device=DEV)
     res = {}
     for ref_mode in ("0", "1"):

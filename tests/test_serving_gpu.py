@@ -245,3 +245,17 @@ def test_gpu_memory_utilization_sizes_kv_pool(lm):
     with pytest.raises(ValueError):
         ServingEngine(lm, _tok(), max_batch=4, max_model_len=2048, use_graphs=False,
                       gpu_memory_utilization=used / total)
+
+
+def test_head_logits_batch_invariant_large_vocab(native_ext):
+    """LM-head logits of a row do not depend on how many rows share the call, at a vocabulary past the skinny
+    kernel's range and batches past 16 (ops/gemm.py head_logits: gemm4w with one K-split at every M)"""
+    from llm_in_practise_amd.ops.gemm import head_logits
+    torch.manual_seed(0)
+    w = (0.02 * torch.randn(20000, 1024, device="cuda")).to(torch.bfloat16)
+    x = torch.randn(300, 1024, device="cuda").to(torch.bfloat16)
+    full = head_logits(x, w)
+    ref = x.float() @ w.float().t()
+    assert (full.float() - ref).norm() / ref.norm() < 1e-2
+    for rows in (1, 5, 16, 17, 37, 256):
+        assert torch.equal(head_logits(x[:rows].contiguous(), w), full[:rows]), rows
