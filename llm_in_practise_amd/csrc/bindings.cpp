@@ -390,6 +390,25 @@ void adamw(Tensor p, Tensor g, Tensor m, Tensor v, optional<Tensor> p16, double 
                stream());
 }
 
+// A device tensor whose storage is pinned, device-mapped HOST memory (hipHostMalloc mapped + its device pointer):
+// kernels read and write it across the host link, nothing of it occupies HBM.  The "paged" placement of the 8-bit
+// optimizer states (optim/adamw.py AdamW8bit(paged="host"), bitsandbytes paged_adamw_8bit's role).
+Tensor host_mapped_empty(int64_t numel, at::ScalarType dtype) {
+  TORCH_CHECK(numel > 0, "host_mapped_empty: numel > 0");
+  const size_t bytes = (size_t)numel * c10::elementSize(dtype);
+  void* hp = nullptr;
+  TORCH_CHECK(hipHostMalloc(&hp, bytes, hipHostMallocMapped) == hipSuccess, "host_mapped_empty: hipHostMalloc failed");
+  void* dp = nullptr;
+  if (hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess) {
+    (void)hipHostFree(hp);
+    TORCH_CHECK(false, "host_mapped_empty: hipHostGetDevicePointer failed");
+  }
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  return torch::from_blob(dp, {numel}, [hp](void*) { (void)hipHostFree(hp); },
+                          torch::TensorOptions().dtype(dtype).device(torch::kCUDA, dev));
+}
+
 void adamw8bit(Tensor p, Tensor g, Tensor qm, Tensor qv, Tensor am, Tensor av, Tensor code_s, Tensor code_u,
                optional<Tensor> p16, double lr, double b1, double b2, double eps, double wd, int64_t step,
                optional<Tensor> gscale, optional<Tensor> skip) {
@@ -1701,6 +1720,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sample", &sample);
   m.def("adamw", &adamw);
   m.def("adamw8bit", &adamw8bit);
+  m.def("host_mapped_empty", &host_mapped_empty, py::arg("numel"), py::arg("dtype"));
   m.def("unscale", &unscale);
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequant", &nf4_dequant);

@@ -85,8 +85,21 @@ def checkpoint(fn, *args, use_reentrant: bool | None = None, policy: str | None 
         # HF's enable_input_require_grads()
         args = tuple(a.detach().requires_grad_() if isinstance(a, torch.Tensor) and i == 0 and
                      a.is_floating_point() and not a.requires_grad else a for i, a in enumerate(args))
-        return ckpt.checkpoint(run, *args, use_reentrant=True)
-    return ckpt.checkpoint(run, *args, use_reentrant=False)
+        return ckpt.checkpoint(run, *args, use_reentrant=True, preserve_rng_state=_torch_rng_used(args))
+    # torch's RNG state is saved / restored around the recompute only where an op of the layer draws from it (the CPU
+    # reference path's F.dropout): the HIP path's dropout comes from the key stream restored above, so the per-layer
+    # CPU + device generator snapshots would be pure host time.  The recompute-matches-forward check is dropped
+    # for the same reason it holds by construction (same key stream, same kernels).
+    return ckpt.checkpoint(run, *args, use_reentrant=False, preserve_rng_state=_torch_rng_used(args),
+                           determinism_check="default" if _torch_rng_used(args) else "none")
+
+
+def _torch_rng_used(args) -> bool:
+    """Whether a checkpointed layer on these inputs draws from torch's RNG: only off the HIP path (CPU tensors or
+    LIPA_REFERENCE=1, where LoRA / attention dropout are torch ops)."""
+    from ._native import force_reference
+    x = next((a for a in args if isinstance(a, torch.Tensor)), None)
+    return x is None or not x.is_cuda or force_reference()
 
 
 

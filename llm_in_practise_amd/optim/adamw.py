@@ -10,8 +10,10 @@ become views into contiguous fp32 buffers.  Consequences (all MI355X-motivated):
 
 ``AdamW``       — torch.optim.AdamW semantics (``optim="adamw_torch"``).
 ``AdamW8bit``   — blockwise 8-bit states with the dynamic maps [ext: bitsandbytes
-                  ``paged_adamw_8bit`` state format]; "paged" (unified-memory spill) is not
-                  needed with 288 GB HBM, so states stay resident on the device.
+                  ``paged_adamw_8bit`` state format].  ``paged="host"`` (or ``LIPA_PAGED_OPTIM=host``)
+                  places the states in pinned, device-mapped host memory: the update kernel reads and
+                  writes them across the host link and they take no HBM (bitsandbytes pages its states
+                  to the host under memory pressure; with 288 GB of HBM the default keeps them resident).
 On CPU both fall back to a reference implementation (used by tests / minigpt).
 """
 from __future__ import annotations
@@ -222,8 +224,11 @@ class AdamW8bit(_FlatOptimizer):
 
     BLOCK = 256
 
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, max_grad_norm=0.0):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, max_grad_norm=0.0,
+                 paged: str | None = None):
         super().__init__(params, lr, betas, eps, weight_decay, max_grad_norm)
+        import os
+
         from ..quant.nf4 import create_dynamic_map
         dev = self.flat.data.device
         n = self.flat.numel
@@ -232,10 +237,21 @@ class AdamW8bit(_FlatOptimizer):
         self.code_u = create_dynamic_map(False).to(dev)
         z_s = int(torch.argmin(self.code_s.abs()))
         z_u = int(torch.argmin(self.code_u.abs()))
-        self.qm = torch.full((n,), z_s, dtype=torch.uint8, device=dev)
-        self.qv = torch.full((n,), z_u, dtype=torch.uint8, device=dev)
-        self.am = torch.zeros(nb, dtype=torch.float32, device=dev)
-        self.av = torch.zeros(nb, dtype=torch.float32, device=dev)
+        paged = paged if paged is not None else os.environ.get("LIPA_PAGED_OPTIM", "device")
+        if paged not in ("device", "host"):
+            raise ValueError(f"paged={paged!r}: 'device' (HBM-resident states) or 'host' (pinned host memory)")
+        # the states' placement: HBM, or pinned device-mapped host memory (GPU only; CPU tensors are host memory)
+        self.paged = paged if use_native(self.flat.data) else "device"
+
+        def state(numel, dtype, fill):
+            if self.paged == "host":
+                t = native().host_mapped_empty(numel, dtype)
+                return t.fill_(fill)
+            return torch.full((numel,), fill, dtype=dtype, device=dev)
+        self.qm = state(n, torch.uint8, z_s)
+        self.qv = state(n, torch.uint8, z_u)
+        self.am = state(nb, torch.float32, 0.0)
+        self.av = state(nb, torch.float32, 0.0)
 
     def _state(self):
         return {"qm": self.qm, "qv": self.qv, "am": self.am, "av": self.av, "flat_data": self.flat.data}

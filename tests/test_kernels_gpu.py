@@ -238,6 +238,36 @@ def test_adamw8bit_tracks_fp32(native_ext):
     assert rel_err(p8, p) < 1e-3
 
 
+def test_adamw8bit_paged_host_states_match_device(native_ext):
+    """paged_adamw_8bit with the states in pinned, device-mapped host memory (AdamW8bit(paged="host")): the kernel
+    updates them across the host link, bit-identical to HBM-resident states; none of them is in HBM"""
+    from llm_in_practise_amd.optim.adamw import AdamW8bit
+    torch.manual_seed(0)
+    shapes = [(96, 40), (1000,), (8, 256)]
+    a = [torch.nn.Parameter(torch.randn(s, device=DEV)) for s in shapes]
+    b = [torch.nn.Parameter(t.detach().clone()) for t in a]
+    o_dev, o_host = AdamW8bit(a, lr=1e-2, max_grad_norm=1.0), AdamW8bit(b, lr=1e-2, max_grad_norm=1.0, paged="host")
+    assert o_host.paged == "host" and o_dev.paged == "device"
+    free0 = torch.cuda.mem_get_info()[0]
+    for _ in range(5):
+        for p1, p2 in zip(a, b):
+            g = torch.randn(p1.shape, device=DEV)
+            p1.grad.copy_(g)
+            p2.grad.copy_(g)
+        o_dev.clip_grad_norm_(1.0)
+        o_host.clip_grad_norm_(1.0)
+        o_dev.step()
+        o_host.step()
+    torch.cuda.synchronize()
+    for p1, p2 in zip(a, b):
+        assert torch.equal(p1.detach(), p2.detach())
+    for k in ("qm", "qv", "am", "av"):
+        assert torch.equal(getattr(o_dev, k), getattr(o_host, k)), k
+    assert abs(torch.cuda.mem_get_info()[0] - free0) < (64 << 20)   # no device allocation grew with the states
+    sd = o_host.state_dict()
+    o_host.load_state_dict(sd)
+
+
 @pytest.mark.parametrize("kind", ["adamw", "adamw8bit"])
 def test_fused_optimizer_param_groups(native_ext, kind):
     """decay / no-decay groups with their own lr: every group is updated (one segment each)."""
