@@ -198,7 +198,7 @@ __device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g))
 #define G4W_ST_NT(P, V) G4W_ST(P, V)
 #else
 #define G4W_ST(P, V) (*(P) = (V))
-#ifdef LIPA_G4W_NT_STORE
+#ifdef LIPA_G4W_NT_STORE   // (probe: the SwiGLU forward's g / u — saved for the backward — as non-temporal stores)
 #define G4W_ST_NT(P, V) __builtin_nontemporal_store((V), (P))
 #else
 #define G4W_ST_NT(P, V) G4W_ST(P, V)
@@ -432,10 +432,7 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   constexpr int NM = 16 + 12 * NCH;
   constexpr int SPAN = KT - 1 - M0S;
   static_assert(!W4 || M0S + (27 * SPAN) / NM > K1, "W4: the first chunk's ds_write must follow barrier 1");
-  // (the LDS-staged epilogue reuses the stage memory: a bf16 tile or half an fp32 tile, rows padded by 16 B)
-  constexpr int EPI_LDS = (BMT * (BN * 2 + 16) > (BMT / 2) * (BN * 4 + 16)) ? BMT * (BN * 2 + 16)
-                                                                           : (BMT / 2) * (BN * 4 + 16);
-  __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE + RING > EPI_LDS ? STAGES * STAGE + RING : EPI_LDS];
+  __shared__ __attribute__((aligned(16))) char lds[STAGES * STAGE + RING];
 
   const int tiles_m = (M + BMT - 1) / BMT, tiles_n = (N + BN - 1) / BN;
   const int nwg = tiles_m * tiles_n * splits;
@@ -904,163 +901,6 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
   }
 
   // ---- epilogue: lane holds C[m = col][n = 4·(lane>>4) + r … +3] of each 16×16 block
-#ifdef LIPA_G4W_LDS_EPI
-  constexpr bool LDS_EPI = true;
-#else
-  constexpr bool LDS_EPI = false;
-#endif
-  if constexpr (LDS_EPI) {
-    // LDS-staged epilogue: the tile is written into the (now idle) stage memory in the accumulator layout, then
-    // every wave moves whole rows — each store instruction writes 2 rows × 512 B contiguous (bf16, BN = 256)
-    // instead of 16 rows × 64 B.  Rounding points are the register epilogue's: bf16 staging where the output
-    // is rounded from the accumulator alone (plain, SwiGLU g / u, the dSwiGLU dh), fp32 staging in two row
-    // halves where fp32 leaves the kernel (split-K slabs) or a residual is added before the rounding.
-    constexpr int RSB = BN * 2 + 16;   // staged row strides (one 16-B pad chunk: conflict-free 16-row writes)
-    constexpr int RSF = BN * 4 + 16;
-    const int r4 = lane >> 4, lr = lane & 15;
-    __syncthreads();                   // every wave's fragment reads of the last K-tile are done
-    const bool f32_stage = SPLIT || (EPI == 0 && residual != nullptr);
-    if (!f32_stage) {
-      if constexpr (EPI == 1) {        // g | u halves of the staged row (h-columns of this tile)
-        constexpr int NH = NB / 2;
-#pragma unroll
-        for (int i = 0; i < NA; ++i) {
-          char* rowp = lds + (wr * (BMT / 2) + i * 16 + lr) * RSB;
-#pragma unroll
-          for (int hp = 0; hp + 1 < NH; hp += 2) {
-            f32x4 g0 = acc[i][2 * hp], g1 = acc[i][2 * hp + 2], u0 = acc[i][2 * hp + 1], u1 = acc[i][2 * hp + 3];
-            pair_swap(g0, g1);
-            pair_swap(u0, u1);
-            const int hc = 16 * (wc * NH + hp + (r4 & 1)) + 8 * (r4 >> 1);
-            bf16x8 g, u;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              g[e] = (bf16)(e < 4 ? g0[e] : g1[e - 4]);
-              u[e] = (bf16)(e < 4 ? u0[e] : u1[e - 4]);
-            }
-            *reinterpret_cast<bf16x8*>(rowp + hc * 2) = g;
-            *reinterpret_cast<bf16x8*>(rowp + BN + hc * 2) = u;
-          }
-          if constexpr (NH % 2) {
-            constexpr int j = NB - 2;
-            const int hc = 16 * (wc * NH + j / 2) + 4 * r4;
-            bf16x4 g, u;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              g[e] = (bf16)acc[i][j][e];
-              u[e] = (bf16)acc[i][j + 1][e];
-            }
-            *reinterpret_cast<bf16x4*>(rowp + hc * 2) = g;
-            *reinterpret_cast<bf16x4*>(rowp + BN + hc * 2) = u;
-          }
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < NA; ++i) {
-          char* rowp = lds + (wr * (BMT / 2) + i * 16 + lr) * RSB;
-#pragma unroll
-          for (int jp = 0; jp < NB / 2; ++jp) {
-            f32x4 a = acc[i][2 * jp], b = acc[i][2 * jp + 1];
-            pair_swap(a, b);
-            const int c = wc * (BN / 2) + 16 * (2 * jp + (r4 & 1)) + 8 * (r4 >> 1);
-            bf16x8 o;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = (bf16)(e < 4 ? a[e] : b[e - 4]);
-            *reinterpret_cast<bf16x8*>(rowp + c * 2) = o;
-          }
-        }
-      }
-      __syncthreads();
-      // whole rows: 8-column chunks, consecutive threads along a row
-      constexpr int CPR = EPI == 1 ? BN / 16 : BN / 8;    // chunks per staged row (EPI 1: of g, u as well)
-      constexpr int NU = BMT * CPR / NT;
-      static_assert(BMT * CPR % NT == 0, "LDS epilogue: whole passes");
-#pragma unroll 4
-      for (int q = 0; q < NU; ++q) {
-        const int idx = q * NT + (int)threadIdx.x;
-        const int row = idx / CPR, c = idx % CPR;
-        const int m = m0 + row;
-        const char* rowp = lds + row * RSB;
-        if constexpr (EPI == 1) {
-          const int hc = tn * (BN / 2) + 8 * c;
-          const bf16x8 g = *reinterpret_cast<const bf16x8*>(rowp + 16 * c);
-          const bf16x8 u = *reinterpret_cast<const bf16x8*>(rowp + BN + 16 * c);
-          if (m < M && hc < F) {
-            bf16x8 h;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) h[e] = (bf16)(silu_f((float)g[e]) * (float)u[e]);
-            bf16* gu = reinterpret_cast<bf16*>(out) + (size_t)m * 2 * F + hc;
-            G4W_ST(reinterpret_cast<bf16x8*>(gu), g);
-            G4W_ST(reinterpret_cast<bf16x8*>(gu + F), u);
-            G4W_ST(reinterpret_cast<bf16x8*>(aux_out + (size_t)m * F + hc), h);
-          }
-        } else {
-          const int n = n0 + 8 * c;
-          const bf16x8 d = *reinterpret_cast<const bf16x8*>(rowp + 16 * c);
-          if (m < M && n < N) {
-            if constexpr (EPI == 2) {
-              const bf16* gp = aux + (size_t)m * 2 * F + n;
-              const bf16x8 gg = *reinterpret_cast<const bf16x8*>(gp);
-              const bf16x8 uu = *reinterpret_cast<const bf16x8*>(gp + F);
-              bf16x8 dg, du;
-#pragma unroll
-              for (int e = 0; e < 8; ++e) {
-                const float dv = (float)d[e], g = (float)gg[e], uv = (float)uu[e];
-                const float sg = 1.f / (1.f + __expf(-g));
-                du[e] = (bf16)(dv * (g * sg));
-                dg[e] = (bf16)(dv * uv * (sg * (1.f + g * (1.f - sg))));
-              }
-              bf16* dp = reinterpret_cast<bf16*>(out) + (size_t)m * 2 * F + n;
-              G4W_ST(reinterpret_cast<bf16x8*>(dp), dg);
-              G4W_ST(reinterpret_cast<bf16x8*>(dp + F), du);
-            } else {
-              G4W_ST(reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(out) + (size_t)m * N + n), d);
-            }
-          }
-        }
-      }
-    } else if constexpr (EPI == 0) {   // fp32 staging, one half of the rows (one wave row) at a time
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (wr == h) {
-#pragma unroll
-          for (int i = 0; i < NA; ++i) {
-            char* rowp = lds + (i * 16 + lr) * RSF;
-#pragma unroll
-            for (int j = 0; j < NB; ++j)
-              *reinterpret_cast<f32x4*>(rowp + (wc * (BN / 2) + j * 16 + 4 * r4) * 4) = acc[i][j];
-          }
-        }
-        __syncthreads();
-        constexpr int CPR = BN / 8;
-        constexpr int NU = (BMT / 2) * CPR / NT;
-        static_assert((BMT / 2) * CPR % NT == 0, "LDS epilogue: whole passes");
-#pragma unroll 4
-        for (int q = 0; q < NU; ++q) {
-          const int idx = q * NT + (int)threadIdx.x;
-          const int row = idx / CPR, c = idx % CPR;
-          const int m = m0 + h * (BMT / 2) + row, n = n0 + 8 * c;
-          const f32x4 v0 = *reinterpret_cast<const f32x4*>(lds + row * RSF + 32 * c);
-          const f32x4 v1 = *reinterpret_cast<const f32x4*>(lds + row * RSF + 32 * c + 16);
-          if (m < M && n < N) {
-            if constexpr (SPLIT) {
-              float* wp = ws + ((size_t)sp * M + m) * N + n;
-              G4W_ST(reinterpret_cast<f32x4*>(wp), v0);
-              G4W_ST(reinterpret_cast<f32x4*>(wp + 4), v1);
-            } else {
-              const bf16x8 rr = *reinterpret_cast<const bf16x8*>(residual + (size_t)m * N + n);
-              bf16x8 o;
-#pragma unroll
-              for (int e = 0; e < 8; ++e) o[e] = (bf16)((e < 4 ? v0[e] : v1[e - 4]) + (float)rr[e]);
-              G4W_ST(reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(out) + (size_t)m * N + n), o);
-            }
-          }
-        }
-        __syncthreads();
-      }
-    }
-    return;
-  }
   if constexpr (EPI == 1) {
     // h-block hb = gate block 2hb + up block 2hb + 1 (the gathered B rows); h-blocks paired for 16-B stores
     constexpr int NH = NB / 2;
