@@ -73,6 +73,8 @@ def build_hip_extension(jobs: int | None = None, verbose: bool = True) -> str:
     headers = sorted(glob.glob(os.path.join(kdir, "*.h")))
     kflags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
               "-ffp-contract=fast", f"-I{kdir}"]
+    # LIPA_HIP_DEFINES="-DNAME ...": A/B builds of kernel variants (scripts/gpu_r6_ab_build.sh); never set by default
+    kflags += [d for d in os.environ.get("LIPA_HIP_DEFINES", "").split() if d.startswith("-D")]
     bflags = ["-O3", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__=1",
               "-DUSE_ROCM=1", "-DTORCH_API_INCLUDE_EXTENSION_H", "-DTORCH_EXTENSION_NAME=_C",
               f"-I{sysconfig.get_paths()['include']}", f"-I{ROCM}/include"] + [f"-I{p}" for p in inc]

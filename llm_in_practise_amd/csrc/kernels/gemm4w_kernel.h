@@ -192,17 +192,13 @@ G4W_SCHED(4, 6)
 __device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g)); }
 
 // epilogue output store (LIPA_G4W_NOSTORE: experiments only — scripts/experiments/epi_probe — keeps every value
-// computed but stores only under an impossible condition, to time the epilogue's store traffic)
+// computed but stores only under an impossible condition, to time the epilogue's store traffic).  Non-temporal
+// stores for the outputs the backward reads much later (SwiGLU g | u) won 20 µs on the isolated kernel and lost
+// 0.1 ms in the step (profiles/r6/gemm4w_epilogue_probe.txt): every store is plain.
 #ifdef LIPA_G4W_NOSTORE
 #define G4W_ST(P, V) do { if (M < 0) *(P) = (V); } while (0)
-#define G4W_ST_NT(P, V) G4W_ST(P, V)
 #else
 #define G4W_ST(P, V) (*(P) = (V))
-#ifdef LIPA_G4W_NT_STORE   // (probe: the SwiGLU forward's g / u — saved for the backward — as non-temporal stores)
-#define G4W_ST_NT(P, V) __builtin_nontemporal_store((V), (P))
-#else
-#define G4W_ST_NT(P, V) G4W_ST(P, V)
-#endif
 #endif
 
 // Widened epilogue stores (cdna_hip_programming.md T21, for the 16×16 layout): lane row r = lane >> 4 holds
@@ -924,8 +920,8 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
           h[e] = (bf16)(silu_f((float)g[e]) * (float)u[e]);
         }
         bf16* gu = reinterpret_cast<bf16*>(out) + (size_t)m * 2 * F + hc;
-        G4W_ST_NT(reinterpret_cast<bf16x8*>(gu), g);
-        G4W_ST_NT(reinterpret_cast<bf16x8*>(gu + F), u);
+        G4W_ST(reinterpret_cast<bf16x8*>(gu), g);
+        G4W_ST(reinterpret_cast<bf16x8*>(gu + F), u);
         G4W_ST(reinterpret_cast<bf16x8*>(aux_out + (size_t)m * F + hc), h);
       }
       if constexpr (NH % 2) {   // the unpaired last h-block (BN = 192): 8-B stores

@@ -1,6 +1,5 @@
-// Epilogue-cost probe for gemm4w: times the step's multi-round GEMM roles with the shipped epilogue, (built with
-// -DLIPA_G4W_NT_STORE) the SwiGLU g / u as non-temporal stores, and (-DLIPA_G4W_NOSTORE) every output value computed
-// but not stored — how much of each kernel is the
+// Epilogue-cost probe for gemm4w: times the step's multi-round GEMM roles with the shipped epilogue and
+// (-DLIPA_G4W_NOSTORE) every output value computed but not stored — how much of each kernel is the
 // serialized store traffic at the end of each round of tiles (the fixed cost per round of
 // profiles/r5/gemm4w_round_fixed_cost.txt).  One process, uniform operands, min of 5 x 10 launches.
 #include <cmath>
@@ -29,8 +28,7 @@ __global__ void hash_k(const uint32_t* p, size_t n, unsigned long long* out) {
 int main() {
 #if defined(LIPA_G4W_NOSTORE)
   const char* tag = "nostore";
-#elif defined(LIPA_G4W_NT_STORE)
-  const char* tag = "nt_gu";
+
 #else
   const char* tag = "shipped";
 #endif
