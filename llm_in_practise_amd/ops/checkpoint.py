@@ -86,12 +86,69 @@ def checkpoint(fn, *args, use_reentrant: bool | None = None, policy: str | None 
         args = tuple(a.detach().requires_grad_() if isinstance(a, torch.Tensor) and i == 0 and
                      a.is_floating_point() and not a.requires_grad else a for i, a in enumerate(args))
         return ckpt.checkpoint(run, *args, use_reentrant=True, preserve_rng_state=_torch_rng_used(args))
-    # torch's RNG state is saved / restored around the recompute only where an op of the layer draws from it (the CPU
-    # reference path's F.dropout): the HIP path's dropout comes from the key stream restored above, so the per-layer
-    # CPU + device generator snapshots would be pure host time.  The recompute-matches-forward check is dropped
-    # for the same reason it holds by construction (same key stream, same kernels).
-    return ckpt.checkpoint(run, *args, use_reentrant=False, preserve_rng_state=_torch_rng_used(args),
-                           determinism_check="default" if _torch_rng_used(args) else "none")
+    if _torch_rng_used(args):
+        # off the HIP path (CPU / LIPA_REFERENCE=1) an op of the layer draws from torch's RNG (F.dropout): torch's
+        # implementation, with its RNG snapshot around the recompute
+        return ckpt.checkpoint(run, *args, use_reentrant=False)
+    return _nonreentrant(run, args)
+
+
+class _Frame:
+    """One checkpointed call in the non-reentrant form (``use_reentrant=False`` semantics, as
+    ``torch.utils.checkpoint`` implements them): the forward runs with autograd on, but every tensor an op saves
+    for backward is replaced by its index (``pack``); the first ``unpack`` in backward re-runs the layer with the
+    same inputs under hooks that collect the saved tensors in the same order, and each unpack hands one over
+    (and drops it: a second backward through a retained graph recomputes again).  Gradients flow through the
+    ORIGINAL graph — inputs that do not require grad, ``torch.autograd.grad`` and partial backwards work as with
+    torch's form.  What is left out is the generality this stack does not use (nested checkpoints, early stop,
+    pytree inputs, torch-RNG replay — the HIP path's dropout comes from the key stream ``checkpoint`` restores)
+    and with it most of the per-layer host time of the reference-faithful step (profiles/r6/)."""
+    __slots__ = ("run", "args", "count", "saved")
+
+    def __init__(self, run, args):
+        self.run, self.args, self.count, self.saved = run, args, 0, None
+
+    def pack(self, t):
+        i = self.count
+        self.count += 1
+        return i
+
+    def unpack(self, i):
+        if self.saved is None or self.saved[i] is None:
+            self._recompute()
+        t = self.saved[i]
+        self.saved[i] = None
+        return t
+
+    def _recompute(self):
+        rec: list = []
+        args = tuple(a.detach().requires_grad_(a.requires_grad) if isinstance(a, torch.Tensor) else a
+                     for a in self.args)
+        with torch.enable_grad(), torch.autograd.graph.saved_tensors_hooks(_Frame._keep(rec), _Frame._give(rec)):
+            self.run(*args)
+        if len(rec) != self.count:
+            raise RuntimeError(f"checkpoint recompute saved {len(rec)} tensors, the forward {self.count}: the layer "
+                               "took a different code path in the recompute")
+        self.saved = rec
+
+    @staticmethod
+    def _keep(rec):
+        def pack(t):
+            rec.append(t)
+            return None
+        return pack
+
+    @staticmethod
+    def _give(rec):
+        def unpack(_):   # (the recompute's own graph is never backpropagated)
+            raise RuntimeError("checkpoint: the recomputed graph is not differentiable")
+        return unpack
+
+
+def _nonreentrant(run, args):
+    frame = _Frame(run, args)
+    with torch.autograd.graph.saved_tensors_hooks(frame.pack, frame.unpack):
+        return run(*args)
 
 
 def _torch_rng_used(args) -> bool:
