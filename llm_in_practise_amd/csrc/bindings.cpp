@@ -93,9 +93,6 @@ int lora_acc_chunks(int M, int K);
 void launch_lora_proj2(const void*, int, const void*, const void*, int, int, int, float*, int, void*, int, int, uint64_t, float, float,
                        uint64_t, float, float, size_t, uint8_t*, float*, hipStream_t);
 int lora_proj2_ws_floats(int, int);
-void launch_lora_acc2(const float*, int, int, const float*, int, int, const void*, int, void*, int, const void*,
-                      const void*, int, float*, float*, int64_t, int64_t, int64_t, int64_t, int, uint64_t, float,
-                      uint64_t, float, size_t, const uint8_t*, hipStream_t);
 void launch_lora_proj_pair(const void*, const void*, int, const void*, const void*, int, int, int, float*, float*, float,
                            float, int, hipStream_t);
 void launch_lora_acc_pair(const float*, const float*, int, int, const void*, const void*, int, int, int, float*, float*,
@@ -1037,7 +1034,7 @@ static uint8_t* keep_bits_ptr(const optional<Tensor>& m, int64_t M, int64_t K, c
   return m->data_ptr<uint8_t>();
 }
 
-// masks (optional, uint8 [2, M, K/8]): the two branches' dropout keep bits, written for lora_acc2
+// masks (optional, uint8 [2, M, K/8]): the two branches' dropout keep bits, written for the backward (lora_acc_quad, gemm4w_loradx, lora_dx2)
 Tensor lora_proj2(Tensor x, Tensor a0, Tensor a1, optional<Tensor> outb, bool want_f32, double p0, int64_t key0,
                   double scale0, double p1, int64_t key1, double scale1, optional<Tensor> masks) {
   CHECK_BF16(x);
@@ -1067,32 +1064,6 @@ Tensor lora_proj2(Tensor x, Tensor a0, Tensor a1, optional<Tensor> outb, bool wa
                     (size_t)x.stride(0), keep_bits_ptr(masks, M, K, "lora_proj2"),
                     wsf ? ws.data_ptr<float>() : nullptr, stream());
   return want_f32 ? of : Tensor();
-}
-
-// dA_i [r_i, K] += G_iᵀ·D_i(x), dx += Σ_i D_i(G_i·A_i) for two branches in one pass (r_i <= 8)
-void lora_acc2(Tensor g0, Tensor g1, Tensor x, Tensor dx, Tensor a0, Tensor a1, Tensor out0, Tensor out1, double p0,
-               int64_t key0, double p1, int64_t key1, optional<Tensor> masks) {
-  for (const Tensor* g : {&g0, &g1})
-    TORCH_CHECK(g->scalar_type() == at::kFloat && g->dim() == 2 && g->stride(1) == 1 && g->size(1) <= 8 &&
-                    g->stride(0) % 4 == 0 && g->stride(0) >= 8 && reinterpret_cast<uintptr_t>(g->data_ptr()) % 16 == 0,
-                "lora_acc2: g fp32 [M, r<=8], row stride >= 8, 16-B aligned rows");
-  CHECK_BF16(x);
-  CHECK_BF16(dx);
-  const int M = x.size(0), K = x.size(1), r0 = g0.size(1), r1 = g1.size(1);
-  TORCH_CHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0 && K % 128 == 0 && g0.size(0) == M && g1.size(0) == M,
-              "lora_acc2: x layout");
-  TORCH_CHECK(dx.stride(1) == 1 && dx.size(0) == M && dx.size(1) == K, "lora_acc2: dx");
-  TORCH_CHECK(a0.is_contiguous() && a0.size(0) == r0 && a0.size(1) == K && a1.is_contiguous() && a1.size(0) == r1 &&
-                  a1.size(1) == K && a0.scalar_type() == at::kBFloat16 && a1.scalar_type() == at::kBFloat16,
-              "lora_acc2: A [r, K] bf16");
-  TORCH_CHECK(out0.scalar_type() == at::kFloat && out0.size(0) == r0 && out0.size(1) == K &&
-                  out1.scalar_type() == at::kFloat && out1.size(0) == r1 && out1.size(1) == K,
-              "lora_acc2: out [r, K] fp32");
-  launch_lora_acc2(g0.data_ptr<float>(), g0.stride(0), r0, g1.data_ptr<float>(), g1.stride(0), r1, x.data_ptr(),
-                   x.stride(0), dx.data_ptr(), dx.stride(0), a0.data_ptr(), a1.data_ptr(), K, out0.data_ptr<float>(),
-                   out1.data_ptr<float>(), out0.stride(0), out0.stride(1), out1.stride(0), out1.stride(1), M,
-                   (uint64_t)key0, (float)p0, (uint64_t)key1, (float)p1, (size_t)x.stride(0),
-                   keep_bits_ptr(masks, M, K, "lora_acc2"), stream());
 }
 
 // y[:, c0_i : c0_i + n_i] += xa_i · B_iᵀ in place (xa_i fp32 [M, r_i], scale folded in; B_i bf16 [n_i, r_i])
@@ -1704,7 +1675,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lora_proj", &lora_proj);
   m.def("lora_acc", &lora_acc);
   m.def("lora_proj2", &lora_proj2);
-  m.def("lora_acc2", &lora_acc2);
   m.def("lora_proj_pair", &lora_proj_pair);
   m.def("lora_acc_pair", &lora_acc_pair);
   m.def("lora_dA_pair", &lora_dA_pair);

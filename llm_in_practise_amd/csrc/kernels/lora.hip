@@ -742,136 +742,6 @@ __global__ __launch_bounds__(256) void lora_proj2_sum_k(const float* __restrict_
   if (outb) outb[(size_t)m * ldob + j] = (bf16)t;
 }
 
-// lora_acc (matrix cores) for two dropout branches over the same x / dx, R = 8 rows each:
-//   out_i[j, k] += Σ_m G_i[m, j]·D_i(X)[m, k]          (dA of each adapter)
-//   DX[m, k]    += Σ_i D_i(Σ_j G_i[m, j]·A_i[j, k])    (both adapters' input gradients, one RW of dx)
-// — the single-branch kernel above run twice read x twice and dx twice; this reads each once.
-template <int SUB>
-__global__ __launch_bounds__(256) void lora_acc2_mfma_k(const float* __restrict__ G0, int ldg0, int r0,
-                                                       const float* __restrict__ G1, int ldg1, int r1,
-                                                       const bf16* __restrict__ X, int ldx, bf16* __restrict__ DX,
-                                                       int lddx, const bf16* __restrict__ W0,
-                                                       const bf16* __restrict__ W1, int K, float* __restrict__ out0,
-                                                       float* __restrict__ out1, int64_t sj0, int64_t sk0, int64_t sj1,
-                                                       int64_t sk1, int M, uint64_t key0, uint64_t key1, uint32_t thr0,
-                                                       uint32_t thr1, float ds0, float ds1, size_t mask_ld,
-                                                       const uint8_t* __restrict__ mki) {
-  constexpr int R = 8;
-  __shared__ float red[4][64][33];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int q = lane >> 4, n = lane & 15;
-  const int kb = blockIdx.x * 128;
-  const int k8 = kb + 8 * n;
-  const int mw = blockIdx.y * (128 * SUB) + w * (32 * SUB);
-  bf16x8 wv0[R], wv1[R];
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    wv0[j] = j < r0 ? *reinterpret_cast<const bf16x8*>(W0 + (size_t)j * K + k8) : bf16x8{};
-    wv1[j] = j < r1 ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)j * K + k8) : bf16x8{};
-  }
-  f32x4 acc0[8], acc1[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) acc0[c] = acc1[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const float d0 = thr0 ? ds0 : 1.f, d1 = thr1 ? ds1 : 1.f;
-#pragma unroll
-  for (int s = 0; s < SUB; ++s) {
-    const int m0 = mw + 32 * s + 8 * q;
-    bf16x8 xb[8], db[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int m = min(m0 + e, M - 1);
-      xb[e] = *reinterpret_cast<const bf16x8*>(X + (size_t)m * ldx + k8);
-      db[e] = *reinterpret_cast<const bf16x8*>(DX + (size_t)m * lddx + k8);
-    }
-    bf16x8 a0, a1;   // Gᵀ fragments: rows j = n (< 8 used), k = the lane group's 8 m
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int m = m0 + e;
-      a0[e] = (bf16)((m < M && n < r0) ? G0[(size_t)m * ldg0 + n] : 0.f);
-      a1[e] = (bf16)((m < M && n < r1) ? G1[(size_t)m * ldg1 + n] : 0.f);
-    }
-    uint32_t keep0[8], keep1[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int m = m0 + e;
-      const size_t v8 = ((size_t)m * mask_ld + k8) >> 3;
-      if (mki) {   // keep bits stored by the forward's lora_proj2 (no hash regeneration)
-        const size_t mi = (size_t)min(m, M - 1) * (K >> 3) + (k8 >> 3);
-        keep0[e] = m >= M ? 0u : (thr0 ? (uint32_t)mki[mi] : 0xFFu);
-        keep1[e] = m >= M ? 0u : (thr1 ? (uint32_t)mki[(size_t)M * (K >> 3) + mi] : 0xFFu);
-      } else {
-        keep0[e] = m >= M ? 0u : (thr0 ? dropout_keep8(key0, v8, thr0) : 0xFFu);
-        keep1[e] = m >= M ? 0u : (thr1 ? dropout_keep8(key1, v8, thr1) : 0xFFu);
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      bf16x8 b0, b1;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        b0[e] = ((keep0[e] >> c) & 1) ? xb[e][c] : (bf16)0.f;
-        b1[e] = ((keep1[e] >> c) & 1) ? xb[e][c] : (bf16)0.f;
-      }
-      acc0[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc0[c], 0, 0, 0);
-      acc1[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc1[c], 0, 0, 0);
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int m = m0 + e;
-      if (m >= M) continue;
-      float g0[R], g1[R];
-#pragma unroll
-      for (int j = 0; j < R; j += 4) {
-        const f32x4 t0 = *reinterpret_cast<const f32x4*>(G0 + (size_t)m * ldg0 + j);
-        const f32x4 t1 = *reinterpret_cast<const f32x4*>(G1 + (size_t)m * ldg1 + j);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          g0[j + u] = j + u < r0 ? t0[u] : 0.f;
-          g1[j + u] = j + u < r1 ? t1[u] : 0.f;
-        }
-      }
-      float t0[8], t1[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) t0[i] = t1[i] = 0.f;
-#pragma unroll
-      for (int j = 0; j < R; ++j)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          t0[i] += g0[j] * (float)wv0[j][i];
-          t1[i] += g1[j] * (float)wv1[j][i];
-        }
-      bf16x8 o;
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        o[i] = (bf16)((float)db[e][i] + (((keep0[e] >> i) & 1) ? t0[i] * d0 : 0.f) +
-                      (((keep1[e] >> i) & 1) ? t1[i] * d1 : 0.f));
-      *reinterpret_cast<bf16x8*>(DX + (size_t)m * lddx + k8) = o;
-    }
-  }
-  // reduce the 4 waves' partials branch by branch through the one LDS array
-#pragma unroll
-  for (int br = 0; br < 2; ++br) {
-    const f32x4* acc = br == 0 ? acc0 : acc1;
-    const int r = br == 0 ? r0 : r1;
-    const int64_t sj = br == 0 ? sj0 : sj1, sk = br == 0 ? sk0 : sk1;
-    float* out = br == 0 ? out0 : out1;
-    const float ds = br == 0 ? d0 : d1;
-    if (br == 1) __syncthreads();        // branch 0's reads of red are done
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) red[w][lane][c * 4 + t] = acc[c][t];
-    __syncthreads();
-    const bool jfast = sj == 1;
-    for (int idx = threadIdx.x; idx < r * 128; idx += 256) {
-      const int j = jfast ? idx % r : idx / 128, kk = jfast ? idx / r : idx % 128;
-      const int ln = 16 * (j >> 2) + (kk >> 3), slot = (kk & 7) * 4 + (j & 3);
-      const float v = (red[0][ln][slot] + red[1][ln][slot] + red[2][ln][slot] + red[3][ln][slot]) * ds;
-      atomicAdd(out + j * sj + (int64_t)(kb + kk) * sk, v);
-    }
-  }
-}
-
 // ---- y[:, c0_i : c0_i + n_i] += xa_i · B_iᵀ for up to 4 branches, in place on the base GEMM's output ----
 // (replaces the rank-Σr addmm over ALL N columns of a fused q|k|v output plus the per-call copies of
 // each B into a zero-padded [N, 32] K-slice buffer: only the adapters' own column blocks are read and
@@ -1320,21 +1190,6 @@ void launch_lora_proj2(const void* X, int ldx, const void* W0, const void* W1, i
     lora_proj2_k<1, 16><<<(M + 15) / 16, 64, 0, st>>>((const bf16*)X, ldx, (const bf16*)W0, (const bf16*)W1, r0, r, K, outf,
                                                       ldof, (bf16*)outb, ldob, M, key0, key1, thr0, thr1, ds0, ds1, scale0,
                                                       scale1, mask_ld, mko);
-  LIPA_CHECK_LAUNCH();
-}
-
-// two dropout branches over the same x / dx (r0, r1 <= 8, K % 128 == 0)
-void launch_lora_acc2(const float* G0, int ldg0, int r0, const float* G1, int ldg1, int r1, const void* X, int ldx,
-                      void* DX, int lddx, const void* W0, const void* W1, int K, float* out0, float* out1, int64_t sj0,
-                      int64_t sk0, int64_t sj1, int64_t sk1, int M, uint64_t key0, float p0, uint64_t key1, float p1,
-                      size_t mask_ld, const uint8_t* mki, hipStream_t st) {
-  const uint32_t thr0 = p0 > 0.f ? (uint32_t)(p0 * 65536.0f + 0.5f) : 0u;
-  const uint32_t thr1 = p1 > 0.f ? (uint32_t)(p1 * 65536.0f + 0.5f) : 0u;
-  const float ds0 = p0 > 0.f ? 1.f / (1.f - p0) : 1.f, ds1 = p1 > 0.f ? 1.f / (1.f - p1) : 1.f;
-  dim3 g2(K / 128, (M + 127) / 128);
-  lora_acc2_mfma_k<1><<<g2, 256, 0, st>>>(G0, ldg0, r0, G1, ldg1, r1, (const bf16*)X, ldx, (bf16*)DX, lddx,
-                                          (const bf16*)W0, (const bf16*)W1, K, out0, out1, sj0, sk0, sj1, sk1, M, key0,
-                                          key1, thr0, thr1, ds0, ds1, mask_ld, mki);
   LIPA_CHECK_LAUNCH();
 }
 

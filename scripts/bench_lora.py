@@ -54,7 +54,6 @@ def main():
         "dropout_fwd": (lambda: N.dropout_fwd(x, 0.1, 7), 2 * M * H * 2),
         "acc_dA_nodx": (lambda: N.lora_acc(g, x, 0, H, outA, False, None, None, 0.0, 0, False), M * H * 2),
         "pair_proj2_fwd_drop": (lambda: N.lora_proj2(x, a, a2, ext, True, 0.1, 7, 2.0, 0.1, 9, 2.0, None), M * H * 2),
-        "pair_acc2_dA_dx_drop": (lambda: N.lora_acc2(g, g2, x, dx, a, a2, outA, outA2, 0.1, 7, 0.1, 9, None), 3 * M * H * 2),
     }
     import os
     only = os.environ.get("LORA_CASES")
