@@ -8,7 +8,8 @@
 //   clusters and each wave's LDS reads + LDS-DMA issue sit beside its partner's MFMAs.
 //   LDS: 2 buffers (tile parity) x 4 quarters of 16 KB: QALO / QAHI = A rows the waves read in their
 //   a-lo / a-hi quadrants, QBLO / QBHI = B rows of the b-lo / b-hi quadrants.  Quarter issue order
-//   (tile T phase k): Qb_hi(T+1), Qb_lo(T+1), Qa_hi(T+1), Qa_lo(T+2); vmcnt(6) in phase 1, vmcnt(4) in phase 3.
+//   (tile T phase k): Qb_hi(T+1), Qb_lo(T+1), Qa_hi(T+1), Qa_lo(T+2); vmcnt(6) in phase 1, vmcnt(4) in phase 3
+//   (vmcnt(0) / vmcnt(2) at the last tiles, where fewer DMAs follow).
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -149,7 +150,8 @@ __global__ __launch_bounds__(NTH, 1) void g8w_k(const bf16* __restrict__ A, int 
   dma_q(QBHI, 0);
   dma_q(QAHI, 0);
   dma_q(QALO, 1);
-  wait_vmcnt<4>();
+  if (nk > 1) wait_vmcnt<4>();   // QAHI(0), QALO(1) may stay in flight
+  else wait_vmcnt<2>();
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
@@ -174,9 +176,21 @@ __global__ __launch_bounds__(NTH, 1) void g8w_k(const bf16* __restrict__ A, int 
           for (int s = 0; s < 2; ++s) fb[f][s] = lds_frag(qb + f * 2048 + lo[s]);
       }
       if constexpr (k == 0) dma_q(QBHI, t + 1);
-      if constexpr (k == 1) { dma_q(QBLO, t + 1); wait_vmcnt<6>(); }
+      // counted waits, exact at the tail too (the round-5 build used vmcnt(6) / vmcnt(4) on every tile: at the last
+      // two tiles the skipped DMAs made those counts let QBLO / QAHI of the current tile through unlanded)
+      //   phase 1: QAHI(t) landed; issued after it: QALO(t+1), QBHI(t+1), QBLO(t+1) — 6 if t+1 < nk, else 0
+      //   phase 3: QALO/QBHI/QBLO(t+1) landed; issued after: QAHI(t+1), QALO(t+2) — 4 if t+2 < nk, 2 if t+1 < nk
+      if constexpr (k == 1) {
+        dma_q(QBLO, t + 1);
+        if (t + 1 < nk) wait_vmcnt<6>();
+        else wait_vmcnt<0>();
+      }
       if constexpr (k == 2) dma_q(QAHI, t + 1);
-      if constexpr (k == 3) { dma_q(QALO, t + 2); wait_vmcnt<4>(); }
+      if constexpr (k == 3) {
+        dma_q(QALO, t + 2);
+        if (t + 2 < nk) wait_vmcnt<4>();
+        else wait_vmcnt<2>();
+      }
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
@@ -283,12 +297,16 @@ int main(int argc, char** argv) {
     int bn = 0, bm = 0;
     const int sp = gemm4w_plan(s.M, s.N, s.K, false, 0, 0, &bn, 0, &bm, false);
     auto run4 = [&]() { launch_gemm4w(a, s.K, b, s.K, nullptr, c1, ws, nullptr, nullptr, s.M, s.N, s.K, sp, false, bn, bm, 0); };
+    // gemm4w forced onto g8w's own tiling (256 x 256, whole K): the same-work comparison
+    int bnf = 0, bmf = 0;
+    const int spf = gemm4w_plan(s.M, s.N, s.K, false, 256, 1, &bnf, 256, &bmf, false);
+    auto run4f = [&]() { launch_gemm4w(a, s.K, b, s.K, nullptr, c1, ws, nullptr, nullptr, s.M, s.N, s.K, spf, false, bnf, bmf, 0); };
     const int grid8 = ((s.M + 255) / 256) * ((s.N + 255) / 256);
     auto run8 = [&](int prio) {
       if (prio) g8::g8w_k<1><<<grid8, 512, 0, 0>>>(a, s.K, b, s.K, nullptr, c2, s.M, s.N, s.K);
       else g8::g8w_k<0><<<grid8, 512, 0, 0>>>(a, s.K, b, s.K, nullptr, c2, s.M, s.N, s.K);
     };
-    run4();
+    run4f();   // the bit-exactness reference: gemm4w on the same tiling (whole K, K-tiles summed in the same order)
     run8(1);
     CK(hipDeviceSynchronize());
     CK(hipMemset(dd, 0, 8));
@@ -307,15 +325,17 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       return ms * 1000.f / it;
     };
-    float b4 = 1e9, b8 = 1e9, b8n = 1e9;
+    float b4 = 1e9, b4f = 1e9, b8 = 1e9, b8n = 1e9;
     for (int r = 0; r < 5; ++r) {
       b4 = fminf(b4, timeit(run4));
+      b4f = fminf(b4f, timeit(run4f));
       b8 = fminf(b8, timeit([&] { run8(1); }));
       b8n = fminf(b8n, timeit([&] { run8(0); }));
     }
-    printf("%-10s M=%5d N=%6d K=%6d  gemm4w(%dx%d s%d) %8.1f us %6.0f TF/s | g8w %8.1f us %6.0f TF/s | g8w-noprio %8.1f us %6.0f TF/s | relerr %.2e\n",
-           s.name, s.M, s.N, s.K, bm, bn, sp, b4, fl / b4 / 1e6, b8, fl / b8 / 1e6, b8n, fl / b8n / 1e6,
-           std::sqrt(h[0] / h[1]));
+    printf("%-10s M=%5d N=%6d K=%6d  gemm4w(%dx%d s%d) %7.1f us %5.0f TF/s | gemm4w(256x256 s%d) %7.1f us %5.0f TF/s | "
+           "g8w %7.1f us %5.0f TF/s | g8w-noprio %7.1f us %5.0f TF/s | g8w vs gemm4w 256x256 s1: %s (relerr %.2e)\n",
+           s.name, s.M, s.N, s.K, bm, bn, sp, b4, fl / b4 / 1e6, spf, b4f, fl / b4f / 1e6, b8, fl / b8 / 1e6, b8n,
+           fl / b8n / 1e6, h[0] == 0.f ? "bit-exact" : "DIFFERENT", std::sqrt(h[0] / h[1]));
     fflush(stdout);
     CK(hipFree(a));
     CK(hipFree(b));
