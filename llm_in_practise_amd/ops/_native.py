@@ -48,8 +48,35 @@ def has_native() -> bool:
         return False
 
 
+# Per-op environment switches are read on every call (tests and smoke() flip them at run time), but through
+# os.environ's encoded mapping: os.environ.get() encodes the key each time (~1.5 us, ~1k calls per step)
+_ENV_DATA = getattr(os.environ, "_data", None)
+
+
+def env_flag(name: str) -> bool:
+    """``os.environ.get(name) == "1"`` at a tenth of its cost (CPython keeps the encoded environment in
+    ``os.environ._data``; any other mapping takes the plain path)."""
+    if _ENV_DATA is not None:
+        return _ENV_DATA.get(name.encode()) == b"1"
+    return os.environ.get(name) == "1"
+
+
 def force_reference() -> bool:
-    return os.environ.get("LIPA_REFERENCE", "0") == "1"
+    return env_flag("LIPA_REFERENCE")
+
+
+_Function = torch.autograd.Function
+_functorch_active = torch._C._are_functorch_transforms_active
+
+
+def fn_apply(fn, *args):
+    """``fn.apply(*args)`` for the ops' autograd Functions without torch's Python prologue: ``Function.apply``
+    binds default arguments when ``setup_context`` is overridden (none of these Functions does) and passes every
+    argument through functorch's dead-wrapper unwrap — 5-8 us per call at 10-25 arguments, ~500 calls in a
+    reference-faithful step.  Under functorch transforms (vmap / grad) the full path runs."""
+    if _functorch_active():
+        return fn.apply(*args)
+    return super(_Function, fn).apply(*args)
 
 
 def use_native(*tensors: torch.Tensor | None) -> bool:

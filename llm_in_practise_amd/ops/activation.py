@@ -5,7 +5,7 @@ import torch
 import torch.nn.functional as F
 
 from . import reference as ref
-from ._native import native, use_native
+from ._native import native, use_native, fn_apply
 
 
 class _SwiGLUFn(torch.autograd.Function):
@@ -23,7 +23,7 @@ class _SwiGLUFn(torch.autograd.Function):
 def swiglu_fused(gu: torch.Tensor) -> torch.Tensor:
     """gu [T, 2F] = [gate | up] → silu(gate)·up [T, F]."""
     if use_native(gu):
-        return _SwiGLUFn.apply(gu.contiguous())
+        return fn_apply(_SwiGLUFn, gu.contiguous())
     f = gu.shape[-1] // 2
     return ref.swiglu(gu[..., :f], gu[..., f:])
 
@@ -43,5 +43,5 @@ class _GeluFn(torch.autograd.Function):
 def gelu(x: torch.Tensor) -> torch.Tensor:
     """Exact (erf) GELU as ``nn.GELU()`` (``ddp_gpt_wikitext2.py:103``)."""
     if use_native(x) and x.is_contiguous():
-        return _GeluFn.apply(x)
+        return fn_apply(_GeluFn, x)
     return F.gelu(x)

@@ -23,7 +23,7 @@ import math
 import torch
 
 from . import reference as ref
-from ._native import native, use_native
+from ._native import native, use_native, fn_apply
 
 HEAD_DIMS = (32, 64, 96, 128)
 _SEED = [0x243F6A8885A308D3]
@@ -74,7 +74,7 @@ def flash_attention(q, k, v, batch: int, seqlen: int, hq: int, hkv: int, d: int,
         if not (_aligned(q, d) and _aligned(k, d) and _aligned(v, d)):
             q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
         seed = _next_seed() if (dropout_p > 0 and seed is None) else (seed or 0)
-        return _FlashAttnFn.apply(q, k, v, batch, seqlen, hq, hkv, d, causal, scale, kv_lens, float(dropout_p), seed)
+        return fn_apply(_FlashAttnFn, q, k, v, batch, seqlen, hq, hkv, d, causal, scale, kv_lens, float(dropout_p), seed)
     qb = q.reshape(batch, seqlen, hq, d)
     kb = k.reshape(batch, seqlen, hkv, d)
     vb = v.reshape(batch, seqlen, hkv, d)

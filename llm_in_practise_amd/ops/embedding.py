@@ -15,7 +15,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ._native import native, use_native
+from ._native import native, use_native, fn_apply
 
 
 # Out-of-range token ids: F.embedding (the reference's op) raises; the gather kernel reads a clamped
@@ -91,7 +91,7 @@ def embedding(ids: torch.Tensor, weight: torch.Tensor, padding_idx: int | None =
             return _gather(weight, ids)
         from .linear import deterministic
         if not deterministic():   # the scatter-add's fp32 atomics sum in arrival order
-            return _EmbeddingFn.apply(ids, weight, padding_idx)
+            return fn_apply(_EmbeddingFn, ids, weight, padding_idx)
     return F.embedding(ids, weight, padding_idx)
 
 

@@ -25,13 +25,12 @@ Reference parity: PEFT ``LoraConfig(r, lora_alpha, lora_dropout, target_modules)
 from __future__ import annotations
 
 import dataclasses
-import os
 
 import torch
 import torch.nn.functional as F
 
 from ..quant.nf4 import NF4Weight, dequantize_nf4
-from ._native import native, use_native
+from ._native import env_flag, fn_apply, native, use_native
 from .checkpoint import _KEY, _sac_recording, checkpoint, next_dropout_key, sac_put, sac_take, seed_dropout  # noqa: F401
 from .gemm import (GEMM_STATS, _MIN_M, _base_gemm, _base_gemm_t, _count, _g4w_ok, _nf4_expand,  # noqa: F401
                    _nf4_w4, _w4_ok, head_logits, nf4_cache_advance)
@@ -95,7 +94,7 @@ def deterministic() -> bool:
     """Bit-reproducible LoRA gradients (``LIPA_DETERMINISTIC=1`` or
     ``torch.use_deterministic_algorithms(True)``): fixed-order partial sums instead of fp32
     atomics in the fused LoRA backward (≈0.5 % slower)."""
-    return os.environ.get("LIPA_DETERMINISTIC", "0") == "1" or torch.are_deterministic_algorithms_enabled()
+    return env_flag("LIPA_DETERMINISTIC") or torch.are_deterministic_algorithms_enabled()
 
 
 _ZBUF: dict = {}
@@ -551,7 +550,7 @@ def fused_linear(x: torch.Tensor, base, bias: torch.Tensor | None = None,
         ab = []
         for br in branches:
             ab += [br.a, br.b]
-        y = _FusedLinearFn.apply(x2.contiguous(), None if res2 is None else res2.contiguous(),
+        y = fn_apply(_FusedLinearFn, x2.contiguous(), None if res2 is None else res2.contiguous(),
                                  weight, bias, (base, tuple(branches), training), *ab)
     else:
         _count("library")

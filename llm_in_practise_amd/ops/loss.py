@@ -14,7 +14,7 @@ import torch
 import torch.nn.functional as F
 
 from . import reference as ref
-from ._native import native, use_native
+from ._native import native, use_native, fn_apply
 from .gemm import _count, _g4w_ok
 
 
@@ -74,7 +74,7 @@ def fused_linear_cross_entropy(h: torch.Tensor, weight: torch.Tensor, labels: to
     of each one's mean loss (gradient-accumulation semantics)."""
     if use_native(h):
         need_w = weight.requires_grad
-        return _FusedLinearCEFn.apply(h.contiguous(), weight, labels.contiguous(), ignore_index, chunk, need_w,
+        return fn_apply(_FusedLinearCEFn, h.contiguous(), weight, labels.contiguous(), ignore_index, chunk, need_w,
                                       groups)
     _count("library")
     logits = h.float() @ weight.float().t()

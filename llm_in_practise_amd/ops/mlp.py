@@ -24,7 +24,7 @@ from __future__ import annotations
 import torch
 
 from ..quant.nf4 import NF4Weight
-from ._native import native
+from ._native import native, fn_apply
 from .checkpoint import sac_put, sac_take
 from .gemm import _MIN_M, _count, _nf4_expand, _nf4_w4
 
@@ -99,5 +99,5 @@ def swiglu_mlp(x: torch.Tensor, gu_base, down_base, residual: torch.Tensor | Non
     shape = x.shape
     x2 = x.reshape(-1, shape[-1]).contiguous()
     r2 = residual.reshape(-1, residual.shape[-1]).contiguous() if residual is not None else None
-    y = _SwiGLUMLPFn.apply(x2, r2, (gu_base, down_base))
+    y = fn_apply(_SwiGLUMLPFn, x2, r2, (gu_base, down_base))
     return y.view(*shape[:-1], y.shape[-1])

@@ -19,7 +19,7 @@ import dataclasses
 import torch
 import torch.nn.functional as F
 
-from ._native import native, use_native
+from ._native import native, use_native, fn_apply
 
 _MODES = {"topk_softmax": 0, "softmax_topk": 1}
 
@@ -48,7 +48,7 @@ def moe_route(logits: torch.Tensor, k: int, mode: str = "topk_softmax"):
     ``softmax_topk``: softmax over all experts, top-k probabilities, unnormalised (notebook)."""
     m = _MODES[mode]
     if use_native(logits) and logits.shape[1] <= 64 and k <= 8:
-        w, idx = _RouteFn.apply(logits, k, m)
+        w, idx = fn_apply(_RouteFn, logits, k, m)
         return w, idx.long()
     if m == 1:
         w, idx = F.softmax(logits.float(), -1).topk(k, -1)
@@ -123,14 +123,14 @@ class _CombineFn(torch.autograd.Function):
 def moe_gather(x: torch.Tensor, d: Dispatch) -> torch.Tensor:
     """x [T, H] → xs [T·k, H] with row p = x[perm[p] // k] (expert-sorted)."""
     if use_native(x) and _native_rows_ok(x):
-        return _GatherFn.apply(x, d.pos_of, d.perm, d.k)
+        return fn_apply(_GatherFn, x, d.pos_of, d.perm, d.k)
     return x.index_select(0, (d.perm // d.k).long())
 
 
 def moe_combine(ys: torch.Tensor, d: Dispatch, w: torch.Tensor, base: torch.Tensor | None = None) -> torch.Tensor:
     """out[t] = base[t] + Σ_j w[t, j] · ys[pos_of[t·k + j]]  (gate-weighted un-permute + sum)."""
     if use_native(ys) and _native_rows_ok(ys) and (base is None or base.dtype == ys.dtype):
-        return _CombineFn.apply(ys, w, base, d.pos_of, d.perm, d.k)
+        return fn_apply(_CombineFn, ys, w, base, d.pos_of, d.perm, d.k)
     T = d.pos_of.numel() // d.k
     g = ys.index_select(0, d.pos_of.long()).view(T, d.k, -1)
     out = (g * w.to(ys.dtype).unsqueeze(-1)).sum(1)

@@ -5,7 +5,7 @@ import torch
 import torch.nn as nn
 
 from . import reference as ref
-from ._native import native, use_native
+from ._native import native, use_native, fn_apply
 
 
 class _RMSNormFn(torch.autograd.Function):
@@ -56,7 +56,7 @@ class _RMSNormResidualFn(torch.autograd.Function):
 
 def rms_norm(x: torch.Tensor, weight: torch.Tensor | None, eps: float = 1e-6) -> torch.Tensor:
     if use_native(x):
-        return _RMSNormFn.apply(x, weight, eps)
+        return fn_apply(_RMSNormFn, x, weight, eps)
     return ref.rmsnorm(x, weight, eps)
 
 
@@ -64,7 +64,7 @@ def rms_norm_residual(x: torch.Tensor, weight: torch.Tensor | None, eps: float =
     """Pre-norm block entry: returns ``(rmsnorm(x), skip)`` where ``skip`` is ``x`` for the
     residual add; on the GPU the two gradients meet inside the norm backward kernel."""
     if use_native(x):
-        return _RMSNormResidualFn.apply(x, weight, eps)
+        return fn_apply(_RMSNormResidualFn, x, weight, eps)
     return ref.rmsnorm(x, weight, eps), x
 
 
@@ -90,7 +90,7 @@ class _LayerNormFn(torch.autograd.Function):
 
 def layer_norm(x, weight, bias, eps: float = 1e-5):
     if use_native(x):
-        return _LayerNormFn.apply(x, weight, bias, eps)
+        return fn_apply(_LayerNormFn, x, weight, bias, eps)
     return torch.nn.functional.layer_norm(x, (x.shape[-1],), weight, bias, eps)
 
 

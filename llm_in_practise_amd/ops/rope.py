@@ -9,7 +9,7 @@ from __future__ import annotations
 import torch
 
 from . import reference as ref
-from ._native import native, use_native
+from ._native import native, use_native, fn_apply
 
 
 def _ref_rope_tok(x, cos, sin, interleaved):
@@ -35,7 +35,7 @@ def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, interleave
     shape = x.shape
     x3 = x.reshape(-1, shape[-2], shape[-1])
     if use_native(x):
-        return _RopeFn.apply(x3, cos, sin, interleaved).view(shape)
+        return fn_apply(_RopeFn, x3, cos, sin, interleaved).view(shape)
     return _ref_rope_tok(x3, cos, sin, interleaved).view(shape)
 
 
@@ -64,7 +64,7 @@ def qk_norm_rope(qkv: torch.Tensor, q_weight, k_weight, cos, sin, hq: int, hkv: 
     """Split fused ``qkv [T, (hq+2hkv)*d]``; RMS-normalise each q/k head (Qwen3 qk-norm) and
     rotate (rotate-half).  Returns q ``[T, hq*d]``, k ``[T, hkv*d]``, v (strided view)."""
     if use_native(qkv):
-        return _QKNormRopeFn.apply(qkv.contiguous(), q_weight, k_weight, cos, sin, hq, hkv, d, eps)
+        return fn_apply(_QKNormRopeFn, qkv.contiguous(), q_weight, k_weight, cos, sin, hq, hkv, d, eps)
     T = qkv.shape[0]
     q = qkv[:, : hq * d].reshape(T, hq, d)
     k = qkv[:, hq * d:(hq + hkv) * d].reshape(T, hkv, d)
