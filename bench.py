@@ -514,16 +514,20 @@ def main():
                 import cProfile
                 prof = cProfile.Profile()
                 torch.autograd.set_multithreading_enabled(False)
+            hs = []
+            for k in range(args.host_steps):     # min over host_steps issues, as the headline's host record
+                sync()
+                h0 = time.perf_counter()
+                if prof is not None and k == 0:
+                    prof.enable()
+                step(fused=0)
+                if prof is not None and k == 0:
+                    prof.disable()
+                hs.append(time.perf_counter() - h0)
+                gcm.step()
+                beat()
             sync()
-            h0 = time.perf_counter()
-            if prof is not None:
-                prof.enable()
-            step(fused=0)
-            if prof is not None:
-                prof.disable()
-            fhost = round(1000 * (time.perf_counter() - h0), 2)
-            gcm.step()
-            sync()
+            fhost = round(1000 * min(hs), 2)
             if prof is not None:
                 torch.autograd.set_multithreading_enabled(True)
                 if D.is_main():

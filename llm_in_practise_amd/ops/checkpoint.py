@@ -100,13 +100,18 @@ class _Frame:
     same inputs under hooks that collect the saved tensors in the same order, and each unpack hands one over
     (and drops it: a second backward through a retained graph recomputes again).  Gradients flow through the
     ORIGINAL graph — inputs that do not require grad, ``torch.autograd.grad`` and partial backwards work as with
-    torch's form.  What is left out is the generality this stack does not use (nested checkpoints, early stop,
-    pytree inputs, torch-RNG replay — the HIP path's dropout comes from the key stream ``checkpoint`` restores)
-    and with it most of the per-layer host time of the reference-faithful step (profiles/r6/)."""
-    __slots__ = ("run", "args", "count", "saved")
+    torch's form.  Like torch's form (early stop, on by default) the recompute does not produce what no saved tensor
+    depends on: an op whose output only later ops consume asks :func:`tail_skippable` and, when the first forward
+    packed nothing after it, skips that output in the recompute (the decoder layer's down projection — its
+    output is the layer output, which the recompute discards).  What is left out is the generality this stack does
+    not use (nested checkpoints, pytree inputs, torch-RNG replay — the HIP path's dropout comes from the key
+    stream ``checkpoint`` restores) and with it most of the per-layer host time of the reference-faithful step
+    (profiles/r6/)."""
+    __slots__ = ("run", "args", "count", "saved", "rec", "tails", "tail", "skip")
 
     def __init__(self, run, args):
         self.run, self.args, self.count, self.saved = run, args, 0, None
+        self.rec, self.tails, self.tail, self.skip = None, 0, None, False
 
     def pack(self, t):
         i = self.count
@@ -124,8 +129,13 @@ class _Frame:
         rec: list = []
         args = tuple(a.detach().requires_grad_(a.requires_grad) if isinstance(a, torch.Tensor) else a
                      for a in self.args)
-        with torch.enable_grad(), torch.autograd.graph.saved_tensors_hooks(_Frame._keep(rec), _Frame._give(rec)):
-            self.run(*args)
+        prev = _FRAME[0]
+        self.rec, self.tails, _FRAME[0] = rec, 0, self
+        try:
+            with torch.enable_grad(), torch.autograd.graph.saved_tensors_hooks(_Frame._keep(rec), _Frame._give(rec)):
+                self.run(*args)
+        finally:
+            self.rec, _FRAME[0] = None, prev
         if len(rec) != self.count:
             raise RuntimeError(f"checkpoint recompute saved {len(rec)} tensors, the forward {self.count}: the layer "
                                "took a different code path in the recompute")
@@ -140,15 +150,43 @@ class _Frame:
 
     @staticmethod
     def _give(rec):
-        def unpack(_):   # (the recompute's own graph is never backpropagated)
+        def unpack(_):   # (the recomputed graph is never backpropagated)
             raise RuntimeError("checkpoint: the recomputed graph is not differentiable")
         return unpack
 
 
+# the _Frame whose first forward or recompute is running (non-reentrant HIP path), else None
+_FRAME: list = [None]
+
+
+def tail_skippable(n_saves: int) -> bool:
+    """Asked by an op right before it computes an output that only LATER ops consume, with the number of tensors
+    the op itself saves for backward.  In a checkpointed first forward it records its position (pack count and
+    call ordinal) and returns False; in the recompute it returns True for the call at that position when the
+    first forward packed nothing after this op's own saves — then no saved tensor depends on the output and the
+    op may leave it uncomputed (torch's non-reentrant checkpoint stops its recompute at the last saved tensor)."""
+    f = _FRAME[0]
+    if f is None:
+        return False
+    f.tails += 1
+    if f.rec is None:                                   # the first forward
+        f.tail = (f.tails, f.count, n_saves)
+        return False
+    return f.skip and f.tail[0] == f.tails and f.tail[1] == len(f.rec)
+
+
 def _nonreentrant(run, args):
     frame = _Frame(run, args)
-    with torch.autograd.graph.saved_tensors_hooks(frame.pack, frame.unpack):
-        return run(*args)
+    prev = _FRAME[0]
+    _FRAME[0] = frame
+    try:
+        with torch.autograd.graph.saved_tensors_hooks(frame.pack, frame.unpack):
+            out = run(*args)
+    finally:
+        _FRAME[0] = prev
+    t = frame.tail
+    frame.skip = t is not None and t[0] == frame.tails and t[1] + t[2] == frame.count
+    return out
 
 
 def _torch_rng_used(args) -> bool:

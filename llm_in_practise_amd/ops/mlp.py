@@ -25,7 +25,7 @@ import torch
 
 from ..quant.nf4 import NF4Weight
 from ._native import native, fn_apply
-from .checkpoint import sac_put, sac_take
+from .checkpoint import sac_put, sac_take, tail_skippable
 from .gemm import _MIN_M, _count, _nf4_expand, _nf4_w4
 
 
@@ -71,9 +71,13 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         else:
             F = gu_base.shape[0] // 2
             _count(_form(s_gu))
-            _count(_form(s_d))
             gu, h = native().gemm4w_swiglu(x, w_gu, s_gu, F)
-            y = native().gemm4w(h, w_d, residual, 0, False, 0, 0, s_d, K)
+            if tail_skippable(1 if need else 0):
+                # recompute of a checkpointed layer: y (the layer output) feeds no saved tensor — early stop
+                y = torch.empty_like(x)
+            else:
+                _count(_form(s_d))
+                y = native().gemm4w(h, w_d, residual, 0, False, 0, 0, s_d, K)
             sac_put((gu, y))
         ctx.save_for_backward(gu if need else None)
         ctx.w = (w_gu, s_gu, w_d, s_d, K) if need else None

@@ -1,6 +1,7 @@
 """The non-reentrant activation checkpoint of the HIP path (ops/checkpoint.py _nonreentrant): use_reentrant=False
 semantics without torch.utils.checkpoint's general machinery — same gradients as no checkpointing, inputs that do
-not require grad, torch.autograd.grad, a retained graph backpropagated twice, the recompute mismatch guard."""
+not require grad, torch.autograd.grad, a retained graph backpropagated twice, the recompute mismatch guard, early
+stop (an output no saved tensor needs is not recomputed)."""
 import pytest
 import torch
 
@@ -55,3 +56,59 @@ def test_recompute_taking_another_path_is_an_error():
     y = _nonreentrant(f, (torch.randn(2, 16),))
     with pytest.raises(RuntimeError, match="different code path"):
         y.backward()
+
+
+class _Tail(torch.autograd.Function):
+    """y = relu(x)·2 + x·w with the x·w term computed only when tail_skippable() says it is needed (the shape of the
+    fused MLP: its own saved tensor first, then an output only later ops consume)."""
+    computed = []
+
+    @staticmethod
+    def forward(ctx, x, w):
+        from llm_in_practise_amd.ops.checkpoint import tail_skippable
+        h = torch.relu(x)
+        skip = tail_skippable(1)
+        _Tail.computed.append(not skip)
+        y = torch.empty_like(x) if skip else h * 2 + x * w
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        return g * ((x > 0).to(g.dtype) * 2), None
+
+
+def test_recompute_skips_an_output_no_saved_tensor_needs():
+    """early stop: the op last to save anything leaves its output uncomputed in the recompute; gradients unchanged"""
+    lin = torch.nn.Linear(8, 8)
+
+    def layer(x, w):
+        return _Tail.apply(lin(x), w)
+    x = torch.randn(3, 8, requires_grad=True)
+    w = torch.randn(8)
+    _Tail.computed.clear()
+    _nonreentrant(layer, (x, w)).sum().backward()
+    assert _Tail.computed == [True, False]                    # forward computed y, the recompute skipped it
+    g = [x.grad.clone(), lin.weight.grad.clone()]
+    x.grad = lin.weight.grad = None
+    layer(x, w).sum().backward()
+    assert torch.equal(g[0], x.grad) and torch.equal(g[1], lin.weight.grad)
+
+
+def test_recompute_keeps_an_output_a_later_saved_tensor_needs():
+    """no early stop when an op after the tail point saves a tensor (its input would be the skipped output)"""
+    lin = torch.nn.Linear(8, 8)
+
+    def layer(x, w):
+        y = _Tail.apply(lin(x), w)
+        return (y * y).sum(-1)                                # y * y saves y
+    x = torch.randn(3, 8, requires_grad=True)
+    w = torch.randn(8)
+    _Tail.computed.clear()
+    _nonreentrant(layer, (x, w)).sum().backward()
+    assert _Tail.computed == [True, True]
+    g = x.grad.clone()
+    x.grad = None
+    layer(x, w).sum().backward()
+    assert torch.equal(g, x.grad)
