@@ -50,14 +50,12 @@ def has_native() -> bool:
 
 # Per-op environment switches are read on every call (tests and smoke() flip them at run time), but through
 # os.environ's encoded mapping: os.environ.get() encodes the key each time (~1.5 us, ~1k calls per step)
-_ENV_DATA = getattr(os.environ, "_data", None)
-
-
 def env_flag(name: str) -> bool:
-    """``os.environ.get(name) == "1"`` at a tenth of its cost (CPython keeps the encoded environment in
-    ``os.environ._data``; any other mapping takes the plain path)."""
-    if _ENV_DATA is not None:
-        return _ENV_DATA.get(name.encode()) == b"1"
+    """``os.environ.get(name) == "1"`` at a fraction of its cost (CPython's os.environ keeps the encoded
+    environment in ``_data``; any other mapping takes the plain path)."""
+    data = getattr(os.environ, "_data", None)
+    if data is not None:
+        return data.get(name.encode()) == b"1"
     return os.environ.get(name) == "1"
 
 
