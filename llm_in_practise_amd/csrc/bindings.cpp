@@ -745,7 +745,8 @@ Tensor gemm4w(Tensor x, Tensor w, optional<Tensor> residual, int64_t splits, boo
 // Fused MLP GEMMs (gemm4w.hip EPI 1 / 2).  gemm4w_swiglu: x [M, K], w_gu [2F, K] ([gate | up] rows)
 // → (gu [M, 2F], h = silu(gate)·up [M, F]).  gemm4w_dswiglu: dy [M, N_w], w_down [N_w, F], gu [M, 2F]
 // → dgu [M, 2F] = SwiGLU-backward(dy·w_down).  wscale: the weight is an NF4 base (g4w_operand).
-std::vector<Tensor> gemm4w_swiglu(Tensor x, Tensor w, optional<Tensor> wscale, int64_t F_w4) {
+std::vector<Tensor> gemm4w_swiglu(Tensor x, Tensor w, optional<Tensor> wscale, int64_t F_w4, bool want_gu,
+                                  bool want_h) {
   CHECK_BF16(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "gemm4w_swiglu: x 2-D");
   const bool w4 = wscale && wscale->defined();
@@ -756,10 +757,12 @@ std::vector<Tensor> gemm4w_swiglu(Tensor x, Tensor w, optional<Tensor> wscale, i
               "gemm4w_swiglu: unsupported shape / alignment");
   int bn = 0, bm = 0;
   gemm4w_plan(M, 2 * F, K, false, 0, 1, &bn, 0, &bm, w4);
-  auto gu = at::empty({M, 2 * F}, x.options());
-  auto h = at::empty({M, F}, x.options());
-  launch_gemm4w_swiglu(x.data_ptr(), x.stride(0), b.ptr, b.scale, gu.data_ptr(), h.data_ptr(), M, F, K, bn, bm,
-                       stream());
+  // an output the caller does not want is neither allocated nor stored (an undefined tensor is returned)
+  Tensor gu, h;
+  if (want_gu) gu = at::empty({M, 2 * F}, x.options());
+  if (want_h) h = at::empty({M, F}, x.options());
+  launch_gemm4w_swiglu(x.data_ptr(), x.stride(0), b.ptr, b.scale, want_gu ? gu.data_ptr() : nullptr,
+                       want_h ? h.data_ptr() : nullptr, M, F, K, bn, bm, stream());
   return {gu, h};
 }
 
@@ -1717,7 +1720,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bt") = false, py::arg("bn") = 0, py::arg("bm") = 0, py::arg("wscale") = py::none(),
         py::arg("n_w4") = 0, py::arg("wzero") = py::none());
   m.def("gemm4w_swiglu", &gemm4w_swiglu, py::arg("x"), py::arg("w"), py::arg("wscale") = py::none(),
-        py::arg("f_w4") = 0);
+        py::arg("f_w4") = 0, py::arg("want_gu") = true, py::arg("want_h") = true);
   m.def("mlora_apply", &mlora_apply);
   m.def("gemm4w_dswiglu", &gemm4w_dswiglu, py::arg("dy"), py::arg("w"), py::arg("gu"), py::arg("wscale") = py::none());
   m.def("attn_fwd", &attn_fwd);

@@ -365,8 +365,9 @@ __device__ __forceinline__ void w4_chunk(W4St& u, uint32_t w) {
 //   1  SwiGLU forward on the gate|up projection (NT, no split).  B = W_gu [2F, K] as stored ([gate | up]
 //      rows); the tile's B rows are gathered so that fragment pair (2c, 2c+1) of a wave is gate rows
 //      16c'…+15 and the matching up rows — every lane then holds g and u of the same (m, col).  Writes
-//      gu [M, 2F] in the [gate | up] layout (saved for backward) and h = silu(g)·u [M, F] to aux_out.
-//      N = 2F (virtual columns).
+//      gu [M, 2F] in the [gate | up] layout (saved for backward) and h = silu(g)·u [M, F] to aux_out;
+//      either store is skipped when its pointer is null (a checkpointed layer's first forward discards gu,
+//      its recompute needs no h).  N = 2F (virtual columns).
 //   2  SwiGLU backward fused into the down projection's dX (BT, no split): the GEMM tile is dh [M, F];
 //      the epilogue reads g, u from aux = gu [M, 2F] and writes dgu = [dh·u·silu'(g) | dh·silu(g)].
 //      N = F.
@@ -919,10 +920,12 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
           u[e] = (bf16)(e < 4 ? u0[e] : u1[e - 4]);
           h[e] = (bf16)(silu_f((float)g[e]) * (float)u[e]);
         }
-        bf16* gu = reinterpret_cast<bf16*>(out) + (size_t)m * 2 * F + hc;
-        G4W_ST(reinterpret_cast<bf16x8*>(gu), g);
-        G4W_ST(reinterpret_cast<bf16x8*>(gu + F), u);
-        G4W_ST(reinterpret_cast<bf16x8*>(aux_out + (size_t)m * F + hc), h);
+        if (out != nullptr) {
+          bf16* gu = reinterpret_cast<bf16*>(out) + (size_t)m * 2 * F + hc;
+          G4W_ST(reinterpret_cast<bf16x8*>(gu), g);
+          G4W_ST(reinterpret_cast<bf16x8*>(gu + F), u);
+        }
+        if (aux_out != nullptr) G4W_ST(reinterpret_cast<bf16x8*>(aux_out + (size_t)m * F + hc), h);
       }
       if constexpr (NH % 2) {   // the unpaired last h-block (BN = 192): 8-B stores
         constexpr int j = NB - 2;
@@ -935,10 +938,12 @@ __global__ __launch_bounds__(NT, 1) void gemm4w_k(const bf16* __restrict__ A, in
             u[e] = (bf16)acc[i][j + 1][e];
             h[e] = (bf16)(silu_f((float)g[e]) * (float)u[e]);
           }
-          bf16* gu = reinterpret_cast<bf16*>(out) + (size_t)m * 2 * F + hc;
-          G4W_ST(reinterpret_cast<bf16x4*>(gu), g);
-          G4W_ST(reinterpret_cast<bf16x4*>(gu + F), u);
-          G4W_ST(reinterpret_cast<bf16x4*>(aux_out + (size_t)m * F + hc), h);
+          if (out != nullptr) {
+            bf16* gu = reinterpret_cast<bf16*>(out) + (size_t)m * 2 * F + hc;
+            G4W_ST(reinterpret_cast<bf16x4*>(gu), g);
+            G4W_ST(reinterpret_cast<bf16x4*>(gu + F), u);
+          }
+          if (aux_out != nullptr) G4W_ST(reinterpret_cast<bf16x4*>(aux_out + (size_t)m * F + hc), h);
         }
       }
     }

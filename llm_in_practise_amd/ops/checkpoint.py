@@ -175,6 +175,14 @@ def tail_skippable(n_saves: int) -> bool:
     return f.skip and f.tail[0] == f.tails and f.tail[1] == len(f.rec)
 
 
+def saves_discarded() -> bool:
+    """True inside the first forward of a lean non-reentrant checkpoint: every tensor saved for backward is dropped
+    (the recompute produces it again), so an op may skip materialising a tensor it computes ONLY to save it — it
+    must still save a placeholder in its place, so the pack count matches the recompute's."""
+    f = _FRAME[0]
+    return f is not None and f.rec is None and not _sac_recording()
+
+
 def _nonreentrant(run, args):
     frame = _Frame(run, args)
     prev = _FRAME[0]

@@ -25,7 +25,7 @@ import torch
 
 from ..quant.nf4 import NF4Weight
 from ._native import native, fn_apply
-from .checkpoint import sac_put, sac_take, tail_skippable
+from .checkpoint import _sac_recording, sac_put, sac_take, saves_discarded, tail_skippable
 from .gemm import _MIN_M, _count, _nf4_expand, _nf4_w4
 
 
@@ -71,13 +71,18 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         else:
             F = gu_base.shape[0] // 2
             _count(_form(s_gu))
-            gu, h = native().gemm4w_swiglu(x, w_gu, s_gu, F)
-            if tail_skippable(1 if need else 0):
-                # recompute of a checkpointed layer: y (the layer output) feeds no saved tensor — early stop
+            # checkpointed layer: the recompute needs only gu (saved) — y, the layer output, feeds no saved tensor
+            # (early stop) and with it h; the first forward needs h and y but drops what it saves, so not gu
+            skip = tail_skippable(1 if need else 0)
+            keep_gu = (need and not saves_discarded()) or _sac_recording()   # (selective: the stash replays gu)
+            gu, h = native().gemm4w_swiglu(x, w_gu, s_gu, F, keep_gu, not skip)
+            if skip:
                 y = torch.empty_like(x)
             else:
                 _count(_form(s_d))
                 y = native().gemm4w(h, w_d, residual, 0, False, 0, 0, s_d, K)
+            if need and gu is None:
+                gu = x.new_empty(0)       # the placeholder a discarded save needs (same pack count as the recompute)
             sac_put((gu, y))
         ctx.save_for_backward(gu if need else None)
         ctx.w = (w_gu, s_gu, w_d, s_d, K) if need else None

@@ -714,6 +714,10 @@ def test_gemm4w_swiglu_epilogues(native_ext, M, Fd, K):
     ur = u.clone().requires_grad_(True)
     (F.silu(gr) * ur).backward(dh)
     assert rel_err(dgu[:, :Fd], gr.grad) < 1e-2 and rel_err(dgu[:, Fd:], ur.grad) < 1e-2
+    # either output left out (checkpointed first forward: no gu; recompute: no h) — the other one unchanged
+    gu0, h1 = native_ext.gemm4w_swiglu(x, w, want_gu=False)
+    gu1, h0 = native_ext.gemm4w_swiglu(x, w, want_h=False)
+    assert gu0 is None and h0 is None and torch.equal(h1, h) and torch.equal(gu1, gu)
 
 
 # NF4 codes fed straight into gemm4w (K9 "NF4 dequant-GEMM"): the in-kernel expansion must give the
