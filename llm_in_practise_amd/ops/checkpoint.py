@@ -1,7 +1,9 @@
 """Activation checkpointing that replays the same LoRA dropout masks, NF4-aware, with a selective policy
 (the reference's ``gradient_checkpointing_enable(gradient_checkpointing_kwargs=...)``,
 ``Fine-Tuning/qwen3-8b-qlora-dist.py:162-163``), and the host-side dropout key stream the fused LoRA kernels
-draw their masks from (``next_dropout_key`` / ``seed_dropout``).
+draw their masks from (``next_dropout_key`` / ``seed_dropout``).  On the HIP path the ``use_reentrant=False`` form
+is a lean frame (``_Frame``) with torch's early stop (``tail_skippable``); ops ask ``saves_discarded`` to skip
+tensors they would only compute to save in a first forward whose saves are dropped.
 """
 from __future__ import annotations
 
